@@ -1,0 +1,363 @@
+// Python bindings of the gfx950 kernels (torch tensors in, launches on the current HIP stream).
+// Kernels themselves live in csrc/kernels/*.hip and see only raw pointers (no torch headers there).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPCachingAllocator.h>
+
+#include "kernels/kernels.h"
+
+using torch::Tensor;
+using namespace tdl;
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_T(t, dt)                                                                        \
+  TORCH_CHECK((t).is_cuda(), #t " must be a HIP tensor");                                     \
+  TORCH_CHECK((t).is_contiguous(), #t " must be contiguous");                                 \
+  TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype ", (t).scalar_type())
+
+#define BF(t) reinterpret_cast<const bf16_t*>((t).data_ptr())
+#define BFW(t) reinterpret_cast<bf16_t*>((t).data_ptr())
+
+const float* optf(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->is_contiguous(), "expected fp32 contiguous");
+  return t->data_ptr<float>();
+}
+float* optfw(const c10::optional<Tensor>& t) { return const_cast<float*>(optf(t)); }
+const bf16_t* optb(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == torch::kBFloat16 && t->is_contiguous(), "expected bf16 contiguous");
+  return BF(*t);
+}
+bf16_t* optbw(const c10::optional<Tensor>& t) { return const_cast<bf16_t*>(optb(t)); }
+
+ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_t H, int64_t W,
+                   int64_t C, int64_t K, int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph,
+                   int64_t pw, int64_t dh, int64_t dw, int64_t Ho, int64_t Wo) {
+  ConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.K = K; a.R = R; a.S = S;
+  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+  a.Ho = Ho; a.Wo = Wo;
+  (void)x_like; (void)w_like;
+  return a;
+}
+
+// ------------------------------------------------------------------------------------------ conv
+void conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::optional<Tensor> stats,
+              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(w, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && y.dim() == 4, "NHWC / KRSC expected");
+  TORCH_CHECK(x.size(3) == w.size(3), "C mismatch");
+  ConvArgs a = conv_args(x, w, x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1),
+                         w.size(2), sh, sw, ph, pw, dh, dw, y.size(1), y.size(2));
+  TORCH_CHECK(y.size(0) == a.N && y.size(3) == a.K, "output shape mismatch");
+  a.x = BF(x); a.w = BF(w); a.out = y.data_ptr();
+  a.bias = optf(bias);
+  a.stats = optfw(stats);
+  if (a.stats) TORCH_CHECK(stats->numel() == 2 * a.K, "stats must be [2, K]");
+  a.M = a.N * a.Ho * a.Wo; a.Ng = a.K; a.Kg = a.R * a.S * a.C; a.ldc = a.K; a.relu = relu;
+  if (a.M == 0) return;
+  conv_fwd_launch(a, stream());
+}
+
+void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                int64_t dh, int64_t dw) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(w, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  ConvArgs a = conv_args(dx, w, dx.size(0), dx.size(1), dx.size(2), dx.size(3), w.size(0), w.size(1),
+                         w.size(2), sh, sw, ph, pw, dh, dw, dy.size(1), dy.size(2));
+  TORCH_CHECK(dx.size(3) == w.size(3) && dy.size(3) == w.size(0), "shape mismatch");
+  a.dy = BF(dy); a.w = BF(w); a.out = dx.data_ptr();
+  a.M = a.N * a.H * a.W; a.Ng = a.C; a.Kg = a.R * a.S * a.K; a.ldc = a.C; a.relu = 0;
+  if (a.M == 0) return;
+  conv_dgrad_launch(a, stream());
+}
+
+void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad, int64_t sh,
+                int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(out, torch::kFloat32);
+  TORCH_CHECK(out.dim() == 4, "dW must be KRSC");
+  ConvArgs a = conv_args(x, out, x.size(0), x.size(1), x.size(2), x.size(3), out.size(0),
+                         out.size(1), out.size(2), sh, sw, ph, pw, dh, dw, dy.size(1), dy.size(2));
+  TORCH_CHECK(out.size(3) == a.C && dy.size(3) == a.K && dy.size(0) == a.N, "shape mismatch");
+  a.dy = BF(dy); a.x = BF(x);
+  a.M = a.K; a.Ng = a.R * a.S * a.C; a.Kg = a.N * a.Ho * a.Wo;
+  int bm, bn, splits, kps;
+  conv_wgrad_plan(a.M, a.Ng, a.Kg, &bm, &bn, &splits, &kps);
+  a.kps = kps;
+  auto ws = torch::empty({(int64_t)splits * a.M * a.Ng}, out.options());
+  a.out = ws.data_ptr();
+  auto st = stream();
+  conv_wgrad_launch(a, bm, bn, splits, out.data_ptr<float>(), accumulate, st);
+  if (bias_grad.has_value() && bias_grad->defined()) {
+    CHECK_T((*bias_grad), torch::kFloat32);
+    hipMemsetAsync(bias_grad->data_ptr(), 0, a.K * sizeof(float), st);
+    colsum_launch(BF(dy), bias_grad->data_ptr<float>(), (long)a.Kg, a.K, st);
+  }
+}
+
+// ------------------------------------------------------------------------------------------- bn
+void bn_stats(Tensor x, Tensor stats) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(stats, torch::kFloat32);
+  const int64_t C = x.size(-1);
+  bn_stats_launch(BF(x), stats.data_ptr<float>(), x.numel() / C, C, stream());
+}
+
+void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor> gamma, Tensor beta,
+                 Tensor rmean, Tensor rvar, double count, double decay, double eps, bool training) {
+  CHECK_T(coef, torch::kFloat32);
+  CHECK_T(beta, torch::kFloat32);
+  CHECK_T(rmean, torch::kFloat32);
+  CHECK_T(rvar, torch::kFloat32);
+  TORCH_CHECK(!training || optf(stats) != nullptr, "training BN needs stats");
+  bn_finalize_launch(optf(stats), coef.data_ptr<float>(), optf(gamma), beta.data_ptr<float>(),
+                     rmean.data_ptr<float>(), rvar.data_ptr<float>(), beta.numel(), (float)count,
+                     (float)decay, (float)eps, training, stream());
+}
+
+void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  CHECK_T(coef, torch::kFloat32);
+  const int64_t C = x.size(-1);
+  bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu, stream());
+}
+
+void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, bool relu) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(red, torch::kFloat32);
+  const int64_t C = x.size(-1);
+  bn_bwd_reduce_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
+                       x.numel() / C, C, relu, stream());
+}
+
+void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red,
+                  c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres, double count,
+                  bool relu) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  const int64_t C = x.size(-1);
+  bn_bwd_apply_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
+                      optf(gamma), BFW(dx), optbw(dres), x.numel() / C, C, (float)count, relu,
+                      stream());
+}
+
+// ---------------------------------------------------------------------------------- elementwise
+void relu_bwd(Tensor dy, Tensor y, Tensor dx) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  relu_bwd_launch(BF(dy), BF(y), BFW(dx), dy.numel(), stream());
+}
+
+void add_act(Tensor a, c10::optional<Tensor> b, Tensor y, bool relu) {
+  CHECK_T(a, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  add_act_launch(BF(a), optb(b), BFW(y), a.numel(), relu, stream());
+}
+
+void scale_by_scalar(Tensor x, Tensor s, Tensor y) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && y.is_contiguous());
+  const bool bf = x.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || x.scalar_type() == torch::kFloat32);
+  scale_by_scalar_launch(x.data_ptr(), s.data_ptr<float>(), y.data_ptr(), x.numel(), bf, stream());
+}
+
+void sigmoid_threshold(Tensor x, Tensor prob, Tensor pred, double thr) {
+  const bool bf = x.scalar_type() == torch::kBFloat16;
+  sigmoid_threshold_launch(x.data_ptr(), bf, prob.data_ptr<float>(), pred.data_ptr<float>(),
+                           x.numel(), (float)thr, stream());
+}
+
+// -------------------------------------------------------------------------------------- pooling
+void maxpool_fwd(Tensor x, Tensor y, Tensor idx, int64_t k, int64_t s, int64_t pt, int64_t pl) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  CHECK_T(idx, torch::kUInt8);
+  TORCH_CHECK(k * k <= 255, "window too large for uint8 argmax");
+  maxpool_fwd_launch(BF(x), BFW(y), idx.data_ptr<uint8_t>(), x.size(0), x.size(1), x.size(2),
+                     x.size(3), y.size(1), y.size(2), k, s, pt, pl, stream());
+}
+
+void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t pt, int64_t pl) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  maxpool_bwd_launch(BF(dy), idx.data_ptr<uint8_t>(), BFW(dx), dx.size(0), dx.size(1), dx.size(2),
+                     dx.size(3), dy.size(1), dy.size(2), k, s, pt, pl, stream());
+}
+
+void avgpool_fwd(Tensor x, Tensor y) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  avgpool_fwd_launch(BF(x), BFW(y), x.size(0), x.size(1) * x.size(2), x.size(3), stream());
+}
+
+void avgpool_bwd(Tensor dy, Tensor dx) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  avgpool_bwd_launch(BF(dy), BFW(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream());
+}
+
+// --------------------------------------------------------------------------------------- losses
+void softmax_xent(Tensor logits, Tensor labels, Tensor loss, Tensor grad, double smoothing) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2);
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32);
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous());
+  TORCH_CHECK(grad.scalar_type() == logits.scalar_type());
+  softmax_xent_launch(logits.data_ptr(), bf, labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                      grad.data_ptr(), logits.size(0), logits.size(1), (float)smoothing, stream());
+}
+
+int label_kind(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case torch::kFloat32: return 0;
+    case torch::kUInt8: return 1;
+    case torch::kBool: return 1;
+    case torch::kInt64: return 2;
+    case torch::kBFloat16: return 3;
+    case torch::kInt32: return 4;
+    default: TORCH_CHECK(false, "unsupported label dtype");
+  }
+  return 0;
+}
+
+void lovasz_hinge(Tensor logits, Tensor labels, Tensor loss, Tensor grad) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && labels.is_contiguous());
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32);
+  const int64_t B = logits.size(0), P = logits.numel() / B;
+  TORCH_CHECK(P <= 16384, "lovasz kernel supports up to 16384 pixels per image");
+  lovasz_hinge_launch(logits.data_ptr(), bf, labels.data_ptr(), label_kind(labels),
+                      loss.data_ptr<float>(), grad.data_ptr<float>(), B, P, stream());
+}
+
+void seg_metrics(Tensor labels, Tensor pred, Tensor score, Tensor acc, bool kaggle) {
+  TORCH_CHECK(pred.scalar_type() == torch::kFloat32 && pred.is_contiguous());
+  const int64_t B = pred.size(0), P = pred.numel() / B;
+  seg_metrics_launch(labels.data_ptr(), label_kind(labels), pred.data_ptr<float>(),
+                     score.data_ptr<float>(), acc.data_ptr<float>(), B, P, kaggle, stream());
+}
+
+// ----------------------------------------------------------------------------------- optimizers
+void sgd_momentum(Tensor p, Tensor g, Tensor m, c10::optional<Tensor> lowp, Tensor flags, double lr,
+                  double mu, double wd, double gs, bool nesterov) {
+  CHECK_T(p, torch::kFloat32);
+  CHECK_T(g, torch::kFloat32);
+  CHECK_T(m, torch::kFloat32);
+  TORCH_CHECK(p.numel() % 64 == 0, "flat buffer must be 64-aligned");
+  sgd_momentum_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), optbw(lowp),
+                      flags.data_ptr<uint8_t>(), p.numel(), lr, mu, wd, gs, nesterov, stream());
+}
+
+void adam(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> lowp, Tensor flags,
+          double lr_t, double b1, double b2, double eps, double wd, double gs) {
+  CHECK_T(p, torch::kFloat32);
+  CHECK_T(g, torch::kFloat32);
+  TORCH_CHECK(p.numel() % 64 == 0, "flat buffer must be 64-aligned");
+  adam_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+              optbw(lowp), flags.data_ptr<uint8_t>(), p.numel(), lr_t, b1, b2, eps, wd, gs,
+              stream());
+}
+
+// ------------------------------------------------------------------------------- depthwise conv
+DwArgs dw_args(const Tensor& x_like, const Tensor& w, int64_t Ho, int64_t Wo, int64_t sh,
+               int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  DwArgs a{};
+  a.N = x_like.size(0); a.H = x_like.size(1); a.W = x_like.size(2); a.C = x_like.size(3);
+  a.R = w.size(0); a.S = w.size(1); a.Ho = Ho; a.Wo = Wo;
+  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dwl = dw;
+  TORCH_CHECK(w.size(2) == a.C, "depthwise weight must be [R,S,C]");
+  return a;
+}
+
+void dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t sh, int64_t sw,
+                int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(w, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  DwArgs a = dw_args(x, w, y.size(1), y.size(2), sh, sw, ph, pw, dh, dw);
+  a.x = BF(x); a.w = BF(w); a.bias = optf(bias); a.out = BFW(y); a.relu = relu;
+  dwconv_fwd_launch(a, stream());
+}
+
+void dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                  int64_t dh, int64_t dw) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(w, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  DwArgs a = dw_args(dx, w, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
+  a.dy = BF(dy); a.w = BF(w); a.out = BFW(dx);
+  dwconv_dgrad_launch(a, stream());
+}
+
+void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int64_t sh, int64_t sw,
+                  int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(dwt, torch::kFloat32);
+  TORCH_CHECK(dwt.size(0) * dwt.size(1) <= 49, "depthwise kernel up to 7x7");
+  DwArgs a = dw_args(x, dwt, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
+  a.dy = BF(dy); a.x = BF(x); a.dw = dwt.data_ptr<float>(); a.db = optfw(db);
+  dwconv_wgrad_launch(a, stream());
+}
+
+// ------------------------------------------------------------------------------------- upsample
+void upsample_fwd(Tensor x, Tensor y, Tensor ih, Tensor wh, Tensor iw, Tensor ww) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  upsample_fwd_launch(BF(x), BFW(y), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
+                      ww.data_ptr<float>(), x.size(0), x.size(1), x.size(2), x.size(3), y.size(1),
+                      y.size(2), stream());
+}
+
+void upsample_bwd(Tensor dy, Tensor dx, Tensor ih, Tensor wh, Tensor iw, Tensor ww) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  upsample_bwd_launch(BF(dy), BFW(dx), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
+                      ww.data_ptr<float>(), dx.size(0), dx.size(1), dx.size(2), dx.size(3),
+                      dy.size(1), dy.size(2), stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "tensorflowdistributedlearning_amd native gfx950 kernels";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("bn_stats", &bn_stats);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("add_act", &add_act);
+  m.def("scale_by_scalar", &scale_by_scalar);
+  m.def("sigmoid_threshold", &sigmoid_threshold);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("lovasz_hinge", &lovasz_hinge);
+  m.def("seg_metrics", &seg_metrics);
+  m.def("sgd_momentum", &sgd_momentum);
+  m.def("adam", &adam);
+  m.def("dwconv_fwd", &dwconv_fwd);
+  m.def("dwconv_dgrad", &dwconv_dgrad);
+  m.def("dwconv_wgrad", &dwconv_wgrad);
+  m.def("upsample_fwd", &upsample_fwd);
+  m.def("upsample_bwd", &upsample_bwd);
+}

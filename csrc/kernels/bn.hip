@@ -1,0 +1,315 @@
+// BatchNorm (NHWC) kernels for gfx950 — memory-bound: every pass reads/writes 16-B bf16 vectors
+// (8 channels per lane); per-channel reductions go lanes → LDS → one contiguous atomic row per
+// workgroup.  A generic scalar path handles C % 8 != 0 (the reference preset's 258-wide block2).
+//
+//   bn_stats       Σx, Σx² (when the producer conv did not fuse them into its epilogue)
+//   bn_finalize    mean, invstd, scale=γ·invstd, shift=β−mean·scale; moving averages (TF decay)
+//   bn_apply       y = act(x·scale + shift [+ res])
+//   bn_bwd_reduce  Σg, Σg·x̂   (g = dy·[y>0] when the forward had a ReLU)
+//   bn_bwd_apply   dx = γ·invstd·(g − Σg/M − x̂·Σg·x̂/M);  dres = g
+#include "common.h"
+#include "kernels.h"
+
+namespace tdl {
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ void unpack(const uint4& v, float f[8]) { unpack8(v, f); }
+
+// ---------------------------------------------------------------------------------------------
+// generic: each block covers 64 channels (one per lane) × a row range, 4 waves stride the rows
+// ---------------------------------------------------------------------------------------------
+template <int KIND>  // 0: stats(x) ; 1: bwd reduce(dy,y,x)
+__global__ void reduce_scalar_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ y,
+                                     const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                     float* __restrict__ out, long M, int C, long rows_per_block,
+                                     int relu) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    if (KIND == 0) {
+      for (long r = r0 + w; r < r1; r += 4) {
+        const float v = bf2f(a[r * C + c]);
+        s0 += v;
+        s1 += v * v;
+      }
+    } else {
+      const float mean = coef[2 * C + c], inv = coef[3 * C + c];
+      for (long r = r0 + w; r < r1; r += 4) {
+        float g = bf2f(a[r * C + c]);
+        if (relu && bf2f(y[r * C + c]) <= 0.f) g = 0.f;
+        const float xh = (bf2f(x[r * C + c]) - mean) * inv;
+        s0 += g;
+        s1 += g * xh;
+      }
+    }
+  }
+  red[0][w][lane] = s0;
+  red[1][w][lane] = s1;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    atomicAdd(out + c, red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane]);
+    atomicAdd(out + C + c, red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// vector path (C % 8 == 0, C/8 <= 256): thread = (row lane, channel vector)
+// ---------------------------------------------------------------------------------------------
+template <int KIND>
+__global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict__ a,
+                                                        const bf16_t* __restrict__ y,
+                                                        const bf16_t* __restrict__ x,
+                                                        const float* __restrict__ coef,
+                                                        float* __restrict__ out, long M, int C,
+                                                        long rows_per_block, int relu) {
+  __shared__ float red[2][NT][9];  // +1 pad against bank conflicts
+  const int cvecs = C >> 3;
+  const int rpp = NT / cvecs;  // rows per pass
+  const int t = threadIdx.x;
+  const int cv = t % cvecs, rl = t / cvecs;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s0[8], s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  if (rl < rpp) {
+    float mean[8], inv[8];
+    if (KIND == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        mean[j] = coef[2 * C + cv * 8 + j];
+        inv[j] = coef[3 * C + cv * 8 + j];
+      }
+    }
+    for (long r = r0 + rl; r < r1; r += rpp) {
+      const long off = r * C + cv * 8;
+      float va[8];
+      unpack(*(const uint4*)(a + off), va);
+      if (KIND == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s0[j] += va[j];
+          s1[j] += va[j] * va[j];
+        }
+      } else {
+        float vx[8];
+        unpack(*(const uint4*)(x + off), vx);
+        if (relu) {
+          float vy[8];
+          unpack(*(const uint4*)(y + off), vy);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) va[j] = vy[j] > 0.f ? va[j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (vx[j] - mean[j]) * inv[j];
+          s0[j] += va[j];
+          s1[j] += va[j] * xh;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][t][j] = s0[j];
+    red[1][t][j] = s1[j];
+  }
+  __syncthreads();
+  // threads t < 2*C: one output channel each (contiguous atomics)
+  for (int o = t; o < 2 * C; o += NT) {
+    const int which = o / C, c = o - which * C;
+    const int v = c >> 3, j = c & 7;
+    float s = 0.f;
+    for (int r = 0; r < rpp; ++r) s += red[which][r * cvecs + v][j];
+    atomicAdd(out + which * C + c, s);
+  }
+}
+
+template <int KIND>
+void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const float* coef, float* out,
+                   long M, int C, bool relu, hipStream_t st) {
+  if (M <= 0) return;
+  if (C % 8 == 0 && C / 8 <= NT) {
+    const int cvecs = C / 8, rpp = NT / cvecs;
+    long blocks = std::min<long>(1024, std::max<long>(1, M / (rpp * 4)));
+    long rpb = (M + blocks - 1) / blocks;
+    blocks = (M + rpb - 1) / rpb;
+    hipLaunchKernelGGL(reduce_vec_kernel<KIND>, dim3(blocks), dim3(NT), 0, st, a, y, x, coef, out, M,
+                       C, rpb, relu ? 1 : 0);
+  } else {
+    long blocks = std::min<long>(512, std::max<long>(1, M / 64));
+    long rpb = (M + blocks - 1) / blocks;
+    blocks = (M + rpb - 1) / rpb;
+    hipLaunchKernelGGL(reduce_scalar_kernel<KIND>, dim3(blocks, (C + 63) / 64), dim3(NT), 0, st, a, y,
+                       x, coef, out, M, C, rpb, relu ? 1 : 0);
+  }
+}
+
+__global__ void finalize_kernel(const float* __restrict__ stats, float* __restrict__ coef,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                float* __restrict__ rmean, float* __restrict__ rvar, int C,
+                                float count, float decay, float eps, int training) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    mean = stats[c] / count;
+    var = fmaxf(stats[C + c] / count - mean * mean, 0.f);
+    const float unb = count > 1.f ? var * count / (count - 1.f) : var;
+    rmean[c] = decay * rmean[c] + (1.f - decay) * mean;
+    rvar[c] = decay * rvar[c] + (1.f - decay) * unb;
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  const float inv = rsqrtf(var + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float sc = g * inv;
+  coef[c] = sc;
+  coef[C + c] = beta[c] - mean * sc;
+  coef[2 * C + c] = mean;
+  coef[3 * C + c] = inv;
+}
+
+__global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict__ x,
+                                                       const float* __restrict__ coef,
+                                                       const bf16_t* __restrict__ res,
+                                                       bf16_t* __restrict__ y, long nvec, int C,
+                                                       int relu) {
+  const int cvecs = C >> 3;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nvec; i += (long)gridDim.x * NT) {
+    const int cv = (int)(i % cvecs);
+    float v[8];
+    unpack(((const uint4*)x)[i], v);
+    const float4 s0 = *(const float4*)(coef + cv * 8), s1 = *(const float4*)(coef + cv * 8 + 4);
+    const float4 h0 = *(const float4*)(coef + C + cv * 8),
+                 h1 = *(const float4*)(coef + C + cv * 8 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
+    if (res) {
+      float r[8];
+      unpack(((const uint4*)res)[i], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    ((uint4*)y)[i] = pack8(v);
+  }
+}
+
+__global__ void apply_scalar_kernel(const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                    const bf16_t* __restrict__ res, bf16_t* __restrict__ y, long n,
+                                    int C, int relu) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float v = bf2f(x[i]) * coef[c] + coef[C + c];
+    if (res) v += bf2f(res[i]);
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = f2bf(v);
+  }
+}
+
+__global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
+    const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long nvec, int C, float inv_count,
+    int relu) {
+  const int cvecs = C >> 3;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nvec; i += (long)gridDim.x * NT) {
+    const int cv = (int)(i % cvecs);
+    float g[8], vx[8];
+    unpack(((const uint4*)dy)[i], g);
+    unpack(((const uint4*)x)[i], vx);
+    if (relu) {
+      float vy[8];
+      unpack(((const uint4*)y)[i], vy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = vy[j] > 0.f ? g[j] : 0.f;
+    }
+    if (dres) ((uint4*)dres)[i] = pack8(g);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cv * 8 + j;
+      const float mean = coef[2 * C + c], inv = coef[3 * C + c];
+      const float k = (gamma ? gamma[c] : 1.f) * inv;
+      const float xh = (vx[j] - mean) * inv;
+      o[j] = k * (g[j] - red[c] * inv_count - xh * red[C + c] * inv_count);
+    }
+    ((uint4*)dx)[i] = pack8(o);
+  }
+}
+
+__global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                        const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                        const float* __restrict__ red,
+                                        const float* __restrict__ gamma, bf16_t* __restrict__ dx,
+                                        bf16_t* __restrict__ dres, long n, int C, float inv_count,
+                                        int relu) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float g = bf2f(dy[i]);
+    if (relu && bf2f(y[i]) <= 0.f) g = 0.f;
+    if (dres) dres[i] = f2bf(g);
+    const float mean = coef[2 * C + c], inv = coef[3 * C + c];
+    const float k = (gamma ? gamma[c] : 1.f) * inv;
+    const float xh = (bf2f(x[i]) - mean) * inv;
+    dx[i] = f2bf(k * (g - red[c] * inv_count - xh * red[C + c] * inv_count));
+  }
+}
+
+inline int ew_blocks(long n) { return (int)std::min<long>(4096, std::max<long>(1, (n + NT - 1) / NT)); }
+
+}  // namespace
+
+void bn_stats_launch(const bf16_t* x, float* stats, long M, int C, hipStream_t st) {
+  reduce_launch<0>(x, nullptr, nullptr, nullptr, stats, M, C, false, st);
+}
+
+void bn_finalize_launch(const float* stats, float* coef, const float* gamma, const float* beta,
+                        float* rmean, float* rvar, int C, float count, float decay, float eps,
+                        bool training, hipStream_t st) {
+  hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, coef, gamma,
+                     beta, rmean, rvar, C, count, decay, eps, training ? 1 : 0);
+}
+
+void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
+                     int C, bool relu, hipStream_t st) {
+  const long n = M * C;
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8)), dim3(NT), 0, st, x, coef, res, y,
+                       n / 8, C, relu ? 1 : 0);
+  } else {
+    hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
+                       C, relu ? 1 : 0);
+  }
+}
+
+void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
+                          float* red, long M, int C, bool relu, hipStream_t st) {
+  reduce_launch<1>(dy, y, x, coef, red, M, C, relu, st);
+}
+
+void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
+                         const float* red, const float* gamma, bf16_t* dx, bf16_t* dres, long M,
+                         int C, float count, bool relu, hipStream_t st) {
+  const long n = M * C;
+  if (C % 8 == 0) {
+    hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(ew_blocks(n / 8)), dim3(NT), 0, st, dy, y, x, coef,
+                       red, gamma, dx, dres, n / 8, C, 1.f / count, relu ? 1 : 0);
+  } else {
+    hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
+                       red, gamma, dx, dres, n, C, 1.f / count, relu ? 1 : 0);
+  }
+}
+
+}  // namespace tdl

@@ -1,0 +1,214 @@
+// Depthwise k×k convolution (depth multiplier 1), NHWC bf16, weights [R][S][C] bf16, fp32 grads.
+// Memory-bound: each lane owns one 16-B channel vector (8 channels) of one output (fwd) or input
+// (dgrad) pixel; wgrad keeps R·S·8 fp32 partial sums per lane over a pixel range, reduces them
+// through LDS and issues one contiguous atomic row per workgroup.  Scalar variants handle
+// C % 8 != 0 (e.g. the single-channel Laplacian of the preprocessing).
+#include "common.h"
+#include "kernels.h"
+
+namespace tdl {
+namespace {
+
+constexpr int NT = 256;
+inline int blocks_for(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT)); }
+
+template <int V>
+__device__ __forceinline__ void ldv(const bf16_t* p, float* f) {
+  if constexpr (V == 8) unpack8(*(const uint4*)p, f);
+  else f[0] = bf2f(*p);
+}
+
+template <int V>
+__device__ __forceinline__ void stv(bf16_t* p, const float* f) {
+  if constexpr (V == 8) *(uint4*)p = pack8(f);
+  else *p = f2bf(f[0]);
+}
+
+template <int V>
+__global__ void dw_fwd_kernel(DwArgs a) {
+  const int cv = a.C / V;
+  const long total = (long)a.N * a.Ho * a.Wo * cv;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * V;
+    long p = t / cv;
+    const int wo = (int)(p % a.Wo);
+    p /= a.Wo;
+    const int ho = (int)(p % a.Ho);
+    const int n = (int)(p / a.Ho);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = a.bias ? a.bias[c + j] : 0.f;
+    for (int r = 0; r < a.R; ++r) {
+      const int hi = ho * a.sh - a.ph + r * a.dh;
+      if ((unsigned)hi >= (unsigned)a.H) continue;
+      for (int s = 0; s < a.S; ++s) {
+        const int wi = wo * a.sw - a.pw + s * a.dwl;
+        if ((unsigned)wi >= (unsigned)a.W) continue;
+        float xv[V], wv[V];
+        ldv<V>(a.x + (((long)n * a.H + hi) * a.W + wi) * a.C + c, xv);
+        ldv<V>(a.w + ((long)r * a.S + s) * a.C + c, wv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] += xv[j] * wv[j];
+      }
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] = fmaxf(acc[j], 0.f);
+    }
+    stv<V>(a.out + (((long)n * a.Ho + ho) * a.Wo + wo) * a.C + c, acc);
+  }
+}
+
+template <int V>
+__global__ void dw_dgrad_kernel(DwArgs a) {
+  const int cv = a.C / V;
+  const long total = (long)a.N * a.H * a.W * cv;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * V;
+    long p = t / cv;
+    const int w = (int)(p % a.W);
+    p /= a.W;
+    const int h = (int)(p % a.H);
+    const int n = (int)(p / a.H);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    for (int r = 0; r < a.R; ++r) {
+      int th = h + a.ph - r * a.dh;
+      if (th < 0 || th % a.sh) continue;
+      th /= a.sh;
+      if (th >= a.Ho) continue;
+      for (int s = 0; s < a.S; ++s) {
+        int tw = w + a.pw - s * a.dwl;
+        if (tw < 0 || tw % a.sw) continue;
+        tw /= a.sw;
+        if (tw >= a.Wo) continue;
+        float gv[V], wv[V];
+        ldv<V>(a.dy + (((long)n * a.Ho + th) * a.Wo + tw) * a.C + c, gv);
+        ldv<V>(a.w + ((long)r * a.S + s) * a.C + c, wv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] += gv[j] * wv[j];
+      }
+    }
+    stv<V>(a.out + (((long)n * a.H + h) * a.W + w) * a.C + c, acc);
+  }
+}
+
+// wgrad: block = (pixel range) × (channel vectors); lane owns one channel vector for all R·S taps
+template <int V, int RS>
+__global__ void __launch_bounds__(NT) dw_wgrad_kernel(DwArgs a, long pix_per_block) {
+  const int cv = a.C / V;
+  const int lanes_c = min(cv, NT);
+  const int rpp = NT / lanes_c;  // pixel lanes per pass
+  const int t = threadIdx.x;
+  const int cvi = t % lanes_c + blockIdx.y * lanes_c;
+  const int pl = t / lanes_c;
+  const long P = (long)a.N * a.Ho * a.Wo;
+  const long p0 = blockIdx.x * pix_per_block, p1 = min(P, p0 + pix_per_block);
+  float acc[RS][V];
+  float db[V];
+#pragma unroll
+  for (int k = 0; k < RS; ++k)
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[k][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) db[j] = 0.f;
+  const bool active = pl < rpp && cvi < cv;
+  const int rsa = a.R * a.S;
+  const int c = cvi * V;
+  if (active) {
+    for (long p = p0 + pl; p < p1; p += rpp) {
+      const int wo = (int)(p % a.Wo);
+      const long q = p / a.Wo;
+      const int ho = (int)(q % a.Ho);
+      const int n = (int)(q / a.Ho);
+      float gv[V];
+      ldv<V>(a.dy + p * a.C + c, gv);
+#pragma unroll
+      for (int j = 0; j < V; ++j) db[j] += gv[j];
+#pragma unroll
+      for (int k = 0; k < RS; ++k) {
+        if (k >= rsa) break;
+        const int r = k / a.S, s = k - (k / a.S) * a.S;
+        const int hi = ho * a.sh - a.ph + r * a.dh, wi = wo * a.sw - a.pw + s * a.dwl;
+        if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) continue;
+        float xv[V];
+        ldv<V>(a.x + (((long)n * a.H + hi) * a.W + wi) * a.C + c, xv);
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[k][j] += gv[j] * xv[j];
+      }
+    }
+  }
+  // reduce across pixel lanes through LDS, one tap at a time
+  __shared__ float red[NT][V + 1];
+#pragma unroll
+  for (int k = 0; k <= RS; ++k) {
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      if constexpr (true) red[t][j] = (k < RS) ? acc[k < RS ? k : 0][j] : db[j];
+    }
+    __syncthreads();
+    if (t < lanes_c * V) {
+      const int lc = t / V, j = t % V;
+      const int cc = (lc + blockIdx.y * lanes_c) * V + j;
+      if (lc + blockIdx.y * lanes_c < cv) {
+        float s = 0.f;
+        for (int r = 0; r < rpp; ++r) s += red[r * lanes_c + lc][j];
+        if (k < rsa)
+          atomicAdd(a.dw + (long)k * a.C + cc, s);
+        else if (k == RS && a.db)
+          atomicAdd(a.db + cc, s);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int V>
+void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
+  const int cv = a.C / V;
+  const int lanes_c = std::min(cv, NT);
+  const int rpp = NT / lanes_c;
+  const long P = (long)a.N * a.Ho * a.Wo;
+  long blocks = std::min<long>(1024, std::max<long>(1, P / (rpp * 8)));
+  const long ppb = (P + blocks - 1) / blocks;
+  blocks = (P + ppb - 1) / ppb;
+  dim3 grid((unsigned)blocks, (unsigned)((cv + lanes_c - 1) / lanes_c));
+  const int RS = a.R * a.S;
+  if (RS == 9)
+    hipLaunchKernelGGL((dw_wgrad_kernel<V, 9>), grid, dim3(NT), 0, st, a, ppb);
+  else if (RS == 1)
+    hipLaunchKernelGGL((dw_wgrad_kernel<V, 1>), grid, dim3(NT), 0, st, a, ppb);
+  else if (RS <= 25 && V == 1)
+    hipLaunchKernelGGL((dw_wgrad_kernel<1, 25>), grid, dim3(NT), 0, st, a, ppb);
+  else if (V == 1)
+    hipLaunchKernelGGL((dw_wgrad_kernel<1, 49>), grid, dim3(NT), 0, st, a, ppb);
+}
+
+}  // namespace
+
+void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
+  const long outs = (long)a.N * a.Ho * a.Wo * a.C;
+  if (a.C % 8 == 0)
+    hipLaunchKernelGGL(dw_fwd_kernel<8>, dim3(blocks_for(outs / 8)), dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL(dw_fwd_kernel<1>, dim3(blocks_for(outs)), dim3(NT), 0, st, a);
+}
+
+void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
+  const long ins = (long)a.N * a.H * a.W * a.C;
+  if (a.C % 8 == 0)
+    hipLaunchKernelGGL(dw_dgrad_kernel<8>, dim3(blocks_for(ins / 8)), dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL(dw_dgrad_kernel<1>, dim3(blocks_for(ins)), dim3(NT), 0, st, a);
+}
+
+void dwconv_wgrad_launch(const DwArgs& a, hipStream_t st) {
+  if (a.R * a.S > 49) return;  // host checks reject this
+  if (a.C % 8 == 0 && (a.R * a.S == 9 || a.R * a.S == 1))
+    wgrad_dispatch<8>(a, st);
+  else
+    wgrad_dispatch<1>(a, st);
+}
+
+}  // namespace tdl

@@ -1,0 +1,103 @@
+// Host-side declarations of the gfx950 kernel launchers (raw pointers + hipStream_t; no torch).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+namespace tdl {
+
+typedef uint16_t bf16_t;
+
+struct ConvArgs {
+  const bf16_t* x;   // FWD / WGRAD: input activations [N,H,W,C]
+  const bf16_t* w;   // FWD / DGRAD: weights [K,R,S,C]
+  const bf16_t* dy;  // DGRAD / WGRAD: output gradient [N,Ho,Wo,K]
+  void* out;         // FWD: y bf16 [M][ldc]; DGRAD: dx bf16 [M][ldc]; WGRAD: fp32 split slabs
+  const float* bias; // FWD: optional bias [K]
+  float* stats;      // FWD: optional BN statistics [2][K] (Σy, Σy²), accumulated
+  int N, H, W, C, K, R, S, Ho, Wo;
+  int sh, sw, ph, pw, dh, dw;
+  int M, Ng, Kg;     // GEMM dims
+  int ldc;
+  int relu;
+  int kps;           // WGRAD: K-steps per split
+};
+
+void conv_fwd_launch(const ConvArgs& a, hipStream_t st);
+void conv_dgrad_launch(const ConvArgs& a, hipStream_t st);
+void conv_wgrad_plan(int M, int Ng, long Kg, int* bm, int* bn, int* splits, int* kps);
+void conv_wgrad_launch(const ConvArgs& a, int bm, int bn, int splits, float* out, bool accumulate,
+                       hipStream_t st);
+void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st);
+
+// batch norm ---------------------------------------------------------------------------------
+void bn_stats_launch(const bf16_t* x, float* stats, long M, int C, hipStream_t st);
+void bn_finalize_launch(const float* stats, float* coef, const float* gamma, const float* beta,
+                        float* rmean, float* rvar, int C, float count, float decay, float eps,
+                        bool training, hipStream_t st);
+void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
+                     int C, bool relu, hipStream_t st);
+void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
+                          float* red, long M, int C, bool relu, hipStream_t st);
+void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
+                         const float* red, const float* gamma, bf16_t* dx, bf16_t* dres, long M,
+                         int C, float count, bool relu, hipStream_t st);
+
+// elementwise --------------------------------------------------------------------------------
+void relu_bwd_launch(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t st);
+void add_act_launch(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, bool relu,
+                    hipStream_t st);
+void scale_by_scalar_launch(const void* x, const float* s, void* y, long n, bool bf16,
+                            hipStream_t st);
+void sigmoid_threshold_launch(const void* x, bool x_bf16, float* prob, float* pred, long n,
+                              float thr, hipStream_t st);
+
+// pooling ------------------------------------------------------------------------------------
+void maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                        int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
+void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
+                        int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
+void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
+void avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
+
+// losses -------------------------------------------------------------------------------------
+void softmax_xent_launch(const void* logits, bool bf16, const int64_t* labels, float* loss,
+                         void* grad, int N, int K, float smoothing, hipStream_t st);
+void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* labels, int label_kind,
+                         float* loss, float* grad, int B, int P, hipStream_t st);
+void seg_metrics_launch(const void* labels, int label_kind, const float* pred, float* score,
+                        float* acc, int B, int P, bool kaggle, hipStream_t st);
+
+// optimizers ---------------------------------------------------------------------------------
+void sgd_momentum_launch(float* p, const float* g, float* mom, bf16_t* lowp, const uint8_t* flags,
+                         long n, float lr, float mu, float wd, float gscale, bool nesterov,
+                         hipStream_t st);
+void adam_launch(float* p, const float* g, float* m, float* v, bf16_t* lowp, const uint8_t* flags,
+                 long n, float lr_t, float b1, float b2, float eps, float wd, float gscale,
+                 hipStream_t st);
+
+// depthwise conv -----------------------------------------------------------------------------
+struct DwArgs {
+  const bf16_t* x;
+  const bf16_t* w;     // [R,S,C]
+  const float* bias;   // [C] or null
+  const bf16_t* dy;
+  bf16_t* out;
+  float* dw;           // fp32 [R,S,C]
+  float* db;           // fp32 [C]
+  int N, H, W, C, R, S, Ho, Wo, sh, sw, ph, pw, dh, dwl;
+  int relu;
+};
+void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
+void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);
+void dwconv_wgrad_launch(const DwArgs& a, hipStream_t st);
+
+// upsample (TF1 legacy bilinear with symmetric pad) -----------------------------------------
+void upsample_fwd_launch(const bf16_t* x, bf16_t* y, const int* ih, const float* wh,
+                         const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
+                         int Wo, hipStream_t st);
+void upsample_bwd_launch(const bf16_t* dy, bf16_t* dx, const int* ih, const float* wh,
+                         const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
+                         int Wo, hipStream_t st);
+
+}  // namespace tdl

@@ -1,0 +1,220 @@
+// Pooling kernels (NHWC bf16).  Max-pool stores the in-window argmax (uint8) so its backward is a
+// deterministic gather: every input pixel visits the ≤⌈k/s⌉² windows that can contain it.
+#include "common.h"
+#include "kernels.h"
+
+namespace tdl {
+namespace {
+
+constexpr int NT = 256;
+inline int blocks_for(long n) {
+  return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT));
+}
+
+template <int V>  // V = 8 (vector) or 1 (scalar)
+__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                   uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
+                                   int Wo, int k, int s, int pt, int pl) {
+  const int cv = C / V;
+  const long total = (long)N * Ho * Wo * cv;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * V;
+    long p = t / cv;
+    const int wo = (int)(p % Wo);
+    p /= Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    float best[V];
+    int arg[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      best[j] = -INFINITY;
+      arg[j] = 0;
+    }
+    for (int r = 0; r < k; ++r) {
+      const int hi = ho * s - pt + r;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int wi = wo * s - pl + q;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        const long off = (((long)n * H + hi) * W + wi) * C + c;
+        float v[V];
+        if constexpr (V == 8) {
+          unpack8(*(const uint4*)(x + off), v);
+        } else {
+          v[0] = bf2f(x[off]);
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j)
+          if (v[j] > best[j]) {
+            best[j] = v[j];
+            arg[j] = r * k + q;
+          }
+      }
+    }
+    const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+    if constexpr (V == 8) {
+      *(uint4*)(y + o) = pack8(best);
+      uint2 packed;
+      packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+      packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+      *(uint2*)(idx + o) = packed;
+    } else {
+      y[o] = f2bf(best[0]);
+      idx[o] = (uint8_t)arg[0];
+    }
+  }
+}
+
+template <int V>
+__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                   bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
+                                   int Wo, int k, int s, int pt, int pl) {
+  const int cv = C / V;
+  const long total = (long)N * H * W * cv;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * V;
+    long p = t / cv;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    // outputs ho with ho*s - pt <= h <= ho*s - pt + k - 1
+    const int hh = h + pt, ww = w + pl;
+    const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
+    const int ho_hi = min(Ho - 1, hh / s);
+    const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
+    const int wo_hi = min(Wo - 1, ww / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int r = hh - ho * s;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int q = ww - wo * s;
+        const int want = r * k + q;
+        const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+        if constexpr (V == 8) {
+          float g[8];
+          unpack8(*(const uint4*)(dy + o), g);
+          const uint2 packed = *(const uint2*)(idx + o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t word = j < 4 ? packed.x : packed.y;
+            const int a = (word >> ((j & 3) * 8)) & 0xff;
+            if (a == want) acc[j] += g[j];
+          }
+        } else {
+          if (idx[o] == want) acc[0] += bf2f(dy[o]);
+        }
+      }
+    }
+    const long off = (((long)n * H + h) * W + w) * C + c;
+    if constexpr (V == 8)
+      *(uint4*)(dx + off) = pack8(acc);
+    else
+      dx[off] = f2bf(acc[0]);
+  }
+}
+
+// global average pool: one thread per (n, channel vector), loop over HW
+__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                   int HW, int C) {
+  const int cv = C / 8;
+  const long total = (long)N * cv;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int n = (int)(t / cv), c = (int)(t % cv) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16_t* base = x + (long)n * HW * C + c;
+    for (int i = 0; i < HW; ++i) {
+      float v[8];
+      unpack8(*(const uint4*)(base + (long)i * C), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    const float inv = 1.f / HW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    *(uint4*)(y + (long)n * C + c) = pack8(acc);
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+                                   int HW, int C) {
+  const int cv = C / 8;
+  const long total = (long)N * HW * cv;
+  const float inv = 1.f / HW;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * 8;
+    const long p = t / cv;
+    const int n = (int)(p / HW);
+    float g[8];
+    unpack8(*(const uint4*)(dy + (long)n * C + c), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= inv;
+    *(uint4*)(dx + p * C + c) = pack8(g);
+  }
+}
+
+__global__ void avgpool_scalar_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                   int HW, int C) {
+  const long total = (long)N * C;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int n = (int)(t / C), c = (int)(t % C);
+    float acc = 0.f;
+    for (int i = 0; i < HW; ++i) acc += bf2f(x[((long)n * HW + i) * C + c]);
+    y[t] = f2bf(acc / HW);
+  }
+}
+
+__global__ void avgpool_scalar_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+                                   int HW, int C) {
+  const long total = (long)N * HW * C;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % C);
+    const int n = (int)(t / ((long)HW * C));
+    dx[t] = f2bf(bf2f(dy[(long)n * C + c]) / HW);
+  }
+}
+
+}  // namespace
+
+void maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                        int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<8>, dim3(blocks_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0,
+                       st, x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<1>, dim3(blocks_for((long)N * Ho * Wo * C)), dim3(NT), 0, st,
+                       x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+}
+
+void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
+                        int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<8>, dim3(blocks_for((long)N * H * W * C / 8)), dim3(NT), 0,
+                       st, dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<1>, dim3(blocks_for((long)N * H * W * C)), dim3(NT), 0, st,
+                       dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+}
+
+void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(blocks_for((long)N * C / 8)), dim3(NT), 0, st, x, y, N,
+                       HW, C);
+  else
+    hipLaunchKernelGGL(avgpool_scalar_fwd, dim3(blocks_for((long)N * C)), dim3(NT), 0, st, x, y, N, HW,
+                       C);
+}
+
+void avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(blocks_for((long)N * HW * C / 8)), dim3(NT), 0, st, dy,
+                       dx, N, HW, C);
+  else
+    hipLaunchKernelGGL(avgpool_scalar_bwd, dim3(blocks_for((long)N * HW * C)), dim3(NT), 0, st, dy, dx,
+                       N, HW, C);
+}
+
+}  // namespace tdl

@@ -1,0 +1,273 @@
+"""NHWC layer modules built on our fused ops.
+
+All activations are NHWC (bf16 on the GPU, fp32 on the CPU oracle path); conv weights are KRSC
+([Cout, R, S, Cin]) so both implicit-GEMM operands of the forward conv are K-contiguous.
+These are the L2 "layer primitives" of the reference (core/layers.py + tf.contrib.slim conv2d /
+batch_norm / max_pool2d / separable_conv2d under resnet_arg_scope, core/resnet.py:357-395).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..ops.conv import ConvGeom, conv2d, same_padding, symmetric_padding
+from ..ops.bn import batch_norm_act
+from ..ops.pool import max_pool2d, global_avg_pool
+from ..ops.dwconv import depthwise_conv2d
+from ..ops.common import compute_weight
+from . import params as _params
+
+
+# ----------------------------------------------------------------------------------------------
+# initialisers
+# ----------------------------------------------------------------------------------------------
+
+def trunc_normal_(t, std, a=-2.0, b=2.0):
+    with torch.no_grad():
+        t.normal_(0, 1)
+        while True:
+            bad = (t < a) | (t > b)
+            if not bad.any():
+                break
+            t[bad] = torch.randn(int(bad.sum()))
+        t.mul_(std)
+    return t
+
+
+def variance_scaling_(t, fan_in, factor=2.0):
+    """tf.contrib.layers.variance_scaling_initializer() default (FAN_IN, truncated normal,
+    stddev = sqrt(1.3·factor/fan_in)) — resnet_arg_scope's initializer (core/resnet.py:383)."""
+    return trunc_normal_(t, math.sqrt(1.3 * factor / fan_in))
+
+
+def kaiming_normal_fan_out_(t, fan_out):
+    with torch.no_grad():
+        return t.normal_(0, math.sqrt(2.0 / fan_out))
+
+
+# ----------------------------------------------------------------------------------------------
+# padding modes
+# ----------------------------------------------------------------------------------------------
+
+def resolve_padding(mode, H, W, R, S, stride, dilation):
+    """mode: 'SAME' (TF, possibly asymmetric), 'VALID', 'sym' (PyTorch-style (k-1)/2 both sides),
+    int, or explicit 4-tuple (top, bottom, left, right)."""
+    if isinstance(mode, tuple) and len(mode) == 4:
+        return mode
+    if isinstance(mode, int):
+        return (mode, mode, mode, mode)
+    if mode == "VALID":
+        return (0, 0, 0, 0)
+    if mode == "SAME":
+        t, b = same_padding(H, R, stride[0], dilation[0])
+        l, r = same_padding(W, S, stride[1], dilation[1])
+        return (t, b, l, r)
+    if mode == "sym":
+        t, b = symmetric_padding(R, dilation[0])
+        l, r = symmetric_padding(S, dilation[1])
+        return (t, b, l, r)
+    raise ValueError(f"unknown padding {mode}")
+
+
+# ----------------------------------------------------------------------------------------------
+# layers
+# ----------------------------------------------------------------------------------------------
+
+class Conv2d(nn.Module):
+    """NHWC conv, KRSC weight, optional bias and fused ReLU.
+
+    ``pad_cin_to``: the bf16 compute copy of the weight is zero-padded along Cin to this multiple
+    (the kernels need Cin % 8 == 0; used for the 3-channel RGB / 2-channel TGS stems whose input
+    tensors are padded the same way).  The fp32 parameter keeps its true shape.
+    """
+
+    def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, bias=False, relu=False,
+                 init="he_tf", init_std=None, pad_cin_to=None):
+        super().__init__()
+        kh, kw = (k, k) if isinstance(k, int) else k
+        self.cin, self.cout, self.k = cin, cout, (kh, kw)
+        self.stride = (stride, stride) if isinstance(stride, int) else tuple(stride)
+        self.dilation = (dilation, dilation) if isinstance(dilation, int) else tuple(dilation)
+        self.padding = padding
+        self.relu = relu
+        self.weight = nn.Parameter(torch.empty(cout, kh, kw, cin))
+        fan_in = cin * kh * kw
+        if init == "he_tf":
+            variance_scaling_(self.weight.data, fan_in)
+        elif init == "kaiming_fan_out":
+            kaiming_normal_fan_out_(self.weight.data, cout * kh * kw)
+        elif init == "trunc_normal":
+            trunc_normal_(self.weight.data, init_std)
+        elif init == "zeros":
+            self.weight.data.zero_()
+        else:
+            raise ValueError(init)
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(cout))
+            self.bias._no_decay = True
+        else:
+            self.bias = None
+        self.pad_cin_to = pad_cin_to
+        self._cin_store = (cin if not pad_cin_to else
+                           (cin + pad_cin_to - 1) // pad_cin_to * pad_cin_to)
+        self._padded = None
+        self._padded_version = -1
+        self._geom_cache = {}
+
+    # weight handling for the kernels -----------------------------------------------------------
+    def grad_needs_unpad(self):
+        return self._cin_store != self.cin
+
+    def padded_weight_shape(self):
+        return (self.cout, self.k[0], self.k[1], self._cin_store)
+
+    def unpad_grad(self, dw):
+        return dw[..., : self.cin]
+
+    def compute_weight(self, dtype):
+        w = compute_weight(self.weight, dtype)
+        if self._cin_store == self.cin:
+            return w
+        v = _params.version()
+        if (self._padded is None or self._padded_version != v or self._padded.dtype != dtype
+                or self._padded.device != w.device):
+            padded = torch.zeros(self.padded_weight_shape(), dtype=dtype, device=w.device)
+            padded[..., : self.cin] = w
+            self._padded = padded
+            self._padded_version = v
+        return self._padded
+
+    def geom(self, H, W):
+        g = self._geom_cache.get((H, W))
+        if g is None:
+            pad = resolve_padding(self.padding, H, W, self.k[0], self.k[1], self.stride,
+                                  self.dilation)
+            g = ConvGeom(self.stride, pad, self.dilation)
+            self._geom_cache[(H, W)] = g
+        return g
+
+    def forward(self, x, want_stats=False):
+        g = self.geom(x.shape[1], x.shape[2])
+        y, stats = conv2d(x, self.weight, self.bias, g, self.relu, want_stats, self)
+        return (y, stats) if want_stats else y
+
+    def extra_repr(self):
+        return (f"{self.cin}->{self.cout}, k={self.k}, s={self.stride}, d={self.dilation}, "
+                f"pad={self.padding}, bias={self.bias is not None}, relu={self.relu}")
+
+
+class BatchNorm(nn.Module):
+    """BN over the channel (last) axis with TF-style moving averages
+    (``m ← decay·m + (1−decay)·batch``).  ``scale=False`` drops γ (slim ``scale`` flag)."""
+
+    def __init__(self, c, decay=0.997, eps=1e-5, scale=True, zero_init=False):
+        super().__init__()
+        self.c, self.decay, self.eps = c, decay, eps
+        self.gamma = nn.Parameter(torch.zeros(c) if zero_init else torch.ones(c)) if scale else None
+        if self.gamma is not None:
+            self.gamma._no_decay = True
+        self.beta = nn.Parameter(torch.zeros(c))
+        self.beta._no_decay = True
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+
+    def forward(self, x, stats=None, residual=None, relu=False):
+        return batch_norm_act(x, self, stats=stats, residual=residual, relu=relu,
+                              training=self.training)
+
+
+class ConvBN(nn.Module):
+    """conv → BN → [+residual] → [ReLU] with BN statistics accumulated in the conv epilogue."""
+
+    def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, relu=True,
+                 bn_decay=0.997, bn_eps=1e-5, bn_scale=True, zero_init_gamma=False, init="he_tf",
+                 init_std=None, pad_cin_to=None):
+        super().__init__()
+        self.conv = Conv2d(cin, cout, k, stride, padding, dilation, bias=False, relu=False,
+                           init=init, init_std=init_std, pad_cin_to=pad_cin_to)
+        self.bn = BatchNorm(cout, bn_decay, bn_eps, bn_scale, zero_init_gamma)
+        self.relu = relu
+
+    def forward(self, x, residual=None):
+        if self.training:
+            y, stats = self.conv(x, want_stats=True)
+        else:
+            y, stats = self.conv(x), None
+        return self.bn(y, stats=stats, residual=residual, relu=self.relu)
+
+
+class BNAct(nn.Module):
+    """standalone BN(+ReLU) — slim.batch_norm(activation_fn=relu) pre-activation / postnorm."""
+
+    def __init__(self, c, decay=0.997, eps=1e-5, scale=True, relu=True):
+        super().__init__()
+        self.bn = BatchNorm(c, decay, eps, scale)
+        self.relu = relu
+
+    def forward(self, x):
+        return self.bn(x, relu=self.relu)
+
+
+class MaxPool(nn.Module):
+    def __init__(self, k, stride, padding="sym"):
+        super().__init__()
+        self.k, self.stride, self.padding = k, stride, padding
+
+    def forward(self, x):
+        pad = resolve_padding(self.padding, x.shape[1], x.shape[2], self.k, self.k,
+                              (self.stride, self.stride), (1, 1))
+        return max_pool2d(x, self.k, self.stride, pad)
+
+
+class GlobalAvgPool(nn.Module):
+    def __init__(self, keepdims=False):
+        super().__init__()
+        self.keepdims = keepdims
+
+    def forward(self, x):
+        return global_avg_pool(x, self.keepdims)
+
+
+class Linear(nn.Module):
+    """Fully connected layer = 1×1 conv on a [N, 1, 1, C] view (same MFMA GEMM kernels)."""
+
+    def __init__(self, cin, cout, bias=True, init_std=None):
+        super().__init__()
+        self.conv = Conv2d(cin, cout, 1, bias=bias, padding=0, init="trunc_normal" if init_std
+                           else "he_tf", init_std=init_std)
+        if init_std is None:
+            bound = 1.0 / math.sqrt(cin)
+            with torch.no_grad():
+                self.conv.weight.uniform_(-bound, bound)
+
+    def forward(self, x):
+        N, C = x.shape
+        y = self.conv(x.reshape(N, 1, 1, C))
+        return y.reshape(N, -1)
+
+
+class DepthwiseConv2d(nn.Module):
+    """Depthwise k×k (depth multiplier 1), weight [R, S, C], optional bias + ReLU."""
+
+    def __init__(self, c, k=3, stride=1, padding="SAME", dilation=1, bias=True, relu=True,
+                 init_std=0.33):
+        super().__init__()
+        self.c, self.k = c, k
+        self.stride = (stride, stride)
+        self.dilation = (dilation, dilation)
+        self.padding = padding
+        self.relu = relu
+        self.weight = nn.Parameter(trunc_normal_(torch.empty(k, k, c), init_std))
+        if bias:
+            self.bias = nn.Parameter(torch.zeros(c))
+            self.bias._no_decay = True
+        else:
+            self.bias = None
+
+    def forward(self, x):
+        pad = resolve_padding(self.padding, x.shape[1], x.shape[2], self.k, self.k, self.stride,
+                              self.dilation)
+        return depthwise_conv2d(x, self.weight, self.bias, ConvGeom(self.stride, pad,
+                                                                    self.dilation), self.relu)

@@ -1,0 +1,134 @@
+"""Standard ImageNet ResNets (v1.5: stride on the 3×3 conv) in NHWC — the north-star workloads of
+BASELINE.json (ResNet-18/50/152 at 224×224).  Not present in the reference, whose only ResNet is the
+beta-variant DeepLab encoder (core/resnet.py:284-354, see :mod:`models.deeplab`); the reference's
+optional classification head (core/resnet.py:246-256) is what ``num_classes`` reproduces.
+
+Every conv is followed by BN whose batch statistics are accumulated in the conv's epilogue; the
+bottleneck's last BN, the residual add and the ReLU are a single fused kernel pass.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .layers import ConvBN, MaxPool, GlobalAvgPool, Linear
+
+_CFG = {
+    18: ("basic", (2, 2, 2, 2)),
+    34: ("basic", (3, 4, 6, 3)),
+    50: ("bottleneck", (3, 4, 6, 3)),
+    101: ("bottleneck", (3, 4, 23, 3)),
+    152: ("bottleneck", (3, 8, 36, 3)),
+}
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, width, stride, bn_kw):
+        super().__init__()
+        self.conv1 = ConvBN(cin, width, 3, stride, "sym", relu=True, init="kaiming_fan_out", **bn_kw)
+        self.conv2 = ConvBN(width, width, 3, 1, "sym", relu=True, init="kaiming_fan_out", **bn_kw)
+        self.downsample = None
+        if stride != 1 or cin != width:
+            self.downsample = ConvBN(cin, width, 1, stride, 0, relu=False,
+                                     init="kaiming_fan_out", **bn_kw)
+
+    def forward(self, x):
+        sc = x if self.downsample is None else self.downsample(x)
+        out = self.conv1(x)
+        return self.conv2(out, residual=sc)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride, bn_kw):
+        super().__init__()
+        out = width * 4
+        self.conv1 = ConvBN(cin, width, 1, 1, 0, relu=True, init="kaiming_fan_out", **bn_kw)
+        self.conv2 = ConvBN(width, width, 3, stride, "sym", relu=True, init="kaiming_fan_out",
+                            **bn_kw)
+        self.conv3 = ConvBN(width, out, 1, 1, 0, relu=True, init="kaiming_fan_out", **bn_kw)
+        self.downsample = None
+        if stride != 1 or cin != out:
+            self.downsample = ConvBN(cin, out, 1, stride, 0, relu=False, init="kaiming_fan_out",
+                                     **bn_kw)
+
+    def forward(self, x):
+        sc = x if self.downsample is None else self.downsample(x)
+        y = self.conv1(x)
+        y = self.conv2(y)
+        return self.conv3(y, residual=sc)
+
+
+class ResNet(nn.Module):
+    """ResNet-{18,34,50,101,152}. Input NHWC [N, H, W, 3 or 8] (channels 3..7 zero)."""
+
+    def __init__(self, depth=50, num_classes=1000, bn_decay=0.9, bn_eps=1e-5, in_channels=3,
+                 width=64):
+        super().__init__()
+        kind, layers = _CFG[depth]
+        block = Bottleneck if kind == "bottleneck" else BasicBlock
+        bn_kw = dict(bn_decay=bn_decay, bn_eps=bn_eps)
+        self.depth = depth
+        self.in_channels = in_channels
+        self.stem = ConvBN(in_channels, width, 7, 2, "sym", relu=True, init="kaiming_fan_out",
+                           pad_cin_to=8, **bn_kw)
+        self.pool = MaxPool(3, 2, "sym")
+        stages = []
+        cin = width
+        for i, n in enumerate(layers):
+            w = width * (2 ** i)
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(block(cin, w, stride, bn_kw))
+                cin = w * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.gap = GlobalAvgPool()
+        self.num_features = cin
+        self.fc = Linear(cin, num_classes) if num_classes else None
+
+    @property
+    def input_channels_padded(self):
+        return self.stem.conv._cin_store
+
+    def forward_features(self, x):
+        if x.shape[-1] != self.stem.conv._cin_store:
+            x = nn.functional.pad(x, (0, self.stem.conv._cin_store - x.shape[-1]))
+        x = self.stem(x)
+        x = self.pool(x)
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        x = self.layer4(x)
+        return x
+
+    def forward(self, x):
+        x = self.forward_features(x)
+        x = self.gap(x)
+        if self.fc is not None:
+            x = self.fc(x)
+        return x
+
+
+def resnet18(**kw):
+    return ResNet(18, **kw)
+
+
+def resnet34(**kw):
+    return ResNet(34, **kw)
+
+
+def resnet50(**kw):
+    return ResNet(50, **kw)
+
+
+def resnet101(**kw):
+    return ResNet(101, **kw)
+
+
+def resnet152(**kw):
+    return ResNet(152, **kw)

@@ -1,0 +1,130 @@
+"""Xception-41 (DeepLab variant), NHWC — the *intended* network of core/xception.py:405-465.
+
+The reference file is not importable (``resnet_utils`` missing, D8), builds only the last unit of
+each block (scope dedented out of the loop, D9) and has no BN on its convs (D10); this is the
+intended DeepLab Xception-41: BN after every conv, 8-unit middle flow, depthwise-separable convs
+with explicit ``fixed_padding`` at stride 2 (core/xception.py:18-35,38-128), skip connections
+'conv' / 'sum' / 'none' (:131-228), atrous output-stride control (:231-292) and optional
+classification head (global pool + logits) for the north-star Xception 299×299 benchmark.
+
+The depthwise 3×3 (+BN) runs on the HIP depthwise kernels; the pointwise 1×1 convs on the MFMA
+GEMM kernels with BN statistics fused into their epilogue.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .layers import ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear
+from ..ops.elementwise import relu as relu_op, add as add_op
+
+
+def _fixed_pad(k, rate):
+    keff = k + (k - 1) * (rate - 1)
+    beg = (keff - 1) // 2
+    return (beg, keff - 1 - beg, beg, keff - 1 - beg)
+
+
+class SeparableConvBN(nn.Module):
+    """separable_conv2d_same (split form): depthwise k×k (stride, rate) → BN [→ReLU] →
+    pointwise 1×1 → BN [→ReLU]."""
+
+    def __init__(self, cin, cout, stride, rate, act_inside, bn_kw):
+        super().__init__()
+        pad = "SAME" if stride == 1 else _fixed_pad(3, rate)
+        self.depthwise = DepthwiseConv2d(cin, 3, stride, pad, rate, bias=False, relu=False,
+                                         init_std=0.33)
+        self.dw_bn = BatchNorm(cin, bn_kw["bn_decay"], bn_kw["bn_eps"])
+        self.pointwise = ConvBN(cin, cout, 1, 1, 0, relu=act_inside, init="trunc_normal",
+                                init_std=0.06, **bn_kw)
+        self.act_inside = act_inside
+
+    def forward(self, x):
+        y = self.depthwise(x)
+        y = self.dw_bn(y, relu=self.act_inside)
+        return self.pointwise(y)
+
+
+class XceptionModule(nn.Module):
+    def __init__(self, cin, depth_list, skip, stride, rate, unit_rates, act_inside, bn_kw):
+        super().__init__()
+        self.skip = skip
+        self.act_inside = act_inside
+        convs = []
+        c = cin
+        for i in range(3):
+            convs.append(SeparableConvBN(c, depth_list[i], stride if i == 2 else 1,
+                                         rate * unit_rates[i], act_inside, bn_kw))
+            c = depth_list[i]
+        self.convs = nn.ModuleList(convs)
+        self.shortcut = (ConvBN(cin, depth_list[-1], 1, stride, 0, relu=False, **bn_kw)
+                         if skip == "conv" else None)
+        self.out_channels = depth_list[-1]
+
+    def forward(self, x):
+        r = x
+        for conv in self.convs:
+            if not self.act_inside:
+                r = relu_op(r)
+            r = conv(r)
+        if self.skip == "conv":
+            return self.shortcut(x, residual=r)  # BN(shortcut) + residual, no act
+        if self.skip == "sum":
+            return add_op(r, x)
+        return r
+
+
+class Xception41(nn.Module):
+    def __init__(self, num_classes=1000, in_channels=3, output_stride=None, multi_grid=None,
+                 bn_decay=0.9997, bn_eps=1e-3):
+        super().__init__()
+        bn_kw = dict(bn_decay=bn_decay, bn_eps=bn_eps)
+        self.conv1_1 = ConvBN(in_channels, 32, 3, 2, _fixed_pad(3, 1), relu=True, pad_cin_to=8,
+                              **bn_kw)
+        self.conv1_2 = ConvBN(32, 64, 3, 1, "SAME", relu=True, **bn_kw)
+        mg = list(multi_grid) if multi_grid else [1, 1, 1]
+        spec = [
+            ("entry_flow/block1", [128, 128, 128], "conv", 1, 2, [1, 1, 1], False),
+            ("entry_flow/block2", [256, 256, 256], "conv", 1, 2, [1, 1, 1], False),
+            ("entry_flow/block3", [728, 728, 728], "conv", 1, 2, [1, 1, 1], False),
+            ("middle_flow/block1", [728, 728, 728], "sum", 8, 1, [1, 1, 1], False),
+            ("exit_flow/block1", [728, 1024, 1024], "conv", 1, 2, [1, 1, 1], False),
+            ("exit_flow/block2", [1536, 1536, 2048], "none", 1, 1, mg, True),
+        ]
+        target = None if output_stride is None else output_stride // 2
+        if output_stride is not None and output_stride % 2 != 0:
+            raise ValueError("The output_stride needs to be a multiple of 2.")
+        current, rate = 1, 1
+        self.units = nn.ModuleList()
+        self.unit_names = []
+        cin = 64
+        for name, depths, skip, n, stride, urates, act in spec:
+            for u in range(n):
+                if target is not None and current == target:
+                    m = XceptionModule(cin, depths, skip, 1, rate, urates, act, bn_kw)
+                    rate *= stride
+                else:
+                    m = XceptionModule(cin, depths, skip, stride, 1, urates, act, bn_kw)
+                    current *= stride
+                cin = m.out_channels
+                self.units.append(m)
+                self.unit_names.append(f"{name}/unit_{u + 1}")
+        if target is not None and current != target:
+            raise ValueError("The target output_stride cannot be reached.")
+        self.num_features = cin
+        self.gap = GlobalAvgPool() if num_classes else None
+        self.fc = Linear(cin, num_classes) if num_classes else None
+
+    def forward(self, x):
+        if x.shape[-1] != self.conv1_1.conv._cin_store:
+            x = nn.functional.pad(x, (0, self.conv1_1.conv._cin_store - x.shape[-1]))
+        x = self.conv1_2(self.conv1_1(x))
+        for u in self.units:
+            x = u(x)
+        if self.fc is not None:
+            x = self.fc(self.gap(x))
+        return x
+
+
+def xception_41(num_classes=1000, **kw):
+    return Xception41(num_classes=num_classes, **kw)

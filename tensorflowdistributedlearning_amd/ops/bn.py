@@ -1,0 +1,166 @@
+"""Batch normalisation (training: batch statistics + moving averages; eval: moving statistics)
+fused with the optional residual add and ReLU, NHWC.
+
+GPU kernels (``csrc/kernels/bn.hip``):
+  * ``bn_stats``       per-channel Σx, Σx² (only when the producing conv did not already
+                       accumulate them in its epilogue — see ``conv2d(want_stats=True)``);
+  * ``bn_finalize``    mean / invstd / scale / shift + moving-average update in one tiny launch;
+  * ``bn_apply``       y = act(x·scale + shift [+ residual]) — one vectorised pass;
+  * ``bn_bwd_reduce``  Σg, Σg·x̂ with g = dy·[y>0];
+  * ``bn_bwd_apply``   dx = γ·invstd·(g − Σg/M − x̂·Σg·x̂/M), plus g for the residual branch.
+
+Reference parity: ``slim.batch_norm`` under ``resnet_arg_scope`` (core/resnet.py:357-395,71,126,242)
+with ``UPDATE_OPS`` moving averages (model.py:465-467) — TF FusedBatchNorm/FusedBatchNormGrad
+(SURVEY N4, N5, K6, K8, K19).  Moving average: ``m ← decay·m + (1−decay)·batch`` (TF convention,
+``decay`` = BATCH_NORM_DECAY); the moving variance uses the unbiased batch variance.
+"""
+from __future__ import annotations
+
+import torch
+
+from .common import on_gpu, ext, deliver_grad
+
+
+# ----------------------------------------------------------------------------------------------
+# raw ops
+# ----------------------------------------------------------------------------------------------
+
+def bn_stats(x, stats=None):
+    C = x.shape[-1]
+    if stats is None:
+        stats = torch.zeros((2, C), device=x.device, dtype=torch.float32)
+    if on_gpu(x):
+        ext().bn_stats(x, stats)
+        return stats
+    xf = x.float().reshape(-1, C)
+    stats[0] += xf.sum(0)
+    stats[1] += (xf * xf).sum(0)
+    return stats
+
+
+def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps, training):
+    """Returns fp32 [4, C] = (scale, shift, mean, invstd); updates moving stats in training."""
+    C = beta.shape[0]
+    if on_gpu(beta):
+        coef = torch.empty((4, C), device=beta.device, dtype=torch.float32)
+        ext().bn_finalize(stats if training else None, coef, gamma, beta, running_mean, running_var,
+                          float(count), float(decay), float(eps), bool(training))
+        return coef
+    g = gamma.detach().float() if gamma is not None else torch.ones_like(beta)
+    if training:
+        mean = stats[0] / count
+        var = (stats[1] / count - mean * mean).clamp_min(0.0)
+        with torch.no_grad():
+            unbiased = var * (count / max(count - 1, 1))
+            running_mean.mul_(decay).add_((1 - decay) * mean)
+            running_var.mul_(decay).add_((1 - decay) * unbiased)
+    else:
+        mean = running_mean.float()
+        var = running_var.float()
+    invstd = torch.rsqrt(var + eps)
+    scale = g * invstd
+    shift = beta.detach().float() - mean * scale
+    return torch.stack([scale, shift, mean, invstd])
+
+
+def bn_apply(x, coef, residual=None, relu=True):
+    if on_gpu(x):
+        y = torch.empty_like(x)
+        ext().bn_apply(x, coef, residual, y, bool(relu))
+        return y
+    C = x.shape[-1]
+    y = x.float() * coef[0].view(*([1] * (x.dim() - 1)), C) + coef[1]
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def bn_bwd_reduce(dy, y, x, coef, relu):
+    """fp32 [2, C]: (Σg, Σg·x̂), g = dy·[y>0] if relu else dy."""
+    C = x.shape[-1]
+    if on_gpu(dy):
+        red = torch.zeros((2, C), device=dy.device, dtype=torch.float32)
+        ext().bn_bwd_reduce(dy, y, x, coef, red, bool(relu))
+        return red
+    g = dy.float().reshape(-1, C)
+    if relu:
+        g = g * (y.float().reshape(-1, C) > 0)
+    xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
+    return torch.stack([g.sum(0), (g * xhat).sum(0)])
+
+
+def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres):
+    """dx (same dtype as x) and optionally the masked gradient g for the residual branch."""
+    C = x.shape[-1]
+    if on_gpu(dy):
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(dy) if want_dres else None
+        ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, float(count), bool(relu))
+        return dx, dres
+    g = dy.float().reshape(-1, C)
+    if relu:
+        g = g * (y.float().reshape(-1, C) > 0)
+    xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
+    gam = gamma.detach().float() if gamma is not None else torch.ones(C)
+    k = gam * coef[3]
+    dx = k * (g - red[0] / count - xhat * red[1] / count)
+    dres = g.reshape(dy.shape).to(dy.dtype) if want_dres else None
+    return dx.reshape(x.shape).to(x.dtype), dres
+
+
+# ----------------------------------------------------------------------------------------------
+# autograd
+# ----------------------------------------------------------------------------------------------
+
+class _BatchNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training):
+        C = x.shape[-1]
+        count = x.numel() // C
+        if training:
+            if stats is None or stats.numel() == 0:
+                stats = bn_stats(x)
+        coef = bn_finalize(stats, count, gamma, beta, bn.running_mean, bn.running_var,
+                           bn.decay, bn.eps, training)
+        y = bn_apply(x, coef, residual, relu)
+        ctx.relu = relu
+        ctx.count = count
+        ctx.training = training
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y, coef, gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, coef, gamma, beta = ctx.saved_tensors
+        dy = dy.contiguous()
+        relu = ctx.relu
+        if not ctx.training:
+            # eval-mode backward (rare): treat statistics as constants
+            C = x.shape[-1]
+            g = dy.float().reshape(-1, C)
+            if relu:
+                g = g * (y.float().reshape(-1, C) > 0)
+            dx = (g * coef[0]).reshape(x.shape).to(x.dtype)
+            xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
+            if gamma is not None and gamma.requires_grad:
+                deliver_grad(gamma, (g * xhat).sum(0))
+            if beta.requires_grad:
+                deliver_grad(beta, g.sum(0))
+            dres = g.reshape(dy.shape).to(dy.dtype) if ctx.has_res else None
+            return dx, None, None, None, dres, None, None, None
+        red = bn_bwd_reduce(dy, y, x, coef, relu)
+        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gamma, ctx.count, relu, ctx.has_res)
+        if gamma is not None and gamma.requires_grad:
+            deliver_grad(gamma, red[1])
+        if beta.requires_grad:
+            deliver_grad(beta, red[0])
+        return dx, None, None, None, dres, None, None, None
+
+
+def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True):
+    """act(BN(x) [+ residual]).  ``bn`` is a :class:`models.layers.BatchNorm` (holds γ, β and the
+    moving statistics).  ``stats`` may carry Σx, Σx² already accumulated by the producer conv."""
+    return _BatchNormActFn.apply(x, stats, bn.gamma, bn.beta, residual, bn, relu, training)

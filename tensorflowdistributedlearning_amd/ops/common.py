@@ -1,0 +1,72 @@
+"""Shared helpers for ops: device dispatch, gradient delivery into flat buffers.
+
+Parameters of our models live in flat buffers (see :mod:`models.params`):
+``p.data`` is a view of the fp32 master buffer, ``p.grad`` a view of the fp32 gradient buffer and
+``p._lowp`` a view of the bf16 compute copy.  Our autograd Functions never hand weight gradients back
+to autograd; they write them straight into ``p.grad`` (the HIP wgrad kernels write there directly)
+and then call ``p._grad_hook(p)`` so the data-parallel bucketer can launch the all-reduce of a
+bucket as soon as its last gradient lands (SURVEY.md §5.8 "GradBucketer").  This replaces the
+reference's MirroredStrategy gradient aggregation (model.py:114-116, Test.ipynb:200).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+
+def on_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def ext():
+    return _native.ext()
+
+
+def compute_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """The tensor the kernels read for parameter ``p`` (bf16 shadow on GPU, else fp32 master)."""
+    lp = getattr(p, "_lowp", None)
+    if lp is not None and lp.dtype == dtype:
+        return lp
+    if p.dtype == dtype:
+        return p.detach()
+    return p.detach().to(dtype)
+
+
+def grad_target(p: torch.Tensor):
+    """Return (tensor, overwrite) where a kernel may write p's gradient directly.
+
+    ``overwrite`` is True when this is the first contribution of the step (the kernel may store
+    instead of accumulate)."""
+    g = p.grad
+    if g is None:
+        return None, True
+    return g, bool(getattr(p, "_grad_fresh", True))
+
+
+def deliver_grad(p: torch.Tensor, g: torch.Tensor | None = None, written: bool = False):
+    """Deliver gradient ``g`` of parameter ``p``.
+
+    If ``written`` the kernel already stored the gradient into ``p.grad``.  Otherwise ``g`` is
+    copied (first contribution) or accumulated into ``p.grad``."""
+    if not written:
+        g = g.to(torch.float32).reshape(p.shape)
+        if p.grad is None:
+            p.grad = g.clone()
+        elif getattr(p, "_grad_fresh", True):
+            p.grad.copy_(g)
+        else:
+            p.grad.add_(g)
+    p._grad_fresh = False
+    hook = getattr(p, "_grad_hook", None)
+    if hook is not None:
+        hook(p)
+
+
+def reset_grad_state(params):
+    for p in params:
+        p._grad_fresh = True
+
+
+def param_requires_grad(p) -> bool:
+    return p is not None and p.requires_grad and torch.is_grad_enabled()

@@ -1,0 +1,223 @@
+"""2-D convolution (dense, strided, dilated) in NHWC with KRSC weights.
+
+GPU path: hand-written gfx950 MFMA implicit-GEMM kernels (``csrc/kernels/conv_gemm.hip``):
+``conv_fwd`` (A = gathered input, B = weights, optional bias / ReLU / BN-statistics epilogue),
+``conv_dgrad`` (A = gathered output-gradient, B = weights read through the LDS transpose path) and
+``conv_wgrad`` (split-K over N·Ho·Wo, both operands through the LDS transpose path, fp32 slab
+reduction straight into the flat gradient buffer).
+
+CPU path: ``torch.nn.functional.conv2d`` in fp32 — the numerics oracle.
+
+Reference parity: replaces every ``layers_lib.conv2d`` / ``slim.conv2d`` of the reference
+(core/resnet.py:75,79,83,130,134,137,142,164-166,250,449,466,471,482,487; core/layers.py:43;
+core/xception.py:111,212) which lowered to cuDNN Conv2D/BackpropInput/BackpropFilter
+and, for ``rate>1``, to SpaceToBatchND (N9) — here dilation is native in the address generator.
+Padding is explicit (top, bottom, left, right) so TF ``SAME`` (asymmetric at stride 2) is exact.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    stride: tuple = (1, 1)
+    padding: tuple = (0, 0, 0, 0)  # top, bottom, left, right
+    dilation: tuple = (1, 1)
+
+    def out_hw(self, H, W, R, S):
+        sh, sw = self.stride
+        pt, pb, pl, pr = self.padding
+        dh, dw = self.dilation
+        Ho = (H + pt + pb - dh * (R - 1) - 1) // sh + 1
+        Wo = (W + pl + pr - dw * (S - 1) - 1) // sw + 1
+        return Ho, Wo
+
+
+def same_padding(size, k, stride, dilation=1):
+    """TF 'SAME' padding (before, after) for one spatial dim."""
+    keff = k + (k - 1) * (dilation - 1)
+    out = -(-size // stride)
+    total = max((out - 1) * stride + keff - size, 0)
+    return total // 2, total - total // 2
+
+
+def symmetric_padding(k, dilation=1):
+    keff = k + (k - 1) * (dilation - 1)
+    p = (keff - 1) // 2
+    return p, keff - 1 - p
+
+
+# ----------------------------------------------------------------------------------------------
+# reference (CPU / oracle) implementations, fp32
+# ----------------------------------------------------------------------------------------------
+
+def ref_conv_fwd(x, w, geom: ConvGeom, bias=None):
+    pt, pb, pl, pr = geom.padding
+    xt = F.pad(x.permute(0, 3, 1, 2).float(), (pl, pr, pt, pb))
+    y = F.conv2d(xt, w.permute(0, 3, 1, 2).float(), None if bias is None else bias.float(),
+                 stride=geom.stride, dilation=geom.dilation)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+def ref_conv_dgrad(dy, w, x_shape, geom: ConvGeom):
+    N, H, W, C = x_shape
+    pt, pb, pl, pr = geom.padding
+    Hp, Wp = H + pt + pb, W + pl + pr
+    dxp = torch.nn.grad.conv2d_input((N, C, Hp, Wp), w.permute(0, 3, 1, 2).float(),
+                                     dy.permute(0, 3, 1, 2).float(), stride=geom.stride,
+                                     dilation=geom.dilation)
+    dx = dxp[:, :, pt:pt + H, pl:pl + W]
+    return dx.permute(0, 2, 3, 1).contiguous()
+
+
+def ref_conv_wgrad(dy, x, w_shape, geom: ConvGeom):
+    K, R, S, C = w_shape
+    pt, pb, pl, pr = geom.padding
+    xt = F.pad(x.permute(0, 3, 1, 2).float(), (pl, pr, pt, pb))
+    dw = torch.nn.grad.conv2d_weight(xt, (K, C, R, S), dy.permute(0, 3, 1, 2).float(),
+                                     stride=geom.stride, dilation=geom.dilation)
+    return dw.permute(0, 2, 3, 1).contiguous()
+
+
+# ----------------------------------------------------------------------------------------------
+# raw ops (dispatch)
+# ----------------------------------------------------------------------------------------------
+
+def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out_dtype=None):
+    """y = conv(x, w) (+bias) (relu).  If ``stats`` (fp32 [2, K]) is given, per-channel sum and
+    sum of squares of the *stored* output are accumulated into it (BN statistics epilogue)."""
+    N, H, W, C = x.shape
+    K, R, S, Cw = w.shape
+    assert C == Cw, f"channel mismatch {C} vs {Cw}"
+    Ho, Wo = geom.out_hw(H, W, R, S)
+    if on_gpu(x):
+        y = torch.empty((N, Ho, Wo, K), device=x.device, dtype=out_dtype or x.dtype)
+        ext().conv_fwd(x, w, y, bias, stats, geom.stride[0], geom.stride[1], geom.padding[0],
+                       geom.padding[2], geom.dilation[0], geom.dilation[1], bool(relu))
+        return y
+    y = ref_conv_fwd(x, w, geom, bias)
+    if relu:
+        y = torch.relu(y)
+    y = y.to(out_dtype or x.dtype)
+    if stats is not None:
+        yf = y.float().reshape(-1, K)
+        stats[0] += yf.sum(0)
+        stats[1] += (yf * yf).sum(0)
+    return y
+
+
+def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None):
+    if on_gpu(dy):
+        dx = torch.empty(x_shape, device=dy.device, dtype=out_dtype or dy.dtype)
+        ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
+                         geom.padding[2], geom.dilation[0], geom.dilation[1])
+        return dx
+    return ref_conv_dgrad(dy, w, x_shape, geom).to(out_dtype or dy.dtype)
+
+
+def conv_wgrad(dy, x, w_shape, geom: ConvGeom, out=None, accumulate=False, bias_grad=None):
+    """dW (fp32, KRSC).  Writes into ``out`` if given (overwrite, or add when ``accumulate``).
+    If ``bias_grad`` (fp32 [K]) is given, the column sums of dy are written into it too."""
+    if on_gpu(dy):
+        if out is None:
+            out = torch.empty(w_shape, device=dy.device, dtype=torch.float32)
+            accumulate = False
+        ext().conv_wgrad(dy, x, out, bias_grad, geom.stride[0], geom.stride[1], geom.padding[0],
+                         geom.padding[2], geom.dilation[0], geom.dilation[1], bool(accumulate))
+        return out
+    dw = ref_conv_wgrad(dy, x, w_shape, geom)
+    if bias_grad is not None:
+        bias_grad.copy_(dy.float().reshape(-1, dy.shape[-1]).sum(0))
+    if out is None:
+        return dw
+    if accumulate:
+        out.add_(dw.reshape(out.shape))
+    else:
+        out.copy_(dw.reshape(out.shape))
+    return out
+
+
+def relu_bwd(dy, y):
+    """dy * (y > 0) — GPU: fused elementwise kernel."""
+    if on_gpu(dy):
+        dx = torch.empty_like(dy)
+        ext().relu_bwd(dy, y, dx)
+        return dx
+    return (dy.float() * (y.float() > 0)).to(dy.dtype)
+
+
+# ----------------------------------------------------------------------------------------------
+# autograd
+# ----------------------------------------------------------------------------------------------
+
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer):
+        w = layer.compute_weight(x.dtype) if layer is not None else compute_weight(weight, x.dtype)
+        stats = None
+        if want_stats:
+            stats = torch.zeros((2, w.shape[0]), device=x.device, dtype=torch.float32)
+        b = None if bias is None else bias.detach()
+        y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats)
+        ctx.geom = geom
+        ctx.relu = relu
+        ctx.layer = layer
+        ctx.x_shape = tuple(x.shape)
+        ctx.save_for_backward(x, weight, bias, y if relu else None)
+        if stats is None:
+            stats = torch.empty(0, device=x.device)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        x, weight, bias, y = ctx.saved_tensors
+        geom = ctx.geom
+        dy = dy.contiguous()
+        if ctx.relu:
+            dy = relu_bwd(dy, y)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
+                compute_weight(weight, dy.dtype)
+            dx = conv_dgrad(dy, w, ctx.x_shape, geom)
+        want_bias = bias is not None and bias.requires_grad
+        bias_buf, bias_direct = None, False
+        if want_bias:
+            bt, bfresh = grad_target(bias)
+            bias_direct = bt is not None and bfresh
+            bias_buf = bt if bias_direct else torch.empty(bias.shape, device=dy.device,
+                                                          dtype=torch.float32)
+        if weight.requires_grad:
+            target, fresh = grad_target(weight)
+            if ctx.layer is not None and ctx.layer.grad_needs_unpad():
+                dw = conv_wgrad(dy, x, ctx.layer.padded_weight_shape(), geom, bias_grad=bias_buf)
+                deliver_grad(weight, ctx.layer.unpad_grad(dw))
+            elif target is not None:
+                conv_wgrad(dy, x, tuple(weight.shape), geom, out=target, accumulate=not fresh,
+                           bias_grad=bias_buf)
+                deliver_grad(weight, written=True)
+            else:
+                dw = conv_wgrad(dy, x, tuple(weight.shape), geom, bias_grad=bias_buf)
+                deliver_grad(weight, dw)
+        elif want_bias:
+            bias_buf.copy_(dy.float().reshape(-1, dy.shape[-1]).sum(0))
+        if want_bias:
+            if bias_direct:
+                deliver_grad(bias, written=True)
+            else:
+                deliver_grad(bias, bias_buf)
+        return dx, None, None, None, None, None, None
+
+
+def conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False, want_stats=False,
+           layer=None):
+    """Differentiable NHWC conv. Returns (y, stats) where stats is fp32 [2, K] (sum, sumsq of y)
+    when ``want_stats`` else an empty tensor."""
+    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer)

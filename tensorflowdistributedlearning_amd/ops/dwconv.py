@@ -1,0 +1,106 @@
+"""Depthwise k×k convolution (depth_multiplier 1), NHWC, weights [R, S, C], dilation/stride/
+explicit padding, optional fused bias + ReLU.
+
+GPU kernels (``csrc/kernels/dwconv.hip``): memory-bound, so no MFMA — each thread owns 8 channels
+(one 16-B bf16 vector) of one output pixel; the wgrad is a per-(r, s, c-vector) reduction over
+N·Ho·Wo with a per-block partial + fp32 atomic, bias-grad fused.
+
+Reference parity: ``slim.separable_conv2d(num_outputs=None)`` (core/layers.py:34-42,
+core/xception.py:90-110) and the fixed Laplacian of preprocessing.py:11-30.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+from .conv import ConvGeom
+
+
+def ref_dw_fwd(x, w, geom: ConvGeom, bias=None):
+    C = x.shape[-1]
+    pt, pb, pl, pr = geom.padding
+    xt = F.pad(x.permute(0, 3, 1, 2).float(), (pl, pr, pt, pb))
+    wt = w.float().permute(2, 0, 1).unsqueeze(1)  # [C,1,R,S]
+    y = F.conv2d(xt, wt, None if bias is None else bias.float(), stride=geom.stride,
+                 dilation=geom.dilation, groups=C)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _DwConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, geom, relu):
+        w = compute_weight(weight, x.dtype)
+        N, H, W, C = x.shape
+        R, S, _ = w.shape
+        Ho, Wo = geom.out_hw(H, W, R, S)
+        if on_gpu(x):
+            y = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
+            ext().dwconv_fwd(x, w, None if bias is None else bias.detach(), y, geom.stride[0],
+                             geom.stride[1], geom.padding[0], geom.padding[2], geom.dilation[0],
+                             geom.dilation[1], bool(relu))
+        else:
+            y = ref_dw_fwd(x, w, geom, None if bias is None else bias.detach())
+            if relu:
+                y = torch.relu(y)
+            y = y.to(x.dtype)
+        ctx.geom, ctx.relu = geom, relu
+        ctx.save_for_backward(x, weight, bias, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, y = ctx.saved_tensors
+        geom = ctx.geom
+        dy = dy.contiguous()
+        if on_gpu(dy):
+            if ctx.relu:
+                g = torch.empty_like(dy)
+                ext().relu_bwd(dy, y, g)
+            else:
+                g = dy
+            w = compute_weight(weight, dy.dtype)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty_like(x)
+                ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
+                                   geom.padding[2], geom.dilation[0], geom.dilation[1])
+            dw = torch.zeros(weight.shape, device=dy.device, dtype=torch.float32)
+            db = torch.zeros(x.shape[-1], device=dy.device, dtype=torch.float32) \
+                if bias is not None else None
+            ext().dwconv_wgrad(g, x, dw, db, geom.stride[0], geom.stride[1], geom.padding[0],
+                               geom.padding[2], geom.dilation[0], geom.dilation[1])
+        else:
+            xr = x.detach().float().requires_grad_(True)
+            wr = weight.detach().float().requires_grad_(True)
+            br = bias.detach().float().requires_grad_(True) if bias is not None else None
+            with torch.enable_grad():
+                yr = ref_dw_fwd(xr, wr, geom, br)
+                if ctx.relu:
+                    yr = torch.relu(yr)
+                grads = torch.autograd.grad(yr, [xr, wr] + ([br] if br is not None else []),
+                                            dy.float())
+            dx = grads[0].to(x.dtype)
+            dw = grads[1]
+            db = grads[2] if br is not None else None
+        if weight.requires_grad:
+            deliver_grad(weight, dw)
+        if bias is not None and bias.requires_grad:
+            deliver_grad(bias, db)
+        return dx, None, None, None, None
+
+
+def depthwise_conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False):
+    return _DwConvFn.apply(x, weight, bias, geom, relu)
+
+
+def laplace(x):
+    """2-D Laplacian of a single-channel NHWC image batch, SAME zero padding
+    (preprocessing.py:11-30; kernel [[.5,1,.5],[1,-6,1],[.5,1,.5]])."""
+    k = torch.tensor([[0.5, 1.0, 0.5], [1.0, -6.0, 1.0], [0.5, 1.0, 0.5]], dtype=torch.float32,
+                     device=x.device).view(3, 3, 1).expand(3, 3, x.shape[-1]).contiguous()
+    geom = ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    if on_gpu(x):
+        with torch.no_grad():
+            return depthwise_conv2d(x, k.to(x.dtype), None, geom, False)
+    return ref_dw_fwd(x, k, geom).to(x.dtype)

@@ -1,0 +1,95 @@
+"""Pooling ops, NHWC.
+
+* ``max_pool2d`` — k×k / stride s with explicit (top, bottom, left, right) padding (TF 'SAME' or
+  PyTorch-style symmetric).  The forward stores the in-window argmax (uint8) so the backward is a
+  deterministic gather (every input pixel sums the ≤⌈k/s⌉² windows that picked it), not a scatter.
+  Reference: ``slim.max_pool2d(3, stride=2, padding='SAME')`` (core/resnet.py:241) and
+  ``resnet_utils.subsample`` (1×1 max-pool stride s, core/resnet.py:73,81,128,140, K10).
+* ``global_avg_pool`` — mean over H, W → [N, C].  Reference: ``tf.reduce_mean(net, [1,2])``
+  (core/resnet.py:247,464, K12).
+
+GPU kernels: ``csrc/kernels/pool.hip``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .common import on_gpu, ext
+
+
+def _out(size, k, s, pb, pa):
+    return (size + pb + pa - k) // s + 1
+
+
+def ref_max_pool(x, k, s, pad):
+    pt, pb, pl, pr = pad
+    xt = x.permute(0, 3, 1, 2).float()
+    xt = F.pad(xt, (pl, pr, pt, pb), value=float("-inf"))
+    y = F.max_pool2d(xt, k, s)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, pad):
+        N, H, W, C = x.shape
+        Ho = _out(H, k, s, pad[0], pad[1])
+        Wo = _out(W, k, s, pad[2], pad[3])
+        ctx.k, ctx.s, ctx.pad, ctx.x_shape = k, s, pad, tuple(x.shape)
+        if on_gpu(x):
+            y = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
+            idx = torch.empty((N, Ho, Wo, C), device=x.device, dtype=torch.uint8)
+            ext().maxpool_fwd(x, y, idx, k, s, pad[0], pad[2])
+            ctx.save_for_backward(idx)
+            return y
+        xr = x.detach().float().requires_grad_(True)
+        with torch.enable_grad():
+            yr = ref_max_pool(xr, k, s, pad)
+        ctx.save_for_backward(xr, yr)
+        return yr.detach().to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        if on_gpu(dy):
+            (idx,) = ctx.saved_tensors
+            dx = torch.empty(ctx.x_shape, device=dy.device, dtype=dy.dtype)
+            ext().maxpool_bwd(dy, idx, dx, ctx.k, ctx.s, ctx.pad[0], ctx.pad[2])
+            return dx, None, None, None
+        xr, yr = ctx.saved_tensors
+        (g,) = torch.autograd.grad(yr, xr, dy.float())
+        return g.to(dy.dtype), None, None, None
+
+
+def max_pool2d(x, k, s, pad):
+    return _MaxPoolFn.apply(x, k, s, tuple(pad))
+
+
+class _GAPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, keepdims):
+        N, H, W, C = x.shape
+        ctx.x_shape = tuple(x.shape)
+        ctx.keepdims = keepdims
+        if on_gpu(x):
+            y = torch.empty((N, C), device=x.device, dtype=x.dtype)
+            ext().avgpool_fwd(x, y)
+        else:
+            y = x.float().mean(dim=(1, 2)).to(x.dtype)
+        return y.view(N, 1, 1, C) if keepdims else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.x_shape
+        dy = dy.reshape(N, C).contiguous()
+        if on_gpu(dy):
+            dx = torch.empty(ctx.x_shape, device=dy.device, dtype=dy.dtype)
+            ext().avgpool_bwd(dy, dx)
+            return dx, None
+        dx = (dy.float() / (H * W)).view(N, 1, 1, C).expand(N, H, W, C).contiguous()
+        return dx.to(dy.dtype), None
+
+
+def global_avg_pool(x, keepdims=False):
+    return _GAPFn.apply(x, keepdims)

@@ -1,0 +1,116 @@
+"""Bucketed gradient all-reduce overlapped with backward.
+
+The reference concatenates ALL gradients into one NCCL pack after the full backward
+(``num_packs=1``, Test.ipynb:200 — SURVEY §2.4/§2.6: 167 MB, no overlap).  Here:
+
+* gradients already live in one flat fp32 buffer (models/params.py) laid out in forward order, so a
+  bucket is just a contiguous slice — no pack/unpack copies;
+* buckets are cut walking the parameters *backwards* (the order backward produces them); each of
+  our autograd Functions calls ``p._grad_hook(p)`` right after its wgrad kernel is enqueued; when
+  the last parameter of a bucket lands, the bucket's all-reduce is issued immediately
+  (``async_op=True``; ProcessGroupNCCL orders it after the producing kernels with an event and
+  runs it on RCCL's own stream, so it overlaps the rest of backward on the compute stream);
+* buckets are always launched in index order (identical on every rank, as RCCL requires);
+* the first-issued bucket is kept small so communication starts early, later ones are large
+  (``bucket_mb``, default 32 MB) — fewer, larger collectives suit xGMI's per-link ring bandwidth
+  (7 links × ≈153 GB/s per MI355X);
+* the 1/world averaging is fused into the optimizer kernel (no extra pass).
+
+A ``comm_hook`` can replace the collective (used by tests to record launch order with a fake
+communicator).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class Bucket:
+    __slots__ = ("index", "lo", "hi", "params", "pending", "launched", "work")
+
+    def __init__(self, index, lo, hi, params):
+        self.index, self.lo, self.hi, self.params = index, lo, hi, params
+        self.pending = len(params)
+        self.launched = False
+        self.work = None
+
+    @property
+    def nbytes(self):
+        return (self.hi - self.lo) * 4
+
+
+class GradBucketer:
+    def __init__(self, flat, ctx=None, bucket_mb=32.0, first_bucket_mb=4.0, comm_hook=None,
+                 group=None):
+        self.flat = flat
+        self.ctx = ctx
+        self.group = group
+        self.comm_hook = comm_hook
+        self.buckets = []
+        self.bucket_of = {}
+        cap_first = int(first_bucket_mb * 2 ** 20 / 4)
+        cap = int(bucket_mb * 2 ** 20 / 4)
+        params = list(flat.params)
+        cur, cur_lo, cur_hi = [], None, None
+        limit = cap_first
+        for p in reversed(params):
+            lo, _ = flat.slice_of(p)
+            hi = lo + ((p.numel() + 63) // 64) * 64
+            if cur_hi is None:
+                cur_hi = hi
+            cur.append(p)
+            cur_lo = lo
+            if (cur_hi - cur_lo) >= limit:
+                self._add_bucket(cur_lo, cur_hi, cur)
+                cur, cur_lo, cur_hi = [], None, None
+                limit = cap
+        if cur:
+            self._add_bucket(cur_lo, cur_hi, cur)
+        self.next_launch = 0
+        for p in params:
+            p._grad_hook = self._on_ready
+
+    def _add_bucket(self, lo, hi, ps):
+        b = Bucket(len(self.buckets), lo, hi, list(ps))
+        self.buckets.append(b)
+        for p in ps:
+            self.bucket_of[id(p)] = b
+
+    # ------------------------------------------------------------------------------------------
+    def _on_ready(self, p):
+        b = self.bucket_of.get(id(p))
+        if b is None:
+            return
+        b.pending -= 1
+        self._launch_ready()
+
+    def _launch_ready(self, force=False):
+        while self.next_launch < len(self.buckets):
+            b = self.buckets[self.next_launch]
+            if b.pending > 0 and not force:
+                break
+            self._launch(b)
+            self.next_launch += 1
+
+    def _launch(self, b):
+        view = self.flat.grad[b.lo:b.hi]
+        if self.comm_hook is not None:
+            b.work = self.comm_hook(b, view)
+        elif self.ctx is not None and self.ctx.is_distributed:
+            b.work = dist.all_reduce(view, async_op=True, group=self.group)
+        b.launched = True
+
+    def finish(self):
+        """After backward: launch any bucket still pending (unused parameters — their grads were
+        zeroed by ``FlatParams.finish_grads``), wait for all collectives, reset for next step."""
+        self._launch_ready(force=True)
+        for b in self.buckets:
+            if b.work is not None and hasattr(b.work, "wait"):
+                b.work.wait()
+            b.work = None
+            b.launched = False
+            b.pending = len(b.params)
+        self.next_launch = 0
+
+    def describe(self):
+        return [(b.index, len(b.params), b.nbytes) for b in self.buckets]

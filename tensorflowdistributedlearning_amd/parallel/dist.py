@@ -1,0 +1,102 @@
+"""Process-group setup: one process per GPU (RCCL over xGMI via torch.distributed 'nccl'),
+gloo on CPU.
+
+Replaces the reference's single-process in-graph towers
+(``tf.contrib.distribute.MirroredStrategy(devices=gpus[:n_gpus])``, model.py:114-116) with the
+idiomatic ROCm layout: N processes, rank r drives GPU ``LOCAL_RANK``; rendezvous through the
+env:// store (MASTER_ADDR=127.0.0.1 by default; the container hostname may not resolve).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_distributed(self):
+        return self.world_size > 1
+
+    @property
+    def is_main(self):
+        return self.rank == 0
+
+    def barrier(self):
+        if self.is_distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_reduce_max(self, value: float) -> float:
+        if not self.is_distributed:
+            return value
+        t = torch.tensor([value], dtype=torch.float64,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_reduce_sum_(self, t):
+        if self.is_distributed:
+            dist.all_reduce(t)
+        return t
+
+    def broadcast_(self, t, src=0):
+        if self.is_distributed:
+            dist.broadcast(t, src)
+        return t
+
+
+_CTX = None
+
+
+def init_distributed(device_type=None, backend=None, timeout_s=600) -> DistContext:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).
+    Single process when WORLD_SIZE is unset or 1."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    be = "none"
+    if world > 1:
+        be = backend or ("nccl" if device_type == "cuda" else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        import datetime
+        kw = {}
+        if be == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(be, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _CTX = DistContext(rank, world, local_rank, device, be)
+    return _CTX
+
+
+def get_context() -> DistContext:
+    return _CTX if _CTX is not None else DistContext()
+
+
+def shutdown():
+    global _CTX
+    if _CTX is not None and _CTX.is_distributed and dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None

@@ -1,0 +1,304 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op
+(SURVEY §7.5 "Kernel" tier).  Inputs are bf16; tolerances are relative to the reference's scale."""
+import math
+
+import pytest
+import torch
+
+from tensorflowdistributedlearning_amd.ops import conv as C
+from tensorflowdistributedlearning_amd.ops import bn as B
+from tensorflowdistributedlearning_amd.ops import pool as P
+from tensorflowdistributedlearning_amd.ops import loss as L
+from tensorflowdistributedlearning_amd.ops import optim as O
+from tensorflowdistributedlearning_amd.ops import dwconv as D
+from tensorflowdistributedlearning_amd.ops import upsample as U
+from tensorflowdistributedlearning_amd.ops import metrics as Mt
+from tensorflowdistributedlearning_amd.ops.common import ext
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def bf(t, dev):
+    return t.to(dev, torch.bfloat16)
+
+
+# (N, H, W, C, K, R, S, stride, pad(t,b,l,r), dil)
+CONV_SHAPES = [
+    (2, 14, 14, 64, 64, 3, 3, 1, (1, 1, 1, 1), 1),      # resnet 3x3
+    (2, 14, 14, 64, 256, 1, 1, 1, (0, 0, 0, 0), 1),     # 1x1 expand
+    (2, 14, 14, 256, 128, 1, 1, 2, (0, 0, 0, 0), 1),    # 1x1 s2 downsample
+    (2, 15, 15, 128, 128, 3, 3, 2, (1, 1, 1, 1), 1),    # 3x3 s2 odd
+    (2, 16, 16, 64, 64, 3, 3, 2, (0, 1, 0, 1), 1),      # TF SAME asymmetric s2
+    (2, 32, 32, 8, 64, 7, 7, 2, (3, 3, 3, 3), 1),       # stem (Cin padded to 8)
+    (2, 13, 13, 64, 64, 3, 3, 1, (2, 2, 2, 2), 2),      # dilated r2
+    (2, 13, 13, 64, 32, 3, 3, 1, (4, 4, 4, 4), 4),      # dilated r4
+    (3, 1, 1, 200, 100, 1, 1, 1, (0, 0, 0, 0), 1),      # FC-shaped, ragged N
+    (2, 13, 13, 258, 258, 3, 3, 1, (1, 1, 1, 1), 1),    # reference preset C=258 (generic path)
+    (2, 9, 9, 40, 1, 3, 3, 1, (1, 1, 1, 1), 1),         # decoder 3x3 -> 1 channel
+    (4, 7, 7, 512, 2048, 1, 1, 1, (0, 0, 0, 0), 1),     # layer4 expand
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_dgrad_wgrad(gpu, shape):
+    N, H, W, Cin, K, R, S, st, pad, dil = shape
+    g = C.ConvGeom((st, st), pad, (dil, dil))
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, Cin)
+    w = torch.randn(K, R, S, Cin) / math.sqrt(R * S * Cin)
+    xb, wb = x.bfloat16(), w.bfloat16()
+    ref = C.ref_conv_fwd(xb.float(), wb.float(), g)
+    stats = torch.zeros(2, K, device=gpu)
+    y = C.conv_fwd(bf(x, gpu), bf(w, gpu), g, stats=stats)
+    assert y.shape == ref.shape
+    assert rel_err(y, ref) < 2e-2
+    yb = y.float().cpu().reshape(-1, K)
+    assert rel_err(stats[0], yb.sum(0)) < 1e-3
+    assert rel_err(stats[1], (yb * yb).sum(0)) < 1e-3
+    dy = torch.randn(ref.shape)
+    dyb = dy.bfloat16()
+    dx_ref = C.ref_conv_dgrad(dyb.float(), wb.float(), x.shape, g)
+    dx = C.conv_dgrad(bf(dy, gpu), bf(w, gpu), x.shape, g)
+    assert rel_err(dx, dx_ref) < 2e-2
+    dw_ref = C.ref_conv_wgrad(dyb.float(), xb.float(), w.shape, g)
+    dw = C.conv_wgrad(bf(dy, gpu), bf(x, gpu), tuple(w.shape), g)
+    assert dw.dtype == torch.float32
+    assert rel_err(dw, dw_ref) < 1e-2
+    # accumulate mode + fused bias grad
+    out = dw.clone()
+    bgrad = torch.empty(K, device=gpu)
+    C.conv_wgrad(bf(dy, gpu), bf(x, gpu), tuple(w.shape), g, out=out, accumulate=True,
+                 bias_grad=bgrad)
+    assert rel_err(out, 2 * dw_ref) < 1e-2
+    assert rel_err(bgrad, dyb.float().reshape(-1, K).sum(0)) < 1e-2
+
+
+def test_conv_bias_relu_epilogue(gpu):
+    torch.manual_seed(1)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    x = torch.randn(2, 10, 10, 16).bfloat16()
+    w = (torch.randn(24, 3, 3, 16) / 12).bfloat16()
+    b = torch.randn(24)
+    ref = torch.relu(C.ref_conv_fwd(x.float(), w.float(), g, b))
+    y = C.conv_fwd(x.to(gpu), w.to(gpu), g, bias=b.to(gpu), relu=True)
+    assert rel_err(y, ref) < 2e-2
+
+
+def test_conv_large_resnet_shape(gpu):
+    """A full-size ResNet-50 layer1 3x3 conv at batch 16 (many tiles, XCD remap, split-K wgrad)."""
+    torch.manual_seed(2)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    x = torch.randn(16, 56, 56, 64).bfloat16()
+    w = (torch.randn(64, 3, 3, 64) / 24).bfloat16()
+    y = C.conv_fwd(x.to(gpu), w.to(gpu), g)
+    ref = C.ref_conv_fwd(x.float(), w.float(), g)
+    assert rel_err(y, ref) < 2e-2
+    dy = torch.randn(ref.shape).bfloat16()
+    dw = C.conv_wgrad(dy.to(gpu), x.to(gpu), tuple(w.shape), g)
+    assert rel_err(dw, C.ref_conv_wgrad(dy.float(), x.float(), w.shape, g)) < 1e-2
+
+
+@pytest.mark.parametrize("C_", [64, 258, 24])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_batchnorm(gpu, C_, relu, res):
+    torch.manual_seed(3)
+    M = 2 * 9 * 11
+    x = (torch.randn(2, 9, 11, C_) * 2 + 0.5).bfloat16()
+    r = torch.randn(2, 9, 11, C_).bfloat16() if res else None
+    gamma = torch.rand(C_) + 0.5
+    beta = torch.randn(C_)
+    rm, rv = torch.zeros(C_), torch.ones(C_)
+    st_ref = B.bn_stats(x.float())
+    coef_ref = B.bn_finalize(st_ref, M, gamma, beta, rm, rv, 0.9, 1e-3, True)
+    y_ref = B.bn_apply(x.float(), coef_ref, None if r is None else r.float(), relu)
+    xd = x.to(gpu)
+    st = B.bn_stats(xd)
+    assert rel_err(st, st_ref) < 1e-3
+    rmd, rvd = torch.zeros(C_, device=gpu), torch.ones(C_, device=gpu)
+    coef = B.bn_finalize(st, M, gamma.to(gpu), beta.to(gpu), rmd, rvd, 0.9, 1e-3, True)
+    assert rel_err(coef, coef_ref) < 1e-3
+    assert rel_err(rmd, rm) < 1e-3 and rel_err(rvd, rv) < 1e-3
+    y = B.bn_apply(xd, coef, None if r is None else r.to(gpu), relu)
+    assert rel_err(y, y_ref) < 2e-2
+    dy = torch.randn(x.shape).bfloat16()
+    red_ref = B.bn_bwd_reduce(dy.float(), y.float().cpu(), x.float(), coef_ref, relu)
+    red = B.bn_bwd_reduce(dy.to(gpu), y, xd, coef, relu)
+    assert rel_err(red, red_ref) < 2e-2
+    dx_ref, dres_ref = B.bn_bwd_apply(dy.float(), y.float().cpu(), x.float(), coef_ref, red_ref,
+                                      gamma, M, relu, res)
+    dx, dres = B.bn_bwd_apply(dy.to(gpu), y, xd, coef, red, gamma.to(gpu), M, relu, res)
+    assert rel_err(dx, dx_ref) < 3e-2
+    if res:
+        assert rel_err(dres, dres_ref) < 1e-2
+
+
+def test_batchnorm_autograd_matches_torch(gpu):
+    """Whole BN+ReLU autograd Function vs torch.nn.functional.batch_norm (fp32)."""
+    from tensorflowdistributedlearning_amd.models.layers import BatchNorm
+    torch.manual_seed(4)
+    bn = BatchNorm(32, decay=0.9, eps=1e-5).to(gpu)
+    x = torch.randn(4, 6, 6, 32).bfloat16()
+    xg = x.to(gpu).requires_grad_(True)
+    y = bn(xg, relu=True)
+    dy = torch.randn(y.shape).bfloat16()
+    y.backward(dy.to(gpu))
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    gr = torch.ones(32, requires_grad=True)
+    br = torch.zeros(32, requires_grad=True)
+    yr = torch.relu(torch.nn.functional.batch_norm(xr, None, None, gr, br, True, 0.1, 1e-5))
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert rel_err(y, yr.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(xg.grad, xr.grad.permute(0, 2, 3, 1)) < 3e-2
+    assert rel_err(bn.gamma.grad, gr.grad) < 2e-2
+    assert rel_err(bn.beta.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("k,s,pad,Cn", [(3, 2, (1, 1, 1, 1), 64), (3, 2, (0, 1, 0, 1), 16),
+                                          (1, 2, (0, 0, 0, 0), 32), (3, 2, (1, 1, 1, 1), 5)])
+def test_maxpool(gpu, k, s, pad, Cn):
+    torch.manual_seed(5)
+    x = torch.randn(2, 11, 12, Cn).bfloat16()
+    xr = x.float().requires_grad_(True)
+    yr = P.ref_max_pool(xr, k, s, pad)
+    xg = x.to(gpu).requires_grad_(True)
+    y = P.max_pool2d(xg, k, s, pad)
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    y.backward(dy.to(gpu))
+    assert rel_err(xg.grad, xr.grad) < 1e-2
+
+
+def test_global_avg_pool(gpu):
+    x = torch.randn(3, 7, 7, 64).bfloat16()
+    xg = x.to(gpu).requires_grad_(True)
+    y = P.global_avg_pool(xg)
+    assert rel_err(y, x.float().mean((1, 2))) < 1e-2
+    y.backward(torch.ones_like(y))
+    assert rel_err(xg.grad, torch.full(x.shape, 1 / 49.0)) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("smooth", [0.0, 0.1])
+def test_softmax_xent(gpu, dtype, smooth):
+    torch.manual_seed(6)
+    logits = (torch.randn(37, 1000) * 3).to(dtype)
+    labels = torch.randint(0, 1000, (37,))
+    l_ref, g_ref = L.ref_softmax_xent(logits.float(), labels, smooth)
+    lg = logits.to(gpu).requires_grad_(True)
+    loss = L.softmax_cross_entropy(lg, labels.to(gpu), smooth)
+    assert abs(loss.item() - l_ref.item()) < 1e-3 * max(1, abs(l_ref.item()))
+    loss.backward()
+    assert rel_err(lg.grad, g_ref) < 2e-2
+
+
+@pytest.mark.parametrize("P_", [101 * 101, 64, 1000])
+def test_lovasz(gpu, P_):
+    torch.manual_seed(7)
+    Bn = 4
+    logits = torch.randn(Bn, P_) * 2
+    labels = (torch.rand(Bn, P_) > 0.6).float()
+    labels[1] = 0.0  # empty mask image
+    l_ref, g_ref = L.ref_lovasz_hinge(logits, labels)
+    lg = logits.to(gpu).requires_grad_(True)
+    loss = L.lovasz_hinge(lg, labels.to(gpu))
+    assert abs(loss.item() - l_ref.item()) < 1e-4 * max(1.0, abs(l_ref.item()))
+    loss.backward()
+    assert rel_err(lg.grad, g_ref) < 1e-3
+
+
+def test_seg_metrics(gpu):
+    torch.manual_seed(8)
+    lab = (torch.rand(6, 101, 101, 1) > 0.5).float()
+    pred = (torch.rand(6, 101, 101, 1) > 0.5).float()
+    pred[0] = lab[0]
+    lab[1] = 0
+    pred[1] = 0
+    for kaggle in (False, True):
+        s_ref, a_ref = Mt.ref_seg_scores(lab, pred, kaggle)
+        s, a = Mt.seg_scores(lab.to(gpu), pred.to(gpu), kaggle)
+        assert rel_err(s, s_ref) < 1e-5 and rel_err(a, a_ref) < 1e-5
+
+
+def test_sgd_adam(gpu):
+    torch.manual_seed(9)
+    n = 64 * 50
+    p = torch.randn(n)
+    g = torch.randn(n)
+    flags = (torch.rand(n // 64) > 0.3).to(torch.uint8)
+    m0 = torch.randn(n)
+    pc, mc = p.clone(), m0.clone()
+    O.sgd_momentum_(pc, g, mc, None, flags, 0.1, 0.9, 1e-4, 0.5, False)
+    pg, mg = p.to(gpu), m0.to(gpu)
+    lowp = torch.empty(n, dtype=torch.bfloat16, device=gpu)
+    O.sgd_momentum_(pg, g.to(gpu), mg, lowp, flags.to(gpu), 0.1, 0.9, 1e-4, 0.5, False)
+    assert rel_err(pg, pc) < 1e-6 and rel_err(mg, mc) < 1e-6
+    assert rel_err(lowp, pc) < 1e-2
+    v0 = torch.rand(n)
+    pc, mc, vc = p.clone(), m0.clone(), v0.clone()
+    O.adam_(pc, g, mc, vc, None, flags, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0)
+    pg, mg, vg = p.to(gpu), m0.to(gpu), v0.to(gpu)
+    O.adam_(pg, g.to(gpu), mg, vg, None, flags.to(gpu), 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0)
+    assert rel_err(pg, pc) < 1e-6 and rel_err(vg, vc) < 1e-6
+
+
+@pytest.mark.parametrize("Cn,rate,stride,relu", [(64, 2, 1, True), (1024, 8, 1, True),
+                                                 (16, 1, 2, False), (1, 1, 1, False)])
+def test_depthwise(gpu, Cn, rate, stride, relu):
+    torch.manual_seed(10)
+    from tensorflowdistributedlearning_amd.models.layers import resolve_padding
+    H = 13
+    pad = resolve_padding("SAME", H, H, 3, 3, (stride, stride), (rate, rate))
+    g = C.ConvGeom((stride, stride), pad, (rate, rate))
+    x = torch.randn(2, H, H, Cn).bfloat16()
+    w = (torch.randn(3, 3, Cn) * 0.3).bfloat16()
+    b = torch.randn(Cn) * 0.1
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = D.ref_dw_fwd(xr, wr, g, br)
+    if relu:
+        yr = torch.relu(yr)
+    wp = torch.nn.Parameter(w.float().to(gpu))
+    wp._lowp = w.to(gpu)
+    bp = torch.nn.Parameter(b.to(gpu))
+    wp.grad = None
+    xg = x.to(gpu).requires_grad_(True)
+    y = D.depthwise_conv2d(xg, wp, bp, g, relu)
+    assert rel_err(y, yr) < 2e-2
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    y.backward(dy.to(gpu))
+    assert rel_err(xg.grad, xr.grad) < 2e-2
+    assert rel_err(wp.grad, wr.grad) < 2e-2
+    assert rel_err(bp.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("hw,out", [((13, 13), (26, 26)), ((1, 1), (13, 13)), ((26, 26), (101, 101)),
+                                    ((7, 5), (9, 12))])
+def test_upsample(gpu, hw, out):
+    torch.manual_seed(11)
+    x = torch.randn(2, hw[0], hw[1], 16).bfloat16()
+    xr = x.float().requires_grad_(True)
+    yr = U.upsample(xr, out)
+    xg = x.to(gpu).requires_grad_(True)
+    y = U.upsample(xg, out)
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    y.backward(dy.to(gpu))
+    assert rel_err(xg.grad, xr.grad) < 2e-2
+
+
+def test_native_extension_is_loaded(gpu):
+    import sys
+    from tensorflowdistributedlearning_amd import _native
+    assert _native.available()
+    assert any("_C" in (getattr(m, "__file__", "") or "") for m in list(sys.modules.values())
+               if m is not None)
