@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Per-shape conv microbenchmark: our MFMA implicit-GEMM kernels (fwd / dgrad / wgrad) on every
+distinct ResNet-50 conv shape at a given batch, with MIOpen (torch channels_last bf16) timed on
+the same box as a yardstick.  Interleaved rounds in one process (guide §5.4 rule 24).
+
+  python bench/conv_bench.py --batch 256 --out gpurun_out/conv_bench.json
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
+
+
+def resnet50_shapes():
+    """(name, H, W, Cin, Cout, k, stride, pad) with multiplicity."""
+    out = {}
+
+    def add(name, H, Cin, Cout, k, s, p):
+        key = (H, Cin, Cout, k, s, p)
+        if key in out:
+            out[key][1] += 1
+        else:
+            out[key] = [name, 1]
+    add("stem7x7", 224, 8, 64, 7, 2, 3)
+    H, cin = 56, 64
+    for i, n in enumerate((3, 4, 6, 3)):
+        w = 64 * 2 ** i
+        for j in range(n):
+            s = 2 if (j == 0 and i > 0) else 1
+            add(f"l{i+1}.conv1", H, cin, w, 1, 1, 0)
+            add(f"l{i+1}.conv2", H, w, w, 3, s, 1)
+            Ho = H // s
+            add(f"l{i+1}.conv3", Ho, w, w * 4, 1, 1, 0)
+            if j == 0:
+                add(f"l{i+1}.down", H, cin, w * 4, 1, s, 0)
+            H, cin = Ho, w * 4
+    return [(v[0], v[1], *k) for k, v in out.items()]
+
+
+def timeit(fn, iters=5):
+    s, e = torch.cuda.Event(True), torch.cuda.Event(True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--no-miopen", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    N = a.batch
+    rows = []
+    tot = {"ours": 0.0, "miopen": 0.0}
+    for name, mult, H, Cin, Cout, k, s, p in resnet50_shapes():
+        g = C.ConvGeom((s, s), (p, p, p, p), (1, 1))
+        x = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
+        w = torch.randn(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16) * 0.05
+        Ho, Wo = g.out_hw(H, H, k, k)
+        dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
+        flop = 2.0 * N * Ho * Wo * Cout * Cin * k * k
+        st = torch.zeros(2, Cout, device=dev)
+        t_f = timeit(lambda: C.conv_fwd(x, w, g, stats=st))
+        t_d = timeit(lambda: C.conv_dgrad(dy, w, x.shape, g))
+        t_w = timeit(lambda: C.conv_wgrad(dy, x, tuple(w.shape), g))
+        r = dict(name=name, mult=mult, H=H, Cin=Cin, Cout=Cout, k=k, s=s,
+                 fwd_us=t_f, dgrad_us=t_d, wgrad_us=t_w, gflop=flop / 1e9,
+                 fwd_tf=flop / t_f / 1e6, dgrad_tf=flop / t_d / 1e6, wgrad_tf=flop / t_w / 1e6)
+        tot["ours"] += mult * (t_f + t_d + t_w)
+        if not a.no_miopen:
+            xm = x.permute(0, 3, 1, 2)  # channels_last view
+            wm = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+            xm.requires_grad_(True)
+            wm.requires_grad_(True)
+            ym = F.conv2d(xm, wm, None, s, p)
+            dym = dy.permute(0, 3, 1, 2)
+            m_f = timeit(lambda: F.conv2d(xm, wm, None, s, p))
+            m_b = timeit(lambda: torch.autograd.grad(ym, [xm, wm], dym, retain_graph=True))
+            r.update(miopen_fwd_us=m_f, miopen_bwd_us=m_b)
+            tot["miopen"] += mult * (m_f + m_b)
+        rows.append(r)
+        msg = (f"{name:10s} x{mult} {H:3d}x{H:<3d} {Cin:4d}->{Cout:4d} k{k} s{s} | "
+               f"fwd {t_f:7.1f}us {r['fwd_tf']:6.0f}TF  dgrad {t_d:7.1f}us {r['dgrad_tf']:6.0f}TF  "
+               f"wgrad {t_w:7.1f}us {r['wgrad_tf']:6.0f}TF")
+        if not a.no_miopen:
+            msg += f" | miopen fwd {r['miopen_fwd_us']:7.1f} bwd {r['miopen_bwd_us']:7.1f}"
+        print(msg, flush=True)
+    print(json.dumps({k: round(v / 1e3, 2) for k, v in tot.items()}) + "  (ms per step, all convs)")
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"batch": N, "rows": rows, "total_ms": tot}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -142,15 +142,16 @@ void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Te
 }
 
 void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red,
-                  c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres, double count,
+                  c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres,
+                  c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
                   bool relu) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   const int64_t C = x.size(-1);
   bn_bwd_apply_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
-                      optf(gamma), BFW(dx), optbw(dres), x.numel() / C, C, (float)count, relu,
-                      stream());
+                      optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
+                      C, (float)count, relu, stream());
 }
 
 // ---------------------------------------------------------------------------------- elementwise

@@ -175,21 +175,32 @@ __global__ void finalize_kernel(const float* __restrict__ stats, float* __restri
   coef[3 * C + c] = inv;
 }
 
+// y = act(x·scale + shift [+ res]).  When the grid stride is a multiple of the channel-vector
+// count (always for power-of-two C ≤ 2048) each thread's channel vector is loop-invariant, so its
+// 16 coefficients are loaded once into registers.
 __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict__ x,
                                                        const float* __restrict__ coef,
                                                        const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y, long nvec, int C,
                                                        int relu) {
   const int cvecs = C >> 3;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nvec; i += (long)gridDim.x * NT) {
-    const int cv = (int)(i % cvecs);
+  const long stride = (long)gridDim.x * NT;
+  const bool hoist = (stride % cvecs) == 0;
+  long i = blockIdx.x * (long)NT + threadIdx.x;
+  float sc[8], sh[8];
+  auto load_coef = [&](int cv) {
+    const float4 s0 = *(const float4*)(coef + cv * 8), s1 = *(const float4*)(coef + cv * 8 + 4);
+    const float4 h0 = *(const float4*)(coef + C + cv * 8), h1 = *(const float4*)(coef + C + cv * 8 + 4);
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
+    sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+  };
+  if (hoist) load_coef((int)(i % cvecs));
+  for (; i < nvec; i += stride) {
+    if (!hoist) load_coef((int)(i % cvecs));
     float v[8];
     unpack(((const uint4*)x)[i], v);
-    const float4 s0 = *(const float4*)(coef + cv * 8), s1 = *(const float4*)(coef + cv * 8 + 4);
-    const float4 h0 = *(const float4*)(coef + C + cv * 8),
-                 h1 = *(const float4*)(coef + C + cv * 8 + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
     if (res) {
@@ -218,14 +229,41 @@ __global__ void apply_scalar_kernel(const bf16_t* __restrict__ x, const float* _
   }
 }
 
+// dx = γ·invstd·(g − Σg/M − x̂·Σg·x̂/M) folded into dx = A·g + B·x + Cc per channel:
+//   A = γ·invstd,  B = −A·invstd·Σg·x̂/M,  Cc = −A·Σg/M − B·mean.
+// Coefficients are hoisted into registers (loop-invariant channel vector, see apply_vec_kernel).
+// Block 0 also writes dγ = Σg·x̂ and dβ = Σg straight into the flat gradient buffer.
 __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, long nvec, int C, float inv_count,
-    int relu) {
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += NT) {
+      if (dgamma) dgamma[c] = red[C + c];
+      if (dbeta) dbeta[c] = red[c];
+    }
+  }
   const int cvecs = C >> 3;
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nvec; i += (long)gridDim.x * NT) {
-    const int cv = (int)(i % cvecs);
+  const long stride = (long)gridDim.x * NT;
+  const bool hoist = (stride % cvecs) == 0;
+  long i = blockIdx.x * (long)NT + threadIdx.x;
+  float A[8], Bc[8], Cc[8];
+  auto load_coef = [&](int cv) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cv * 8 + j;
+      const float mean = coef[2 * C + c], inv = coef[3 * C + c];
+      const float a = (gamma ? gamma[c] : 1.f) * inv;
+      const float b = -a * inv * red[C + c] * inv_count;
+      A[j] = a;
+      Bc[j] = b;
+      Cc[j] = -a * red[c] * inv_count - b * mean;
+    }
+  };
+  if (hoist) load_coef((int)(i % cvecs));
+  for (; i < nvec; i += stride) {
+    if (!hoist) load_coef((int)(i % cvecs));
     float g[8], vx[8];
     unpack(((const uint4*)dy)[i], g);
     unpack(((const uint4*)x)[i], vx);
@@ -238,13 +276,7 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     if (dres) ((uint4*)dres)[i] = pack8(g);
     float o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = cv * 8 + j;
-      const float mean = coef[2 * C + c], inv = coef[3 * C + c];
-      const float k = (gamma ? gamma[c] : 1.f) * inv;
-      const float xh = (vx[j] - mean) * inv;
-      o[j] = k * (g[j] - red[c] * inv_count - xh * red[C + c] * inv_count);
-    }
+    for (int j = 0; j < 8; ++j) o[j] = A[j] * g[j] + Bc[j] * vx[j] + Cc[j];
     ((uint4*)dx)[i] = pack8(o);
   }
 }
@@ -253,8 +285,15 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
                                         const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                         const float* __restrict__ red,
                                         const float* __restrict__ gamma, bf16_t* __restrict__ dx,
-                                        bf16_t* __restrict__ dres, long n, int C, float inv_count,
+                                        bf16_t* __restrict__ dres, float* __restrict__ dgamma,
+                                        float* __restrict__ dbeta, long n, int C, float inv_count,
                                         int relu) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (dgamma) dgamma[c] = red[C + c];
+      if (dbeta) dbeta[c] = red[c];
+    }
+  }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
     float g = bf2f(dy[i]);
@@ -267,7 +306,14 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
   }
 }
 
-inline int ew_blocks(long n) { return (int)std::min<long>(4096, std::max<long>(1, (n + NT - 1) / NT)); }
+inline int ew_blocks(long n) {
+  // power-of-two block count (≤ 2048): the grid stride is then a multiple of any power-of-two
+  // channel-vector count ≤ 256, which lets the kernels hoist per-channel coefficients
+  long b = std::max<long>(1, (n + NT - 1) / NT);
+  int p = 1;
+  while (p < b && p < 2048) p <<= 1;
+  return p;
+}
 
 }  // namespace
 
@@ -300,15 +346,16 @@ void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, co
 }
 
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                         const float* red, const float* gamma, bf16_t* dx, bf16_t* dres, long M,
-                         int C, float count, bool relu, hipStream_t st) {
+                         const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
+                         float* dgamma, float* dbeta, long M, int C, float count, bool relu,
+                         hipStream_t st) {
   const long n = M * C;
   if (C % 8 == 0) {
     hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(ew_blocks(n / 8)), dim3(NT), 0, st, dy, y, x, coef,
-                       red, gamma, dx, dres, n / 8, C, 1.f / count, relu ? 1 : 0);
+                       red, gamma, dx, dres, dgamma, dbeta, n / 8, C, 1.f / count, relu ? 1 : 0);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
-                       red, gamma, dx, dres, n, C, 1.f / count, relu ? 1 : 0);
+                       red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu ? 1 : 0);
   }
 }
 

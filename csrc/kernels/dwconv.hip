@@ -148,8 +148,8 @@ __global__ void __launch_bounds__(NT) dw_wgrad_kernel(DwArgs a, long pix_per_blo
       if constexpr (true) red[t][j] = (k < RS) ? acc[k < RS ? k : 0][j] : db[j];
     }
     __syncthreads();
-    if (t < lanes_c * V) {
-      const int lc = t / V, j = t % V;
+    for (int o = t; o < lanes_c * V; o += NT) {
+      const int lc = o / V, j = o % V;
       const int cc = (lc + blockIdx.y * lanes_c) * V + j;
       if (lc + blockIdx.y * lanes_c < cv) {
         float s = 0.f;

@@ -40,8 +40,9 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                           float* red, long M, int C, bool relu, hipStream_t st);
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                         const float* red, const float* gamma, bf16_t* dx, bf16_t* dres, long M,
-                         int C, float count, bool relu, hipStream_t st);
+                         const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
+                         float* dgamma, float* dbeta, long M, int C, float count, bool relu,
+                         hipStream_t st);
 
 // elementwise --------------------------------------------------------------------------------
 void relu_bwd_launch(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t st);

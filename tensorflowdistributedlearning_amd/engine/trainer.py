@@ -15,6 +15,7 @@ from ..models.params import FlatParams
 from ..parallel.bucketer import GradBucketer
 from ..parallel.dist import get_context
 from .optimizer import build_optimizer
+from ..ops import workspace
 
 
 class Trainer:
@@ -33,6 +34,7 @@ class Trainer:
         self.bucketer = (GradBucketer(self.flat, self.ctx, bucket_mb, first_bucket_mb)
                          if self.ctx.is_distributed else None)
         self.global_step = 0
+        self.train_mode = True  # False: BN uses moving statistics while training (frozen BN)
 
     # ------------------------------------------------------------------------------------------
     def broadcast_state(self):
@@ -43,7 +45,8 @@ class Trainer:
         self.flat.sync_lowp()
 
     def train_step(self, x, y):
-        self.model.train()
+        self.model.train(self.train_mode)
+        workspace.reset(self.device)
         self.flat.begin_step()
         out = self.model(x)
         loss = self.loss_fn(out, y)

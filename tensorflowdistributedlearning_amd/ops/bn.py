@@ -18,7 +18,8 @@ from __future__ import annotations
 
 import torch
 
-from .common import on_gpu, ext, deliver_grad
+from .common import on_gpu, ext, deliver_grad, grad_target
+from . import workspace
 
 
 # ----------------------------------------------------------------------------------------------
@@ -28,7 +29,7 @@ from .common import on_gpu, ext, deliver_grad
 def bn_stats(x, stats=None):
     C = x.shape[-1]
     if stats is None:
-        stats = torch.zeros((2, C), device=x.device, dtype=torch.float32)
+        stats = workspace.zeros((2, C), x.device)
     if on_gpu(x):
         ext().bn_stats(x, stats)
         return stats
@@ -81,7 +82,7 @@ def bn_bwd_reduce(dy, y, x, coef, relu):
     """fp32 [2, C]: (Σg, Σg·x̂), g = dy·[y>0] if relu else dy."""
     C = x.shape[-1]
     if on_gpu(dy):
-        red = torch.zeros((2, C), device=dy.device, dtype=torch.float32)
+        red = workspace.zeros((2, C), dy.device)
         ext().bn_bwd_reduce(dy, y, x, coef, red, bool(relu))
         return red
     g = dy.float().reshape(-1, C)
@@ -91,13 +92,15 @@ def bn_bwd_reduce(dy, y, x, coef, relu):
     return torch.stack([g.sum(0), (g * xhat).sum(0)])
 
 
-def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres):
-    """dx (same dtype as x) and optionally the masked gradient g for the residual branch."""
+def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None, dbeta=None):
+    """dx (same dtype as x) and optionally the masked gradient g for the residual branch.
+    On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch."""
     C = x.shape[-1]
     if on_gpu(dy):
         dx = torch.empty_like(x)
         dres = torch.empty_like(dy) if want_dres else None
-        ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, float(count), bool(relu))
+        ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
+                           bool(relu))
         return dx, dres
     g = dy.float().reshape(-1, C)
     if relu:
@@ -152,11 +155,18 @@ class _BatchNormActFn(torch.autograd.Function):
             dres = g.reshape(dy.shape).to(dy.dtype) if ctx.has_res else None
             return dx, None, None, None, dres, None, None, None
         red = bn_bwd_reduce(dy, y, x, coef, relu)
-        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gamma, ctx.count, relu, ctx.has_res)
-        if gamma is not None and gamma.requires_grad:
-            deliver_grad(gamma, red[1])
-        if beta.requires_grad:
-            deliver_grad(beta, red[0])
+        want_g = gamma is not None and gamma.requires_grad
+        want_b = beta.requires_grad
+        gt, gfresh = grad_target(gamma) if want_g else (None, False)
+        bt, bfresh = grad_target(beta) if want_b else (None, False)
+        direct_g = on_gpu(dy) and gt is not None and gfresh
+        direct_b = on_gpu(dy) and bt is not None and bfresh
+        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gamma, ctx.count, relu, ctx.has_res,
+                                gt if direct_g else None, bt if direct_b else None)
+        if want_g:
+            deliver_grad(gamma, None if direct_g else red[1], written=direct_g)
+        if want_b:
+            deliver_grad(beta, None if direct_b else red[0], written=direct_b)
         return dx, None, None, None, dres, None, None, None
 
 

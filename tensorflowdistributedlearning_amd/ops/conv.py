@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+from . import workspace
 
 
 @dataclass(frozen=True)
@@ -162,7 +163,7 @@ class _Conv2dFn(torch.autograd.Function):
         w = layer.compute_weight(x.dtype) if layer is not None else compute_weight(weight, x.dtype)
         stats = None
         if want_stats:
-            stats = torch.zeros((2, w.shape[0]), device=x.device, dtype=torch.float32)
+            stats = workspace.zeros((2, w.shape[0]), x.device)
         b = None if bias is None else bias.detach()
         y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats)
         ctx.geom = geom

@@ -1,0 +1,126 @@
+"""Data-parallel logic on the CPU (SURVEY §7.5 "Dist logic"): bucket layout, launch order with a
+fake communicator, and real multi-process gloo training equivalence (world_size 2)."""
+import os
+
+import pytest
+import torch
+import torch.nn as nn
+
+from tensorflowdistributedlearning_amd.models.params import FlatParams
+from tensorflowdistributedlearning_amd.parallel.bucketer import GradBucketer
+from tensorflowdistributedlearning_amd.parallel import launcher
+from tensorflowdistributedlearning_amd.models.layers import Conv2d, Linear
+from tensorflowdistributedlearning_amd.ops.pool import global_avg_pool
+from tensorflowdistributedlearning_amd.ops.elementwise import relu
+
+
+class TinyNet(nn.Module):
+    """conv-only net (no BN: per-rank BN statistics would make DP != large-batch)."""
+
+    def __init__(self):
+        super().__init__()
+        self.c1 = Conv2d(8, 16, 3, 2, "sym", bias=True)
+        self.c2 = Conv2d(16, 32, 3, 1, "sym", bias=True)
+        self.c3 = Conv2d(32, 32, 1, 1, 0)
+        self.fc = Linear(32, 5)
+
+    def forward(self, x):
+        x = relu(self.c1(x))
+        x = relu(self.c2(x))
+        x = relu(self.c3(x))
+        return self.fc(global_avg_pool(x))
+
+
+def test_flat_params_layout_and_views():
+    m = TinyNet()
+    f = FlatParams(m, "cpu", lowp_dtype=None)
+    assert f.total % 64 == 0
+    for p in f.params:
+        o = p._flat_offset
+        assert o % 64 == 0
+        assert p.data.data_ptr() == f.master[o:].data_ptr()
+        assert p.grad.data_ptr() == f.grad[o:].data_ptr()
+    # biases flagged no-decay, weights decay
+    assert f.decay_flags[m.c1.bias._flat_offset // 64] == 0
+    assert f.decay_flags[m.c1.weight._flat_offset // 64] == 1
+
+
+def test_bucketer_fills_in_backward_order_and_launches_in_index_order():
+    torch.manual_seed(0)
+    m = TinyNet()
+    f = FlatParams(m, "cpu", lowp_dtype=None)
+    log = []
+    b = GradBucketer(f, ctx=None, bucket_mb=0.004, first_bucket_mb=0.001,
+                     comm_hook=lambda bk, view: log.append((bk.index, view.numel())))
+    assert len(b.buckets) >= 3
+    # contiguous, covering, in reverse flat order
+    cov = sorted((bk.lo, bk.hi) for bk in b.buckets)
+    assert cov[0][0] == 0
+    for (lo0, hi0), (lo1, hi1) in zip(cov, cov[1:]):
+        assert hi0 == lo1
+    assert b.buckets[0].hi == max(h for _, h in cov)  # first bucket = last params (fc)
+    f.begin_step()
+    out = m(torch.randn(2, 8, 8, 8))
+    out.sum().backward()
+    f.finish_grads()
+    b.finish()
+    assert [i for i, _ in log] == list(range(len(b.buckets)))
+    # readiness order: the fc bucket must be complete before the first conv's bucket
+    assert sum(n for _, n in log) == sum(bk.hi - bk.lo for bk in b.buckets)
+
+
+def test_bucketer_reset_between_steps():
+    m = TinyNet()
+    f = FlatParams(m, "cpu", lowp_dtype=None)
+    log = []
+    b = GradBucketer(f, None, 0.004, 0.001, comm_hook=lambda bk, v: log.append(bk.index))
+    for _ in range(2):
+        f.begin_step()
+        m(torch.randn(2, 8, 8, 8)).sum().backward()
+        f.finish_grads()
+        b.finish()
+    assert log == list(range(len(b.buckets))) * 2
+
+
+def _dp_worker(rank, tmpdir):
+    import torch
+    from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown
+    from tensorflowdistributedlearning_amd.engine.trainer import Trainer
+    from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy
+    ctx = init_distributed(device_type="cpu")
+    torch.manual_seed(123)  # same init on all ranks is NOT assumed: rank 0 broadcasts
+    if rank == 1:
+        torch.manual_seed(999)
+    m = TinyNet()
+    tr = Trainer(m, softmax_cross_entropy, "cpu", "sgd", dict(lr=0.1, momentum=0.9,
+                                                              weight_decay=1e-4),
+                 ctx=ctx, bucket_mb=0.004, first_bucket_mb=0.001, lowp_dtype=None)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 8, 8, 8, generator=g)
+    y = torch.randint(0, 5, (8,), generator=g)
+    xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+    for _ in range(3):
+        tr.train_step(xs, ys)
+    torch.save(tr.flat.master.clone(), os.path.join(tmpdir, f"rank{rank}.pt"))
+    shutdown()
+
+
+@pytest.mark.timeout(240)
+def test_gloo_dp_equals_large_batch(tmp_path):
+    """2 ranks × batch 4 with mean-gradient all-reduce == 1 process × batch 8."""
+    launcher.spawn(_dp_worker, 2, args=(str(tmp_path),))
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert torch.equal(r0, r1)  # replicas stay identical
+    from tensorflowdistributedlearning_amd.engine.trainer import Trainer
+    from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy
+    torch.manual_seed(123)
+    m = TinyNet()
+    tr = Trainer(m, softmax_cross_entropy, "cpu", "sgd", dict(lr=0.1, momentum=0.9,
+                                                              weight_decay=1e-4), lowp_dtype=None)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(8, 8, 8, 8, generator=g)
+    y = torch.randint(0, 5, (8,), generator=g)
+    for _ in range(3):
+        tr.train_step(x, y)
+    assert torch.allclose(r0, tr.flat.master, atol=1e-5, rtol=1e-4)

@@ -1,0 +1,96 @@
+"""Model structure parity (CPU): parameter counts / tensor counts / shapes vs SURVEY Appendix A,
+checkpoint naming vs Appendix B, and the atrous output-stride control."""
+import pytest
+import torch
+
+from tensorflowdistributedlearning_amd import models
+
+
+def count(m):
+    return sum(p.numel() for p in m.parameters()), len(list(m.parameters()))
+
+
+def test_resnet_param_counts():
+    assert count(models.resnet50())[0] == 25_557_032
+    assert count(models.resnet18())[0] == 11_689_512
+    assert count(models.resnet152())[0] == 60_192_808
+
+
+def test_deeplab_reference_preset_matches_appendix_a():
+    m = models.DeepLabResNet(model_name="model", input_shape=(101, 101))
+    n, t = count(m)
+    assert n == 41_814_025          # SURVEY Appendix A (exact replay of core/resnet.py)
+    assert t == 208                 # 66 conv/dw weights + 24 biases + 59 BN x (gamma, beta)
+    bn_moving = sum(b.numel() for name, b in m.named_buffers() if "running" in name)
+    assert bn_moving == 65_632       # moving mean + variance of the 59 BN layers
+    assert sum(1 for name, _ in m.named_buffers() if "running_mean" in name) == 59
+
+
+def test_deeplab_shapes_and_end_points():
+    m = models.DeepLabResNet(model_name="model", input_shape=(101, 101))
+    x = torch.randn(2, 101, 101, 2)
+    out, ep = m(x, return_end_points=True)
+    assert out.shape == (2, 101, 101, 1)
+    assert ep["model/resnet_v2/block4"].shape == (2, 13, 13, 1024)
+    assert ep["model/resnet_v2/block1/unit_1/bottleneck_v2/conv3"].shape == (2, 26, 26, 512)
+    assert ep["model/resnet_v2/block3"].shape == (2, 13, 13, 2048)
+
+
+def test_deeplab_dilation_rates():
+    m = models.DeepLabResNet(model_name="model")
+    rates = [[u.conv2.conv.dilation[0] for u in blk] for blk in m.blocks]
+    assert rates == [[1, 1, 1], [1, 1, 1, 1], [2] * 6, [4, 8, 4]]
+
+
+def test_deeplab_output_stride_none_and_16():
+    m = models.DeepLabResNet(model_name="m", output_stride=None, input_shape=(64, 64))
+    out, ep = m(torch.randn(1, 64, 64, 2), return_end_points=True)
+    assert out.shape == (1, 64, 64, 1)
+    assert ep["m/resnet_v2/block4"].shape[1] == 2  # full striding: 64/32
+    m16 = models.DeepLabResNet(model_name="m", output_stride=16, input_shape=(64, 64))
+    _, ep = m16(torch.randn(1, 64, 64, 2), return_end_points=True)
+    assert ep["m/resnet_v2/block4"].shape[1] == 4
+    with pytest.raises(ValueError):
+        models.DeepLabResNet(output_stride=6)
+
+
+def test_deeplab_plumbing_32x32_even_input():
+    """D11: decoder size derived, so even-sized inputs (TF SAME asymmetric padding) work."""
+    m = models.DeepLabResNet(model_name="m", input_shape=(32, 32), n_blocks=(1, 1, 1))
+    assert m(torch.randn(2, 32, 32, 2)).shape == (2, 32, 32, 1)
+
+
+def test_deeplab_basic_block_variant():
+    m = models.DeepLabResNet(model_name="m", block_type="basic_block", input_shape=(33, 33))
+    out, ep = m(torch.randn(1, 33, 33, 2), return_end_points=True)
+    assert out.shape == (1, 33, 33, 1)
+    assert "m/resnet_v2/block1/unit_1/bottleneck_v2/conv2" in ep
+
+
+def test_tf_names_cover_every_tensor():
+    m = models.DeepLabResNet(model_name="fold_model")
+    names = m.tf_names()
+    sd = m.state_dict()
+    assert set(names) == set(sd.keys())
+    assert names["conv1_1.conv.weight"] == "fold_model/resnet_v2/conv1_1/weights"
+    assert names["blocks.0.0.conv2.bn.running_var"] == \
+        "fold_model/resnet_v2/block1/unit_1/bottleneck_v2/Conv/BatchNorm/moving_variance"
+    assert names["assp_conv_3x3_2.depthwise.weight"] == \
+        "fold_model/assp/conv/conv_3x3_2_depthwise/depthwise_weights"
+    assert names["decoder_conv_3x3.bias"] == "fold_model/decoder/conv_3x3/biases"
+    assert len(set(names.values())) == len(names)
+
+
+def test_xception41_intended_structure():
+    m = models.xception_41(num_classes=1000)
+    assert len(m.units) == 3 + 8 + 2  # 8-unit middle flow (D9 fixed)
+    x = torch.randn(1, 65, 65, 3)
+    assert m(x).shape == (1, 1000)
+    feat = models.xception_41(num_classes=0, output_stride=16)
+    y = feat(torch.randn(1, 65, 65, 3))
+    assert y.shape[1] == 5 and y.shape[-1] == 2048
+
+
+def test_resnet_forward_shapes():
+    m = models.resnet18(num_classes=10)
+    assert m(torch.randn(2, 32, 32, 3)).shape == (2, 10)

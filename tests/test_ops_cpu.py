@@ -1,0 +1,210 @@
+"""CPU oracle tests: reference-semantics parity of the op layer (TF SAME, subsample folding, TF1
+legacy bilinear upsample, Lovász, mIoU formula, BN, optimizers).  NumPy re-implementations of
+the reference's TF code paths serve as independent oracles (TF is not installed: parity is pinned
+to the reference's documented algorithms)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tensorflowdistributedlearning_amd.ops import conv as C
+from tensorflowdistributedlearning_amd.ops import bn as B
+from tensorflowdistributedlearning_amd.ops import loss as L
+from tensorflowdistributedlearning_amd.ops import upsample as U
+from tensorflowdistributedlearning_amd.ops import metrics as Mt
+from tensorflowdistributedlearning_amd.ops import optim as O
+from tensorflowdistributedlearning_amd.models.layers import resolve_padding
+
+
+def test_tf_same_padding():
+    assert C.same_padding(101, 3, 2) == (1, 1)     # 101 -> 51
+    assert C.same_padding(32, 3, 2) == (0, 1)      # even input: asymmetric
+    assert C.same_padding(51, 3, 2) == (1, 1)      # pool1 51 -> 26
+    assert C.same_padding(13, 3, 1, 2) == (2, 2)   # dilated
+    assert C.ConvGeom((2, 2), (1, 1, 1, 1)).out_hw(101, 101, 3, 3) == (51, 51)
+
+
+def test_subsample_folding_equivalence():
+    """3x3 stride-1 SAME conv + 1x1 max-pool stride 2 == stride-2 conv with symmetric padding
+    (core/resnet.py:137-140 folded)."""
+    torch.manual_seed(0)
+    x = torch.randn(2, 26, 26, 8)
+    w = torch.randn(4, 3, 3, 8)
+    for rate in (1, 2):
+        pad = resolve_padding("SAME", 26, 26, 3, 3, (1, 1), (rate, rate))
+        full = C.ref_conv_fwd(x, w, C.ConvGeom((1, 1), pad, (rate, rate)))
+        sub = full[:, ::2, ::2, :]
+        folded = C.ref_conv_fwd(x, w, C.ConvGeom((2, 2), resolve_padding(
+            "sym", 26, 26, 3, 3, (2, 2), (rate, rate)), (rate, rate)))
+        assert torch.allclose(sub, folded, atol=1e-4)
+
+
+def test_conv_ref_grads_match_autograd():
+    torch.manual_seed(1)
+    g = C.ConvGeom((2, 2), (0, 1, 0, 1), (1, 1))
+    x = torch.randn(2, 8, 8, 4, requires_grad=True)
+    w = torch.randn(6, 3, 3, 4, requires_grad=True)
+    y = C.ref_conv_fwd(x, w, g)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    assert torch.allclose(C.ref_conv_dgrad(dy, w.detach(), x.shape, g), x.grad, atol=1e-4)
+    assert torch.allclose(C.ref_conv_wgrad(dy, x.detach(), w.shape, g), w.grad, atol=1e-4)
+
+
+def _tf1_upsample_numpy(x, out_h, out_w):
+    """Literal NumPy replay of core/layers.py _upsample: SYMMETRIC pad 1 → TF1 resize_bilinear
+    (align_corners=False, legacy src = dst·in/out) to out+4 → crop [2:-2]."""
+    xp = np.pad(x, ((0, 0), (1, 1), (1, 1), (0, 0)), mode="symmetric")
+    N, H, W, Cc = xp.shape
+    nh, nw = out_h + 4, out_w + 4
+    sh, sw = H / nh, W / nw
+    out = np.zeros((N, nh, nw, Cc), dtype=np.float64)
+    for i in range(nh):
+        src = i * sh
+        y0 = int(math.floor(src))
+        y1 = min(y0 + 1, H - 1)
+        fy = src - y0
+        for j in range(nw):
+            srcx = j * sw
+            x0 = int(math.floor(srcx))
+            x1 = min(x0 + 1, W - 1)
+            fx = srcx - x0
+            top = xp[:, y0, x0] * (1 - fx) + xp[:, y0, x1] * fx
+            bot = xp[:, y1, x0] * (1 - fx) + xp[:, y1, x1] * fx
+            out[:, i, j] = top * (1 - fy) + bot * fy
+    return out[:, 2:-2, 2:-2]
+
+
+@pytest.mark.parametrize("hw,out", [((13, 13), (26, 26)), ((1, 1), (13, 13)),
+                                    ((26, 26), (101, 101)), ((5, 7), (9, 12))])
+def test_upsample_matches_tf1_legacy(hw, out):
+    x = np.random.RandomState(0).randn(2, hw[0], hw[1], 3)
+    ref = _tf1_upsample_numpy(x, *out)
+    got = U.upsample(torch.tensor(x, dtype=torch.float32), out).numpy()
+    assert np.abs(got - ref).max() < 1e-5
+
+
+def _np_lovasz(logit, label):
+    """NumPy replay of core/losses.py lovasz_hinge_flat + lovasz_grad."""
+    signs = 2.0 * label - 1.0
+    errors = 1.0 - logit * signs
+    order = np.argsort(-errors, kind="stable")
+    es = errors[order]
+    gt = label[order]
+    gts = gt.sum()
+    inter = gts - np.cumsum(gt)
+    union = gts + np.cumsum(1 - gt)
+    jac = 1.0 - inter / union
+    jac[1:] = jac[1:] - jac[:-1]
+    return float(np.dot(np.maximum(es, 0), jac))
+
+
+def test_lovasz_matches_numpy_and_autograd():
+    rs = np.random.RandomState(1)
+    logits = rs.randn(3, 200).astype(np.float32)
+    labels = (rs.rand(3, 200) > 0.5).astype(np.float32)
+    labels[2] = 0
+    loss, grad = L.ref_lovasz_hinge(torch.tensor(logits), torch.tensor(labels))
+    ref = np.mean([_np_lovasz(logits[i], labels[i]) for i in range(3)])
+    assert abs(loss.item() - ref) < 1e-5
+    # closed-form gradient == autograd through the sorted errors (stop_grad on lovasz_grad)
+    lt = torch.tensor(logits, requires_grad=True)
+    tot = 0
+    for i in range(3):
+        lab = torch.tensor(labels[i])
+        sg = 2 * lab - 1
+        err = 1 - lt[i] * sg
+        es, perm = torch.sort(err, descending=True, stable=True)
+        gvec = L.lovasz_grad(lab[perm]).detach()
+        tot = tot + torch.dot(torch.relu(es), gvec)
+    (tot / 3).backward()
+    assert torch.allclose(grad, lt.grad, atol=1e-6)
+
+
+def test_lovasz_autograd_function():
+    torch.manual_seed(2)
+    x = torch.randn(2, 10, 10, 1, requires_grad=True)
+    y = (torch.rand(2, 10, 10, 1) > 0.5).float()
+    loss = L.lovasz_hinge(x, y)
+    loss.backward()
+    assert x.grad.shape == x.shape and torch.isfinite(x.grad).all()
+
+
+def test_miou_reference_formula():
+    lab = torch.zeros(2, 4, 4, 1)
+    pred = torch.zeros(2, 4, 4, 1)
+    lab[0, :2] = 1
+    pred[0, :3] = 1  # TP 8, FP 4 -> IoU 2/3
+    s, a = Mt.ref_seg_scores(lab, pred)
+    iou = 8 / 12
+    thr = np.array(Mt.IOU_THRESHOLDS)
+    assert abs(s[0].item() - np.mean(iou * (iou > thr))) < 1e-6   # D16 formula (parity)
+    assert s[1].item() == 1.0                                      # empty mask, empty pred
+    sk, _ = Mt.ref_seg_scores(lab, pred, kaggle=True)
+    assert abs(sk[0].item() - np.mean(iou > thr)) < 1e-6
+    assert abs(a[0].item() - 12 / 16) < 1e-6
+
+
+def test_streaming_mean():
+    sm = Mt.StreamingMean()
+    sm.update(torch.tensor([1.0, 2.0]))
+    sm.update(torch.tensor([3.0]))
+    assert abs(sm.result().item() - 2.0) < 1e-9
+
+
+def test_softmax_xent_ref():
+    torch.manual_seed(3)
+    lg = torch.randn(5, 7, requires_grad=True)
+    y = torch.randint(0, 7, (5,))
+    loss, grad = L.ref_softmax_xent(lg.detach(), y)
+    F.cross_entropy(lg, y).backward()
+    assert torch.allclose(loss, F.cross_entropy(lg.detach(), y), atol=1e-6)
+    assert torch.allclose(grad, lg.grad, atol=1e-6)
+    l2 = L.softmax_cross_entropy(lg.detach().requires_grad_(True), y, 0.1)
+    assert torch.allclose(l2, F.cross_entropy(lg.detach(), y, label_smoothing=0.1), atol=1e-5)
+
+
+def test_bn_reference_against_torch():
+    torch.manual_seed(4)
+    from tensorflowdistributedlearning_amd.models.layers import BatchNorm
+    bn = BatchNorm(6, decay=0.9, eps=1e-3)
+    x = torch.randn(3, 5, 5, 6, requires_grad=True)
+    r = torch.randn(3, 5, 5, 6, requires_grad=True)
+    y = bn(x, residual=r, relu=True)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    x2 = x.detach().permute(0, 3, 1, 2).requires_grad_(True)
+    r2 = r.detach().permute(0, 3, 1, 2).requires_grad_(True)
+    g2 = torch.ones(6, requires_grad=True)
+    b2 = torch.zeros(6, requires_grad=True)
+    rm, rv = torch.zeros(6), torch.ones(6)
+    y2 = torch.relu(F.batch_norm(x2, rm, rv, g2, b2, True, 0.1, 1e-3) + r2)
+    y2.backward(dy.permute(0, 3, 1, 2))
+    assert torch.allclose(y, y2.permute(0, 2, 3, 1), atol=1e-5)
+    assert torch.allclose(x.grad, x2.grad.permute(0, 2, 3, 1), atol=1e-5)
+    assert torch.allclose(r.grad, r2.grad.permute(0, 2, 3, 1), atol=1e-5)
+    assert torch.allclose(bn.gamma.grad, g2.grad, atol=1e-4)
+    assert torch.allclose(bn.running_mean, rm, atol=1e-6)
+    assert torch.allclose(bn.running_var, rv, atol=1e-5)
+
+
+def test_tf_adam_formula():
+    p = torch.tensor([1.0, -2.0] * 32)
+    g = torch.tensor([0.5, 0.1] * 32)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    flags = torch.zeros(1, dtype=torch.uint8)
+    lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-8
+    t = 1
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    O.adam_(p, g, m, v, None, flags, lr_t, b1, b2, eps)
+    # TF: m=0.1g, v=0.001g², p -= lr_t·m/(√v+ε)
+    exp = torch.tensor([1.0, -2.0] * 32) - lr_t * (0.1 * g) / (torch.sqrt(0.001 * g * g) + eps)
+    assert torch.allclose(p, exp, atol=1e-7)
+
+
+def test_exponential_decay():
+    assert O.exponential_decay(1e-3, 0) == 1e-3
+    assert abs(O.exponential_decay(1e-3, 10000) - 5e-4) < 1e-12
+    assert abs(O.exponential_decay(1e-3, 5000) - 1e-3 * 0.5 ** 0.5) < 1e-12
