@@ -34,6 +34,12 @@ const bf16_t* optb(const c10::optional<Tensor>& t) {
 }
 bf16_t* optbw(const c10::optional<Tensor>& t) { return const_cast<bf16_t*>(optb(t)); }
 
+uint32_t nbytes32(const Tensor& t) {
+  const int64_t n = t.numel() * t.element_size();
+  TORCH_CHECK(n < (int64_t(1) << 32) - 64, "tensor too large for 32-bit buffer addressing");
+  return (uint32_t)n;
+}
+
 ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_t H, int64_t W,
                    int64_t C, int64_t K, int64_t R, int64_t S, int64_t sh, int64_t sw, int64_t ph,
                    int64_t pw, int64_t dh, int64_t dw, int64_t Ho, int64_t Wo) {
@@ -57,6 +63,7 @@ void conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::opt
                          w.size(2), sh, sw, ph, pw, dh, dw, y.size(1), y.size(2));
   TORCH_CHECK(y.size(0) == a.N && y.size(3) == a.K, "output shape mismatch");
   a.x = BF(x); a.w = BF(w); a.out = y.data_ptr();
+  a.x_bytes = nbytes32(x); a.w_bytes = nbytes32(w); a.out_bytes = nbytes32(y);
   a.bias = optf(bias);
   a.stats = optfw(stats);
   if (a.stats) TORCH_CHECK(stats->numel() == 2 * a.K, "stats must be [2, K]");
@@ -74,6 +81,7 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
                          w.size(2), sh, sw, ph, pw, dh, dw, dy.size(1), dy.size(2));
   TORCH_CHECK(dx.size(3) == w.size(3) && dy.size(3) == w.size(0), "shape mismatch");
   a.dy = BF(dy); a.w = BF(w); a.out = dx.data_ptr();
+  a.dy_bytes = nbytes32(dy); a.w_bytes = nbytes32(w); a.out_bytes = nbytes32(dx);
   a.M = a.N * a.H * a.W; a.Ng = a.C; a.Kg = a.R * a.S * a.K; a.ldc = a.C; a.relu = 0;
   if (a.M == 0) return;
   conv_dgrad_launch(a, stream());
@@ -89,12 +97,14 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad
                          out.size(1), out.size(2), sh, sw, ph, pw, dh, dw, dy.size(1), dy.size(2));
   TORCH_CHECK(out.size(3) == a.C && dy.size(3) == a.K && dy.size(0) == a.N, "shape mismatch");
   a.dy = BF(dy); a.x = BF(x);
+  a.dy_bytes = nbytes32(dy); a.x_bytes = nbytes32(x);
   a.M = a.K; a.Ng = a.R * a.S * a.C; a.Kg = a.N * a.Ho * a.Wo;
   int bm, bn, splits, kps;
   conv_wgrad_plan(a.M, a.Ng, a.Kg, &bm, &bn, &splits, &kps);
   a.kps = kps;
   auto ws = torch::empty({(int64_t)splits * a.M * a.Ng}, out.options());
   a.out = ws.data_ptr();
+  a.out_bytes = nbytes32(ws);
   auto st = stream();
   conv_wgrad_launch(a, bm, bn, splits, out.data_ptr<float>(), accumulate, st);
   if (bias_grad.has_value() && bias_grad->defined()) {

@@ -5,23 +5,31 @@
 //
 //   mode   GEMM C[M][N] = Σ_k A[m][k]·B[n][k]                A operand            B operand
 //   FWD    y[m=(n,ho,wo)][co]    k = (r,s,ci)   M=N·Ho·Wo     x gathered (k-contig) w[co][k] (k-contig)
-//   DGRAD  dx[m=(n,h,w)][ci]     k = (r,s,co)   M=N·H·W       dy gathered (k-contig) w[co][r][s][ci] (n-contig)
+//   DGRAD  dx[m=(n,h,w)][ci]     k = (t,co)     per class     dy gathered (k-contig) w[co][r][s][ci] (n-contig)
 //   WGRAD  dw[m=co][n=(r,s,ci)]  k = (n,ho,wo)  split-K       dy[p][co] (m-contig)   x gathered (n-contig)
+//
+// DGRAD parity classes: for stride s the input pixels split into s_h·s_w classes (h mod s_h,
+// w mod s_w); inside a class exactly the taps r ≡ (h+pad) (mod s) contribute, and
+// ho = (h + pad − r)/s is exact — so a strided dgrad is s² dense sub-GEMMs with no masked-out
+// work (a 3×3/s2 dgrad does the FLOPs of the forward, not 4× that; a 1×1/s2 dgrad writes zeros
+// for 3 of 4 classes).  Stride 1 is the single-class case (dilation allowed).
 //
 // Operands whose 16-B global vectors run along K ("KC") are staged into an LDS image
 // [rows][64] (128-B rows, 16-B chunk index XOR ((row>>1)&7): conflict-free ds_read_b128 for the
 // 16x16x32 fragment pattern).  Operands whose vectors run along M/N ("MC", i.e. K is strided in
 // memory) are staged as [64 k-rows][cols] (32-B pair index XOR f(k)) and read with gfx950's
 // ds_read_b64_tr_b16 hardware transpose, so dgrad needs no weight transpose and wgrad no
-// activation transpose.  Staging is register double-buffered (global→VGPR for tile t+1 is in
-// flight while the MFMAs consume tile t from LDS; one barrier per 64-deep K step).
+// activation transpose.  Staging is register double-buffered.
 //
-// Tile: BM×BN×64 per 256-thread workgroup, 2×2 waves, each wave (BM/2)×(BN/2) as 16×16 MFMA
-// tiles (v_mfma_f32_16x16x32_bf16).  The MFMA is issued with the operands swapped (D = Bᵀ·Aᵀ) so
-// each lane ends up holding 4 consecutive output channels of one output row → 8-B bf16 / 16-B
-// fp32 vector stores.  Epilogue options: bias, ReLU, and per-channel Σy / Σy² of the stored bf16
-// values (BatchNorm statistics) reduced across lanes, then waves through LDS, then one contiguous
-// atomicAdd row per workgroup.  Workgroup ids are remapped so each XCD owns a contiguous tile range.
+// Scheduling: a workgroup walks `tpb` consecutive output tiles as ONE flat sequence of 64-deep
+// K steps; the global→VGPR loads of step s+1 (possibly the first step of the next tile) are in
+// flight while the MFMAs of step s run, so small-K (1×1, Cin ≤ 128) convs are not serialised on
+// per-tile load latency.  Workgroup ids are remapped so each XCD owns a contiguous tile range.
+//
+// Tile: BM×BN×64 per 256-thread workgroup, 2×2 waves, v_mfma_f32_16x16x32_bf16, operands swapped
+// (D = Bᵀ·Aᵀ) so each lane holds 4 consecutive output channels of one output row → 8-B bf16 /
+// 16-B fp32 vector stores.  Epilogue: bias, ReLU, and per-channel Σy / Σy² of the stored bf16
+// values (BatchNorm statistics) reduced lanes → waves (LDS) → one contiguous atomic row per tile.
 #include "common.h"
 #include "kernels.h"
 
@@ -66,13 +74,87 @@ __device__ __forceinline__ bf16x8 read_mc(const char* tile, int krow, int col) {
   return __builtin_bit_cast(bf16x8, cat);
 }
 
+// Range-checked buffer access: an offset beyond the descriptor's byte count returns 0 on load
+// and is dropped on store, so padding / ragged edges need no branch (a per-element branch around
+// a load makes hipcc wait vmcnt(0) per element and serialises the staging pipeline).
+constexpr uint32_t OOB = 0xFFFFFFF0u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ uint4 gather8(const bf16_t* v) {
+  return make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                    (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-tile geometry
+// ---------------------------------------------------------------------------------------------
+struct Tile {
+  int bm0, bn0;   // first row / column of the tile (class-local rows for DGRAD)
+  int cls;        // DGRAD class
+  int Mc, Kgc;    // rows / K of the (class) GEMM
+  int kt0, kt1;   // K-step range (split range for WGRAD)
+  int split;      // WGRAD split index
+};
+
+template <int MODE, int BM, int BN>
+__device__ __forceinline__ Tile tile_of(const ConvArgs& a, int t) {
+  Tile T;
+  const int ntn = (a.Ng + BN - 1) / BN;
+  T.cls = 0;
+  T.split = 0;
+  T.Mc = a.M;
+  T.Kgc = a.Kg;
+  int local = t;
+  if constexpr (MODE == DGRAD) {
+    int c = 0;
+    while (c + 1 < a.ncls && t >= a.cls_tile0[c + 1]) ++c;
+    T.cls = c;
+    local = t - a.cls_tile0[c];
+    T.Mc = a.N * a.cls_Hc[c] * a.cls_Wc[c];
+    T.Kgc = a.cls_Th[c] * a.cls_Tw[c] * a.K;
+  } else if constexpr (MODE == WGRAD) {
+    const int ntm = (a.M + BM - 1) / BM;
+    const int nt = ntm * ntn;
+    T.split = t / nt;
+    local = t - T.split * nt;
+  }
+  if constexpr (MODE == FWD) {
+    // workgroup b owns column tile (b % ntn) and row tiles [(b / ntn)·tpb, +tpb): its tiles share
+    // bn0 (BN statistics accumulate in registers, one flush per workgroup) and the ntn workgroups
+    // of a row group run together, re-reading the same A tiles from L2
+    const int grp = local / (a.tpb * ntn), r = local - grp * a.tpb * ntn;
+    T.bn0 = (r / a.tpb) * BN;
+    T.bm0 = (grp * a.tpb + r % a.tpb) * BM;
+  } else {
+    T.bm0 = (local / ntn) * BM;
+    T.bn0 = (local % ntn) * BN;
+  }
+  const int nkt = (T.Kgc + BK - 1) / BK;
+  if constexpr (MODE == WGRAD) {
+    T.kt0 = T.split * a.kps;
+    T.kt1 = min(nkt, T.kt0 + a.kps);
+    if (T.kt1 <= T.kt0) T.kt1 = T.kt0 + 1;  // empty split: one zero step (slab must be written)
+  } else {
+    T.kt0 = 0;
+    T.kt1 = max(nkt, 1);  // a class with no taps still writes its (zero) tile
+  }
+  return T;
+}
+
 // ---------------------------------------------------------------------------------------------
 // generic per-element operand access (used when C or K is not a multiple of 8)
-// A(m, k), B(n, k) in GEMM terms.
 // ---------------------------------------------------------------------------------------------
 template <int MODE>
-__device__ __forceinline__ bf16_t elemA(const ConvArgs& a, int m, int k) {
-  if (m >= a.M || k >= a.Kg) return 0;
+__device__ __forceinline__ bf16_t elemA(const ConvArgs& a, const Tile& T, int m, int k) {
+  if (m >= T.Mc || k >= T.Kgc) return 0;
   if constexpr (MODE == FWD) {
     const int HoWo = a.Ho * a.Wo;
     const int n = m / HoWo, rem = m - n * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
@@ -81,28 +163,36 @@ __device__ __forceinline__ bf16_t elemA(const ConvArgs& a, int m, int k) {
     if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) return 0;
     return a.x[(((long)n * a.H + hi) * a.W + wi) * a.C + c];
   } else if constexpr (MODE == DGRAD) {
-    const int HW = a.H * a.W;
-    const int n = m / HW, rem = m - n * HW, h = rem / a.W, w = rem - h * a.W;
-    const int co = k % a.K, rs = k / a.K, r = rs / a.S, s = rs - r * a.S;
-    int th = h + a.ph - r * a.dh, tw = w + a.pw - s * a.dw;
-    if (th < 0 || tw < 0 || th % a.sh || tw % a.sw) return 0;
-    th /= a.sh;
-    tw /= a.sw;
-    if (th >= a.Ho || tw >= a.Wo) return 0;
-    return a.dy[(((long)n * a.Ho + th) * a.Wo + tw) * a.K + co];
+    const int c = T.cls;
+    const int Hc = a.cls_Hc[c], Wc = a.cls_Wc[c];
+    const int n = m / (Hc * Wc), rem = m - n * Hc * Wc, i = rem / Wc, j = rem - i * Wc;
+    const int psh = a.dg_masked ? 1 : a.sh, psw = a.dg_masked ? 1 : a.sw;
+    const int h = a.cls_a[c] + psh * i, w = a.cls_b[c] + psw * j;
+    const int co = k % a.K, t = k / a.K, th = t / a.cls_Tw[c], tw = t - th * a.cls_Tw[c];
+    const int rsh = a.dg_masked ? 1 : a.sh, rsw = a.dg_masked ? 1 : a.sw;
+    const int r = a.cls_r0[c] + rsh * th, s = a.cls_s0[c] + rsw * tw;
+    int nh = h + a.ph - r * a.dh, nw = w + a.pw - s * a.dw;
+    if (nh < 0 || nw < 0) return 0;
+    if (a.dg_masked && (nh % a.sh || nw % a.sw)) return 0;
+    const int ho = nh / a.sh, wo = nw / a.sw;
+    if (ho >= a.Ho || wo >= a.Wo) return 0;
+    return a.dy[(((long)n * a.Ho + ho) * a.Wo + wo) * a.K + co];
   } else {  // WGRAD: A[m=co][k=p] = dy[p][co]
     return a.dy[(long)k * a.K + m];
   }
 }
 
 template <int MODE>
-__device__ __forceinline__ bf16_t elemB(const ConvArgs& a, int n, int k) {
-  if (n >= a.Ng || k >= a.Kg) return 0;
+__device__ __forceinline__ bf16_t elemB(const ConvArgs& a, const Tile& T, int n, int k) {
+  if (n >= a.Ng || k >= T.Kgc) return 0;
   if constexpr (MODE == FWD) {
     return a.w[(long)n * a.Kg + k];
-  } else if constexpr (MODE == DGRAD) {  // B[n=ci][k=(r,s,co)] = w[co][r][s][ci]
-    const int co = k % a.K, rs = k / a.K;
-    return a.w[((long)co * a.R * a.S + rs) * a.C + n];
+  } else if constexpr (MODE == DGRAD) {  // B[n=ci][k=(t,co)] = w[co][r][s][ci]
+    const int c = T.cls;
+    const int co = k % a.K, t = k / a.K, th = t / a.cls_Tw[c], tw = t - th * a.cls_Tw[c];
+    const int rsh = a.dg_masked ? 1 : a.sh, rsw = a.dg_masked ? 1 : a.sw;
+    const int r = a.cls_r0[c] + rsh * th, s = a.cls_s0[c] + rsw * tw;
+    return a.w[(((long)co * a.R + r) * a.S + s) * a.C + n];
   } else {  // WGRAD: B[n=(r,s,ci)][k=p] = x[n_img, ho*sh-ph+r*dh, wo*sw-pw+s*dw, ci]
     const int HoWo = a.Ho * a.Wo;
     const int ni = k / HoWo, rem = k - ni * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
@@ -113,15 +203,25 @@ __device__ __forceinline__ bf16_t elemB(const ConvArgs& a, int n, int k) {
   }
 }
 
-__device__ __forceinline__ uint4 gather8(const bf16_t* v) {
-  return make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
-                    (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
+// global output row for a tile-local row (DGRAD classes interleave into the NHWC dx)
+template <int MODE>
+__device__ __forceinline__ long out_row(const ConvArgs& a, const Tile& T, int m) {
+  if constexpr (MODE == DGRAD) {
+    const int c = T.cls;
+    const int Hc = a.cls_Hc[c], Wc = a.cls_Wc[c];
+    const int n = m / (Hc * Wc), rem = m - n * Hc * Wc, i = rem / Wc, j = rem - i * Wc;
+    const int psh = a.dg_masked ? 1 : a.sh, psw = a.dg_masked ? 1 : a.sw;
+    const int h = a.cls_a[c] + psh * i, w = a.cls_b[c] + psw * j;
+    return ((long)n * a.H + h) * a.W + w;
+  } else {
+    return m;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------------
-template <int MODE, int BM, int BN, bool ALIGNED, bool STATS>
+template <int MODE, int BM, int BN, bool ALIGNED, bool STATS, bool BIAS>
 __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
@@ -129,42 +229,37 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int PA = BM * BK / 8 / NT, PB = BN * BK / 8 / NT;
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;  // MC: 16-B chunks per k-row
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int RED_BYTES = STATS ? 2 * WM * BN * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + RED_BYTES + 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int ntn = (a.Ng + BN - 1) / BN;
-  const int ntm = (a.M + BM - 1) / BM;
-  const int ntiles = ntn * ntm;
-  int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = id / ntiles;
-  const int tile = id - split * ntiles;
-  const int bm0 = (tile / ntn) * BM, bn0 = (tile % ntn) * BN;
-
-  const int nkt = (a.Kg + BK - 1) / BK;
-  int kt0 = 0, kt1 = nkt;
-  if constexpr (MODE == WGRAD) {
-    kt0 = split * a.kps;
-    kt1 = min(nkt, kt0 + a.kps);
-  }
-
-  // ---------------- per-thread precomputation (aligned path) ----------------
-  // A side
-  long a_base[PA];
-  int a_p0[PA], a_p1[PA];
-  // B side
-  long b_base[PB];
-  int b_p0[PB], b_p1[PB];
-  int a_fix = 0, b_fix = 0, b_fix2 = 0;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_begin = blk * a.tpb;
+  const int tile_end = min(a.cls_tile0[a.ncls], tile_begin + a.tpb);
+  if (tile_begin >= tile_end) return;
   const int HoWo = a.Ho * a.Wo;
-  if constexpr (ALIGNED) {
+  const rsrc_t rx = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t rw = make_rsrc(a.w, a.w_bytes);
+  const rsrc_t rdy = make_rsrc(a.dy, a.dy_bytes);
+  const rsrc_t rout = make_rsrc(a.out, a.out_bytes);
+
+  // ---------------- load-side per-tile state (aligned path) ----------------
+  int a_base[PA];
+  int a_p0[PA], a_p1[PA];
+  int b_base[PB];
+  int b_ok[PB];
+  int a_fix = 0, b_fix = 0, b_fix2 = 0, b_fix3 = 0;
+
+  auto prep_tile = [&](const Tile& T) {
+    if constexpr (!ALIGNED) return;
     if constexpr (MODE == FWD) {
 #pragma unroll
       for (int i = 0; i < PA; ++i) {
-        const int m = bm0 + (tid >> 3) + i * (NT / 8);
-        if (m < a.M) {
+        const int m = T.bm0 + (tid >> 3) + i * (NT / 8);
+        if (m < T.Mc) {
           const int n = m / HoWo, rem = m - n * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
-          a_base[i] = (long)n * a.H * a.W * a.C;
+          a_base[i] = n * a.H * a.W * a.C;
           a_p0[i] = ho * a.sh - a.ph;
           a_p1[i] = wo * a.sw - a.pw;
         } else {
@@ -175,47 +270,50 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < PB; ++i) {
-        const int n = bn0 + (tid >> 3) + i * (NT / 8);
-        b_base[i] = (long)n * a.Kg;
-        b_p0[i] = n < a.Ng;
-        b_p1[i] = 0;
+        const int n = T.bn0 + (tid >> 3) + i * (NT / 8);
+        b_base[i] = n * a.Kg;
+        b_ok[i] = n < a.Ng;
       }
     } else if constexpr (MODE == DGRAD) {
-      const int HW = a.H * a.W;
+      const int c = T.cls;
+      const int Hc = a.cls_Hc[c], Wc = a.cls_Wc[c], HWc = Hc * Wc;
+      const int ca = a.cls_a[c], cb = a.cls_b[c], r0 = a.cls_r0[c], s0 = a.cls_s0[c];
 #pragma unroll
       for (int i = 0; i < PA; ++i) {
-        const int m = bm0 + (tid >> 3) + i * (NT / 8);
-        if (m < a.M) {
-          const int n = m / HW, rem = m - n * HW, h = rem / a.W, w = rem - h * a.W;
-          a_base[i] = (long)n * HoWo * a.K;
-          a_p0[i] = h + a.ph;
-          a_p1[i] = w + a.pw;
+        const int m = T.bm0 + (tid >> 3) + i * (NT / 8);
+        if (m < T.Mc) {
+          const int n = m / HWc, rem = m - n * HWc, ii = rem / Wc, jj = rem - ii * Wc;
+          const int h = ca + a.sh * ii, w = cb + a.sw * jj;
+          a_base[i] = n * HoWo * a.K;
+          // ho = (h + ph - r0·dh)/sh − th·step (exact for the class)
+          a_p0[i] = (h + a.ph - r0 * a.dh) / a.sh;
+          a_p1[i] = (w + a.pw - s0 * a.dw) / a.sw;
         } else {
           a_base[i] = 0;
           a_p0[i] = -(1 << 28);
           a_p1[i] = -(1 << 28);
         }
       }
-      b_fix = bn0 + (tid % B_CPR) * 8;  // ci
+      b_fix = T.bn0 + (tid % B_CPR) * 8;  // ci
     } else {  // WGRAD
-      a_fix = bm0 + (tid % A_CPR) * 8;  // co
-      const int nn = bn0 + (tid % B_CPR) * 8;
+      a_fix = T.bm0 + (tid % A_CPR) * 8;  // co
+      const int nn = T.bn0 + (tid % B_CPR) * 8;
       if (nn < a.Ng) {
         const int ci = nn % a.C, rs = nn / a.C, r = rs / a.S, s = rs - r * a.S;
         b_fix = ci;
         b_fix2 = r * a.dh - a.ph;
-        b_p0[0] = s * a.dw - a.pw;
+        b_fix3 = s * a.dw - a.pw;
       } else {
         b_fix = -1;
         b_fix2 = -(1 << 28);
-        b_p0[0] = 0;
+        b_fix3 = 0;
       }
     }
-  }
+  };
 
   uint4 ra[PA], rb[PB];
 
-  auto load_tiles = [&](int kt) {
+  auto load_step = [&](const Tile& T, int kt) {
     if constexpr (ALIGNED) {
       if constexpr (MODE == FWD) {
         const int k = kt * BK + (tid & 7) * 8;
@@ -226,62 +324,55 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
         for (int i = 0; i < PA; ++i) {
           const int hi = a_p0[i] + ro, wi = a_p1[i] + so;
           const bool v = kv && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-          ra[i] = v ? *(const uint4*)(a.x + a_base[i] + ((long)hi * a.W + wi) * a.C + c)
-                    : make_uint4(0, 0, 0, 0);
+          const uint32_t off = (uint32_t)(a_base[i] + (hi * a.W + wi) * a.C + c) * 2u;
+          ra[i] = bload16(rx, v ? off : OOB);
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
-          const bool v = kv && b_p0[i];
-          rb[i] = v ? *(const uint4*)(a.w + b_base[i] + k) : make_uint4(0, 0, 0, 0);
+          const bool v = kv && b_ok[i];
+          rb[i] = bload16(rw, v ? (uint32_t)(b_base[i] + k) * 2u : OOB);
         }
       } else if constexpr (MODE == DGRAD) {
+        const int c = T.cls;
+        const int Tw = a.cls_Tw[c];
+        const int step_h = a.sh == 1 ? a.dh : 1, step_w = a.sw == 1 ? a.dw : 1;
         const int k = kt * BK + (tid & 7) * 8;
-        const bool kv = k < a.Kg;
-        const int co = k % a.K, rs = k / a.K, r = rs / a.S, s = rs - r * a.S;
-        const int ro = r * a.dh, so = s * a.dw;
+        const bool kv = k < T.Kgc;
+        const int co = k % a.K, t = k / a.K, th = t / Tw, tw = t - th * Tw;
+        const int ro = th * step_h, so = tw * step_w;
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
-          int th = a_p0[i] - ro, tw = a_p1[i] - so;
-          bool v = kv && th >= 0 && tw >= 0;
-          if (a.sh != 1) {
-            v = v && (th % a.sh) == 0 && (tw % a.sw) == 0;
-            th /= a.sh;
-            tw /= a.sw;
-          }
-          v = v && th < a.Ho && tw < a.Wo;
-          ra[i] = v ? *(const uint4*)(a.dy + a_base[i] + ((long)th * a.Wo + tw) * a.K + co)
-                    : make_uint4(0, 0, 0, 0);
+          const int ho = a_p0[i] - ro, wo = a_p1[i] - so;
+          const bool v = kv && (unsigned)ho < (unsigned)a.Ho && (unsigned)wo < (unsigned)a.Wo;
+          const uint32_t off = (uint32_t)(a_base[i] + (ho * a.Wo + wo) * a.K + co) * 2u;
+          ra[i] = bload16(rdy, v ? off : OOB);
         }
+        const int r0 = a.cls_r0[c], s0 = a.cls_s0[c];
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
           const int kk = kt * BK + tid / B_CPR + i * (NT / B_CPR);
-          const bool v = kk < a.Kg && b_fix < a.Ng;
-          if (v) {
-            const int co2 = kk % a.K, rs2 = kk / a.K;
-            rb[i] = *(const uint4*)(a.w + ((long)co2 * a.R * a.S + rs2) * a.C + b_fix);
-          } else {
-            rb[i] = make_uint4(0, 0, 0, 0);
-          }
+          const bool v = kk < T.Kgc && b_fix < a.Ng;
+          const int co2 = kk % a.K, t2 = kk / a.K, th2 = t2 / Tw, tw2 = t2 - th2 * Tw;
+          const int r = r0 + a.sh * th2, s = s0 + a.sw * tw2;
+          const uint32_t off = (uint32_t)(((co2 * a.R + r) * a.S + s) * a.C + b_fix) * 2u;
+          rb[i] = bload16(rw, v ? off : OOB);
         }
       } else {  // WGRAD
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
           const int p = kt * BK + tid / A_CPR + i * (NT / A_CPR);
           const bool v = p < a.Kg && a_fix < a.M;
-          ra[i] = v ? *(const uint4*)(a.dy + (long)p * a.K + a_fix) : make_uint4(0, 0, 0, 0);
+          ra[i] = bload16(rdy, v ? (uint32_t)(p * a.K + a_fix) * 2u : OOB);
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
           const int p = kt * BK + tid / B_CPR + i * (NT / B_CPR);
-          bool v = p < a.Kg && b_fix >= 0;
-          uint4 val = make_uint4(0, 0, 0, 0);
-          if (v) {
-            const int ni = p / HoWo, rem = p - ni * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
-            const int hi = ho * a.sh + b_fix2, wi = wo * a.sw + b_p0[0];
-            if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-              val = *(const uint4*)(a.x + (((long)ni * a.H + hi) * a.W + wi) * a.C + b_fix);
-          }
-          rb[i] = val;
+          const int ni = p / HoWo, rem = p - ni * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
+          const int hi = ho * a.sh + b_fix2, wi = wo * a.sw + b_fix3;
+          const bool v = p < a.Kg && b_fix >= 0 && (unsigned)hi < (unsigned)a.H &&
+                         (unsigned)wi < (unsigned)a.W;
+          const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_fix) * 2u;
+          rb[i] = bload16(rx, v ? off : OOB);
         }
       }
     } else {
@@ -290,15 +381,15 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       for (int i = 0; i < PA; ++i) {
         bf16_t e[8];
         if constexpr (!A_MC) {
-          const int m = bm0 + (tid >> 3) + i * (NT / 8);
+          const int m = T.bm0 + (tid >> 3) + i * (NT / 8);
           const int k = kt * BK + (tid & 7) * 8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = elemA<MODE>(a, m, k + j);
+          for (int j = 0; j < 8; ++j) e[j] = elemA<MODE>(a, T, m, k + j);
         } else {
           const int k = kt * BK + tid / A_CPR + i * (NT / A_CPR);
-          const int m = bm0 + (tid % A_CPR) * 8;
+          const int m = T.bm0 + (tid % A_CPR) * 8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = elemA<MODE>(a, m + j, k);
+          for (int j = 0; j < 8; ++j) e[j] = elemA<MODE>(a, T, m + j, k);
         }
         ra[i] = gather8(e);
       }
@@ -306,22 +397,22 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       for (int i = 0; i < PB; ++i) {
         bf16_t e[8];
         if constexpr (!B_MC) {
-          const int n = bn0 + (tid >> 3) + i * (NT / 8);
+          const int n = T.bn0 + (tid >> 3) + i * (NT / 8);
           const int k = kt * BK + (tid & 7) * 8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = elemB<MODE>(a, n, k + j);
+          for (int j = 0; j < 8; ++j) e[j] = elemB<MODE>(a, T, n, k + j);
         } else {
           const int k = kt * BK + tid / B_CPR + i * (NT / B_CPR);
-          const int n = bn0 + (tid % B_CPR) * 8;
+          const int n = T.bn0 + (tid % B_CPR) * 8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) e[j] = elemB<MODE>(a, n + j, k);
+          for (int j = 0; j < 8; ++j) e[j] = elemB<MODE>(a, T, n + j, k);
         }
         rb[i] = gather8(e);
       }
     }
   };
 
-  auto store_tiles = [&](int buf) {
+  auto store_step = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + A_BYTES;
 #pragma unroll
@@ -343,22 +434,15 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
   };
 
   f32x4 acc[RM][RN];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+    for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
 
-  if (kt0 < kt1) {
-    load_tiles(kt0);
-    store_tiles(0);
-  }
-  __syncthreads();
-
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) load_tiles(kt + 1);
-    const char* As = smem + cur * STAGE;
+  auto compute_step = [&](int buf) {
+    const char* As = smem + buf * STAGE;
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -385,136 +469,239 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
         for (int rn = 0; rn < RN; ++rn)
           acc[rm][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[rn], af[rm], acc[rm][rn], 0, 0, 0);
     }
-    if (more) store_tiles(cur ^ 1);
-    __syncthreads();
-  }
+  };
 
-  // ---------------- epilogue ----------------
+  // per-lane BN statistics, accumulated over all tiles of the workgroup (they share bn0)
+  float s_sum[RN][4], s_sq[RN][4];
+#pragma unroll
+  for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
+
   // lane holds C[m = bm0 + wm*TM + rm*16 + (lane&15)][n = bn0 + wn*TN + rn*16 + (lane>>4)*4 + i]
-  if constexpr (MODE == WGRAD) {
-    float* out = (float*)a.out + (long)split * a.M * a.Ng;
-    const bool vec = (a.Ng & 3) == 0;
+  auto epilogue = [&](const Tile& T) {
+    if constexpr (MODE == WGRAD) {
+      if ((a.Ng & 3) == 0) {
+        const uint32_t slab0 = (uint32_t)T.split * (uint32_t)(a.M * a.Ng);
 #pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      const int m = bm0 + wm * TM + rm * 16 + (lane & 15);
-      if (m >= a.M) continue;
+        for (int rm = 0; rm < RM; ++rm) {
+          const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
 #pragma unroll
-      for (int rn = 0; rn < RN; ++rn) {
-        const int n0 = bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
-        float* p = out + (long)m * a.Ng + n0;
-        if (vec && n0 + 3 < a.Ng) {
-          *(float4*)p = make_float4(acc[rm][rn][0], acc[rm][rn][1], acc[rm][rn][2], acc[rm][rn][3]);
-        } else {
+          for (int rn = 0; rn < RN; ++rn) {
+            const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+            const bool v = m < a.M && n0 < a.Ng;
+            const uint32_t off = (slab0 + (uint32_t)(m * a.Ng + n0)) * 4u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, acc[rm][rn]), rout,
+                                                   v ? off : OOB, 0, 0);
+          }
+        }
+      } else {
+        float* out = (float*)a.out + (long)T.split * a.M * a.Ng;
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (n0 + i < a.Ng) p[i] = acc[rm][rn][i];
+        for (int rm = 0; rm < RM; ++rm) {
+          const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
+          if (m >= a.M) continue;
+#pragma unroll
+          for (int rn = 0; rn < RN; ++rn) {
+            const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+            float* p = out + (long)m * a.Ng + n0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (n0 + i < a.Ng) p[i] = acc[rm][rn][i];
+          }
         }
       }
-    }
-  } else {
-    bf16_t* out = (bf16_t*)a.out;
-    const bool vec = ((a.ldc & 3) == 0);
-    float s_sum[RN][4], s_sq[RN][4];
+    } else {
+      bf16_t* out = (bf16_t*)a.out;
+      const bool fast = ((a.Ng & 3) == 0) && ((a.ldc & 3) == 0);
+      const rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)a.Ng * 4u : 0u);
 #pragma unroll
-    for (int rn = 0; rn < RN; ++rn)
+      for (int rm = 0; rm < RM; ++rm) {
+        const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
+        const bool mv = m < T.Mc;
+        const long orow = mv ? out_row<MODE>(a, T, m) : 0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
+        for (int rn = 0; rn < RN; ++rn) {
+          const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (BIAS) {
+            if (fast) {
+              const v4u32 b = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
 #pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      const int m = bm0 + wm * TM + rm * 16 + (lane & 15);
-      const bool mv = m < a.M;
+              for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(b[i]);
+            } else {
 #pragma unroll
-      for (int rn = 0; rn < RN; ++rn) {
-        const int n0 = bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
-        float v[4];
-        bf16_t h[4];
+              for (int i = 0; i < 4; ++i) bv[i] = (n0 + i < a.Ng) ? a.bias[n0 + i] : 0.f;
+            }
+          }
+          float v[4];
+          bf16_t h[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float t = acc[rm][rn][i];
-          if (a.bias != nullptr && n0 + i < a.Ng) t += a.bias[n0 + i];
-          if (a.relu) t = fmaxf(t, 0.f);
-          h[i] = f2bf(t);
-          v[i] = bf2f(h[i]);
-        }
-        if (mv) {
-          bf16_t* p = out + (long)m * a.ldc + n0;
-          if (vec && n0 + 3 < a.Ng) {
-            *(uint2*)p = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16),
-                                    (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-          } else {
+          for (int i = 0; i < 4; ++i) {
+            float t = acc[rm][rn][i] + bv[i];
+            if (a.relu) t = fmaxf(t, 0.f);
+            h[i] = f2bf(t);
+            v[i] = bf2f(h[i]);
+          }
+          if (fast) {
+            const bool v_ok = mv && n0 < a.Ng;
+            const uint32_t off = (uint32_t)(orow * a.ldc + n0) * 2u;
+            v2u32 pk;
+            pk[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+            pk[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+            __builtin_amdgcn_raw_buffer_store_b64(pk, rout, v_ok ? off : OOB, 0, 0);
+            if constexpr (STATS) {
+              const float msk = v_ok ? 1.f : 0.f;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                s_sum[rn][i] += msk * v[i];
+                s_sq[rn][i] += msk * v[i] * v[i];
+              }
+            }
+          } else if (mv) {
+            bf16_t* p = out + orow * a.ldc + n0;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
               if (n0 + i < a.Ng) p[i] = h[i];
-          }
-          if constexpr (STATS) {
+            if constexpr (STATS) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              s_sum[rn][i] += v[i];
-              s_sq[rn][i] += v[i] * v[i];
+              for (int i = 0; i < 4; ++i) {
+                const float msk = (n0 + i < a.Ng) ? 1.f : 0.f;
+                s_sum[rn][i] += msk * v[i];
+                s_sq[rn][i] += msk * v[i] * v[i];
+              }
             }
           }
         }
       }
     }
-    if constexpr (STATS) {
-      // reduce over the 16 lanes that share (lane>>4): they hold different m of the same n
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            s_sum[rn][i] += __shfl_xor(s_sum[rn][i], o, 64);
-            s_sq[rn][i] += __shfl_xor(s_sq[rn][i], o, 64);
-          }
-        }
-      // LDS: red[wm][2][BN]
-      float* red = (float*)smem;  // main loop ended with a barrier: smem is free
-      if ((lane & 15) == 0) {
+  };
+
+  auto flush_stats = [&](int bn0) {
+    if constexpr (STATS && MODE != WGRAD) {
+      const int nb = bn0;
+      {
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int nl = wn * TN + rn * 16 + (lane >> 4) * 4 + i;
-            red[(wm * 2 + 0) * BN + nl] = s_sum[rn][i];
-            red[(wm * 2 + 1) * BN + nl] = s_sq[rn][i];
-          }
-      }
-      __syncthreads();
-      for (int t = tid; t < 2 * BN; t += NT) {
-        const int which = t / BN, nl = t - which * BN;
-        const int n = bn0 + nl;
-        if (n < a.Ng) {
-          float v = 0.f;
 #pragma unroll
-          for (int w = 0; w < WM; ++w) v += red[(w * 2 + which) * BN + nl];
-          atomicAdd(a.stats + which * a.Ng + n, v);
+            for (int o = 1; o < 16; o <<= 1) {
+              s_sum[rn][i] += __shfl_xor(s_sum[rn][i], o, 64);
+              s_sq[rn][i] += __shfl_xor(s_sq[rn][i], o, 64);
+            }
+          }
+        float* red = (float*)(smem + 2 * STAGE);  // dedicated region (staging may be in flight)
+        if ((lane & 15) == 0) {
+#pragma unroll
+          for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int nl = wn * TN + rn * 16 + (lane >> 4) * 4 + i;
+              red[(wm * 2 + 0) * BN + nl] = s_sum[rn][i];
+              red[(wm * 2 + 1) * BN + nl] = s_sq[rn][i];
+            }
+        }
+        __syncthreads();
+        for (int t = tid; t < 2 * BN; t += NT) {
+          const int which = t / BN, nl = t - which * BN;
+          const int n = nb + nl;
+          if (n < a.Ng) {
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) v += red[(w * 2 + which) * BN + nl];
+            atomicAdd(a.stats + which * a.Ng + n, v);
+          }
         }
       }
     }
+  };
+
+  // ---------------- flat (tile, k-step) pipeline ----------------
+  int lt = tile_begin;             // load cursor
+  Tile LT = tile_of<MODE, BM, BN>(a, lt);
+  int lkt = LT.kt0;
+  prep_tile(LT);
+  Tile CT = LT;                    // compute cursor
+  int ckt = lkt;
+  zero_acc();
+  load_step(LT, lkt);
+  store_step(0);
+  __syncthreads();
+  int buf = 0;
+  for (;;) {
+    // advance the load cursor
+    bool more = true;
+    if (lkt + 1 < LT.kt1) {
+      ++lkt;
+    } else if (lt + 1 < tile_end) {
+      ++lt;
+      LT = tile_of<MODE, BM, BN>(a, lt);
+      lkt = LT.kt0;
+      prep_tile(LT);
+    } else {
+      more = false;
+    }
+    if (more) load_step(LT, lkt);
+    compute_step(buf);
+    if (ckt + 1 >= CT.kt1) {
+      epilogue(CT);
+      zero_acc();
+      if (more) {
+        CT = LT;   // next computed step is the first step of the (just loaded) next tile
+        ckt = lkt;
+      }
+    } else {
+      ++ckt;
+    }
+    if (!more) break;
+    store_step(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
   }
+  flush_stats(CT.bn0);
 }
 
-// fp32 split-K slab reduction: out[i] (+)= Σ_z slab[z][i]
-__global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                     long n, int splits, int accumulate) {
+// fp32 split-K slab reduction: out[i] (+)= Σ_z slab[z][i].  2-D parallel: each workgroup owns
+// PPB float4 positions × G split groups (G = 256/PPB), partial sums combined through LDS.
+template <int G>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab,
+                                                            float* __restrict__ out, long n,
+                                                            int splits, int accumulate) {
+  constexpr int PPB = 256 / G;
+  __shared__ float4 part[G][PPB];
+  const int pl = threadIdx.x % PPB, g = threadIdx.x / PPB;
   const long n4 = n / 4;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 s = accumulate ? ((const float4*)out)[i] : make_float4(0, 0, 0, 0);
-    for (int z = 0; z < splits; ++z) {
+  const long i = blockIdx.x * (long)PPB + pl;
+  float4 s = make_float4(0, 0, 0, 0);
+  if (i < n4) {
+    for (int z = g; z < splits; z += G) {
       const float4 v = ((const float4*)(slab + (long)z * n))[i];
       s.x += v.x;
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
     }
-    ((float4*)out)[i] = s;
   }
-  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
-       i += (long)gridDim.x * blockDim.x) {
-    float s = accumulate ? out[i] : 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[(long)z * n + i];
-    out[i] = s;
+  part[g][pl] = s;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 t = accumulate ? ((const float4*)out)[i] : make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      t.x += part[q][pl].x;
+      t.y += part[q][pl].y;
+      t.z += part[q][pl].z;
+      t.w += part[q][pl].w;
+    }
+    ((float4*)out)[i] = t;
+  }
+  // scalar tail (n % 4)
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long j = n4 * 4 + threadIdx.x;
+    float t = accumulate ? out[j] : 0.f;
+    for (int z = 0; z < splits; ++z) t += slab[(long)z * n + j];
+    out[j] = t;
   }
 }
 
@@ -535,28 +722,26 @@ __global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ 
                                               red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-template <int MODE, int BM, int BN, bool AL, bool ST>
-void launch_t(const ConvArgs& a, int splits, hipStream_t st) {
-  const int tiles = cdiv(a.M, BM) * cdiv(a.Ng, BN);
-  hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, AL, ST>), dim3(tiles * splits), dim3(NT), 0, st,
-                     a);
+template <int MODE, int BM, int BN, bool AL, bool ST, bool BI>
+void launch_t(const ConvArgs& a, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, AL, ST, BI>), dim3(blocks), dim3(NT), 0, st, a);
 }
 
-template <int MODE, bool AL, bool ST>
-void launch_cfg(const ConvArgs& a, int bm, int bn, int splits, hipStream_t st) {
+template <int MODE, bool AL, bool ST, bool BI = false>
+void launch_cfg(const ConvArgs& a, int bm, int bn, int blocks, hipStream_t st) {
   if (bm == 128 && bn == 128)
-    launch_t<MODE, 128, 128, AL, ST>(a, splits, st);
+    launch_t<MODE, 128, 128, AL, ST, BI>(a, blocks, st);
   else if (bm == 128 && bn == 64)
-    launch_t<MODE, 128, 64, AL, ST>(a, splits, st);
+    launch_t<MODE, 128, 64, AL, ST, BI>(a, blocks, st);
   else if (bm == 64 && bn == 128)
-    launch_t<MODE, 64, 128, AL, ST>(a, splits, st);
+    launch_t<MODE, 64, 128, AL, ST, BI>(a, blocks, st);
   else
-    launch_t<MODE, 64, 64, AL, ST>(a, splits, st);
+    launch_t<MODE, 64, 64, AL, ST, BI>(a, blocks, st);
 }
 
 }  // namespace
 
-static void pick_tile(int M, int Ng, int& bm, int& bn) {
+static void pick_tile(long M, int Ng, int& bm, int& bn) {
   bn = Ng <= 64 ? 64 : 128;
   bm = M <= 64 ? 64 : 128;
   // small problems: prefer more workgroups
@@ -564,26 +749,129 @@ static void pick_tile(int M, int Ng, int& bm, int& bn) {
   if (bm == 128 && (long)cdiv(M, bm) * cdiv(Ng, bn) < 256) bm = 64;
 }
 
-void conv_fwd_launch(const ConvArgs& a, hipStream_t st) {
+// tiles per workgroup: keep ≥ ~2 workgroups per CU, and ≥ ~8 K-steps per workgroup
+static int pick_tpb(long tiles, int nkt) {
+  const char* env = getenv("TDL_CONV_TPB");
+  if (env) return std::max(1, atoi(env));
+  const long want_steps = 8;
+  long tpb = (want_steps + nkt - 1) / std::max(nkt, 1);
+  const long cap = std::max<long>(1, tiles / 512);
+  tpb = std::max<long>(1, std::min(tpb, cap));
+  return (int)tpb;
+}
+
+void conv_fwd_launch(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
   int bm, bn;
   pick_tile(a.M, a.Ng, bm, bn);
+  const long ntm = cdiv(a.M, bm), ntn = cdiv(a.Ng, bn);
+  a.ncls = 1;
+  a.tpb = pick_tpb(ntm * ntn, cdiv(a.Kg, BK));
+  // row groups of tpb tiles × column tiles (see tile_of: FWD ordering)
+  const long groups = (ntm + a.tpb - 1) / a.tpb;
+  const int blocks = (int)(groups * ntn);
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+  a.splits = 1;
   const bool al = (a.C % 8 == 0) && (a.K % 8 == 0);
   const bool stats = a.stats != nullptr;
+  const bool bias = a.bias != nullptr;
   if (al) {
-    if (stats) launch_cfg<FWD, true, true>(a, bm, bn, 1, st);
-    else launch_cfg<FWD, true, false>(a, bm, bn, 1, st);
+    if (bias) {
+      if (stats) launch_cfg<FWD, true, true, true>(a, bm, bn, blocks, st);
+      else launch_cfg<FWD, true, false, true>(a, bm, bn, blocks, st);
+    } else {
+      if (stats) launch_cfg<FWD, true, true>(a, bm, bn, blocks, st);
+      else launch_cfg<FWD, true, false>(a, bm, bn, blocks, st);
+    }
   } else {
-    if (stats) launch_cfg<FWD, false, true>(a, bm, bn, 1, st);
-    else launch_cfg<FWD, false, false>(a, bm, bn, 1, st);
+    if (bias) {
+      if (stats) launch_cfg<FWD, false, true, true>(a, bm, bn, blocks, st);
+      else launch_cfg<FWD, false, false, true>(a, bm, bn, blocks, st);
+    } else {
+      if (stats) launch_cfg<FWD, false, true>(a, bm, bn, blocks, st);
+      else launch_cfg<FWD, false, false>(a, bm, bn, blocks, st);
+    }
   }
 }
 
-void conv_dgrad_launch(const ConvArgs& a, hipStream_t st) {
+void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  const bool masked = (a.sh > 1 && a.dh > 1) || (a.sw > 1 && a.dw > 1) ||
+                      a.sh * a.sw > MAX_DG_CLASSES;
+  a.dg_masked = masked ? 1 : 0;
+  // build parity classes
+  int ncls = 0;
+  long Mmax = 0;
+  const int sh = masked ? 1 : a.sh, sw = masked ? 1 : a.sw;
+  for (int ca = 0; ca < sh; ++ca)
+    for (int cb = 0; cb < sw; ++cb) {
+      const int c = ncls++;
+      a.cls_a[c] = ca;
+      a.cls_b[c] = cb;
+      a.cls_Hc[c] = ca < a.H ? (a.H - ca + sh - 1) / sh : 0;
+      a.cls_Wc[c] = cb < a.W ? (a.W - cb + sw - 1) / sw : 0;
+      if (masked || a.sh == 1) {
+        a.cls_r0[c] = 0;
+        a.cls_Th[c] = a.R;
+      } else {
+        const int r0 = ((ca + a.ph) % a.sh + a.sh) % a.sh;
+        a.cls_r0[c] = r0;
+        a.cls_Th[c] = r0 < a.R ? (a.R - r0 + a.sh - 1) / a.sh : 0;
+      }
+      if (masked || a.sw == 1) {
+        a.cls_s0[c] = 0;
+        a.cls_Tw[c] = a.S;
+      } else {
+        const int s0 = ((cb + a.pw) % a.sw + a.sw) % a.sw;
+        a.cls_s0[c] = s0;
+        a.cls_Tw[c] = s0 < a.S ? (a.S - s0 + a.sw - 1) / a.sw : 0;
+      }
+      Mmax = std::max<long>(Mmax, (long)a.N * a.cls_Hc[c] * a.cls_Wc[c]);
+    }
+  // heaviest classes first (longest-processing-time order: no heavy tail at the end of the grid)
+  for (int i = 0; i < ncls; ++i)
+    for (int j = i + 1; j < ncls; ++j)
+      if (a.cls_Th[j] * a.cls_Tw[j] > a.cls_Th[i] * a.cls_Tw[i]) {
+        std::swap(a.cls_a[i], a.cls_a[j]);
+        std::swap(a.cls_b[i], a.cls_b[j]);
+        std::swap(a.cls_Hc[i], a.cls_Hc[j]);
+        std::swap(a.cls_Wc[i], a.cls_Wc[j]);
+        std::swap(a.cls_r0[i], a.cls_r0[j]);
+        std::swap(a.cls_Th[i], a.cls_Th[j]);
+        std::swap(a.cls_s0[i], a.cls_s0[j]);
+        std::swap(a.cls_Tw[i], a.cls_Tw[j]);
+      }
+  if (masked) {  // single class with original (masked) stride semantics
+    a.cls_Hc[0] = a.H;
+    a.cls_Wc[0] = a.W;
+    Mmax = (long)a.N * a.H * a.W;
+  }
+  // classes with no contributing taps (e.g. 3 of 4 for a 1×1/s2 conv) are zero: one memset
+  // instead of GEMM tiles (they are last after the LPT sort)
+  int nz = ncls;
+  while (nz > 0 && a.cls_Th[nz - 1] * a.cls_Tw[nz - 1] == 0) --nz;
+  if (nz < ncls) hipMemsetAsync(a.out, 0, (size_t)a.out_bytes, st);
+  ncls = nz;
+  if (ncls == 0) return;
+  a.ncls = ncls;
   int bm, bn;
-  pick_tile(a.M, a.Ng, bm, bn);
-  const bool al = (a.C % 8 == 0) && (a.K % 8 == 0);
-  if (al) launch_cfg<DGRAD, true, false>(a, bm, bn, 1, st);
-  else launch_cfg<DGRAD, false, false>(a, bm, bn, 1, st);
+  pick_tile(Mmax * ncls, a.Ng, bm, bn);
+  a.cls_tile0[0] = 0;
+  int maxkt = 1;
+  for (int c = 0; c < ncls; ++c) {
+    const long Mc = (long)a.N * a.cls_Hc[c] * a.cls_Wc[c];
+    a.cls_tile0[c + 1] = a.cls_tile0[c] + (int)(cdiv(Mc, bm) * (long)cdiv(a.Ng, bn));
+    maxkt = std::max(maxkt, cdiv((long)a.cls_Th[c] * a.cls_Tw[c] * a.K, BK));
+  }
+  const long tiles = a.cls_tile0[ncls];
+  if (tiles == 0) return;
+  a.tpb = pick_tpb(tiles, maxkt);
+  a.splits = 1;
+  const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
+  const bool al = (a.C % 8 == 0) && (a.K % 8 == 0) && !masked;
+  if (al) launch_cfg<DGRAD, true, false>(a, bm, bn, blocks, st);
+  else launch_cfg<DGRAD, false, false>(a, bm, bn, blocks, st);
 }
 
 void conv_wgrad_plan(int M, int Ng, long Kg, int* bm, int* bn, int* splits, int* kps) {
@@ -591,23 +879,39 @@ void conv_wgrad_plan(int M, int Ng, long Kg, int* bm, int* bn, int* splits, int*
   *bn = Ng <= 64 ? 64 : 128;
   const int tiles = cdiv(M, *bm) * cdiv(Ng, *bn);
   const int nkt = cdiv(Kg, BK);
-  int target = 1024;  // ≈4 workgroups per CU over 256 CUs
+  const char* env = getenv("TDL_WGRAD_TARGET");
+  const int target = env ? atoi(env) : 768;  // ≈3 workgroups per CU over 256 CUs
   int s = std::max(1, std::min(nkt, target / std::max(tiles, 1)));
   int per = cdiv(nkt, s);
-  per = std::max(per, 4);  // at least 4 K-steps per split
+  per = std::max(per, 8);  // at least 8 K-steps per split
   *kps = per;
   *splits = cdiv(nkt, per);
 }
 
-void conv_wgrad_launch(const ConvArgs& a, int bm, int bn, int splits, float* out, bool accumulate,
+void conv_wgrad_launch(const ConvArgs& a0, int bm, int bn, int splits, float* out, bool accumulate,
                        hipStream_t st) {
+  ConvArgs a = a0;
+  const long tiles = (long)cdiv(a.M, bm) * cdiv(a.Ng, bn) * splits;
+  a.ncls = 1;
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)tiles;
+  a.tpb = 1;
+  a.splits = splits;
   const bool al = (a.C % 8 == 0) && (a.K % 8 == 0);
-  if (al) launch_cfg<WGRAD, true, false>(a, bm, bn, splits, st);
-  else launch_cfg<WGRAD, false, false>(a, bm, bn, splits, st);
+  if (al) launch_cfg<WGRAD, true, false>(a, bm, bn, (int)tiles, st);
+  else launch_cfg<WGRAD, false, false>(a, bm, bn, (int)tiles, st);
   const long n = (long)a.M * a.Ng;
-  const int blocks = (int)std::min<long>(2048, std::max<long>(1, (n / 4 + 255) / 256));
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)a.out, out,
-                     n, splits, accumulate ? 1 : 0);
+  const long n4 = std::max<long>(1, n / 4);
+  if (splits >= 64) {
+    hipLaunchKernelGGL(splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
+                       (const float*)a.out, out, n, splits, accumulate ? 1 : 0);
+  } else if (splits >= 8) {
+    hipLaunchKernelGGL(splitk_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st,
+                       (const float*)a.out, out, n, splits, accumulate ? 1 : 0);
+  } else {
+    hipLaunchKernelGGL(splitk_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
+                       (const float*)a.out, out, n, splits, accumulate ? 1 : 0);
+  }
 }
 
 void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st) {

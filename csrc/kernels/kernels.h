@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <cstdlib>
 
 namespace tdl {
 
@@ -20,8 +21,18 @@ struct ConvArgs {
   int M, Ng, Kg;     // GEMM dims
   int ldc;
   int relu;
+  uint32_t x_bytes, w_bytes, dy_bytes, out_bytes;  // buffer-descriptor ranges (OOB -> 0 / dropped)
   int kps;           // WGRAD: K-steps per split
+  int splits;        // WGRAD: number of K splits
+  int tpb;           // tiles per workgroup (FWD / DGRAD multi-tile pipelining)
+  // DGRAD parity classes (stride s: s_h·s_w classes of input pixels, each with its exact taps)
+  int ncls;
+  int dg_masked;     // 1: stride>1 with dilation>1 — single class, divisibility-masked taps
+  int cls_tile0[17]; // prefix sum of tiles per class
+  int cls_a[16], cls_b[16], cls_Hc[16], cls_Wc[16];
+  int cls_r0[16], cls_Th[16], cls_s0[16], cls_Tw[16];
 };
+constexpr int MAX_DG_CLASSES = 16;
 
 void conv_fwd_launch(const ConvArgs& a, hipStream_t st);
 void conv_dgrad_launch(const ConvArgs& a, hipStream_t st);

@@ -42,6 +42,11 @@ CONV_SHAPES = [
     (2, 13, 13, 258, 258, 3, 3, 1, (1, 1, 1, 1), 1),    # reference preset C=258 (generic path)
     (2, 9, 9, 40, 1, 3, 3, 1, (1, 1, 1, 1), 1),         # decoder 3x3 -> 1 channel
     (4, 7, 7, 512, 2048, 1, 1, 1, (0, 0, 0, 0), 1),     # layer4 expand
+    (2, 13, 13, 24, 16, 3, 3, 2, (2, 2, 2, 2), 2),      # stride 2 + dilation 2 (masked dgrad)
+    (1, 9, 9, 258, 40, 3, 3, 2, (1, 1, 1, 1), 1),       # C % 8 != 0 with parity classes
+    (2, 11, 12, 16, 24, 1, 1, 2, (0, 0, 0, 0), 1),      # 1x1 s2 on odd/even sizes
+    (2, 12, 12, 16, 16, 3, 3, 3, (1, 1, 1, 1), 1),      # stride 3 (9 parity classes)
+    (64, 28, 28, 128, 128, 1, 1, 1, (0, 0, 0, 0), 1),   # multi-tile pipelining (tpb > 1)
 ]
 
 
