@@ -66,6 +66,10 @@ def build(verbose=True, force=False):
         obj = os.path.join(OBJ, os.path.basename(src) + ".o")
         if force or _newer(src, obj, headers):
             jobs.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", "-o", obj, src])
+    for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
+        obj = os.path.join(OBJ, "rt_" + os.path.basename(src) + ".o")
+        if force or _newer(src, obj, headers):
+            jobs.append([HIPCC, *common, "-pthread", "-c", "-o", obj, src])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")
     if force or _newer(bsrc, bobj, headers):
@@ -86,7 +90,7 @@ def build(verbose=True, force=False):
         torch_lib = libdirs[0]
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
                 "-L" + torch_lib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-                "-ltorch_hip", "-lamdhip64", f"-Wl,-rpath,{torch_lib}"]
+                "-ltorch_hip", "-lamdhip64", "-lz", "-pthread", f"-Wl,-rpath,{torch_lib}"]
         _run(link)
         if verbose:
             print(f"[build_ext] linked {os.path.relpath(out, ROOT)}", flush=True)

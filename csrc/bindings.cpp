@@ -5,6 +5,7 @@
 #include <c10/hip/HIPCachingAllocator.h>
 
 #include "kernels/kernels.h"
+#include "runtime/loader.h"
 
 using torch::Tensor;
 using namespace tdl;
@@ -341,6 +342,82 @@ void upsample_bwd(Tensor dy, Tensor dx, Tensor ih, Tensor wh, Tensor iw, Tensor 
                       dy.size(1), dy.size(2), stream());
 }
 
+
+// --------------------------------------------------------------------------- native data loader
+struct PyLoader {
+  std::unique_ptr<tdl_rt::BatchLoader> impl;
+  bool has_masks;
+  bool pin;
+  PyLoader(std::vector<std::string> images, std::vector<std::string> masks, int batch, bool augment,
+           bool shuffle, bool repeat, int64_t seed, int threads, int prefetch, int channels,
+           int transformation, bool pin_memory)
+      : has_masks(!masks.empty()), pin(pin_memory) {
+    impl.reset(new tdl_rt::BatchLoader(images, masks, batch, augment, shuffle, repeat,
+                                       (uint64_t)seed, threads, prefetch, channels,
+                                       transformation, 0.0));
+  }
+  py::object next() {
+    tdl_rt::Batch b;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = impl->next(b);
+    }
+    if (!ok) return py::none();
+    const int B = impl->batch(), H = impl->height(), W = impl->width(), C = impl->channels();
+    auto opt = torch::TensorOptions().pinned_memory(pin);
+    Tensor x = torch::empty({B, H, W, C}, opt.dtype(torch::kBFloat16));
+    memcpy(x.data_ptr(), b.x.data(), b.x.size() * 2);
+    Tensor ids = torch::from_blob(b.ids.data(), {(int64_t)b.ids.size()}, torch::kInt64).clone();
+    if (has_masks) {
+      Tensor y = torch::empty({B, H, W, 1}, opt.dtype(torch::kFloat32));
+      memcpy(y.data_ptr(), b.y.data(), b.y.size() * 4);
+      return py::make_tuple(x, y, ids, b.count);
+    }
+    return py::make_tuple(x, py::none(), ids, b.count);
+  }
+};
+
+Tensor png_decode_gray(const std::string& path) {
+  tdl_rt::GrayImage g = tdl_rt::load_png_gray(path);
+  Tensor t = torch::empty({g.h, g.w}, torch::kFloat32);
+  memcpy(t.data_ptr(), g.px.data(), g.px.size() * 4);
+  return t;
+}
+
+py::tuple augment_one(Tensor img, c10::optional<Tensor> mask, bool transpose, bool hflip, bool vflip,
+                      double angle, double tx, double ty, int64_t pad) {
+  TORCH_CHECK(img.dim() == 2 && img.scalar_type() == torch::kFloat32 && img.is_contiguous());
+  tdl_rt::GrayImage gi;
+  gi.h = img.size(0);
+  gi.w = img.size(1);
+  gi.px.assign(img.data_ptr<float>(), img.data_ptr<float>() + img.numel());
+  tdl_rt::GrayImage gm;
+  const bool hm = mask.has_value() && mask->defined();
+  if (hm) {
+    gm.h = gi.h;
+    gm.w = gi.w;
+    gm.px.assign(mask->data_ptr<float>(), mask->data_ptr<float>() + mask->numel());
+  }
+  tdl_rt::AugParams p;
+  p.transpose = transpose; p.hflip = hflip; p.vflip = vflip; p.angle = angle; p.tx = tx; p.ty = ty;
+  Tensor oi = torch::empty_like(img), om = torch::empty_like(img);
+  tdl_rt::augment_sample(gi, hm ? &gm : nullptr, p, (int)pad, oi.data_ptr<float>(),
+                         hm ? om.data_ptr<float>() : nullptr);
+  Tensor lap = torch::empty_like(img);
+  tdl_rt::laplace(oi.data_ptr<float>(), gi.h, gi.w, lap.data_ptr<float>());
+  return py::make_tuple(oi, hm ? py::object(py::cast(om)) : py::none(), lap);
+}
+
+std::vector<double> transform_matrix(bool hflip, bool vflip, double angle, double tx, double ty,
+                                     int64_t H, int64_t W) {
+  tdl_rt::AugParams p;
+  p.hflip = hflip; p.vflip = vflip; p.angle = angle; p.tx = tx; p.ty = ty;
+  double t[8];
+  tdl_rt::make_transform(p, (int)H, (int)W, t);
+  return std::vector<double>(t, t + 8);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -371,4 +448,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dwconv_wgrad", &dwconv_wgrad);
   m.def("upsample_fwd", &upsample_fwd);
   m.def("upsample_bwd", &upsample_bwd);
+  py::class_<PyLoader>(m, "BatchLoader")
+      .def(py::init<std::vector<std::string>, std::vector<std::string>, int, bool, bool, bool,
+                    int64_t, int, int, int, int, bool>(),
+           py::arg("images"), py::arg("masks"), py::arg("batch"), py::arg("augment"),
+           py::arg("shuffle"), py::arg("repeat"), py::arg("seed"), py::arg("threads"),
+           py::arg("prefetch"), py::arg("channels"), py::arg("transformation"),
+           py::arg("pin_memory") = false)
+      .def("next", &PyLoader::next)
+      .def_property_readonly("num_batches", [](PyLoader& l) { return l.impl->num_batches(); })
+      .def_property_readonly("height", [](PyLoader& l) { return l.impl->height(); })
+      .def_property_readonly("width", [](PyLoader& l) { return l.impl->width(); });
+  m.def("png_decode_gray", &png_decode_gray);
+  m.def("augment_one", &augment_one);
+  m.def("transform_matrix", &transform_matrix);
 }

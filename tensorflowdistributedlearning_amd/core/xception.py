@@ -1,0 +1,73 @@
+"""core.xception — reference API (core/xception.py:6-509), built as the *intended* DeepLab
+Xception-41 (D8–D10 fixed: importable, 8-unit middle flow, BN after every conv); see
+:mod:`models.xception`.
+"""
+from __future__ import annotations
+
+import collections
+
+import torch.nn.functional as F
+
+from ..models.xception import Xception41, XceptionModule, SeparableConvBN, _fixed_pad
+from ..models.deeplab import SplitSeparableConv  # noqa: F401  (split_separable_conv2d lives in core.layers)
+from .layers import split_separable_conv2d  # noqa: F401
+from ._scope import get_or_create, to_nhwc, from_nhwc, device_of
+
+Block = collections.namedtuple("Block", ["scope", "unit_fn", "args"])
+
+
+def fixed_padding(inputs, kernel_size, rate=1):
+    """Zero-pad for a k×k (rate) conv with 'VALID' padding (xception.py:18-35), NHWC."""
+    t, b, l, r = _fixed_pad(kernel_size, rate)
+    return F.pad(inputs, (0, 0, l, r, t, b))
+
+
+def separable_conv2d_same(in_channels, num_outputs, kernel_size=3, depth_multiplier=1, stride=1,
+                          rate=1, activation_fn_in_separable_conv=False, bn_decay=0.9997,
+                          bn_eps=1e-3):
+    """Module: depthwise (explicit fixed padding at stride>1) + BN → pointwise + BN."""
+    if kernel_size != 3 or depth_multiplier != 1:
+        raise ValueError("3x3, depth_multiplier 1 only")
+    return SeparableConvBN(in_channels, num_outputs, stride, rate, activation_fn_in_separable_conv,
+                           dict(bn_decay=bn_decay, bn_eps=bn_eps))
+
+
+def xception_module(in_channels, depth_list, skip_connection_type, stride, unit_rate_list=None,
+                    rate=1, activation_fn_in_separable_conv=False, bn_decay=0.9997, bn_eps=1e-3):
+    if len(depth_list) != 3:
+        raise ValueError("Expect three elements in depth_list.")
+    unit_rate_list = unit_rate_list or [1, 1, 1]
+    if len(unit_rate_list) != 3:
+        raise ValueError("Expect three elements in unit_rate_list.")
+    if skip_connection_type not in ("conv", "sum", "none"):
+        raise ValueError("Unsupported skip connection type.")
+    return XceptionModule(in_channels, depth_list, skip_connection_type, stride, rate,
+                          unit_rate_list, activation_fn_in_separable_conv,
+                          dict(bn_decay=bn_decay, bn_eps=bn_eps))
+
+
+def xception_block(scope, depth_list, skip_connection_type, activation_fn_in_separable_conv,
+                   regularize_depthwise, num_units, stride, unit_rate_list=None):
+    if unit_rate_list is None:
+        unit_rate_list = [1, 1, 1]
+    return Block(scope, xception_module, [{
+        "depth_list": depth_list, "skip_connection_type": skip_connection_type,
+        "activation_fn_in_separable_conv": activation_fn_in_separable_conv,
+        "regularize_depthwise": regularize_depthwise, "stride": stride,
+        "unit_rate_list": unit_rate_list}] * num_units)
+
+
+def xception_41(inputs, is_training=True, keep_prob=0.5, output_stride=None,
+                regularize_depthwise=False, multi_grid=None, reuse=None, scope="xception_41",
+                num_classes=None, data_format="NHWC"):
+    """Builds (or reuses, per ``scope``) Xception-41 and applies it.  Returns (net, end_points)
+    with ``net`` the exit-flow features (or logits when ``num_classes``)."""
+    x = to_nhwc(inputs, data_format)
+    m = get_or_create(("xception_41", scope, output_stride, tuple(multi_grid or []), num_classes),
+                      lambda: Xception41(num_classes=num_classes or 0,
+                                         in_channels=min(x.shape[-1], 8),
+                                         output_stride=output_stride, multi_grid=multi_grid),
+                      device_of(x))
+    m.train(bool(is_training))
+    y = m(x)
+    return from_nhwc(y, data_format) if y.dim() == 4 else y, {f"{scope}/output": y}

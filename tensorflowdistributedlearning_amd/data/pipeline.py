@@ -1,0 +1,93 @@
+"""Input pipelines on top of the native C++ loader (csrc/runtime/loader.cpp).
+
+``SegmentationPipeline`` is the reference's ``Model._make_input_fn`` (model.py:285-324):
+glob ``{model_dir}/{mode}/images/fold{k}/*.png`` and the parallel masks, ``shuffle_and_repeat``
+(or ``repeat``), ``map(read_and_preprocess(augment))``, ``batch``, ``prefetch(2·n_gpus)`` — but the
+decode/augment/batch work runs in native worker threads writing pinned host buffers, and the
+H2D copy is asynchronous on the current stream.  In data-parallel runs each rank reads a disjoint
+shard (images[rank::world]) with its own seed — the per-tower batches of MirroredStrategy.
+``TestPipeline`` is ``Model._make_test_input`` (model.py:257-283) with a TTA transformation.
+"""
+from __future__ import annotations
+
+import glob
+import os
+
+import torch
+
+from .. import _native
+
+TRANSFORMS = {"none": 0, "vertical": 1, "horizontal": 2, "transpose": 3}
+
+
+def fold_files(model_dir, mode, fold):
+    images = sorted(glob.glob(os.path.join(model_dir, mode, "images", f"fold{fold}", "*.png")))
+    masks = sorted(glob.glob(os.path.join(model_dir, mode, "masks", f"fold{fold}", "*.png")))
+    return images, masks
+
+
+class SegmentationPipeline:
+    def __init__(self, images, masks, batch_size, augment, shuffle, repeat=True, seed=0,
+                 device="cpu", rank=0, world=1, threads=4, prefetch=4, channels=8):
+        if world > 1:
+            images = images[rank::world]
+            masks = masks[rank::world] if masks else masks
+        if masks and len(masks) != len(images):
+            raise ValueError("image/mask count mismatch")
+        self.n = len(images)
+        self.device = torch.device(device)
+        self.batch_size = batch_size
+        self.ids = [os.path.splitext(os.path.basename(p))[0] for p in images]
+        self._loader = _native.load().BatchLoader(
+            list(images), list(masks or []), int(batch_size), bool(augment), bool(shuffle),
+            bool(repeat), int(seed) * 1000 + rank, int(threads), int(prefetch), int(channels), 0,
+            self.device.type == "cuda")
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        out = self._loader.next()
+        if out is None:
+            raise StopIteration
+        x, y, ids, count = out
+        if self.device.type == "cuda":
+            x = x.to(self.device, non_blocking=True)
+            y = y.to(self.device, non_blocking=True) if y is not None else None
+        if count < x.shape[0]:
+            x = x[:count]
+            y = y[:count] if y is not None else None
+            ids = ids[:count]
+        return x, y
+
+    @property
+    def steps_per_epoch(self):
+        return max(1, self.n // self.batch_size)
+
+
+class TestPipeline:
+    """Images only, no shuffle/repeat, optional TTA transformation; yields (x, ids)."""
+
+    __test__ = False  # not a pytest class
+
+    def __init__(self, images, batch_size, transformation="none", device="cpu", threads=4,
+                 prefetch=4, channels=8):
+        self.device = torch.device(device)
+        self.ids = [os.path.splitext(os.path.basename(p))[0] for p in images]
+        self._loader = _native.load().BatchLoader(
+            list(images), [], int(batch_size), False, False, False, 0, int(threads), int(prefetch),
+            int(channels), TRANSFORMS[transformation], self.device.type == "cuda")
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        out = self._loader.next()
+        if out is None:
+            raise StopIteration
+        x, _, ids, count = out
+        x = x[:count]
+        ids = ids[:count]
+        if self.device.type == "cuda":
+            x = x.to(self.device, non_blocking=True)
+        return x, [self.ids[i] for i in ids.tolist()]

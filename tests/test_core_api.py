@@ -1,0 +1,139 @@
+"""Reference-compatible ``core`` facade (core/resnet.py, layers.py, losses.py, metric.py,
+xception.py) — signatures, shapes and numerics against plain PyTorch references."""
+import numpy as np
+import pytest
+import torch
+
+from tensorflowdistributedlearning_amd.core import resnet, layers, losses, metric, xception, _scope
+from tensorflowdistributedlearning_amd.ops.loss import ref_lovasz_hinge
+
+
+@pytest.fixture(autouse=True)
+def _fresh_scope():
+    _scope.clear()
+    metric.reset()
+    yield
+    _scope.clear()
+
+
+def test_resnet_model_shapes_and_reuse():
+    x = torch.randn(2, 2, 32, 32)
+    kw = dict(model_name="m", weight_decay=1e-3, batch_norm_decay=0.99, batch_norm_epsilon=1e-3,
+              batch_norm_scale=True, is_training=True, output_stride=8, base_depth=8,
+              input_shape=(32, 32), n_blocks=(1, 1, 1), block_type="bottleneck")
+    y = resnet.resnet_model(x, data_format="NCHW", **kw)
+    assert y.shape == (2, 1, 32, 32)
+    y2 = resnet.resnet_model(x.permute(0, 2, 3, 1), data_format="NHWC",
+                             **dict(kw, is_training=False))
+    assert y2.shape == (2, 32, 32, 1)
+    assert len(_scope._CACHE) == 1  # variables reused under the same model_name scope
+    with pytest.raises(ValueError):
+        resnet.resnet_model(x, data_format="NCHW", **dict(kw, n_blocks=(1, 1)))
+
+
+def test_resnet_v2_specs_and_helpers():
+    blocks = resnet.resnet_v2(n_blocks=(3, 4, 6))
+    assert [b.scope for b in blocks] == ["block1", "block2", "block3", "block4"]
+    assert len(blocks[0].args) == 3 and blocks[0].args[-1]["stride"] == 2
+    assert blocks[1].args[0]["depth"] == 258 * 4
+    assert [a["unit_rate"] for a in blocks[3].args] == [2, 2, 2]
+    with pytest.raises(ValueError):
+        resnet.resnet_v2(multi_grid=[1, 2])
+    assert resnet.channel_dimension((2, 3, 5, 7), "NCHW") == 3
+    assert resnet.channel_dimension((2, 3, 5, 7), "NHWC") == 7
+    with pytest.raises(ValueError):
+        resnet.channel_dimension((2, None), "NHWC")
+    sc = resnet.resnet_arg_scope(weight_decay=1e-4)
+    assert sc["weight_decay"] == 1e-4 and sc["max_pool_padding"] == "SAME"
+    u = resnet.bottleneck(64, 256, 64, 2)
+    assert u(torch.randn(1, 8, 8, 64)).shape == (1, 4, 4, 256)
+    b = resnet.basic_block(64, 64, 64, 1, rate=2)
+    assert b(torch.randn(1, 8, 8, 64)).shape == (1, 8, 8, 64)
+    root = resnet.root_block_fn_for_beta_variant(2)
+    assert root(torch.randn(1, 16, 16, 8)).shape == (1, 8, 8, 128)
+
+
+def test_fixed_padding_matches_numpy():
+    x = torch.randn(1, 3, 5, 6)
+    for k in (1, 2, 3, 4, 7):
+        b = (k - 1) // 2
+        e = k - 1 - b
+        got = layers._fixed_padding(x, k, "NCHW", "CONSTANT")
+        ref = np.pad(x.numpy(), ((0, 0), (0, 0), (b, e), (b, e)))
+        np.testing.assert_array_equal(got.numpy(), ref)
+        got = layers._fixed_padding(x, k, "NCHW", "SYMMETRIC")
+        ref = np.pad(x.numpy(), ((0, 0), (0, 0), (b, e), (b, e)), mode="symmetric")
+        np.testing.assert_array_equal(got.numpy(), ref)
+    with pytest.raises(ValueError):
+        layers._fixed_padding(x, 3, "NCHW", "WRAP")
+
+
+def test_upsample_and_separable():
+    from tensorflowdistributedlearning_amd.ops.upsample import interp_matrix
+    x = torch.randn(1, 1, 13, 13)
+    y = layers._upsample(x, (101, 101), "NCHW")
+    assert y.shape == (1, 1, 101, 101)
+    # separable: out = Mh · x · Mwᵀ
+    Mh = interp_matrix(13, 101)
+    Mh = Mh.double()
+    ref = Mh @ x[0, 0].double() @ Mh.T
+    torch.testing.assert_close(y[0, 0].double(), ref, rtol=1e-5, atol=1e-5)
+    z = layers.split_separable_conv2d(torch.randn(1, 8, 8, 16), 32, rate=2, scope="s")
+    assert z.shape == (1, 8, 8, 32) and bool((z >= 0).all())
+
+
+def test_lovasz_facade_matches_reference():
+    torch.manual_seed(0)
+    lg = torch.randn(3, 16, 16, 1, requires_grad=True)
+    lb = (torch.rand(3, 16, 16, 1) > 0.5).float()
+    loss = losses.lovasz_loss(lb, lg)
+    ref, g = ref_lovasz_hinge(lg.detach().reshape(3, -1), lb.reshape(3, -1))
+    torch.testing.assert_close(loss, ref)
+    loss.backward()
+    torch.testing.assert_close(lg.grad.reshape(3, -1), g)
+    # ignore-label path and batch (per_image=False) path
+    lb2 = lb.clone().squeeze(-1)
+    lb2[:, :2] = 255
+    l_ign = losses.lovasz_hinge(lg.detach().squeeze(-1), lb2, per_image=True, ignore=255)
+    manual = torch.stack([ref_lovasz_hinge(lg.detach()[i, 2:].reshape(1, -1),
+                                           lb2[i, 2:].reshape(1, -1))[0] for i in range(3)]).mean()
+    torch.testing.assert_close(l_ign, manual)
+    s, l = losses.flatten_binary_scores(torch.arange(4.0), torch.tensor([0, 1, 255, 1]), 255)
+    assert s.tolist() == [0.0, 1.0, 3.0] and l.tolist() == [0, 1, 1]
+    g = losses.lovasz_grad(torch.tensor([1.0, 0.0, 1.0, 0.0]))
+    torch.testing.assert_close(g.sum(), torch.tensor(1.0))
+
+
+def test_streaming_metrics():
+    lab = torch.zeros(2, 8, 8, 1)
+    lab[0, :4] = 1
+    pred = lab.clone()
+    v, upd = metric.mIOU(lab, pred, name="iou")
+    assert float(v) == pytest.approx(np.mean([1.0 * (1.0 > t) for t in metric.IOU_THRESHOLDS]))
+    pred2 = torch.zeros_like(lab)
+    pred2[0, :2] = 1  # IoU 0.5 on image 0; image 1 empty/empty → 1
+    v2, _ = metric.mIOU(lab, pred2, name="iou")
+    s0 = np.mean([0.5 * (0.5 > t) for t in metric.IOU_THRESHOLDS])
+    assert float(v2) == pytest.approx((2 + s0 + 1) / 4)
+    assert float(upd()) == pytest.approx(float(v2))
+    a, _ = metric.mean_accuracy(lab, pred2, name="acc")
+    assert float(a) == pytest.approx(np.mean([1 - 16 / 64, 1.0]))
+    k, _ = metric.mIOU(lab, pred2, name="kag", kaggle=True)
+    assert float(k) == pytest.approx((0.0 + 1) / 2)  # IoU 0.5 passes no threshold (strict >)
+
+
+def test_xception_facade():
+    net, ep = xception.xception_41(torch.randn(1, 3, 64, 64), num_classes=10, output_stride=16)
+    assert net.shape == (1, 10)
+    p = xception.fixed_padding(torch.randn(1, 5, 5, 3), 3, rate=2)
+    assert p.shape == (1, 9, 9, 3)
+    m = xception.xception_module(64, [128, 128, 128], "conv", 2)
+    assert m(torch.randn(1, 16, 16, 64)).shape == (1, 8, 8, 128)
+    with pytest.raises(ValueError):
+        xception.xception_module(64, [128, 128], "conv", 2)
+    with pytest.raises(ValueError):
+        xception.xception_module(64, [128, 128, 128], "concat", 2)
+    b = xception.xception_block("entry_flow/block1", [128] * 3, "conv", False, False, 2, 2)
+    assert len(b.args) == 2
+    s = xception.separable_conv2d_same(32, 64, stride=2)
+    assert s(torch.randn(1, 8, 8, 32)).shape == (1, 4, 4, 64)
