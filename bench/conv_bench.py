@@ -15,6 +15,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
+from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
 
 
 def resnet50_shapes():
@@ -60,11 +61,14 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--modes", default="1", help="comma list of conv kernel modes to time "
+                    "(0 register-staged, 1 default selection, 2 LDS-DMA whenever aligned)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N = a.batch
     rows = []
-    tot = {"ours": 0.0, "miopen": 0.0}
+    tot = {"miopen": 0.0}
+    modes = [int(m) for m in a.modes.split(",")]
     for name, mult, H, Cin, Cout, k, s, p in resnet50_shapes():
         g = C.ConvGeom((s, s), (p, p, p, p), (1, 1))
         x = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
@@ -73,13 +77,19 @@ def main():
         dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
         flop = 2.0 * N * Ho * Wo * Cout * Cin * k * k
         st = torch.zeros(2, Cout, device=dev)
-        t_f = timeit(lambda: C.conv_fwd(x, w, g, stats=st))
-        t_d = timeit(lambda: C.conv_dgrad(dy, w, x.shape, g))
-        t_w = timeit(lambda: C.conv_wgrad(dy, x, tuple(w.shape), g))
-        r = dict(name=name, mult=mult, H=H, Cin=Cin, Cout=Cout, k=k, s=s,
-                 fwd_us=t_f, dgrad_us=t_d, wgrad_us=t_w, gflop=flop / 1e9,
-                 fwd_tf=flop / t_f / 1e6, dgrad_tf=flop / t_d / 1e6, wgrad_tf=flop / t_w / 1e6)
-        tot["ours"] += mult * (t_f + t_d + t_w)
+        r = dict(name=name, mult=mult, H=H, Cin=Cin, Cout=Cout, k=k, s=s, gflop=flop / 1e9)
+        msg = f"{name:10s} x{mult} {H:3d}x{H:<3d} {Cin:4d}->{Cout:4d} k{k} s{s} |"
+        for mode in modes:
+            ext().conv_set_glds_mode(mode)
+            t_f = timeit(lambda: C.conv_fwd(x, w, g, stats=st))
+            t_d = timeit(lambda: C.conv_dgrad(dy, w, x.shape, g)) if name != "stem7x7" else 0.0
+            t_w = timeit(lambda: C.conv_wgrad(dy, x, tuple(w.shape), g))
+            r[f"m{mode}"] = dict(fwd_us=t_f, dgrad_us=t_d, wgrad_us=t_w)
+            tot.setdefault(f"m{mode}", 0.0)
+            tot[f"m{mode}"] += mult * (t_f + t_d + t_w)
+            msg += (f" m{mode}: fwd {t_f:6.1f} ({flop / t_f / 1e6:4.0f}TF) dgrad {t_d:6.1f} "
+                    f"wgrad {t_w:6.1f} ({flop / t_w / 1e6:4.0f}TF) |")
+        ext().conv_set_glds_mode(-1)
         if not a.no_miopen:
             xm = x.permute(0, 3, 1, 2)  # channels_last view
             wm = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
@@ -91,14 +101,10 @@ def main():
             m_b = timeit(lambda: torch.autograd.grad(ym, [xm, wm], dym, retain_graph=True))
             r.update(miopen_fwd_us=m_f, miopen_bwd_us=m_b)
             tot["miopen"] += mult * (m_f + m_b)
+            msg += f" miopen fwd {m_f:6.1f} bwd {m_b:6.1f}"
         rows.append(r)
-        msg = (f"{name:10s} x{mult} {H:3d}x{H:<3d} {Cin:4d}->{Cout:4d} k{k} s{s} | "
-               f"fwd {t_f:7.1f}us {r['fwd_tf']:6.0f}TF  dgrad {t_d:7.1f}us {r['dgrad_tf']:6.0f}TF  "
-               f"wgrad {t_w:7.1f}us {r['wgrad_tf']:6.0f}TF")
-        if not a.no_miopen:
-            msg += f" | miopen fwd {r['miopen_fwd_us']:7.1f} bwd {r['miopen_bwd_us']:7.1f}"
         print(msg, flush=True)
-    print(json.dumps({k: round(v / 1e3, 2) for k, v in tot.items()}) + "  (ms per step, all convs)")
+    print(json.dumps({k: round(v / 1e3, 2) for k, v in tot.items()}) + "  (ms per step, all convs; stem dgrad excluded for ours)")
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"batch": N, "rows": rows, "total_ms": tot}, f, indent=1)

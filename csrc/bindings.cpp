@@ -100,14 +100,14 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad
   a.dy = BF(dy); a.x = BF(x);
   a.dy_bytes = nbytes32(dy); a.x_bytes = nbytes32(x);
   a.M = a.K; a.Ng = a.R * a.S * a.C; a.Kg = a.N * a.Ho * a.Wo;
-  int bm, bn, splits, kps;
-  conv_wgrad_plan(a.M, a.Ng, a.Kg, &bm, &bn, &splits, &kps);
-  a.kps = kps;
-  auto ws = torch::empty({(int64_t)splits * a.M * a.Ng}, out.options());
+  WgradPlan plan;
+  conv_wgrad_plan(a, &plan);
+  a.kps = plan.kps;
+  auto ws = torch::empty({(int64_t)plan.splits * a.M * a.Ng}, out.options());
   a.out = ws.data_ptr();
   a.out_bytes = nbytes32(ws);
   auto st = stream();
-  conv_wgrad_launch(a, bm, bn, splits, out.data_ptr<float>(), accumulate, st);
+  conv_wgrad_launch(a, plan, out.data_ptr<float>(), accumulate, st);
   if (bias_grad.has_value() && bias_grad->defined()) {
     CHECK_T((*bias_grad), torch::kFloat32);
     hipMemsetAsync(bias_grad->data_ptr(), 0, a.K * sizeof(float), st);
@@ -448,6 +448,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dwconv_wgrad", &dwconv_wgrad);
   m.def("upsample_fwd", &upsample_fwd);
   m.def("upsample_bwd", &upsample_bwd);
+  m.def("conv_set_glds_mode", &conv_set_glds_mode,
+        "conv kernel selection: 0 register-staged only, 1 LDS-DMA for large problems (default), "
+        "2 LDS-DMA whenever aligned, -1 environment (TDL_CONV_GLDS)");
+  m.def("conv_glds_mode", &conv_glds_mode);
+  m.def("fastdiv", [](uint32_t d) { auto f = make_fastdiv(d); return py::make_tuple(f.m, f.s); },
+        "magic (m, s) with n / d == (n * m) >> s for 0 <= n < 2^31");
   py::class_<PyLoader>(m, "BatchLoader")
       .def(py::init<std::vector<std::string>, std::vector<std::string>, int, bool, bool, bool,
                     int64_t, int, int, int, int, bool>(),

@@ -1,0 +1,754 @@
+// LDS-DMA pipelined implicit-GEMM convolution for gfx950 (MI355X / CDNA4) — the large-problem
+// path of FWD / DGRAD / WGRAD (conv_gemm.hip keeps the register-staged kernel for small or
+// unaligned problems).
+//
+// Why a second kernel: the register-staged 128×128 kernel issues the loads of K-step s+1, runs
+// the 16 MFMAs of step s (≈256 cycles) and then waits for those loads — far shorter than an
+// HBM/L2 round trip, so every step exposes most of the memory latency (300–550 TF/s measured on
+// the ResNet-50 shapes).  Here:
+//
+//  * operands go global → LDS directly with `buffer_load_dwordx4 … lds` (LDS-DMA, 16 B per lane).
+//    The buffer form keeps the range-checked descriptors of conv_gemm.hip: a padding tap / ragged
+//    edge gets offset OOB and the DMA writes zeros — the implicit-GEMM gather needs no branches.
+//    The LDS image is lane-linear per wave instruction (1 KiB), so the bank swizzles of
+//    conv_common.h are applied on the SOURCE side (each lane fetches the logical chunk that
+//    belongs at its physical slot) and again on the ds_read side (guide rule 21).
+//  * a STAGES-deep ring (3–4 × up to 48 KiB), one raw `s_barrier` per K-step and a counted
+//    `s_waitcnt vmcnt(N)` that leaves the younger stages in flight across the barrier
+//    (`__syncthreads()` would emit vmcnt(0) and drain the ring).
+//  * 256-row tiles on 8 (or 4) waves, each wave a 64×64 sub-tile (RM = RN = 4 16×16×32 MFMA
+//    fragments): 32 FLOP per LDS byte read.
+//  * persistent workgroups: one workgroup per CU walks ⌈tiles/256⌉ tiles as one flat
+//    (tile, K-step) sequence, so the ring stays full across tile boundaries and the pipeline
+//    fill is paid once per CU, not once per tile.
+//
+// Epilogue (bias, ReLU, BN Σ/Σ² statistics of the stored bf16 values, DGRAD class scatter, WGRAD
+// fp32 split-K slabs) is the same as conv_gemm.hip's.
+#include "conv_common.h"
+
+namespace tdl {
+
+namespace {
+using namespace convk;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+typedef __attribute__((address_space(3))) char lds_char_t;
+
+// Fragment reads are inline asm: hipcc cannot order LDS reads against in-flight LDS-DMA and
+// otherwise emits `s_waitcnt vmcnt(0)` before the first ds_read of every K-step, draining the
+// ring.  Visibility of the DMA'd data is established explicitly (counted vmcnt + s_barrier), and
+// the reads are retired with an explicit lgkmcnt wait followed by sched_barrier(0) so no MFMA is
+// hoisted above it (guide rule 18).
+__device__ __forceinline__ bf16x8 lds_read_kc(uint32_t tile, int row, int chunk) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(tile + (uint32_t)kc_off(row, chunk)) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+template <int COLS>
+__device__ __forceinline__ bf16x8 lds_read_mc(uint32_t tile, int krow, int col) {
+  v2u32 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(tile + (uint32_t)mc_off<COLS>(krow, col)) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(tile + (uint32_t)mc_off<COLS>(krow + 4, col)) : "memory");
+  uint4 v = make_uint4(lo[0], lo[1], hi[0], hi[1]);
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ void lgkm_wait0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// one wave instruction: 64 lanes × 16 B from per-lane buffer offsets into LDS [base, base+1 KiB)
+__device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_base, 16, voff, 0, 0, 0);
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, bool FASTK>
+__global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
+  constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE != FWD);
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int IA = A_BYTES / (1024 * NW), IB = B_BYTES / (1024 * NW);
+  static_assert(IA * 1024 * NW == A_BYTES && IB * 1024 * NW == B_BYTES, "tile / wave mismatch");
+  constexpr int LPS = IA + IB;  // DMA instructions per wave per K-step
+  static_assert(STAGES >= 2 && STAGES <= 4, "ring depth");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_begin = blk * a.tpb;
+  const int tile_end = min(a.cls_tile0[a.ncls], tile_begin + a.tpb);
+  if (tile_begin >= tile_end) return;
+  const int HoWo = a.Ho * a.Wo;
+  const bool no_loads = a.dbg & 1;
+  const rsrc_t rx = make_rsrc(a.x, no_loads ? 0u : a.x_bytes);
+  const rsrc_t rw = make_rsrc(a.w, no_loads ? 0u : a.w_bytes);
+  const rsrc_t rdy = make_rsrc(a.dy, no_loads ? 0u : a.dy_bytes);
+  const rsrc_t rout = make_rsrc(a.out, a.out_bytes);
+  const rsrc_t ra_src = (MODE == FWD) ? rx : rdy;
+  const rsrc_t rb_src = (MODE == WGRAD) ? rx : rw;
+
+  // ---- per-lane slot geometry (tile independent) ----
+  // KC image [rows][64]: instruction j of this wave fills rows (j·NW + wid)·8 … +8
+  // MC image [64][COLS]: instruction j fills k-rows (j·NW + wid)·RPI … +RPI
+  auto kc_row = [&](int j) { return (j * NW + wid) * 8 + (lane >> 3); };
+  const bool lin_src = a.dbg & 8;  // timing-only: natural source order (wrong LDS image)
+  auto kc_lchunk = [&](int j) { return lin_src ? (lane & 7) : ((lane & 7) ^ ((kc_row(j) >> 1) & 7)); };
+  auto mc_krow = [&](int j, int cols) { return (j * NW + wid) * (512 / cols) + lane / (cols / 8); };
+  auto mc_col = [&](int j, int cols, int krow) {
+    const int q = lane % (cols / 8);
+    const int swz = cols >= 128 ? ((krow & 3) | (((krow >> 3) & 1) << 2))
+                                : (((krow >> 1) & 1) | (((krow >> 3) & 1) << 1));
+    return lin_src ? (q << 3) : ((((q >> 1) ^ swz) << 4) + ((q & 1) << 3));
+  };
+
+  // ---- per-tile load state ----
+  int a_base[IA], a_p0[IA], a_p1[IA];  // KC A: pixel base / spatial origin; MC A: column
+  int b_base[IB], b_f2[IB], b_f3[IB];  // KC B: row base; MC B: column / tap offsets
+  // load-cursor position inside the filter (FWD: tap r, s and channel c0; DGRAD: class tap
+  // th, tw and output channel c0) — FWD / DGRAD tiles always start at K-step 0
+  int pos_r = 0, pos_s = 0, pos_c0 = 0;
+
+  auto prep_tile = [&](const Tile& T) {
+    if constexpr (MODE == FWD) {
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int m = T.bm0 + kc_row(j);
+        if (m < T.Mc) {
+          const int n = fdiv(m, a.fd_HoWo), rem = m - n * HoWo;
+          const int ho = fdiv(rem, a.fd_Wo), wo = rem - ho * a.Wo;
+          a_base[j] = n * a.H * a.W * a.C;
+          a_p0[j] = ho * a.sh - a.ph;
+          a_p1[j] = wo * a.sw - a.pw;
+        } else {
+          a_base[j] = 0;
+          a_p0[j] = -(1 << 28);
+          a_p1[j] = 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const int n = T.bn0 + kc_row(j);
+        b_base[j] = n < a.Ng ? n * a.Kg : -1;
+      }
+    } else if constexpr (MODE == DGRAD) {
+      const int c = T.cls;
+      const int Hc = a.cls_Hc[c], Wc = a.cls_Wc[c], HWc = Hc * Wc;
+      const int ca = a.cls_a[c], cb = a.cls_b[c], r0 = a.cls_r0[c], s0 = a.cls_s0[c];
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int m = T.bm0 + kc_row(j);
+        if (m < T.Mc) {
+          const int n = fdiv(m, a.cls_fdHW[c]), rem = m - n * HWc;
+          const int ii = fdiv(rem, a.cls_fdW[c]), jj = rem - ii * Wc;
+          const int h = ca + a.sh * ii, w = cb + a.sw * jj;
+          a_base[j] = n * HoWo * a.K;
+          // exact and non-negative for the class's first tap (r0 ≡ h + ph mod sh)
+          a_p0[j] = fdiv(h + a.ph - r0 * a.dh, a.fd_sh);
+          a_p1[j] = fdiv(w + a.pw - s0 * a.dw, a.fd_sw);
+        } else {
+          a_base[j] = 0;
+          a_p0[j] = -(1 << 28);
+          a_p1[j] = -(1 << 28);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const int ci = T.bn0 + mc_col(j, BN, mc_krow(j, BN));
+        b_base[j] = ci < a.Ng ? ci : -1;
+      }
+    } else {  // WGRAD
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int co = T.bm0 + mc_col(j, BM, mc_krow(j, BM));
+        a_base[j] = co < a.M ? co : -1;
+      }
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const int nn = T.bn0 + mc_col(j, BN, mc_krow(j, BN));
+        if (nn < a.Ng) {
+          const int rs = fdiv(nn, a.fd_C), ci = nn - rs * a.C;
+          const int r = fdiv(rs, a.fd_S), s = rs - r * a.S;
+          b_base[j] = ci;
+          b_f2[j] = r * a.dh - a.ph;
+          b_f3[j] = s * a.dw - a.pw;
+        } else {
+          b_base[j] = -1;
+          b_f2[j] = -(1 << 28);
+          b_f3[j] = 0;
+        }
+      }
+    }
+  };
+
+  // ---- issue the DMAs of one K-step into ring slot `slot` ----
+  auto issue_step = [&](const Tile& T, int kt, int slot) {
+    char* As = smem + slot * STAGE;
+    char* Bs = As + A_BYTES;
+    const int kb = kt * BK;
+    if constexpr (MODE == FWD) {
+      // FASTK (C % 64 == 0): the K-step is one filter tap (pos_r, pos_s) and channels
+      // pos_c0 … +63, advanced incrementally by advance_load (no division in the loop)
+      const int tap_r = pos_r, tap_s = pos_s, c0 = pos_c0;
+      const int kbase = kb;
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int lc = kc_lchunk(j);
+        int r = tap_r, s = tap_s, c = c0 + lc * 8;
+        bool kv = kb < a.Kg;
+        if constexpr (!FASTK) {
+          const int k = kb + lc * 8;
+          kv = k < a.Kg;
+          const int rs = fdiv(k, a.fd_C);
+          c = k - rs * a.C;
+          r = fdiv(rs, a.fd_S);
+          s = rs - r * a.S;
+        }
+        const int hi = a_p0[j] + r * a.dh, wi = a_p1[j] + s * a.dw;
+        const bool v = kv && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const uint32_t off = (uint32_t)(a_base[j] + (hi * a.W + wi) * a.C + c) * 2u;
+        dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
+      }
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const int k = kbase + kc_lchunk(j) * 8;
+        const bool v = k < a.Kg && b_base[j] >= 0;
+        dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_base[j] + k) * 2u : OOB);
+      }
+    } else if constexpr (MODE == DGRAD) {
+      const int c = T.cls;
+      const int Tw = a.cls_Tw[c];
+      const int step_h = a.sh == 1 ? a.dh : 1, step_w = a.sw == 1 ? a.dw : 1;
+      // FASTK (K % 64 == 0): one tap (pos_r = th, pos_s = tw) per K-step, channels pos_c0 … +63
+      const int co0 = pos_c0;
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int lc = kc_lchunk(j);
+        int th = pos_r, tw = pos_s, co = co0 + lc * 8;
+        bool kv = kb < T.Kgc;
+        if constexpr (!FASTK) {
+          const int k = kb + lc * 8;
+          kv = k < T.Kgc;
+          co = k % a.K;
+          const int t = k / a.K;
+          th = t / Tw;
+          tw = t - th * Tw;
+        }
+        const int ho = a_p0[j] - th * step_h, wo = a_p1[j] - tw * step_w;
+        const bool v = kv && (unsigned)ho < (unsigned)a.Ho && (unsigned)wo < (unsigned)a.Wo;
+        const uint32_t off = (uint32_t)(a_base[j] + (ho * a.Wo + wo) * a.K + co) * 2u;
+        dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
+      }
+      const int r0 = a.cls_r0[c], s0 = a.cls_s0[c];
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const int kk = kb + mc_krow(j, BN);
+        int co2, th2, tw2;
+        if constexpr (FASTK) {
+          th2 = pos_r;
+          tw2 = pos_s;
+          co2 = co0 + mc_krow(j, BN);
+        } else {
+          co2 = kk % a.K;
+          const int t2 = kk / a.K;
+          th2 = t2 / Tw;
+          tw2 = t2 - th2 * Tw;
+        }
+        const int r = r0 + a.sh * th2, s = s0 + a.sw * tw2;
+        const bool v = kk < T.Kgc && b_base[j] >= 0;
+        const uint32_t off = (uint32_t)(((co2 * a.R + r) * a.S + s) * a.C + b_base[j]) * 2u;
+        dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? off : OOB);
+      }
+    } else {  // WGRAD
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int p = kb + mc_krow(j, BM);
+        const bool v = p < a.Kg && a_base[j] >= 0;
+        dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.K + a_base[j]) * 2u : OOB);
+      }
+#pragma unroll
+      for (int j = 0; j < IB; ++j) {
+        const int p = kb + mc_krow(j, BN);
+        const int ni = fdiv(p, a.fd_HoWo), rem = p - ni * HoWo;
+        const int ho = fdiv(rem, a.fd_Wo), wo = rem - ho * a.Wo;
+        const int hi = ho * a.sh + b_f2[j], wi = wo * a.sw + b_f3[j];
+        const bool v = p < a.Kg && b_base[j] >= 0 && (unsigned)hi < (unsigned)a.H &&
+                       (unsigned)wi < (unsigned)a.W;
+        const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_base[j]) * 2u;
+        dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? off : OOB);
+      }
+    }
+  };
+
+  f32x4 acc[RM][RN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  const uint32_t smem_lds = (uint32_t)(size_t)(lds_char_t*)smem;
+  const bool no_reads = a.dbg & 16, no_barrier = a.dbg & 32, no_dma = a.dbg & 64;
+  auto load_frags = [&](uint32_t As, uint32_t Bs, int kk, bf16x8(&af)[RM], bf16x8(&bfg)[RN]) {
+    if (no_reads) return;
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const int row = wm * TM + rm * 16;
+      if constexpr (A_MC)
+        af[rm] = lds_read_mc<BM>(As, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), row + 4 * (lane & 3));
+      else
+        af[rm] = lds_read_kc(As, row + (lane & 15), kk * 4 + (lane >> 4));
+    }
+#pragma unroll
+    for (int rn = 0; rn < RN; ++rn) {
+      const int row = wn * TN + rn * 16;
+      if constexpr (B_MC)
+        bfg[rn] = lds_read_mc<BN>(Bs, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), row + 4 * (lane & 3));
+      else
+        bfg[rn] = lds_read_kc(Bs, row + (lane & 15), kk * 4 + (lane >> 4));
+    }
+  };
+  const bool no_mfma = a.dbg & 2;
+  auto mfmas = [&](const bf16x8(&af)[RM], const bf16x8(&bfg)[RN]) {
+    if (no_mfma) {
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) asm volatile("" ::"v"(af[rm]));
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) asm volatile("" ::"v"(bfg[rn]));
+      return;
+    }
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+        acc[rm][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[rn], af[rm], acc[rm][rn], 0, 0, 0);
+  };
+  static_assert(BK == 64, "two 32-deep fragment sets per K-step");
+
+  float s_sum[RN][4], s_sq[RN][4];
+#pragma unroll
+  for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
+
+  // lane holds C[m = bm0 + wm*TM + rm*16 + (lane&15)][n = bn0 + wn*TN + rn*16 + (lane>>4)*4 + i]
+  auto epilogue = [&](const Tile& T) {
+    if constexpr (MODE == WGRAD) {
+      const uint32_t slab0 = (uint32_t)T.split * (uint32_t)(a.M * a.Ng);
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) {
+        const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn) {
+          const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+          const bool v = m < a.M && n0 < a.Ng;
+          const uint32_t off = (slab0 + (uint32_t)(m * a.Ng + n0)) * 4u;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, acc[rm][rn]), rout,
+                                                 v ? off : OOB, 0, 0);
+        }
+      }
+    } else {
+      const rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)a.Ng * 4u : 0u);
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) {
+        const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
+        const bool mv = m < T.Mc;
+        const long orow = mv ? out_row<MODE>(a, T, m) : 0;
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn) {
+          const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (BIAS) {
+            const v4u32 b = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(b[i]);
+          }
+          bf16_t h[4];
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float t = acc[rm][rn][i] + bv[i];
+            if (a.relu) t = fmaxf(t, 0.f);
+            h[i] = f2bf(t);
+            v[i] = bf2f(h[i]);
+          }
+          const bool v_ok = mv && n0 < a.Ng;
+          const uint32_t off = (uint32_t)(orow * a.ldc + n0) * 2u;
+          v2u32 pk;
+          pk[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+          pk[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, rout, v_ok ? off : OOB, 0, 0);
+          if constexpr (STATS) {
+            const float msk = v_ok ? 1.f : 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              s_sum[rn][i] += msk * v[i];
+              s_sq[rn][i] += msk * v[i] * v[i];
+            }
+          }
+        }
+      }
+    }
+  };
+
+  auto flush_stats = [&](int bn0) {
+    if constexpr (STATS && MODE != WGRAD) {
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s_sum[rn][i] += __shfl_xor(s_sum[rn][i], o, 64);
+            s_sq[rn][i] += __shfl_xor(s_sq[rn][i], o, 64);
+          }
+        }
+      float* red = (float*)(smem + STAGES * STAGE);
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int nl = wn * TN + rn * 16 + (lane >> 4) * 4 + i;
+            red[(wm * 2 + 0) * BN + nl] = s_sum[rn][i];
+            red[(wm * 2 + 1) * BN + nl] = s_sq[rn][i];
+          }
+      }
+      __syncthreads();
+      for (int t = tid; t < 2 * BN; t += NT) {
+        const int which = t / BN, nl = t - which * BN;
+        const int n = bn0 + nl;
+        if (n < a.Ng) {
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < WM; ++w) v += red[(w * 2 + which) * BN + nl];
+          atomicAdd(a.stats + which * a.Ng + n, v);
+        }
+      }
+    }
+  };
+
+  // Next tile of this workgroup without the divisions of tile_of: FWD workgroups walk one
+  // column's consecutive row tiles; DGRAD / WGRAD walk row-major (n fastest) inside a class /
+  // split, and fall back to tile_of at a class or split boundary.
+  const int ntn_c = (a.Ng + BN - 1) / BN;
+  auto next_tile = [&](Tile& T, int t) {
+    if constexpr (MODE == FWD) {
+      T.bm0 += BM;
+    } else {
+      T.bn0 += BN;
+      if (T.bn0 >= a.Ng) {
+        T.bn0 = 0;
+        T.bm0 += BM;
+        if (T.bm0 >= T.Mc) T = tile_of<MODE, BM, BN>(a, t);
+      }
+    }
+    (void)ntn_c;
+  };
+
+  // ---- flat (tile, K-step) pipeline over this workgroup's tiles ----
+  int lt = tile_begin;
+  Tile LT = tile_of<MODE, BM, BN>(a, lt);
+  int lkt = LT.kt0;
+  bool lmore = LT.bm0 < LT.Mc;
+  if (!lmore) return;
+  prep_tile(LT);
+  const int pos_C = MODE == FWD ? a.C : a.K;
+  auto advance_load = [&]() {
+    if (lkt + 1 < LT.kt1) {
+      ++lkt;
+      if constexpr (FASTK && MODE != WGRAD) {
+        pos_c0 += BK;
+        if (pos_c0 >= pos_C) {
+          pos_c0 = 0;
+          const int Sl = MODE == FWD ? a.S : a.cls_Tw[LT.cls];
+          if (++pos_s == Sl) {
+            pos_s = 0;
+            ++pos_r;
+          }
+        }
+      }
+    } else if (lt + 1 < tile_end) {
+      ++lt;
+      next_tile(LT, lt);
+      lkt = LT.kt0;
+      pos_r = pos_s = pos_c0 = 0;
+      if (LT.bm0 < LT.Mc)
+        prep_tile(LT);
+      else
+        lmore = false;  // FWD row groups: trailing empty tiles
+    } else {
+      lmore = false;
+    }
+  };
+
+  int ct = tile_begin;
+  Tile CT = LT;
+  int ckt = CT.kt0;
+  int inflight = 0;  // steps issued and not yet fully computed
+  constexpr int E = RM * RN;  // epilogue stores per lane
+  bool epi = false;
+  int slot_load = 0, slot_comp = 0;
+  auto issue_next = [&]() {
+    if (!no_dma) issue_step(LT, lkt, slot_load);
+    slot_load = slot_load + 1 == STAGES ? 0 : slot_load + 1;
+    ++inflight;
+    advance_load();
+  };
+  // Retire the DMAs of the step about to be read while `ahead` younger steps stay in flight,
+  // then make them visible to every wave.  vmcnt retires in issue order; right after an epilogue
+  // its E stores are the youngest VMEM ops.
+  auto ring_wait_barrier = [&](int ahead) {
+    if (epi) {
+      if (STAGES >= 4 && ahead >= 2)
+        wait_vmcnt<2 * LPS + E>();
+      else if (ahead >= 1)
+        wait_vmcnt<LPS + E>();
+      else
+        wait_vmcnt<E>();
+    } else {
+      if (STAGES >= 4 && ahead >= 2)
+        wait_vmcnt<2 * LPS>();
+      else if (ahead >= 1)
+        wait_vmcnt<LPS>();
+      else
+        wait_vmcnt<0>();
+    }
+    epi = false;
+    if (!no_barrier) raw_barrier();
+  };
+
+  // Software pipeline across K-steps (one barrier per step):
+  //   reads(t, k0..31) ready → issue reads(t, k32..63) → MFMA(t, first half) → lgkm(0) →
+  //   [wait DMA(t+1), barrier, DMA(t+S) into the slot just drained, reads(t+1, k0..31)] →
+  //   MFMA(t, second half) → epilogue if the tile ends → lgkm(0)
+  // so the barrier, the DMA address math and the next step's first fragment reads all sit under
+  // 16 MFMAs instead of in front of an idle MFMA pipe.
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (lmore) issue_next();
+  zero_acc();
+  bf16x8 f0a[RM], f0b[RN], f1a[RM], f1b[RN];
+  ring_wait_barrier(inflight - 1);
+  if (lmore) issue_next();
+  load_frags(smem_lds + (uint32_t)(slot_comp * STAGE), smem_lds + (uint32_t)(slot_comp * STAGE + A_BYTES), 0, f0a, f0b);
+  lgkm_wait0();
+  while (inflight > 0) {
+    const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;
+    load_frags(As, Bs, 1, f1a, f1b);
+    mfmas(f0a, f0b);
+    lgkm_wait0();
+    const bool has_next = inflight > 1;
+    slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;
+    if (has_next) {
+      ring_wait_barrier(inflight - 2);
+      if (lmore) issue_next();
+      const uint32_t An = smem_lds + (uint32_t)(slot_comp * STAGE), Bn = An + A_BYTES;
+      load_frags(An, Bn, 0, f0a, f0b);
+    }
+    mfmas(f1a, f1b);
+    --inflight;
+    if (ckt + 1 >= CT.kt1) {
+      epilogue(CT);
+      epi = true;
+      zero_acc();
+      if (inflight > 0) {
+        ++ct;
+        next_tile(CT, ct);
+        ckt = CT.kt0;
+      }
+    } else {
+      ++ckt;
+    }
+    if (has_next) lgkm_wait0();
+  }
+  flush_stats(CT.bn0);
+}
+
+// ------------------------------------------------------------------------------------------
+// configurations
+// ------------------------------------------------------------------------------------------
+struct GCfg {
+  int bm, bn, wm, wn, stages;
+};
+constexpr GCfg G256x128{256, 128, 4, 2, 3};
+constexpr GCfg G256x64{256, 64, 4, 1, 3};
+constexpr GCfg G128x128{128, 128, 2, 2, 4};
+
+constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
+  return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, bool FK>
+void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK>;
+  constexpr int lds = lds_bytes(BM, BN, WM, ST);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), lds, st, a);
+}
+
+template <int MODE, bool STATS, bool BIAS, bool FK>
+void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
+  if (cfg == 0)
+    launch_g<MODE, 256, 128, 4, 2, 3, STATS, BIAS, FK>(a, blocks, st);
+  else if (cfg == 1)
+    launch_g<MODE, 256, 64, 4, 1, 3, STATS, BIAS, FK>(a, blocks, st);
+  else
+    launch_g<MODE, 128, 128, 2, 2, 4, STATS, BIAS, FK>(a, blocks, st);
+}
+
+const GCfg& cfg_of(int c) { return c == 0 ? G256x128 : (c == 1 ? G256x64 : G128x128); }
+
+void set_fastdivs(ConvArgs& a) {
+  a.fd_sh = make_fastdiv((uint32_t)std::max(1, a.sh));
+  a.fd_sw = make_fastdiv((uint32_t)std::max(1, a.sw));
+  for (int c = 0; c < MAX_DG_CLASSES; ++c) {
+    a.cls_fdHW[c] = make_fastdiv((uint32_t)std::max(1, a.cls_Hc[c] * a.cls_Wc[c]));
+    a.cls_fdW[c] = make_fastdiv((uint32_t)std::max(1, a.cls_Wc[c]));
+  }
+  a.fd_HoWo = make_fastdiv((uint32_t)std::max(1, a.Ho * a.Wo));
+  a.fd_Wo = make_fastdiv((uint32_t)std::max(1, a.Wo));
+  a.fd_C = make_fastdiv((uint32_t)std::max(1, a.C));
+  a.fd_S = make_fastdiv((uint32_t)std::max(1, a.S));
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// persistent grid: ⌈tiles / CUs⌉ consecutive tiles per workgroup
+int persistent_tpb(long tiles) {
+  const int cus = env_int("TDL_GLDS_SLOTS", 256);
+  return (int)std::max<long>(1, (tiles + cus - 1) / cus);
+}
+
+}  // namespace
+
+// Mode selection: 0 = register-staged kernel only, 1 = glds for eligible problems (default),
+// 2 = glds whenever aligned (testing).
+static int g_glds_override = -1;
+int conv_glds_mode() {
+  static int m = env_int("TDL_CONV_GLDS", 1);
+  return g_glds_override >= 0 ? g_glds_override : m;
+}
+void conv_set_glds_mode(int mode) { g_glds_override = mode; }
+
+bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
+  const int mode = conv_glds_mode();
+  if (mode == 0 || a0.C % 8 || a0.K % 8) return false;
+  // default selection (conv_bench, ResNet-50 b256): faster for ≥ 128 output channels; the
+  // 4-wave 256×64 configuration loses to the register-staged kernel
+  if (mode == 1 && ((long)a0.M < 4096 || a0.Ng < 128)) return false;
+  ConvArgs a = a0;
+  a.dbg = env_int("TDL_CONV_DBG", 0);
+  set_fastdivs(a);
+  int cfg = a.Ng <= 64 ? 1 : 0;
+  cfg = env_int("TDL_GLDS_CFG_FWD", cfg);
+  const GCfg& g = cfg_of(cfg);
+  const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
+  a.ncls = 1;
+  a.splits = 1;
+  // FWD tile order (tile_of): a workgroup owns one column tile and tpb consecutive row tiles
+  a.tpb = std::max(1, persistent_tpb(ntm * ntn) );
+  a.tpb = std::min<long>(a.tpb, ntm);
+  const long groups = (ntm + a.tpb - 1) / a.tpb;
+  const int blocks = (int)(groups * ntn);
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+  const bool fk = a.C % 64 == 0;
+  const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
+#define TDL_G(ST, BI, FK) launch_gcfg<FWD, ST, BI, FK>(a, cfg, blocks, st)
+  if (fk) {
+    if (bias) { if (stats) TDL_G(true, true, true); else TDL_G(false, true, true); }
+    else { if (stats) TDL_G(true, false, true); else TDL_G(false, false, true); }
+  } else {
+    if (bias) { if (stats) TDL_G(true, true, false); else TDL_G(false, true, false); }
+    else { if (stats) TDL_G(true, false, false); else TDL_G(false, false, false); }
+  }
+#undef TDL_G
+  return true;
+}
+
+// DGRAD with prepared parity classes (conv_dgrad_launch builds them); returns false when the
+// register-staged kernel should run instead.
+bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
+  const int mode = conv_glds_mode();
+  if (mode == 0 || a0.C % 8 || a0.K % 8 || a0.dg_masked) return false;
+  if (mode == 1 && (Mmax_total < 4096 || a0.Ng < 128)) return false;
+  ConvArgs a = a0;
+  a.dbg = env_int("TDL_CONV_DBG", 0);
+  set_fastdivs(a);
+  int cfg = a.Ng <= 64 ? 1 : 0;
+  cfg = env_int("TDL_GLDS_CFG_DGRAD", cfg);
+  const GCfg& g = cfg_of(cfg);
+  a.cls_tile0[0] = 0;
+  for (int c = 0; c < a.ncls; ++c) {
+    const long Mc = (long)a.N * a.cls_Hc[c] * a.cls_Wc[c];
+    a.cls_tile0[c + 1] = a.cls_tile0[c] + (int)(cdiv(Mc, g.bm) * (long)cdiv(a.Ng, g.bn));
+  }
+  const long tiles = a.cls_tile0[a.ncls];
+  if (tiles == 0) return true;
+  a.tpb = persistent_tpb(tiles);
+  a.splits = 1;
+  const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
+  if (a.K % 64 == 0)
+    launch_gcfg<DGRAD, false, false, true>(a, cfg, blocks, st);
+  else
+    launch_gcfg<DGRAD, false, false, false>(a, cfg, blocks, st);
+  return true;
+}
+
+// WGRAD split-K plan for the LDS-DMA kernel: ≈ one tile-split per CU slot, ≥ 16 K-steps each
+bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
+  const int mode = conv_glds_mode();
+  if (mode == 0 || a.C % 8 || a.K % 8) return false;
+  // default: 1×1 filters with ≥ 256 output channels (3×3 gathers of x favour the other kernel)
+  if (mode == 1 && ((long)a.Kg < 4096 || a.M < 256 || a.R * a.S != 1)) return false;
+  int cfg = a.M <= 128 ? 2 : 0;
+  cfg = env_int("TDL_GLDS_CFG_WGRAD", cfg);
+  const GCfg& g = cfg_of(cfg);
+  const long tiles = (long)cdiv(a.M, g.bm) * cdiv(a.Ng, g.bn);
+  const int nkt = cdiv(a.Kg, BK);
+  const int target = env_int("TDL_GLDS_WGRAD_TARGET", 256);
+  int s = (int)std::max<long>(1, std::min<long>(nkt, (target + tiles - 1) / tiles));
+  int per = std::max(cdiv(nkt, s), env_int("TDL_GLDS_WGRAD_MINSTEPS", 16));
+  s = cdiv(nkt, per);
+  p->impl = 1;
+  p->cfg = cfg;
+  p->bm = g.bm;
+  p->bn = g.bn;
+  p->splits = s;
+  p->kps = per;
+  return true;
+}
+
+void conv_wgrad_glds_kernel_launch(const ConvArgs& a0, const WgradPlan& p, hipStream_t st) {
+  ConvArgs a = a0;
+  a.dbg = env_int("TDL_CONV_DBG", 0);
+  set_fastdivs(a);
+  const long tiles = (long)cdiv(a.M, p.bm) * cdiv(a.Ng, p.bn) * p.splits;
+  a.kps = p.kps;
+  a.splits = p.splits;
+  a.ncls = 1;
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)tiles;
+  a.tpb = persistent_tpb(tiles);
+  const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
+  launch_gcfg<WGRAD, false, false, true>(a, p.cfg, blocks, st);
+}
+
+}  // namespace tdl

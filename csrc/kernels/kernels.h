@@ -9,6 +9,24 @@ namespace tdl {
 
 typedef uint16_t bf16_t;
 
+struct FastDiv {
+  uint32_t m, s;
+};
+// Division by a runtime constant d via a host-computed magic number: n / d = (n·m) >> s, exact for
+// 0 ≤ n < 2^31 (m = ⌈2^(31+l)/d⌉, l = ⌈log2 d⌉; checked exhaustively in tests/test_ops_cpu.py).
+// Replaces the ~40-instruction v_rcp/readfirstlane sequences hipcc emits for `/` in hot loops.
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint32_t sh = 31 + l;
+  const uint64_t m = ((1ull << sh) + d - 1) / d;
+  return FastDiv{(uint32_t)m, sh};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
+}
+
+
 struct ConvArgs {
   const bf16_t* x;   // FWD / WGRAD: input activations [N,H,W,C]
   const bf16_t* w;   // FWD / DGRAD: weights [K,R,S,C]
@@ -25,6 +43,9 @@ struct ConvArgs {
   int kps;           // WGRAD: K-steps per split
   int splits;        // WGRAD: number of K splits
   int tpb;           // tiles per workgroup (FWD / DGRAD multi-tile pipelining)
+  FastDiv fd_HoWo, fd_Wo, fd_C, fd_S, fd_sh, fd_sw;  // magic divisors (LDS-DMA launchers)
+  FastDiv cls_fdHW[16], cls_fdW[16];                 // DGRAD per-class pixel decomposition
+  int dbg;           // ablation flags (TDL_CONV_DBG, diagnostics only): 1 drop operand loads, 2 skip MFMA
   // DGRAD parity classes (stride s: s_h·s_w classes of input pixels, each with its exact taps)
   int ncls;
   int dg_masked;     // 1: stride>1 with dilation>1 — single class, divisibility-masked taps
@@ -36,9 +57,21 @@ constexpr int MAX_DG_CLASSES = 16;
 
 void conv_fwd_launch(const ConvArgs& a, hipStream_t st);
 void conv_dgrad_launch(const ConvArgs& a, hipStream_t st);
-void conv_wgrad_plan(int M, int Ng, long Kg, int* bm, int* bn, int* splits, int* kps);
-void conv_wgrad_launch(const ConvArgs& a, int bm, int bn, int splits, float* out, bool accumulate,
+// WGRAD plan: impl 0 = register-staged kernel (bm × bn tiles), 1 = LDS-DMA kernel (config cfg);
+// the caller allocates splits·M·Ng fp32 slab floats and passes them in a.out.
+struct WgradPlan {
+  int impl, cfg, bm, bn, splits, kps;
+};
+void conv_wgrad_plan(const ConvArgs& a, WgradPlan* p);
+void conv_wgrad_launch(const ConvArgs& a, const WgradPlan& p, float* out, bool accumulate,
                        hipStream_t st);
+// LDS-DMA pipelined kernels (conv_glds.hip); false / 0 = not eligible, use the register-staged one
+int conv_glds_mode();
+void conv_set_glds_mode(int mode);  // -1: environment / default
+bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
+bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st);
+bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);
+void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st);
 
 // batch norm ---------------------------------------------------------------------------------

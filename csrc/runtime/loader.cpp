@@ -319,7 +319,6 @@ std::vector<int64_t> BatchLoader::indices_for(long b) {
       out[i] = pos;
       continue;
     }
-    std::vector<int64_t>* perm;
     {
       std::lock_guard<std::mutex> lk(perm_mu_);
       auto it = perms_.find(epoch);
@@ -329,11 +328,14 @@ std::vector<int64_t> BatchLoader::indices_for(long b) {
         std::mt19937_64 rng(seed_ * 1000003ull + epoch);
         std::shuffle(p.begin(), p.end(), rng);
         it = perms_.emplace(epoch, std::move(p)).first;
-        // drop old epochs
-        while (perms_.size() > 3) perms_.erase(perms_.begin());
       }
-      perm = &it->second;
-      out[i] = (*perm)[pos];
+      out[i] = it->second[pos];
+      // bound the cache (a regenerated old epoch is the smallest key: never evict the entry in use)
+      while (perms_.size() > 8) {
+        auto victim = perms_.begin();
+        if (victim == it) ++victim;
+        perms_.erase(victim);
+      }
     }
   }
   return out;

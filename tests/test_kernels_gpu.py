@@ -47,11 +47,26 @@ CONV_SHAPES = [
     (2, 11, 12, 16, 24, 1, 1, 2, (0, 0, 0, 0), 1),      # 1x1 s2 on odd/even sizes
     (2, 12, 12, 16, 16, 3, 3, 3, (1, 1, 1, 1), 1),      # stride 3 (9 parity classes)
     (64, 28, 28, 128, 128, 1, 1, 1, (0, 0, 0, 0), 1),   # multi-tile pipelining (tpb > 1)
+    (16, 28, 28, 64, 64, 3, 3, 1, (1, 1, 1, 1), 1),     # LDS-DMA ring: many tiles per workgroup
+    (8, 29, 27, 128, 192, 3, 3, 2, (1, 1, 1, 1), 1),    # ragged rows / cols, 4 parity classes
+    (8, 20, 20, 40, 24, 3, 3, 1, (1, 1, 1, 1), 1),      # C, K % 64 != 0 (tap-crossing K-steps)
+    (4, 33, 33, 256, 512, 1, 1, 2, (0, 0, 0, 0), 1),    # 1x1 s2, zero parity classes
 ]
+
+CONV_IMPLS = ["reg", "glds"]
+
+
+@pytest.fixture(params=CONV_IMPLS)
+def conv_impl(request, gpu):
+    """Run a conv test with the register-staged kernels (0) or the LDS-DMA kernels forced for
+    every aligned problem (2)."""
+    ext().conv_set_glds_mode(0 if request.param == "reg" else 2)
+    yield request.param
+    ext().conv_set_glds_mode(-1)
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
-def test_conv_fwd_dgrad_wgrad(gpu, shape):
+def test_conv_fwd_dgrad_wgrad(gpu, conv_impl, shape):
     N, H, W, Cin, K, R, S, st, pad, dil = shape
     g = C.ConvGeom((st, st), pad, (dil, dil))
     torch.manual_seed(0)
@@ -84,7 +99,7 @@ def test_conv_fwd_dgrad_wgrad(gpu, shape):
     assert rel_err(bgrad, dyb.float().reshape(-1, K).sum(0)) < 1e-2
 
 
-def test_conv_bias_relu_epilogue(gpu):
+def test_conv_bias_relu_epilogue(gpu, conv_impl):
     torch.manual_seed(1)
     g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
     x = torch.randn(2, 10, 10, 16).bfloat16()

@@ -109,3 +109,16 @@ def test_model_data_parallel_gloo(tmp_path):
     res = m.train(X, y, batch_size=4, steps=2)
     assert len(res) == 2 and all(r["steps"] == 2 for r in res)
     assert ckpt.latest_checkpoint(os.path.join(md, "fold1")).endswith("model.ckpt-2.safetensors")
+
+
+@pytest.mark.gpu
+def test_model_train_predict_on_gpu(tmp_path, gpu):
+    """Same k-fold flow on the GPU at the reference's 101×101 input (native kernels + loader)."""
+    X, y = _dataset(str(tmp_path / "data"), n=8, hw=101, seed=3)
+    md = str(tmp_path / "runs" / "gpu")
+    kw = dict(SMALL, device=None, input_shape=(101, 101), save_checkpoints_steps=3)
+    m = Model(md, str(tmp_path / "data"), n_gpus=1, n_fold=2, save_best=1, **kw)
+    res = m.train(X, y, batch_size=4, steps=3)
+    assert all(np.isfinite(r["eval"]["loss/lovasz_loss"]) for r in res)
+    out = m.predict(os.path.join(str(tmp_path / "data"), "images"), batch_size=4, tti=True)
+    assert out["probabilities"].shape == (8, 101, 101)

@@ -208,3 +208,19 @@ def test_exponential_decay():
     assert O.exponential_decay(1e-3, 0) == 1e-3
     assert abs(O.exponential_decay(1e-3, 10000) - 5e-4) < 1e-12
     assert abs(O.exponential_decay(1e-3, 5000) - 1e-3 * 0.5 ** 0.5) < 1e-12
+
+
+def test_fastdiv_magic_numbers_exact():
+    """Host-generated magic divisors used by the LDS-DMA conv kernels (csrc/kernels/kernels.h)."""
+    import random
+    from tensorflowdistributedlearning_amd import _native
+    ext = _native.load()
+    rng = random.Random(0)
+    divisors = list(range(1, 3000)) + [rng.randrange(1, 1 << 24) for _ in range(500)] + \
+        [7, 14, 28, 56, 112, 3136, 12544, 50176, 802816]
+    for d in divisors:
+        m, s = ext.fastdiv(d)
+        assert m < (1 << 32)
+        ns = [0, 1, d - 1, d, d + 1, (1 << 31) - 1] + [rng.randrange(0, 1 << 31) for _ in range(50)]
+        for n in ns:
+            assert (n * m) >> s == n // d, (n, d)

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Run one conv pass (fwd / dgrad / wgrad) repeatedly under a chosen kernel mode — a target for
+rocprofv3 counter collection.
+
+  python tools/conv_one.py --mode 2 --op fwd --shape 256,14,512,512,3,2,1 --iters 20
+  shape = N,H,Cin,Cout,k,stride,pad (square images)
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
+from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", type=int, default=1)
+    ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--shape", default="256,14,512,512,3,2,1")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    N, H, Cin, Cout, k, s, p = [int(v) for v in a.shape.split(",")]
+    dev = torch.device("cuda")
+    g = C.ConvGeom((s, s), (p, p, p, p), (1, 1))
+    x = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16) * 0.05
+    Ho, Wo = g.out_hw(H, H, k, k)
+    dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
+    ext().conv_set_glds_mode(a.mode)
+    for _ in range(a.iters):
+        if a.op == "fwd":
+            C.conv_fwd(x, w, g)
+        elif a.op == "dgrad":
+            C.conv_dgrad(dy, w, x.shape, g)
+        else:
+            C.conv_wgrad(dy, x, tuple(w.shape), g)
+    torch.cuda.synchronize()
+    print("done", a.mode, a.op, a.shape)
+
+
+if __name__ == "__main__":
+    main()
