@@ -74,7 +74,7 @@ void conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::opt
 }
 
 void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                int64_t dh, int64_t dw) {
+                int64_t dh, int64_t dw, bool accumulate) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -84,6 +84,7 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
   a.dy = BF(dy); a.w = BF(w); a.out = dx.data_ptr();
   a.dy_bytes = nbytes32(dy); a.w_bytes = nbytes32(w); a.out_bytes = nbytes32(dx);
   a.M = a.N * a.H * a.W; a.Ng = a.C; a.Kg = a.R * a.S * a.K; a.ldc = a.C; a.relu = 0;
+  a.beta = accumulate ? 1 : 0;
   if (a.M == 0) return;
   conv_dgrad_launch(a, stream());
 }
@@ -143,26 +144,27 @@ void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool r
   bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu, stream());
 }
 
-void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, bool relu) {
+void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, int64_t relu) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(red, torch::kFloat32);
   const int64_t C = x.size(-1);
+  TORCH_CHECK(relu != 1 || (y.has_value() && y->defined()), "relu mask mode 1 needs y");
   bn_bwd_reduce_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
-                       x.numel() / C, C, relu, stream());
+                       x.numel() / C, C, (int)relu, stream());
 }
 
 void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red,
                   c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres,
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
-                  bool relu) {
+                  int64_t relu) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   const int64_t C = x.size(-1);
   bn_bwd_apply_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
                       optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
-                      C, (float)count, relu, stream());
+                      C, (float)count, (int)relu, stream());
 }
 
 // ---------------------------------------------------------------------------------- elementwise
@@ -423,7 +425,9 @@ std::vector<double> transform_matrix(bool hflip, bool vflip, double angle, doubl
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "tensorflowdistributedlearning_amd native gfx950 kernels";
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
+        py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
+        py::arg("accumulate") = false);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);

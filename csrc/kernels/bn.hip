@@ -41,7 +41,8 @@ __global__ void reduce_scalar_kernel(const bf16_t* __restrict__ a, const bf16_t*
       const float mean = coef[2 * C + c], inv = coef[3 * C + c];
       for (long r = r0 + w; r < r1; r += 4) {
         float g = bf2f(a[r * C + c]);
-        if (relu && bf2f(y[r * C + c]) <= 0.f) g = 0.f;
+        if (relu == 1 && bf2f(y[r * C + c]) <= 0.f) g = 0.f;
+        if (relu == 2 && bf2f(x[r * C + c]) * coef[c] + coef[C + c] <= 0.f) g = 0.f;
         const float xh = (bf2f(x[r * C + c]) - mean) * inv;
         s0 += g;
         s1 += g * xh;
@@ -77,12 +78,14 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
   if (rl < rpp) {
-    float mean[8], inv[8];
+    float mean[8], inv[8], sc[8], sh[8];
     if (KIND == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         mean[j] = coef[2 * C + cv * 8 + j];
         inv[j] = coef[3 * C + cv * 8 + j];
+        sc[j] = coef[cv * 8 + j];
+        sh[j] = coef[C + cv * 8 + j];
       }
     }
     for (long r = r0 + rl; r < r1; r += rpp) {
@@ -98,11 +101,14 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
       } else {
         float vx[8];
         unpack(*(const uint4*)(x + off), vx);
-        if (relu) {
+        if (relu == 1) {
           float vy[8];
           unpack(*(const uint4*)(y + off), vy);
 #pragma unroll
           for (int j = 0; j < 8; ++j) va[j] = vy[j] > 0.f ? va[j] : 0.f;
+        } else if (relu == 2) {  // y = relu(x·scale + shift): the mask without reading y
+#pragma unroll
+          for (int j = 0; j < 8; ++j) va[j] = vx[j] * sc[j] + sh[j] > 0.f ? va[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -131,7 +137,7 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
 
 template <int KIND>
 void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const float* coef, float* out,
-                   long M, int C, bool relu, hipStream_t st) {
+                   long M, int C, int relu, hipStream_t st) {
   if (M <= 0) return;
   if (C % 8 == 0 && C / 8 <= NT) {
     const int cvecs = C / 8, rpp = NT / cvecs;
@@ -139,13 +145,13 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
     hipLaunchKernelGGL(reduce_vec_kernel<KIND>, dim3(blocks), dim3(NT), 0, st, a, y, x, coef, out, M,
-                       C, rpb, relu ? 1 : 0);
+                       C, rpb, relu);
   } else {
     long blocks = std::min<long>(512, std::max<long>(1, M / 64));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
     hipLaunchKernelGGL(reduce_scalar_kernel<KIND>, dim3(blocks, (C + 63) / 64), dim3(NT), 0, st, a, y,
-                       x, coef, out, M, C, rpb, relu ? 1 : 0);
+                       x, coef, out, M, C, rpb, relu);
   }
 }
 
@@ -248,11 +254,13 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
   const long stride = (long)gridDim.x * NT;
   const bool hoist = (stride % cvecs) == 0;
   long i = blockIdx.x * (long)NT + threadIdx.x;
-  float A[8], Bc[8], Cc[8];
+  float A[8], Bc[8], Cc[8], Sc[8], Sh[8];
   auto load_coef = [&](int cv) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = cv * 8 + j;
+      Sc[j] = coef[c];
+      Sh[j] = coef[C + c];
       const float mean = coef[2 * C + c], inv = coef[3 * C + c];
       const float a = (gamma ? gamma[c] : 1.f) * inv;
       const float b = -a * inv * red[C + c] * inv_count;
@@ -267,11 +275,14 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     float g[8], vx[8];
     unpack(((const uint4*)dy)[i], g);
     unpack(((const uint4*)x)[i], vx);
-    if (relu) {
+    if (relu == 1) {
       float vy[8];
       unpack(((const uint4*)y)[i], vy);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = vy[j] > 0.f ? g[j] : 0.f;
+    } else if (relu == 2) {  // mask recomputed from x (no residual): one tensor read saved
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = vx[j] * Sc[j] + Sh[j] > 0.f ? g[j] : 0.f;
     }
     if (dres) ((uint4*)dres)[i] = pack8(g);
     float o[8];
@@ -297,7 +308,8 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
     float g = bf2f(dy[i]);
-    if (relu && bf2f(y[i]) <= 0.f) g = 0.f;
+    if (relu == 1 && bf2f(y[i]) <= 0.f) g = 0.f;
+    if (relu == 2 && bf2f(x[i]) * coef[c] + coef[C + c] <= 0.f) g = 0.f;
     if (dres) dres[i] = f2bf(g);
     const float mean = coef[2 * C + c], inv = coef[3 * C + c];
     const float k = (gamma ? gamma[c] : 1.f) * inv;
@@ -318,7 +330,7 @@ inline int ew_blocks(long n) {
 }  // namespace
 
 void bn_stats_launch(const bf16_t* x, float* stats, long M, int C, hipStream_t st) {
-  reduce_launch<0>(x, nullptr, nullptr, nullptr, stats, M, C, false, st);
+  reduce_launch<0>(x, nullptr, nullptr, nullptr, stats, M, C, 0, st);
 }
 
 void bn_finalize_launch(const float* stats, float* coef, const float* gamma, const float* beta,
@@ -341,21 +353,21 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
 }
 
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                          float* red, long M, int C, bool relu, hipStream_t st) {
+                          float* red, long M, int C, int relu, hipStream_t st) {
   reduce_launch<1>(dy, y, x, coef, red, M, C, relu, st);
 }
 
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
-                         float* dgamma, float* dbeta, long M, int C, float count, bool relu,
+                         float* dgamma, float* dbeta, long M, int C, float count, int relu,
                          hipStream_t st) {
   const long n = M * C;
   if (C % 8 == 0) {
     hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(ew_blocks(n / 8)), dim3(NT), 0, st, dy, y, x, coef,
-                       red, gamma, dx, dres, dgamma, dbeta, n / 8, C, 1.f / count, relu ? 1 : 0);
+                       red, gamma, dx, dres, dgamma, dbeta, n / 8, C, 1.f / count, relu);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
-                       red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu ? 1 : 0);
+                       red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu);
   }
 }
 

@@ -357,9 +357,26 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
           }
           float v[4];
           bf16_t h[4];
+          float prev[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (MODE == DGRAD) {
+            if (a.beta) {  // residual-gradient join: dx += this conv's dgrad
+              if (fast) {
+                const uint32_t poff = (uint32_t)(orow * a.ldc + n0) * 2u;
+                const v2u32 pv = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv && n0 < a.Ng) ? poff : OOB, 0, 0);
+                prev[0] = __uint_as_float(pv[0] << 16);
+                prev[1] = __uint_as_float(pv[0] & 0xffff0000u);
+                prev[2] = __uint_as_float(pv[1] << 16);
+                prev[3] = __uint_as_float(pv[1] & 0xffff0000u);
+              } else if (mv) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                  prev[i] = (n0 + i < a.Ng) ? bf2f(out[orow * a.ldc + n0 + i]) : 0.f;
+              }
+            }
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float t = acc[rm][rn][i] + bv[i];
+            float t = acc[rm][rn][i] + bv[i] + prev[i];
             if (a.relu) t = fmaxf(t, 0.f);
             h[i] = f2bf(t);
             v[i] = bf2f(h[i]);
@@ -673,7 +690,8 @@ void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   // instead of GEMM tiles (they are last after the LPT sort)
   int nz = ncls;
   while (nz > 0 && a.cls_Th[nz - 1] * a.cls_Tw[nz - 1] == 0) --nz;
-  if (nz < ncls) (void)hipMemsetAsync(a.out, 0, (size_t)a.out_bytes, st);
+  // (when accumulating into an existing dx the zero classes simply keep their values)
+  if (nz < ncls && !a.beta) (void)hipMemsetAsync(a.out, 0, (size_t)a.out_bytes, st);
   ncls = nz;
   if (ncls == 0) return;
   a.ncls = ncls;

@@ -375,9 +375,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           }
           bf16_t h[4];
           float v[4];
+          float prev[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (MODE == DGRAD) {
+            if (a.beta) {  // residual-gradient join: dx += this conv's dgrad
+              const uint32_t poff = (uint32_t)(orow * a.ldc + n0) * 2u;
+              const v2u32 pv = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv && n0 < a.Ng) ? poff : OOB, 0, 0);
+              prev[0] = __uint_as_float(pv[0] << 16);
+              prev[1] = __uint_as_float(pv[0] & 0xffff0000u);
+              prev[2] = __uint_as_float(pv[1] << 16);
+              prev[3] = __uint_as_float(pv[1] & 0xffff0000u);
+            }
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float t = acc[rm][rn][i] + bv[i];
+            float t = acc[rm][rn][i] + bv[i] + prev[i];
             if (a.relu) t = fmaxf(t, 0.f);
             h[i] = f2bf(t);
             v[i] = bf2f(h[i]);

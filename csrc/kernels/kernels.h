@@ -39,6 +39,7 @@ struct ConvArgs {
   int M, Ng, Kg;     // GEMM dims
   int ldc;
   int relu;
+  int beta;          // DGRAD: 1 = accumulate into the existing dx (residual-gradient join)
   uint32_t x_bytes, w_bytes, dy_bytes, out_bytes;  // buffer-descriptor ranges (OOB -> 0 / dropped)
   int kps;           // WGRAD: K-steps per split
   int splits;        // WGRAD: number of K splits
@@ -82,10 +83,10 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st);
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                          float* red, long M, int C, bool relu, hipStream_t st);
+                          float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
-                         float* dgamma, float* dbeta, long M, int C, float count, bool relu,
+                         float* dgamma, float* dbeta, long M, int C, float count, int relu,
                          hipStream_t st);
 
 // elementwise --------------------------------------------------------------------------------

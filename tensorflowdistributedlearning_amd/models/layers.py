@@ -148,9 +148,9 @@ class Conv2d(nn.Module):
             self._geom_cache[(H, W)] = g
         return g
 
-    def forward(self, x, want_stats=False):
+    def forward(self, x, want_stats=False, join=None):
         g = self.geom(x.shape[1], x.shape[2])
-        y, stats = conv2d(x, self.weight, self.bias, g, self.relu, want_stats, self)
+        y, stats = conv2d(x, self.weight, self.bias, g, self.relu, want_stats, self, join)
         return (y, stats) if want_stats else y
 
     def extra_repr(self):
@@ -173,9 +173,9 @@ class BatchNorm(nn.Module):
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
 
-    def forward(self, x, stats=None, residual=None, relu=False):
+    def forward(self, x, stats=None, residual=None, relu=False, res_join=None):
         return batch_norm_act(x, self, stats=stats, residual=residual, relu=relu,
-                              training=self.training)
+                              training=self.training, res_join=res_join)
 
 
 class ConvBN(nn.Module):
@@ -190,12 +190,13 @@ class ConvBN(nn.Module):
         self.bn = BatchNorm(cout, bn_decay, bn_eps, bn_scale, zero_init_gamma)
         self.relu = relu
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, join=None, res_join=None):
+        """``join``: gradient join for x (ops/gradjoin.py); ``res_join``: for the residual."""
         if self.training:
-            y, stats = self.conv(x, want_stats=True)
+            y, stats = self.conv(x, want_stats=True, join=join)
         else:
-            y, stats = self.conv(x), None
-        return self.bn(y, stats=stats, residual=residual, relu=self.relu)
+            y, stats = self.conv(x, join=join), None
+        return self.bn(y, stats=stats, residual=residual, relu=self.relu, res_join=res_join)
 
 
 class BNAct(nn.Module):

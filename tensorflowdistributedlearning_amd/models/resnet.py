@@ -11,6 +11,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops import gradjoin
+
 from .layers import ConvBN, MaxPool, GlobalAvgPool, Linear
 
 _CFG = {
@@ -35,9 +37,14 @@ class BasicBlock(nn.Module):
                                      init="kaiming_fan_out", **bn_kw)
 
     def forward(self, x):
-        sc = x if self.downsample is None else self.downsample(x)
-        out = self.conv1(x)
-        return self.conv2(out, residual=sc)
+        # x feeds conv1 and the shortcut: one shared gradient buffer (ops/gradjoin.py)
+        join = gradjoin.make(2, x) if self.training else None
+        if self.downsample is None:
+            sc, res_join = x, join
+        else:
+            sc, res_join = self.downsample(x, join=join), None
+        out = self.conv1(x, join=join)
+        return self.conv2(out, residual=sc, res_join=res_join)
 
 
 class Bottleneck(nn.Module):
@@ -56,10 +63,15 @@ class Bottleneck(nn.Module):
                                      **bn_kw)
 
     def forward(self, x):
-        sc = x if self.downsample is None else self.downsample(x)
-        y = self.conv1(x)
+        # x feeds conv1 and the shortcut: one shared gradient buffer (ops/gradjoin.py)
+        join = gradjoin.make(2, x) if self.training else None
+        if self.downsample is None:
+            sc, res_join = x, join
+        else:
+            sc, res_join = self.downsample(x, join=join), None
+        y = self.conv1(x, join=join)
         y = self.conv2(y)
-        return self.conv3(y, residual=sc)
+        return self.conv3(y, residual=sc, res_join=res_join)
 
 
 class ResNet(nn.Module):

@@ -78,16 +78,25 @@ def bn_apply(x, coef, residual=None, relu=True):
     return y.to(x.dtype)
 
 
+def _relu_mask(relu, y, x, coef, C):
+    """ReLU mask of the BN output: from y (relu=True / 1), or — without residual — recomputed as
+    x·scale + shift > 0 (relu=2) so the backward never reads y."""
+    if relu == 2:
+        return (x.float().reshape(-1, C) * coef[0] + coef[1]) > 0
+    return y.float().reshape(-1, C) > 0
+
+
 def bn_bwd_reduce(dy, y, x, coef, relu):
-    """fp32 [2, C]: (Σg, Σg·x̂), g = dy·[y>0] if relu else dy."""
+    """fp32 [2, C]: (Σg, Σg·x̂), g = dy·mask if relu else dy (relu: 0/False, 1/True = mask from y,
+    2 = mask from x·scale+shift)."""
     C = x.shape[-1]
     if on_gpu(dy):
         red = workspace.zeros((2, C), dy.device)
-        ext().bn_bwd_reduce(dy, y, x, coef, red, bool(relu))
+        ext().bn_bwd_reduce(dy, y, x, coef, red, int(relu))
         return red
     g = dy.float().reshape(-1, C)
     if relu:
-        g = g * (y.float().reshape(-1, C) > 0)
+        g = g * _relu_mask(relu, y, x, coef, C)
     xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
     return torch.stack([g.sum(0), (g * xhat).sum(0)])
 
@@ -100,11 +109,11 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
         dx = torch.empty_like(x)
         dres = torch.empty_like(dy) if want_dres else None
         ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
-                           bool(relu))
+                           int(relu))
         return dx, dres
     g = dy.float().reshape(-1, C)
     if relu:
-        g = g * (y.float().reshape(-1, C) > 0)
+        g = g * _relu_mask(relu, y, x, coef, C)
     xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
     gam = gamma.detach().float() if gamma is not None else torch.ones(C)
     k = gam * coef[3]
@@ -119,7 +128,7 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
 
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training):
+    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training, res_join):
         C = x.shape[-1]
         count = x.numel() // C
         if training:
@@ -128,11 +137,14 @@ class _BatchNormActFn(torch.autograd.Function):
         coef = bn_finalize(stats, count, gamma, beta, bn.running_mean, bn.running_var,
                            bn.decay, bn.eps, training)
         y = bn_apply(x, coef, residual, relu)
-        ctx.relu = relu
         ctx.count = count
         ctx.training = training
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y, coef, gamma, beta)
+        ctx.res_join = res_join if residual is not None else None
+        # without a residual the ReLU mask is recomputed from x (relu mode 2): y is not saved and
+        # the backward kernels read two tensors instead of three
+        ctx.relu = (2 if residual is None else 1) if relu else 0
+        ctx.save_for_backward(x, y if ctx.relu == 1 else None, coef, gamma, beta)
         return y
 
     @staticmethod
@@ -145,7 +157,7 @@ class _BatchNormActFn(torch.autograd.Function):
             C = x.shape[-1]
             g = dy.float().reshape(-1, C)
             if relu:
-                g = g * (y.float().reshape(-1, C) > 0)
+                g = g * _relu_mask(relu, y, x, coef, C)
             dx = (g * coef[0]).reshape(x.shape).to(x.dtype)
             xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
             if gamma is not None and gamma.requires_grad:
@@ -153,7 +165,7 @@ class _BatchNormActFn(torch.autograd.Function):
             if beta.requires_grad:
                 deliver_grad(beta, g.sum(0))
             dres = g.reshape(dy.shape).to(dy.dtype) if ctx.has_res else None
-            return dx, None, None, None, dres, None, None, None
+            return dx, None, None, None, _join_res(ctx, dres), None, None, None, None
         red = bn_bwd_reduce(dy, y, x, coef, relu)
         want_g = gamma is not None and gamma.requires_grad
         want_b = beta.requires_grad
@@ -167,10 +179,24 @@ class _BatchNormActFn(torch.autograd.Function):
             deliver_grad(gamma, None if direct_g else red[1], written=direct_g)
         if want_b:
             deliver_grad(beta, None if direct_b else red[0], written=direct_b)
-        return dx, None, None, None, dres, None, None, None
+        return dx, None, None, None, _join_res(ctx, dres), None, None, None, None
 
 
-def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True):
+def _join_res(ctx, dres):
+    """Residual gradient into the block input's shared buffer (ops/gradjoin.py)."""
+    join = ctx.res_join
+    if join is None or dres is None:
+        return dres
+    if join.buf is None:
+        join.buf = dres
+    else:  # another consumer ran first (not the usual order): plain add
+        join.buf.add_(dres)
+    return join.take()
+
+
+def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True, res_join=None):
     """act(BN(x) [+ residual]).  ``bn`` is a :class:`models.layers.BatchNorm` (holds γ, β and the
-    moving statistics).  ``stats`` may carry Σx, Σx² already accumulated by the producer conv."""
-    return _BatchNormActFn.apply(x, stats, bn.gamma, bn.beta, residual, bn, relu, training)
+    moving statistics).  ``stats`` may carry Σx, Σx² already accumulated by the producer conv.
+    ``res_join`` shares the residual's gradient buffer with its other consumers."""
+    return _BatchNormActFn.apply(x, stats, bn.gamma, bn.beta, residual, bn, relu, training,
+                                 res_join)

@@ -113,13 +113,24 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out_dtype=
     return y
 
 
-def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None):
+def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumulate=False):
+    """dx.  With ``out`` the result is written there (``accumulate``: dx += …, fused in the GEMM
+    epilogue — used by the residual-gradient join, ops/gradjoin.py)."""
     if on_gpu(dy):
-        dx = torch.empty(x_shape, device=dy.device, dtype=out_dtype or dy.dtype)
+        dx = out if out is not None else torch.empty(x_shape, device=dy.device,
+                                                     dtype=out_dtype or dy.dtype)
         ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
-                         geom.padding[2], geom.dilation[0], geom.dilation[1])
+                         geom.padding[2], geom.dilation[0], geom.dilation[1],
+                         bool(accumulate and out is not None))
         return dx
-    return ref_conv_dgrad(dy, w, x_shape, geom).to(out_dtype or dy.dtype)
+    r = ref_conv_dgrad(dy, w, x_shape, geom)
+    if out is None:
+        return r.to(out_dtype or dy.dtype)
+    if accumulate:
+        out.copy_((out.float() + r).to(out.dtype))
+    else:
+        out.copy_(r.to(out.dtype))
+    return out
 
 
 def conv_wgrad(dy, x, w_shape, geom: ConvGeom, out=None, accumulate=False, bias_grad=None):
@@ -159,7 +170,7 @@ def relu_bwd(dy, y):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer):
+    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer, join):
         w = layer.compute_weight(x.dtype) if layer is not None else compute_weight(weight, x.dtype)
         stats = None
         if want_stats:
@@ -169,6 +180,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.geom = geom
         ctx.relu = relu
         ctx.layer = layer
+        ctx.join = join
         ctx.x_shape = tuple(x.shape)
         ctx.save_for_backward(x, weight, bias, y if relu else None)
         if stats is None:
@@ -187,7 +199,15 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
                 compute_weight(weight, dy.dtype)
-            dx = conv_dgrad(dy, w, ctx.x_shape, geom)
+            join = ctx.join
+            if join is None:
+                dx = conv_dgrad(dy, w, ctx.x_shape, geom)
+            else:  # residual-gradient join: first consumer writes, later ones accumulate
+                if join.buf is None:
+                    join.buf = conv_dgrad(dy, w, ctx.x_shape, geom)
+                else:
+                    conv_dgrad(dy, w, ctx.x_shape, geom, out=join.buf, accumulate=True)
+                dx = join.take()
         want_bias = bias is not None and bias.requires_grad
         bias_buf, bias_direct = None, False
         if want_bias:
@@ -214,11 +234,12 @@ class _Conv2dFn(torch.autograd.Function):
                 deliver_grad(bias, written=True)
             else:
                 deliver_grad(bias, bias_buf)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
 def conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False, want_stats=False,
-           layer=None):
+           layer=None, join=None):
     """Differentiable NHWC conv. Returns (y, stats) where stats is fp32 [2, K] (sum, sumsq of y)
-    when ``want_stats`` else an empty tensor."""
-    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer)
+    when ``want_stats`` else an empty tensor.  ``join`` (ops.gradjoin.GradJoin) makes dx share one
+    buffer with the other consumers of ``x``."""
+    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer, join)

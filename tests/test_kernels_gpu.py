@@ -125,8 +125,10 @@ def test_conv_large_resnet_shape(gpu):
 
 
 @pytest.mark.parametrize("C_", [64, 258, 24])
-@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False), (2, False)])
 def test_batchnorm(gpu, C_, relu, res):
+    """relu=2: the backward kernels re-derive the ReLU mask from x·scale+shift (y not passed);
+    checked against the mask-from-y reference."""
     torch.manual_seed(3)
     M = 2 * 9 * 11
     x = (torch.randn(2, 9, 11, C_) * 2 + 0.5).bfloat16()
@@ -147,12 +149,14 @@ def test_batchnorm(gpu, C_, relu, res):
     y = B.bn_apply(xd, coef, None if r is None else r.to(gpu), relu)
     assert rel_err(y, y_ref) < 2e-2
     dy = torch.randn(x.shape).bfloat16()
-    red_ref = B.bn_bwd_reduce(dy.float(), y.float().cpu(), x.float(), coef_ref, relu)
-    red = B.bn_bwd_reduce(dy.to(gpu), y, xd, coef, relu)
+    ref_relu = bool(relu)
+    y_dev = None if relu == 2 else y
+    red_ref = B.bn_bwd_reduce(dy.float(), y.float().cpu(), x.float(), coef_ref, ref_relu)
+    red = B.bn_bwd_reduce(dy.to(gpu), y_dev, xd, coef, relu)
     assert rel_err(red, red_ref) < 2e-2
     dx_ref, dres_ref = B.bn_bwd_apply(dy.float(), y.float().cpu(), x.float(), coef_ref, red_ref,
-                                      gamma, M, relu, res)
-    dx, dres = B.bn_bwd_apply(dy.to(gpu), y, xd, coef, red, gamma.to(gpu), M, relu, res)
+                                      gamma, M, ref_relu, res)
+    dx, dres = B.bn_bwd_apply(dy.to(gpu), y_dev, xd, coef, red, gamma.to(gpu), M, relu, res)
     assert rel_err(dx, dx_ref) < 3e-2
     if res:
         assert rel_err(dres, dres_ref) < 1e-2
@@ -322,3 +326,23 @@ def test_native_extension_is_loaded(gpu):
     assert _native.available()
     assert any("_C" in (getattr(m, "__file__", "") or "") for m in list(sys.modules.values())
                if m is not None)
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 256, 64, 1, 1, 1, (0, 0, 0, 0), 1),
+                                   (4, 15, 15, 128, 256, 1, 1, 2, (0, 0, 0, 0), 1),
+                                   (4, 14, 14, 64, 64, 3, 3, 1, (1, 1, 1, 1), 1),
+                                   (8, 28, 28, 128, 128, 3, 3, 2, (1, 1, 1, 1), 1)])
+def test_conv_dgrad_accumulate(gpu, conv_impl, shape):
+    """Residual-gradient join: dgrad epilogue adds into an existing dx (zero parity classes of a
+    strided 1x1 keep the existing values)."""
+    N, H, W, Cin, K, R, S, st, pad, dil = shape
+    g = C.ConvGeom((st, st), pad, (dil, dil))
+    torch.manual_seed(5)
+    w = (torch.randn(K, R, S, Cin) / math.sqrt(R * S * Cin)).bfloat16()
+    Ho, Wo = g.out_hw(H, W, R, S)
+    dy = torch.randn(N, Ho, Wo, K).bfloat16()
+    prev = torch.randn(N, H, W, Cin).bfloat16()
+    ref = prev.float() + C.ref_conv_dgrad(dy.float(), w.float(), (N, H, W, Cin), g)
+    out = prev.to(gpu)
+    C.conv_dgrad(dy.to(gpu), w.to(gpu), (N, H, W, Cin), g, out=out, accumulate=True)
+    assert rel_err(out, ref) < 2e-2

@@ -94,3 +94,27 @@ def test_xception41_intended_structure():
 def test_resnet_forward_shapes():
     m = models.resnet18(num_classes=10)
     assert m(torch.randn(2, 32, 32, 3)).shape == (2, 10)
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_residual_gradient_join_matches_autograd(depth):
+    """ops/gradjoin.py: sharing one dx buffer between a block input's consumers gives the same
+    gradients as autograd's separate sum (identity and downsample shortcuts)."""
+    from tensorflowdistributedlearning_amd.ops import gradjoin
+    torch.manual_seed(0)
+    m = models.build(f"resnet{depth}", num_classes=5, width=8)
+    x = torch.randn(2, 32, 32, 8)
+    grads = []
+    for enabled in (False, True):
+        gradjoin.ENABLED = enabled
+        try:
+            m.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            m.train()
+            out = m(xi)
+            out.float().pow(2).sum().backward()
+            grads.append([xi.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+        finally:
+            gradjoin.ENABLED = True
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)

@@ -100,3 +100,32 @@ def test_xception_forward_backward(gpu):
     x, y = imagenet_batch(4, 64, num_classes=10, device=gpu)
     l = float(tr.train_step(x, y)[0])
     assert l == l
+
+
+def test_residual_join_gpu_matches_plain_autograd(gpu):
+    """Block-input gradient via the shared-buffer join (accumulating dgrad epilogue) vs autograd's
+    separate add, on the GPU kernels (frozen BN: no batch-statistics chaos in the comparison)."""
+    from tensorflowdistributedlearning_amd.ops import gradjoin
+    torch.manual_seed(6)
+    m = models.resnet50(num_classes=10).to(gpu)
+    m.eval()  # moving statistics: deterministic, well-conditioned backward
+    x = torch.randn(4, 64, 64, 8, device=gpu, dtype=torch.bfloat16)
+    outs = []
+    for enabled in (False, True):
+        gradjoin.ENABLED = enabled
+        try:
+            for p in m.parameters():
+                p.grad = None
+            xi = x.clone().requires_grad_(True)
+            m.train()
+            for mod in m.modules():  # BN in eval mode inside a training-mode forward
+                if mod.__class__.__name__ == "BatchNorm":
+                    mod.train(False)
+            y = m(xi)
+            y.float().sum().backward()
+            outs.append(torch.cat([p.grad.float().flatten() for p in m.parameters()
+                                   if p.grad is not None]))
+        finally:
+            gradjoin.ENABLED = True
+    cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=0).item()
+    assert cos > 0.999, cos
