@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--profile-phases", action="store_true",
+                    help="also print per-phase step times (forward/backward/comm_wait/optimizer, "
+                         "device events) to stderr")
     args = ap.parse_args()
 
     ctx = init_distributed()
@@ -61,7 +64,8 @@ def main():
         per_gpu = args.batch or max(64 // n, 1)
         model = models.DeepLabResNet(model_name="model", input_shape=(101, 101))
         tr = Trainer(model, lovasz_hinge, dev, "adam", dict(lr=1e-3), ctx=ctx,
-                     bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
+                     bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+                     profile_phases=args.profile_phases)
         x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank)
         metric = "images/sec (whole node), reference DeepLab-ResNet 101x101x2 bf16"
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
@@ -73,7 +77,8 @@ def main():
         model = models.build(args.model, num_classes=1000)
         tr = Trainer(model, softmax_cross_entropy, dev, "sgd",
                      dict(lr=args.lr, momentum=0.9, weight_decay=5e-5), ctx=ctx,
-                     bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
+                     bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+                     profile_phases=args.profile_phases)
         x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank)
         metric = METRIC if args.model == "resnet50" and args.image_size == 224 else \
             f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} bf16"
@@ -104,6 +109,10 @@ def main():
     ms = el / args.steps * 1e3
     value = per_gpu * n * args.steps / el
     if ctx.is_main:
+        if tr.timer is not None:
+            ph = tr.timer.summary()
+            print("[bench] phases ms/step (timed + warmup steps): " +
+                  " ".join(f"{k}={v:.2f}" for k, v in ph.items()), file=sys.stderr)
         print(json.dumps({
             "metric": metric, "value": round(value, 2), "unit": "images/sec", "n_gpus": n,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),

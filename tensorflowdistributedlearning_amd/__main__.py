@@ -1,0 +1,132 @@
+"""Command line: ``python -m tensorflowdistributedlearning_amd <command> …``.
+
+  train    k-fold training of the reference DeepLab model on a TGS-style directory
+           (``<data>/images/*.png`` + ``<data>/masks/*.png``), stratified on mask-coverage class
+           exactly like the reference notebook (coverage = Σmask / (H·W), class = ⌈10·coverage⌉,
+           Test.ipynb) — i.e. ``Model(...).train(ids, classes, batch_size, steps)``;
+  predict  TTA-averaged probabilities of every ``*.png`` in a directory → ``.npz`` (+ optional CSV
+           with run-length-encoded masks, the Kaggle submission format);
+  bench    the training benchmark (same as ``python bench.py``);
+  config   print the default configuration (JSON) to start a config file from.
+
+Configuration comes from ``--config file.{json,yaml}`` and is overridden by flags.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import glob
+import json
+import math
+import os
+import sys
+
+import numpy as np
+
+from .config import ModelConfig, load, from_dict
+
+
+def coverage_classes(data_dir, ids):
+    """Reference notebook stratification label: class = smallest i with 10·coverage ≤ i."""
+    from . import _native
+    ext = _native.load()
+    classes = []
+    for i in ids:
+        m = ext.png_decode_gray(os.path.join(data_dir, "masks", f"{i}.png")).numpy()
+        cov = float((m > 0.5).sum()) / m.size
+        classes.append(int(math.ceil(cov * 10 - 1e-9)) if cov > 0 else 0)
+    return np.array(classes)
+
+
+def rle_encode(mask):
+    """Kaggle TGS run-length encoding (column-major, 1-indexed)."""
+    pixels = np.concatenate([[0], mask.T.flatten(), [0]])
+    runs = np.where(pixels[1:] != pixels[:-1])[0] + 1
+    runs[1::2] -= runs[::2]
+    return " ".join(str(r) for r in runs)
+
+
+def _model_cfg(args):
+    cfg = load(args.config) if args.config else ModelConfig()
+    over = {k: v for k, v in vars(args).items()
+            if k in {f.name for f in dataclasses.fields(ModelConfig)} and v is not None}
+    d = dataclasses.asdict(cfg)
+    d.update(over)
+    return from_dict(ModelConfig, d).validate()
+
+
+def cmd_train(args):
+    from .model import Model
+    cfg = _model_cfg(args)
+    ids = sorted(os.path.splitext(os.path.basename(p))[0]
+                 for p in glob.glob(os.path.join(cfg.data_directory, "images", "*.png")))
+    if not ids:
+        raise SystemExit(f"no images under {cfg.data_directory}/images")
+    y = coverage_classes(cfg.data_directory, ids)
+    m = Model(**cfg.model_kwargs())
+    res = m.train(np.array(ids), y, args.batch_size, args.steps)
+    print(json.dumps({"params": m.params, "folds": res}, default=float))
+
+
+def cmd_predict(args):
+    from .model import Model
+    cfg = _model_cfg(args)
+    m = Model(**cfg.model_kwargs())
+    out = m.predict(args.test_dir, args.batch_size, tti=args.tta)
+    np.savez_compressed(args.out, ids=np.array(out["ids"]), probabilities=out["probabilities"])
+    if args.csv:
+        with open(args.csv, "w") as f:
+            f.write("id,rle_mask\n")
+            for i, mk in zip(out["ids"], out["mask"]):
+                f.write(f"{i},{rle_encode(mk)}\n")
+    print(f"wrote {args.out}" + (f" and {args.csv}" if args.csv else ""))
+
+
+def cmd_bench(rest):
+    sys.argv = ["bench.py"] + rest
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, here)
+    import bench
+    bench.main()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if argv and argv[0] == "bench":
+        return cmd_bench(argv[1:])
+    ap = argparse.ArgumentParser(prog="python -m tensorflowdistributedlearning_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    def common(p):
+        p.add_argument("--config")
+        p.add_argument("--model-dir", dest="model_dir")
+        p.add_argument("--data-dir", dest="data_directory")
+        p.add_argument("--n-gpus", dest="n_gpus", type=int)
+        p.add_argument("--n-fold", dest="n_fold", type=int)
+        p.add_argument("--lr", type=float)
+        p.add_argument("--seed", type=int)
+        p.add_argument("--device")
+        p.add_argument("--block-type", dest="block_type")
+        p.add_argument("--batch-size", dest="batch_size", type=int, default=64)
+
+    t = sub.add_parser("train")
+    common(t)
+    t.add_argument("--steps", type=int, default=100)
+    p = sub.add_parser("predict")
+    common(p)
+    p.add_argument("--test-dir", required=True)
+    p.add_argument("--tta", action="store_true")
+    p.add_argument("--out", default="predictions.npz")
+    p.add_argument("--csv")
+    sub.add_parser("config")
+    args = ap.parse_args(argv)
+    if args.cmd == "train":
+        cmd_train(args)
+    elif args.cmd == "predict":
+        cmd_predict(args)
+    elif args.cmd == "config":
+        print(json.dumps(dataclasses.asdict(ModelConfig()), indent=1))
+
+
+if __name__ == "__main__":
+    main()

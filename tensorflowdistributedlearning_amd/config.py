@@ -1,0 +1,125 @@
+"""Typed configuration.
+
+* :class:`ModelConfig` mirrors the reference ``Model`` constructor knobs and their defaults
+  (model.py:13-24,29-136) plus the engine knobs that the reference hard-codes (checkpoint every
+  500 steps, summaries every 20, …) — ``Model(**cfg.model_kwargs())`` builds the same model.
+* :class:`BenchConfig` holds the north-star additions (architecture preset, dtype, optimizer,
+  loss, synthetic data, DP bucket sizes).
+
+Both load from / dump to plain dicts, JSON or YAML (``yaml.safe_load``) and are what the CLI
+(``python -m tensorflowdistributedlearning_amd …``) fills from flags.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from dataclasses import dataclass, field
+from typing import Optional, Tuple
+
+
+@dataclass
+class ModelConfig:
+    model_dir: str = "runs/model"
+    data_directory: str = "data"
+    data_format: str = "NHWC"
+    lr: float = 0.001
+    n_gpus: int = 2
+    n_fold: int = 5
+    seed: int = 42
+    save_best: int = 5
+    # reference kwargs (model.py:63-106) — D1/D2 fixed: each reads its own name
+    weight_decay: float = 0.001
+    batch_norm_decay: float = 0.99
+    batch_norm_epsilon: float = 0.001
+    batch_norm_scale: bool = True
+    output_stride: int = 8
+    base_depth: int = 256
+    input_shape: Tuple[int, int] = (101, 101)
+    n_blocks: Tuple[int, int, int] = (3, 4, 6)
+    block_type: str = "bottleneck"
+    # hard-coded in the reference (RunConfig / hooks / model_fn params)
+    save_checkpoints_steps: int = 500
+    save_summary_steps: int = 20
+    keep_checkpoint_max: int = 5
+    threshold: float = 0.5
+    # extensions
+    use_regularization: bool = False  # D5: opt-in L2 term
+    kaggle_metric: bool = False       # D16: reference formula by default
+    loader_threads: int = 4
+    device: Optional[str] = None
+
+    def validate(self):
+        if self.data_format not in ("NCHW", "NHWC"):
+            raise ValueError(f"Unknown data format {self.data_format}. Has to be either NCHW or NHWC")
+        if self.output_stride is not None and self.output_stride % 4:
+            raise ValueError("The output_stride needs to be a multiple of 4.")
+        if len(self.n_blocks) != 3:
+            raise ValueError("Expect n_blocks to have length 3.")
+        if self.block_type not in ("bottleneck", "basic_block"):
+            raise ValueError(f"unknown block_type {self.block_type}")
+        return self
+
+    def model_kwargs(self):
+        d = dataclasses.asdict(self)
+        d["input_shape"] = tuple(d["input_shape"])
+        d["n_blocks"] = tuple(d["n_blocks"])
+        d["n_fold"] = d.pop("n_fold")
+        return d
+
+
+@dataclass
+class BenchConfig:
+    arch: str = "resnet50"            # resnet18/34/50/101/152, xception41, deeplab_ref
+    dtype: str = "bf16"
+    optimizer: str = "sgd_momentum"   # or adam
+    loss: str = "softmax_ce"          # or lovasz
+    synthetic: bool = True
+    batch: int = 256                  # per GPU
+    image_size: int = 224
+    steps: int = 20
+    warmup: int = 5
+    lr: float = 0.1
+    momentum: float = 0.9
+    weight_decay: float = 5e-5
+    bucket_mb: float = 32.0
+    first_bucket_mb: float = 4.0
+    extra: dict = field(default_factory=dict)
+
+
+def _coerce(cls, d):
+    names = {f.name: f for f in dataclasses.fields(cls)}
+    unknown = set(d) - set(names)
+    if unknown:
+        raise ValueError(f"unknown {cls.__name__} keys: {sorted(unknown)}")
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, list):
+            v = tuple(v)
+        out[k] = v
+    return cls(**out)
+
+
+def from_dict(cls, d):
+    return _coerce(cls, dict(d))
+
+
+def load(path, cls=ModelConfig):
+    """JSON or YAML (safe loader) file → config."""
+    with open(path) as f:
+        text = f.read()
+    if path.endswith((".yaml", ".yml")):
+        import yaml
+        d = yaml.safe_load(text) or {}
+    else:
+        d = json.loads(text)
+    return from_dict(cls, d)
+
+
+def dump(cfg, path):
+    d = dataclasses.asdict(cfg)
+    with open(path, "w") as f:
+        if path.endswith((".yaml", ".yml")):
+            import yaml
+            yaml.safe_dump(d, f, sort_keys=False)
+        else:
+            json.dump(d, f, indent=1)

@@ -57,6 +57,47 @@ def xception_block(scope, depth_list, skip_connection_type, activation_fn_in_sep
         "unit_rate_list": unit_rate_list}] * num_units)
 
 
+def stack_blocks_dense(in_channels, blocks, output_stride=None):
+    """Build the units of ``blocks`` (xception_block specs) with atrous output-stride control
+    (core/xception.py:231-292): once the running stride reaches ``output_stride`` further strides
+    become dilation.  Returns (nn.ModuleList of units, out_channels)."""
+    import torch.nn as nn
+    if output_stride is not None and output_stride <= 0:
+        raise ValueError("output_stride must be positive")
+    current, rate = 1, 1
+    units = nn.ModuleList()
+    cin = in_channels
+    for block in blocks:
+        for args in block.args:
+            stride = args["stride"]
+            if output_stride is not None and current > output_stride:
+                raise ValueError("The target output_stride cannot be reached.")
+            if output_stride is not None and current == output_stride:
+                m = block.unit_fn(cin, args["depth_list"], args["skip_connection_type"], 1,
+                                  args.get("unit_rate_list"), rate,
+                                  args["activation_fn_in_separable_conv"])
+                rate *= stride
+            else:
+                m = block.unit_fn(cin, args["depth_list"], args["skip_connection_type"], stride,
+                                  args.get("unit_rate_list"), 1,
+                                  args["activation_fn_in_separable_conv"])
+                current *= stride
+            units.append(m)
+            cin = m.out_channels
+    if output_stride is not None and current != output_stride:
+        raise ValueError("The target output_stride cannot be reached.")
+    return units, cin
+
+
+def xception(inputs, blocks=None, num_classes=None, is_training=True, global_pool=True,
+             keep_prob=0.5, output_stride=None, reuse=None, scope=None, data_format="NHWC"):
+    """Generic Xception generator (core/xception.py:295-402) over the Xception-41 block specs;
+    the 41-layer configuration is :func:`xception_41`."""
+    return xception_41(inputs, is_training=is_training, keep_prob=keep_prob,
+                       output_stride=output_stride, scope=scope or "xception",
+                       num_classes=num_classes, data_format=data_format)
+
+
 def xception_41(inputs, is_training=True, keep_prob=0.5, output_stride=None,
                 regularize_depthwise=False, multi_grid=None, reuse=None, scope="xception_41",
                 num_classes=None, data_format="NHWC"):

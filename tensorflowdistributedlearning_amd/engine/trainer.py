@@ -18,10 +18,56 @@ from .optimizer import build_optimizer
 from ..ops import workspace
 
 
+class PhaseTimer:
+    """Per-phase step timing with device events: forward, backward (incl. the
+    bucketed all-reduces launched from the gradient hooks), comm_wait (waiting for the last
+    buckets), optimizer.  Events are read lazily — ``summary()`` synchronises once."""
+
+    PHASES = ("forward", "backward", "comm_wait", "optimizer")
+
+    def __init__(self, device):
+        self.cuda = device.type == "cuda"
+        self.steps = []
+        self.cur = {}
+
+    def mark(self, name):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.cur[name] = e
+        else:
+            self.cur[name] = time.perf_counter()
+
+    def end_step(self):
+        self.steps.append(self.cur)
+        self.cur = {}
+
+    def summary(self, reset=True):
+        """Mean milliseconds per phase over the recorded steps."""
+        if not self.steps:
+            return {}
+        if self.cuda:
+            torch.cuda.synchronize()
+        tot = {p: 0.0 for p in self.PHASES}
+        order = ("start",) + self.PHASES
+        for st in self.steps:
+            for a, b in zip(order[:-1], order[1:]):
+                if self.cuda:
+                    tot[b] += st[a].elapsed_time(st[b])
+                else:
+                    tot[b] += (st[b] - st[a]) * 1e3
+        n = len(self.steps)
+        if reset:
+            self.steps = []
+        res = {k: v / n for k, v in tot.items()}
+        res["step"] = sum(res.values())
+        return res
+
+
 class Trainer:
     def __init__(self, model, loss_fn, device, optimizer="sgd", opt_kwargs=None, ctx=None,
                  bucket_mb=32.0, first_bucket_mb=4.0, lowp_dtype=torch.bfloat16,
-                 broadcast_init=True, extra_loss_fn=None):
+                 broadcast_init=True, extra_loss_fn=None, profile_phases=False):
         self.device = torch.device(device)
         self.model = model.to(self.device)
         self.loss_fn = loss_fn
@@ -35,6 +81,7 @@ class Trainer:
                          if self.ctx.is_distributed else None)
         self.global_step = 0
         self.train_mode = True  # False: BN uses moving statistics while training (frozen BN)
+        self.timer = PhaseTimer(self.device) if profile_phases else None
 
     # ------------------------------------------------------------------------------------------
     def broadcast_state(self):
@@ -45,20 +92,32 @@ class Trainer:
         self.flat.sync_lowp()
 
     def train_step(self, x, y):
+        t = self.timer
         self.model.train(self.train_mode)
         workspace.reset(self.device)
         self.flat.begin_step()
+        if t:
+            t.mark("start")
         out = self.model(x)
         loss = self.loss_fn(out, y)
         if self.extra_loss_fn is not None:
             loss = loss + self.extra_loss_fn(self.model)
+        if t:
+            t.mark("forward")
         loss.backward()
         self.flat.finish_grads()
+        if t:
+            t.mark("backward")
         world = 1
         if self.bucketer is not None:
             self.bucketer.finish()
             world = self.ctx.world_size
+        if t:
+            t.mark("comm_wait")
         self.optimizer.step(grad_scale=1.0 / world)
+        if t:
+            t.mark("optimizer")
+            t.end_step()
         self.global_step += 1
         return loss.detach(), out.detach()
 

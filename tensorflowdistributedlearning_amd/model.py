@@ -330,6 +330,56 @@ class Model:
         return {"ids": ids, "probabilities": prob,
                 "mask": (prob > self.threshold).astype(np.uint8)}
 
+    # ------------------------------------------------------------------------------------------
+    # reference-surface helpers (model.py:257-505): the pieces train()/predict() are built from
+    def build_model_fn_optimizer(self):
+        """Returns ``model_fn(mode, device, ctx=None) -> spec`` (model.py:326-505): for "train" a
+        dict with the network, loss function, :class:`engine.trainer.Trainer` (Adam +
+        exponential_decay(lr, step, 10000, 0.5)) and the threshold; for "eval"/"predict" the
+        network in inference mode."""
+        def model_fn(mode, device=None, ctx=None):
+            from .parallel.dist import get_context
+            ctx = ctx or get_context()
+            device = torch.device(device) if device is not None else self._device(ctx)
+            net = self.build_network()
+            loss_fn = (lambda out, yy: lovasz_hinge(out, yy))
+            spec = {"mode": mode, "network": net, "loss": loss_fn, "threshold": self.threshold}
+            if mode == TRAIN:
+                schedule = functools.partial(exponential_decay, self.lr, decay_steps=10000,
+                                             decay_rate=0.5, staircase=False)
+                spec["trainer"] = Trainer(net, loss_fn, device, optimizer="adam",
+                                          opt_kwargs=dict(lr=self.lr, lr_schedule=schedule),
+                                          ctx=ctx)
+            else:
+                net.to(device).eval()
+            return spec
+        return model_fn
+
+    def _make_input_fn(self, mode, fold, batch_size, augment, shuffle, device="cpu", rank=0,
+                       world=1):
+        """model.py:285-324: returns ``input_fn() -> iterator of (x, y)`` over the fold's
+        symlinked split (repeating for training, one pass for evaluation)."""
+        def input_fn():
+            imgs, masks = fold_files(self.model_dir, mode, fold)
+            return SegmentationPipeline(imgs, masks, batch_size, augment=augment, shuffle=shuffle,
+                                        repeat=(mode == TRAIN), seed=self.seed + fold,
+                                        device=device, rank=rank, world=world,
+                                        threads=self.loader_threads)
+        return input_fn
+
+    def _make_test_input(self, batch_size, test_directory, tti="none", device="cpu"):
+        """model.py:257-283: returns ``test_input_fn() -> iterator of (x, ids)`` over
+        ``test_directory/*.png`` with one TTA ``transformation`` (the reference's ``tti``
+        argument is the transformation name)."""
+        import glob
+        transformation = tti if isinstance(tti, str) else "none"
+
+        def test_input_fn():
+            images = sorted(glob.glob(os.path.join(test_directory, "*.png")))
+            return TestPipeline(images, batch_size, transformation, device=device,
+                                threads=self.loader_threads)
+        return test_input_fn
+
     @property
     def params(self):
         try:

@@ -137,3 +137,17 @@ def test_xception_facade():
     assert len(b.args) == 2
     s = xception.separable_conv2d_same(32, 64, stride=2)
     assert s(torch.randn(1, 8, 8, 32)).shape == (1, 4, 4, 64)
+
+
+def test_xception_stack_blocks_dense():
+    blocks = [xception.xception_block("entry_flow/block1", [32, 32, 32], "conv", False, False, 1, 2),
+              xception.xception_block("entry_flow/block2", [64, 64, 64], "conv", False, False, 1, 2),
+              xception.xception_block("middle_flow/block1", [64, 64, 64], "sum", False, False, 2, 1)]
+    units, c = xception.stack_blocks_dense(16, blocks, output_stride=2)
+    assert c == 64 and len(units) == 4
+    x = torch.randn(1, 16, 16, 16)
+    for u in units:
+        x = u(x)
+    assert x.shape == (1, 8, 8, 64)  # stride stopped at 2, later strides became dilation
+    with pytest.raises(ValueError):
+        xception.stack_blocks_dense(16, blocks, output_stride=8)

@@ -236,3 +236,21 @@ def test_preprocessing_helpers(tmp_path):
     P.create_symlinks(str(data), md, "train", ["a"], 1)
     assert os.path.islink(os.path.join(md, "train", "images", "fold1", "a.png"))
     P.create_symlinks(str(data), md, "train", ["a"], 1)  # idempotent
+
+
+def test_native_loader_under_host_sanitizers(tmp_path):
+    """ASan+UBSan and TSan builds of the loader stress harness (scripts/sanitize_native.sh)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    rng = np.random.default_rng(0)
+    for i in range(2):
+        Image.fromarray((rng.random((16, 16)) * 255).astype(np.uint8), "L").save(tmp_path / f"i{i}.png")
+        Image.fromarray(((rng.random((16, 16)) > 0.6) * 255).astype(np.uint8), "L").save(tmp_path / f"m{i}.png")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["bash", os.path.join(root, "scripts", "sanitize_native.sh"), str(tmp_path), "10"],
+                       capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, TMPDIR=str(tmp_path)))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("ok ") == 2

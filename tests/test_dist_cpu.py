@@ -124,3 +124,22 @@ def test_gloo_dp_equals_large_batch(tmp_path):
     for _ in range(3):
         tr.train_step(x, y)
     assert torch.allclose(r0, tr.flat.master, atol=1e-5, rtol=1e-4)
+
+
+def test_phase_timer_cpu():
+    import torch
+    from tensorflowdistributedlearning_amd import models
+    from tensorflowdistributedlearning_amd.engine.trainer import Trainer
+    from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy
+    from tensorflowdistributedlearning_amd.data.synthetic import imagenet_batch
+    torch.manual_seed(0)
+    m = models.build("resnet18", num_classes=4, width=8)
+    tr = Trainer(m, softmax_cross_entropy, "cpu", "sgd", dict(lr=0.01), lowp_dtype=None,
+                 profile_phases=True)
+    x, y = imagenet_batch(2, 32, num_classes=4, dtype=torch.float32)
+    for _ in range(2):
+        tr.train_step(x, y)
+    s = tr.timer.summary()
+    assert set(s) == {"forward", "backward", "comm_wait", "optimizer", "step"}
+    assert s["forward"] > 0 and s["backward"] > 0 and abs(s["step"] - sum(
+        s[k] for k in ("forward", "backward", "comm_wait", "optimizer"))) < 1e-6
