@@ -324,7 +324,10 @@ void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int
   TORCH_CHECK(dwt.size(0) * dwt.size(1) <= 49, "depthwise kernel up to 7x7");
   DwArgs a = dw_args(x, dwt, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
   a.dy = BF(dy); a.x = BF(x); a.dw = dwt.data_ptr<float>(); a.db = optfw(db);
-  dwconv_wgrad_launch(a, stream());
+  const int slabs = dwconv_wgrad_slabs(a);
+  Tensor ws;
+  if (slabs > 0) ws = torch::empty({(int64_t)slabs * (a.R * a.S + 1) * a.C}, dwt.options());
+  dwconv_wgrad_launch(a, slabs > 0 ? ws.data_ptr<float>() : nullptr, stream());
 }
 
 // ------------------------------------------------------------------------------------- upsample

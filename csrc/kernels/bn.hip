@@ -318,13 +318,20 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
   }
 }
 
-inline int ew_blocks(long n) {
-  // power-of-two block count (≤ 2048): the grid stride is then a multiple of any power-of-two
-  // channel-vector count ≤ 256, which lets the kernels hoist per-channel coefficients
+inline int ew_blocks(long n, int cvecs = 1) {
+  // block count whose grid stride (blocks·NT vectors) is a multiple of the channel-vector count:
+  // each thread's channel vector is then loop-invariant and the kernels hoist the per-channel
+  // coefficients into registers (C = 728 or 1536 in Xception-41 are not powers of two)
   long b = std::max<long>(1, (n + NT - 1) / NT);
-  int p = 1;
-  while (p < b && p < 2048) p <<= 1;
-  return p;
+  b = std::min<long>(b, 2048);
+  int g = NT, c = std::max(cvecs, 1);
+  while (c) {  // gcd(NT, cvecs)
+    const int t = g % c;
+    g = c;
+    c = t;
+  }
+  const long b0 = std::max(cvecs, 1) / g;
+  return (int)(((b + b0 - 1) / b0) * b0);
 }
 
 }  // namespace
@@ -344,7 +351,7 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
                      int C, bool relu, hipStream_t st) {
   const long n = M * C;
   if (C % 8 == 0) {
-    hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8)), dim3(NT), 0, st, x, coef, res, y,
+    hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, x, coef, res, y,
                        n / 8, C, relu ? 1 : 0);
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
@@ -363,7 +370,7 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          hipStream_t st) {
   const long n = M * C;
   if (C % 8 == 0) {
-    hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(ew_blocks(n / 8)), dim3(NT), 0, st, dy, y, x, coef,
+    hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n / 8, C, 1.f / count, relu);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,

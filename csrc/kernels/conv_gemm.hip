@@ -750,17 +750,21 @@ void conv_wgrad_launch(const ConvArgs& a0, const WgradPlan& p, float* out, bool 
     if (al) launch_cfg<WGRAD, true, false>(a, p.bm, p.bn, (int)tiles, st);
     else launch_cfg<WGRAD, false, false>(a, p.bm, p.bn, (int)tiles, st);
   }
-  const long n = (long)a.M * a.Ng;
+  splitk_reduce_launch((const float*)a.out, out, (long)a.M * a.Ng, splits, accumulate, st);
+}
+
+void splitk_reduce_launch(const float* slab, float* out, long n, int splits, bool accumulate,
+                          hipStream_t st) {
   const long n4 = std::max<long>(1, n / 4);
   if (splits >= 64) {
     hipLaunchKernelGGL(splitk_reduce_kernel<16>, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st,
-                       (const float*)a.out, out, n, splits, accumulate ? 1 : 0);
+                       slab, out, n, splits, accumulate ? 1 : 0);
   } else if (splits >= 8) {
     hipLaunchKernelGGL(splitk_reduce_kernel<4>, dim3((unsigned)((n4 + 63) / 64)), dim3(256), 0, st,
-                       (const float*)a.out, out, n, splits, accumulate ? 1 : 0);
+                       slab, out, n, splits, accumulate ? 1 : 0);
   } else {
     hipLaunchKernelGGL(splitk_reduce_kernel<1>, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st,
-                       (const float*)a.out, out, n, splits, accumulate ? 1 : 0);
+                       slab, out, n, splits, accumulate ? 1 : 0);
   }
 }
 

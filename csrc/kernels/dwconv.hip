@@ -164,6 +164,165 @@ __global__ void __launch_bounds__(NT) dw_wgrad_kernel(DwArgs a, long pix_per_blo
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-oriented kernels for C % 8 == 0 (the model path).  A workgroup owns one output row (fwd) /
+// input row (dgrad) of one channel group: lane = (channel vector, pixel lane), so the R·S filter
+// taps of the lane's 8 channels live in registers for the whole row and there is no per-pixel
+// index division (the generic kernels above divide 64-bit indices per element).
+// ---------------------------------------------------------------------------------------------
+struct RowGeom {
+  int lanes_c, rpp;  // channel-vector lanes per group, pixel lanes
+};
+inline RowGeom row_geom(int cv) {
+  RowGeom g;
+  g.lanes_c = std::min(cv, NT);
+  g.rpp = std::max(1, NT / g.lanes_c);
+  return g;
+}
+
+template <int RS>
+__global__ void __launch_bounds__(NT) dw_fwd_rows(DwArgs a, int lanes_c, int rpp) {
+  const int cv = a.C / 8;
+  const int t = threadIdx.x, lc = t % lanes_c, pl = t / lanes_c;
+  const int cvi = lc + blockIdx.y * lanes_c;
+  if (pl >= rpp || cvi >= cv) return;
+  const int c = cvi * 8;
+  const int row = blockIdx.x, n = row / a.Ho, ho = row - n * a.Ho;
+  float wv[RS][8], bias[8];
+#pragma unroll
+  for (int k = 0; k < RS; ++k) unpack8(*(const uint4*)(a.w + (long)k * a.C + c), wv[k]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bias[j] = a.bias ? a.bias[c + j] : 0.f;
+  const bf16_t* xn = a.x + (long)n * a.H * a.W * a.C + c;
+  bf16_t* yrow = a.out + ((long)row * a.Wo) * a.C + c;
+  for (int wo = pl; wo < a.Wo; wo += rpp) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = bias[j];
+#pragma unroll
+    for (int k = 0; k < RS; ++k) {
+      const int r = k / a.S, s = k - r * a.S;
+      const int hi = ho * a.sh - a.ph + r * a.dh, wi = wo * a.sw - a.pw + s * a.dwl;
+      if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) continue;
+      float xv[8];
+      unpack8(*(const uint4*)(xn + ((long)hi * a.W + wi) * a.C), xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += xv[j] * wv[k][j];
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
+    }
+    *(uint4*)(yrow + (long)wo * a.C) = pack8(acc);
+  }
+}
+
+template <int RS>
+__global__ void __launch_bounds__(NT) dw_dgrad_rows(DwArgs a, int lanes_c, int rpp) {
+  const int cv = a.C / 8;
+  const int t = threadIdx.x, lc = t % lanes_c, pl = t / lanes_c;
+  const int cvi = lc + blockIdx.y * lanes_c;
+  if (pl >= rpp || cvi >= cv) return;
+  const int c = cvi * 8;
+  const int row = blockIdx.x, n = row / a.H, h = row - n * a.H;
+  float wv[RS][8];
+#pragma unroll
+  for (int k = 0; k < RS; ++k) unpack8(*(const uint4*)(a.w + (long)k * a.C + c), wv[k]);
+  const bf16_t* gn = a.dy + (long)n * a.Ho * a.Wo * a.C + c;
+  bf16_t* xrow = a.out + ((long)row * a.W) * a.C + c;
+  for (int w = pl; w < a.W; w += rpp) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < RS; ++k) {
+      const int r = k / a.S, s = k - r * a.S;
+      int th = h + a.ph - r * a.dh, tw = w + a.pw - s * a.dwl;
+      if (th < 0 || tw < 0) continue;
+      if (a.sh > 1) {
+        if (th % a.sh) continue;
+        th /= a.sh;
+      }
+      if (a.sw > 1) {
+        if (tw % a.sw) continue;
+        tw /= a.sw;
+      }
+      if (th >= a.Ho || tw >= a.Wo) continue;
+      float gv[8];
+      unpack8(*(const uint4*)(gn + ((long)th * a.Wo + tw) * a.C), gv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += gv[j] * wv[k][j];
+    }
+    *(uint4*)(xrow + (long)w * a.C) = pack8(acc);
+  }
+}
+
+// wgrad: workgroup = a range of output rows × one channel group; R·S·8 (+8 bias) fp32 partials per
+// lane, combined over pixel lanes in LDS and written as this workgroup's slab row — no atomics
+// (the generic kernel's per-block atomics all hit the same R·S·C addresses); the slabs are then
+// summed by the split-K reduction kernel.
+template <int RS>
+__global__ void __launch_bounds__(NT) dw_wgrad_rows(DwArgs a, int lanes_c, int rpp,
+                                                    int rows_per_block, float* ws_w, float* ws_b) {
+  const int cv = a.C / 8;
+  const int t = threadIdx.x, lc = t % lanes_c, pl = t / lanes_c;
+  const int cvi = lc + blockIdx.y * lanes_c;
+  const bool active = pl < rpp && cvi < cv;
+  const int c = cvi * 8;
+  const int rows = a.N * a.Ho;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  float acc[RS][8], db[8];
+#pragma unroll
+  for (int k = 0; k < RS; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db[j] = 0.f;
+  if (active) {
+    for (int row = r0; row < r1; ++row) {
+      const int n = row / a.Ho, ho = row - n * a.Ho;
+      const bf16_t* grow = a.dy + ((long)row * a.Wo) * a.C + c;
+      const bf16_t* xn = a.x + (long)n * a.H * a.W * a.C + c;
+      for (int wo = pl; wo < a.Wo; wo += rpp) {
+        float gv[8];
+        unpack8(*(const uint4*)(grow + (long)wo * a.C), gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db[j] += gv[j];
+#pragma unroll
+        for (int k = 0; k < RS; ++k) {
+          const int r = k / a.S, s = k - r * a.S;
+          const int hi = ho * a.sh - a.ph + r * a.dh, wi = wo * a.sw - a.pw + s * a.dwl;
+          if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) continue;
+          float xv[8];
+          unpack8(*(const uint4*)(xn + ((long)hi * a.W + wi) * a.C), xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[k][j] += gv[j] * xv[j];
+        }
+      }
+    }
+  }
+  __shared__ float red[NT][9];
+  const long slab_w = (long)blockIdx.x * RS * a.C, slab_b = (long)blockIdx.x * a.C;
+#pragma unroll
+  for (int k = 0; k <= RS; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t][j] = (k < RS) ? acc[k < RS ? k : 0][j] : db[j];
+    __syncthreads();
+    if (pl == 0 && cvi < cv) {
+      float sum[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum[j] = 0.f;
+      for (int q = 0; q < rpp; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum[j] += red[q * lanes_c + lc][j];
+      float* dst = (k < RS) ? ws_w + slab_w + (long)k * a.C + c : ws_b + slab_b + c;
+      *(float4*)dst = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      *(float4*)(dst + 4) = make_float4(sum[4], sum[5], sum[6], sum[7]);
+    }
+    __syncthreads();
+  }
+}
+
 template <int V>
 void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
   const int cv = a.C / V;
@@ -189,22 +348,57 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
-  if (a.C % 8 == 0)
+  if (a.C % 8 == 0 && a.R * a.S == 9) {
+    const RowGeom g = row_geom(a.C / 8);
+    dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
+    hipLaunchKernelGGL(dw_fwd_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp);
+  } else if (a.C % 8 == 0) {
     hipLaunchKernelGGL(dw_fwd_kernel<8>, dim3(blocks_for(outs / 8)), dim3(NT), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL(dw_fwd_kernel<1>, dim3(blocks_for(outs)), dim3(NT), 0, st, a);
+  }
 }
 
 void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
-  if (a.C % 8 == 0)
+  if (a.C % 8 == 0 && a.R * a.S == 9) {
+    const RowGeom g = row_geom(a.C / 8);
+    dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));
+    hipLaunchKernelGGL(dw_dgrad_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp);
+  } else if (a.C % 8 == 0) {
     hipLaunchKernelGGL(dw_dgrad_kernel<8>, dim3(blocks_for(ins / 8)), dim3(NT), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL(dw_dgrad_kernel<1>, dim3(blocks_for(ins)), dim3(NT), 0, st, a);
+  }
 }
 
-void dwconv_wgrad_launch(const DwArgs& a, hipStream_t st) {
+// slab rows for the row-oriented wgrad (0: generic atomic kernel)
+int dwconv_wgrad_slabs(const DwArgs& a) {
+  if (!(a.C % 8 == 0 && a.R * a.S == 9)) return 0;
+  const int rows = a.N * a.Ho;
+  const RowGeom g = row_geom(a.C / 8);
+  const int groups = cdiv(a.C / 8, g.lanes_c);
+  const int target = std::max(1, 1024 / groups);  // ≈4 workgroups per CU
+  const int rpb = std::max(1, cdiv(rows, target));
+  return cdiv(rows, rpb);
+}
+
+void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st) {
   if (a.R * a.S > 49) return;  // host checks reject this
+  const int slabs = dwconv_wgrad_slabs(a);
+  if (slabs > 0 && ws != nullptr) {
+    const RowGeom g = row_geom(a.C / 8);
+    const int rows = a.N * a.Ho;
+    const int rpb = cdiv(rows, slabs);
+    dim3 grid((unsigned)slabs, (unsigned)cdiv(a.C / 8, g.lanes_c));
+    float* ws_w = ws;
+    float* ws_b = ws + (long)slabs * 9 * a.C;
+    hipLaunchKernelGGL(dw_wgrad_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp, rpb, ws_w,
+                       ws_b);
+    splitk_reduce_launch(ws_w, a.dw, 9L * a.C, slabs, true, st);
+    if (a.db) splitk_reduce_launch(ws_b, a.db, a.C, slabs, true, st);
+    return;
+  }
   if (a.C % 8 == 0 && (a.R * a.S == 9 || a.R * a.S == 1))
     wgrad_dispatch<8>(a, st);
   else

@@ -136,7 +136,12 @@ struct DwArgs {
 };
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
 void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);
-void dwconv_wgrad_launch(const DwArgs& a, hipStream_t st);
+int dwconv_wgrad_slabs(const DwArgs& a);  // row-slab count of the fast wgrad (0: generic)
+// adds dW / db into a.dw / a.db; ws: slabs·(R·S + 1)·C floats when dwconv_wgrad_slabs(a) > 0
+void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st);
+// out[i] (+)= Σ_z slab[z·n + i]  (split-K / slab reduction, conv_gemm.hip)
+void splitk_reduce_launch(const float* slab, float* out, long n, int splits, bool accumulate,
+                          hipStream_t st);
 
 // upsample (TF1 legacy bilinear with symmetric pad) -----------------------------------------
 void upsample_fwd_launch(const bf16_t* x, bf16_t* y, const int* ih, const float* wh,

@@ -273,7 +273,9 @@ def test_sgd_adam(gpu):
 
 
 @pytest.mark.parametrize("Cn,rate,stride,relu", [(64, 2, 1, True), (1024, 8, 1, True),
-                                                 (16, 1, 2, False), (1, 1, 1, False)])
+                                                 (16, 1, 2, False), (1, 1, 1, False),
+                                                 (728, 1, 1, False), (2048, 2, 1, True),
+                                                 (128, 1, 2, True), (40, 1, 1, False)])
 def test_depthwise(gpu, Cn, rate, stride, relu):
     torch.manual_seed(10)
     from tensorflowdistributedlearning_amd.models.layers import resolve_padding
