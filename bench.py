@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--fp8", action="store_true",
+                    help="fp8 (OCP e4m3, per-tensor scales) forward GEMMs on the CDNA4 "
+                         "16x16x128 MFMA for every eligible conv; backward stays bf16")
     ap.add_argument("--profile-phases", action="store_true",
                     help="also print per-phase step times (forward/backward/comm_wait/optimizer, "
                          "device events) to stderr")
@@ -75,13 +78,16 @@ def main():
     else:
         per_gpu = args.batch or 256
         model = models.build(args.model, num_classes=1000)
+        if args.fp8:
+            models.enable_fp8(model)
         tr = Trainer(model, softmax_cross_entropy, dev, "sgd",
                      dict(lr=args.lr, momentum=0.9, weight_decay=5e-5), ctx=ctx,
                      bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
                      profile_phases=args.profile_phases)
         x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank)
-        metric = METRIC if args.model == "resnet50" and args.image_size == 224 else \
-            f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} bf16"
+        metric = METRIC if args.model == "resnet50" and args.image_size == 224 and not args.fp8 \
+            else (f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} "
+                  f"{'fp8 (e4m3 fwd GEMMs, bf16 bwd)' if args.fp8 else 'bf16'}")
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "optimizer": "sgd_momentum", "loss": "softmax_ce"}
@@ -121,7 +127,8 @@ def main():
             "baseline": ("BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
                          "ResNet-50 number)" if args.model != "deeplab_ref" else
                          "BASELINE.md measured 90.7 img/s on 2 GPUs, scaled per GPU"),
-            "dtype": "bf16", "data": "synthetic (device-resident random batch, random-init weights)",
+            "dtype": "fp8e4m3-fwd/bf16-bwd" if getattr(args, "fp8", False) else "bf16",
+            "data": "synthetic (device-resident random batch, random-init weights)",
             "config": cfg}), flush=True)
     shutdown()
 

@@ -73,6 +73,54 @@ void conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::opt
   conv_fwd_launch(a, stream());
 }
 
+// fp8 (e4m3) forward conv: x8 [N,H,W,C] and w8 [K,R,S,C] as 1-byte tensors, sx / sw fp32 [1]
+void conv_fwd_fp8(Tensor x8, Tensor w8, Tensor y, c10::optional<Tensor> stats, Tensor sx, Tensor sw_,
+                  int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu) {
+  TORCH_CHECK(x8.is_cuda() && w8.is_cuda() && x8.element_size() == 1 && w8.element_size() == 1,
+              "fp8 operands expected");
+  TORCH_CHECK(x8.is_contiguous() && w8.is_contiguous(), "contiguous operands expected");
+  CHECK_T(y, torch::kBFloat16);
+  CHECK_T(sx, torch::kFloat32);
+  CHECK_T(sw_, torch::kFloat32);
+  TORCH_CHECK(x8.size(3) == w8.size(3) && x8.size(3) % 16 == 0, "fp8 conv needs C % 16 == 0");
+  ConvArgs a = conv_args(x8, w8, x8.size(0), x8.size(1), x8.size(2), x8.size(3), w8.size(0),
+                         w8.size(1), w8.size(2), sh, sw, ph, pw, dh, dw, y.size(1), y.size(2));
+  TORCH_CHECK(y.size(0) == a.N && y.size(3) == a.K && a.K % 8 == 0, "output shape mismatch");
+  a.x = (const bf16_t*)x8.data_ptr(); a.w = (const bf16_t*)w8.data_ptr(); a.out = y.data_ptr();
+  a.x_bytes = (uint32_t)x8.numel(); a.w_bytes = (uint32_t)w8.numel(); a.out_bytes = nbytes32(y);
+  TORCH_CHECK(x8.numel() < (1LL << 32) && w8.numel() < (1LL << 32), "tensor too large");
+  a.stats = optfw(stats);
+  if (a.stats) TORCH_CHECK(stats->numel() == 2 * a.K, "stats must be [2, K]");
+  a.scale_x = sx.data_ptr<float>(); a.scale_w = sw_.data_ptr<float>();
+  a.M = a.N * a.Ho * a.Wo; a.Ng = a.K; a.Kg = a.R * a.S * a.C; a.ldc = a.K; a.relu = relu;
+  if (a.M == 0) return;
+  conv_fwd_fp8_launch(a, stream());
+}
+
+void fp8_amax(Tensor x, Tensor amax) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(amax, torch::kFloat32);
+  TORCH_CHECK(x.numel() % 8 == 0, "numel % 8");
+  fp8_amax_launch(BF(x), x.numel(), amax.data_ptr<float>(), stream());
+}
+
+void fp8_quantize(Tensor x, Tensor amax, Tensor scale, Tensor y8) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(amax, torch::kFloat32);
+  CHECK_T(scale, torch::kFloat32);
+  TORCH_CHECK(y8.is_cuda() && y8.element_size() == 1 && y8.is_contiguous() && y8.numel() == x.numel());
+  TORCH_CHECK(x.numel() % 16 == 0, "numel % 16");
+  fp8_quantize_launch(BF(x), x.numel(), amax.data_ptr<float>(), scale.data_ptr<float>(),
+                      (uint8_t*)y8.data_ptr(), stream());
+}
+
+void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
+  TORCH_CHECK(y8.is_cuda() && y8.element_size() == 1 && y8.is_contiguous());
+  CHECK_T(out, torch::kFloat32);
+  fp8_dequantize_launch((const uint8_t*)y8.data_ptr(), y8.numel(), scale.data_ptr<float>(),
+                        out.data_ptr<float>(), stream());
+}
+
 void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                 int64_t dh, int64_t dw, bool accumulate) {
   CHECK_T(dy, torch::kBFloat16);
@@ -136,12 +184,26 @@ void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor>
                      (float)decay, (float)eps, training, stream());
 }
 
-void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu) {
+void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu,
+              c10::optional<Tensor> y8, c10::optional<Tensor> amax_prev,
+              c10::optional<Tensor> scale_out, c10::optional<Tensor> amax_out) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   CHECK_T(coef, torch::kFloat32);
   const int64_t C = x.size(-1);
-  bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu, stream());
+  uint8_t* y8p = nullptr;
+  const bool fp8 = amax_out.has_value() && amax_out->defined();
+  if (fp8) {
+    TORCH_CHECK(C % 8 == 0, "fp8 side output needs C % 8 == 0");
+    TORCH_CHECK(amax_prev.has_value() && amax_prev->defined(), "amax_prev required");
+    if (y8.has_value() && y8->defined()) {
+      TORCH_CHECK(y8->element_size() == 1 && y8->numel() == x.numel() && y8->is_contiguous());
+      y8p = (uint8_t*)y8->data_ptr();
+    }
+  }
+  bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu,
+                  stream(), y8p, fp8 ? amax_prev->data_ptr<float>() : nullptr,
+                  fp8 ? optfw(scale_out) : nullptr, fp8 ? amax_out->data_ptr<float>() : nullptr);
 }
 
 void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, int64_t relu) {
@@ -432,9 +494,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
         py::arg("accumulate") = false);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_fwd_fp8", &conv_fwd_fp8);
+  m.def("fp8_amax", &fp8_amax);
+  m.def("fp8_quantize", &fp8_quantize);
+  m.def("fp8_dequantize", &fp8_dequantize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("res"), py::arg("y"),
+        py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_prev") = py::none(),
+        py::arg("scale_out") = py::none(), py::arg("amax_out") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("relu_bwd", &relu_bwd);

@@ -184,11 +184,31 @@ __global__ void finalize_kernel(const float* __restrict__ stats, float* __restri
 // y = act(x·scale + shift [+ res]).  When the grid stride is a multiple of the channel-vector
 // count (always for power-of-two C ≤ 2048) each thread's channel vector is loop-invariant, so its
 // 16 coefficients are loaded once into registers.
+// Optional fp8 side output (delayed scaling, fp8 forward convs): y8 = e4m3(sat(y·448/amax_prev))
+// in the same pass, scale_out = amax_prev/448 for the consumer GEMM, and this step's |y|max into
+// amax_out (the next step's scale).  y8 is skipped while amax_prev is still 0 (first step).
+__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
 __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict__ x,
                                                        const float* __restrict__ coef,
                                                        const bf16_t* __restrict__ res,
                                                        bf16_t* __restrict__ y, long nvec, int C,
-                                                       int relu) {
+                                                       int relu, uint8_t* __restrict__ y8,
+                                                       const float* __restrict__ amax_prev,
+                                                       float* __restrict__ scale_out,
+                                                       float* __restrict__ amax_out) {
+  float inv8 = 0.f, vmax = 0.f;
+  bool emit8 = false;
+  if (amax_out) {
+    const float ap = *amax_prev;
+    emit8 = y8 != nullptr && ap > 0.f;
+    inv8 = ap > 0.f ? 448.f / ap : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = ap / 448.f;
+  }
   const int cvecs = C >> 3;
   const long stride = (long)gridDim.x * NT;
   const bool hoist = (stride % cvecs) == 0;
@@ -219,7 +239,26 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
-    ((uint4*)y)[i] = pack8(v);
+    const uint4 packed = pack8(v);
+    ((uint4*)y)[i] = packed;
+    if (amax_out) {
+      float q[8];
+      unpack8(packed, q);  // quantise the stored bf16 values (what the bf16 path would read)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vmax = fmaxf(vmax, fabsf(q[j]));
+      if (emit8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) q[j] = fminf(fmaxf(q[j] * inv8, -448.f), 448.f);
+        uint2 o;
+        o.x = e4m3x4(q[0], q[1], q[2], q[3]);
+        o.y = e4m3x4(q[4], q[5], q[6], q[7]);
+        ((uint2*)y8)[i] = o;
+      }
+    }
+  }
+  if (amax_out) {
+    vmax = wave_max(vmax);
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)amax_out, __float_as_uint(vmax));
   }
 }
 
@@ -348,11 +387,12 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 }
 
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
-                     int C, bool relu, hipStream_t st) {
+                     int C, bool relu, hipStream_t st, uint8_t* y8, const float* amax_prev,
+                     float* scale_out, float* amax_out) {
   const long n = M * C;
   if (C % 8 == 0) {
     hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, x, coef, res, y,
-                       n / 8, C, relu ? 1 : 0);
+                       n / 8, C, relu ? 1 : 0, y8, amax_prev, scale_out, amax_out);
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
                        C, relu ? 1 : 0);

@@ -74,7 +74,7 @@ struct Tile {
   int split;      // WGRAD split index
 };
 
-template <int MODE, int BM, int BN>
+template <int MODE, int BM, int BN, int KS = BK>
 __device__ __forceinline__ Tile tile_of(const ConvArgs& a, int t) {
   Tile T;
   const int ntn = (a.Ng + BN - 1) / BN;
@@ -107,7 +107,7 @@ __device__ __forceinline__ Tile tile_of(const ConvArgs& a, int t) {
     T.bm0 = (local / ntn) * BM;
     T.bn0 = (local % ntn) * BN;
   }
-  const int nkt = (T.Kgc + BK - 1) / BK;
+  const int nkt = (T.Kgc + KS - 1) / KS;  // KS: GEMM K per step (64 bf16 / 128 fp8)
   if constexpr (MODE == WGRAD) {
     T.kt0 = T.split * a.kps;
     T.kt1 = min(nkt, T.kt0 + a.kps);

@@ -59,6 +59,19 @@ __device__ __forceinline__ bf16x8 lds_read_mc(uint32_t tile, int krow, int col) 
   uint4 v = make_uint4(lo[0], lo[1], hi[0], hi[1]);
   return __builtin_bit_cast(bf16x8, v);
 }
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// fp8 A/B fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds bytes k = 32·(l>>4) … +31 of
+// row l&15 (any k permutation applied to both operands is exact; tools/mfma_fp8_layout.hip)
+__device__ __forceinline__ i32x8 lds_read_kc_f8(uint32_t tile, int row, int g) {
+  uint4 lo, hi;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(tile + (uint32_t)kc_off(row, 2 * g)) : "memory");
+  asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(tile + (uint32_t)kc_off(row, 2 * g + 1)) : "memory");
+  i32x8 v;
+  v[0] = (int)lo.x; v[1] = (int)lo.y; v[2] = (int)lo.z; v[3] = (int)lo.w;
+  v[4] = (int)hi.x; v[5] = (int)hi.y; v[6] = (int)hi.z; v[7] = (int)hi.w;
+  return v;
+}
+
 __device__ __forceinline__ void lgkm_wait0() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -69,8 +82,16 @@ __device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_base, 16, voff, 0, 0, 0);
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, bool FASTK>
+template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, bool FASTK,
+          bool FP8 = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  // FP8 (FWD only): operands are OCP e4m3 bytes, a K-step is 128 deep (one 128-B LDS row per
+  // tile row, as for bf16), fragments are 32 B and feed v_mfma_scale_f32_16x16x128_f8f6f4 with
+  // unit E8M0 block scales; the per-tensor scales s_x·s_w are applied in the epilogue.
+  static_assert(!FP8 || MODE == FWD, "fp8 forward only");
+  constexpr int ESZ = FP8 ? 1 : 2;         // bytes per element
+  constexpr int EPC = 16 / ESZ;            // elements per 16-B chunk
+  constexpr int KSTEP = 128 / ESZ;         // GEMM K per step (one 128-B LDS row)
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
   constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE != FWD);
@@ -194,7 +215,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   auto issue_step = [&](const Tile& T, int kt, int slot) {
     char* As = smem + slot * STAGE;
     char* Bs = As + A_BYTES;
-    const int kb = kt * BK;
+    const int kb = kt * KSTEP;
     if constexpr (MODE == FWD) {
       // FASTK (C % 64 == 0): the K-step is one filter tap (pos_r, pos_s) and channels
       // pos_c0 … +63, advanced incrementally by advance_load (no division in the loop)
@@ -203,10 +224,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
       for (int j = 0; j < IA; ++j) {
         const int lc = kc_lchunk(j);
-        int r = tap_r, s = tap_s, c = c0 + lc * 8;
+        int r = tap_r, s = tap_s, c = c0 + lc * EPC;
         bool kv = kb < a.Kg;
         if constexpr (!FASTK) {
-          const int k = kb + lc * 8;
+          const int k = kb + lc * EPC;
           kv = k < a.Kg;
           const int rs = fdiv(k, a.fd_C);
           c = k - rs * a.C;
@@ -215,14 +236,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
         const int hi = a_p0[j] + r * a.dh, wi = a_p1[j] + s * a.dw;
         const bool v = kv && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const uint32_t off = (uint32_t)(a_base[j] + (hi * a.W + wi) * a.C + c) * 2u;
+        const uint32_t off = (uint32_t)(a_base[j] + (hi * a.W + wi) * a.C + c) * (uint32_t)ESZ;
         dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
       }
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
-        const int k = kbase + kc_lchunk(j) * 8;
+        const int k = kbase + kc_lchunk(j) * EPC;
         const bool v = k < a.Kg && b_base[j] >= 0;
-        dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_base[j] + k) * 2u : OOB);
+        dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_base[j] + k) * (uint32_t)ESZ : OOB);
       }
     } else if constexpr (MODE == DGRAD) {
       const int c = T.cls;
@@ -342,6 +363,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
 
   // lane holds C[m = bm0 + wm*TM + rm*16 + (lane&15)][n = bn0 + wn*TN + rn*16 + (lane>>4)*4 + i]
+  const float out_scale = FP8 ? (*a.scale_x) * (*a.scale_w) : 1.f;
   auto epilogue = [&](const Tile& T) {
     if constexpr (MODE == WGRAD) {
       const uint32_t slab0 = (uint32_t)T.split * (uint32_t)(a.M * a.Ng);
@@ -388,7 +410,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float t = acc[rm][rn][i] + bv[i] + prev[i];
+            float t = acc[rm][rn][i] * out_scale + bv[i] + prev[i];
             if (a.relu) t = fmaxf(t, 0.f);
             h[i] = f2bf(t);
             v[i] = bf2f(h[i]);
@@ -461,7 +483,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       if (T.bn0 >= a.Ng) {
         T.bn0 = 0;
         T.bm0 += BM;
-        if (T.bm0 >= T.Mc) T = tile_of<MODE, BM, BN>(a, t);
+        if (T.bm0 >= T.Mc) T = tile_of<MODE, BM, BN, KSTEP>(a, t);
       }
     }
     (void)ntn_c;
@@ -469,7 +491,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 
   // ---- flat (tile, K-step) pipeline over this workgroup's tiles ----
   int lt = tile_begin;
-  Tile LT = tile_of<MODE, BM, BN>(a, lt);
+  Tile LT = tile_of<MODE, BM, BN, KSTEP>(a, lt);
   int lkt = LT.kt0;
   bool lmore = LT.bm0 < LT.Mc;
   if (!lmore) return;
@@ -479,7 +501,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     if (lkt + 1 < LT.kt1) {
       ++lkt;
       if constexpr (FASTK && MODE != WGRAD) {
-        pos_c0 += BK;
+        pos_c0 += KSTEP;
         if (pos_c0 >= pos_C) {
           pos_c0 = 0;
           const int Sl = MODE == FWD ? a.S : a.cls_Tw[LT.cls];
@@ -539,6 +561,46 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     if (!no_barrier) raw_barrier();
   };
 
+  if constexpr (FP8) {
+    // fp8: one 128-deep MFMA per fragment pair; straight ring loop (wait → barrier → refill the
+    // slot every wave has finished → read fragments → MFMAs)
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (lmore) issue_next();
+    zero_acc();
+    while (inflight > 0) {
+      ring_wait_barrier(inflight - 1);
+      if (lmore) issue_next();
+      const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;
+      i32x8 a8[RM], b8[RN];
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) a8[rm] = lds_read_kc_f8(As, wm * TM + rm * 16 + (lane & 15), lane >> 4);
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) b8[rn] = lds_read_kc_f8(Bs, wn * TN + rn * 16 + (lane & 15), lane >> 4);
+      lgkm_wait0();
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn)
+          acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b8[rn], a8[rm], acc[rm][rn],
+                                                                         0, 0, 0, 127, 0, 127);
+      slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;
+      --inflight;
+      if (ckt + 1 >= CT.kt1) {
+        epilogue(CT);
+        epi = true;
+        zero_acc();
+        if (inflight > 0) {
+          ++ct;
+          next_tile(CT, ct);
+          ckt = CT.kt0;
+        }
+      } else {
+        ++ckt;
+      }
+    }
+    flush_stats(CT.bn0);
+    return;
+  }
   // Software pipeline across K-steps (one barrier per step):
   //   reads(t, k0..31) ready → issue reads(t, k32..63) → MFMA(t, first half) → lgkm(0) →
   //   [wait DMA(t+1), barrier, DMA(t+S) into the slot just drained, reads(t+1, k0..31)] →
@@ -599,9 +661,10 @@ constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
   return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, bool FK>
+template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, bool FK,
+          bool F8 = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK>;
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8>;
   constexpr int lds = lds_bytes(BM, BN, WM, ST);
   static bool attr = false;
   if (!attr) {
@@ -648,6 +711,36 @@ int persistent_tpb(long tiles) {
 }
 
 }  // namespace
+
+// fp8 forward: LDS-DMA kernel only (C % 16 == 0: a 16-B chunk never crosses a filter tap)
+void conv_fwd_fp8_launch(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  a.dbg = 0;
+  set_fastdivs(a);
+  const int cfg = a.Ng >= 128 ? 0 : 1;
+  const GCfg& g = cfg_of(cfg);
+  const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
+  a.ncls = 1;
+  a.splits = 1;
+  a.tpb = std::max(1, persistent_tpb(ntm * ntn));
+  a.tpb = (int)std::min<long>(a.tpb, ntm);
+  const long groups = (ntm + a.tpb - 1) / a.tpb;
+  const int blocks = (int)(groups * ntn);
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+  const bool fk = a.C % 128 == 0, stats = a.stats != nullptr;
+#define TDL_F8(ST, FK)                                                              \
+  do {                                                                              \
+    if (cfg == 0) launch_g<FWD, 256, 128, 4, 2, 3, ST, false, FK, true>(a, blocks, st); \
+    else launch_g<FWD, 256, 64, 4, 1, 3, ST, false, FK, true>(a, blocks, st);       \
+  } while (0)
+  if (fk) {
+    if (stats) TDL_F8(true, true); else TDL_F8(false, true);
+  } else {
+    if (stats) TDL_F8(true, false); else TDL_F8(false, false);
+  }
+#undef TDL_F8
+}
 
 // Mode selection: 0 = register-staged kernel only, 1 = glds for eligible problems (default),
 // 2 = glds whenever aligned (testing).

@@ -1,0 +1,96 @@
+// fp8 (OCP e4m3fn, gfx950) quantisation with per-tensor scaling for the fp8 forward convolution
+// (ResNet-152 fp8 weights/activations on the CDNA4 fp8 MFMA).
+//
+//   amax      : |x|max over a bf16 tensor → fp32 (atomicMax on the IEEE bits: valid for x ≥ 0)
+//   quantize  : scale = amax / 448 (E4M3 max normal), y8 = sat(x / scale) as e4m3; the scale is
+//               also written to device memory for the GEMM epilogue (acc · s_x · s_w)
+//   dequantize: tests / debugging
+// Everything stays on the device: no host synchronisation for the scale.
+#include "common.h"
+#include "kernels.h"
+
+namespace tdl {
+namespace {
+
+constexpr int NT = 256;
+constexpr float E4M3_MAX = 448.f;
+
+__global__ void __launch_bounds__(NT) amax_kernel(const bf16_t* __restrict__ x, long nvec,
+                                                  float* __restrict__ amax) {
+  float m = 0.f;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nvec; i += (long)gridDim.x * NT) {
+    float v[8];
+    unpack8(((const uint4*)x)[i], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
+  }
+  m = wave_max(m);
+  __shared__ float red[NT / 64];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = red[0];
+    for (int w = 1; w < NT / 64; ++w) b = fmaxf(b, red[w]);
+    atomicMax((unsigned int*)amax, __float_as_uint(b));
+  }
+}
+
+__device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+// 16 elements per thread: two 16-B bf16 vectors in, one 16-B e4m3 vector out
+__global__ void __launch_bounds__(NT) quantize_kernel(const bf16_t* __restrict__ x, long n16,
+                                                      const float* __restrict__ amax,
+                                                      float* __restrict__ scale_out,
+                                                      uint8_t* __restrict__ y) {
+  const float am = fmaxf(*amax, 1e-12f);
+  const float inv = E4M3_MAX / am;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = am / E4M3_MAX;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n16; i += (long)gridDim.x * NT) {
+    float v[16];
+    unpack8(((const uint4*)x)[2 * i], v);
+    unpack8(((const uint4*)x)[2 * i + 1], v + 8);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = fminf(fmaxf(v[j] * inv, -E4M3_MAX), E4M3_MAX);
+    uint4 o;
+    o.x = pack4_e4m3(v[0], v[1], v[2], v[3]);
+    o.y = pack4_e4m3(v[4], v[5], v[6], v[7]);
+    o.z = pack4_e4m3(v[8], v[9], v[10], v[11]);
+    o.w = pack4_e4m3(v[12], v[13], v[14], v[15]);
+    ((uint4*)y)[i] = o;
+  }
+}
+
+__global__ void dequantize_kernel(const uint8_t* __restrict__ y, long n, const float* __restrict__ scale,
+                                  float* __restrict__ out) {
+  const float s = *scale;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int w = (int)y[i];
+    out[i] = __builtin_amdgcn_cvt_f32_fp8(w, 0) * s;
+  }
+}
+
+inline int grid_for(long n) { return (int)std::min<long>(4096, std::max<long>(1, (n + NT - 1) / NT)); }
+
+}  // namespace
+
+void fp8_amax_launch(const bf16_t* x, long n, float* amax, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, st, x, n / 8, amax);
+}
+
+void fp8_quantize_launch(const bf16_t* x, long n, const float* amax, float* scale_out, uint8_t* y,
+                         hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n / 16)), dim3(NT), 0, st, x, n / 16, amax,
+                     scale_out, y);
+}
+
+void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(dequantize_kernel, dim3(grid_for(n)), dim3(NT), 0, st, y, n, scale, out);
+}
+
+}  // namespace tdl

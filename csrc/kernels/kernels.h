@@ -39,6 +39,8 @@ struct ConvArgs {
   int M, Ng, Kg;     // GEMM dims
   int ldc;
   int relu;
+  const float* scale_x;  // fp8 FWD: per-tensor scales of x and w (device scalars)
+  const float* scale_w;
   int beta;          // DGRAD: 1 = accumulate into the existing dx (residual-gradient join)
   uint32_t x_bytes, w_bytes, dy_bytes, out_bytes;  // buffer-descriptor ranges (OOB -> 0 / dropped)
   int kps;           // WGRAD: K-steps per split
@@ -73,6 +75,12 @@ bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
 bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st);
 bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);
 void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
+// fp8 (OCP e4m3) forward conv: a.x / a.w point at e4m3 bytes, a.scale_x / a.scale_w at their fp32 scales
+void conv_fwd_fp8_launch(const ConvArgs& a, hipStream_t st);
+void fp8_amax_launch(const bf16_t* x, long n, float* amax, hipStream_t st);
+void fp8_quantize_launch(const bf16_t* x, long n, const float* amax, float* scale_out, uint8_t* y,
+                         hipStream_t st);
+void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st);
 void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st);
 
 // batch norm ---------------------------------------------------------------------------------
@@ -81,7 +89,9 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
                         float* rmean, float* rvar, int C, float count, float decay, float eps,
                         bool training, hipStream_t st);
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
-                     int C, bool relu, hipStream_t st);
+                     int C, bool relu, hipStream_t st, uint8_t* y8 = nullptr,
+                     const float* amax_prev = nullptr, float* scale_out = nullptr,
+                     float* amax_out = nullptr);
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                           float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,

@@ -16,11 +16,23 @@ _REGISTRY = {
 }
 
 
+def enable_fp8(model):
+    """fp8 (e4m3) forward GEMMs for every bias-free conv whose input channels are a multiple of 16
+    (the 3-channel stem and biased heads stay bf16); backward stays bf16.  Returns the count."""
+    from .layers import Conv2d
+    n = 0
+    for m in model.modules():
+        if isinstance(m, Conv2d) and m.bias is None and m._cin_store % 16 == 0:
+            m.fp8 = True
+            n += 1
+    return n
+
+
 def build(name, **kw):
     if name not in _REGISTRY:
         raise KeyError(f"unknown model {name}; have {sorted(_REGISTRY)}")
     return _REGISTRY[name](**kw)
 
 
-__all__ = ["ResNet", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
+__all__ = ["enable_fp8", "ResNet", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
            "DeepLabResNet", "Xception41", "xception_41", "FlatParams", "build"]

@@ -148,6 +148,20 @@ class Conv2d(nn.Module):
             self._geom_cache[(H, W)] = g
         return g
 
+    fp8 = False  # set by models.enable_fp8: e4m3 forward GEMM (ops/fp8.py)
+
+    def fp8_weight(self, w_lowp):
+        """e4m3 copy of the weight + its scale, re-quantised once per optimizer step."""
+        from ..ops.fp8 import quantize_e4m3
+        from .params import version
+        cache = getattr(self, "_fp8_cache", None)
+        v = version()
+        if cache is None or cache[0] != v or cache[1].device != w_lowp.device:
+            w8, sw = quantize_e4m3(w_lowp)
+            cache = (v, w8, sw)
+            self._fp8_cache = cache
+        return cache[1], cache[2]
+
     def forward(self, x, want_stats=False, join=None):
         g = self.geom(x.shape[1], x.shape[2])
         y, stats = conv2d(x, self.weight, self.bias, g, self.relu, want_stats, self, join)

@@ -113,6 +113,29 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out_dtype=
     return y
 
 
+def conv_fwd_fp8(x8, sx, w8, sw, geom: ConvGeom, relu=False, stats=None):
+    """Forward conv on fp8 e4m3 operands with per-tensor scales (y = Σ x8·w8 · sx·sw), bf16 out.
+    GPU: LDS-DMA kernel on v_mfma_scale_f32_16x16x128_f8f6f4.  CPU: fp32 on dequantised data."""
+    N, H, W, C = x8.shape
+    K, R, S, _ = w8.shape
+    Ho, Wo = geom.out_hw(H, W, R, S)
+    if on_gpu(x8):
+        y = torch.empty((N, Ho, Wo, K), device=x8.device, dtype=torch.bfloat16)
+        ext().conv_fwd_fp8(x8, w8, y, stats, sx, sw, geom.stride[0], geom.stride[1],
+                           geom.padding[0], geom.padding[2], geom.dilation[0], geom.dilation[1],
+                           bool(relu))
+        return y
+    y = ref_conv_fwd(x8.float() * sx, w8.float() * sw, geom)
+    if relu:
+        y = torch.relu(y)
+    y = y.to(torch.bfloat16)
+    if stats is not None:
+        yf = y.float().reshape(-1, K)
+        stats[0] += yf.sum(0)
+        stats[1] += (yf * yf).sum(0)
+    return y
+
+
 def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumulate=False):
     """dx.  With ``out`` the result is written there (``accumulate``: dx += …, fused in the GEMM
     epilogue — used by the residual-gradient join, ops/gradjoin.py)."""
@@ -176,7 +199,14 @@ class _Conv2dFn(torch.autograd.Function):
         if want_stats:
             stats = workspace.zeros((2, w.shape[0]), x.device)
         b = None if bias is None else bias.detach()
-        y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats)
+        if layer is not None and getattr(layer, "fp8", False) and b is None and on_gpu(x):
+            # fp8 forward (weights + activations e4m3, per-tensor scales); backward stays bf16
+            from .fp8 import quantize_e4m3
+            x8, sx = quantize_e4m3(x)
+            w8, sw = layer.fp8_weight(w)
+            y = conv_fwd_fp8(x8, sx, w8, sw, geom, relu=relu, stats=stats)
+        else:
+            y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats)
         ctx.geom = geom
         ctx.relu = relu
         ctx.layer = layer

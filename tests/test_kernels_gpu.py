@@ -348,3 +348,41 @@ def test_conv_dgrad_accumulate(gpu, conv_impl, shape):
     out = prev.to(gpu)
     C.conv_dgrad(dy.to(gpu), w.to(gpu), (N, H, W, Cin), g, out=out, accumulate=True)
     assert rel_err(out, ref) < 2e-2
+
+
+def test_fp8_quantize_matches_cpu(gpu):
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    torch.manual_seed(12)
+    x = (torch.randn(4, 7, 9, 32) * 3).bfloat16()
+    y8c, sc = F8.quantize_e4m3(x)
+    y8g, sg = F8.quantize_e4m3(x.to(gpu))
+    assert abs(float(sg) - float(sc)) / float(sc) < 1e-6
+    diff = (y8g.cpu().view(torch.uint8).int() - y8c.view(torch.uint8).int()).abs()
+    assert (diff > 0).float().mean() < 1e-3 and diff.max() <= 1  # RNE ties at most one ulp apart
+    back = F8.dequantize(y8g, sg).cpu()
+    assert rel_err(back, x.float()) < 0.07  # e4m3: 3 mantissa bits
+
+
+@pytest.mark.parametrize("shape", [(8, 14, 14, 128, 256, 3, 3, 1, 1),     # C % 128 == 0: tap per step
+                                   (8, 14, 14, 64, 128, 3, 3, 1, 1),      # 2 taps per 128-deep step
+                                   (4, 15, 15, 256, 64, 1, 1, 2, 0),      # 1x1 s2, 256x64 config
+                                   (16, 7, 7, 512, 512, 3, 3, 1, 1),
+                                   (2, 9, 11, 48, 40, 3, 3, 2, 1)])       # ragged everything
+def test_conv_fwd_fp8(gpu, shape):
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    N, H, W, Cin, K, R, S, st, p = shape
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
+    torch.manual_seed(13)
+    x = torch.randn(N, H, W, Cin).bfloat16()
+    w = (torch.randn(K, R, S, Cin) / math.sqrt(R * S * Cin)).bfloat16()
+    x8, sx = F8.quantize_e4m3(x.to(gpu))
+    w8, sw = F8.quantize_e4m3(w.to(gpu))
+    ref = C.ref_conv_fwd(F8.dequantize(x8, sx).cpu(), F8.dequantize(w8, sw).cpu(), g)
+    stats = torch.zeros(2, K, device=gpu)
+    y = C.conv_fwd_fp8(x8, sx, w8, sw, g, stats=stats)
+    assert y.dtype == torch.bfloat16 and y.shape == ref.shape
+    assert rel_err(y, ref) < 1e-2
+    yb = y.float().cpu().reshape(-1, K)
+    assert rel_err(stats[0], yb.sum(0)) < 1e-3
+    # fp8 vs the bf16 conv of the unquantised data: quantisation error only
+    assert rel_err(y, C.ref_conv_fwd(x.float(), w.float(), g)) < 0.08

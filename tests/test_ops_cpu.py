@@ -224,3 +224,22 @@ def test_fastdiv_magic_numbers_exact():
         ns = [0, 1, d - 1, d, d + 1, (1 << 31) - 1] + [rng.randrange(0, 1 << 31) for _ in range(50)]
         for n in ns:
             assert (n * m) >> s == n // d, (n, d)
+
+
+def test_fp8_quantize_and_conv_reference_cpu():
+    import math
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    from tensorflowdistributedlearning_amd.ops import conv as C
+    torch.manual_seed(0)
+    x = torch.randn(2, 6, 6, 32)
+    y8, s = F8.quantize_e4m3(x)
+    assert y8.dtype == torch.float8_e4m3fn and abs(float(s) - float(x.abs().max()) / 448) < 1e-6
+    assert float(y8.float().abs().max()) == 448.0
+    back = F8.dequantize(y8, s)
+    assert ((back - x).abs() <= x.abs() * 0.0625 + 1e-3).all()  # within half an e4m3 ulp
+    w = torch.randn(8, 3, 3, 32) / math.sqrt(288)
+    w8, sw = F8.quantize_e4m3(w)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    y = C.conv_fwd_fp8(y8, s, w8, sw, g)
+    ref = C.ref_conv_fwd(F8.dequantize(y8, s), F8.dequantize(w8, sw), g)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)

@@ -129,3 +129,17 @@ def test_residual_join_gpu_matches_plain_autograd(gpu):
             gradjoin.ENABLED = True
     cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=0).item()
     assert cos > 0.999, cos
+
+
+def test_resnet_fp8_forward_trains(gpu):
+    """fp8 (e4m3) forward GEMMs, bf16 backward: loss finite and falling on a fixed batch."""
+    torch.manual_seed(0)
+    m = models.resnet18(num_classes=10)
+    n = models.enable_fp8(m)
+    assert n >= 15
+    tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01, momentum=0.9,
+                                                          weight_decay=0.0))
+    x, y = imagenet_batch(32, 64, num_classes=10, device=gpu)
+    losses = [float(tr.train_step(x, y)[0]) for _ in range(12)]
+    assert all(l == l for l in losses), losses
+    assert min(losses[-3:]) < losses[0], losses
