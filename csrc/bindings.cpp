@@ -97,21 +97,48 @@ void conv_fwd_fp8(Tensor x8, Tensor w8, Tensor y, c10::optional<Tensor> stats, T
   conv_fwd_fp8_launch(a, stream());
 }
 
-void fp8_amax(Tensor x, Tensor amax) {
-  CHECK_T(x, torch::kBFloat16);
-  CHECK_T(amax, torch::kFloat32);
-  TORCH_CHECK(x.numel() % 8 == 0, "numel % 8");
-  fp8_amax_launch(BF(x), x.numel(), amax.data_ptr<float>(), stream());
+// amax rings are fp32 [3, AMAX_SLOT] (kernels.h); slot indices 0..2
+float* ring_slot(const Tensor& ring, int64_t k) {
+  CHECK_T(ring, torch::kFloat32);
+  TORCH_CHECK(ring.numel() == 3 * AMAX_SLOT && ring.is_contiguous(), "amax ring: fp32[3, AMAX_SLOT]");
+  return ring.data_ptr<float>() + ((k % 3) + 3) % 3 * AMAX_SLOT;
 }
 
-void fp8_quantize(Tensor x, Tensor amax, Tensor scale, Tensor y8) {
+void fp8_amax(Tensor x, Tensor ring, int64_t slot) {
   CHECK_T(x, torch::kBFloat16);
-  CHECK_T(amax, torch::kFloat32);
+  TORCH_CHECK(x.numel() % 8 == 0, "numel % 8");
+  fp8_amax_launch(BF(x), x.numel(), ring_slot(ring, slot), stream());
+}
+
+// scale from ring[phase]; measure: |x|max into ring[phase+1], ring[phase+2] cleared
+void fp8_quantize(Tensor x, Tensor ring, int64_t phase, bool measure, Tensor scale, Tensor y8) {
+  CHECK_T(x, torch::kBFloat16);
   CHECK_T(scale, torch::kFloat32);
   TORCH_CHECK(y8.is_cuda() && y8.element_size() == 1 && y8.is_contiguous() && y8.numel() == x.numel());
   TORCH_CHECK(x.numel() % 16 == 0, "numel % 16");
-  fp8_quantize_launch(BF(x), x.numel(), amax.data_ptr<float>(), scale.data_ptr<float>(),
+  fp8_quantize_launch(BF(x), x.numel(), ring_slot(ring, phase),
+                      measure ? ring_slot(ring, phase + 1) : nullptr,
+                      measure ? ring_slot(ring, phase + 2) : nullptr, scale.data_ptr<float>(),
                       (uint8_t*)y8.data_ptr(), stream());
+}
+
+// src: flat bf16 buffer; dst: flat 1-byte buffer of the same numel; chunks int64 [n,4];
+// rings fp32 [S,3,AMAX_SLOT]; scales fp32 [S]
+void fp8_multi_quantize(Tensor src, Tensor dst, Tensor chunks, Tensor rings, Tensor scales,
+                        int64_t phase, bool prime) {
+  CHECK_T(src, torch::kBFloat16);
+  CHECK_T(rings, torch::kFloat32);
+  CHECK_T(scales, torch::kFloat32);
+  TORCH_CHECK(dst.is_cuda() && dst.element_size() == 1 && dst.is_contiguous() &&
+              dst.numel() == src.numel(), "dst: flat 1-byte buffer like src");
+  TORCH_CHECK(chunks.is_cuda() && chunks.scalar_type() == torch::kInt64 && chunks.dim() == 2 &&
+              chunks.size(1) == 4 && chunks.is_contiguous(), "chunks: int64 [n,4]");
+  TORCH_CHECK(rings.dim() == 3 && rings.size(1) == 3 && rings.size(2) == AMAX_SLOT &&
+              rings.is_contiguous() && scales.numel() == rings.size(0), "rings [S,3,AMAX_SLOT]");
+  TORCH_CHECK(phase >= 0 && phase < 3);
+  fp8_multi_quantize_launch(BF(src), (uint8_t*)dst.data_ptr(), chunks.data_ptr<int64_t>(),
+                            (int)chunks.size(0), rings.data_ptr<float>(), scales.data_ptr<float>(),
+                            (int)phase, prime, stream());
 }
 
 void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
@@ -184,26 +211,34 @@ void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor>
                      (float)decay, (float)eps, training, stream());
 }
 
+// fp8 side output (delayed scaling): amax_ring is fp32[3, AMAX_SLOT]; slot `phase` holds the previous
+// step's |y|max (scale source), slot phase+1 accumulates this step's, slot phase+2 is cleared
+// for the next step — no separate memset launch.
 void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu,
-              c10::optional<Tensor> y8, c10::optional<Tensor> amax_prev,
-              c10::optional<Tensor> scale_out, c10::optional<Tensor> amax_out) {
+              c10::optional<Tensor> y8, c10::optional<Tensor> amax_ring, int64_t phase,
+              c10::optional<Tensor> scale_out) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   CHECK_T(coef, torch::kFloat32);
   const int64_t C = x.size(-1);
   uint8_t* y8p = nullptr;
-  const bool fp8 = amax_out.has_value() && amax_out->defined();
-  if (fp8) {
+  float *prev = nullptr, *out = nullptr, *zero = nullptr;
+  if (amax_ring.has_value() && amax_ring->defined()) {
     TORCH_CHECK(C % 8 == 0, "fp8 side output needs C % 8 == 0");
-    TORCH_CHECK(amax_prev.has_value() && amax_prev->defined(), "amax_prev required");
+    CHECK_T(*amax_ring, torch::kFloat32);
+    TORCH_CHECK(amax_ring->numel() == 3 * AMAX_SLOT && phase >= 0 && phase < 3,
+                "amax_ring: fp32[3, AMAX_SLOT], phase 0..2");
+    float* r = amax_ring->data_ptr<float>();
+    prev = r + phase * AMAX_SLOT;
+    out = r + (phase + 1) % 3 * AMAX_SLOT;
+    zero = r + (phase + 2) % 3 * AMAX_SLOT;
     if (y8.has_value() && y8->defined()) {
       TORCH_CHECK(y8->element_size() == 1 && y8->numel() == x.numel() && y8->is_contiguous());
       y8p = (uint8_t*)y8->data_ptr();
     }
   }
   bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu,
-                  stream(), y8p, fp8 ? amax_prev->data_ptr<float>() : nullptr,
-                  fp8 ? optfw(scale_out) : nullptr, fp8 ? amax_out->data_ptr<float>() : nullptr);
+                  stream(), y8p, prev, optfw(scale_out), out, zero);
 }
 
 void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, int64_t relu) {
@@ -495,14 +530,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
+  m.attr("AMAX_SLOT") = AMAX_SLOT;
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_quantize", &fp8_quantize);
+  m.def("fp8_multi_quantize", &fp8_multi_quantize);
   m.def("fp8_dequantize", &fp8_dequantize);
   m.def("bn_stats", &bn_stats);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("res"), py::arg("y"),
-        py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_prev") = py::none(),
-        py::arg("scale_out") = py::none(), py::arg("amax_out") = py::none());
+        py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_ring") = py::none(),
+        py::arg("phase") = 0, py::arg("scale_out") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("relu_bwd", &relu_bwd);

@@ -88,10 +88,24 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
         sh[j] = coef[C + cv * 8 + j];
       }
     }
-    for (long r = r0 + rl; r < r1; r += rpp) {
-      const long off = r * C + cv * 8;
+    // U rows in flight per thread: all loads of a group are issued before any use
+    constexpr int U = 4;
+    long r = r0 + rl;
+    for (; r < r1; r += U * rpp) {
+      uint4 la[U], lx[U], ly[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + u * rpp;
+        const long off = (rr < r1 ? rr : r) * C + cv * 8;
+        la[u] = *(const uint4*)(a + off);
+        if (KIND == 1) lx[u] = *(const uint4*)(x + off);
+        if (KIND == 1 && relu == 1) ly[u] = *(const uint4*)(y + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+      if (r + u * rpp >= r1) break;
       float va[8];
-      unpack(*(const uint4*)(a + off), va);
+      unpack(la[u], va);
       if (KIND == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -100,10 +114,10 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
         }
       } else {
         float vx[8];
-        unpack(*(const uint4*)(x + off), vx);
+        unpack(lx[u], vx);
         if (relu == 1) {
           float vy[8];
-          unpack(*(const uint4*)(y + off), vy);
+          unpack(ly[u], vy);
 #pragma unroll
           for (int j = 0; j < 8; ++j) va[j] = vy[j] > 0.f ? va[j] : 0.f;
         } else if (relu == 2) {  // y = relu(x·scale + shift): the mask without reading y
@@ -116,6 +130,7 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
           s0[j] += va[j];
           s1[j] += va[j] * xh;
         }
+      }
       }
     }
   }
@@ -140,8 +155,10 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
                    long M, int C, int relu, hipStream_t st) {
   if (M <= 0) return;
   if (C % 8 == 0 && C / 8 <= NT) {
+    // ≈ one or two workgroups per CU, ≥ 16 rows per thread: few atomics per output address
+    // (every workgroup adds one row of 2C partial sums)
     const int cvecs = C / 8, rpp = NT / cvecs;
-    long blocks = std::min<long>(1024, std::max<long>(1, M / (rpp * 4)));
+    long blocks = std::min<long>(512, std::max<long>(1, M / (rpp * 16)));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
     hipLaunchKernelGGL(reduce_vec_kernel<KIND>, dim3(blocks), dim3(NT), 0, st, a, y, x, coef, out, M,
@@ -185,8 +202,9 @@ __global__ void finalize_kernel(const float* __restrict__ stats, float* __restri
 // count (always for power-of-two C ≤ 2048) each thread's channel vector is loop-invariant, so its
 // 16 coefficients are loaded once into registers.
 // Optional fp8 side output (delayed scaling, fp8 forward convs): y8 = e4m3(sat(y·448/amax_prev))
-// in the same pass, scale_out = amax_prev/448 for the consumer GEMM, and this step's |y|max into
-// amax_out (the next step's scale).  y8 is skipped while amax_prev is still 0 (first step).
+// in the same pass, scale_out = amax_prev/448 for the consumer GEMM, and this call's |y|max into
+// amax_out (the next call's scale) — amax slots as in common.h.  y8 is skipped while amax_prev is
+// still 0 (first call).
 __device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
   int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
   v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
@@ -200,14 +218,16 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
                                                        int relu, uint8_t* __restrict__ y8,
                                                        const float* __restrict__ amax_prev,
                                                        float* __restrict__ scale_out,
-                                                       float* __restrict__ amax_out) {
+                                                       float* __restrict__ amax_out,
+                                                       float* __restrict__ amax_zero) {
   float inv8 = 0.f, vmax = 0.f;
   bool emit8 = false;
   if (amax_out) {
-    const float ap = *amax_prev;
+    const float ap = amax_read(amax_prev);
     emit8 = y8 != nullptr && ap > 0.f;
     inv8 = ap > 0.f ? 448.f / ap : 0.f;
     if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = ap / 448.f;
+    amax_clear(amax_zero);  // the slot the next call accumulates into
   }
   const int cvecs = C >> 3;
   const long stride = (long)gridDim.x * NT;
@@ -256,10 +276,7 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
       }
     }
   }
-  if (amax_out) {
-    vmax = wave_max(vmax);
-    if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)amax_out, __float_as_uint(vmax));
-  }
+  if (amax_out) amax_publish(amax_out, vmax);
 }
 
 __global__ void apply_scalar_kernel(const bf16_t* __restrict__ x, const float* __restrict__ coef,
@@ -278,6 +295,13 @@ __global__ void apply_scalar_kernel(const bf16_t* __restrict__ x, const float* _
 //   A = γ·invstd,  B = −A·invstd·Σg·x̂/M,  Cc = −A·Σg/M − B·mean.
 // Coefficients are hoisted into registers (loop-invariant channel vector, see apply_vec_kernel).
 // Block 0 also writes dγ = Σg·x̂ and dβ = Σg straight into the flat gradient buffer.
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+template <bool HOIST>
 __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
@@ -291,26 +315,34 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
   }
   const int cvecs = C >> 3;
   const long stride = (long)gridDim.x * NT;
-  const bool hoist = (stride % cvecs) == 0;
   long i = blockIdx.x * (long)NT + threadIdx.x;
   float A[8], Bc[8], Cc[8], Sc[8], Sh[8];
   auto load_coef = [&](int cv) {
+    float mean[8], inv[8], s0[8], s1[8], gm[8];
+    load8f(coef + cv * 8, Sc);
+    load8f(coef + C + cv * 8, Sh);
+    load8f(coef + 2 * C + cv * 8, mean);
+    load8f(coef + 3 * C + cv * 8, inv);
+    load8f(red + cv * 8, s0);
+    load8f(red + C + cv * 8, s1);
+    if (gamma) {
+      load8f(gamma + cv * 8, gm);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gm[j] = 1.f;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = cv * 8 + j;
-      Sc[j] = coef[c];
-      Sh[j] = coef[C + c];
-      const float mean = coef[2 * C + c], inv = coef[3 * C + c];
-      const float a = (gamma ? gamma[c] : 1.f) * inv;
-      const float b = -a * inv * red[C + c] * inv_count;
+      const float a = gm[j] * inv[j];
+      const float b = -a * inv[j] * s1[j] * inv_count;
       A[j] = a;
       Bc[j] = b;
-      Cc[j] = -a * red[c] * inv_count - b * mean;
+      Cc[j] = -a * s0[j] * inv_count - b * mean[j];
     }
   };
-  if (hoist) load_coef((int)(i % cvecs));
+  if (HOIST) load_coef((int)(i % cvecs));
   for (; i < nvec; i += stride) {
-    if (!hoist) load_coef((int)(i % cvecs));
+    if (!HOIST) load_coef((int)(i % cvecs));
     float g[8], vx[8];
     unpack(((const uint4*)dy)[i], g);
     unpack(((const uint4*)x)[i], vx);
@@ -388,11 +420,11 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st, uint8_t* y8, const float* amax_prev,
-                     float* scale_out, float* amax_out) {
+                     float* scale_out, float* amax_out, float* amax_zero) {
   const long n = M * C;
   if (C % 8 == 0) {
     hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, x, coef, res, y,
-                       n / 8, C, relu ? 1 : 0, y8, amax_prev, scale_out, amax_out);
+                       n / 8, C, relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero);
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
                        C, relu ? 1 : 0);
@@ -410,8 +442,11 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          hipStream_t st) {
   const long n = M * C;
   if (C % 8 == 0) {
-    hipLaunchKernelGGL(bwd_apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, dy, y, x, coef,
-                       red, gamma, dx, dres, dgamma, dbeta, n / 8, C, 1.f / count, relu);
+    const int blocks = ew_blocks(n / 8, C / 8);
+    const bool hoist = ((long)blocks * NT) % (C / 8) == 0;
+    hipLaunchKernelGGL(hoist ? bwd_apply_vec_kernel<true> : bwd_apply_vec_kernel<false>, dim3(blocks),
+                       dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, n / 8, C,
+                       1.f / count, relu);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu);

@@ -2,10 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "kernels.h"
 
 namespace tdl {
 
-typedef uint16_t bf16_t;  // storage type of bf16 tensors (raw bits)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -50,6 +50,36 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// Device-side |x|max for fp8 scaling.  A single float hit by one atomic per wave serialises in
+// L2 (~10 ns each: 8k waves ≈ 90 µs), so a "slot" is AMAX_SPREAD partial maxima 256 B apart
+// (different L2 channels); each workgroup reduces in LDS and issues one atomicMax to the partial
+// blockIdx % AMAX_SPREAD.  Readers max the partials (one load per lane).  A delayed-scaling ring
+// is 3 slots: read slot p (previous call), accumulate into p+1, clear p+2 for the next call.
+
+// all threads of the block must call it (contains __syncthreads); v ≥ 0
+__device__ __forceinline__ void amax_publish(float* slot, float v) {
+  __shared__ float red[16];
+  v = wave_max(v);
+  const int nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = red[0];
+    for (int w = 1; w < nw; ++w) b = fmaxf(b, red[w]);
+    if (b > 0.f)
+      atomicMax((unsigned int*)(slot + (blockIdx.x % AMAX_SPREAD) * AMAX_STRIDE), __float_as_uint(b));
+  }
+}
+
+__device__ __forceinline__ float amax_read(const float* slot) {
+  const int l = threadIdx.x & 63;
+  return wave_max(l < AMAX_SPREAD ? slot[l * AMAX_STRIDE] : 0.f);
+}
+
+__device__ __forceinline__ void amax_clear(float* slot) {
+  if (blockIdx.x == 0 && threadIdx.x < AMAX_SPREAD) slot[threadIdx.x * AMAX_STRIDE] = 0.f;
 }
 
 // XCD-aware bijective remap of a linear workgroup id (MI355X: 8 XCDs, blocks dealt round robin;

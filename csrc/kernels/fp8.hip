@@ -1,9 +1,12 @@
 // fp8 (OCP e4m3fn, gfx950) quantisation with per-tensor scaling for the fp8 forward convolution
 // (ResNet-152 fp8 weights/activations on the CDNA4 fp8 MFMA).
 //
-//   amax      : |x|max over a bf16 tensor → fp32 (atomicMax on the IEEE bits: valid for x ≥ 0)
+//   amax      : |x|max over a bf16 tensor → an amax slot (common.h: spread partial maxima, one
+//               atomicMax on the IEEE bits per workgroup — valid for values ≥ 0)
 //   quantize  : scale = amax / 448 (E4M3 max normal), y8 = sat(x / scale) as e4m3; the scale is
-//               also written to device memory for the GEMM epilogue (acc · s_x · s_w)
+//               also written to device memory for the GEMM epilogue (acc · s_x · s_w).  Delayed
+//               scaling: the scale comes from the previous call's slot while this call measures
+//               its own amax (one pass, no host sync, no memset)
 //   dequantize: tests / debugging
 // Everything stays on the device: no host synchronisation for the scale.
 #include "common.h"
@@ -16,7 +19,7 @@ constexpr int NT = 256;
 constexpr float E4M3_MAX = 448.f;
 
 __global__ void __launch_bounds__(NT) amax_kernel(const bf16_t* __restrict__ x, long nvec,
-                                                  float* __restrict__ amax) {
+                                                  float* __restrict__ slot) {
   float m = 0.f;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nvec; i += (long)gridDim.x * NT) {
     float v[8];
@@ -24,15 +27,7 @@ __global__ void __launch_bounds__(NT) amax_kernel(const bf16_t* __restrict__ x, 
 #pragma unroll
     for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[j]));
   }
-  m = wave_max(m);
-  __shared__ float red[NT / 64];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float b = red[0];
-    for (int w = 1; w < NT / 64; ++w) b = fmaxf(b, red[w]);
-    atomicMax((unsigned int*)amax, __float_as_uint(b));
-  }
+  amax_publish(slot, m);
 }
 
 __device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float d) {
@@ -41,20 +36,28 @@ __device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float 
   return (uint32_t)v;
 }
 
-// 16 elements per thread: two 16-B bf16 vectors in, one 16-B e4m3 vector out
+// 16 elements per thread: two 16-B bf16 vectors in, one 16-B e4m3 vector out.  scale = amax(slot
+// `prev`)/448; with `meas` the |x|max of this call is accumulated into `meas` (the next call's
+// scale: delayed scaling) and `clr` is cleared for the call after.
 __global__ void __launch_bounds__(NT) quantize_kernel(const bf16_t* __restrict__ x, long n16,
-                                                      const float* __restrict__ amax,
+                                                      const float* __restrict__ prev,
+                                                      float* __restrict__ meas, float* __restrict__ clr,
                                                       float* __restrict__ scale_out,
                                                       uint8_t* __restrict__ y) {
-  const float am = fmaxf(*amax, 1e-12f);
+  const float am = fmaxf(amax_read(prev), 1e-12f);
   const float inv = E4M3_MAX / am;
   if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = am / E4M3_MAX;
+  if (clr) amax_clear(clr);
+  float m = 0.f;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n16; i += (long)gridDim.x * NT) {
     float v[16];
     unpack8(((const uint4*)x)[2 * i], v);
     unpack8(((const uint4*)x)[2 * i + 1], v + 8);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = fminf(fmaxf(v[j] * inv, -E4M3_MAX), E4M3_MAX);
+    for (int j = 0; j < 16; ++j) {
+      m = fmaxf(m, fabsf(v[j]));
+      v[j] = fminf(fmaxf(v[j] * inv, -E4M3_MAX), E4M3_MAX);
+    }
     uint4 o;
     o.x = pack4_e4m3(v[0], v[1], v[2], v[3]);
     o.y = pack4_e4m3(v[4], v[5], v[6], v[7]);
@@ -62,6 +65,60 @@ __global__ void __launch_bounds__(NT) quantize_kernel(const bf16_t* __restrict__
     o.w = pack4_e4m3(v[12], v[13], v[14], v[15]);
     ((uint4*)y)[i] = o;
   }
+  if (meas) amax_publish(meas, m);
+}
+
+// All fp8 weights of a model in ONE launch (after each optimizer step): the bf16 compute copies
+// live in one flat buffer (models/params.py), the e4m3 copies in a parallel flat byte buffer.
+// Work list: chunk c = (segment, start, len, first) with len % 16 == 0; each segment (weight
+// tensor) has its own delayed-scaling amax ring rings[seg] = fp32[3][AMAX_SLOT] and scale
+// scales[seg].  prime = 1: measure |w|max into slot `phase` only (first call).
+__global__ void __launch_bounds__(NT) multi_quantize_kernel(const bf16_t* __restrict__ src,
+                                                            uint8_t* __restrict__ dst,
+                                                            const long* __restrict__ chunks,
+                                                            float* __restrict__ rings,
+                                                            float* __restrict__ scales, int phase,
+                                                            int prime) {
+  const long* c = chunks + 4 * (long)blockIdx.x;
+  const long seg = c[0], start = c[1], n16 = c[2] / 16;
+  float* ring = rings + seg * 3 * AMAX_SLOT;
+  float* prev = ring + phase * AMAX_SLOT;
+  const uint4* s4 = (const uint4*)(src + start);
+  float m = 0.f;
+  if (prime) {
+    for (long i = threadIdx.x; i < n16; i += NT) {
+      float v[16];
+      unpack8(s4[2 * i], v);
+      unpack8(s4[2 * i + 1], v + 8);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[j]));
+    }
+    amax_publish(prev, m);
+    return;
+  }
+  const float am = fmaxf(amax_read(prev), 1e-12f);
+  const float inv = E4M3_MAX / am;
+  if (c[3] && threadIdx.x == 0) scales[seg] = am / E4M3_MAX;
+  if (c[3] && threadIdx.x < AMAX_SPREAD)
+    ring[(phase + 2) % 3 * AMAX_SLOT + threadIdx.x * AMAX_STRIDE] = 0.f;
+  uint4* d4 = (uint4*)(dst + start);
+  for (long i = threadIdx.x; i < n16; i += NT) {
+    float v[16];
+    unpack8(s4[2 * i], v);
+    unpack8(s4[2 * i + 1], v + 8);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      m = fmaxf(m, fabsf(v[j]));
+      v[j] = fminf(fmaxf(v[j] * inv, -E4M3_MAX), E4M3_MAX);
+    }
+    uint4 o;
+    o.x = pack4_e4m3(v[0], v[1], v[2], v[3]);
+    o.y = pack4_e4m3(v[4], v[5], v[6], v[7]);
+    o.z = pack4_e4m3(v[8], v[9], v[10], v[11]);
+    o.w = pack4_e4m3(v[12], v[13], v[14], v[15]);
+    d4[i] = o;
+  }
+  amax_publish(ring + (phase + 1) % 3 * AMAX_SLOT, m);
 }
 
 __global__ void dequantize_kernel(const uint8_t* __restrict__ y, long n, const float* __restrict__ scale,
@@ -77,16 +134,23 @@ inline int grid_for(long n) { return (int)std::min<long>(4096, std::max<long>(1,
 
 }  // namespace
 
-void fp8_amax_launch(const bf16_t* x, long n, float* amax, hipStream_t st) {
+void fp8_amax_launch(const bf16_t* x, long n, float* slot, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, st, x, n / 8, amax);
+  hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, st, x, n / 8, slot);
 }
 
-void fp8_quantize_launch(const bf16_t* x, long n, const float* amax, float* scale_out, uint8_t* y,
-                         hipStream_t st) {
+void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,
+                         float* scale_out, uint8_t* y, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n / 16)), dim3(NT), 0, st, x, n / 16, amax,
-                     scale_out, y);
+  hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n / 16)), dim3(NT), 0, st, x, n / 16, prev, meas,
+                     clr, scale_out, y);
+}
+
+void fp8_multi_quantize_launch(const bf16_t* src, uint8_t* dst, const long* chunks, int nchunks,
+                               float* rings, float* scales, int phase, bool prime, hipStream_t st) {
+  if (nchunks <= 0) return;
+  hipLaunchKernelGGL(multi_quantize_kernel, dim3(nchunks), dim3(NT), 0, st, src, dst, chunks, rings,
+                     scales, phase, prime ? 1 : 0);
 }
 
 void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st) {

@@ -7,7 +7,11 @@
 
 namespace tdl {
 
-typedef uint16_t bf16_t;
+typedef uint16_t bf16_t;  // storage type of bf16 tensors (raw bits)
+
+// fp8 amax "slot": AMAX_SPREAD partial maxima AMAX_STRIDE floats apart (common.h amax_publish);
+// a delayed-scaling ring is 3 slots
+constexpr int AMAX_SPREAD = 16, AMAX_STRIDE = 64, AMAX_SLOT = AMAX_SPREAD * AMAX_STRIDE;
 
 struct FastDiv {
   uint32_t m, s;
@@ -77,9 +81,14 @@ bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);
 void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 // fp8 (OCP e4m3) forward conv: a.x / a.w point at e4m3 bytes, a.scale_x / a.scale_w at their fp32 scales
 void conv_fwd_fp8_launch(const ConvArgs& a, hipStream_t st);
-void fp8_amax_launch(const bf16_t* x, long n, float* amax, hipStream_t st);
-void fp8_quantize_launch(const bf16_t* x, long n, const float* amax, float* scale_out, uint8_t* y,
-                         hipStream_t st);
+void fp8_amax_launch(const bf16_t* x, long n, float* slot, hipStream_t st);
+// prev: amax slot giving the scale; meas (optional): slot accumulating |x|max; clr (optional):
+// slot cleared for the next call
+void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,
+                         float* scale_out, uint8_t* y, hipStream_t st);
+// chunks: int64 [nchunks][4] = (segment, start element, length (% 16 == 0), first-of-segment)
+void fp8_multi_quantize_launch(const bf16_t* src, uint8_t* dst, const long* chunks, int nchunks,
+                               float* rings, float* scales, int phase, bool prime, hipStream_t st);
 void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st);
 void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st);
 
@@ -91,7 +100,7 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st, uint8_t* y8 = nullptr,
                      const float* amax_prev = nullptr, float* scale_out = nullptr,
-                     float* amax_out = nullptr);
+                     float* amax_out = nullptr, float* amax_zero = nullptr);
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                           float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,

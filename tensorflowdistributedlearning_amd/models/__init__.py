@@ -16,15 +16,19 @@ _REGISTRY = {
 }
 
 
-def enable_fp8(model):
+def enable_fp8(model, fuse_bn=True):
     """fp8 (e4m3) forward GEMMs for every bias-free conv whose input channels are a multiple of 16
-    (the 3-channel stem and biased heads stay bf16); backward stays bf16.  Returns the count."""
-    from .layers import Conv2d
+    (the 3-channel stem and biased heads stay bf16); backward stays bf16.  With ``fuse_bn`` the BN
+    layers write the e4m3 copy of their output in the same pass (scale from the previous step's
+    |y|max), so those conv inputs need no separate quantisation pass.  Returns the conv count."""
+    from .layers import Conv2d, BatchNorm
     n = 0
     for m in model.modules():
         if isinstance(m, Conv2d) and m.bias is None and m._cin_store % 16 == 0:
             m.fp8 = True
             n += 1
+        elif isinstance(m, BatchNorm) and fuse_bn:
+            m.emit_fp8 = True  # conv inputs arrive pre-quantised (delayed scaling, ops/bn.py)
     return n
 
 

@@ -151,16 +151,29 @@ class Conv2d(nn.Module):
     fp8 = False  # set by models.enable_fp8: e4m3 forward GEMM (ops/fp8.py)
 
     def fp8_weight(self, w_lowp):
-        """e4m3 copy of the weight + its scale, re-quantised once per optimizer step."""
-        from ..ops.fp8 import quantize_e4m3
+        """e4m3 copy of the weight + its scale, re-quantised once per optimizer step (delayed
+        scaling: one pass per step)."""
+        from ..ops.fp8 import DelayedScaler, flat_weights_for
         from .params import version
-        cache = getattr(self, "_fp8_cache", None)
         v = version()
+        if self._cin_store == self.cin:  # the weight is the flat bf16 buffer slice itself
+            fw = flat_weights_for(self.weight)
+            got = fw.get(self.weight, v) if fw is not None else None
+            if got is not None:
+                return got
+        cache = self.__dict__.get("_fp8_cache")
         if cache is None or cache[0] != v or cache[1].device != w_lowp.device:
-            w8, sw = quantize_e4m3(w_lowp)
+            sc = self.__dict__.setdefault("_fp8_w", DelayedScaler())
+            w8, sw = sc.quantize(w_lowp)
             cache = (v, w8, sw)
-            self._fp8_cache = cache
+            self.__dict__["_fp8_cache"] = cache
         return cache[1], cache[2]
+
+    def fp8_input(self, x):
+        """e4m3 copy of an input no BN pre-quantised (delayed scaling, per layer)."""
+        from ..ops.fp8 import DelayedScaler
+        sc = self.__dict__.setdefault("_fp8_x", DelayedScaler())
+        return sc.quantize(x)
 
     def forward(self, x, want_stats=False, join=None):
         g = self.geom(x.shape[1], x.shape[2])
@@ -186,6 +199,19 @@ class BatchNorm(nn.Module):
         self.beta._no_decay = True
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
+
+    emit_fp8 = False  # set by models.enable_fp8: also emit an e4m3 copy for the fp8 consumer conv
+
+    def fp8_state(self, x):
+        """(amax ring, phase, scale, emit) for the delayed-scaling e4m3 side output of bn_apply
+        (ops/bn.py, ops/fp8.DelayedScaler), or None where it does not apply."""
+        if not (x.is_cuda and self.c % 16 == 0):
+            return None
+        from ..ops.fp8 import DelayedScaler
+        sc = self.__dict__.get("_fp8")
+        if sc is None:
+            sc = self.__dict__["_fp8"] = DelayedScaler()
+        return sc.bn_args(x)
 
     def forward(self, x, stats=None, residual=None, relu=False, res_join=None):
         return batch_norm_act(x, self, stats=stats, residual=residual, relu=relu,

@@ -80,6 +80,7 @@ class FlatParams:
             p.grad = self.grad[o:o + n].view(p.shape)
             p._lowp = self.lowp[o:o + n].view(p.shape) if self.lowp is not None else None
             p._flat_offset = o
+            p._flat_lowp = self.lowp
             p._grad_fresh = True
         self.sync_lowp()
 

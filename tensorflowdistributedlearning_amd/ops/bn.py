@@ -64,10 +64,21 @@ def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps
     return torch.stack([scale, shift, mean, invstd])
 
 
-def bn_apply(x, coef, residual=None, relu=True):
+def bn_apply(x, coef, residual=None, relu=True, fp8=None):
+    """``fp8`` = (amax_ring fp32[3], phase, scale fp32[1], emit): also write an e4m3 copy of y
+    scaled by the previous call's |y|max (delayed scaling) — returned as ``y._tdl_fp8`` =
+    (y8, scale) for an fp8 consumer conv (ops/conv.py) when ``emit``."""
     if on_gpu(x):
         y = torch.empty_like(x)
-        ext().bn_apply(x, coef, residual, y, bool(relu))
+        if fp8 is None:
+            ext().bn_apply(x, coef, residual, y, bool(relu))
+            return y
+        ring, phase, scale, emit = fp8
+        y8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e4m3fn) if emit else None
+        ext().bn_apply(x, coef, residual, y, bool(relu), y8.view(torch.uint8) if emit else None,
+                       ring, int(phase), scale)
+        if emit:
+            y._tdl_fp8 = (y8, scale)
         return y
     C = x.shape[-1]
     y = x.float() * coef[0].view(*([1] * (x.dim() - 1)), C) + coef[1]
@@ -136,7 +147,8 @@ class _BatchNormActFn(torch.autograd.Function):
                 stats = bn_stats(x)
         coef = bn_finalize(stats, count, gamma, beta, bn.running_mean, bn.running_var,
                            bn.decay, bn.eps, training)
-        y = bn_apply(x, coef, residual, relu)
+        fp8 = bn.fp8_state(x) if getattr(bn, "emit_fp8", False) else None
+        y = bn_apply(x, coef, residual, relu, fp8)
         ctx.count = count
         ctx.training = training
         ctx.has_res = residual is not None

@@ -201,8 +201,8 @@ class _Conv2dFn(torch.autograd.Function):
         b = None if bias is None else bias.detach()
         if layer is not None and getattr(layer, "fp8", False) and b is None and on_gpu(x):
             # fp8 forward (weights + activations e4m3, per-tensor scales); backward stays bf16
-            from .fp8 import quantize_e4m3
-            x8, sx = quantize_e4m3(x)
+            pre = getattr(x, "_tdl_fp8", None)  # e4m3 copy emitted by the producing BN
+            x8, sx = pre if pre is not None else layer.fp8_input(x)
             w8, sw = layer.fp8_weight(w)
             y = conv_fwd_fp8(x8, sx, w8, sw, geom, relu=relu, stats=stats)
         else:
@@ -216,12 +216,17 @@ class _Conv2dFn(torch.autograd.Function):
         if stats is None:
             stats = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(stats)
+        # the stats output never receives a gradient: without this autograd zero-fills one
+        # (a fill launch per conv per step)
+        ctx.set_materialize_grads(False)
         return y, stats
 
     @staticmethod
     def backward(ctx, dy, _dstats):
         x, weight, bias, y = ctx.saved_tensors
         geom = ctx.geom
+        if dy is None:
+            return (None,) * 8
         dy = dy.contiguous()
         if ctx.relu:
             dy = relu_bwd(dy, y)

@@ -15,20 +15,146 @@ E4M3 = torch.float8_e4m3fn
 E4M3_MAX = 448.0
 
 
+AMAX_SLOT = 1024  # fp32 partial maxima per amax slot (csrc/kernels/kernels.h AMAX_SLOT)
+
+
+def _new_ring(device):
+    return torch.zeros(3, AMAX_SLOT, device=device, dtype=torch.float32)
+
+
 def quantize_e4m3(x):
+    """Just-in-time scaling: scale from this tensor's own amax (amax pass + quantise pass)."""
     if on_gpu(x):
-        amax = torch.zeros(1, device=x.device, dtype=torch.float32)
+        ring = _new_ring(x.device)
         scale = torch.empty(1, device=x.device, dtype=torch.float32)
         y8 = torch.empty(x.shape, device=x.device, dtype=E4M3)
         xc = x.contiguous()
-        ext().fp8_amax(xc, amax)
-        ext().fp8_quantize(xc, amax, scale, y8)
+        ext().fp8_amax(xc, ring, 0)
+        ext().fp8_quantize(xc, ring, 0, False, scale, y8.view(torch.uint8))
         return y8, scale
     xf = x.float()
     amax = xf.abs().max().clamp_min(1e-12)
     scale = (amax / E4M3_MAX).reshape(1)
     y8 = (xf / scale).clamp(-E4M3_MAX, E4M3_MAX).to(E4M3)
     return y8, scale
+
+
+class DelayedScaler:
+    """Per-tensor delayed scaling (the fp8 training recipe): call t quantises with the |x|max
+    measured by call t−1 while measuring its own — one pass over x, no host sync, no memset
+    (a 3-slot amax ring: read p, accumulate p+1, clear p+2).  The very first call primes the
+    ring with an amax pass, so it is exact.  Values beyond the previous amax saturate at ±448.
+    ``bn_args`` hands the same state to the BN apply kernel's fused e4m3 side output
+    (ops/bn.py), whose first call only measures."""
+
+    def __init__(self):
+        self.ring = None
+        self.scale = None
+        self.phase = 0
+        self.calls = 0
+
+    def _ensure(self, device):
+        if self.ring is None or self.ring.device != device:
+            self.ring = _new_ring(device)
+            self.scale = torch.zeros(1, device=device, dtype=torch.float32)
+            self.phase = 0
+            self.calls = 0
+
+    def _advance(self):
+        self.phase = (self.phase + 1) % 3
+        self.calls += 1
+
+    def quantize(self, x):
+        if not on_gpu(x):
+            return quantize_e4m3(x)
+        self._ensure(x.device)
+        xc = x.contiguous()
+        if self.calls == 0:
+            ext().fp8_amax(xc, self.ring, self.phase)
+        y8 = torch.empty(x.shape, device=x.device, dtype=E4M3)
+        # a fresh scale tensor per call: the consumer may still hold the previous one
+        scale = torch.empty(1, device=x.device, dtype=torch.float32)
+        ext().fp8_quantize(xc, self.ring, self.phase, True, scale, y8.view(torch.uint8))
+        self._advance()
+        return y8, scale
+
+    def bn_args(self, x):
+        self._ensure(x.device)
+        scale = torch.empty(1, device=x.device, dtype=torch.float32)
+        out = (self.ring, self.phase, scale, self.calls > 0)
+        self._advance()
+        return out
+
+
+class FlatFp8Weights:
+    """e4m3 copies of every fp8 conv weight that lives in one flat bf16 buffer
+    (models/params.FlatParams), refreshed by ONE launch per optimizer step
+    (``fp8_multi_quantize``: delayed scaling per weight tensor) instead of one amax+quantise pair
+    per layer.  Layers join on their first call (served by their own scaler for that call) and the
+    work list is rebuilt at the next parameter version."""
+
+    CHUNK = 16384  # elements per workgroup
+
+    def __init__(self, flat_lowp):
+        self.flat = flat_lowp
+        self.w8 = torch.empty(flat_lowp.numel(), device=flat_lowp.device, dtype=E4M3)
+        self.index = {}     # id(param) -> segment
+        self.pending = {}   # id(param) -> (offset, numel)
+        self.spans = []     # segment -> (offset, numel)
+        self.version = None
+        self.phase = 0
+
+    def _rebuild(self):
+        for k, sp in self.pending.items():
+            self.index[k] = len(self.spans)
+            self.spans.append(sp)
+        self.pending = {}
+        rows = []
+        total = self.flat.numel()
+        for seg, (off, n) in enumerate(self.spans):
+            if n % 16 or off % 16 or off + n > total:
+                raise ValueError(f"fp8 weight span ({off}, {n}) not 16-aligned inside the buffer")
+            for c in range(0, n, self.CHUNK):
+                rows.append((seg, off + c, min(self.CHUNK, n - c), int(c == 0)))
+        dev = self.flat.device
+        self.chunks = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self.rings = torch.zeros(len(self.spans), 3, AMAX_SLOT, device=dev)
+        self.scales = torch.zeros(len(self.spans), device=dev)
+        self.phase = 0
+        ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
+                                 self.scales, self.phase, True)  # prime: exact first scales
+
+    def get(self, p, version):
+        """(w8, scale) for parameter ``p`` at parameter version ``version``, or None the first
+        time ``p`` is seen (caller quantises it itself)."""
+        k = id(p)
+        if k not in self.index and k not in self.pending:
+            self.pending[k] = (p._flat_offset, p.numel())
+            return None
+        if self.version != version:
+            if self.pending:
+                self._rebuild()
+            ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
+                                     self.scales, self.phase, False)
+            self.phase = (self.phase + 1) % 3
+            self.version = version
+        seg = self.index.get(k)
+        if seg is None:  # joined during this version
+            return None
+        off, n = self.spans[seg]
+        return self.w8[off:off + n].view(p.shape), self.scales[seg:seg + 1]
+
+
+def flat_weights_for(p):
+    """The :class:`FlatFp8Weights` of ``p``'s flat buffer (None if ``p`` is not flat-backed);
+    kept on the buffer tensor itself, so it lives and dies with the FlatParams."""
+    flat = getattr(p, "_flat_lowp", None)
+    if flat is None or not on_gpu(flat):
+        return None
+    fw = getattr(flat, "_tdl_fp8w", None)
+    if fw is None:
+        fw = flat._tdl_fp8w = FlatFp8Weights(flat)
+    return fw
 
 
 def dequantize(y8, scale):

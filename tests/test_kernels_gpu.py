@@ -363,6 +363,52 @@ def test_fp8_quantize_matches_cpu(gpu):
     assert rel_err(back, x.float()) < 0.07  # e4m3: 3 mantissa bits
 
 
+@pytest.mark.parametrize("res", [False, True])
+def test_bn_apply_fp8_side_output(gpu, res):
+    """Delayed scaling: call 1 only measures |y|max; call 2 writes e4m3(y / (amax_1/448)) and the
+    scale; the ring rotates (prev, out, cleared) without a memset launch."""
+    from tensorflowdistributedlearning_amd.ops import bn as B, fp8 as F8
+    torch.manual_seed(21)
+    Cc = 64
+    x = torch.randn(64, 15, 17, Cc, device=gpu).bfloat16()  # > AMAX_SPREAD workgroups
+    r = torch.randn(64, 15, 17, Cc, device=gpu).bfloat16() if res else None
+    coef = torch.stack([torch.rand(Cc) + 0.5, torch.randn(Cc) * 0.1,
+                        torch.zeros(Cc), torch.ones(Cc)]).to(gpu)
+    ring = torch.zeros(3, F8.AMAX_SLOT, device=gpu)
+    ring[2] = 123.0  # stale value: must be cleared by call 1
+    slot = lambda k: float(ring[k].view(16, 64)[:, 0].max())
+    y1 = B.bn_apply(x, coef, r, True, (ring, 0, torch.zeros(1, device=gpu), False))
+    assert not hasattr(y1, "_tdl_fp8")
+    amax1 = float(y1.float().abs().max())
+    assert slot(1) == amax1 and slot(2) == 0.0
+    x2 = x * 0.5
+    y2 = B.bn_apply(x2, coef, r, True, (ring, 1, torch.zeros(1, device=gpu), True))
+    y8, sc = y2._tdl_fp8
+    assert abs(float(sc) - amax1 / 448) < 1e-7 * amax1
+    assert slot(2) == float(y2.float().abs().max()) and slot(0) == 0.0
+    back = F8.dequantize(y8, sc).cpu()
+    assert rel_err(back, y2.float().cpu()) < 0.07
+    assert torch.equal(y2, B.bn_apply(x2, coef, r, True))  # bf16 output unchanged
+
+
+def test_fp8_delayed_scaler(gpu):
+    """First call exact (primed), later calls use the previous call's amax and saturate."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    torch.manual_seed(22)
+    sc = F8.DelayedScaler()
+    x1 = torch.randn(1000, 64, device=gpu).bfloat16()
+    y1, s1 = sc.quantize(x1)
+    ref1, r1 = F8.quantize_e4m3(x1.cpu())
+    assert abs(float(s1) - float(r1)) <= 1e-6 * float(r1)
+    x2 = x1 * 2
+    y2, s2 = sc.quantize(x2)
+    assert abs(float(s2) - float(s1)) <= 1e-7  # scale from call 1
+    d2 = F8.dequantize(y2, s2).cpu()
+    assert float(d2.abs().max()) <= float(s1) * 448 * (1 + 1e-6)  # saturated at the old amax
+    y3, s3 = sc.quantize(x2)
+    assert abs(float(s3) - 2 * float(s1)) <= 1e-6 * float(s3)  # call 2 measured 2x
+
+
 @pytest.mark.parametrize("shape", [(8, 14, 14, 128, 256, 3, 3, 1, 1),     # C % 128 == 0: tap per step
                                    (8, 14, 14, 64, 128, 3, 3, 1, 1),      # 2 taps per 128-deep step
                                    (4, 15, 15, 256, 64, 1, 1, 2, 0),      # 1x1 s2, 256x64 config
@@ -386,3 +432,36 @@ def test_conv_fwd_fp8(gpu, shape):
     assert rel_err(stats[0], yb.sum(0)) < 1e-3
     # fp8 vs the bf16 conv of the unquantised data: quantisation error only
     assert rel_err(y, C.ref_conv_fwd(x.float(), w.float(), g)) < 0.08
+
+
+def test_fp8_flat_weights_one_launch(gpu):
+    """All fp8 weights of a flat buffer re-quantised by one launch per parameter version; the
+    first version is exact (primed), later versions use the previous amax."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    from tensorflowdistributedlearning_amd.models.params import FlatParams, version, bump_version
+    torch.manual_seed(23)
+    mod = torch.nn.Module()
+    mod.a = torch.nn.Parameter(torch.randn(64, 3, 3, 32))
+    mod.b = torch.nn.Parameter(torch.randn(40000, 16) * 5)  # > one chunk
+    mod.c = torch.nn.Parameter(torch.randn(7))               # not fp8
+    fp = FlatParams(mod, gpu)
+    fw = F8.flat_weights_for(mod.a)
+    assert fw.get(mod.a, version()) is None and fw.get(mod.b, version()) is None
+    bump_version()
+    for p in (mod.a, mod.b):
+        w8, s = fw.get(p, version())
+        ref8, rs = F8.quantize_e4m3(p._lowp.cpu())
+        assert abs(float(s) - float(rs)) <= 1e-6 * float(rs)
+        assert w8.shape == p.shape
+        assert rel_err(F8.dequantize(w8, s).cpu(), p._lowp.float().cpu()) < 0.07
+    with torch.no_grad():
+        mod.b.mul_(2)
+    fp.sync_lowp()
+    w8, s = fw.get(mod.b, version())
+    w8b, sb = fw.get(mod.b, version())  # same version: no relaunch, same views
+    assert w8b.data_ptr() == w8.data_ptr()
+    amax_old = float(mod.b._lowp.float().abs().max()) / 2  # bf16 copy: exact halving
+    assert abs(float(s) - amax_old / 448) <= 1e-5 * float(s)  # delayed: previous version's amax
+    fp.sync_lowp()
+    w8, s = fw.get(mod.b, version())
+    assert abs(float(s) - 2 * amax_old / 448) <= 1e-5 * float(s)

@@ -131,11 +131,13 @@ def test_residual_join_gpu_matches_plain_autograd(gpu):
     assert cos > 0.999, cos
 
 
-def test_resnet_fp8_forward_trains(gpu):
-    """fp8 (e4m3) forward GEMMs, bf16 backward: loss finite and falling on a fixed batch."""
+@pytest.mark.parametrize("fuse_bn", [False, True])
+def test_resnet_fp8_forward_trains(gpu, fuse_bn):
+    """fp8 (e4m3) forward GEMMs, bf16 backward: loss finite and falling on a fixed batch
+    (fuse_bn: conv inputs quantised by the producing BN with delayed scaling)."""
     torch.manual_seed(0)
     m = models.resnet18(num_classes=10)
-    n = models.enable_fp8(m)
+    n = models.enable_fp8(m, fuse_bn=fuse_bn)
     assert n >= 15
     tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01, momentum=0.9,
                                                           weight_decay=0.0))
