@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--comm", choices=["torch", "rccl"], default=os.environ.get("TDL_COMM", "torch"),
+                    help="gradient all-reduce backend: torch.distributed ProcessGroupNCCL (RCCL) or "
+                         "the native RCCL communicator with watchdog (parallel/rccl.py)")
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 (OCP e4m3, per-tensor scales) forward GEMMs on the CDNA4 "
                          "16x16x128 MFMA for every eligible conv; backward stays bf16")
@@ -56,7 +59,7 @@ def main():
                          "device events) to stderr")
     args = ap.parse_args()
 
-    ctx = init_distributed()
+    ctx = init_distributed(comm=args.comm)
     n = ctx.world_size
     if n != args.gpus and ctx.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}", file=sys.stderr)
@@ -72,7 +75,7 @@ def main():
         x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank)
         metric = "images/sec (whole node), reference DeepLab-ResNet 101x101x2 bf16"
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
-               "image": "101x101x2", "parallelism": f"dp{n}", "optimizer": "adam",
+               "image": "101x101x2", "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "adam",
                "loss": "lovasz_hinge"}
         base = REF_DEEPLAB_2GPU / 2 * n
     else:
@@ -90,7 +93,8 @@ def main():
                   f"{'fp8 (e4m3 fwd GEMMs, bf16 bwd)' if args.fp8 else 'bf16'}")
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
-               "parallelism": f"dp{n}", "optimizer": "sgd_momentum", "loss": "softmax_ce"}
+               "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "sgd_momentum",
+               "loss": "softmax_ce"}
         base = REF_PER_GPU_DERIVED * n
 
     def step():

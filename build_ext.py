@@ -69,7 +69,7 @@ def build(verbose=True, force=False):
     for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
         obj = os.path.join(OBJ, "rt_" + os.path.basename(src) + ".o")
         if force or _newer(src, obj, headers):
-            jobs.append([HIPCC, *common, "-pthread", "-c", "-o", obj, src])
+            jobs.append([HIPCC, *common, "-pthread", "-D__HIP_PLATFORM_AMD__=1", "-c", "-o", obj, src])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")
     if force or _newer(bsrc, bobj, headers):
@@ -90,7 +90,10 @@ def build(verbose=True, force=False):
         torch_lib = libdirs[0]
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
                 "-L" + torch_lib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip",
-                "-ltorch_hip", "-lamdhip64", "-lz", "-pthread", f"-Wl,-rpath,{torch_lib}"]
+                "-ltorch_hip", "-lamdhip64", "-lz", "-pthread", f"-Wl,-rpath,{torch_lib}",
+                # RCCL: torch ships librccl.so (soname librccl.so.1) and loads it first, so the
+                # native communicator (csrc/runtime/comm.cpp) shares torch's RCCL instance
+                "-L" + torch_lib, "-lrccl"]
         _run(link)
         if verbose:
             print(f"[build_ext] linked {os.path.relpath(out, ROOT)}", flush=True)

@@ -6,6 +6,7 @@
 
 #include "kernels/kernels.h"
 #include "runtime/loader.h"
+#include "runtime/comm.h"
 
 using torch::Tensor;
 using namespace tdl;
@@ -446,6 +447,88 @@ void upsample_bwd(Tensor dy, Tensor dx, Tensor ih, Tensor wh, Tensor iw, Tensor 
 
 
 // --------------------------------------------------------------------------- native data loader
+// ------------------------------------------------------------------------- native RCCL comm
+comm::DType comm_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case torch::kFloat32: return comm::DType::F32;
+    case torch::kBFloat16: return comm::DType::BF16;
+    case torch::kFloat16: return comm::DType::F16;
+    case torch::kFloat64: return comm::DType::F64;
+    case torch::kInt32: return comm::DType::I32;
+    case torch::kInt64: return comm::DType::I64;
+    case torch::kUInt8: return comm::DType::U8;
+    default: TORCH_CHECK(false, "unsupported dtype for RCCL: ", t.scalar_type());
+  }
+  return comm::DType::F32;
+}
+
+comm::Op comm_op(const std::string& op) {
+  if (op == "sum") return comm::Op::Sum;
+  if (op == "max") return comm::Op::Max;
+  if (op == "min") return comm::Op::Min;
+  if (op == "prod") return comm::Op::Prod;
+  if (op == "avg") return comm::Op::Avg;
+  TORCH_CHECK(false, "unknown reduce op ", op);
+  return comm::Op::Sum;
+}
+
+// Collectives run on a dedicated high-priority stream from torch's pool, ordered after the
+// current (compute) stream; the caching allocator is told the comm stream uses each buffer.
+struct PyComm {
+  std::unique_ptr<comm::Communicator> c;
+  c10::hip::HIPStream cs;
+  int device;
+
+  PyComm(py::bytes uid, int rank, int world, int dev, double timeout_s)
+      : cs(c10::hip::getStreamFromPool(true, dev)), device(dev) {
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)dev));
+    py::gil_scoped_release nogil;  // ncclCommInitRank blocks until every rank joined
+    c = std::make_unique<comm::Communicator>(std::string(uid), rank, world, dev, timeout_s);
+  }
+  void use(const Tensor& t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL buffers must be contiguous HIP tensors");
+    TORCH_CHECK(t.device().index() == device, "tensor on device ", t.device().index(),
+                ", communicator on ", device);
+    c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), cs);
+  }
+  int64_t all_reduce(Tensor t, const std::string& op) {
+    use(t);
+    return (int64_t)c->all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), comm_dtype(t), comm_op(op),
+                                  stream(), cs.stream());
+  }
+  int64_t broadcast(Tensor t, int root) {
+    use(t);
+    return (int64_t)c->broadcast(t.data_ptr(), t.data_ptr(), t.numel(), comm_dtype(t), root, stream(),
+                                 cs.stream());
+  }
+  int64_t reduce_scatter(Tensor in, Tensor out, const std::string& op) {
+    use(in);
+    use(out);
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel() * c->world(),
+                "reduce_scatter: in must hold world x out elements");
+    return (int64_t)c->reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), comm_dtype(in),
+                                      comm_op(op), stream(), cs.stream());
+  }
+  int64_t all_gather(Tensor in, Tensor out) {
+    use(in);
+    use(out);
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() && out.numel() == in.numel() * c->world(),
+                "all_gather: out must hold world x in elements");
+    return (int64_t)c->all_gather(in.data_ptr(), out.data_ptr(), in.numel(), comm_dtype(in), stream(),
+                                  cs.stream());
+  }
+  void wait(int64_t ticket) { c->wait((uint64_t)ticket, stream()); }
+  void synchronize() {
+    py::gil_scoped_release nogil;
+    c->synchronize();
+  }
+  // fault injection: delay the comm stream by `ms` (bounded spin kernel) — watchdog tests
+  int64_t debug_delay(double ms, bool track) {
+    debug_spin_launch(ms, cs.stream());
+    return track ? (int64_t)c->track("debug_delay", cs.stream()) : 0;
+  }
+};
+
 struct PyLoader {
   std::unique_ptr<tdl_rt::BatchLoader> impl;
   bool has_masks;
@@ -566,6 +649,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_glds_mode", &conv_glds_mode);
   m.def("fastdiv", [](uint32_t d) { auto f = make_fastdiv(d); return py::make_tuple(f.m, f.s); },
         "magic (m, s) with n / d == (n * m) >> s for 0 <= n < 2^31");
+  m.def("rccl_unique_id", []() { return py::bytes(comm::get_unique_id()); });
+  m.def("rccl_version", &comm::rccl_version);
+  py::class_<PyComm>(m, "RcclComm")
+      .def(py::init<py::bytes, int, int, int, double>(), py::arg("uid"), py::arg("rank"),
+           py::arg("world"), py::arg("device"), py::arg("timeout_s") = 600.0)
+      .def("all_reduce", &PyComm::all_reduce, py::arg("t"), py::arg("op") = "sum")
+      .def("broadcast", &PyComm::broadcast, py::arg("t"), py::arg("root") = 0)
+      .def("reduce_scatter", &PyComm::reduce_scatter, py::arg("inp"), py::arg("out"),
+           py::arg("op") = "sum")
+      .def("all_gather", &PyComm::all_gather)
+      .def("wait", &PyComm::wait)
+      .def("synchronize", &PyComm::synchronize)
+      .def("debug_delay", &PyComm::debug_delay, py::arg("ms"), py::arg("track") = false)
+      .def("abort", [](PyComm& p, const std::string& why) { p.c->abort(why); })
+      .def_property_readonly("error", [](PyComm& p) { return p.c->error(); })
+      .def_property_readonly("ok", [](PyComm& p) { return p.c->ok(); })
+      .def_property_readonly("outstanding", [](PyComm& p) { return p.c->outstanding(); })
+      .def_property_readonly("rank", [](PyComm& p) { return p.c->rank(); })
+      .def_property_readonly("world", [](PyComm& p) { return p.c->world(); });
   py::class_<PyLoader>(m, "BatchLoader")
       .def(py::init<std::vector<std::string>, std::vector<std::string>, int, bool, bool, bool,
                     int64_t, int, int, int, int, bool>(),

@@ -170,4 +170,7 @@ void upsample_bwd_launch(const bf16_t* dy, bf16_t* dx, const int* ih, const floa
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
                          int Wo, hipStream_t st);
 
+// fault injection: a 1-lane kernel that spins `ms` milliseconds (≤ 60 s) on stream st
+void debug_spin_launch(double ms, hipStream_t st);
+
 }  // namespace tdl

@@ -97,7 +97,10 @@ class GradBucketer:
         if self.comm_hook is not None:
             b.work = self.comm_hook(b, view)
         elif self.ctx is not None and self.ctx.is_distributed:
-            b.work = dist.all_reduce(view, async_op=True, group=self.group)
+            if getattr(self.ctx, "native", None) is not None:
+                b.work = self.ctx.all_reduce_async(view)  # native RCCL (parallel/rccl.py)
+            else:
+                b.work = dist.all_reduce(view, async_op=True, group=self.group)
         b.launched = True
 
     def finish(self):
@@ -111,6 +114,8 @@ class GradBucketer:
             b.launched = False
             b.pending = len(b.params)
         self.next_launch = 0
+        if self.ctx is not None and hasattr(self.ctx, "check"):
+            self.ctx.check()  # native comm watchdog: fail fast on timeout / RCCL error
 
     def describe(self):
         return [(b.index, len(b.params), b.nbytes) for b in self.buckets]

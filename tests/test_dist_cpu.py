@@ -143,3 +143,17 @@ def test_phase_timer_cpu():
     assert set(s) == {"forward", "backward", "comm_wait", "optimizer", "step"}
     assert s["forward"] > 0 and s["backward"] > 0 and abs(s["step"] - sum(
         s[k] for k in ("forward", "backward", "comm_wait", "optimizer"))) < 1e-6
+
+
+def test_native_comm_selector_cpu():
+    """comm="rccl" only engages the native communicator for GPU runs with world > 1."""
+    from tensorflowdistributedlearning_amd.parallel import dist as D
+    from tensorflowdistributedlearning_amd.parallel import rccl  # importable without a GPU
+    D.shutdown()
+    ctx = D.init_distributed(device_type="cpu", comm="rccl")
+    try:
+        assert ctx.native is None and not ctx.is_distributed
+        ctx.check()
+        assert issubclass(rccl.CommError, RuntimeError)
+    finally:
+        D.shutdown()

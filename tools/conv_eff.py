@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Per-conv achieved TFLOP/s from a rocprofv3 kernel trace of bench.py (last training step):
+forward convs are matched in forward order, dgrad/wgrad in reverse order, by kernel mode.
+python tools/conv_eff.py gpurun_out/prof_r50/run_kernel_trace.csv --model resnet50 --batch 256"""
+import argparse, csv, re, sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def conv_list(model, batch, image):
+    from tensorflowdistributedlearning_amd import models
+    from tensorflowdistributedlearning_amd.models.layers import Conv2d
+    m = models.build(model, num_classes=1000) if model != "xception41" else models.build(model)
+    out = []
+    def hook(mod, inp, o):
+        x = inp[0]
+        y = o[0] if isinstance(o, tuple) else o
+        N, H, W, C = x.shape
+        _, Ho, Wo, K = y.shape
+        fl = 2.0 * batch * Ho * Wo * K * C * mod.k[0] * mod.k[1]
+        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{mod.stride[0] if isinstance(mod.stride, tuple) else mod.stride}", fl))
+    for mod in m.modules():
+        if isinstance(mod, Conv2d):
+            mod.register_forward_hook(hook)
+    m.eval()
+    with torch.no_grad():
+        m(torch.zeros(1, image, image, 3))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--image", type=int, default=224)
+    a = ap.parse_args()
+    convs = conv_list(a.model, a.batch, a.image)
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+    seg = rows[idx[-2] + 1: idx[-1] + 1]
+    by = {0: [], 1: [], 2: []}
+    for r in seg:
+        mm = re.search(r"conv_(glds|gemm)_kernel<(\d)", r["Kernel_Name"])
+        if mm:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            by[int(mm.group(2))].append((d, mm.group(1)))
+    print(f"{len(convs)} convs; kernels fwd {len(by[0])} dgrad {len(by[1])} wgrad {len(by[2])}")
+    fw = by[0]
+    tot = {}
+    if len(fw) == len(convs):
+        print("forward:")
+        agg = {}
+        for (d, impl), (name, fl) in zip(fw, convs):
+            k = (name, impl)
+            e = agg.setdefault(k, [0, 0.0, fl])
+            e[0] += 1
+            e[1] += d
+        for (name, impl), (n, d, fl) in sorted(agg.items(), key=lambda x: -x[1][1]):
+            print(f"  {name:32s} {impl:5s} x{n:2d} {d / n:7.1f} us  {fl / (d / n) / 1e6:7.1f} TF/s  total {d:7.1f} us")
+    else:
+        print("forward count mismatch")
+
+
+if __name__ == "__main__":
+    main()
