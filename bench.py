@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 (OCP e4m3, per-tensor scales) forward GEMMs on the CDNA4 "
                          "16x16x128 MFMA for every eligible conv; backward stays bf16")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step as a HIP graph and replay it (single "
+                         "process; removes host launch overhead in launch-bound configs)")
     ap.add_argument("--profile-phases", action="store_true",
                     help="also print per-phase step times (forward/backward/comm_wait/optimizer, "
                          "device events) to stderr")
@@ -76,7 +79,7 @@ def main():
         metric = "images/sec (whole node), reference DeepLab-ResNet 101x101x2 bf16"
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
                "image": "101x101x2", "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "adam",
-               "loss": "lovasz_hinge"}
+               "loss": "lovasz_hinge", "hip_graph": args.graph}
         base = REF_DEEPLAB_2GPU / 2 * n
     else:
         per_gpu = args.batch or 256
@@ -94,17 +97,26 @@ def main():
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "sgd_momentum",
-               "loss": "softmax_ce"}
+               "loss": "softmax_ce", "hip_graph": args.graph}
         base = REF_PER_GPU_DERIVED * n
 
     def step():
         tr.train_step(x, y)
 
-    for i in range(args.warmup):
-        step()
-        if ctx.is_main and i == 0:
-            print(f"[bench] first step done ({args.model}, batch {per_gpu}/gpu, n={n})",
-                  file=sys.stderr, flush=True)
+    if args.graph:
+        if n > 1:
+            raise SystemExit("--graph is single-process (the bucketed all-reduce is eager)")
+        tr.capture(x, y, warmup=args.warmup)  # W eager warm-up steps, then the capture
+        step = tr.replay
+        step()  # first replay (graph upload) stays untimed
+        print(f"[bench] step captured as a HIP graph ({args.model}, batch {per_gpu}/gpu)",
+              file=sys.stderr, flush=True)
+    else:
+        for i in range(args.warmup):
+            step()
+            if ctx.is_main and i == 0:
+                print(f"[bench] first step done ({args.model}, batch {per_gpu}/gpu, n={n})",
+                      file=sys.stderr, flush=True)
     ctx.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)

@@ -187,8 +187,10 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad
   conv_wgrad_launch(a, plan, out.data_ptr<float>(), accumulate, st);
   if (bias_grad.has_value() && bias_grad->defined()) {
     CHECK_T((*bias_grad), torch::kFloat32);
-    hipMemsetAsync(bias_grad->data_ptr(), 0, a.K * sizeof(float), st);
-    colsum_launch(BF(dy), bias_grad->data_ptr<float>(), (long)a.Kg, a.K, st);
+    TORCH_CHECK(bias_grad->numel() == a.K, "bias_grad must have K elements");
+    auto part = torch::empty({(int64_t)colsum_blocks((long)a.Kg, a.K) * a.K}, out.options());
+    colsum_launch(BF(dy), bias_grad->data_ptr<float>(), part.data_ptr<float>(), (long)a.Kg, a.K,
+                  false, st);
   }
 }
 
@@ -207,9 +209,16 @@ void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor>
   CHECK_T(rmean, torch::kFloat32);
   CHECK_T(rvar, torch::kFloat32);
   TORCH_CHECK(!training || optf(stats) != nullptr, "training BN needs stats");
+  // beta may be the channel-padded view (physical C); the moving statistics cover the logical
+  // channels only
+  TORCH_CHECK(rmean.numel() == rvar.numel() && rmean.numel() <= beta.numel(), "bn_finalize shapes");
+  TORCH_CHECK(coef.numel() >= 4 * beta.numel(), "bn_finalize coef size");
+  if (gamma.has_value() && gamma->defined())
+    TORCH_CHECK(gamma->numel() == beta.numel(), "bn_finalize gamma / beta size");
   bn_finalize_launch(optf(stats), coef.data_ptr<float>(), optf(gamma), beta.data_ptr<float>(),
-                     rmean.data_ptr<float>(), rvar.data_ptr<float>(), beta.numel(), (float)count,
-                     (float)decay, (float)eps, training, stream());
+                     rmean.data_ptr<float>(), rvar.data_ptr<float>(), beta.numel(),
+                     (int)rmean.numel(), (float)count, (float)decay, (float)eps, training,
+                     stream());
 }
 
 // fp8 side output (delayed scaling): amax_ring is fp32[3, AMAX_SLOT]; slot `phase` holds the previous
@@ -364,23 +373,25 @@ void seg_metrics(Tensor labels, Tensor pred, Tensor score, Tensor acc, bool kagg
 
 // ----------------------------------------------------------------------------------- optimizers
 void sgd_momentum(Tensor p, Tensor g, Tensor m, c10::optional<Tensor> lowp, Tensor flags, double lr,
-                  double mu, double wd, double gs, bool nesterov) {
+                  double mu, double wd, double gs, bool nesterov, c10::optional<Tensor> lr_scale) {
   CHECK_T(p, torch::kFloat32);
   CHECK_T(g, torch::kFloat32);
   CHECK_T(m, torch::kFloat32);
   TORCH_CHECK(p.numel() % 64 == 0, "flat buffer must be 64-aligned");
   sgd_momentum_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), optbw(lowp),
-                      flags.data_ptr<uint8_t>(), p.numel(), lr, mu, wd, gs, nesterov, stream());
+                      flags.data_ptr<uint8_t>(), p.numel(), lr, optf(lr_scale), mu, wd, gs,
+                      nesterov, stream());
 }
 
 void adam(Tensor p, Tensor g, Tensor m, Tensor v, c10::optional<Tensor> lowp, Tensor flags,
-          double lr_t, double b1, double b2, double eps, double wd, double gs) {
+          double lr_t, double b1, double b2, double eps, double wd, double gs,
+          c10::optional<Tensor> lr_scale) {
   CHECK_T(p, torch::kFloat32);
   CHECK_T(g, torch::kFloat32);
   TORCH_CHECK(p.numel() % 64 == 0, "flat buffer must be 64-aligned");
   adam_launch(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
-              optbw(lowp), flags.data_ptr<uint8_t>(), p.numel(), lr_t, b1, b2, eps, wd, gs,
-              stream());
+              optbw(lowp), flags.data_ptr<uint8_t>(), p.numel(), lr_t, optf(lr_scale), b1, b2, eps,
+              wd, gs, stream());
 }
 
 // ------------------------------------------------------------------------------- depthwise conv

@@ -175,7 +175,8 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
 __global__ void finalize_kernel(const float* __restrict__ stats, float* __restrict__ coef,
                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                 float* __restrict__ rmean, float* __restrict__ rvar, int C,
-                                float count, float decay, float eps, int training) {
+                                int c_run, float count, float decay, float eps, int training) {
+  // channels [c_run, C) are physical padding (zero γ/β, zero input): no moving statistics
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float mean, var;
@@ -183,11 +184,13 @@ __global__ void finalize_kernel(const float* __restrict__ stats, float* __restri
     mean = stats[c] / count;
     var = fmaxf(stats[C + c] / count - mean * mean, 0.f);
     const float unb = count > 1.f ? var * count / (count - 1.f) : var;
-    rmean[c] = decay * rmean[c] + (1.f - decay) * mean;
-    rvar[c] = decay * rvar[c] + (1.f - decay) * unb;
+    if (c < c_run) {
+      rmean[c] = decay * rmean[c] + (1.f - decay) * mean;
+      rvar[c] = decay * rvar[c] + (1.f - decay) * unb;
+    }
   } else {
-    mean = rmean[c];
-    var = rvar[c];
+    mean = c < c_run ? rmean[c] : 0.f;
+    var = c < c_run ? rvar[c] : 1.f;
   }
   const float inv = rsqrtf(var + eps);
   const float g = gamma ? gamma[c] : 1.f;
@@ -412,10 +415,10 @@ void bn_stats_launch(const bf16_t* x, float* stats, long M, int C, hipStream_t s
 }
 
 void bn_finalize_launch(const float* stats, float* coef, const float* gamma, const float* beta,
-                        float* rmean, float* rvar, int C, float count, float decay, float eps,
-                        bool training, hipStream_t st) {
+                        float* rmean, float* rvar, int C, int c_run, float count, float decay,
+                        float eps, bool training, hipStream_t st) {
   hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, stats, coef, gamma,
-                     beta, rmean, rvar, C, count, decay, eps, training ? 1 : 0);
+                     beta, rmean, rvar, C, c_run, count, decay, eps, training ? 1 : 0);
 }
 
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,

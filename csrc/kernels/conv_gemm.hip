@@ -543,21 +543,87 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
-// column sums of a bf16 [P][K] matrix into fp32 out[K] (zeroed by caller): bias gradient
-__global__ void colsum_kernel(const bf16_t* __restrict__ x, float* __restrict__ out, long P, int K,
-                              long rows_per_block) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  const long r0 = blockIdx.y * rows_per_block;
-  const long r1 = min(P, r0 + rows_per_block);
-  float s = 0.f;
-  if (c < K)
-    for (long r = r0 + w; r < r1; r += 4) s += bf2f(x[r * K + c]);
-  red[w][threadIdx.x & 63] = s;
+// Bias gradient = column sums of a bf16 [P][K] matrix, in two deterministic launches without
+// atomics or a memset: colsum_part_kernel writes one fp32 partial row per row-block into a slab,
+// colsum_reduce_kernel sums the slab rows into out (overwrite, or accumulate).  Vector path
+// (K % 8 == 0): a lane owns 8 channels (one 16-B load per row, 4 rows in flight), the 4 waves of
+// a workgroup stride the rows and meet in LDS.
+template <bool VEC>
+__global__ void __launch_bounds__(256) colsum_part_kernel(const bf16_t* __restrict__ x,
+                                                         float* __restrict__ part, long P, int K,
+                                                         long rows_per_block) {
+  __shared__ float red[4][8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(P, r0 + rows_per_block);
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if constexpr (VEC) {
+    const int cv = blockIdx.y * 64 + lane;  // channel vector
+    if (cv < (K >> 3)) {
+      const bf16_t* base = x + cv * 8;
+      long r = r0 + w;
+      for (; r + 12 < r1; r += 16) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const uint4*)(base + (r + 4 * u) * K);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float f[8];
+          unpack8(v[u], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += f[j];
+        }
+      }
+      for (; r < r1; r += 4) {
+        float f[8];
+        unpack8(*(const uint4*)(base + r * K), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    }
+  } else {
+    const int c = blockIdx.y * 64 + lane;  // one channel per lane
+    if (c < K)
+      for (long r = r0 + w; r < r1; r += 4) s[0] += bf2f(x[r * K + c]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[w][j][lane] = s[j];
   __syncthreads();
-  if (w == 0 && c < K) atomicAdd(out + c, red[0][threadIdx.x] + red[1][threadIdx.x] +
-                                              red[2][threadIdx.x] + red[3][threadIdx.x]);
+  if (w == 0) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = red[0][j][lane] + red[1][j][lane] + red[2][j][lane] + red[3][j][lane];
+    float* dst = part + blockIdx.x * (long)K;
+    if constexpr (VEC) {
+      const int cv = blockIdx.y * 64 + lane;
+      if (cv < (K >> 3)) {
+        *(float4*)(dst + cv * 8) = make_float4(t[0], t[1], t[2], t[3]);
+        *(float4*)(dst + cv * 8 + 4) = make_float4(t[4], t[5], t[6], t[7]);
+      }
+    } else {
+      const int c = blockIdx.y * 64 + lane;
+      if (c < K) dst[c] = t[0];
+    }
+  }
+}
+
+// out[c] (+)= Σ_b part[b][c]: 64 channels per workgroup, the 4 waves split the partial rows
+__global__ void __launch_bounds__(256) colsum_reduce_kernel(const float* __restrict__ part,
+                                                           float* __restrict__ out, int nb, int K,
+                                                           int accumulate) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float t = 0.f;
+  if (c < K)
+    for (int b = w; b < nb; b += 4) t += part[(long)b * K + c];
+  red[w][lane] = t;
+  __syncthreads();
+  if (w == 0 && c < K) {
+    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[c] = accumulate ? out[c] + s : s;
+  }
 }
 
 template <int MODE, int BM, int BN, bool AL, bool ST, bool BI>
@@ -768,10 +834,27 @@ void splitk_reduce_launch(const float* slab, float* out, long n, int splits, boo
   }
 }
 
-void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st) {
-  const long rpb = 1024;
-  dim3 grid(cdiv(K, 64), (int)std::max<long>(1, (P + rpb - 1) / rpb));
-  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, st, x, out, P, K, rpb);
+int colsum_blocks(long P, int K) {
+  // row blocks of ≥ 64 rows, at most 64 of them (≈ one workgroup per CU across the channel
+  // chunks, and a short serial sum per thread in colsum_reduce_kernel)
+  const int ychunks = (K % 8 == 0) ? cdiv(K / 8, 64) : cdiv(K, 64);
+  const long want = std::max<long>(8, std::min<long>(64, 256 / ychunks));
+  return (int)std::max<long>(1, std::min<long>(want, (P + 63) / 64));
+}
+
+void colsum_launch(const bf16_t* x, float* out, float* part, long P, int K, bool accumulate,
+                   hipStream_t st) {
+  const int nb = colsum_blocks(P, K);
+  const long rpb = (P + nb - 1) / nb;
+  if (K % 8 == 0) {
+    dim3 grid(nb, cdiv(K / 8, 64));
+    hipLaunchKernelGGL(colsum_part_kernel<true>, grid, dim3(256), 0, st, x, part, P, K, rpb);
+  } else {
+    dim3 grid(nb, cdiv(K, 64));
+    hipLaunchKernelGGL(colsum_part_kernel<false>, grid, dim3(256), 0, st, x, part, P, K, rpb);
+  }
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cdiv(K, 64)), dim3(256), 0, st, part, out, nb, K,
+                     accumulate ? 1 : 0);
 }
 
 }  // namespace tdl

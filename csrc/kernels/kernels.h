@@ -90,13 +90,16 @@ void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas
 void fp8_multi_quantize_launch(const bf16_t* src, uint8_t* dst, const long* chunks, int nchunks,
                                float* rings, float* scales, int phase, bool prime, hipStream_t st);
 void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st);
-void colsum_launch(const bf16_t* x, float* out, long P, int K, hipStream_t st);
+// bias gradient: out[K] (+)= column sums of x[P][K]; part = fp32 scratch of colsum_blocks(P, K)·K
+int colsum_blocks(long P, int K);
+void colsum_launch(const bf16_t* x, float* out, float* part, long P, int K, bool accumulate,
+                   hipStream_t st);
 
 // batch norm ---------------------------------------------------------------------------------
 void bn_stats_launch(const bf16_t* x, float* stats, long M, int C, hipStream_t st);
 void bn_finalize_launch(const float* stats, float* coef, const float* gamma, const float* beta,
-                        float* rmean, float* rvar, int C, float count, float decay, float eps,
-                        bool training, hipStream_t st);
+                        float* rmean, float* rvar, int C, int c_run, float count, float decay,
+                        float eps, bool training, hipStream_t st);
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st, uint8_t* y8 = nullptr,
                      const float* amax_prev = nullptr, float* scale_out = nullptr,
@@ -134,12 +137,13 @@ void seg_metrics_launch(const void* labels, int label_kind, const float* pred, f
                         float* acc, int B, int P, bool kaggle, hipStream_t st);
 
 // optimizers ---------------------------------------------------------------------------------
+// lr_scale (optional device scalar) multiplies lr / lr_t inside the kernel (HIP-graph replays)
 void sgd_momentum_launch(float* p, const float* g, float* mom, bf16_t* lowp, const uint8_t* flags,
-                         long n, float lr, float mu, float wd, float gscale, bool nesterov,
-                         hipStream_t st);
+                         long n, float lr, const float* lr_scale, float mu, float wd, float gscale,
+                         bool nesterov, hipStream_t st);
 void adam_launch(float* p, const float* g, float* m, float* v, bf16_t* lowp, const uint8_t* flags,
-                 long n, float lr_t, float b1, float b2, float eps, float wd, float gscale,
-                 hipStream_t st);
+                 long n, float lr_t, const float* lr_scale, float b1, float b2, float eps, float wd,
+                 float gscale, hipStream_t st);
 
 // depthwise conv -----------------------------------------------------------------------------
 struct DwArgs {

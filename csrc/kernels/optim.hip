@@ -1,7 +1,9 @@
 // Fused optimizer updates over the flat parameter buffers (models/params.py): one launch updates
 // the whole model — fp32 master, fp32 slots, bf16 compute copy — reading the data-parallel
 // gradient scale and a per-64-element weight-decay flag.  float4 vectorised (offsets of every
-// parameter are 64-element aligned, the buffer length is a multiple of 64).
+// parameter are 64-element aligned, the buffer length is a multiple of 64).  An optional device
+// scalar multiplies the learning rate (HIP-graph replays: the host writes the step's lr there
+// instead of baking it into the captured kernel arguments).
 #include "common.h"
 #include "kernels.h"
 
@@ -12,7 +14,9 @@ constexpr int NT = 256;
 
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                            bf16_t* __restrict__ lowp, const uint8_t* __restrict__ flags, long n4,
-                           float lr, float mu, float wd, float gs, int nesterov) {
+                           float lr, const float* __restrict__ lr_scale, float mu, float wd,
+                           float gs, int nesterov) {
+  if (lr_scale) lr *= *lr_scale;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const float d = flags[(i * 4) >> 6] ? wd : 0.f;
     float4 pv = ((float4*)p)[i];
@@ -35,8 +39,10 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, f
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, bf16_t* __restrict__ lowp,
-                            const uint8_t* __restrict__ flags, long n4, float lr_t, float b1,
-                            float b2, float eps, float wd, float gs) {
+                            const uint8_t* __restrict__ flags, long n4, float lr_t,
+                            const float* __restrict__ lr_scale, float b1, float b2, float eps,
+                            float wd, float gs) {
+  if (lr_scale) lr_t *= *lr_scale;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
     const float d = flags[(i * 4) >> 6] ? wd : 0.f;
     float4 pv = ((float4*)p)[i];
@@ -66,17 +72,17 @@ inline int blocks_for(long n) { return (int)std::min<long>(2048, std::max<long>(
 }  // namespace
 
 void sgd_momentum_launch(float* p, const float* g, float* mom, bf16_t* lowp, const uint8_t* flags,
-                         long n, float lr, float mu, float wd, float gscale, bool nesterov,
-                         hipStream_t st) {
+                         long n, float lr, const float* lr_scale, float mu, float wd, float gscale,
+                         bool nesterov, hipStream_t st) {
   hipLaunchKernelGGL(sgd_kernel, dim3(blocks_for(n / 4)), dim3(NT), 0, st, p, g, mom, lowp, flags,
-                     n / 4, lr, mu, wd, gscale, nesterov ? 1 : 0);
+                     n / 4, lr, lr_scale, mu, wd, gscale, nesterov ? 1 : 0);
 }
 
 void adam_launch(float* p, const float* g, float* m, float* v, bf16_t* lowp, const uint8_t* flags,
-                 long n, float lr_t, float b1, float b2, float eps, float wd, float gscale,
-                 hipStream_t st) {
+                 long n, float lr_t, const float* lr_scale, float b1, float b2, float eps, float wd,
+                 float gscale, hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(n / 4)), dim3(NT), 0, st, p, g, m, v, lowp, flags,
-                     n / 4, lr_t, b1, b2, eps, wd, gscale);
+                     n / 4, lr_t, lr_scale, b1, b2, eps, wd, gscale);
 }
 
 }  // namespace tdl

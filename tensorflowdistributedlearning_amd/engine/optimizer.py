@@ -23,6 +23,21 @@ class _FlatOptimizer:
         self.weight_decay = weight_decay
         self.lr_schedule = lr_schedule
         self.step_count = 0
+        self.lr_dev = None  # graph mode: fp32 [1] device lr the kernel reads (set_device_lr)
+
+    def set_device_lr(self, enabled=True):
+        """HIP-graph mode: the update kernel reads the learning rate from a device scalar that
+        :meth:`prepare_replay` refreshes before every replay (a captured launch keeps its host
+        arguments frozen, and the schedule / Adam bias correction change every step)."""
+        self.lr_dev = (torch.zeros(1, device=self.flat.master.device, dtype=torch.float32)
+                       if enabled else None)
+
+    def prepare_replay(self):
+        """Write this step's effective lr into the device scalar (stream-ordered fill)."""
+        self.lr_dev.fill_(self._effective_lr(self.step_count))
+
+    def _effective_lr(self, step):
+        return self.lr_at(step)
 
     def lr_at(self, step):
         return self.lr_schedule(step) if self.lr_schedule is not None else self.base_lr
@@ -32,7 +47,7 @@ class _FlatOptimizer:
         return self.lr_at(self.step_count)
 
     def step(self, grad_scale=1.0):
-        self._update(self.lr_at(self.step_count), grad_scale)
+        self._update(self._effective_lr(self.step_count), grad_scale)
         self.step_count += 1
         _params.bump_version()
 
@@ -55,8 +70,10 @@ class FusedSGD(_FlatOptimizer):
 
     def _update(self, lr, grad_scale):
         f = self.flat
+        if self.lr_dev is not None:
+            lr = 1.0
         _ops.sgd_momentum_(f.master, f.grad, self.mom, f.lowp, f.decay_flags, lr, self.momentum,
-                           self.weight_decay, grad_scale, self.nesterov)
+                           self.weight_decay, grad_scale, self.nesterov, self.lr_dev)
 
     def state_tensors(self):
         return {"Momentum": self.mom}
@@ -70,12 +87,16 @@ class FusedAdam(_FlatOptimizer):
         self.m = torch.zeros_like(flat.master)
         self.v = torch.zeros_like(flat.master)
 
-    def _update(self, lr, grad_scale):
-        t = self.step_count + 1
-        lr_t = lr * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
+    def _effective_lr(self, step):
+        t = step + 1  # TF: bias correction folded into the step size
+        return self.lr_at(step) * math.sqrt(1 - self.beta2 ** t) / (1 - self.beta1 ** t)
+
+    def _update(self, lr_t, grad_scale):
         f = self.flat
+        if self.lr_dev is not None:
+            lr_t = 1.0
         _ops.adam_(f.master, f.grad, self.m, self.v, f.lowp, f.decay_flags, lr_t, self.beta1,
-                   self.beta2, self.eps, self.weight_decay, grad_scale)
+                   self.beta2, self.eps, self.weight_decay, grad_scale, self.lr_dev)
 
     def state_tensors(self):
         return {"Adam": self.m, "Adam_1": self.v}

@@ -11,6 +11,7 @@ import time
 
 import torch
 
+from ..models import params as _params
 from ..models.params import FlatParams
 from ..parallel.bucketer import GradBucketer
 from ..parallel.dist import get_context
@@ -82,6 +83,7 @@ class Trainer:
         self.global_step = 0
         self.train_mode = True  # False: BN uses moving statistics while training (frozen BN)
         self.timer = PhaseTimer(self.device) if profile_phases else None
+        self.graph = None  # HIP graph of one whole step (capture / replay)
 
     # ------------------------------------------------------------------------------------------
     def broadcast_state(self):
@@ -92,6 +94,11 @@ class Trainer:
         self.flat.sync_lowp()
 
     def train_step(self, x, y):
+        if self.graph is not None:
+            raise RuntimeError("this Trainer runs a captured graph: use replay()")
+        return self._step(x, y)
+
+    def _step(self, x, y):
         t = self.timer
         self.model.train(self.train_mode)
         workspace.reset(self.device)
@@ -120,6 +127,59 @@ class Trainer:
             t.end_step()
         self.global_step += 1
         return loss.detach(), out.detach()
+
+    # ------------------------------------------------------------------------------------------
+    def capture(self, x, y, warmup=3):
+        """Record one whole training step — forward, backward, gradient delivery, the fused
+        optimizer update — as a HIP graph over static copies of ``x``/``y``; :meth:`replay` then
+        runs a step with a single graph launch instead of ~10³ host-side kernel launches (the
+        launch-bound small-batch configs, e.g. the reference preset at 32 images per GPU).
+
+        The step must be host-synchronisation-free (it is: losses stay on the device) and its
+        Python-side choices static across steps; the learning rate moves to a device scalar
+        (optimizer ``set_device_lr``).  Single-process only: the bucketed all-reduce stays eager.
+        The fp8 delayed-scaling state rotates on the host, so fp8 models are not capturable."""
+        if self.device.type != "cuda":
+            raise RuntimeError("graph capture needs a GPU")
+        if self.bucketer is not None:
+            raise RuntimeError("graph capture is single-process (the bucketed all-reduce is eager)")
+        if any(getattr(m, "fp8", False) or getattr(m, "emit_fp8", False)
+               for m in self.model.modules()):
+            raise RuntimeError("fp8 delayed scaling keeps host-side state: not capturable")
+        self.timer = None
+        self.static_x = x.detach().clone()
+        self.static_y = y.detach().clone()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):  # warm-up: caches, workspace arena, kernel attributes
+            for _ in range(warmup):
+                self._step(self.static_x, self.static_y)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        self.optimizer.set_device_lr(True)
+        step_count, global_step = self.optimizer.step_count, self.global_step
+        _params.bump_version()  # derived weight copies (channel padding) refresh inside the graph
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.graph_out = self._step(self.static_x, self.static_y)
+        # capture records without executing: the host-side counters did not really advance
+        self.optimizer.step_count, self.global_step = step_count, global_step
+        self.graph = g
+        return self
+
+    def replay(self, x=None, y=None):
+        """One captured training step (``x``/``y`` are copied into the static inputs if given).
+        Returns the static (loss, output) tensors, overwritten by the next replay."""
+        if x is not None:
+            self.static_x.copy_(x, non_blocking=True)
+        if y is not None:
+            self.static_y.copy_(y, non_blocking=True)
+        self.optimizer.prepare_replay()
+        self.graph.replay()
+        self.optimizer.step_count += 1
+        self.global_step += 1
+        _params.bump_version()
+        return self.graph_out
 
     @torch.no_grad()
     def eval_step(self, x):

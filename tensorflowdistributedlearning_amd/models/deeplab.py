@@ -44,30 +44,35 @@ class _Subsample(nn.Module):
 class BetaUnit(nn.Module):
     """``bottleneck`` / ``basic_block`` unit of core/resnet.py (hybrid pre/post activation)."""
 
-    def __init__(self, cin, depth, depth_bottleneck, stride, rate, block_type, bn_kw, pad_to=None):
+    def __init__(self, cin, depth, depth_bottleneck, stride, rate, block_type, bn_kw, align=None):
+        """``align``: channel counts that are not a multiple of it (the reference's 258-wide
+        block2 bottleneck, defect D7) are carried physically padded with zero channels, so every conv of the unit
+        runs on the aligned LDS-DMA kernels; parameters keep their logical shapes."""
         super().__init__()
         self.block_type = block_type
         self.stride = stride
-        self.preact = BNAct(cin, relu=True, **bn_kw)
+        pad = dict(pad_cin_to=align, pad_cout_to=align)
+        self.preact = BNAct(cin, relu=True, c_phys=_round_up(cin, align), **bn_kw)
         out_c = depth if block_type == "bottleneck" else depth_bottleneck
         self.out_channels = out_c
         if out_c == cin:
             self.shortcut = None
             self.subsample = _Subsample(stride)
         else:
-            self.shortcut = Conv2d(cin, out_c, 1, stride, 0, bias=True)
+            self.shortcut = Conv2d(cin, out_c, 1, stride, 0, bias=True, **pad)
             self.subsample = None
-        cbn = dict(bn_decay=bn_kw["decay"], bn_eps=bn_kw["eps"], bn_scale=bn_kw["scale"])
+        cbn = dict(bn_decay=bn_kw["decay"], bn_eps=bn_kw["eps"], bn_scale=bn_kw["scale"], **pad)
         if block_type == "bottleneck":
             self.conv1 = ConvBN(cin, depth_bottleneck, 1, 1, 0, relu=True, **cbn)
             # 3×3 (rate) at stride 1 + subsample(stride) == stride-s conv, symmetric padding
             self.conv2 = ConvBN(depth_bottleneck, depth_bottleneck, 3, stride, "sym", rate,
                                 relu=True, **cbn)
-            self.conv3 = Conv2d(depth_bottleneck, depth, 1, 1, 0, bias=True)
+            self.conv3 = Conv2d(depth_bottleneck, depth, 1, 1, 0, bias=True, **pad)
         else:
             self.conv1 = ConvBN(cin, depth_bottleneck, 3, stride, "sym", 1, relu=True, **cbn)
             self.conv2 = None
-            self.conv3 = Conv2d(depth_bottleneck, depth_bottleneck, 3, 1, "sym", rate, bias=True)
+            self.conv3 = Conv2d(depth_bottleneck, depth_bottleneck, 3, 1, "sym", rate, bias=True,
+                                **pad)
 
     def forward(self, x, end_points=None, name=None):
         preact = self.preact(x)
@@ -78,8 +83,17 @@ class BetaUnit(nn.Module):
         r = self.conv3(r)
         if end_points is not None and name is not None:
             last = "conv3" if self.block_type == "bottleneck" else "conv2"
-            end_points[f"{name}/bottleneck_v2/{last}"] = r
+            end_points[f"{name}/bottleneck_v2/{last}"] = _logical(r, self.out_channels)
         return add_relu(sc, r)
+
+
+def _round_up(c, multiple):
+    return c if not multiple else (c + multiple - 1) // multiple * multiple
+
+
+def _logical(t, c):
+    """The logical channels of a (possibly channel-padded) NHWC tensor."""
+    return t if t.shape[-1] == c else t[..., :c]
 
 
 class SplitSeparableConv(nn.Module):
@@ -104,7 +118,8 @@ class DeepLabResNet(nn.Module):
     def __init__(self, model_name="model", in_channels=2, output_stride=8, base_depth=256,
                  input_shape=(101, 101), n_blocks=(3, 4, 6), block_type="bottleneck",
                  batch_norm_decay=0.99, batch_norm_epsilon=0.001, batch_norm_scale=True,
-                 weight_decay=0.001, multi_grid=(1, 2, 1), block_widths=(128, 258, 512)):
+                 weight_decay=0.001, multi_grid=(1, 2, 1), block_widths=(128, 258, 512),
+                 channel_align=8):
         super().__init__()
         if len(n_blocks) != 3:
             raise ValueError("Expect n_blocks to have length 3.")
@@ -145,11 +160,11 @@ class DeepLabResNet(nn.Module):
             for u in units:
                 if target is not None and current_stride == target:
                     unit = BetaUnit(cin, u["depth"], u["depth_bottleneck"], 1, rate * u["unit_rate"],
-                                    block_type, bn_kw)
+                                    block_type, bn_kw, channel_align)
                     rate *= u["stride"]
                 else:
                     unit = BetaUnit(cin, u["depth"], u["depth_bottleneck"], u["stride"],
-                                    u["unit_rate"], block_type, bn_kw)
+                                    u["unit_rate"], block_type, bn_kw, channel_align)
                     current_stride *= u["stride"]
                 cin = unit.out_channels
                 mods.append(unit)
@@ -168,7 +183,10 @@ class DeepLabResNet(nn.Module):
         # decoder
         b1_out = block_widths[0] * 4 if block_type == "bottleneck" else block_widths[0]
         self.decoder_conv_1x1 = ConvBN(b1_out, base_depth, 1, 1, 0, relu=True, **cbn)
-        self.decoder_conv_3x3 = Conv2d(2 * base_depth, 1, 3, 1, "SAME", bias=True)
+        # one logit channel: computed as 8 (zero weights / bias beyond the first) so the conv runs
+        # on the aligned kernels instead of the per-element generic path
+        self.decoder_conv_3x3 = Conv2d(2 * base_depth, 1, 3, 1, "SAME", bias=True,
+                                       pad_cout_to=channel_align)
 
     def forward(self, x, return_end_points=False):
         if x.shape[-1] != self.conv1_1.conv._cin_store:
@@ -180,8 +198,8 @@ class DeepLabResNet(nn.Module):
         for bname, mods in zip(self.block_names, self.blocks):
             for ui, unit in enumerate(mods):
                 net = unit(net, end_points, f"{root}/{bname}/unit_{ui + 1}")
-            end_points[f"{root}/{bname}"] = net
-        atrous = end_points[f"{root}/block4"]
+            end_points[f"{root}/{bname}"] = _logical(net, mods[-1].out_channels)
+        atrous = end_points[f"{root}/block4"].contiguous()  # a copy only for unaligned widths
         size = (atrous.shape[1], atrous.shape[2])
         a1 = self.assp_conv_1x1(atrous)
         a2 = self.assp_conv_3x3_1(atrous)
@@ -192,11 +210,11 @@ class DeepLabResNet(nn.Module):
         a5 = upsample(a5, size)
         assp = self.assp_out(torch.cat([a1, a2, a3, a4, a5], dim=-1))
         last = 3 if self.block_type == "bottleneck" else 2
-        b1 = end_points[f"{root}/block1/unit_1/bottleneck_v2/conv{last}"]
+        b1 = end_points[f"{root}/block1/unit_1/bottleneck_v2/conv{last}"].contiguous()
         assp_up = upsample(assp, (b1.shape[1], b1.shape[2]))
         dec = self.decoder_conv_1x1(b1)
         dec = torch.cat([dec, assp_up], dim=-1)
-        dec = self.decoder_conv_3x3(dec)
+        dec = _logical(self.decoder_conv_3x3(dec), 1).contiguous()
         out = upsample(dec, self.input_shape)
         return (out, end_points) if return_end_points else out
 

@@ -16,8 +16,12 @@ from ..ops.conv import ConvGeom, conv2d, same_padding, symmetric_padding
 from ..ops.bn import batch_norm_act
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
-from ..ops.common import compute_weight
+from ..ops.common import compute_weight, flat_view
 from . import params as _params
+
+
+def _round_up(c, multiple):
+    return c if not multiple else (c + multiple - 1) // multiple * multiple
 
 
 # ----------------------------------------------------------------------------------------------
@@ -80,11 +84,14 @@ class Conv2d(nn.Module):
 
     ``pad_cin_to``: the bf16 compute copy of the weight is zero-padded along Cin to this multiple
     (the kernels need Cin % 8 == 0; used for the 3-channel RGB / 2-channel TGS stems whose input
-    tensors are padded the same way).  The fp32 parameter keeps its true shape.
+    tensors are padded the same way).  ``pad_cout_to``: likewise along Cout, so the output tensor
+    carries zero channels up to the multiple (the reference preset's 258-wide block2 bottleneck,
+    defect D7, runs on the LDS-DMA kernels as 264 channels).  The fp32 parameter keeps its true
+    shape; gradients are un-padded on delivery.
     """
 
     def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, bias=False, relu=False,
-                 init="he_tf", init_std=None, pad_cin_to=None):
+                 init="he_tf", init_std=None, pad_cin_to=None, pad_cout_to=None):
         super().__init__()
         kh, kw = (k, k) if isinstance(k, int) else k
         self.cin, self.cout, self.k = cin, cout, (kh, kw)
@@ -110,34 +117,46 @@ class Conv2d(nn.Module):
         else:
             self.bias = None
         self.pad_cin_to = pad_cin_to
-        self._cin_store = (cin if not pad_cin_to else
-                           (cin + pad_cin_to - 1) // pad_cin_to * pad_cin_to)
+        self._cin_store = _round_up(cin, pad_cin_to)
+        self._cout_store = _round_up(cout, pad_cout_to)
         self._padded = None
         self._padded_version = -1
         self._geom_cache = {}
 
     # weight handling for the kernels -----------------------------------------------------------
     def grad_needs_unpad(self):
-        return self._cin_store != self.cin
+        return self._cin_store != self.cin or self._cout_store != self.cout
 
     def padded_weight_shape(self):
-        return (self.cout, self.k[0], self.k[1], self._cin_store)
+        return (self._cout_store, self.k[0], self.k[1], self._cin_store)
 
     def unpad_grad(self, dw):
-        return dw[..., : self.cin]
+        return dw[: self.cout, ..., : self.cin]
 
     def compute_weight(self, dtype):
         w = compute_weight(self.weight, dtype)
-        if self._cin_store == self.cin:
+        if not self.grad_needs_unpad():
             return w
-        v = _params.version()
-        if (self._padded is None or self._padded_version != v or self._padded.dtype != dtype
+        # one persistent zero-padded copy, refreshed in place once per parameter version (the
+        # padding never changes; a fixed address also keeps HIP-graph replays valid)
+        if (self._padded is None or self._padded.dtype != dtype
                 or self._padded.device != w.device):
-            padded = torch.zeros(self.padded_weight_shape(), dtype=dtype, device=w.device)
-            padded[..., : self.cin] = w
-            self._padded = padded
+            self._padded = torch.zeros(self.padded_weight_shape(), dtype=dtype, device=w.device)
+            self._padded_version = -1
+        v = _params.version()
+        if self._padded_version != v:
+            self._padded[: self.cout, ..., : self.cin].copy_(w)
             self._padded_version = v
         return self._padded
+
+    def compute_bias(self):
+        """fp32 bias as the kernels read it, ``_cout_store`` long with zero padding channels (the
+        flat master buffer's slack when flat-backed, else a padded copy)."""
+        b = self.bias.detach()
+        if self._cout_store == self.cout:
+            return b
+        v = flat_view(self.bias, self._cout_store)
+        return v if v is not None else torch.nn.functional.pad(b, (0, self._cout_store - self.cout))
 
     def geom(self, H, W):
         g = self._geom_cache.get((H, W))
@@ -156,7 +175,7 @@ class Conv2d(nn.Module):
         from ..ops.fp8 import DelayedScaler, flat_weights_for
         from .params import version
         v = version()
-        if self._cin_store == self.cin:  # the weight is the flat bf16 buffer slice itself
+        if not self.grad_needs_unpad():  # the weight is the flat bf16 buffer slice itself
             fw = flat_weights_for(self.weight)
             got = fw.get(self.weight, v) if fw is not None else None
             if got is not None:
@@ -187,11 +206,16 @@ class Conv2d(nn.Module):
 
 class BatchNorm(nn.Module):
     """BN over the channel (last) axis with TF-style moving averages
-    (``m ← decay·m + (1−decay)·batch``).  ``scale=False`` drops γ (slim ``scale`` flag)."""
+    (``m ← decay·m + (1−decay)·batch``).  ``scale=False`` drops γ (slim ``scale`` flag).
 
-    def __init__(self, c, decay=0.997, eps=1e-5, scale=True, zero_init=False):
+    ``c_phys`` > ``c``: the input carries zero padding channels up to ``c_phys`` (channel-padded
+    convs, :class:`Conv2d` ``pad_cout_to``); γ/β are read zero-padded so those channels stay
+    exactly zero, and the moving statistics keep their logical size ``c``."""
+
+    def __init__(self, c, decay=0.997, eps=1e-5, scale=True, zero_init=False, c_phys=None):
         super().__init__()
         self.c, self.decay, self.eps = c, decay, eps
+        self.c_phys = c_phys or c
         self.gamma = nn.Parameter(torch.zeros(c) if zero_init else torch.ones(c)) if scale else None
         if self.gamma is not None:
             self.gamma._no_decay = True
@@ -200,12 +224,25 @@ class BatchNorm(nn.Module):
         self.register_buffer("running_mean", torch.zeros(c))
         self.register_buffer("running_var", torch.ones(c))
 
+    def phys_params(self):
+        """(γ, β) as the kernels read them: fp32 vectors of ``c_phys`` with zero padding (views of
+        the flat master buffer's slack when flat-backed, else padded copies)."""
+        g = None if self.gamma is None else self.gamma.detach()
+        b = self.beta.detach()
+        if self.c_phys == self.c:
+            return g, b
+
+        def pad(p, t):
+            v = flat_view(p, self.c_phys)
+            return v if v is not None else torch.nn.functional.pad(t, (0, self.c_phys - self.c))
+        return (None if g is None else pad(self.gamma, g)), pad(self.beta, b)
+
     emit_fp8 = False  # set by models.enable_fp8: also emit an e4m3 copy for the fp8 consumer conv
 
     def fp8_state(self, x):
         """(amax ring, phase, scale, emit) for the delayed-scaling e4m3 side output of bn_apply
         (ops/bn.py, ops/fp8.DelayedScaler), or None where it does not apply."""
-        if not (x.is_cuda and self.c % 16 == 0):
+        if not (x.is_cuda and self.c_phys % 16 == 0):
             return None
         from ..ops.fp8 import DelayedScaler
         sc = self.__dict__.get("_fp8")
@@ -223,11 +260,13 @@ class ConvBN(nn.Module):
 
     def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, relu=True,
                  bn_decay=0.997, bn_eps=1e-5, bn_scale=True, zero_init_gamma=False, init="he_tf",
-                 init_std=None, pad_cin_to=None):
+                 init_std=None, pad_cin_to=None, pad_cout_to=None):
         super().__init__()
         self.conv = Conv2d(cin, cout, k, stride, padding, dilation, bias=False, relu=False,
-                           init=init, init_std=init_std, pad_cin_to=pad_cin_to)
-        self.bn = BatchNorm(cout, bn_decay, bn_eps, bn_scale, zero_init_gamma)
+                           init=init, init_std=init_std, pad_cin_to=pad_cin_to,
+                           pad_cout_to=pad_cout_to)
+        self.bn = BatchNorm(cout, bn_decay, bn_eps, bn_scale, zero_init_gamma,
+                            c_phys=self.conv._cout_store)
         self.relu = relu
 
     def forward(self, x, residual=None, join=None, res_join=None):
@@ -242,9 +281,9 @@ class ConvBN(nn.Module):
 class BNAct(nn.Module):
     """standalone BN(+ReLU) — slim.batch_norm(activation_fn=relu) pre-activation / postnorm."""
 
-    def __init__(self, c, decay=0.997, eps=1e-5, scale=True, relu=True):
+    def __init__(self, c, decay=0.997, eps=1e-5, scale=True, relu=True, c_phys=None):
         super().__init__()
-        self.bn = BatchNorm(c, decay, eps, scale)
+        self.bn = BatchNorm(c, decay, eps, scale, c_phys=c_phys)
         self.relu = relu
 
     def forward(self, x):

@@ -81,6 +81,8 @@ class FlatParams:
             p._lowp = self.lowp[o:o + n].view(p.shape) if self.lowp is not None else None
             p._flat_offset = o
             p._flat_lowp = self.lowp
+            p._flat_master = self.master
+            p._flat_grad = self.grad
             p._grad_fresh = True
         self.sync_lowp()
 

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import torch
 
-from .common import on_gpu, ext, deliver_grad, grad_target
+from .common import on_gpu, ext, deliver_grad, grad_target, flat_view
 from . import workspace
 
 
@@ -40,8 +40,11 @@ def bn_stats(x, stats=None):
 
 
 def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps, training):
-    """Returns fp32 [4, C] = (scale, shift, mean, invstd); updates moving stats in training."""
+    """Returns fp32 [4, C] = (scale, shift, mean, invstd); updates moving stats in training.
+    ``gamma``/``beta`` may be channel-padded (C physical channels) while the moving statistics
+    cover the first ``running_mean.numel()`` (logical) channels only."""
     C = beta.shape[0]
+    cr = running_mean.numel()
     if on_gpu(beta):
         coef = torch.empty((4, C), device=beta.device, dtype=torch.float32)
         ext().bn_finalize(stats if training else None, coef, gamma, beta, running_mean, running_var,
@@ -53,11 +56,11 @@ def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps
         var = (stats[1] / count - mean * mean).clamp_min(0.0)
         with torch.no_grad():
             unbiased = var * (count / max(count - 1, 1))
-            running_mean.mul_(decay).add_((1 - decay) * mean)
-            running_var.mul_(decay).add_((1 - decay) * unbiased)
+            running_mean.mul_(decay).add_((1 - decay) * mean[:cr])
+            running_var.mul_(decay).add_((1 - decay) * unbiased[:cr])
     else:
-        mean = running_mean.float()
-        var = running_var.float()
+        mean = torch.nn.functional.pad(running_mean.float(), (0, C - cr))
+        var = torch.nn.functional.pad(running_var.float(), (0, C - cr), value=1.0)
     invstd = torch.rsqrt(var + eps)
     scale = g * invstd
     shift = beta.detach().float() - mean * scale
@@ -145,11 +148,13 @@ class _BatchNormActFn(torch.autograd.Function):
         if training:
             if stats is None or stats.numel() == 0:
                 stats = bn_stats(x)
-        coef = bn_finalize(stats, count, gamma, beta, bn.running_mean, bn.running_var,
+        gp, bp = _phys_params(bn, gamma, beta)
+        coef = bn_finalize(stats, count, gp, bp, bn.running_mean, bn.running_var,
                            bn.decay, bn.eps, training)
         fp8 = bn.fp8_state(x) if getattr(bn, "emit_fp8", False) else None
         y = bn_apply(x, coef, residual, relu, fp8)
         ctx.count = count
+        ctx.bn = bn
         ctx.training = training
         ctx.has_res = residual is not None
         ctx.res_join = res_join if residual is not None else None
@@ -164,34 +169,53 @@ class _BatchNormActFn(torch.autograd.Function):
         x, y, coef, gamma, beta = ctx.saved_tensors
         dy = dy.contiguous()
         relu = ctx.relu
+        C = x.shape[-1]  # physical channels (≥ beta.numel() when channel-padded)
+        c = beta.numel()
         if not ctx.training:
             # eval-mode backward (rare): treat statistics as constants
-            C = x.shape[-1]
             g = dy.float().reshape(-1, C)
             if relu:
                 g = g * _relu_mask(relu, y, x, coef, C)
             dx = (g * coef[0]).reshape(x.shape).to(x.dtype)
             xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
             if gamma is not None and gamma.requires_grad:
-                deliver_grad(gamma, (g * xhat).sum(0))
+                deliver_grad(gamma, (g * xhat).sum(0)[:c])
             if beta.requires_grad:
-                deliver_grad(beta, g.sum(0))
+                deliver_grad(beta, g.sum(0)[:c])
             dres = g.reshape(dy.shape).to(dy.dtype) if ctx.has_res else None
             return dx, None, None, None, _join_res(ctx, dres), None, None, None, None
         red = bn_bwd_reduce(dy, y, x, coef, relu)
         want_g = gamma is not None and gamma.requires_grad
         want_b = beta.requires_grad
-        gt, gfresh = grad_target(gamma) if want_g else (None, False)
-        bt, bfresh = grad_target(beta) if want_b else (None, False)
+        gt, gfresh = _grad_target_phys(gamma, C) if want_g else (None, False)
+        bt, bfresh = _grad_target_phys(beta, C) if want_b else (None, False)
         direct_g = on_gpu(dy) and gt is not None and gfresh
         direct_b = on_gpu(dy) and bt is not None and bfresh
-        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gamma, ctx.count, relu, ctx.has_res,
+        gp, _ = _phys_params(ctx.bn, gamma, beta)
+        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, ctx.count, relu, ctx.has_res,
                                 gt if direct_g else None, bt if direct_b else None)
         if want_g:
-            deliver_grad(gamma, None if direct_g else red[1], written=direct_g)
+            deliver_grad(gamma, None if direct_g else red[1][:c], written=direct_g)
         if want_b:
-            deliver_grad(beta, None if direct_b else red[0], written=direct_b)
+            deliver_grad(beta, None if direct_b else red[0][:c], written=direct_b)
         return dx, None, None, None, _join_res(ctx, dres), None, None, None, None
+
+
+def _phys_params(bn, gamma, beta):
+    """γ/β padded to the physical channel count of a channel-padded BN (models.layers.BatchNorm
+    ``c_phys``); the parameters themselves otherwise."""
+    if getattr(bn, "c_phys", None) not in (None, beta.numel()):
+        return bn.phys_params()
+    return gamma, beta
+
+
+def _grad_target_phys(p, C):
+    """grad_target for a gradient of C ≥ p.numel() channels: the flat gradient buffer's slack
+    after p takes the padding channels (their gradient is exactly zero)."""
+    t, fresh = grad_target(p)
+    if t is not None and C != p.numel():
+        t = flat_view(p, C, "grad")
+    return t, fresh
 
 
 def _join_res(ctx, dres):

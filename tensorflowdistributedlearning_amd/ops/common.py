@@ -63,6 +63,23 @@ def deliver_grad(p: torch.Tensor, g: torch.Tensor | None = None, written: bool =
         hook(p)
 
 
+def flat_view(p: torch.Tensor, n: int, which: str = "master"):
+    """``n`` ≥ p.numel() fp32 elements of p's flat buffer starting at p (``which``: "master" data or
+    "grad"), or None when p is not flat-backed or its 64-aligned slot is shorter than ``n``.
+
+    The slack between p.numel() and the aligned slot belongs to p and stays zero (models/params.py:
+    zero-initialised, zero gradient, so the optimizer never moves it), which is what lets
+    channel-padded layers read γ/β/bias as one padded vector and write their padded gradients
+    straight into the flat gradient buffer."""
+    buf = getattr(p, "_flat_master" if which == "master" else "_flat_grad", None)
+    if buf is None:
+        return None
+    o = p._flat_offset
+    if n > (p.numel() + 63) // 64 * 64 or o + n > buf.numel():
+        return None
+    return buf[o:o + n]
+
+
 def reset_grad_state(params):
     for p in params:
         p._grad_fresh = True

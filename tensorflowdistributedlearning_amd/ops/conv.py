@@ -21,7 +21,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
-from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view
 from . import workspace
 
 
@@ -198,7 +198,8 @@ class _Conv2dFn(torch.autograd.Function):
         stats = None
         if want_stats:
             stats = workspace.zeros((2, w.shape[0]), x.device)
-        b = None if bias is None else bias.detach()
+        b = None if bias is None else (layer.compute_bias() if layer is not None
+                                       else bias.detach())
         if layer is not None and getattr(layer, "fp8", False) and b is None and on_gpu(x):
             # fp8 forward (weights + activations e4m3, per-tensor scales); backward stays bf16
             pre = getattr(x, "_tdl_fp8", None)  # e4m3 copy emitted by the producing BN
@@ -246,9 +247,12 @@ class _Conv2dFn(torch.autograd.Function):
         want_bias = bias is not None and bias.requires_grad
         bias_buf, bias_direct = None, False
         if want_bias:
+            nb = dy.shape[-1]  # physical output channels (> bias.numel() when channel-padded)
             bt, bfresh = grad_target(bias)
+            if bt is not None and nb != bias.numel():
+                bt = flat_view(bias, nb, "grad")  # the zero slack after the bias takes the pad
             bias_direct = bt is not None and bfresh
-            bias_buf = bt if bias_direct else torch.empty(bias.shape, device=dy.device,
+            bias_buf = bt if bias_direct else torch.empty(nb, device=dy.device,
                                                           dtype=torch.float32)
         if weight.requires_grad:
             target, fresh = grad_target(weight)
@@ -268,7 +272,7 @@ class _Conv2dFn(torch.autograd.Function):
             if bias_direct:
                 deliver_grad(bias, written=True)
             else:
-                deliver_grad(bias, bias_buf)
+                deliver_grad(bias, bias_buf[: bias.numel()])
         return dx, None, None, None, None, None, None, None
 
 

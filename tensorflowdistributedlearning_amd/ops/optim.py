@@ -34,12 +34,15 @@ def _flags(decay_flags, n):
 
 
 def sgd_momentum_(master, grad, mom, lowp, decay_flags, lr, momentum, weight_decay,
-                  grad_scale=1.0, nesterov=False):
-    """g' = g·grad_scale + wd·p·flag;  v = μv + g';  p -= lr·(g' + μv if nesterov else v)."""
+                  grad_scale=1.0, nesterov=False, lr_scale=None):
+    """g' = g·grad_scale + wd·p·flag;  v = μv + g';  p -= lr·(g' + μv if nesterov else v).
+    ``lr_scale``: optional fp32 [1] device tensor multiplying ``lr`` (read by the kernel)."""
     if on_gpu(master):
         ext().sgd_momentum(master, grad, mom, lowp, decay_flags, float(lr), float(momentum),
-                           float(weight_decay), float(grad_scale), bool(nesterov))
+                           float(weight_decay), float(grad_scale), bool(nesterov), lr_scale)
         return
+    if lr_scale is not None:
+        lr = lr * float(lr_scale)
     g = grad * grad_scale + weight_decay * _flags(decay_flags, master.numel()) * master
     mom.mul_(momentum).add_(g)
     upd = g + momentum * mom if nesterov else mom
@@ -49,13 +52,15 @@ def sgd_momentum_(master, grad, mom, lowp, decay_flags, lr, momentum, weight_dec
 
 
 def adam_(master, grad, m, v, lowp, decay_flags, lr_t, beta1, beta2, eps, weight_decay=0.0,
-          grad_scale=1.0):
+          grad_scale=1.0, lr_scale=None):
     """TF Adam: m = β1 m + (1-β1) g; v = β2 v + (1-β2) g²; p -= lr_t·m/(√v + ε), with
-    lr_t = lr·√(1-β2^t)/(1-β1^t) computed on the host."""
+    lr_t = lr·√(1-β2^t)/(1-β1^t) computed on the host (times the optional device ``lr_scale``)."""
     if on_gpu(master):
         ext().adam(master, grad, m, v, lowp, decay_flags, float(lr_t), float(beta1), float(beta2),
-                   float(eps), float(weight_decay), float(grad_scale))
+                   float(eps), float(weight_decay), float(grad_scale), lr_scale)
         return
+    if lr_scale is not None:
+        lr_t = lr_t * float(lr_scale)
     g = grad * grad_scale + weight_decay * _flags(decay_flags, master.numel()) * master
     m.mul_(beta1).add_((1 - beta1) * g)
     v.mul_(beta2).add_((1 - beta2) * g * g)

@@ -118,3 +118,44 @@ def test_residual_gradient_join_matches_autograd(depth):
             gradjoin.ENABLED = True
     for a, b in zip(*grads):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_deeplab_channel_padding_is_exact(flat):
+    """Physical channel padding of the 258-wide block2 (defect D7; the LDS-DMA conv kernels
+    need C % 8 == 0): the padded model gives the same logits, parameter gradients and moving
+    statistics as the unpadded one, both through standalone parameters and through the flat
+    buffers (where γ/β/bias are read from and their gradients written into the aligned slack)."""
+    from tensorflowdistributedlearning_amd.models.params import FlatParams
+    torch.manual_seed(0)
+    kw = dict(model_name="m", input_shape=(33, 33), n_blocks=(1, 2, 1), base_depth=16)
+    ref = models.DeepLabResNet(channel_align=None, **kw)
+    pad = models.DeepLabResNet(channel_align=8, **kw)
+    pad.load_state_dict(ref.state_dict())
+    assert count(pad) == count(ref)
+    assert pad.blocks[1][0].conv2.conv.padded_weight_shape() == (264, 3, 3, 264)
+    assert pad.blocks[1][0].conv3.padded_weight_shape() == (1032, 1, 1, 264)
+    flats = [FlatParams(m, "cpu", lowp_dtype=None) for m in (ref, pad)] if flat else None
+    x = torch.randn(2, 33, 33, 2)
+    res = []
+    for m in (ref, pad):
+        m.train()
+        out, ep = m(x, return_end_points=True)
+        out.float().pow(2).mean().backward()
+        res.append((out, ep, [p.grad.clone() for p in m.parameters()]))
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-4, atol=1e-5)
+    assert ep["m/resnet_v2/block2"].shape[-1] == 1032
+    torch.testing.assert_close(res[0][1]["m/resnet_v2/block2"], res[1][1]["m/resnet_v2/block2"],
+                               rtol=1e-4, atol=1e-5)
+    for (name, a), b in zip(ref.named_parameters(), res[1][2]):
+        torch.testing.assert_close(res[0][2][[n for n, _ in ref.named_parameters()].index(name)],
+                                   b, rtol=2e-3, atol=1e-5)
+    for a, b in zip(ref.buffers(), pad.buffers()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    if flat:  # the padding slack of every flat slot is still zero
+        f = flats[1]
+        for p, o in zip(f.params, f.offsets):
+            n = p.numel()
+            end = o + (n + 63) // 64 * 64
+            assert f.master[o + n:end].abs().max() == 0 if end > o + n else True
+            assert f.grad[o + n:end].abs().max() == 0 if end > o + n else True

@@ -145,3 +145,74 @@ def test_resnet_fp8_forward_trains(gpu, fuse_bn):
     losses = [float(tr.train_step(x, y)[0]) for _ in range(12)]
     assert all(l == l for l in losses), losses
     assert min(losses[-3:]) < losses[0], losses
+
+
+def test_deeplab_channel_padding_gpu_matches_unpadded(gpu):
+    """The reference preset with its 258-wide block2 carried as 264 physical channels (LDS-DMA
+    kernels, flat-buffer slack for γ/β/bias) vs the unpadded generic-kernel path: same logits and
+    gradients within bf16 tolerance.  BN runs on moving statistics (frozen) for the comparison:
+    with batch statistics of a 4-image batch the two kernel paths' bf16 rounding differences are
+    amplified chaotically through 60 BN layers (cos ≈ 0.97 either way), see
+    test_gpu_step_matches_cpu_reference; one training-mode step then checks the moving statistics
+    and the zero slack."""
+    torch.manual_seed(5)
+    kw = dict(model_name="m", input_shape=(65, 65))
+    a = models.DeepLabResNet(channel_align=None, **kw)
+    b = models.DeepLabResNet(channel_align=8, **kw)
+    b.load_state_dict(a.state_dict())
+    opt = dict(lr=0.0)
+    ta = Trainer(a, lovasz_hinge, gpu, "adam", opt)
+    tb = Trainer(b, lovasz_hinge, gpu, "adam", opt)
+    x, y = segmentation_batch(4, size=(65, 65), device=gpu)
+    ta.train_mode = tb.train_mode = False
+    la, oa = ta.train_step(x, y)
+    lb, ob = tb.train_step(x, y)
+    cos = torch.nn.functional.cosine_similarity(oa.float().flatten(), ob.float().flatten(), dim=0)
+    assert cos.item() > 0.999, cos.item()
+    gcos = torch.nn.functional.cosine_similarity(ta.flat.grad, tb.flat.grad, dim=0).item()
+    assert gcos > 0.99, gcos
+    ta.train_mode = tb.train_mode = True
+    ta.train_step(x, y)
+    tb.train_step(x, y)
+    for (n, ra), rb in zip(a.named_buffers(), b.buffers()):
+        assert ra.shape == rb.shape
+        if "blocks.1" in n:  # block2: the padded BN layers
+            torch.testing.assert_close(ra, rb, rtol=0.1, atol=0.05)
+    # the slack after every parameter stays zero in the flat buffers
+    f = tb.flat
+    for p, o in zip(f.params, f.offsets):
+        n = p.numel()
+        assert float(f.grad[o + n:o + (n + 63) // 64 * 64].abs().sum()) == 0.0
+        assert float(f.master[o + n:o + (n + 63) // 64 * 64].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_graph_replay_matches_eager(gpu, opt):
+    """A HIP-graph-captured training step (Trainer.capture / replay) follows the same trajectory
+    as eager steps: parameters after 3 replays match 3 more eager steps of an identical twin
+    (device-side learning rate incl. Adam's per-step bias correction)."""
+    torch.manual_seed(7)
+    kw = dict(model_name="m", input_shape=(33, 33), n_blocks=(1, 1, 1))
+    a = models.DeepLabResNet(**kw)
+    b = models.DeepLabResNet(**kw)
+    b.load_state_dict(a.state_dict())
+    okw = dict(lr=1e-3) if opt == "adam" else dict(lr=0.01, momentum=0.9)
+    ta = Trainer(a, lovasz_hinge, gpu, opt, okw)
+    tb = Trainer(b, lovasz_hinge, gpu, opt, okw)
+    # frozen BN: batch statistics of a 4-image batch (fp32 atomics, non-associative) would let the
+    # two runs drift apart chaotically within a few steps even eager-vs-eager
+    ta.train_mode = tb.train_mode = False
+    x, y = segmentation_batch(4, size=(33, 33), device=gpu)
+    tb.capture(x, y, warmup=2)
+    for _ in range(2):
+        ta.train_step(x, y)
+    assert ta.optimizer.step_count == tb.optimizer.step_count == 2
+    for _ in range(3):
+        la, _ = ta.train_step(x, y)
+        lb, _ = tb.replay()
+    torch.cuda.synchronize()
+    assert tb.optimizer.step_count == 5 and tb.global_step == 5
+    torch.testing.assert_close(float(lb), float(la), rtol=2e-2, atol=2e-3)
+    cos = torch.nn.functional.cosine_similarity(ta.flat.master, tb.flat.master, dim=0).item()
+    assert cos > 0.9999, cos
+    assert (ta.flat.master - tb.flat.master).abs().max().item() < 5e-3

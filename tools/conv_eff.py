@@ -10,7 +10,12 @@ import torch
 def conv_list(model, batch, image):
     from tensorflowdistributedlearning_amd import models
     from tensorflowdistributedlearning_amd.models.layers import Conv2d
-    m = models.build(model, num_classes=1000) if model != "xception41" else models.build(model)
+    if model == "deeplab_ref":
+        m = models.DeepLabResNet(model_name="model", input_shape=(image, image))
+        cin = 2
+    else:
+        m = models.build(model, num_classes=1000) if model != "xception41" else models.build(model)
+        cin = 3
     out = []
     def hook(mod, inp, o):
         x = inp[0]
@@ -18,13 +23,15 @@ def conv_list(model, batch, image):
         N, H, W, C = x.shape
         _, Ho, Wo, K = y.shape
         fl = 2.0 * batch * Ho * Wo * K * C * mod.k[0] * mod.k[1]
-        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{mod.stride[0] if isinstance(mod.stride, tuple) else mod.stride}", fl))
+        st = mod.stride[0] if isinstance(mod.stride, tuple) else mod.stride
+        dl = mod.dilation[0]
+        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{st}" + (f" d{dl}" if dl > 1 else ""), fl))
     for mod in m.modules():
         if isinstance(mod, Conv2d):
             mod.register_forward_hook(hook)
     m.eval()
     with torch.no_grad():
-        m(torch.zeros(1, image, image, 3))
+        m(torch.zeros(1, image, image, cin))
     return out
 
 
@@ -34,10 +41,11 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--marker", default="sgd_kernel", help="optimizer kernel delimiting steps")
     a = ap.parse_args()
     convs = conv_list(a.model, a.batch, a.image)
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     seg = rows[idx[-2] + 1: idx[-1] + 1]
     by = {0: [], 1: [], 2: []}
     for r in seg:
@@ -60,6 +68,13 @@ def main():
             print(f"  {name:32s} {impl:5s} x{n:2d} {d / n:7.1f} us  {fl / (d / n) / 1e6:7.1f} TF/s  total {d:7.1f} us")
     else:
         print("forward count mismatch")
+    for mode, nm in ((1, "dgrad"), (2, "wgrad")):
+        agg = {}
+        for d, impl in by[mode]:
+            e = agg.setdefault(impl, [0, 0.0])
+            e[0] += 1
+            e[1] += d
+        print(f"{nm}: " + ", ".join(f"{impl} x{n} {d:.1f} us" for impl, (n, d) in sorted(agg.items())))
 
 
 if __name__ == "__main__":
