@@ -226,7 +226,7 @@ void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor>
 // for the next step — no separate memset launch.
 void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu,
               c10::optional<Tensor> y8, c10::optional<Tensor> amax_ring, int64_t phase,
-              c10::optional<Tensor> scale_out) {
+              c10::optional<Tensor> scale_out, c10::optional<Tensor> mask) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   CHECK_T(coef, torch::kFloat32);
@@ -247,8 +247,26 @@ void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool r
       y8p = (uint8_t*)y8->data_ptr();
     }
   }
+  uint8_t* maskp = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(C % 8 == 0 && mask->is_cuda() && mask->element_size() == 1 &&
+                mask->is_contiguous() && mask->numel() * 8 == x.numel(),
+                "relu bit mask: uint8 [numel/8], C % 8 == 0");
+    maskp = (uint8_t*)mask->data_ptr();
+  }
   bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu,
-                  stream(), y8p, prev, optfw(scale_out), out, zero);
+                  stream(), y8p, prev, optfw(scale_out), out, zero, maskp);
+}
+
+// relu mode 3: `y` is the uint8 bit mask bn_apply wrote (vector kernels only: C % 8 == 0 and
+// C / 8 <= 256), passed through the y pointer slot
+const bf16_t* mask_or_y(const c10::optional<Tensor>& y, const Tensor& x, int64_t relu) {
+  if (relu != 3) return optb(y);
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(y.has_value() && y->defined() && y->is_cuda() && y->element_size() == 1 &&
+              y->is_contiguous() && y->numel() * 8 == x.numel() && C % 8 == 0 && C <= 2048,
+              "relu mask mode 3 needs the uint8 bit mask and C % 8 == 0, C <= 2048");
+  return (const bf16_t*)y->data_ptr();
 }
 
 void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, int64_t relu) {
@@ -257,8 +275,8 @@ void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Te
   CHECK_T(red, torch::kFloat32);
   const int64_t C = x.size(-1);
   TORCH_CHECK(relu != 1 || (y.has_value() && y->defined()), "relu mask mode 1 needs y");
-  bn_bwd_reduce_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
-                       x.numel() / C, C, (int)relu, stream());
+  bn_bwd_reduce_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(),
+                       red.data_ptr<float>(), x.numel() / C, C, (int)relu, stream());
 }
 
 void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red,
@@ -269,7 +287,7 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   const int64_t C = x.size(-1);
-  bn_bwd_apply_launch(BF(dy), optb(y), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
+  bn_bwd_apply_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
                       optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
                       C, (float)count, (int)relu, stream());
 }
@@ -633,7 +651,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("res"), py::arg("y"),
         py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_ring") = py::none(),
-        py::arg("phase") = 0, py::arg("scale_out") = py::none());
+        py::arg("phase") = 0, py::arg("scale_out") = py::none(), py::arg("mask") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("relu_bwd", &relu_bwd);
@@ -647,8 +665,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("lovasz_hinge", &lovasz_hinge);
   m.def("seg_metrics", &seg_metrics);
-  m.def("sgd_momentum", &sgd_momentum);
-  m.def("adam", &adam);
+  m.def("sgd_momentum", &sgd_momentum, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("lowp"),
+        py::arg("flags"), py::arg("lr"), py::arg("mu"), py::arg("wd"), py::arg("gs"),
+        py::arg("nesterov"), py::arg("lr_scale") = py::none());
+  m.def("adam", &adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lowp"),
+        py::arg("flags"), py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+        py::arg("wd"), py::arg("gs"), py::arg("lr_scale") = py::none());
   m.def("dwconv_fwd", &dwconv_fwd);
   m.def("dwconv_dgrad", &dwconv_dgrad);
   m.def("dwconv_wgrad", &dwconv_wgrad);

@@ -5,7 +5,9 @@
 //   bn_stats       Σx, Σx² (when the producer conv did not fuse them into its epilogue)
 //   bn_finalize    mean, invstd, scale=γ·invstd, shift=β−mean·scale; moving averages (TF decay)
 //   bn_apply       y = act(x·scale + shift [+ res])
-//   bn_bwd_reduce  Σg, Σg·x̂   (g = dy·[y>0] when the forward had a ReLU)
+//   bn_bwd_reduce  Σg, Σg·x̂   (g = dy·[y>0] when the forward had a ReLU; the mask comes from y
+//                  (relu 1), from x·scale+shift (2, no residual) or from a 1-bit-per-element mask
+//                  the forward apply wrote (3, residual BN: saves re-reading y twice)
 //   bn_bwd_apply   dx = γ·invstd·(g − Σg/M − x̂·Σg·x̂/M);  dres = g
 #include "common.h"
 #include "kernels.h"
@@ -93,6 +95,7 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
     long r = r0 + rl;
     for (; r < r1; r += U * rpp) {
       uint4 la[U], lx[U], ly[U];
+      uint32_t lm[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long rr = r + u * rpp;
@@ -100,6 +103,7 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
         la[u] = *(const uint4*)(a + off);
         if (KIND == 1) lx[u] = *(const uint4*)(x + off);
         if (KIND == 1 && relu == 1) ly[u] = *(const uint4*)(y + off);
+        if (KIND == 1 && relu == 3) lm[u] = ((const uint8_t*)y)[off >> 3];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -123,6 +127,9 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
         } else if (relu == 2) {  // y = relu(x·scale + shift): the mask without reading y
 #pragma unroll
           for (int j = 0; j < 8; ++j) va[j] = vx[j] * sc[j] + sh[j] > 0.f ? va[j] : 0.f;
+        } else if (relu == 3) {  // bit mask written by the forward apply (1/16 of y's bytes)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) va[j] = (lm[u] >> j) & 1u ? va[j] : 0.f;
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -222,7 +229,8 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ amax_prev,
                                                        float* __restrict__ scale_out,
                                                        float* __restrict__ amax_out,
-                                                       float* __restrict__ amax_zero) {
+                                                       float* __restrict__ amax_zero,
+                                                       uint8_t* __restrict__ mask) {
   float inv8 = 0.f, vmax = 0.f;
   bool emit8 = false;
   if (amax_out) {
@@ -264,6 +272,14 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
     }
     const uint4 packed = pack8(v);
     ((uint4*)y)[i] = packed;
+    if (mask) {  // ReLU mask of the stored bf16 values, one bit per element (backward relu mode 3)
+      float q[8];
+      unpack8(packed, q);
+      uint32_t b = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b |= (q[j] > 0.f ? 1u : 0u) << j;
+      mask[i] = (uint8_t)b;
+    }
     if (amax_out) {
       float q[8];
       unpack8(packed, q);  // quantise the stored bf16 values (what the bf16 path would read)
@@ -357,6 +373,10 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     } else if (relu == 2) {  // mask recomputed from x (no residual): one tensor read saved
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = vx[j] * Sc[j] + Sh[j] > 0.f ? g[j] : 0.f;
+    } else if (relu == 3) {  // bit mask from the forward apply (residual BN: y not re-read)
+      const uint32_t b = ((const uint8_t*)y)[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (b >> j) & 1u ? g[j] : 0.f;
     }
     if (dres) ((uint4*)dres)[i] = pack8(g);
     float o[8];
@@ -423,11 +443,11 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st, uint8_t* y8, const float* amax_prev,
-                     float* scale_out, float* amax_out, float* amax_zero) {
+                     float* scale_out, float* amax_out, float* amax_zero, uint8_t* mask) {
   const long n = M * C;
   if (C % 8 == 0) {
     hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, x, coef, res, y,
-                       n / 8, C, relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero);
+                       n / 8, C, relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask);
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
                        C, relu ? 1 : 0);

@@ -700,6 +700,21 @@ void conv_fwd_launch(const ConvArgs& a0, hipStream_t st) {
   }
 }
 
+// zero a byte range (multiple of 4) with a kernel rather than hipMemsetAsync: an ordinary kernel
+// node under HIP-graph capture, ordered on `st` like every other launch of the step
+__global__ void zero_fill_kernel(uint32_t* __restrict__ p, long n4) {
+  const long n16 = n4 >> 2;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256)
+    ((uint4*)p)[i] = make_uint4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x < (n4 & 3)) p[n16 * 4 + threadIdx.x] = 0u;
+}
+
+static void zero_fill(void* p, uint32_t bytes, hipStream_t st) {
+  const long n4 = bytes / 4;
+  const int blocks = (int)std::min<long>(2048, std::max<long>(1, (n4 / 4 + 255) / 256));
+  hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)p, n4);
+}
+
 void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   const bool masked = (a.sh > 1 && a.dh > 1) || (a.sw > 1 && a.dw > 1) ||
@@ -757,7 +772,7 @@ void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   int nz = ncls;
   while (nz > 0 && a.cls_Th[nz - 1] * a.cls_Tw[nz - 1] == 0) --nz;
   // (when accumulating into an existing dx the zero classes simply keep their values)
-  if (nz < ncls && !a.beta) (void)hipMemsetAsync(a.out, 0, (size_t)a.out_bytes, st);
+  if (nz < ncls && !a.beta) zero_fill(a.out, a.out_bytes, st);
   ncls = nz;
   if (ncls == 0) return;
   a.ncls = ncls;

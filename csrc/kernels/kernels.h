@@ -103,9 +103,10 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st, uint8_t* y8 = nullptr,
                      const float* amax_prev = nullptr, float* scale_out = nullptr,
-                     float* amax_out = nullptr, float* amax_zero = nullptr);
+                     float* amax_out = nullptr, float* amax_zero = nullptr,
+                     uint8_t* mask = nullptr);  // mask: 1 bit per element of y > 0 (C % 8 == 0)
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                          float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0
+                          float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0, 3 bit mask (y = uint8 mask, C % 8 == 0, C <= 2048)
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,

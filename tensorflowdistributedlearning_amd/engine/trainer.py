@@ -149,19 +149,21 @@ class Trainer:
         self.timer = None
         self.static_x = x.detach().clone()
         self.static_y = y.detach().clone()
+        self.graph_arena = workspace.ZeroArena()  # private: its addresses are baked in
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side):  # warm-up: caches, workspace arena, kernel attributes
-            for _ in range(warmup):
-                self._step(self.static_x, self.static_y)
-        torch.cuda.current_stream(self.device).wait_stream(side)
-        torch.cuda.synchronize(self.device)
-        self.optimizer.set_device_lr(True)
-        step_count, global_step = self.optimizer.step_count, self.global_step
-        _params.bump_version()  # derived weight copies (channel padding) refresh inside the graph
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.graph_out = self._step(self.static_x, self.static_y)
+        with workspace.use_arena(self.graph_arena):
+            with torch.cuda.stream(side):  # warm-up: caches, arena size, kernel attributes
+                for _ in range(warmup):
+                    self._step(self.static_x, self.static_y)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            torch.cuda.synchronize(self.device)
+            self.optimizer.set_device_lr(True)
+            step_count, global_step = self.optimizer.step_count, self.global_step
+            _params.bump_version()  # derived weight copies (channel padding) refresh in-graph
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.graph_out = self._step(self.static_x, self.static_y)
         # capture records without executing: the host-side counters did not really advance
         self.optimizer.step_count, self.global_step = step_count, global_step
         self.graph = g

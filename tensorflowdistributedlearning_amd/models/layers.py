@@ -17,6 +17,7 @@ from ..ops.bn import batch_norm_act
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
 from ..ops.common import compute_weight, flat_view
+from ..ops.fp8 import DelayedScaler, flat_weights_for
 from . import params as _params
 
 
@@ -172,9 +173,7 @@ class Conv2d(nn.Module):
     def fp8_weight(self, w_lowp):
         """e4m3 copy of the weight + its scale, re-quantised once per optimizer step (delayed
         scaling: one pass per step)."""
-        from ..ops.fp8 import DelayedScaler, flat_weights_for
-        from .params import version
-        v = version()
+        v = _params.version()
         if not self.grad_needs_unpad():  # the weight is the flat bf16 buffer slice itself
             fw = flat_weights_for(self.weight)
             got = fw.get(self.weight, v) if fw is not None else None
@@ -182,7 +181,9 @@ class Conv2d(nn.Module):
                 return got
         cache = self.__dict__.get("_fp8_cache")
         if cache is None or cache[0] != v or cache[1].device != w_lowp.device:
-            sc = self.__dict__.setdefault("_fp8_w", DelayedScaler())
+            sc = self.__dict__.get("_fp8_w")
+            if sc is None:
+                sc = self.__dict__["_fp8_w"] = DelayedScaler()
             w8, sw = sc.quantize(w_lowp)
             cache = (v, w8, sw)
             self.__dict__["_fp8_cache"] = cache
@@ -190,8 +191,9 @@ class Conv2d(nn.Module):
 
     def fp8_input(self, x):
         """e4m3 copy of an input no BN pre-quantised (delayed scaling, per layer)."""
-        from ..ops.fp8 import DelayedScaler
-        sc = self.__dict__.setdefault("_fp8_x", DelayedScaler())
+        sc = self.__dict__.get("_fp8_x")
+        if sc is None:
+            sc = self.__dict__["_fp8_x"] = DelayedScaler()
         return sc.quantize(x)
 
     def forward(self, x, want_stats=False, join=None):
@@ -244,7 +246,6 @@ class BatchNorm(nn.Module):
         (ops/bn.py, ops/fp8.DelayedScaler), or None where it does not apply."""
         if not (x.is_cuda and self.c_phys % 16 == 0):
             return None
-        from ..ops.fp8 import DelayedScaler
         sc = self.__dict__.get("_fp8")
         if sc is None:
             sc = self.__dict__["_fp8"] = DelayedScaler()

@@ -67,19 +67,20 @@ def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps
     return torch.stack([scale, shift, mean, invstd])
 
 
-def bn_apply(x, coef, residual=None, relu=True, fp8=None):
+def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None):
     """``fp8`` = (amax_ring fp32[3], phase, scale fp32[1], emit): also write an e4m3 copy of y
     scaled by the previous call's |y|max (delayed scaling) — returned as ``y._tdl_fp8`` =
-    (y8, scale) for an fp8 consumer conv (ops/conv.py) when ``emit``."""
+    (y8, scale) for an fp8 consumer conv (ops/conv.py) when ``emit``.  ``mask`` (uint8
+    [numel/8], GPU): also write the ReLU mask y > 0 as one bit per element (relu mode 3)."""
     if on_gpu(x):
         y = torch.empty_like(x)
         if fp8 is None:
-            ext().bn_apply(x, coef, residual, y, bool(relu))
+            ext().bn_apply(x, coef, residual, y, bool(relu), mask=mask)
             return y
         ring, phase, scale, emit = fp8
         y8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e4m3fn) if emit else None
         ext().bn_apply(x, coef, residual, y, bool(relu), y8.view(torch.uint8) if emit else None,
-                       ring, int(phase), scale)
+                       ring, int(phase), scale, mask)
         if emit:
             y._tdl_fp8 = (y8, scale)
         return y
@@ -92,11 +93,21 @@ def bn_apply(x, coef, residual=None, relu=True, fp8=None):
     return y.to(x.dtype)
 
 
+def unpack_relu_mask(mask, C):
+    """[M, C] bool from the 1-bit-per-element mask of relu mode 3 (bit j of byte i = element
+    8·i + j)."""
+    bits = torch.arange(8, device=mask.device, dtype=torch.uint8)
+    return ((mask.view(-1, 1) >> bits) & 1).bool().reshape(-1, C)
+
+
 def _relu_mask(relu, y, x, coef, C):
     """ReLU mask of the BN output: from y (relu=True / 1), or — without residual — recomputed as
-    x·scale + shift > 0 (relu=2) so the backward never reads y."""
+    x·scale + shift > 0 (relu=2) so the backward never reads y, or unpacked from the bit mask the
+    forward wrote (relu=3, ``y`` is then that uint8 mask)."""
     if relu == 2:
         return (x.float().reshape(-1, C) * coef[0] + coef[1]) > 0
+    if relu == 3:
+        return unpack_relu_mask(y, C)
     return y.float().reshape(-1, C) > 0
 
 
@@ -152,16 +163,21 @@ class _BatchNormActFn(torch.autograd.Function):
         coef = bn_finalize(stats, count, gp, bp, bn.running_mean, bn.running_var,
                            bn.decay, bn.eps, training)
         fp8 = bn.fp8_state(x) if getattr(bn, "emit_fp8", False) else None
-        y = bn_apply(x, coef, residual, relu, fp8)
+        # ReLU mask for the backward: without a residual it is recomputed from x (relu mode 2,
+        # nothing saved); with one, the forward writes it as 1 bit per element (mode 3: the two
+        # backward kernels read 1/16 of y's bytes instead of y itself)
+        mask = None
+        if relu and residual is not None and training and on_gpu(x) and C % 8 == 0 and C <= 2048:
+            mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8)
+        y = bn_apply(x, coef, residual, relu, fp8, mask)
         ctx.count = count
         ctx.bn = bn
         ctx.training = training
         ctx.has_res = residual is not None
         ctx.res_join = res_join if residual is not None else None
-        # without a residual the ReLU mask is recomputed from x (relu mode 2): y is not saved and
-        # the backward kernels read two tensors instead of three
-        ctx.relu = (2 if residual is None else 1) if relu else 0
-        ctx.save_for_backward(x, y if ctx.relu == 1 else None, coef, gamma, beta)
+        ctx.relu = 0 if not relu else (2 if residual is None else (3 if mask is not None else 1))
+        ctx.save_for_backward(x, mask if ctx.relu == 3 else (y if ctx.relu == 1 else None), coef,
+                              gamma, beta)
         return y
 
     @staticmethod

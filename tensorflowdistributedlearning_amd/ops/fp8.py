@@ -45,18 +45,24 @@ class DelayedScaler:
     (a 3-slot amax ring: read p, accumulate p+1, clear p+2).  The very first call primes the
     ring with an amax pass, so it is exact.  Values beyond the previous amax saturate at ±448.
     ``bn_args`` hands the same state to the BN apply kernel's fused e4m3 side output
-    (ops/bn.py), whose first call only measures."""
+    (ops/bn.py), whose first call only measures.
+
+    The scale each call produces lives in one of 3 preallocated slots rotating with the phase: a
+    consumer kernel of call t is stream-ordered before call t+3 rewrites the slot, and no
+    allocation or view is created per call (this state is touched once per layer per step, so its
+    host cost is on the critical path of launch-bound steps)."""
 
     def __init__(self):
         self.ring = None
-        self.scale = None
+        self.scale_slots = None
         self.phase = 0
         self.calls = 0
 
     def _ensure(self, device):
         if self.ring is None or self.ring.device != device:
             self.ring = _new_ring(device)
-            self.scale = torch.zeros(1, device=device, dtype=torch.float32)
+            slots = torch.zeros(3, 1, device=device, dtype=torch.float32)
+            self.scale_slots = [slots[i] for i in range(3)]
             self.phase = 0
             self.calls = 0
 
@@ -72,16 +78,14 @@ class DelayedScaler:
         if self.calls == 0:
             ext().fp8_amax(xc, self.ring, self.phase)
         y8 = torch.empty(x.shape, device=x.device, dtype=E4M3)
-        # a fresh scale tensor per call: the consumer may still hold the previous one
-        scale = torch.empty(1, device=x.device, dtype=torch.float32)
+        scale = self.scale_slots[self.phase]
         ext().fp8_quantize(xc, self.ring, self.phase, True, scale, y8.view(torch.uint8))
         self._advance()
         return y8, scale
 
     def bn_args(self, x):
         self._ensure(x.device)
-        scale = torch.empty(1, device=x.device, dtype=torch.float32)
-        out = (self.ring, self.phase, scale, self.calls > 0)
+        out = (self.ring, self.phase, self.scale_slots[self.phase], self.calls > 0)
         self._advance()
         return out
 
@@ -98,20 +102,19 @@ class FlatFp8Weights:
     def __init__(self, flat_lowp):
         self.flat = flat_lowp
         self.w8 = torch.empty(flat_lowp.numel(), device=flat_lowp.device, dtype=E4M3)
-        self.index = {}     # id(param) -> segment
-        self.pending = {}   # id(param) -> (offset, numel)
-        self.spans = []     # segment -> (offset, numel)
+        self.views = {}     # id(param) -> (w8 view, scale view), valid for the buffers' lifetime
+        self.pending = {}   # id(param) -> (offset, numel, shape)
+        self.spans = []     # segment -> (offset, numel, shape)
         self.version = None
         self.phase = 0
 
     def _rebuild(self):
-        for k, sp in self.pending.items():
-            self.index[k] = len(self.spans)
-            self.spans.append(sp)
+        keys = list(self.views) + list(self.pending)
+        self.spans = [s for s in self.spans] + list(self.pending.values())
         self.pending = {}
         rows = []
         total = self.flat.numel()
-        for seg, (off, n) in enumerate(self.spans):
+        for seg, (off, n, _) in enumerate(self.spans):
             if n % 16 or off % 16 or off + n > total:
                 raise ValueError(f"fp8 weight span ({off}, {n}) not 16-aligned inside the buffer")
             for c in range(0, n, self.CHUNK):
@@ -120,6 +123,8 @@ class FlatFp8Weights:
         self.chunks = torch.tensor(rows, dtype=torch.int64).to(dev)
         self.rings = torch.zeros(len(self.spans), 3, AMAX_SLOT, device=dev)
         self.scales = torch.zeros(len(self.spans), device=dev)
+        self.views = {k: (self.w8[off:off + n].view(shape), self.scales[seg:seg + 1])
+                      for seg, (k, (off, n, shape)) in enumerate(zip(keys, self.spans))}
         self.phase = 0
         ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
                                  self.scales, self.phase, True)  # prime: exact first scales
@@ -128,8 +133,8 @@ class FlatFp8Weights:
         """(w8, scale) for parameter ``p`` at parameter version ``version``, or None the first
         time ``p`` is seen (caller quantises it itself)."""
         k = id(p)
-        if k not in self.index and k not in self.pending:
-            self.pending[k] = (p._flat_offset, p.numel())
+        if k not in self.views and k not in self.pending:
+            self.pending[k] = (p._flat_offset, p.numel(), tuple(p.shape))
             return None
         if self.version != version:
             if self.pending:
@@ -138,11 +143,7 @@ class FlatFp8Weights:
                                      self.scales, self.phase, False)
             self.phase = (self.phase + 1) % 3
             self.version = version
-        seg = self.index.get(k)
-        if seg is None:  # joined during this version
-            return None
-        off, n = self.spans[seg]
-        return self.w8[off:off + n].view(p.shape), self.scales[seg:seg + 1]
+        return self.views.get(k)  # None: joined during this version
 
 
 def flat_weights_for(p):

@@ -49,6 +49,25 @@ class ZeroArena:
 _ARENA = ZeroArena()
 
 
+class use_arena:
+    """Route ``zeros`` / ``reset`` to ``arena`` inside the block.  A HIP-graph capture gives its
+    step a private arena (engine/trainer.py ``capture``): the graph bakes the arena's addresses
+    in, so eager steps of other trainers in the process must not grow or reallocate it."""
+
+    def __init__(self, arena):
+        self.arena = arena
+
+    def __enter__(self):
+        global _ARENA
+        self.prev, _ARENA = _ARENA, self.arena
+        return self.arena
+
+    def __exit__(self, *exc):
+        global _ARENA
+        _ARENA = self.prev
+        return False
+
+
 def zeros(shape, device):
     """A zero-filled fp32 tensor valid until the next ``reset`` (i.e. within one step)."""
     if torch.device(device).type != "cuda":

@@ -465,3 +465,29 @@ def test_fp8_flat_weights_one_launch(gpu):
     fp.sync_lowp()
     w8, s = fw.get(mod.b, version())
     assert abs(float(s) - 2 * amax_old / 448) <= 1e-5 * float(s)
+
+
+@pytest.mark.parametrize("C_", [64, 264, 2048])
+def test_batchnorm_bitmask_relu(gpu, C_):
+    """relu mode 3 (residual BN): bn_apply writes the ReLU mask as one bit per element and both
+    backward kernels read it instead of y — same results as the mask-from-y mode 1."""
+    torch.manual_seed(8)
+    M = 2 * 9 * 11
+    x = (torch.randn(2, 9, 11, C_) * 2 + 0.5).bfloat16().to(gpu)
+    r = torch.randn(2, 9, 11, C_).bfloat16().to(gpu)
+    gamma = (torch.rand(C_) + 0.5).to(gpu)
+    beta = torch.randn(C_).to(gpu)
+    st = B.bn_stats(x)
+    coef = B.bn_finalize(st, M, gamma, beta, torch.zeros(C_, device=gpu),
+                         torch.ones(C_, device=gpu), 0.9, 1e-3, True)
+    mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+    y = B.bn_apply(x, coef, r, True, mask=mask)
+    assert torch.equal(y, B.bn_apply(x, coef, r, True))
+    assert torch.equal(B.unpack_relu_mask(mask, C_), y.float().reshape(-1, C_) > 0)
+    dy = torch.randn(x.shape).bfloat16().to(gpu)
+    red1 = B.bn_bwd_reduce(dy, y, x, coef, 1)
+    red3 = B.bn_bwd_reduce(dy, mask, x, coef, 3)
+    torch.testing.assert_close(red3, red1, rtol=1e-4, atol=1e-4)
+    dx1, dr1 = B.bn_bwd_apply(dy, y, x, coef, red1, gamma, M, 1, True)
+    dx3, dr3 = B.bn_bwd_apply(dy, mask, x, coef, red1, gamma, M, 3, True)
+    assert torch.equal(dx1, dx3) and torch.equal(dr1, dr3)

@@ -243,3 +243,13 @@ def test_fp8_quantize_and_conv_reference_cpu():
     y = C.conv_fwd_fp8(y8, s, w8, sw, g)
     ref = C.ref_conv_fwd(F8.dequantize(y8, s), F8.dequantize(w8, sw), g)
     torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_relu_bitmask_layout():
+    """Bit j of mask byte i is element 8·i + j (the layout bn_apply's relu mode 3 writes)."""
+    import numpy as np
+    from tensorflowdistributedlearning_amd.ops.bn import unpack_relu_mask
+    g = torch.Generator().manual_seed(0)
+    m = torch.rand(6, 24, generator=g) > 0.5
+    packed = torch.from_numpy(np.packbits(m.numpy().reshape(-1), bitorder="little"))
+    assert torch.equal(unpack_relu_mask(packed, 24), m)

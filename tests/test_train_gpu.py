@@ -189,30 +189,34 @@ def test_deeplab_channel_padding_gpu_matches_unpadded(gpu):
 @pytest.mark.parametrize("opt", ["sgd", "adam"])
 def test_graph_replay_matches_eager(gpu, opt):
     """A HIP-graph-captured training step (Trainer.capture / replay) follows the same trajectory
-    as eager steps: parameters after 3 replays match 3 more eager steps of an identical twin
-    (device-side learning rate incl. Adam's per-step bias correction)."""
+    as eager steps (device-side learning rate incl. Adam's per-step bias correction, padded
+    weight copies refreshed inside the graph, no stale memset / copy nodes).  Frozen BN keeps the
+    step free of float atomics; what remains is fp32 summation order inside PyTorch reductions
+    whose vectorisation depends on buffer alignment (graph-pool vs eager addresses — measured
+    with tools/graph_debug.py: after the first replay only the stem BN γ gradient differs), so
+    the updates are compared with a tolerance rather than bit for bit."""
     torch.manual_seed(7)
-    kw = dict(model_name="m", input_shape=(33, 33), n_blocks=(1, 1, 1))
-    a = models.DeepLabResNet(**kw)
-    b = models.DeepLabResNet(**kw)
-    b.load_state_dict(a.state_dict())
-    okw = dict(lr=1e-3) if opt == "adam" else dict(lr=0.01, momentum=0.9)
-    ta = Trainer(a, lovasz_hinge, gpu, opt, okw)
-    tb = Trainer(b, lovasz_hinge, gpu, opt, okw)
-    # frozen BN: batch statistics of a 4-image batch (fp32 atomics, non-associative) would let the
-    # two runs drift apart chaotically within a few steps even eager-vs-eager
+    nets = [models.resnet18(num_classes=10) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    okw = dict(lr=1e-3) if opt == "adam" else dict(lr=0.05, momentum=0.9)
+    ta, tb = [Trainer(n, softmax_cross_entropy, gpu, opt, dict(okw)) for n in nets]
     ta.train_mode = tb.train_mode = False
-    x, y = segmentation_batch(4, size=(33, 33), device=gpu)
+    x, y = imagenet_batch(8, 32, num_classes=10, device=gpu)
     tb.capture(x, y, warmup=2)
     for _ in range(2):
         ta.train_step(x, y)
     assert ta.optimizer.step_count == tb.optimizer.step_count == 2
+    torch.cuda.synchronize()
+    assert torch.equal(ta.flat.master, tb.flat.master)  # capture left the state untouched
+    m0 = ta.flat.master.clone()
     for _ in range(3):
         la, _ = ta.train_step(x, y)
         lb, _ = tb.replay()
     torch.cuda.synchronize()
     assert tb.optimizer.step_count == 5 and tb.global_step == 5
-    torch.testing.assert_close(float(lb), float(la), rtol=2e-2, atol=2e-3)
-    cos = torch.nn.functional.cosine_similarity(ta.flat.master, tb.flat.master, dim=0).item()
-    assert cos > 0.9999, cos
-    assert (ta.flat.master - tb.flat.master).abs().max().item() < 5e-3
+    ua, ub = ta.flat.master - m0, tb.flat.master - m0
+    assert ua.norm() > 0 and torch.isfinite(ub).all()
+    cos = torch.nn.functional.cosine_similarity(ua, ub, dim=0).item()
+    assert cos > 0.999, cos
+    assert ((ua - ub).norm() / ua.norm()).item() < 0.05
+    torch.testing.assert_close(float(lb), float(la), rtol=1e-3, atol=1e-4)
