@@ -17,6 +17,11 @@ namespace {
 
 constexpr int NT = 256;
 
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 __device__ __forceinline__ void unpack(const uint4& v, float f[8]) { unpack8(v, f); }
 
 // ---------------------------------------------------------------------------------------------
@@ -63,7 +68,7 @@ __global__ void reduce_scalar_kernel(const bf16_t* __restrict__ a, const bf16_t*
 // ---------------------------------------------------------------------------------------------
 // vector path (C % 8 == 0, C/8 <= 256): thread = (row lane, channel vector)
 // ---------------------------------------------------------------------------------------------
-template <int KIND>
+template <int KIND, int U>
 __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict__ a,
                                                         const bf16_t* __restrict__ y,
                                                         const bf16_t* __restrict__ x,
@@ -91,7 +96,6 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
       }
     }
     // U rows in flight per thread: all loads of a group are issued before any use
-    constexpr int U = 4;
     long r = r0 + rl;
     for (; r < r1; r += U * rpp) {
       uint4 la[U], lx[U], ly[U];
@@ -165,11 +169,20 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     // ≈ one or two workgroups per CU, ≥ 16 rows per thread: few atomics per output address
     // (every workgroup adds one row of 2C partial sums)
     const int cvecs = C / 8, rpp = NT / cvecs;
-    long blocks = std::min<long>(512, std::max<long>(1, M / (rpp * 16)));
+    static const int cap = env_int("TDL_BN_RED_BLOCKS", 512);
+    static const int u = env_int("TDL_BN_RED_U", 4);
+    long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * 16)));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
-    hipLaunchKernelGGL(reduce_vec_kernel<KIND>, dim3(blocks), dim3(NT), 0, st, a, y, x, coef, out, M,
-                       C, rpb, relu);
+    if (u == 8)
+      hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
+                         out, M, C, rpb, relu);
+    else if (u == 2)
+      hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
+                         out, M, C, rpb, relu);
+    else
+      hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
+                         out, M, C, rpb, relu);
   } else {
     long blocks = std::min<long>(512, std::max<long>(1, M / 64));
     long rpb = (M + blocks - 1) / blocks;

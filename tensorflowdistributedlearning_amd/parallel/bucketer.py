@@ -14,6 +14,9 @@ The reference concatenates ALL gradients into one NCCL pack after the full backw
 * the first-issued bucket is kept small so communication starts early, later ones are large
   (``bucket_mb``, default 32 MB) — fewer, larger collectives suit xGMI's per-link ring bandwidth
   (7 links × ≈153 GB/s per MI355X);
+* the last-issued bucket (the network's first layers, whose gradients arrive when backward
+  ends) is also kept small: it is the one collective nothing overlaps, so its size is exposed
+  step time — the remainder is split off the bucket before it;
 * the 1/world averaging is fused into the optimizer kernel (no extra pass).
 
 A ``comm_hook`` can replace the collective (used by tests to record launch order with a fake
@@ -37,6 +40,11 @@ class Bucket:
     @property
     def nbytes(self):
         return (self.hi - self.lo) * 4
+
+    @staticmethod
+    def hi_of(p, flat):
+        lo, _ = flat.slice_of(p)
+        return lo + ((p.numel() + 63) // 64) * 64
 
 
 class GradBucketer:
@@ -66,9 +74,30 @@ class GradBucketer:
                 limit = cap
         if cur:
             self._add_bucket(cur_lo, cur_hi, cur)
+        self._shrink_tail(cap_first)
         self.next_launch = 0
         for p in params:
             p._grad_hook = self._on_ready
+
+    def _shrink_tail(self, cap):
+        """Split the last bucket so that its trailing part (the earliest parameters) holds at
+        most ~``cap`` elements: all but that part goes into its own bucket before it."""
+        last = self.buckets[-1]
+        if len(last.params) < 2 or last.hi - last.lo <= cap:
+            return
+        # last.params runs from high to low offsets; keep the lowest-offset params ≤ cap
+        keep = []
+        for p in reversed(last.params):
+            if keep and last.hi_of(p, self.flat) - last.lo > cap:
+                break
+            keep.append(p)
+        head = last.params[: len(last.params) - len(keep)]
+        if not head:
+            return
+        split = self.flat.slice_of(keep[-1])[0] + ((keep[-1].numel() + 63) // 64) * 64
+        self.buckets.pop()
+        self._add_bucket(split, last.hi, head)
+        self._add_bucket(last.lo, split, list(reversed(keep)))
 
     def _add_bucket(self, lo, hi, ps):
         b = Bucket(len(self.buckets), lo, hi, list(ps))

@@ -157,3 +157,27 @@ def test_native_comm_selector_cpu():
         assert issubclass(rccl.CommError, RuntimeError)
     finally:
         D.shutdown()
+
+
+def test_bucketer_last_bucket_is_small():
+    """The bucket launched last (earliest layers, exposed after backward) is split down to about
+    the first-bucket size; buckets still tile the flat buffer contiguously."""
+    from tensorflowdistributedlearning_amd import models
+    m = models.resnet18(num_classes=10)
+    f = FlatParams(m, "cpu", lowp_dtype=None)
+    b = GradBucketer(f, None, bucket_mb=8.0, first_bucket_mb=0.5,
+                     comm_hook=lambda bk, v: None)
+    cap = int(0.5 * 2 ** 20 / 4)
+    assert b.buckets[-1].hi - b.buckets[-1].lo <= cap
+    assert b.buckets[-1].lo == 0
+    cov = sorted((bk.lo, bk.hi) for bk in b.buckets)
+    for (lo0, hi0), (lo1, hi1) in zip(cov, cov[1:]):
+        assert hi0 == lo1
+    assert cov[-1][1] == f.total or cov[-1][1] == sum(((p.numel() + 63) // 64) * 64
+                                                       for p in f.params)
+    seen = [id(p) for bk in b.buckets for p in bk.params]
+    assert sorted(seen) == sorted(id(p) for p in f.params)
+    for bk in b.buckets:  # every param lies inside its bucket's range
+        for p in bk.params:
+            lo, hi = f.slice_of(p)
+            assert bk.lo <= lo and hi <= bk.hi
