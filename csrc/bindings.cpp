@@ -424,33 +424,42 @@ DwArgs dw_args(const Tensor& x_like, const Tensor& w, int64_t Ho, int64_t Wo, in
 }
 
 void dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t sh, int64_t sw,
-                int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu) {
+                int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu, bool relu_in) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   DwArgs a = dw_args(x, w, y.size(1), y.size(2), sh, sw, ph, pw, dh, dw);
   a.x = BF(x); a.w = BF(w); a.bias = optf(bias); a.out = BFW(y); a.relu = relu;
+  TORCH_CHECK(!relu_in || (a.C % 8 == 0 && a.R * a.S == 9), "fused input ReLU: 3x3, C % 8 == 0");
+  a.relu_in = relu_in;
   dwconv_fwd_launch(a, stream());
 }
 
 void dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                  int64_t dh, int64_t dw) {
+                  int64_t dh, int64_t dw, c10::optional<Tensor> mask_x) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   DwArgs a = dw_args(dx, w, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
   a.dy = BF(dy); a.w = BF(w); a.out = BFW(dx);
+  a.mask_x = optb(mask_x);
+  if (a.mask_x) {
+    TORCH_CHECK(mask_x->sizes() == dx.sizes(), "mask_x must be shaped like dx");
+    TORCH_CHECK(a.C % 8 == 0 && a.R * a.S == 9, "fused input ReLU: 3x3, C % 8 == 0");
+  }
   dwconv_dgrad_launch(a, stream());
 }
 
 void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int64_t sh, int64_t sw,
-                  int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+                  int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu_in) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dwt, torch::kFloat32);
   TORCH_CHECK(dwt.size(0) * dwt.size(1) <= 49, "depthwise kernel up to 7x7");
   DwArgs a = dw_args(x, dwt, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
   a.dy = BF(dy); a.x = BF(x); a.dw = dwt.data_ptr<float>(); a.db = optfw(db);
+  TORCH_CHECK(!relu_in || (a.C % 8 == 0 && a.R * a.S == 9), "fused input ReLU: 3x3, C % 8 == 0");
+  a.relu_in = relu_in;
   const int slabs = dwconv_wgrad_slabs(a);
   Tensor ws;
   if (slabs > 0) ws = torch::empty({(int64_t)slabs * (a.R * a.S + 1) * a.C}, dwt.options());

@@ -12,6 +12,21 @@ namespace {
 constexpr int NT = 256;
 inline int blocks_for(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT)); }
 
+// ReLU on 8 packed bf16 values: clear every half whose sign bit is set
+__device__ __forceinline__ uint32_t relu2(uint32_t v) {
+  return v & ~(((v >> 15) & 0x00010001u) * 0xFFFFu);
+}
+__device__ __forceinline__ uint4 relu8(uint4 v) {
+  return make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
+}
+// dx · [x > 0] for the fused input ReLU's backward
+__device__ __forceinline__ void mask_pos(float* acc, const bf16_t* xp) {
+  float xv[8];
+  unpack8(*(const uint4*)xp, xv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = xv[j] > 0.f ? acc[j] : 0.f;
+}
+
 template <int V>
 __device__ __forceinline__ void ldv(const bf16_t* p, float* f) {
   if constexpr (V == 8) unpack8(*(const uint4*)p, f);
@@ -205,7 +220,9 @@ __global__ void __launch_bounds__(NT) dw_fwd_rows(DwArgs a, int lanes_c, int rpp
       const int hi = ho * a.sh - a.ph + r * a.dh, wi = wo * a.sw - a.pw + s * a.dwl;
       if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) continue;
       float xv[8];
-      unpack8(*(const uint4*)(xn + ((long)hi * a.W + wi) * a.C), xv);
+      uint4 xr = *(const uint4*)(xn + ((long)hi * a.W + wi) * a.C);
+      if (a.relu_in) xr = relu8(xr);
+      unpack8(xr, xv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += xv[j] * wv[k][j];
     }
@@ -253,6 +270,7 @@ __global__ void __launch_bounds__(NT) dw_dgrad_rows(DwArgs a, int lanes_c, int r
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += gv[j] * wv[k][j];
     }
+    if (a.mask_x) mask_pos(acc, a.mask_x + ((long)row * a.W + w) * a.C + c);
     *(uint4*)(xrow + (long)w * a.C) = pack8(acc);
   }
 }
@@ -294,7 +312,9 @@ __global__ void __launch_bounds__(NT) dw_wgrad_rows(DwArgs a, int lanes_c, int r
           const int hi = ho * a.sh - a.ph + r * a.dh, wi = wo * a.sw - a.pw + s * a.dwl;
           if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) continue;
           float xv[8];
-          unpack8(*(const uint4*)(xn + ((long)hi * a.W + wi) * a.C), xv);
+          uint4 xr = *(const uint4*)(xn + ((long)hi * a.W + wi) * a.C);
+          if (a.relu_in) xr = relu8(xr);
+          unpack8(xr, xv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[k][j] += gv[j] * xv[j];
         }
@@ -323,6 +343,205 @@ __global__ void __launch_bounds__(NT) dw_wgrad_rows(DwArgs a, int lanes_c, int r
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Sliding-window kernels for the common 3×3 / stride 1 / dilation 1 case (Xception's separable
+// convs, the preprocessing Laplacian's shape class).  The row kernels above load all 9 taps of
+// every output pixel from the cache hierarchy (9 × 16 B per 16 B written: L1/TA-bound at ≈1/3
+// of HBM bandwidth).  Here a lane walks a CONTIGUOUS run of output columns and keeps the 3×3
+// input window in registers (packed bf16): each step loads only the 3 vectors of the new input
+// column.  One kernel serves the forward and, with the filter rotated 180° (FLIP) and the
+// complementary padding, the stride-1 dgrad:
+//   out[h, w] = Σ_{r,s} in[h − P_h + r, w − P_w + s] · W[r, s]
+// (dgrad: in = dy, P = 2 − pad, W[r, s] = w[2 − r, 2 − s]).
+// ---------------------------------------------------------------------------------------------
+template <bool FLIP>
+__global__ void __launch_bounds__(NT) dw_slide_kernel(const bf16_t* __restrict__ in,
+                                                      const bf16_t* __restrict__ wt,
+                                                      const float* __restrict__ bias,
+                                                      bf16_t* __restrict__ out, int Hi, int Wi,
+                                                      int Ho, int Wo, int C, int Ph, int Pw,
+                                                      int relu, int lanes_c, int rpp, int seg,
+                                                      int relu_in,
+                                                      const bf16_t* __restrict__ mask_x) {
+  const int cv = C / 8;
+  const int t = threadIdx.x, lc = t % lanes_c, pl = t / lanes_c;
+  const int cvi = lc + blockIdx.y * lanes_c;
+  if (pl >= rpp || cvi >= cv) return;
+  const int c = cvi * 8;
+  const int row = blockIdx.x, n = row / Ho, ho = row - n * Ho;
+  const int w0 = pl * seg, w1 = min(Wo, w0 + seg);
+  if (w0 >= w1) return;
+  float wv[9][8], b[8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) unpack8(*(const uint4*)(wt + (long)(FLIP ? 8 - k : k) * C + c), wv[k]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = bias ? bias[c + j] : 0.f;
+  const bf16_t* base = in + (long)n * Hi * Wi * C + c;
+  int hi[3];
+  bool hv[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    hi[r] = ho - Ph + r;
+    hv[r] = (unsigned)hi[r] < (unsigned)Hi;
+  }
+  auto col = [&](int r, int wi) -> uint4 {
+    if (!hv[r] || (unsigned)wi >= (unsigned)Wi) return make_uint4(0, 0, 0, 0);
+    const uint4 v = *(const uint4*)(base + ((long)hi[r] * Wi + wi) * C);
+    return relu_in ? relu8(v) : v;
+  };
+  // (no software prefetch here: the extra column pushes the kernel to 178 VGPRs and 2 waves per
+  // SIMD, measured slower than 3 waves without it; the wgrad kernel below does gain from it)
+  uint4 win[3][3];  // [row][column], packed bf16
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    win[r][1] = col(r, w0 - Pw);
+    win[r][2] = col(r, w0 - Pw + 1);
+  }
+  bf16_t* orow = out + ((long)row * Wo) * C + c;
+  for (int w = w0; w < w1; ++w) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      win[r][0] = win[r][1];
+      win[r][1] = win[r][2];
+      win[r][2] = col(r, w - Pw + 2);
+    }
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = b[j];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        float xv[8];
+        unpack8(win[r][s], xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += xv[j] * wv[r * 3 + s][j];
+      }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
+    }
+    if (mask_x) mask_pos(acc, mask_x + ((long)row * Wo + w) * C + c);
+    *(uint4*)(orow + (long)w * C) = pack8(acc);
+  }
+}
+
+// wgrad with the same sliding window over x: a lane walks a contiguous run of output columns of
+// each of its workgroup's rows; per output pixel one dy vector + the 3 vectors of the new x column.
+__global__ void __launch_bounds__(NT) dw_wgrad_slide(DwArgs a, int lanes_c, int rpp, int seg,
+                                                     int rows_per_block, float* ws_w, float* ws_b) {
+  const int cv = a.C / 8;
+  const int t = threadIdx.x, lc = t % lanes_c, pl = t / lanes_c;
+  const int cvi = lc + blockIdx.y * lanes_c;
+  const bool active = pl < rpp && cvi < cv;
+  const int c = cvi * 8;
+  const int rows = a.N * a.Ho;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  const int w0 = pl * seg, w1 = min(a.Wo, w0 + seg);
+  float acc[9][8], db[8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db[j] = 0.f;
+  if (active && w0 < w1) {
+    for (int row = r0; row < r1; ++row) {
+      const int n = row / a.Ho, ho = row - n * a.Ho;
+      const bf16_t* grow = a.dy + ((long)row * a.Wo) * a.C + c;
+      const bf16_t* xn = a.x + (long)n * a.H * a.W * a.C + c;
+      int hi[3];
+      bool hv[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        hi[r] = ho - a.ph + r;
+        hv[r] = (unsigned)hi[r] < (unsigned)a.H;
+      }
+      auto col = [&](int r, int wi) -> uint4 {
+        if (!hv[r] || (unsigned)wi >= (unsigned)a.W) return make_uint4(0, 0, 0, 0);
+        const uint4 v = *(const uint4*)(xn + ((long)hi[r] * a.W + wi) * a.C);
+        return a.relu_in ? relu8(v) : v;
+      };
+      uint4 win[3][3], nxt[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        win[r][1] = col(r, w0 - a.pw);
+        win[r][2] = col(r, w0 - a.pw + 1);
+        nxt[r] = col(r, w0 - a.pw + 2);
+      }
+      uint4 gnext = *(const uint4*)(grow + (long)w0 * a.C);
+      for (int wo = w0; wo < w1; ++wo) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          win[r][0] = win[r][1];
+          win[r][1] = win[r][2];
+          win[r][2] = nxt[r];
+        }
+        const uint4 gcur = gnext;
+        if (wo + 1 < w1) {  // next column's x and dy loads in flight under this column's FMAs
+#pragma unroll
+          for (int r = 0; r < 3; ++r) nxt[r] = col(r, wo - a.pw + 3);
+          gnext = *(const uint4*)(grow + (long)(wo + 1) * a.C);
+        }
+        float gv[8];
+        unpack8(gcur, gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db[j] += gv[j];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            float xv[8];
+            unpack8(win[r][s], xv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[r * 3 + s][j] += gv[j] * xv[j];
+          }
+      }
+    }
+  }
+  __shared__ float red[NT][9];
+  const long slab_w = (long)blockIdx.x * 9 * a.C, slab_b = (long)blockIdx.x * a.C;
+#pragma unroll
+  for (int k = 0; k <= 9; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t][j] = (k < 9) ? acc[k < 9 ? k : 0][j] : db[j];
+    __syncthreads();
+    if (pl == 0 && cvi < cv) {
+      float sum[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum[j] = 0.f;
+      for (int q = 0; q < rpp; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum[j] += red[q * lanes_c + lc][j];
+      float* dst = (k < 9) ? ws_w + slab_w + (long)k * a.C + c : ws_b + slab_b + c;
+      *(float4*)dst = make_float4(sum[0], sum[1], sum[2], sum[3]);
+      *(float4*)(dst + 4) = make_float4(sum[4], sum[5], sum[6], sum[7]);
+    }
+    __syncthreads();
+  }
+}
+
+// the sliding-window path: 3×3, stride 1, dilation 1, C % 8 == 0, and the padding keeps every
+// window inside [−2, W + 1] (0 ≤ pad ≤ 2)
+bool slide_ok(const DwArgs& a) {
+  return a.C % 8 == 0 && a.R == 3 && a.S == 3 && a.sh == 1 && a.sw == 1 && a.dh == 1 &&
+         a.dwl == 1 && a.ph >= 0 && a.ph <= 2 && a.pw >= 0 && a.pw <= 2 &&
+         getenv("TDL_DW_SLIDE_OFF") == nullptr;
+}
+
+// lanes: channel vectors × pixel lanes; each pixel lane owns ⌈W / rpp⌉ consecutive columns
+struct SlideGeom {
+  int lanes_c, rpp, seg;
+};
+SlideGeom slide_geom(int cv, int W) {
+  SlideGeom g;
+  g.lanes_c = std::min(cv, NT);
+  g.rpp = std::max(1, std::min(NT / g.lanes_c, W));
+  g.seg = cdiv(W, g.rpp);
+  g.rpp = cdiv(W, g.seg);
+  return g;
+}
+
 template <int V>
 void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
   const int cv = a.C / V;
@@ -348,7 +567,13 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
-  if (a.C % 8 == 0 && a.R * a.S == 9) {
+  if (slide_ok(a)) {
+    const SlideGeom g = slide_geom(a.C / 8, a.Wo);
+    dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
+    hipLaunchKernelGGL(dw_slide_kernel<false>, grid, dim3(NT), 0, st, a.x, a.w, a.bias, a.out, a.H,
+                       a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.lanes_c, g.rpp, g.seg, a.relu_in,
+                       (const bf16_t*)nullptr);
+  } else if (a.C % 8 == 0 && a.R * a.S == 9) {
     const RowGeom g = row_geom(a.C / 8);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
     hipLaunchKernelGGL(dw_fwd_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp);
@@ -361,7 +586,13 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
-  if (a.C % 8 == 0 && a.R * a.S == 9) {
+  if (slide_ok(a)) {  // stride-1 dgrad = forward of dy with the rotated filter, padding 2 − p
+    const SlideGeom g = slide_geom(a.C / 8, a.W);
+    dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));
+    hipLaunchKernelGGL(dw_slide_kernel<true>, grid, dim3(NT), 0, st, a.dy, a.w, nullptr, a.out,
+                       a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.lanes_c, g.rpp, g.seg, 0,
+                       a.mask_x);
+  } else if (a.C % 8 == 0 && a.R * a.S == 9) {
     const RowGeom g = row_geom(a.C / 8);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));
     hipLaunchKernelGGL(dw_dgrad_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp);
@@ -393,8 +624,14 @@ void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st) {
     dim3 grid((unsigned)slabs, (unsigned)cdiv(a.C / 8, g.lanes_c));
     float* ws_w = ws;
     float* ws_b = ws + (long)slabs * 9 * a.C;
-    hipLaunchKernelGGL(dw_wgrad_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp, rpb, ws_w,
-                       ws_b);
+    if (slide_ok(a)) {
+      const SlideGeom sg = slide_geom(a.C / 8, a.Wo);
+      hipLaunchKernelGGL(dw_wgrad_slide, grid, dim3(NT), 0, st, a, sg.lanes_c, sg.rpp, sg.seg, rpb,
+                         ws_w, ws_b);
+    } else {
+      hipLaunchKernelGGL(dw_wgrad_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp, rpb, ws_w,
+                         ws_b);
+    }
     splitk_reduce_launch(ws_w, a.dw, 9L * a.C, slabs, true, st);
     if (a.db) splitk_reduce_launch(ws_b, a.db, a.C, slabs, true, st);
     return;

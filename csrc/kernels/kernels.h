@@ -157,6 +157,10 @@ struct DwArgs {
   float* db;           // fp32 [C]
   int N, H, W, C, R, S, Ho, Wo, sh, sw, ph, pw, dh, dwl;
   int relu;
+  // fused pre-activation ReLU of the input (Xception's relu → separable conv): fwd / wgrad read
+  // max(x, 0); dgrad zeroes dx where mask_x ≤ 0 (mask_x = the un-rectified x).  3×3, C % 8 == 0.
+  int relu_in = 0;
+  const bf16_t* mask_x = nullptr;
 };
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
 void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);

@@ -347,8 +347,9 @@ class DepthwiseConv2d(nn.Module):
         else:
             self.bias = None
 
-    def forward(self, x):
+    def forward(self, x, relu_in=False):
         pad = resolve_padding(self.padding, x.shape[1], x.shape[2], self.k, self.k, self.stride,
                               self.dilation)
         return depthwise_conv2d(x, self.weight, self.bias, ConvGeom(self.stride, pad,
-                                                                    self.dilation), self.relu)
+                                                                    self.dilation), self.relu,
+                                relu_in)

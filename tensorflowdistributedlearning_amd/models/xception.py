@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from .layers import ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear
-from ..ops.elementwise import relu as relu_op, add as add_op
+from ..ops.elementwise import add as add_op
 
 
 def _fixed_pad(k, rate):
@@ -26,21 +26,23 @@ def _fixed_pad(k, rate):
 
 
 class SeparableConvBN(nn.Module):
-    """separable_conv2d_same (split form): depthwise k×k (stride, rate) → BN [→ReLU] →
-    pointwise 1×1 → BN [→ReLU]."""
+    """separable_conv2d_same (split form): [ReLU →] depthwise k×k (stride, rate) → BN [→ReLU] →
+    pointwise 1×1 → BN [→ReLU].  ``relu_out`` rectifies the pointwise BN output even when the
+    activation is not 'inside' (it then belongs to the next unit's pre-activation ReLU)."""
 
-    def __init__(self, cin, cout, stride, rate, act_inside, bn_kw):
+    def __init__(self, cin, cout, stride, rate, act_inside, bn_kw, relu_out=None):
         super().__init__()
         pad = "SAME" if stride == 1 else _fixed_pad(3, rate)
         self.depthwise = DepthwiseConv2d(cin, 3, stride, pad, rate, bias=False, relu=False,
                                          init_std=0.33)
         self.dw_bn = BatchNorm(cin, bn_kw["bn_decay"], bn_kw["bn_eps"])
-        self.pointwise = ConvBN(cin, cout, 1, 1, 0, relu=act_inside, init="trunc_normal",
-                                init_std=0.06, **bn_kw)
+        self.pointwise = ConvBN(cin, cout, 1, 1, 0,
+                                relu=act_inside if relu_out is None else relu_out,
+                                init="trunc_normal", init_std=0.06, **bn_kw)
         self.act_inside = act_inside
 
-    def forward(self, x):
-        y = self.depthwise(x)
+    def forward(self, x, relu_in=False):
+        y = self.depthwise(x, relu_in=relu_in)
         y = self.dw_bn(y, relu=self.act_inside)
         return self.pointwise(y)
 
@@ -53,8 +55,13 @@ class XceptionModule(nn.Module):
         convs = []
         c = cin
         for i in range(3):
+            # pre-activation (act_inside False): the ReLU in front of separable convs 2 and 3
+            # reads only the previous pointwise BN output, so it is fused into that BN's apply;
+            # the one in front of conv 1 reads the unit input (also the skip path's operand), so
+            # the depthwise kernel applies it on load instead.
             convs.append(SeparableConvBN(c, depth_list[i], stride if i == 2 else 1,
-                                         rate * unit_rates[i], act_inside, bn_kw))
+                                         rate * unit_rates[i], act_inside, bn_kw,
+                                         relu_out=(not act_inside and i < 2) or act_inside))
             c = depth_list[i]
         self.convs = nn.ModuleList(convs)
         self.shortcut = (ConvBN(cin, depth_list[-1], 1, stride, 0, relu=False, **bn_kw)
@@ -62,11 +69,8 @@ class XceptionModule(nn.Module):
         self.out_channels = depth_list[-1]
 
     def forward(self, x):
-        r = x
-        for conv in self.convs:
-            if not self.act_inside:
-                r = relu_op(r)
-            r = conv(r)
+        r = self.convs[0](x, relu_in=not self.act_inside)
+        r = self.convs[2](self.convs[1](r))
         if self.skip == "conv":
             return self.shortcut(x, residual=r)  # BN(shortcut) + residual, no act
         if self.skip == "sum":

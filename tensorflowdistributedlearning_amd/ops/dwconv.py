@@ -27,9 +27,14 @@ def ref_dw_fwd(x, w, geom: ConvGeom, bias=None):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
+def _fusable_relu_in(x, R, S):
+    """The kernels fold an input ReLU into their loads for 3×3 filters on 8-channel vectors."""
+    return x.shape[-1] % 8 == 0 and R * S == 9
+
+
 class _DwConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, relu):
+    def forward(ctx, x, weight, bias, geom, relu, relu_in):
         w = compute_weight(weight, x.dtype)
         N, H, W, C = x.shape
         R, S, _ = w.shape
@@ -38,13 +43,14 @@ class _DwConvFn(torch.autograd.Function):
             y = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
             ext().dwconv_fwd(x, w, None if bias is None else bias.detach(), y, geom.stride[0],
                              geom.stride[1], geom.padding[0], geom.padding[2], geom.dilation[0],
-                             geom.dilation[1], bool(relu))
+                             geom.dilation[1], bool(relu), bool(relu_in))
         else:
-            y = ref_dw_fwd(x, w, geom, None if bias is None else bias.detach())
+            y = ref_dw_fwd(torch.relu(x) if relu_in else x, w, geom,
+                           None if bias is None else bias.detach())
             if relu:
                 y = torch.relu(y)
             y = y.to(x.dtype)
-        ctx.geom, ctx.relu = geom, relu
+        ctx.geom, ctx.relu, ctx.relu_in = geom, relu, relu_in
         ctx.save_for_backward(x, weight, bias, y if relu else None)
         return y
 
@@ -64,18 +70,20 @@ class _DwConvFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
                 ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
-                                   geom.padding[2], geom.dilation[0], geom.dilation[1])
+                                   geom.padding[2], geom.dilation[0], geom.dilation[1],
+                                   x if ctx.relu_in else None)
             dw = torch.zeros(weight.shape, device=dy.device, dtype=torch.float32)
             db = torch.zeros(x.shape[-1], device=dy.device, dtype=torch.float32) \
                 if bias is not None else None
             ext().dwconv_wgrad(g, x, dw, db, geom.stride[0], geom.stride[1], geom.padding[0],
-                               geom.padding[2], geom.dilation[0], geom.dilation[1])
+                               geom.padding[2], geom.dilation[0], geom.dilation[1],
+                               bool(ctx.relu_in))
         else:
             xr = x.detach().float().requires_grad_(True)
             wr = weight.detach().float().requires_grad_(True)
             br = bias.detach().float().requires_grad_(True) if bias is not None else None
             with torch.enable_grad():
-                yr = ref_dw_fwd(xr, wr, geom, br)
+                yr = ref_dw_fwd(torch.relu(xr) if ctx.relu_in else xr, wr, geom, br)
                 if ctx.relu:
                     yr = torch.relu(yr)
                 grads = torch.autograd.grad(yr, [xr, wr] + ([br] if br is not None else []),
@@ -87,11 +95,17 @@ class _DwConvFn(torch.autograd.Function):
             deliver_grad(weight, dw)
         if bias is not None and bias.requires_grad:
             deliver_grad(bias, db)
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
-def depthwise_conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False):
-    return _DwConvFn.apply(x, weight, bias, geom, relu)
+def depthwise_conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False,
+                     relu_in=False):
+    """``relu_in``: convolve max(x, 0) without materialising it (Xception's pre-activation ReLU
+    in front of each separable conv, core/xception.py:90-110); the backward masks dx by x > 0."""
+    if relu_in and on_gpu(x) and not _fusable_relu_in(x, weight.shape[0], weight.shape[1]):
+        from .elementwise import relu as relu_op
+        x, relu_in = relu_op(x), False
+    return _DwConvFn.apply(x, weight, bias, geom, relu, relu_in)
 
 
 def laplace(x):

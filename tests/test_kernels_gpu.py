@@ -306,6 +306,34 @@ def test_depthwise(gpu, Cn, rate, stride, relu):
     assert rel_err(bp.grad, br.grad) < 2e-2
 
 
+@pytest.mark.parametrize("Cn,rate,stride", [(64, 1, 1), (728, 1, 2), (128, 2, 1), (40, 1, 1),
+                                            (1024, 1, 1)])
+def test_depthwise_fused_input_relu(gpu, Cn, rate, stride):
+    """relu_in: the kernels rectify x on load (fwd, wgrad) and mask dx by x > 0 (dgrad) — vs the
+    fp32 reference of relu → depthwise conv (C = 40 takes the unfused fallback)."""
+    torch.manual_seed(12)
+    from tensorflowdistributedlearning_amd.models.layers import resolve_padding
+    H = 17
+    pad = resolve_padding("SAME", H, H, 3, 3, (stride, stride), (rate, rate))
+    g = C.ConvGeom((stride, stride), pad, (rate, rate))
+    x = torch.randn(2, H, H, Cn).bfloat16()
+    w = (torch.randn(3, 3, Cn) * 0.3).bfloat16()
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = D.ref_dw_fwd(torch.relu(xr), wr, g)
+    wp = torch.nn.Parameter(w.float().to(gpu))
+    wp._lowp = w.to(gpu)
+    xg = x.to(gpu).requires_grad_(True)
+    y = D.depthwise_conv2d(xg, wp, None, g, False, relu_in=True)
+    assert rel_err(y, yr) < 2e-2
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    y.backward(dy.to(gpu))
+    assert rel_err(xg.grad, xr.grad) < 2e-2
+    assert rel_err(wp.grad, wr.grad) < 2e-2
+    assert float(xg.grad.float()[xg.detach() <= 0].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("hw,out", [((13, 13), (26, 26)), ((1, 1), (13, 13)), ((26, 26), (101, 101)),
                                     ((7, 5), (9, 12))])
 def test_upsample(gpu, hw, out):

@@ -253,3 +253,36 @@ def test_relu_bitmask_layout():
     m = torch.rand(6, 24, generator=g) > 0.5
     packed = torch.from_numpy(np.packbits(m.numpy().reshape(-1), bitorder="little"))
     assert torch.equal(unpack_relu_mask(packed, 24), m)
+
+
+def test_depthwise_relu_in_matches_explicit_relu_cpu():
+    """depthwise_conv2d(relu_in=True) ≡ depthwise_conv2d(relu(x)) incl. the input gradient mask;
+    and Xception's fused pre-activation placement gives the unfused network's output."""
+    from tensorflowdistributedlearning_amd.ops import dwconv as D
+    torch.manual_seed(3)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    x = torch.randn(2, 9, 9, 16)
+    w = torch.nn.Parameter(torch.randn(3, 3, 16) * 0.3)
+    xa = x.clone().requires_grad_(True)
+    xb = x.clone().requires_grad_(True)
+    ya = D.depthwise_conv2d(xa, w, None, g, False, relu_in=True)
+    yb = D.depthwise_conv2d(torch.relu(xb), w, None, g, False)
+    torch.testing.assert_close(ya, yb)
+    dy = torch.randn_like(ya)
+    ya.backward(dy)
+    yb.backward(dy)
+    torch.testing.assert_close(xa.grad, xb.grad)
+
+    from tensorflowdistributedlearning_amd.models.xception import XceptionModule
+    m = XceptionModule(16, [16, 16, 16], "sum", 1, 1, [1, 1, 1], False,
+                       dict(bn_decay=0.9, bn_eps=1e-3)).eval()
+    xi = torch.randn(2, 9, 9, 16)
+    with torch.no_grad():
+        r = xi
+        for conv in m.convs:  # the unfused pre-activation order of core/xception.py:90-110
+            r = conv.depthwise(torch.relu(r))
+            r = conv.dw_bn(r, relu=False)
+            pw = conv.pointwise
+            r = pw.bn(pw.conv(r), relu=False)
+        ref = r + xi
+        torch.testing.assert_close(m(xi), ref, rtol=1e-4, atol=1e-4)
