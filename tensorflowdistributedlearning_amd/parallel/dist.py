@@ -102,14 +102,20 @@ def init_distributed(device_type=None, backend=None, timeout_s=600, comm="torch"
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # TDL_SHARE_GPU=1 (rehearsal only): ranks share the visible devices round-robin, so the
+        # multi-rank path can be exercised on a one-GPU box (with TDL_DIST_BACKEND=gloo)
+        dev_idx = local_rank
+        if os.environ.get("TDL_SHARE_GPU") == "1":
+            dev_idx = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     be = "none"
     native = comm == "rccl" and device_type == "cuda" and world > 1
     if world > 1:
-        be = backend or ("nccl" if device_type == "cuda" and not native else "gloo")
+        be = backend or os.environ.get("TDL_DIST_BACKEND") or \
+            ("nccl" if device_type == "cuda" and not native else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
         import datetime

@@ -220,3 +220,27 @@ def test_graph_replay_matches_eager(gpu, opt):
     assert cos > 0.999, cos
     assert ((ua - ub).norm() / ua.norm()).item() < 0.05
     torch.testing.assert_close(float(lb), float(la), rtol=1e-3, atol=1e-4)
+
+
+def test_bench_two_ranks_share_one_gpu(gpu, tmp_path):
+    """bench.py's multi-rank path on real GPU tensors: torchrun with 2 ranks on the one visible
+    device (TDL_SHARE_GPU), gloo for the bucketed gradient all-reduce (RCCL refuses two ranks on
+    one device) — rendezvous, overlap hooks, barrier-bracketed timing, MAX over ranks, one JSON
+    line from rank 0."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TDL_SHARE_GPU="1", TDL_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29633",
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "8", "--model", "resnet18", "--image-size", "64"]
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
