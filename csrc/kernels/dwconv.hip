@@ -426,6 +426,120 @@ __global__ void __launch_bounds__(NT) dw_slide_kernel(const bf16_t* __restrict__
   }
 }
 
+// The same sliding window with 4 channels per lane (8-B vectors) and the next column prefetched
+// one step ahead: half the registers of the 8-channel kernel (≈ 70 VGPRs → ≥ 6 waves per SIMD)
+// and a load in flight under every step's FMAs, so more bytes are in flight per CU; the block is
+// sized to the active lanes (channel vectors × pixel lanes rounded up to a wave).
+__device__ __forceinline__ void unpack4(const uint2& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 lo_hi(uint32_t v) {  // two bf16 → two fp32
+  f32x2 r;
+  r.x = __uint_as_float(v << 16);
+  r.y = __uint_as_float(v & 0xffff0000u);
+  return r;
+}
+
+template <bool FLIP>
+__global__ void __launch_bounds__(NT) dw_slide4_kernel(const bf16_t* __restrict__ in,
+                                                       const bf16_t* __restrict__ wt,
+                                                       const float* __restrict__ bias,
+                                                       bf16_t* __restrict__ out, int Hi, int Wi,
+                                                       int Ho, int Wo, int C, int Ph, int Pw,
+                                                       int relu, int lanes_c, int rpp, int seg,
+                                                       int relu_in,
+                                                       const bf16_t* __restrict__ mask_x) {
+  // The window is kept unpacked (fp32 pairs), so a step converts only its new column, and the
+  // FMAs run as packed fp32 pairs (v_pk_fma_f32).  (Measured alternatives, Xception-41 b128:
+  // columns prefetched in blocks of 4 — 141 VGPRs, 3 waves — 2394 img/s; XCD-aware row order
+  // 2471; both vs 2488 for this form.)
+  const int cv = C / 4;
+  const int t = threadIdx.x, lc = t % lanes_c, pb = t / lanes_c;
+  const int cvi = lc + blockIdx.y * lanes_c;
+  if (pb >= rpp || cvi >= cv) return;
+  const int pl = blockIdx.z * rpp + pb;  // pixel lane of the row (blockIdx.z: lane group)
+  const int c = cvi * 4;
+  const int row = blockIdx.x, n = row / Ho, ho = row - n * Ho;
+  const int w0 = pl * seg, w1 = min(Wo, w0 + seg);
+  if (w0 >= w1) return;
+  f32x2 wv[9][2], b[2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const uint2 q = *(const uint2*)(wt + (long)(FLIP ? 8 - k : k) * C + c);
+    wv[k][0] = lo_hi(q.x);
+    wv[k][1] = lo_hi(q.y);
+  }
+  b[0] = bias ? f32x2{bias[c], bias[c + 1]} : f32x2{0.f, 0.f};
+  b[1] = bias ? f32x2{bias[c + 2], bias[c + 3]} : f32x2{0.f, 0.f};
+  const bf16_t* base = in + (long)n * Hi * Wi * C + c;
+  int hi[3];
+  bool hv[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    hi[r] = ho - Ph + r;
+    hv[r] = (unsigned)hi[r] < (unsigned)Hi;
+  }
+  auto col = [&](int r, int wi) -> uint2 {
+    if (!hv[r] || (unsigned)wi >= (unsigned)Wi) return make_uint2(0, 0);
+    const uint2 v = *(const uint2*)(base + ((long)hi[r] * Wi + wi) * C);
+    return relu_in ? make_uint2(relu2(v.x), relu2(v.y)) : v;
+  };
+  f32x2 win[3][3][2];  // [row][column][channel pair], fp32
+  uint2 nxt[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const uint2 a1 = col(r, w0 - Pw), a2 = col(r, w0 - Pw + 1);
+    win[r][1][0] = lo_hi(a1.x);
+    win[r][1][1] = lo_hi(a1.y);
+    win[r][2][0] = lo_hi(a2.x);
+    win[r][2][1] = lo_hi(a2.y);
+    nxt[r] = col(r, w0 - Pw + 2);
+  }
+  bf16_t* orow = out + ((long)row * Wo) * C + c;
+#pragma unroll 3
+  for (int w = w0; w < w1; ++w) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        win[r][0][h] = win[r][1][h];
+        win[r][1][h] = win[r][2][h];
+      }
+      win[r][2][0] = lo_hi(nxt[r].x);
+      win[r][2][1] = lo_hi(nxt[r].y);
+      nxt[r] = col(r, w - Pw + 3);  // next step's column, in flight under this step's FMAs
+    }
+    f32x2 acc[2] = {b[0], b[1]};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          acc[h] = __builtin_elementwise_fma(win[r][s2][h], wv[r * 3 + s2][h], acc[h]);
+    float o[4] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y};
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    if (mask_x) {
+      const uint2 m = *(const uint2*)(mask_x + ((long)row * Wo + w) * C + c);
+      const f32x2 m0 = lo_hi(m.x), m1 = lo_hi(m.y);
+      o[0] = m0.x > 0.f ? o[0] : 0.f;
+      o[1] = m0.y > 0.f ? o[1] : 0.f;
+      o[2] = m1.x > 0.f ? o[2] : 0.f;
+      o[3] = m1.y > 0.f ? o[3] : 0.f;
+    }
+    *(uint2*)(orow + (long)w * C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+  }
+}
+
 // wgrad with the same sliding window over x: a lane walks a contiguous run of output columns of
 // each of its workgroup's rows; per output pixel one dy vector + the 3 vectors of the new x column.
 __global__ void __launch_bounds__(NT) dw_wgrad_slide(DwArgs a, int lanes_c, int rpp, int seg,
@@ -533,6 +647,38 @@ bool slide_ok(const DwArgs& a) {
 struct SlideGeom {
   int lanes_c, rpp, seg;
 };
+// 4-channel sliding kernel (default; TDL_DW_VEC=8 selects the 8-channel one)
+bool slide4() {
+  static const int v = [] {
+    const char* e = getenv("TDL_DW_VEC");
+    return e ? atoi(e) : 4;
+  }();
+  return v == 4;
+}
+
+// 4-channel kernel: TDL_DW_SEG > 0 spreads a row's pixel lanes over blockIdx.z so that each
+// lane's run is ≈ that many columns.  Default 0 (one block's lanes per row): measured on
+// Xception-41, runs of 2 / 4 / 8 columns lose to whole-row runs (2278 / 2402 / 2448 vs 2489
+// img/s) — the 2 warm-up columns each run loads cost more than the shorter dependency chain.
+struct Slide4Geom {
+  int lanes_c, rpp, seg, gz, nt;
+};
+Slide4Geom slide4_geom(int cv, int W) {
+  static const int target = [] {
+    const char* e = getenv("TDL_DW_SEG");
+    return e ? atoi(e) : 0;
+  }();
+  Slide4Geom g;
+  g.lanes_c = std::min(cv, NT);
+  g.rpp = std::max(1, std::min(NT / g.lanes_c, W));
+  const int lanes = target > 0 ? std::max(1, cdiv(W, target)) : g.rpp;
+  g.gz = std::max(1, cdiv(lanes, g.rpp));
+  g.rpp = cdiv(lanes, g.gz);
+  g.seg = cdiv(W, g.rpp * g.gz);
+  g.nt = cdiv(g.lanes_c * g.rpp, 64) * 64;
+  return g;
+}
+
 SlideGeom slide_geom(int cv, int W) {
   SlideGeom g;
   g.lanes_c = std::min(cv, NT);
@@ -567,7 +713,13 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
-  if (slide_ok(a)) {
+  if (slide_ok(a) && slide4()) {
+    const Slide4Geom g = slide4_geom(a.C / 4, a.Wo);
+    dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
+    hipLaunchKernelGGL(dw_slide4_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
+                       a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.lanes_c, g.rpp, g.seg,
+                       a.relu_in, (const bf16_t*)nullptr);
+  } else if (slide_ok(a)) {
     const SlideGeom g = slide_geom(a.C / 8, a.Wo);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
     hipLaunchKernelGGL(dw_slide_kernel<false>, grid, dim3(NT), 0, st, a.x, a.w, a.bias, a.out, a.H,
@@ -586,7 +738,13 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
-  if (slide_ok(a)) {  // stride-1 dgrad = forward of dy with the rotated filter, padding 2 − p
+  if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
+    const Slide4Geom g = slide4_geom(a.C / 4, a.W);
+    dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
+    hipLaunchKernelGGL(dw_slide4_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
+                       a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.lanes_c, g.rpp, g.seg,
+                       0, a.mask_x);
+  } else if (slide_ok(a)) {  // stride-1 dgrad = forward of dy with the rotated filter, padding 2 − p
     const SlideGeom g = slide_geom(a.C / 8, a.W);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));
     hipLaunchKernelGGL(dw_slide_kernel<true>, grid, dim3(NT), 0, st, a.dy, a.w, nullptr, a.out,
