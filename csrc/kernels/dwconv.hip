@@ -540,6 +540,119 @@ __global__ void __launch_bounds__(NT) dw_slide4_kernel(const bf16_t* __restrict_
   }
 }
 
+// LDS-tiled depthwise 3×3 stride 1: a workgroup stages its (TR+2)×(TW+2) input pixels × 64
+// channels once (coalesced 16-B loads, ≈1.3× the tile's own bytes incl. halo), then every lane
+// (8 channels × one output column) slides down the TR rows reading its 3×3 window from LDS.
+// The register-window kernels above re-fetch each input row for 3 output-row workgroups from the
+// fabric (PMC: 3.2× the input bytes); here the re-reads are LDS reads.
+constexpr int DT_TR = 8, DT_TW = 32, DT_CH = 64;
+constexpr int DT_CHUNKS = (DT_TR + 2) * (DT_TW + 2) * (DT_CH / 8);
+
+__device__ __forceinline__ void unpack8x2(const uint4& v, f32x2* f) {
+  f[0] = lo_hi(v.x);
+  f[1] = lo_hi(v.y);
+  f[2] = lo_hi(v.z);
+  f[3] = lo_hi(v.w);
+}
+
+template <bool FLIP>
+__global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ in,
+                                                     const bf16_t* __restrict__ wt,
+                                                     const float* __restrict__ bias,
+                                                     bf16_t* __restrict__ out, int Hi, int Wi,
+                                                     int Ho, int Wo, int C, int Ph, int Pw,
+                                                     int relu, int tr, int tw, int rg, int tiles_h,
+                                                     int tiles_w, int relu_in,
+                                                     const bf16_t* __restrict__ mask_x) {
+  // tile: tr × tw output pixels (runtime, ≤ DT_TR × DT_TW, balanced splits of Ho / Wo); lanes:
+  // 8 channel lanes × tw column lanes × rg row groups (each slides over ⌈tr / rg⌉ rows)
+  __shared__ uint4 tile[DT_CHUNKS];
+  const int t = threadIdx.x;
+  int b = blockIdx.x;
+  const int tx = b % tiles_w;
+  b /= tiles_w;
+  const int ty = b % tiles_h;
+  const int n = b / tiles_h;
+  const int h0 = ty * tr, w0 = tx * tw, cg0 = blockIdx.y * DT_CH;
+  const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
+  const bf16_t* src = in + (long)n * Hi * Wi * C;
+  for (int i = t; i < chunks; i += blockDim.x) {
+    const int k = i & 7, pix = i >> 3;
+    const int r = pix / pitch, cc = pix - r * pitch;
+    const int hi = h0 - Ph + r, wi = w0 - Pw + cc, ch = cg0 + k * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if ((unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi && ch < C) {
+      v = *(const uint4*)(src + ((long)hi * Wi + wi) * C + ch);
+      if (relu_in) v = relu8(v);
+    }
+    tile[i] = v;
+  }
+  __syncthreads();
+  const int cl = t & 7, rest = t >> 3, pw = rest % tw, g = rest / tw;
+  const int w = w0 + pw, c = cg0 + cl * 8;
+  const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
+  const int r1 = min(min(tr, r0 + rpg), Ho - h0);
+  if (g >= rg || w >= Wo || c >= C || r0 >= r1) return;
+  f32x2 wv[9][4], bb[4];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) unpack8x2(*(const uint4*)(wt + (long)(FLIP ? 8 - k : k) * C + c), wv[k]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    bb[q] = bias ? f32x2{bias[c + 2 * q], bias[c + 2 * q + 1]} : f32x2{0.f, 0.f};
+  f32x2 win[3][3][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) unpack8x2(tile[((r0 + r) * pitch + pw + s2) * 8 + cl], win[r + 1][s2]);
+  for (int h = r0; h < r1; ++h) {
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        win[0][s2][q] = win[1][s2][q];
+        win[1][s2][q] = win[2][s2][q];
+      }
+      unpack8x2(tile[((h + 2) * pitch + pw + s2) * 8 + cl], win[2][s2]);
+    }
+    f32x2 acc[4] = {bb[0], bb[1], bb[2], bb[3]};
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[q] = __builtin_elementwise_fma(win[r][s2][q], wv[r * 3 + s2][q], acc[q]);
+    float o[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[2 * q] = acc[q].x;
+      o[2 * q + 1] = acc[q].y;
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    const long op = (((long)n * Ho + h0 + h) * Wo + w) * C + c;
+    if (mask_x) mask_pos(o, mask_x + op);
+    *(uint4*)(out + op) = pack8(o);
+  }
+}
+
+// balanced tiling of an Ho × Wo output: tw ≤ 32 columns, tr ≤ 8 rows, rg = 32 / tw row groups
+struct DwTileGeom {
+  int tr, tw, rg, th, twn, nt;
+};
+DwTileGeom dw_tile_geom(int Ho, int Wo) {
+  DwTileGeom g;
+  g.twn = cdiv(Wo, DT_TW);
+  g.tw = cdiv(Wo, g.twn);
+  g.th = cdiv(Ho, DT_TR);
+  g.tr = cdiv(Ho, g.th);
+  g.rg = std::max(1, std::min(DT_TW / g.tw, g.tr));
+  g.nt = cdiv(8 * g.tw * g.rg, 64) * 64;
+  return g;
+}
+
 // wgrad with the same sliding window over x: a lane walks a contiguous run of output columns of
 // each of its workgroup's rows; per output pixel one dy vector + the 3 vectors of the new x column.
 __global__ void __launch_bounds__(NT) dw_wgrad_slide(DwArgs a, int lanes_c, int rpp, int seg,
@@ -647,6 +760,15 @@ bool slide_ok(const DwArgs& a) {
 struct SlideGeom {
   int lanes_c, rpp, seg;
 };
+// LDS-tiled kernel (default; TDL_DW_TILE=0 falls back to the sliding-window kernels)
+bool dw_tile() {
+  static const int v = [] {
+    const char* e = getenv("TDL_DW_TILE");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
 // 4-channel sliding kernel (default; TDL_DW_VEC=8 selects the 8-channel one)
 bool slide4() {
   static const int v = [] {
@@ -713,7 +835,13 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
-  if (slide_ok(a) && slide4()) {
+  if (slide_ok(a) && dw_tile()) {
+    const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
+    dim3 grid((unsigned)(a.N * g.th * g.twn), (unsigned)cdiv(a.C, DT_CH));
+    hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
+                       a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
+                       g.twn, a.relu_in, (const bf16_t*)nullptr);
+  } else if (slide_ok(a) && slide4()) {
     const Slide4Geom g = slide4_geom(a.C / 4, a.Wo);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
     hipLaunchKernelGGL(dw_slide4_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
@@ -738,7 +866,13 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
 
 void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
-  if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
+  if (slide_ok(a) && dw_tile()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
+    const DwTileGeom g = dw_tile_geom(a.H, a.W);
+    dim3 grid((unsigned)(a.N * g.th * g.twn), (unsigned)cdiv(a.C, DT_CH));
+    hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
+                       a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
+                       g.twn, 0, a.mask_x);
+  } else if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const Slide4Geom g = slide4_geom(a.C / 4, a.W);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
     hipLaunchKernelGGL(dw_slide4_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
