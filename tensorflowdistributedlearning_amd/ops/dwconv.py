@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+from . import workspace
 from .conv import ConvGeom
 
 
@@ -72,9 +73,10 @@ class _DwConvFn(torch.autograd.Function):
                 ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
                                    geom.padding[2], geom.dilation[0], geom.dilation[1],
                                    x if ctx.relu_in else None)
-            dw = torch.zeros(weight.shape, device=dy.device, dtype=torch.float32)
-            db = torch.zeros(x.shape[-1], device=dy.device, dtype=torch.float32) \
-                if bias is not None else None
+            # accumulated by the kernels: pre-zeroed slices of the per-step arena (one fill per
+            # step instead of one per layer); deliver_grad copies them out
+            dw = workspace.zeros(tuple(weight.shape), dy.device)
+            db = workspace.zeros((x.shape[-1],), dy.device) if bias is not None else None
             ext().dwconv_wgrad(g, x, dw, db, geom.stride[0], geom.stride[1], geom.padding[0],
                                geom.padding[2], geom.dilation[0], geom.dilation[1],
                                bool(ctx.relu_in))
