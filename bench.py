@@ -27,6 +27,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown  # noqa: E402
+from tensorflowdistributedlearning_amd.ops import streams  # noqa: E402
 from tensorflowdistributedlearning_amd.engine.trainer import Trainer  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy, lovasz_hinge  # noqa: E402
 from tensorflowdistributedlearning_amd.data.synthetic import imagenet_batch, segmentation_batch  # noqa: E402
@@ -79,7 +80,8 @@ def main():
         metric = "images/sec (whole node), reference DeepLab-ResNet 101x101x2 bf16"
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
                "image": "101x101x2", "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "adam",
-               "loss": "lovasz_hinge", "hip_graph": args.graph}
+               "loss": "lovasz_hinge", "hip_graph": args.graph,
+               "wgrad_side_stream": streams.enabled()}
         base = REF_DEEPLAB_2GPU / 2 * n
     else:
         per_gpu = args.batch or 256
@@ -97,7 +99,8 @@ def main():
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "sgd_momentum",
-               "loss": "softmax_ce", "hip_graph": args.graph}
+               "loss": "softmax_ce", "hip_graph": args.graph,
+               "wgrad_side_stream": streams.enabled()}
         base = REF_PER_GPU_DERIVED * n
 
     def step():

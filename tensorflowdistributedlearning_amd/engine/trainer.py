@@ -16,7 +16,7 @@ from ..models.params import FlatParams
 from ..parallel.bucketer import GradBucketer
 from ..parallel.dist import get_context
 from .optimizer import build_optimizer
-from ..ops import workspace
+from ..ops import workspace, streams
 
 
 class PhaseTimer:
@@ -112,6 +112,8 @@ class Trainer:
         if t:
             t.mark("forward")
         loss.backward()
+        if self.device.type == "cuda":
+            streams.join(self.device)  # side-stream wgrads (ops/streams.py)
         self.flat.finish_grads()
         if t:
             t.mark("backward")

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view
 from . import workspace
+from . import streams
 
 
 @dataclass(frozen=True)
@@ -244,36 +245,51 @@ class _Conv2dFn(torch.autograd.Function):
                 else:
                     conv_dgrad(dy, w, ctx.x_shape, geom, out=join.buf, accumulate=True)
                 dx = join.take()
-        want_bias = bias is not None and bias.requires_grad
-        bias_buf, bias_direct = None, False
-        if want_bias:
-            nb = dy.shape[-1]  # physical output channels (> bias.numel() when channel-padded)
-            bt, bfresh = grad_target(bias)
-            if bt is not None and nb != bias.numel():
-                bt = flat_view(bias, nb, "grad")  # the zero slack after the bias takes the pad
-            bias_direct = bt is not None and bfresh
-            bias_buf = bt if bias_direct else torch.empty(nb, device=dy.device,
-                                                          dtype=torch.float32)
-        if weight.requires_grad:
-            target, fresh = grad_target(weight)
-            if ctx.layer is not None and ctx.layer.grad_needs_unpad():
-                dw = conv_wgrad(dy, x, ctx.layer.padded_weight_shape(), geom, bias_grad=bias_buf)
-                deliver_grad(weight, ctx.layer.unpad_grad(dw))
-            elif target is not None:
-                conv_wgrad(dy, x, tuple(weight.shape), geom, out=target, accumulate=not fresh,
-                           bias_grad=bias_buf)
-                deliver_grad(weight, written=True)
-            else:
-                dw = conv_wgrad(dy, x, tuple(weight.shape), geom, bias_grad=bias_buf)
-                deliver_grad(weight, dw)
-        elif want_bias:
-            bias_buf.copy_(dy.float().reshape(-1, dy.shape[-1]).sum(0))
-        if want_bias:
-            if bias_direct:
-                deliver_grad(bias, written=True)
-            else:
-                deliver_grad(bias, bias_buf[: bias.numel()])
+        side = streams.side(dy.device) if (weight.requires_grad or
+                                            (bias is not None and bias.requires_grad)) else None
+        if side is None:
+            _conv_param_grads(ctx, dy, x, weight, bias)
+        else:  # weight / bias gradients on the side stream, concurrent with the dgrad chain
+            side.wait_stream(torch.cuda.current_stream(dy.device))
+            with torch.cuda.stream(side):
+                _conv_param_grads(ctx, dy, x, weight, bias)
+            dy.record_stream(side)
+            x.record_stream(side)
         return dx, None, None, None, None, None, None, None
+
+
+def _conv_param_grads(ctx, dy, x, weight, bias):
+    """dW (+ bias gradient) of one conv backward, delivered to the parameters."""
+    geom = ctx.geom
+    want_bias = bias is not None and bias.requires_grad
+    bias_buf, bias_direct = None, False
+    if want_bias:
+        nb = dy.shape[-1]  # physical output channels (> bias.numel() when channel-padded)
+        bt, bfresh = grad_target(bias)
+        if bt is not None and nb != bias.numel():
+            bt = flat_view(bias, nb, "grad")  # the zero slack after the bias takes the pad
+        bias_direct = bt is not None and bfresh
+        bias_buf = bt if bias_direct else torch.empty(nb, device=dy.device,
+                                                      dtype=torch.float32)
+    if weight.requires_grad:
+        target, fresh = grad_target(weight)
+        if ctx.layer is not None and ctx.layer.grad_needs_unpad():
+            dw = conv_wgrad(dy, x, ctx.layer.padded_weight_shape(), geom, bias_grad=bias_buf)
+            deliver_grad(weight, ctx.layer.unpad_grad(dw))
+        elif target is not None:
+            conv_wgrad(dy, x, tuple(weight.shape), geom, out=target, accumulate=not fresh,
+                       bias_grad=bias_buf)
+            deliver_grad(weight, written=True)
+        else:
+            dw = conv_wgrad(dy, x, tuple(weight.shape), geom, bias_grad=bias_buf)
+            deliver_grad(weight, dw)
+    elif want_bias:
+        bias_buf.copy_(dy.float().reshape(-1, dy.shape[-1]).sum(0))
+    if want_bias:
+        if bias_direct:
+            deliver_grad(bias, written=True)
+        else:
+            deliver_grad(bias, bias_buf[: bias.numel()])
 
 
 def conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False, want_stats=False,

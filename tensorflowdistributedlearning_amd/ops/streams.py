@@ -1,0 +1,50 @@
+"""Side HIP stream for weight gradients (default on; ``TDL_WGRAD_STREAM=0`` disables).
+
+A conv's wgrad and dgrad both read only dy; the rest of the backward chain (the BN backward of the
+layer below, its dgrad, …) needs only dgrad.  With the side stream the wgrad (+ bias colsum)
+runs concurrently with that chain, so the memory-bound BN kernels can overlap the MFMA-bound
+wgrads.  Ordering: the side stream waits for the compute stream before each wgrad (dy ready);
+the compute stream joins the side stream before any gradient bucket is all-reduced
+(parallel/bucketer.py) and after backward (engine/trainer.py), so no collective or optimizer
+reads a gradient that is still being written.  Disabled during HIP-graph capture.
+
+Measured on one MI355X (bench.py, eager): ResNet-50 b256 9646 → 9925 img/s, Xception-41 b128
+2551 → 2650, reference DeepLab preset b64 4685 → 4814."""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_ENABLED = os.environ.get("TDL_WGRAD_STREAM", "1") == "1"
+_SIDE: dict = {}
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def set_enabled(flag: bool):
+    global _ENABLED
+    _ENABLED = bool(flag)
+
+
+def side(device):
+    """The side stream for ``device`` when enabled (and not capturing a graph), else None."""
+    if not _ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return None
+    s = _SIDE.get(device)
+    if s is None:
+        s = _SIDE[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def join(device=None):
+    """Make the current stream wait for all work queued on the side stream(s).  A no-op while a
+    HIP graph is being captured: nothing is queued on the side stream then (``side`` returns
+    None), and a wait on an event of a non-captured stream must not enter the graph."""
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return
+    for dev, s in _SIDE.items():
+        if device is None or dev == torch.device(device):
+            torch.cuda.current_stream(dev).wait_stream(s)

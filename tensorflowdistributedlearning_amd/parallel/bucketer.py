@@ -27,6 +27,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..ops import streams
+
 
 class Bucket:
     __slots__ = ("index", "lo", "hi", "params", "pending", "launched", "work")
@@ -123,6 +125,8 @@ class GradBucketer:
 
     def _launch(self, b):
         view = self.flat.grad[b.lo:b.hi]
+        if view.is_cuda:
+            streams.join(view.device)  # wgrads still running on the side stream (ops/streams.py)
         if self.comm_hook is not None:
             b.work = self.comm_hook(b, view)
         elif self.ctx is not None and self.ctx.is_distributed:
