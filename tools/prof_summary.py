@@ -36,6 +36,26 @@ def main():
     gaps = [int(seg[i + 1]["Start_Timestamp"]) - int(seg[i]["End_Timestamp"]) for i in range(len(seg) - 1)]
     print(f"idle between kernels {sum(g for g in gaps if g > 0) / 1e6 / k:.2f} ms/step "
           f"({sum(1 for g in gaps if g > 5000) / k:.0f} gaps > 5 us per step)")
+    # With the side (wgrad) stream, launch-order gaps overstate idleness: report the time no
+    # stream has a kernel running, and the kernel transitions that leave the device idle.
+    idle, end, prev = 0, t0, None
+    trans = collections.Counter()
+    for r in seg:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if s > end:
+            idle += s - end
+            if prev is not None and s - end > 5000:
+                trans[(prev, _short(r["Kernel_Name"]))] += s - end
+        if e > end:
+            end, prev = e, _short(r["Kernel_Name"])
+    print(f"device idle (no stream busy) {idle / 1e6 / k:.2f} ms/step; largest idle transitions:")
+    for (p, n), t in trans.most_common(5):
+        print(f"  {t / 1e3 / k:7.1f} us/step  {p} -> {n}")
+
+
+def _short(name):
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))
+    return re.sub(r"^void ", "", n)[:60]
 
 
 if __name__ == "__main__":
