@@ -233,6 +233,10 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.relu:
             dy = relu_bwd(dy, y)
         dx = None
+        side = streams.side(dy.device) if (weight.requires_grad or
+                                            (bias is not None and bias.requires_grad)) else None
+        if side is not None:  # dy is ready here: the wgrad may overlap this conv's own dgrad
+            side.wait_stream(torch.cuda.current_stream(dy.device))
         if ctx.needs_input_grad[0]:
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
                 compute_weight(weight, dy.dtype)
@@ -245,12 +249,9 @@ class _Conv2dFn(torch.autograd.Function):
                 else:
                     conv_dgrad(dy, w, ctx.x_shape, geom, out=join.buf, accumulate=True)
                 dx = join.take()
-        side = streams.side(dy.device) if (weight.requires_grad or
-                                            (bias is not None and bias.requires_grad)) else None
         if side is None:
             _conv_param_grads(ctx, dy, x, weight, bias)
         else:  # weight / bias gradients on the side stream, concurrent with the dgrad chain
-            side.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(side):
                 _conv_param_grads(ctx, dy, x, weight, bias)
             dy.record_stream(side)
