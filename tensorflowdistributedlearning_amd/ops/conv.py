@@ -235,7 +235,7 @@ class _Conv2dFn(torch.autograd.Function):
         dx = None
         side = streams.side(dy.device) if (weight.requires_grad or
                                             (bias is not None and bias.requires_grad)) else None
-        if side is not None:  # dy is ready here: the wgrad may overlap this conv's own dgrad
+        if side is not None and streams.EARLY_WAIT:  # dy is ready: wgrad may overlap this dgrad
             side.wait_stream(torch.cuda.current_stream(dy.device))
         if ctx.needs_input_grad[0]:
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
@@ -252,6 +252,8 @@ class _Conv2dFn(torch.autograd.Function):
         if side is None:
             _conv_param_grads(ctx, dy, x, weight, bias)
         else:  # weight / bias gradients on the side stream, concurrent with the dgrad chain
+            if not streams.EARLY_WAIT:
+                side.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(side):
                 _conv_param_grads(ctx, dy, x, weight, bias)
             dy.record_stream(side)

@@ -17,6 +17,9 @@ import os
 import torch
 
 _ENABLED = os.environ.get("TDL_WGRAD_STREAM", "1") == "1"
+# Record the side stream's wait on dy before the conv's dgrad is launched (the wgrad overlaps that
+# dgrad too); TDL_WGRAD_EARLY=0 records it after the dgrad launch (the previous ordering, for A/B).
+EARLY_WAIT = os.environ.get("TDL_WGRAD_EARLY", "1") == "1"
 _SIDE: dict = {}
 
 
