@@ -97,6 +97,7 @@ Communicator::~Communicator() {
   }
   for (auto& w : works_) hipEventDestroy(w.done);
   for (auto e : free_events_) hipEventDestroy(e);
+  for (auto e : parked_events_) hipEventDestroy(e);
   if (ready_) hipEventDestroy(ready_);
 }
 
@@ -181,11 +182,18 @@ void Communicator::synchronize() {
   {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& w : works_) evs.push_back(w.done);
+    ++sync_pins_;  // none of these handles is recycled until we are done with them
   }
-  // events are only recycled after they completed, so synchronising a stale handle is harmless
   for (auto e : evs) {
     if (failed_) break;
     hipEventSynchronize(e);
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (--sync_pins_ == 0) {
+      free_events_.insert(free_events_.end(), parked_events_.begin(), parked_events_.end());
+      parked_events_.clear();
+    }
   }
   if (failed_) throw std::runtime_error("RCCL communicator failed: " + error());
 }
@@ -225,7 +233,7 @@ void Communicator::watchdog() {
       std::lock_guard<std::mutex> g(mu_);
       // retire completed collectives in issue order (the comm stream is in-order)
       while (!works_.empty() && hipEventQuery(works_.front().done) == hipSuccess) {
-        free_events_.push_back(works_.front().done);
+        (sync_pins_ > 0 ? parked_events_ : free_events_).push_back(works_.front().done);
         works_.pop_front();
       }
       if (!works_.empty()) {

@@ -83,6 +83,11 @@ class Communicator {
   mutable std::mutex mu_;
   std::deque<Work> works_;
   std::vector<hipEvent_t> free_events_;
+  // synchronize() waits on snapshotted event handles outside the lock: while any such wait is in
+  // progress, retired events are parked here instead of being recycled, so a handle it holds is
+  // never re-recorded by a later collective (it would then also wait for that newer work)
+  std::vector<hipEvent_t> parked_events_;
+  int sync_pins_ = 0;
   uint64_t next_ticket_ = 1;
   std::atomic<bool> failed_{false};
   std::atomic<bool> stop_{false};

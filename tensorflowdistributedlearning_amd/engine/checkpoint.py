@@ -109,18 +109,24 @@ def latest_checkpoint(directory):
     return os.path.join(directory, f"model.ckpt-{steps[-1]}.safetensors") if steps else None
 
 
-def restore(path, model, optimizer=None, flat=None):
-    """Load a checkpoint written by :func:`save`; returns the global step."""
+class CheckpointMismatchError(KeyError):
+    """A checkpoint lacks variables the model (or optimizer) needs — TF's Saver raises
+    ``NotFoundError`` in the same situation; training must not continue silently from a partial
+    random init (e.g. a checkpoint of another preset, or a renamed ``tf_names()`` mapping)."""
+
+
+def restore(path, model, optimizer=None, flat=None, strict=True):
+    """Load a checkpoint written by :func:`save`; returns the global step.
+
+    ``strict`` (default): every model variable — and, with ``optimizer``, every slot variable —
+    must be present with a matching element count, else :class:`CheckpointMismatchError` lists
+    them and nothing is loaded.  ``strict=False`` loads what matches and warns about the rest."""
     tensors = load_file(path)
     names = _names(model)
     sd = model.state_dict()
-    with torch.no_grad():
-        for k, v in sd.items():
-            key = names[k]
-            if key in tensors:
-                v.copy_(tensors[key].to(v.device, v.dtype).reshape(v.shape))
-    if flat is not None:
-        flat.sync_lowp()
+    missing = [names[k] for k, v in sd.items()
+               if names[k] not in tensors or tensors[names[k]].numel() != v.numel()]
+    slot_plan = []
     if optimizer is not None:
         pname = {id(p): n for n, p in model.named_parameters()}
         slots = optimizer.state_tensors()
@@ -129,8 +135,26 @@ def restore(path, model, optimizer=None, flat=None):
             base = names.get(pname[id(p)], pname[id(p)])
             for sname, st in slots.items():
                 key = f"{base}/{sname}"
-                if key in tensors:
-                    st[o:e].copy_(tensors[key].reshape(-1).to(st.device))
+                if key in tensors and tensors[key].numel() == e - o:
+                    slot_plan.append((key, st, o, e))
+                else:
+                    missing.append(key)
+    if missing:
+        msg = (f"{path}: {len(missing)} variable(s) missing or of another size, e.g. "
+               f"{missing[:5]}")
+        if strict:
+            raise CheckpointMismatchError(msg)
+        import warnings
+        warnings.warn("partial restore — " + msg)
+    with torch.no_grad():
+        for k, v in sd.items():
+            key = names[k]
+            if key in tensors and tensors[key].numel() == v.numel():
+                v.copy_(tensors[key].to(v.device, v.dtype).reshape(v.shape))
+        for key, st, o, e in slot_plan:
+            st[o:e].copy_(tensors[key].reshape(-1).to(st.device))
+    if flat is not None:
+        flat.sync_lowp()
     step = int(tensors["global_step"][0]) if "global_step" in tensors else 0
     if optimizer is not None:
         optimizer.step_count = step

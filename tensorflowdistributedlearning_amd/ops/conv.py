@@ -258,6 +258,7 @@ class _Conv2dFn(torch.autograd.Function):
                 _conv_param_grads(ctx, dy, x, weight, bias)
             dy.record_stream(side)
             x.record_stream(side)
+            streams.join_at_backward_end(dy.device)  # backward() returns joined
         return dx, None, None, None, None, None, None, None
 
 

@@ -42,6 +42,37 @@ def side(device):
     return s
 
 
+_JOIN_QUEUED: dict = {}  # device -> autograd graph-task id whose final callback joins it
+
+
+def join_at_backward_end(device):
+    """Make the running autograd pass end with the caller's stream joined to the side stream.
+
+    Called by every backward that queues work on the side stream.  The first call of a pass
+    registers an autograd final callback; the engine runs final callbacks on the streams that
+    were current around the user's ``backward()`` call (after syncing them with the leaf
+    streams), so ``loss.backward()`` returns with every gradient the side stream writes ordered
+    before anything the caller queues next — also outside :class:`Trainer`, which joins
+    explicitly as well.  Parameters' ``.grad`` tensors are therefore safe to read on the
+    caller's stream without a manual :func:`join`.  Keyed by the graph-task id, so a pass that
+    died before its callbacks ran cannot suppress the next pass's registration."""
+    dev = torch.device(device)
+    task = torch._C._current_graph_task_id()
+    if task < 0:  # not inside a backward pass (a direct call of the backward function):
+        join(dev)  # called after the side-stream work was queued, so join right away
+        return
+    if _JOIN_QUEUED.get(dev) == task:
+        return
+
+    def _cb():
+        if _JOIN_QUEUED.get(dev) == task:
+            del _JOIN_QUEUED[dev]
+        join(dev)
+
+    torch.autograd.Variable._execution_engine.queue_callback(_cb)
+    _JOIN_QUEUED[dev] = task
+
+
 def join(device=None):
     """Make the current stream wait for all work queued on the side stream(s).  A no-op while a
     HIP graph is being captured: nothing is queued on the side stream then (``side`` returns

@@ -85,6 +85,15 @@ def test_checkpoint_roundtrip_with_adam_slots(tmp_path):
     tr.train_step(x, y)
     tr2.train_step(x, y)
     torch.testing.assert_close(tr.flat.master, tr2.flat.master, rtol=1e-5, atol=1e-6)
+    # a checkpoint of another preset (different depth) is refused, not half-loaded
+    net3 = DeepLabResNet(model_name="m", in_channels=2, output_stride=8, base_depth=8,
+                         input_shape=(16, 16), n_blocks=(1, 2, 1))
+    before = {k: v.clone() for k, v in net3.state_dict().items()}
+    with pytest.raises(ckpt.CheckpointMismatchError, match="missing"):
+        ckpt.restore(ckpt.latest_checkpoint(d), net3)
+    assert all(torch.equal(before[k], v) for k, v in net3.state_dict().items())
+    with pytest.warns(UserWarning, match="partial restore"):
+        ckpt.restore(ckpt.latest_checkpoint(d), net3, strict=False)
 
 
 def test_crc32c_and_tfrecord_framing(tmp_path):

@@ -264,27 +264,128 @@ def test_bench_two_ranks_share_one_gpu(gpu, tmp_path):
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
 
 
+def _stall_side_stream(gpu, cycles=20_000_000):
+    """Queue a long spin kernel on the wgrad side stream so that every side-stream write lands
+    milliseconds after the compute stream could have moved on: a missing join then reads stale
+    gradients instead of passing by luck of timing."""
+    from tensorflowdistributedlearning_amd.ops import streams
+    s = streams.side(gpu)
+    assert s is not None
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(cycles)
+
+
 @pytest.mark.parametrize("model", ["resnet18", "resnet50"])
 def test_side_stream_wgrad_matches_serial(gpu, model):
-    """Weight gradients on the side stream (ops/streams.py) vs all on one stream: same gradients
-    (frozen BN: no float atomics in the step), i.e. the stream joins leave no race."""
+    """Weight gradients on the side stream (ops/streams.py) vs all on one stream, with a real
+    learning rate and momentum: the parameters after several steps must agree bit for bit
+    (frozen BN: no float atomics in the step).  No host synchronisation between the steps and
+    the read-back, and the side stream is stalled before every step, so an optimizer that read a
+    half-written gradient would change the trajectory."""
     from tensorflowdistributedlearning_amd.ops import streams
     torch.manual_seed(9)
     nets = [models.build(model, num_classes=10) for _ in range(2)]
     nets[1].load_state_dict(nets[0].state_dict())
     x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
-    grads = []
+    masters, start = [], None
     old = streams.enabled()
     try:
         for flag, net in zip((False, True), nets):
             streams.set_enabled(flag)
-            tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.0, momentum=0.0,
-                                                                      weight_decay=0.0))
+            tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.05, momentum=0.9,
+                                                                      weight_decay=1e-4))
             tr.train_mode = False
-            for _ in range(2):
+            if start is None:
+                start = tr.flat.master.clone()
+            for _ in range(4):
+                if flag:
+                    _stall_side_stream(gpu)
                 tr.train_step(x, y)
-            torch.cuda.synchronize()
-            grads.append(tr.flat.grad.clone())
+            masters.append(tr.flat.master.clone())  # queued on the compute stream, no sync
     finally:
         streams.set_enabled(old)
-    torch.testing.assert_close(grads[1], grads[0], rtol=1e-5, atol=1e-6)
+    torch.cuda.synchronize()
+    assert not torch.equal(masters[0], start)  # the steps really updated the parameters
+    torch.testing.assert_close(masters[1], masters[0], rtol=0, atol=0)
+
+
+def test_plain_backward_joins_side_stream(gpu):
+    """``loss.backward()`` outside the Trainer returns with the side-stream weight gradients
+    ordered before the caller's stream (autograd final callback, ops/streams.py): ``p.grad`` read
+    right after backward — no join, no synchronize — equals the single-stream gradient even
+    with the side stream stalled."""
+    from tensorflowdistributedlearning_amd.ops import streams
+    torch.manual_seed(6)
+    m = models.resnet18(num_classes=10).to(gpu)
+    m.train()
+    for mod in m.modules():
+        if mod.__class__.__name__ == "BatchNorm":
+            mod.train(False)
+    x = torch.randn(8, 64, 64, 8, device=gpu, dtype=torch.bfloat16)
+    outs = []
+    old = streams.enabled()
+    try:
+        for flag in (False, True):
+            streams.set_enabled(flag)
+            for p in m.parameters():
+                p.grad = None
+            if flag:
+                _stall_side_stream(gpu)
+            m(x).float().sum().backward()
+            outs.append(torch.cat([p.grad.float().flatten() for p in m.parameters()
+                                   if p.grad is not None]))  # read on the caller's stream
+    finally:
+        streams.set_enabled(old)
+    torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("early", [True, False])
+def test_bucket_launch_sees_complete_gradients(gpu, early, monkeypatch):
+    """GradBucketer with a fake communicator that behaves like ProcessGroupNCCL: its 'collective'
+    stream waits on whatever stream is current at launch and snapshots the bucket there.  Every
+    snapshot must equal the bucket's final gradient (no launch ordered before a producer), for
+    both side-stream wait orderings (streams.EARLY_WAIT); the streams the launches came from are
+    recorded to show both the side and the compute stream issue collectives."""
+    from tensorflowdistributedlearning_amd.ops import streams
+    from tensorflowdistributedlearning_amd.parallel.bucketer import GradBucketer
+    monkeypatch.setattr(streams, "EARLY_WAIT", early)
+    old = streams.enabled()
+    streams.set_enabled(True)
+    try:
+        torch.manual_seed(11)
+        m = models.resnet50(num_classes=10)
+        tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.0, momentum=0.0))
+        tr.train_mode = False
+        comm = torch.cuda.Stream(gpu)
+        snaps, launch_streams = {}, []
+
+        class Work:
+            def __init__(self, ev):
+                self.ev = ev
+
+            def wait(self):
+                torch.cuda.current_stream(gpu).wait_event(self.ev)
+
+        def hook(b, view):
+            cur = torch.cuda.current_stream(gpu)
+            launch_streams.append(cur.stream_id)
+            comm.wait_stream(cur)
+            with torch.cuda.stream(comm):
+                snaps[b.index] = view.clone()
+                ev = torch.cuda.Event()
+                ev.record(comm)
+            return Work(ev)
+
+        tr.bucketer = GradBucketer(tr.flat, None, bucket_mb=2.0, first_bucket_mb=0.5,
+                                   comm_hook=hook)
+        x, y = imagenet_batch(8, 64, num_classes=10, device=gpu)
+        _stall_side_stream(gpu)
+        tr.train_step(x, y)
+        torch.cuda.synchronize()
+        assert len(snaps) == len(tr.bucketer.buckets) > 4
+        for b in tr.bucketer.buckets:
+            torch.testing.assert_close(snaps[b.index], tr.flat.grad[b.lo:b.hi], rtol=0, atol=0)
+        side_id = streams.side(gpu).stream_id
+        assert side_id in launch_streams  # hooks fired inside the side-stream block
+    finally:
+        streams.set_enabled(old)
