@@ -68,6 +68,9 @@ def main():
     if n != args.gpus and ctx.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}", file=sys.stderr)
     dev = ctx.device
+    prio = int(os.environ.get("TDL_STREAM_PRIO", "0"))
+    if prio and dev.type == "cuda":  # experiment: run the compute stream at a given priority
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=prio))
     torch.manual_seed(1234)
 
     if args.model == "deeplab_ref":

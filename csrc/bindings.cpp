@@ -150,7 +150,7 @@ void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
 }
 
 void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                int64_t dh, int64_t dw, bool accumulate) {
+                int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -161,6 +161,13 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
   a.dy_bytes = nbytes32(dy); a.w_bytes = nbytes32(w); a.out_bytes = nbytes32(dx);
   a.M = a.N * a.H * a.W; a.Ng = a.C; a.Kg = a.R * a.S * a.K; a.ldc = a.C; a.relu = 0;
   a.beta = accumulate ? 1 : 0;
+  a.mask = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == torch::kUInt8 && mask->is_contiguous() &&
+                mask->numel() * 8 == dx.numel() && dx.size(3) % 64 == 0,
+                "conv_dgrad mask: uint8 [numel(dx)/8], C % 64 == 0");
+    a.mask = (const uint8_t*)mask->data_ptr();
+  }
   if (a.M == 0) return;
   conv_dgrad_launch(a, stream());
 }
@@ -648,7 +655,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
-        py::arg("accumulate") = false);
+        py::arg("accumulate") = false, py::arg("mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
   m.attr("AMAX_SLOT") = AMAX_SLOT;

@@ -171,7 +171,8 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     const int cvecs = C / 8, rpp = NT / cvecs;
     static const int cap = env_int("TDL_BN_RED_BLOCKS", 512);
     static const int u = env_int("TDL_BN_RED_U", 4);
-    long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * 16)));
+    static const int minr = env_int("TDL_BN_RED_MINR", 16);
+    long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * minr)));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
     if (u == 8)
@@ -234,6 +235,7 @@ __device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
   return (uint32_t)v;
 }
 
+template <int U>
 __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict__ x,
                                                        const float* __restrict__ coef,
                                                        const bf16_t* __restrict__ res,
@@ -267,15 +269,26 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
     sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
   };
   if (hoist) load_coef((int)(i % cvecs));
-  for (; i < nvec; i += stride) {
-    if (!hoist) load_coef((int)(i % cvecs));
+  for (; i < nvec; i += U * stride) {
+    uint4 lx[U], lr[U];  // U vectors per thread in flight: all loads issued before any use
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long k = i + u * stride < nvec ? i + u * stride : i;
+      lx[u] = ((const uint4*)x)[k];
+      if (res) lr[u] = ((const uint4*)res)[k];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+    const long k = i + u * stride;
+    if (k >= nvec) break;
+    if (!hoist) load_coef((int)(k % cvecs));
     float v[8];
-    unpack(((const uint4*)x)[i], v);
+    unpack(lx[u], v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
     if (res) {
       float r[8];
-      unpack(((const uint4*)res)[i], r);
+      unpack(lr[u], r);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += r[j];
     }
@@ -284,14 +297,14 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
     const uint4 packed = pack8(v);
-    ((uint4*)y)[i] = packed;
+    ((uint4*)y)[k] = packed;
     if (mask) {  // ReLU mask of the stored bf16 values, one bit per element (backward relu mode 3)
       float q[8];
       unpack8(packed, q);
       uint32_t b = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) b |= (q[j] > 0.f ? 1u : 0u) << j;
-      mask[i] = (uint8_t)b;
+      mask[k] = (uint8_t)b;
     }
     if (amax_out) {
       float q[8];
@@ -304,8 +317,9 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
         uint2 o;
         o.x = e4m3x4(q[0], q[1], q[2], q[3]);
         o.y = e4m3x4(q[4], q[5], q[6], q[7]);
-        ((uint2*)y8)[i] = o;
+        ((uint2*)y8)[k] = o;
       }
+    }
     }
   }
   if (amax_out) amax_publish(amax_out, vmax);
@@ -333,7 +347,7 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
   f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
-template <bool HOIST>
+template <bool HOIST, int U>
 __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
@@ -373,29 +387,44 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     }
   };
   if (HOIST) load_coef((int)(i % cvecs));
-  for (; i < nvec; i += stride) {
-    if (!HOIST) load_coef((int)(i % cvecs));
-    float g[8], vx[8];
-    unpack(((const uint4*)dy)[i], g);
-    unpack(((const uint4*)x)[i], vx);
-    if (relu == 1) {
-      float vy[8];
-      unpack(((const uint4*)y)[i], vy);
+  for (; i < nvec; i += U * stride) {
+    // U vectors per thread in flight: every load of the group is issued before any use
+    uint4 lg[U], lx[U], ly[U];
+    uint32_t lm[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = vy[j] > 0.f ? g[j] : 0.f;
-    } else if (relu == 2) {  // mask recomputed from x (no residual): one tensor read saved
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = vx[j] * Sc[j] + Sh[j] > 0.f ? g[j] : 0.f;
-    } else if (relu == 3) {  // bit mask from the forward apply (residual BN: y not re-read)
-      const uint32_t b = ((const uint8_t*)y)[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = (b >> j) & 1u ? g[j] : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const long k = i + u * stride < nvec ? i + u * stride : i;
+      lg[u] = ((const uint4*)dy)[k];
+      lx[u] = ((const uint4*)x)[k];
+      if (relu == 1) ly[u] = ((const uint4*)y)[k];
+      if (relu == 3) lm[u] = ((const uint8_t*)y)[k];
     }
-    if (dres) ((uint4*)dres)[i] = pack8(g);
-    float o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = A[j] * g[j] + Bc[j] * vx[j] + Cc[j];
-    ((uint4*)dx)[i] = pack8(o);
+    for (int u = 0; u < U; ++u) {
+      const long k = i + u * stride;
+      if (k >= nvec) break;
+      if (!HOIST) load_coef((int)(k % cvecs));
+      float g[8], vx[8];
+      unpack(lg[u], g);
+      unpack(lx[u], vx);
+      if (relu == 1) {
+        float vy[8];
+        unpack(ly[u], vy);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = vy[j] > 0.f ? g[j] : 0.f;
+      } else if (relu == 2) {  // mask recomputed from x (no residual): one tensor read saved
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = vx[j] * Sc[j] + Sh[j] > 0.f ? g[j] : 0.f;
+      } else if (relu == 3) {  // bit mask from the forward apply (residual BN: y not re-read)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = (lm[u] >> j) & 1u ? g[j] : 0.f;
+      }
+      if (dres) ((uint4*)dres)[k] = pack8(g);
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = A[j] * g[j] + Bc[j] * vx[j] + Cc[j];
+      ((uint4*)dx)[k] = pack8(o);
+    }
   }
 }
 
@@ -425,12 +454,13 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
   }
 }
 
-inline int ew_blocks(long n, int cvecs = 1) {
+inline int ew_blocks(long n, int cvecs = 1, int per_thread = 1) {
   // block count whose grid stride (blocks·NT vectors) is a multiple of the channel-vector count:
   // each thread's channel vector is then loop-invariant and the kernels hoist the per-channel
   // coefficients into registers (C = 728 or 1536 in Xception-41 are not powers of two)
-  long b = std::max<long>(1, (n + NT - 1) / NT);
-  b = std::min<long>(b, 2048);
+  static const long cap = env_int("TDL_BN_EW_BLOCKS", 1024);
+  long b = std::max<long>(1, (n + (long)NT * per_thread - 1) / ((long)NT * per_thread));
+  b = std::min<long>(b, cap);
   int g = NT, c = std::max(cvecs, 1);
   while (c) {  // gcd(NT, cvecs)
     const int t = g % c;
@@ -459,8 +489,10 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
                      float* scale_out, float* amax_out, float* amax_zero, uint8_t* mask) {
   const long n = M * C;
   if (C % 8 == 0) {
-    hipLaunchKernelGGL(apply_vec_kernel, dim3(ew_blocks(n / 8, C / 8)), dim3(NT), 0, st, x, coef, res, y,
-                       n / 8, C, relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask);
+    static const int u = env_int("TDL_BN_APPLY_U", 1);
+    auto k = u == 2 ? apply_vec_kernel<2> : u == 4 ? apply_vec_kernel<4> : apply_vec_kernel<1>;
+    hipLaunchKernelGGL(k, dim3(ew_blocks(n / 8, C / 8, u)), dim3(NT), 0, st, x, coef, res, y, n / 8, C,
+                       relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask);
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
                        C, relu ? 1 : 0);
@@ -478,11 +510,14 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          hipStream_t st) {
   const long n = M * C;
   if (C % 8 == 0) {
-    const int blocks = ew_blocks(n / 8, C / 8);
+    static const int u = env_int("TDL_BN_BWD_U", 2);
+    const int blocks = ew_blocks(n / 8, C / 8, u);
     const bool hoist = ((long)blocks * NT) % (C / 8) == 0;
-    hipLaunchKernelGGL(hoist ? bwd_apply_vec_kernel<true> : bwd_apply_vec_kernel<false>, dim3(blocks),
-                       dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, n / 8, C,
-                       1.f / count, relu);
+    auto k = hoist ? (u == 2 ? bwd_apply_vec_kernel<true, 2> : u == 4 ? bwd_apply_vec_kernel<true, 4>
+                                                                     : bwd_apply_vec_kernel<true, 1>)
+                   : bwd_apply_vec_kernel<false, 1>;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
+                       dbeta, n / 8, C, 1.f / count, relu);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu);

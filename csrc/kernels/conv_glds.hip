@@ -381,11 +381,27 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }
     } else {
       const rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)a.Ng * 4u : 0u);
+      const rsrc_t rmask = make_rsrc(a.mask, a.mask ? a.out_bytes / 16u : 0u);
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm) {
         const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
         const bool mv = m < T.Mc;
         const long orow = mv ? out_row<MODE>(a, T, m) : 0;
+        // DGRAD ReLU mask (pre-masked join): this row's TN mask bits of the wave's columns in
+        // one 4- / 8-byte load (ldc % 64 == 0: byte-aligned slab), reused by every rn fragment
+        uint64_t mrow = ~0ull;
+        if constexpr (MODE == DGRAD) {
+          if (a.mask) {
+            const uint32_t boff = (uint32_t)((orow * a.ldc + T.bn0 + wn * TN) >> 3);
+            if constexpr (TN == 64) {
+              const v2u32 mv2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, mv ? boff : OOB, 0, 0);
+              mrow = (uint64_t)mv2[0] | ((uint64_t)mv2[1] << 32);
+            } else {
+              static_assert(TN == 32, "mask slab of 4 or 8 bytes");
+              mrow = __builtin_amdgcn_raw_buffer_load_b32(rmask, mv ? boff : OOB, 0, 0);
+            }
+          }
+        }
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
           const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
@@ -398,7 +414,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           bf16_t h[4];
           float v[4];
           float prev[4] = {0.f, 0.f, 0.f, 0.f};
+          uint32_t mbits = 0xFu;
           if constexpr (MODE == DGRAD) {
+            if (a.mask) mbits = (uint32_t)(mrow >> (rn * 16 + (lane >> 4) * 4)) & 0xFu;
             if (a.beta) {  // residual-gradient join: dx += this conv's dgrad
               const uint32_t poff = (uint32_t)(orow * a.ldc + n0) * 2u;
               const v2u32 pv = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv && n0 < a.Ng) ? poff : OOB, 0, 0);
@@ -411,6 +429,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float t = acc[rm][rn][i] * out_scale + bv[i] + prev[i];
+            if (!((mbits >> i) & 1u)) t = 0.f;
             if (a.relu) t = fmaxf(t, 0.f);
             h[i] = f2bf(t);
             v[i] = bf2f(h[i]);

@@ -46,6 +46,9 @@ struct ConvArgs {
   const float* scale_x;  // fp8 FWD: per-tensor scales of x and w (device scalars)
   const float* scale_w;
   int beta;          // DGRAD: 1 = accumulate into the existing dx (residual-gradient join)
+  const uint8_t* mask;  // DGRAD: optional ReLU bit mask of dx (1 bit per element, NHWC order):
+                        // dx = ([dx +] dgrad)·[bit] — the consumers of a block output apply the
+                        // mask of its ReLU, so the producer BN's backward reads no mask
   uint32_t x_bytes, w_bytes, dy_bytes, out_bytes;  // buffer-descriptor ranges (OOB -> 0 / dropped)
   int kps;           // WGRAD: K-steps per split
   int splits;        // WGRAD: number of K splits

@@ -20,6 +20,7 @@ import torch
 
 from .common import on_gpu, ext, deliver_grad, grad_target, flat_view
 from . import workspace
+from . import gradjoin
 
 
 # ----------------------------------------------------------------------------------------------
@@ -153,7 +154,7 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
 
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training, res_join):
+    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training, res_join, need_grad):
         C = x.shape[-1]
         count = x.numel() // C
         if training:
@@ -167,9 +168,12 @@ class _BatchNormActFn(torch.autograd.Function):
         # nothing saved); with one, the forward writes it as 1 bit per element (mode 3: the two
         # backward kernels read 1/16 of y's bytes instead of y itself)
         mask = None
-        if relu and residual is not None and training and on_gpu(x) and C % 8 == 0 and C <= 2048:
+        if relu and residual is not None and need_grad and on_gpu(x) and C % 8 == 0 and C <= 2048:
             mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8)
         y = bn_apply(x, coef, residual, relu, fp8, mask)
+        ctx.mask_token = None
+        if mask is not None:  # the consumers' dgrads may apply it for us (ops/gradjoin.py)
+            ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask)
         ctx.count = count
         ctx.bn = bn
         ctx.training = training
@@ -187,10 +191,11 @@ class _BatchNormActFn(torch.autograd.Function):
         relu = ctx.relu
         C = x.shape[-1]  # physical channels (≥ beta.numel() when channel-padded)
         c = beta.numel()
+        premasked = ctx.mask_token is not None and ctx.mask_token.is_premasked(dy)
         if not ctx.training:
-            # eval-mode backward (rare): treat statistics as constants
+            # eval-mode backward (frozen BN): treat statistics as constants
             g = dy.float().reshape(-1, C)
-            if relu:
+            if relu and not premasked:
                 g = g * _relu_mask(relu, y, x, coef, C)
             dx = (g * coef[0]).reshape(x.shape).to(x.dtype)
             xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
@@ -198,8 +203,14 @@ class _BatchNormActFn(torch.autograd.Function):
                 deliver_grad(gamma, (g * xhat).sum(0)[:c])
             if beta.requires_grad:
                 deliver_grad(beta, g.sum(0)[:c])
-            dres = g.reshape(dy.shape).to(dy.dtype) if ctx.has_res else None
-            return dx, None, None, None, _join_res(ctx, dres), None, None, None, None
+            dres = None
+            if ctx.has_res:
+                dres = dy if premasked else g.reshape(dy.shape).to(dy.dtype)
+            return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None
+        # pre-masked: the block output's consumers already applied this ReLU's mask to dy
+        # (ops/gradjoin.py) — no mask reads, and dy itself is the residual gradient
+        if premasked:
+            relu, y = 0, None
         red = bn_bwd_reduce(dy, y, x, coef, relu)
         want_g = gamma is not None and gamma.requires_grad
         want_b = beta.requires_grad
@@ -208,13 +219,16 @@ class _BatchNormActFn(torch.autograd.Function):
         direct_g = on_gpu(dy) and gt is not None and gfresh
         direct_b = on_gpu(dy) and bt is not None and bfresh
         gp, _ = _phys_params(ctx.bn, gamma, beta)
-        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, ctx.count, relu, ctx.has_res,
+        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, ctx.count, relu,
+                                ctx.has_res and not premasked,
                                 gt if direct_g else None, bt if direct_b else None)
+        if premasked and ctx.has_res:
+            dres = dy
         if want_g:
             deliver_grad(gamma, None if direct_g else red[1][:c], written=direct_g)
         if want_b:
             deliver_grad(beta, None if direct_b else red[0][:c], written=direct_b)
-        return dx, None, None, None, _join_res(ctx, dres), None, None, None, None
+        return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None
 
 
 def _phys_params(bn, gamma, beta):
@@ -243,6 +257,7 @@ def _join_res(ctx, dres):
         join.buf = dres
     else:  # another consumer ran first (not the usual order): plain add
         join.buf.add_(dres)
+    join.note(False)  # not masked (a later full-coverage masking dgrad re-masks everything)
     return join.take()
 
 
@@ -250,5 +265,8 @@ def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True, r
     """act(BN(x) [+ residual]).  ``bn`` is a :class:`models.layers.BatchNorm` (holds γ, β and the
     moving statistics).  ``stats`` may carry Σx, Σx² already accumulated by the producer conv.
     ``res_join`` shares the residual's gradient buffer with its other consumers."""
+    # (grad mode is off inside Function.forward: decide here whether a backward will follow)
+    need_grad = torch.is_grad_enabled() and (
+        x.requires_grad or (residual is not None and residual.requires_grad))
     return _BatchNormActFn.apply(x, stats, bn.gamma, bn.beta, residual, bn, relu, training,
-                                 res_join)
+                                 res_join, need_grad)

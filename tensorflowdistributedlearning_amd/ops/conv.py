@@ -137,24 +137,50 @@ def conv_fwd_fp8(x8, sx, w8, sw, geom: ConvGeom, relu=False, stats=None):
     return y
 
 
-def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumulate=False):
+def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumulate=False,
+               mask=None):
     """dx.  With ``out`` the result is written there (``accumulate``: dx += …, fused in the GEMM
-    epilogue — used by the residual-gradient join, ops/gradjoin.py)."""
+    epilogue — used by the residual-gradient join, ops/gradjoin.py).  ``mask`` (uint8, 1 bit per
+    element of dx, GPU): dx = ([dx +] dgrad)·[bit] for the elements this dgrad writes."""
     if on_gpu(dy):
         dx = out if out is not None else torch.empty(x_shape, device=dy.device,
                                                      dtype=out_dtype or dy.dtype)
         ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
                          geom.padding[2], geom.dilation[0], geom.dilation[1],
-                         bool(accumulate and out is not None))
+                         bool(accumulate and out is not None), mask)
         return dx
     r = ref_conv_dgrad(dy, w, x_shape, geom)
+    if mask is not None:
+        from .bn import unpack_relu_mask
+        keep = unpack_relu_mask(mask, r.shape[-1]).reshape(r.shape)
+        if accumulate and out is not None:  # pixels this dgrad does not write keep their value
+            keep = keep | ~_dgrad_touched(w.shape, x_shape, geom)
+        r = r + out.float() if accumulate and out is not None else r
+        r = r * keep
+    elif accumulate and out is not None:
+        r = out.float() + r
     if out is None:
         return r.to(out_dtype or dy.dtype)
-    if accumulate:
-        out.copy_((out.float() + r).to(out.dtype))
-    else:
-        out.copy_(r.to(out.dtype))
+    out.copy_(r.to(out.dtype))
     return out
+
+
+def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
+    """[N, H, W, 1] bool: input pixels the dgrad writes (a strided conv with taps of fewer than
+    ``stride`` rows / columns leaves whole parity classes untouched)."""
+    K, R, S, C = w_shape
+    N, H, W, _ = x_shape
+    Ho, Wo = geom.out_hw(H, W, R, S)
+    cover = ref_conv_dgrad(torch.ones(1, Ho, Wo, 1), torch.ones(1, R, S, 1), (1, H, W, 1), geom)
+    return cover > 0
+
+
+def dgrad_covers_input(geom: ConvGeom, R, S):
+    """Does the dgrad of this conv write every input pixel (no empty stride parity class)?"""
+    (sh, sw), (dh, dw) = geom.stride, geom.dilation
+    if (sh, sw) == (1, 1):
+        return True
+    return dh == 1 and dw == 1 and R >= sh and S >= sw
 
 
 def conv_wgrad(dy, x, w_shape, geom: ConvGeom, out=None, accumulate=False, bias_grad=None):
@@ -244,10 +270,14 @@ class _Conv2dFn(torch.autograd.Function):
             if join is None:
                 dx = conv_dgrad(dy, w, ctx.x_shape, geom)
             else:  # residual-gradient join: first consumer writes, later ones accumulate
+                # pre-masked join (ops/gradjoin.py); the epilogue reads 64-channel mask slabs
+                mask = join.mask if on_gpu(dy) and ctx.x_shape[-1] % 64 == 0 else None
                 if join.buf is None:
-                    join.buf = conv_dgrad(dy, w, ctx.x_shape, geom)
+                    join.buf = conv_dgrad(dy, w, ctx.x_shape, geom, mask=mask)
+                    join.note(mask is not None)
                 else:
-                    conv_dgrad(dy, w, ctx.x_shape, geom, out=join.buf, accumulate=True)
+                    conv_dgrad(dy, w, ctx.x_shape, geom, out=join.buf, accumulate=True, mask=mask)
+                    join.note(mask is not None, dgrad_covers_input(geom, w.shape[1], w.shape[2]))
                 dx = join.take()
         if side is None:
             _conv_param_grads(ctx, dy, x, weight, bias)

@@ -11,28 +11,77 @@ autograd — the others return ``None`` (zero) for ``x``.
 
 Order independence: whichever consumer's backward runs first creates the buffer; correctness
 only needs every consumer to run, which holds inside a block (all branches reach the loss).
+
+Pre-masked joins: when ``x`` is the output of a residual BN + ReLU (the previous block's
+``relu(bn3(y) + shortcut)``), that BN's backward needs g = dx·[x > 0].  The forward attached a
+:class:`MaskToken` (the 1-bit ReLU mask) to ``x``; the join's dgrad consumers apply the mask in
+their epilogue (dx = ([dx +] dgrad)·[bit], exact: masking is linear in the contributions), and if
+the finished buffer is masked everywhere the token records it — the BN backward then reads no
+mask and returns the incoming gradient itself as the residual gradient instead of writing a copy
+(ResNet-50 b256: one full activation write and the mask reads of 16 residual BN backwards).
+Anything that breaks the protocol (an unmasked contribution last, autograd summing another
+gradient into the buffer) leaves the token unset, and the BN applies the mask itself as before.
 """
 from __future__ import annotations
+
+import os
 
 ENABLED = True
 
 
-class GradJoin:
-    __slots__ = ("n", "count", "buf")
+MASK_ENABLED = os.environ.get("TDL_PREMASK", "1") == "1"  # 0: the BN applies its mask
 
-    def __init__(self, n):
+
+class MaskToken:
+    """The ReLU bit mask of a residual BN output, and (after backward) which gradient buffer the
+    consumers handed back already masked: ``(data_ptr, version)`` of that tensor."""
+    __slots__ = ("mask", "premasked")
+
+    def __init__(self, mask):
+        self.mask = mask
+        self.premasked = None
+
+    def is_premasked(self, g):
+        return self.premasked is not None and self.premasked == (g.data_ptr(), g._version)
+
+
+class GradJoin:
+    __slots__ = ("n", "count", "buf", "mask_token", "unmasked")
+
+    def __init__(self, n, mask_token=None):
         self.n = n
         self.count = 0
         self.buf = None
+        self.mask_token = mask_token
+        self.unmasked = False  # some element of buf holds a contribution not yet masked
+
+    @property
+    def mask(self):
+        """The ReLU bit mask the dgrad consumers apply in their epilogue (None: no masking)."""
+        return self.mask_token.mask if self.mask_token is not None else None
+
+    def note(self, masked, full=True):
+        """Record a contribution: ``masked`` — written through the mask epilogue; ``full`` — it
+        rewrote every element (a strided dgrad leaves some pixels untouched)."""
+        if not masked:
+            self.unmasked = True
+        elif full:
+            self.unmasked = False
 
     def take(self):
         """Register one consumer's contribution; returns the buffer for the last one, else None."""
         self.count += 1
-        return self.buf if self.count == self.n else None
+        if self.count != self.n:
+            return None
+        if self.mask_token is not None and not self.unmasked and self.buf is not None:
+            self.mask_token.premasked = (self.buf.data_ptr(), self.buf._version)
+        return self.buf
 
 
 def make(n, x):
-    """A join for ``n`` consumers of ``x`` when enabled and ``x`` needs a gradient."""
+    """A join for ``n`` consumers of ``x`` when enabled and ``x`` needs a gradient (pre-masked
+    when ``x`` carries the ReLU mask token of a residual BN)."""
     if ENABLED and x.requires_grad:
-        return GradJoin(n)
+        tok = getattr(x, "_tdl_mask_token", None) if MASK_ENABLED else None
+        return GradJoin(n, tok)
     return None

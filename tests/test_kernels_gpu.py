@@ -378,6 +378,42 @@ def test_conv_dgrad_accumulate(gpu, conv_impl, shape):
     assert rel_err(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("shape", [(4, 14, 14, 256, 64, 1, 1, 1, (0, 0, 0, 0), 1),
+                                   (4, 15, 15, 128, 256, 1, 1, 2, (0, 0, 0, 0), 1),
+                                   (8, 28, 28, 128, 128, 3, 3, 2, (1, 1, 1, 1), 1),
+                                   (64, 28, 28, 128, 128, 1, 1, 1, (0, 0, 0, 0), 1)])
+def test_conv_dgrad_relu_mask(gpu, conv_impl, shape, accumulate):
+    """Pre-masked join (ops/gradjoin.py): the dgrad epilogue multiplies what it writes by a
+    1-bit-per-element ReLU mask, dx = ([dx +] dgrad)·[bit]; pixels a strided dgrad does not
+    touch keep their previous value (accumulate) or are zero (overwrite) — vs the CPU oracle."""
+    from tensorflowdistributedlearning_amd.ops import bn as BN
+    N, H, W, Cin, K, R, S, st, pad, dil = shape
+    g = C.ConvGeom((st, st), pad, (dil, dil))
+    torch.manual_seed(9)
+    w = (torch.randn(K, R, S, Cin) / math.sqrt(R * S * Cin)).bfloat16()
+    Ho, Wo = g.out_hw(H, W, R, S)
+    dy = torch.randn(N, Ho, Wo, K).bfloat16()
+    prev = torch.randn(N, H, W, Cin).bfloat16()
+    keep = torch.rand(N, H, W, Cin) > 0.4
+    bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)
+    mask = bits.sum(1).to(torch.uint8)
+    assert torch.equal(BN.unpack_relu_mask(mask, Cin).reshape(keep.shape), keep)
+    ref = C.ref_conv_dgrad(dy.float(), w.float(), (N, H, W, Cin), g)
+    if accumulate:
+        ref = ref + prev.float()
+        keep = keep | ~C._dgrad_touched(w.shape, (N, H, W, Cin), g)  # untouched: prev kept
+    ref = ref * keep
+    cpu = C.conv_dgrad(dy.float(), w.float(), (N, H, W, Cin), g, mask=mask,
+                       out=prev.float().clone() if accumulate else None, accumulate=accumulate)
+    assert rel_err(cpu, ref) < 1e-5
+    out = prev.to(gpu) if accumulate else None
+    dx = C.conv_dgrad(dy.to(gpu), w.to(gpu), (N, H, W, Cin), g, out=out, accumulate=accumulate,
+                      mask=mask.to(gpu))
+    assert rel_err(dx, ref) < 2e-2
+    assert (dx.float().cpu()[~keep] == 0).all()  # masked elements exactly zero
+
+
 def test_fp8_quantize_matches_cpu(gpu):
     from tensorflowdistributedlearning_amd.ops import fp8 as F8
     torch.manual_seed(12)

@@ -131,6 +131,52 @@ def test_residual_join_gpu_matches_plain_autograd(gpu):
     assert cos > 0.999, cos
 
 
+@pytest.mark.parametrize("depth", [18, 50])
+def test_premasked_join_matches_bn_masking(gpu, depth, monkeypatch):
+    """The block output's ReLU mask applied by the next block's dgrad epilogues (pre-masked join,
+    ops/gradjoin.py) vs the residual BN applying it: same gradients, and the pre-masked path is
+    taken for every residual BN that feeds another block.  Frozen BN (moving statistics, as in
+    test_residual_join_gpu_matches_plain_autograd): with batch statistics a tiny random net
+    turns fp32 atomic-order noise into O(1) gradient differences run to run; the exact epilogue
+    semantics are pinned by test_kernels_gpu.py::test_conv_dgrad_relu_mask."""
+    from tensorflowdistributedlearning_amd.ops import gradjoin
+    torch.manual_seed(7)
+    m = models.build(f"resnet{depth}", num_classes=10).to(gpu)
+    m.train()
+    for mod in m.modules():  # BN in eval mode inside a training-mode forward
+        if mod.__class__.__name__ == "BatchNorm":
+            mod.train(False)
+    x = torch.randn(8, 64, 64, 8, device=gpu, dtype=torch.bfloat16)
+    hits = []
+    orig = gradjoin.MaskToken.is_premasked
+
+    def spy(self, g):
+        r = orig(self, g)
+        hits.append(r)
+        return r
+
+    monkeypatch.setattr(gradjoin.MaskToken, "is_premasked", spy)
+    nblocks = sum(1 for mod in m.modules()
+                  if mod.__class__.__name__ in ("Bottleneck", "BasicBlock"))
+    outs = []
+    for enabled in (False, True):
+        gradjoin.MASK_ENABLED = enabled
+        try:
+            hits.clear()
+            for p in m.parameters():
+                p.grad = None
+            xi = x.clone().requires_grad_(True)
+            y = m(xi)
+            (y.float() * torch.linspace(-1, 1, 10, device=gpu)).sum().backward()
+            outs.append(torch.cat([p.grad.float().flatten() for p in m.parameters()
+                                   if p.grad is not None] + [xi.grad.float().flatten()]))
+            assert sum(hits) == (nblocks - 1 if enabled else 0), hits
+        finally:
+            gradjoin.MASK_ENABLED = True
+    cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=0).item()
+    assert cos > 0.9999, cos
+
+
 @pytest.mark.parametrize("fuse_bn", [False, True])
 def test_resnet_fp8_forward_trains(gpu, fuse_bn):
     """fp8 (e4m3) forward GEMMs, bf16 backward: loss finite and falling on a fixed batch
