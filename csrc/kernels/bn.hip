@@ -169,9 +169,9 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     // ≈ one or two workgroups per CU, ≥ 16 rows per thread: few atomics per output address
     // (every workgroup adds one row of 2C partial sums)
     const int cvecs = C / 8, rpp = NT / cvecs;
-    static const int cap = env_int("TDL_BN_RED_BLOCKS", 512);
+    static const int cap = env_int("TDL_BN_RED_BLOCKS", 1024);
     static const int u = env_int("TDL_BN_RED_U", 4);
-    static const int minr = env_int("TDL_BN_RED_MINR", 16);
+    static const int minr = env_int("TDL_BN_RED_MINR", 8);
     long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * minr)));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;

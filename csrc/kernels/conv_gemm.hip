@@ -337,35 +337,69 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       const bool fast = ((a.Ng & 3) == 0) && ((a.ldc & 3) == 0);
       const rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)a.Ng * 4u : 0u);
       const rsrc_t rmask = make_rsrc(a.mask, a.mask ? a.out_bytes / 16u : 0u);
+      // Phase 1 (fast layout): every epilogue load — bias, the DGRAD join's previous dx, the
+      // ReLU mask — is issued before any is used (one memory round trip per tile instead of a
+      // vmcnt(0) drain per fragment; see conv_glds.hip)
+      long orows[RM];
+      bool mvs[RM];
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm) {
         const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-        const bool mv = m < T.Mc;
-        const long orow = mv ? out_row<MODE>(a, T, m) : 0;
-        // DGRAD ReLU mask (pre-masked join): this row's TN mask bits of the wave's columns in
-        // one 4- / 8-byte load (ldc % 64 == 0: byte-aligned slab), reused by every rn fragment
-        uint64_t mrow = ~0ull;
+        mvs[rm] = m < T.Mc;
+        orows[rm] = mvs[rm] ? out_row<MODE>(a, T, m) : 0;
+      }
+      v4u32 bias_v[RN];
+      if constexpr (BIAS) {
+        if (fast) {
+#pragma unroll
+          for (int rn = 0; rn < RN; ++rn) {
+            const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+            bias_v[rn] = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
+          }
+        }
+      }
+      uint64_t mrows[RM];
+      v2u32 pvs[RM][RN];
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) {
+        mrows[rm] = ~0ull;
         if constexpr (MODE == DGRAD) {
+          // DGRAD ReLU mask (pre-masked join): a row's TN mask bits of the wave's columns in one
+          // 4- / 8-byte load (ldc % 64 == 0: byte-aligned slab), reused by every rn fragment
           if (a.mask) {
-            const uint32_t boff = (uint32_t)((orow * a.ldc + T.bn0 + wn * TN) >> 3);
+            const uint32_t boff = (uint32_t)((orows[rm] * a.ldc + T.bn0 + wn * TN) >> 3);
             if constexpr (TN == 64) {
-              const v2u32 mv2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, mv ? boff : OOB, 0, 0);
-              mrow = (uint64_t)mv2[0] | ((uint64_t)mv2[1] << 32);
+              const v2u32 mv2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, mvs[rm] ? boff : OOB, 0, 0);
+              mrows[rm] = (uint64_t)mv2[0] | ((uint64_t)mv2[1] << 32);
             } else {
               static_assert(TN == 32, "mask slab of 4 or 8 bytes");
-              mrow = __builtin_amdgcn_raw_buffer_load_b32(rmask, mv ? boff : OOB, 0, 0);
+              mrows[rm] = __builtin_amdgcn_raw_buffer_load_b32(rmask, mvs[rm] ? boff : OOB, 0, 0);
+            }
+          }
+          if (a.beta && fast) {  // residual-gradient join: dx += this conv's dgrad
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn) {
+              const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+              const uint32_t poff = (uint32_t)(orows[rm] * a.ldc + n0) * 2u;
+              pvs[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(rout, (mvs[rm] && n0 < a.Ng) ? poff : OOB, 0, 0);
             }
           }
         }
+      }
+      // Phase 2: combine and store
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) {
+        const bool mv = mvs[rm];
+        const long orow = orows[rm];
+        const uint64_t mrow = mrows[rm];
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
           const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
           float bv[4] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (BIAS) {
             if (fast) {
-              const v4u32 b = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(b[i]);
+              for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(bias_v[rn][i]);
             } else {
 #pragma unroll
               for (int i = 0; i < 4; ++i) bv[i] = (n0 + i < a.Ng) ? a.bias[n0 + i] : 0.f;
@@ -379,8 +413,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
             if (a.mask) mbits = (uint32_t)(mrow >> (rn * 16 + (lane >> 4) * 4)) & 0xFu;
             if (a.beta) {  // residual-gradient join: dx += this conv's dgrad
               if (fast) {
-                const uint32_t poff = (uint32_t)(orow * a.ldc + n0) * 2u;
-                const v2u32 pv = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv && n0 < a.Ng) ? poff : OOB, 0, 0);
+                const v2u32 pv = pvs[rm][rn];
                 prev[0] = __uint_as_float(pv[0] << 16);
                 prev[1] = __uint_as_float(pv[0] & 0xffff0000u);
                 prev[2] = __uint_as_float(pv[1] << 16);

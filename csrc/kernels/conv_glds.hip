@@ -340,6 +340,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     }
   };
   const bool no_mfma = a.dbg & 2;
+  const bool no_epi_mem = a.dbg & 128;  // timing-only: epilogue issues no global loads / stores
   auto mfmas = [&](const bf16x8(&af)[RM], const bf16x8(&bfg)[RN]) {
     if (no_mfma) {
 #pragma unroll
@@ -382,48 +383,77 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     } else {
       const rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)a.Ng * 4u : 0u);
       const rsrc_t rmask = make_rsrc(a.mask, a.mask ? a.out_bytes / 16u : 0u);
+      // Phase 1: every load the epilogue needs (bias, the DGRAD join's previous dx, the ReLU
+      // mask) is issued before any is used — one memory round trip per tile.  Interleaved
+      // load → use per fragment made hipcc wait vmcnt(0) RM·RN times per tile, draining the
+      // next tile's in-flight operand DMA each time (the accumulating join dgrads ran 2-3x slower
+      // than the same GEMM without them).
+      long orow[RM];
+      bool mv[RM];
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm) {
         const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-        const bool mv = m < T.Mc;
-        const long orow = mv ? out_row<MODE>(a, T, m) : 0;
-        // DGRAD ReLU mask (pre-masked join): this row's TN mask bits of the wave's columns in
-        // one 4- / 8-byte load (ldc % 64 == 0: byte-aligned slab), reused by every rn fragment
-        uint64_t mrow = ~0ull;
+        mv[rm] = m < T.Mc;
+        orow[rm] = mv[rm] ? out_row<MODE>(a, T, m) : 0;
+      }
+      v4u32 bias_v[RN];
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn) {
+          const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+          bias_v[rn] = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
+        }
+      }
+      // DGRAD ReLU mask (pre-masked join): a row's TN mask bits of the wave's columns in one 4- /
+      // 8-byte load (ldc % 64 == 0: byte-aligned slab), reused by every rn fragment
+      uint64_t mrow[RM];
+      v2u32 pv[RM][RN];
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) {
+        mrow[rm] = ~0ull;
         if constexpr (MODE == DGRAD) {
-          if (a.mask) {
-            const uint32_t boff = (uint32_t)((orow * a.ldc + T.bn0 + wn * TN) >> 3);
+          if (a.mask && !no_epi_mem) {
+            const uint32_t boff = (uint32_t)((orow[rm] * a.ldc + T.bn0 + wn * TN) >> 3);
             if constexpr (TN == 64) {
-              const v2u32 mv2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, mv ? boff : OOB, 0, 0);
-              mrow = (uint64_t)mv2[0] | ((uint64_t)mv2[1] << 32);
+              const v2u32 mv2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, mv[rm] ? boff : OOB, 0, 0);
+              mrow[rm] = (uint64_t)mv2[0] | ((uint64_t)mv2[1] << 32);
             } else {
               static_assert(TN == 32, "mask slab of 4 or 8 bytes");
-              mrow = __builtin_amdgcn_raw_buffer_load_b32(rmask, mv ? boff : OOB, 0, 0);
+              mrow[rm] = __builtin_amdgcn_raw_buffer_load_b32(rmask, mv[rm] ? boff : OOB, 0, 0);
+            }
+          }
+          if (a.beta && !no_epi_mem) {  // residual-gradient join: dx += this conv's dgrad
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn) {
+              const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+              const uint32_t poff = (uint32_t)(orow[rm] * a.ldc + n0) * 2u;
+              pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv[rm] && n0 < a.Ng) ? poff : OOB, 0, 0);
             }
           }
         }
+      }
+      // Phase 2: combine and store
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) {
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
           const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
           float bv[4] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (BIAS) {
-            const v4u32 b = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(b[i]);
+            for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(bias_v[rn][i]);
           }
           bf16_t h[4];
           float v[4];
           float prev[4] = {0.f, 0.f, 0.f, 0.f};
           uint32_t mbits = 0xFu;
           if constexpr (MODE == DGRAD) {
-            if (a.mask) mbits = (uint32_t)(mrow >> (rn * 16 + (lane >> 4) * 4)) & 0xFu;
-            if (a.beta) {  // residual-gradient join: dx += this conv's dgrad
-              const uint32_t poff = (uint32_t)(orow * a.ldc + n0) * 2u;
-              const v2u32 pv = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv && n0 < a.Ng) ? poff : OOB, 0, 0);
-              prev[0] = __uint_as_float(pv[0] << 16);
-              prev[1] = __uint_as_float(pv[0] & 0xffff0000u);
-              prev[2] = __uint_as_float(pv[1] << 16);
-              prev[3] = __uint_as_float(pv[1] & 0xffff0000u);
+            if (a.mask) mbits = (uint32_t)(mrow[rm] >> (rn * 16 + (lane >> 4) * 4)) & 0xFu;
+            if (a.beta && !no_epi_mem) {
+              prev[0] = __uint_as_float(pv[rm][rn][0] << 16);
+              prev[1] = __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
+              prev[2] = __uint_as_float(pv[rm][rn][1] << 16);
+              prev[3] = __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
             }
           }
 #pragma unroll
@@ -434,12 +464,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
             h[i] = f2bf(t);
             v[i] = bf2f(h[i]);
           }
-          const bool v_ok = mv && n0 < a.Ng;
-          const uint32_t off = (uint32_t)(orow * a.ldc + n0) * 2u;
+          const bool v_ok = mv[rm] && n0 < a.Ng;
+          const uint32_t off = (uint32_t)(orow[rm] * a.ldc + n0) * 2u;
           v2u32 pk;
           pk[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
           pk[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-          __builtin_amdgcn_raw_buffer_store_b64(pk, rout, v_ok ? off : OOB, 0, 0);
+          if (!no_epi_mem) __builtin_amdgcn_raw_buffer_store_b64(pk, rout, v_ok ? off : OOB, 0, 0);
           if constexpr (STATS) {
             const float msk = v_ok ? 1.f : 0.f;
 #pragma unroll
@@ -675,6 +705,7 @@ struct GCfg {
 constexpr GCfg G256x128{256, 128, 4, 2, 3};
 constexpr GCfg G256x64{256, 64, 4, 1, 3};
 constexpr GCfg G128x128{128, 128, 2, 2, 4};
+constexpr GCfg G128x128s2{128, 128, 2, 2, 2};  // 66 KB LDS: two workgroups per CU
 
 constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
   return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
@@ -699,11 +730,15 @@ void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
     launch_g<MODE, 256, 128, 4, 2, 3, STATS, BIAS, FK>(a, blocks, st);
   else if (cfg == 1)
     launch_g<MODE, 256, 64, 4, 1, 3, STATS, BIAS, FK>(a, blocks, st);
-  else
+  else if (cfg == 2)
     launch_g<MODE, 128, 128, 2, 2, 4, STATS, BIAS, FK>(a, blocks, st);
+  else
+    launch_g<MODE, 128, 128, 2, 2, 2, STATS, BIAS, FK>(a, blocks, st);
 }
 
-const GCfg& cfg_of(int c) { return c == 0 ? G256x128 : (c == 1 ? G256x64 : G128x128); }
+const GCfg& cfg_of(int c) {
+  return c == 0 ? G256x128 : (c == 1 ? G256x64 : (c == 2 ? G128x128 : G128x128s2));
+}
 
 void set_fastdivs(ConvArgs& a) {
   a.fd_sh = make_fastdiv((uint32_t)std::max(1, a.sh));
