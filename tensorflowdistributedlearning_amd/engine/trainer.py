@@ -164,8 +164,13 @@ class Trainer:
             step_count, global_step = self.optimizer.step_count, self.global_step
             _params.bump_version()  # derived weight copies (channel padding) refresh in-graph
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self.graph_out = self._step(self.static_x, self.static_y)
+            try:
+                with torch.cuda.graph(g):
+                    # wgrads fork onto the side stream inside the capture and are joined back
+                    # after backward (ops/streams.py), as in eager steps
+                    self.graph_out = self._step(self.static_x, self.static_y)
+            finally:
+                streams.end_capture()
         # capture records without executing: the host-side counters did not really advance
         self.optimizer.step_count, self.global_step = step_count, global_step
         self.graph = g

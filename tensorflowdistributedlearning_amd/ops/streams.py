@@ -6,7 +6,11 @@ runs concurrently with that chain, so the memory-bound BN kernels can overlap th
 wgrads.  Ordering: the side stream waits for the compute stream before each wgrad (dy ready);
 the compute stream joins the side stream before any gradient bucket is all-reduced
 (parallel/bucketer.py) and after backward (engine/trainer.py), so no collective or optimizer
-reads a gradient that is still being written.  Disabled during HIP-graph capture.
+reads a gradient that is still being written.
+
+Under HIP-graph capture the side stream is forked into the capture by that same event wait (a
+captured cross-stream dependency) and joined back before the capture ends, so a captured training
+step keeps the wgrad overlap (``TDL_WGRAD_IN_GRAPH=0``: wgrads on the capturing stream instead).
 
 Measured on one MI355X (bench.py, eager): ResNet-50 b256 9646 → 9925 img/s, Xception-41 b128
 2551 → 2650, reference DeepLab preset b64 4685 → 4814."""
@@ -17,6 +21,8 @@ import os
 import torch
 
 _ENABLED = os.environ.get("TDL_WGRAD_STREAM", "1") == "1"
+IN_GRAPH = os.environ.get("TDL_WGRAD_IN_GRAPH", "1") == "1"
+_FORKED: set = set()  # devices whose side stream joined the capture in progress
 # Record the side stream's wait on dy before the conv's dgrad is launched (the wgrad overlaps that
 # dgrad too); TDL_WGRAD_EARLY=0 records it after the dgrad launch (the previous ordering, for A/B).
 EARLY_WAIT = os.environ.get("TDL_WGRAD_EARLY", "1") == "1"
@@ -33,13 +39,24 @@ def set_enabled(flag: bool):
 
 
 def side(device):
-    """The side stream for ``device`` when enabled (and not capturing a graph), else None."""
-    if not _ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+    """The side stream for ``device`` when enabled, else None.  During a graph capture the
+    caller's ``side.wait_stream(current)`` forks it into the capture; :func:`join` merges it
+    back."""
+    if not _ENABLED or device.type != "cuda":
         return None
+    if torch.cuda.is_current_stream_capturing():
+        if not IN_GRAPH:
+            return None
+        _FORKED.add(torch.device(device))
     s = _SIDE.get(device)
     if s is None:
         s = _SIDE[device] = torch.cuda.Stream(device=device)
     return s
+
+
+def end_capture():
+    """Forget the capture's forked side streams (call once the capture has ended)."""
+    _FORKED.clear()
 
 
 _JOIN_QUEUED: dict = {}  # device -> autograd graph-task id whose final callback joins it
@@ -74,11 +91,12 @@ def join_at_backward_end(device):
 
 
 def join(device=None):
-    """Make the current stream wait for all work queued on the side stream(s).  A no-op while a
-    HIP graph is being captured: nothing is queued on the side stream then (``side`` returns
-    None), and a wait on an event of a non-captured stream must not enter the graph."""
-    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        return
+    """Make the current stream wait for all work queued on the side stream(s).  While a HIP graph
+    is being captured only side streams forked into that capture are joined (a wait on an event
+    of a stream outside the capture must not enter the graph)."""
+    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
     for dev, s in _SIDE.items():
         if device is None or dev == torch.device(device):
+            if capturing and dev not in _FORKED:
+                continue
             torch.cuda.current_stream(dev).wait_stream(s)

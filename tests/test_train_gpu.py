@@ -242,16 +242,15 @@ def test_graph_replay_matches_eager(gpu, opt):
     with tools/graph_debug.py: after the first replay only the stem BN γ gradient differs), so
     the updates are compared with a tolerance rather than bit for bit."""
     from tensorflowdistributedlearning_amd.ops import streams
-    # the captured step runs its wgrads on the compute stream (no side stream under capture); the
-    # eager twin does the same so that buffer placement — which moves PyTorch's reduction
-    # vectorisation, amplified by Adam's normalisation — matches (side vs serial eager is
-    # test_side_stream_wgrad_matches_serial)
+    # side=True: the captured step forks its wgrads onto the side stream inside the graph (as the
+    # eager twin does); side=False: both run their wgrads on the compute stream
     old = streams.enabled()
-    streams.set_enabled(False)
-    try:
-        _graph_replay_case(gpu, opt)
-    finally:
-        streams.set_enabled(old)
+    for side in (False, True):
+        streams.set_enabled(side)
+        try:
+            _graph_replay_case(gpu, opt)
+        finally:
+            streams.set_enabled(old)
 
 
 def _graph_replay_case(gpu, opt):
