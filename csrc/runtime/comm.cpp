@@ -98,6 +98,7 @@ Communicator::~Communicator() {
   for (auto& w : works_) hipEventDestroy(w.done);
   for (auto e : free_events_) hipEventDestroy(e);
   for (auto e : parked_events_) hipEventDestroy(e);
+  for (auto e : graph_events_) hipEventDestroy(e);
   if (ready_) hipEventDestroy(ready_);
 }
 
@@ -116,6 +117,26 @@ template <class F>
 uint64_t Communicator::enqueue(const char* name, hipStream_t producer, hipStream_t comm, F&& issue) {
   std::lock_guard<std::mutex> g(mu_);
   if (failed_ || !comm_) throw std::runtime_error("RCCL communicator failed: " + error_);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  check_hip(hipStreamIsCapturing(producer, &cap), "hipStreamIsCapturing");
+  if (cap == hipStreamCaptureStatusActive) {
+    // HIP-graph capture: fresh events (graph nodes reference them), comm stream forked into the
+    // capture by the wait, collective captured, completion event for the consumer's wait
+    hipEvent_t rdy, done;
+    check_hip(hipEventCreateWithFlags(&rdy, hipEventDisableTiming), "hipEventCreate");
+    graph_events_.push_back(rdy);
+    check_hip(hipEventCreateWithFlags(&done, hipEventDisableTiming), "hipEventCreate");
+    graph_events_.push_back(done);
+    check_hip(hipEventRecord(rdy, producer), "hipEventRecord (capture)");
+    check_hip(hipStreamWaitEvent(comm, rdy, 0), "hipStreamWaitEvent (capture)");
+    check_nccl(issue((ncclComm_t)comm_), name);
+    check_hip(hipEventRecord(done, comm), "hipEventRecord (capture)");
+    const uint64_t t = next_ticket_++;
+    graph_works_.emplace_back(t, done);
+    return t;
+  }
+  if (cap != hipStreamCaptureStatusNone)
+    throw std::runtime_error("RCCL collective on a stream whose capture was invalidated");
   if (producer != comm) {
     check_hip(hipEventRecord(ready_, producer), "hipEventRecord");
     check_hip(hipStreamWaitEvent(comm, ready_, 0), "hipStreamWaitEvent");
@@ -168,6 +189,12 @@ uint64_t Communicator::track(const char* name, hipStream_t comm) {
 
 void Communicator::wait(uint64_t ticket, hipStream_t consumer) {
   std::lock_guard<std::mutex> g(mu_);
+  for (auto& w : graph_works_) {
+    if (w.first == ticket) {
+      check_hip(hipStreamWaitEvent(consumer, w.second, 0), "hipStreamWaitEvent");
+      return;
+    }
+  }
   for (auto& w : works_) {
     if (w.ticket == ticket) {
       check_hip(hipStreamWaitEvent(consumer, w.done, 0), "hipStreamWaitEvent");

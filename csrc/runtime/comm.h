@@ -6,6 +6,8 @@
 //   * every collective is enqueued on the caller-supplied comm stream after an event recorded on
 //     the producer (compute) stream — no host synchronisation — and returns a ticket; wait(ticket,
 //     consumer) makes the consumer stream wait on the collective's completion event;
+//   * collectives enqueued while the producer stream is capturing a HIP graph are captured with
+//     it (event record / wait nodes fork the comm stream into the capture) and replay with it;
 //   * the watchdog polls outstanding collectives (hipEventQuery) and ncclCommGetAsyncError; a
 //     collective older than `timeout_s` or an async RCCL error aborts the communicator
 //     (ncclCommAbort) and latches an error string the Python side raises on (fail fast instead of
@@ -55,7 +57,8 @@ class Communicator {
   // RCCL operation in flight
   uint64_t track(const char* name, hipStream_t comm);
 
-  void wait(uint64_t ticket, hipStream_t consumer);  // stream-level, no host block
+  // stream-level, no host block (tickets of collectives captured into a HIP graph included)
+  void wait(uint64_t ticket, hipStream_t consumer);
   void synchronize();                                  // host waits for every outstanding collective
   std::string error() const;
   bool ok() const { return !failed_.load(); }
@@ -87,6 +90,11 @@ class Communicator {
   // progress, retired events are parked here instead of being recycled, so a handle it holds is
   // never re-recorded by a later collective (it would then also wait for that newer work)
   std::vector<hipEvent_t> parked_events_;
+  // collectives issued while the producer stream is being captured into a HIP graph: they run
+  // at every replay, so they are not watched as outstanding work (ncclCommGetAsyncError still
+  // is); their ordering events belong to the graph and live as long as the communicator
+  std::vector<std::pair<uint64_t, hipEvent_t>> graph_works_;
+  std::vector<hipEvent_t> graph_events_;
   int sync_pins_ = 0;
   uint64_t next_ticket_ = 1;
   std::atomic<bool> failed_{false};

@@ -139,12 +139,16 @@ class Trainer:
 
         The step must be host-synchronisation-free (it is: losses stay on the device) and its
         Python-side choices static across steps; the learning rate moves to a device scalar
-        (optimizer ``set_device_lr``).  Single-process only: the bucketed all-reduce stays eager.
+        (optimizer ``set_device_lr``).  Data parallel: with the native RCCL communicator
+        (``init_distributed(comm="rccl")``) the bucketed all-reduces are captured into the graph
+        too (csrc/runtime/comm.cpp forks its comm stream into the capture) and overlap backward
+        at every replay; ProcessGroupNCCL collectives stay eager-only.
         The fp8 delayed-scaling state rotates on the host, so fp8 models are not capturable."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs a GPU")
-        if self.bucketer is not None:
-            raise RuntimeError("graph capture is single-process (the bucketed all-reduce is eager)")
+        if self.bucketer is not None and getattr(self.ctx, "native", None) is None:
+            raise RuntimeError("data-parallel graph capture needs the native RCCL communicator "
+                               "(init_distributed(comm='rccl'))")
         if any(getattr(m, "fp8", False) or getattr(m, "emit_fp8", False)
                for m in self.model.modules()):
             raise RuntimeError("fp8 delayed scaling keeps host-side state: not capturable")
@@ -165,7 +169,10 @@ class Trainer:
             _params.bump_version()  # derived weight copies (channel padding) refresh in-graph
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g):
+                # thread_local: the native communicator's watchdog thread keeps polling its
+                # eager collectives' events during the capture (a global-mode capture would be
+                # invalidated by that)
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     # wgrads fork onto the side stream inside the capture and are joined back
                     # after backward (ops/streams.py), as in eager steps
                     self.graph_out = self._step(self.static_x, self.static_y)

@@ -192,8 +192,9 @@ class _BatchNormActFn(torch.autograd.Function):
         C = x.shape[-1]  # physical channels (≥ beta.numel() when channel-padded)
         c = beta.numel()
         premasked = ctx.mask_token is not None and ctx.mask_token.is_premasked(dy)
-        if not ctx.training:
-            # eval-mode backward (frozen BN): treat statistics as constants
+        if not ctx.training and not on_gpu(dy):
+            # eval-mode backward (frozen BN): treat statistics as constants.  On the GPU this is
+            # the training path's kernels with 1/count = 0 (no batch-statistics terms)
             g = dy.float().reshape(-1, C)
             if relu and not premasked:
                 g = g * _relu_mask(relu, y, x, coef, C)
@@ -219,7 +220,8 @@ class _BatchNormActFn(torch.autograd.Function):
         direct_g = on_gpu(dy) and gt is not None and gfresh
         direct_b = on_gpu(dy) and bt is not None and bfresh
         gp, _ = _phys_params(ctx.bn, gamma, beta)
-        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, ctx.count, relu,
+        count = ctx.count if ctx.training else float("inf")  # frozen BN: dx = γ·invstd·g
+        dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, count, relu,
                                 ctx.has_res and not premasked,
                                 gt if direct_g else None, bt if direct_b else None)
         if premasked and ctx.has_res:

@@ -23,6 +23,7 @@ import torch
 _ENABLED = os.environ.get("TDL_WGRAD_STREAM", "1") == "1"
 IN_GRAPH = os.environ.get("TDL_WGRAD_IN_GRAPH", "1") == "1"
 _FORKED: set = set()  # devices whose side stream joined the capture in progress
+_ORIGIN: dict = {}    # device -> the stream that last forked work onto the side stream
 # Record the side stream's wait on dy before the conv's dgrad is launched (the wgrad overlaps that
 # dgrad too); TDL_WGRAD_EARLY=0 records it after the dgrad launch (the previous ordering, for A/B).
 EARLY_WAIT = os.environ.get("TDL_WGRAD_EARLY", "1") == "1"
@@ -51,7 +52,21 @@ def side(device):
     s = _SIDE.get(device)
     if s is None:
         s = _SIDE[device] = torch.cuda.Stream(device=device)
+    cur = torch.cuda.current_stream(device)
+    if cur != s:
+        _ORIGIN[torch.device(device)] = cur
     return s
+
+
+def is_side(stream, device) -> bool:
+    """Is ``stream`` the side stream of ``device``?"""
+    s = _SIDE.get(torch.device(device))
+    return s is not None and stream == s
+
+
+def origin(device):
+    """The stream that forks work onto the side stream (the compute / capturing stream)."""
+    return _ORIGIN.get(torch.device(device), torch.cuda.current_stream(device))
 
 
 def end_capture():

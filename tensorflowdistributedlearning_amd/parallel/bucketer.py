@@ -126,7 +126,22 @@ class GradBucketer:
     def _launch(self, b):
         view = self.flat.grad[b.lo:b.hi]
         if view.is_cuda:
+            cur = torch.cuda.current_stream(view.device)
+            if streams.is_side(cur, view.device) and torch.cuda.is_current_stream_capturing():
+                # the hook fired inside a side-stream wgrad (ops/conv.py) during a HIP-graph
+                # capture: issue the collective from the capturing stream, joined to the side
+                # stream, so the comm stream forks off the capture's origin stream
+                org = streams.origin(view.device)
+                org.wait_stream(cur)
+                with torch.cuda.stream(org):
+                    self._issue(b, view)
+                b.launched = True
+                return
             streams.join(view.device)  # wgrads still running on the side stream (ops/streams.py)
+        self._issue(b, view)
+        b.launched = True
+
+    def _issue(self, b, view):
         if self.comm_hook is not None:
             b.work = self.comm_hook(b, view)
         elif self.ctx is not None and self.ctx.is_distributed:
@@ -134,7 +149,6 @@ class GradBucketer:
                 b.work = self.ctx.all_reduce_async(view)  # native RCCL (parallel/rccl.py)
             else:
                 b.work = dist.all_reduce(view, async_op=True, group=self.group)
-        b.launched = True
 
     def finish(self):
         """After backward: launch any bucket still pending (unused parameters — their grads were
