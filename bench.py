@@ -138,6 +138,10 @@ def main():
     ms = el / args.steps * 1e3
     value = per_gpu * n * args.steps / el
     if ctx.is_main:
+        if dev.type == "cuda":
+            print(f"[bench] peak device memory {torch.cuda.max_memory_allocated(dev) / 2**30:.1f} "
+                  f"GiB allocated, {torch.cuda.max_memory_reserved(dev) / 2**30:.1f} GiB reserved",
+                  file=sys.stderr, flush=True)
         if tr.timer is not None:
             ph = tr.timer.summary()
             print("[bench] phases ms/step (timed + warmup steps): " +

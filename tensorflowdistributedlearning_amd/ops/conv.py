@@ -286,8 +286,7 @@ class _Conv2dFn(torch.autograd.Function):
                 side.wait_stream(torch.cuda.current_stream(dy.device))
             with torch.cuda.stream(side):
                 _conv_param_grads(ctx, dy, x, weight, bias)
-            dy.record_stream(side)
-            x.record_stream(side)
+            streams.keep_alive(dy.device, dy, x)  # until the next join (no record_stream)
             streams.join_at_backward_end(dy.device)  # backward() returns joined
         return dx, None, None, None, None, None, None, None
 

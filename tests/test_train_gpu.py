@@ -357,7 +357,7 @@ def test_side_stream_wgrad_matches_serial(gpu, model):
     torch.cuda.synchronize()
     assert torch.isfinite(masters[0]).all()
     assert not torch.equal(masters[0], start)  # the steps really updated the parameters
-    torch.testing.assert_close(masters[1], masters[0], rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(masters[1], masters[0], rtol=1e-4, atol=1e-7)
 
 
 def test_plain_backward_joins_side_stream(gpu):
@@ -389,7 +389,7 @@ def test_plain_backward_joins_side_stream(gpu):
         streams.set_enabled(old)
     # equal up to the BN backward's fp32 atomic summation order; a read before the stalled side
     # stream finished would see stale gradients (tools/race_negative_control.py)
-    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.parametrize("early", [True, False])
