@@ -54,8 +54,9 @@ def main():
                     help="gradient all-reduce backend: torch.distributed ProcessGroupNCCL (RCCL) or "
                          "the native RCCL communicator with watchdog (parallel/rccl.py)")
     ap.add_argument("--fp8", action="store_true",
-                    help="fp8 (OCP e4m3, per-tensor scales) forward GEMMs on the CDNA4 "
-                         "16x16x128 MFMA for every eligible conv; backward stays bf16")
+                    help="fp8 GEMMs on the CDNA4 16x16x128 f8f6f4 MFMA for every eligible conv: "
+                         "forward e4m3 x e4m3, input gradient e5m2 x e4m3 (TDL_FP8_DGRAD=0: "
+                         "forward only); weight gradients stay bf16")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step as a HIP graph and replay it (removes "
                          "host launch overhead in launch-bound configs; with N>1 the bucketed "
@@ -101,7 +102,7 @@ def main():
         x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank)
         metric = METRIC if args.model == "resnet50" and args.image_size == 224 and not args.fp8 \
             else (f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} "
-                  f"{'fp8 (e4m3 fwd GEMMs, bf16 bwd)' if args.fp8 else 'bf16'}")
+                  f"{'fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad)' if args.fp8 else 'bf16'}")
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "sgd_momentum",
@@ -154,7 +155,7 @@ def main():
             "baseline": ("BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
                          "ResNet-50 number)" if args.model != "deeplab_ref" else
                          "BASELINE.md measured 90.7 img/s on 2 GPUs, scaled per GPU"),
-            "dtype": "fp8e4m3-fwd/bf16-bwd" if getattr(args, "fp8", False) else "bf16",
+            "dtype": "fp8 (e4m3 fwd / e5m2 dgrad, bf16 wgrad + BN)" if args.fp8 else "bf16",
             "data": "synthetic (device-resident random batch, random-init weights)",
             "config": cfg}), flush=True)
     shutdown()

@@ -172,6 +172,45 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
   conv_dgrad_launch(a, stream());
 }
 
+// fp8 dgrad: dy8 e5m2 [N,Ho,Wo,K], w8t e4m3 transposed weights [R,S,C,K] (ops/fp8.py), dx bf16
+// [N,H,W,C]; per-tensor scales sdy, sw (device scalars); join accumulate / ReLU mask as conv_dgrad
+void conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, int64_t sh, int64_t sw,
+                    int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate,
+                    c10::optional<Tensor> mask) {
+  TORCH_CHECK(dy8.is_cuda() && w8t.is_cuda() && dy8.element_size() == 1 && w8t.element_size() == 1,
+              "fp8 operands expected");
+  TORCH_CHECK(dy8.is_contiguous() && w8t.is_contiguous(), "contiguous operands expected");
+  CHECK_T(dx, torch::kBFloat16);
+  CHECK_T(sdy, torch::kFloat32);
+  CHECK_T(sw_, torch::kFloat32);
+  // logical weight shape K×R×S×C from the transposed copy R×S×C×K
+  const int64_t K = w8t.size(3), R = w8t.size(0), S = w8t.size(1), C = w8t.size(2);
+  TORCH_CHECK(dx.size(3) == C && dy8.size(3) == K && K % 128 == 0 && C % 8 == 0,
+              "fp8 dgrad shapes: K % 128 == 0, C % 8 == 0");
+  ConvArgs a = conv_args(dx, dx, dx.size(0), dx.size(1), dx.size(2), C, K, R, S, sh, sw, ph, pw, dh,
+                         dw, dy8.size(1), dy8.size(2));
+  a.dy = (const bf16_t*)dy8.data_ptr(); a.w = (const bf16_t*)w8t.data_ptr(); a.out = dx.data_ptr();
+  TORCH_CHECK(dy8.numel() < (1LL << 32) && w8t.numel() < (1LL << 32), "tensor too large");
+  a.dy_bytes = (uint32_t)dy8.numel(); a.w_bytes = (uint32_t)w8t.numel(); a.out_bytes = nbytes32(dx);
+  a.M = a.N * a.H * a.W; a.Ng = a.C; a.Kg = a.R * a.S * a.K; a.ldc = a.C; a.relu = 0;
+  a.beta = accumulate ? 1 : 0;
+  a.fp8 = 1;
+  a.scale_x = sdy.data_ptr<float>(); a.scale_w = sw_.data_ptr<float>();
+  a.mask = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == torch::kUInt8 && mask->is_contiguous() &&
+                mask->numel() * 8 == dx.numel() && dx.size(3) % 64 == 0,
+                "conv_dgrad mask: uint8 [numel(dx)/8], C % 64 == 0");
+    a.mask = (const uint8_t*)mask->data_ptr();
+  }
+  if (a.M == 0) return;
+  try {
+    conv_dgrad_launch(a, stream());
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, e.what());
+  }
+}
+
 void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad, int64_t sh,
                 int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate) {
   CHECK_T(dy, torch::kBFloat16);
@@ -289,14 +328,27 @@ void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Te
 void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red,
                   c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres,
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
-                  int64_t relu) {
+                  int64_t relu, c10::optional<Tensor> dx8, c10::optional<Tensor> amax_ring,
+                  int64_t phase, c10::optional<Tensor> scale_out) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   const int64_t C = x.size(-1);
+  uint8_t* d8 = nullptr;
+  float *prev = nullptr, *out = nullptr, *zero = nullptr;
+  if (amax_ring.has_value() && amax_ring->defined()) {  // e5m2 side output (fp8 dgrad)
+    TORCH_CHECK(C % 8 == 0, "fp8 side output needs C % 8 == 0");
+    prev = ring_slot(*amax_ring, phase);
+    out = ring_slot(*amax_ring, phase + 1);
+    zero = ring_slot(*amax_ring, phase + 2);
+    if (dx8.has_value() && dx8->defined()) {
+      TORCH_CHECK(dx8->element_size() == 1 && dx8->numel() == dx.numel() && dx8->is_contiguous());
+      d8 = (uint8_t*)dx8->data_ptr();
+    }
+  }
   bn_bwd_apply_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
                       optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
-                      C, (float)count, (int)relu, stream());
+                      C, (float)count, (int)relu, stream(), d8, prev, optfw(scale_out), out, zero);
 }
 
 // ---------------------------------------------------------------------------------- elementwise
@@ -658,6 +710,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false, py::arg("mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
+  m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dy8"), py::arg("w8t"), py::arg("dx"),
+        py::arg("scale_dy"), py::arg("scale_w"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dh"), py::arg("dw"), py::arg("accumulate") = false, py::arg("mask") = py::none());
   m.attr("AMAX_SLOT") = AMAX_SLOT;
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_quantize", &fp8_quantize);
@@ -669,7 +724,36 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_ring") = py::none(),
         py::arg("phase") = 0, py::arg("scale_out") = py::none(), py::arg("mask") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
-  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("coef"),
+        py::arg("red"), py::arg("gamma"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("count"), py::arg("relu"), py::arg("dx8") = py::none(),
+        py::arg("amax_ring") = py::none(), py::arg("phase") = 0, py::arg("scale_out") = py::none());
+  m.def("fp8_quantize_e5m2", [](Tensor x, Tensor ring, int64_t phase, bool measure, Tensor scale,
+                                Tensor y8) {
+    CHECK_T(x, torch::kBFloat16);
+    CHECK_T(scale, torch::kFloat32);
+    TORCH_CHECK(x.numel() % 16 == 0 && y8.element_size() == 1 && y8.numel() == x.numel() &&
+                y8.is_contiguous(), "fp8_quantize_e5m2: numel % 16 == 0, byte output");
+    fp8_quantize_e5m2_launch(BF(x), x.numel(), ring_slot(ring, phase),
+                             measure ? ring_slot(ring, phase + 1) : nullptr,
+                             measure ? ring_slot(ring, phase + 2) : nullptr, scale.data_ptr<float>(),
+                             (uint8_t*)y8.data_ptr(), stream());
+  });
+  m.def("fp8_dequantize_e5m2", [](Tensor y8, Tensor scale, Tensor out) {
+    TORCH_CHECK(y8.is_cuda() && y8.element_size() == 1 && y8.is_contiguous());
+    CHECK_T(out, torch::kFloat32);
+    fp8_dequantize_e5m2_launch((const uint8_t*)y8.data_ptr(), y8.numel(), scale.data_ptr<float>(),
+                               out.data_ptr<float>(), stream());
+  });
+  m.def("fp8_multi_transpose", [](Tensor src, Tensor dst, Tensor tiles) {
+    TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.element_size() == 1 && dst.element_size() == 1 &&
+                src.numel() == dst.numel() && src.is_contiguous() && dst.is_contiguous(),
+                "fp8_multi_transpose: flat byte buffers of equal size");
+    TORCH_CHECK(tiles.is_cuda() && tiles.scalar_type() == torch::kInt64 && tiles.dim() == 2 &&
+                tiles.size(1) == 4 && tiles.is_contiguous(), "tiles: int64 [n,4]");
+    fp8_multi_transpose_launch((const uint8_t*)src.data_ptr(), (uint8_t*)dst.data_ptr(),
+                               tiles.data_ptr<int64_t>(), (int)tiles.size(0), stream());
+  });
   m.def("relu_bwd", &relu_bwd);
   m.def("add_act", &add_act);
   m.def("scale_by_scalar", &scale_by_scalar);

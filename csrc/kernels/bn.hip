@@ -347,12 +347,32 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
   f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
 
+__device__ __forceinline__ uint32_t e5m2x4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
 template <bool HOIST, int U>
 __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu) {
+    float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu,
+    uint8_t* __restrict__ dx8, const float* __restrict__ amax_prev, float* __restrict__ scale_out,
+    float* __restrict__ amax_out, float* __restrict__ amax_zero) {
+  // optional e5m2 side output of dx (fp8 dgrad of the producing conv; delayed scaling with 4×
+  // headroom over the previous call's |dx|max: gradients can grow step to step, e5m2 has 30
+  // binades to spare, a clipped gradient biases the update)
+  float inv8 = 0.f, vmax = 0.f;
+  bool emit8 = false;
+  if (amax_out) {
+    const float ap = amax_read(amax_prev) * 4.f;
+    emit8 = dx8 != nullptr && ap > 0.f;
+    inv8 = ap > 0.f ? 57344.f / ap : 0.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = ap / 57344.f;
+    amax_clear(amax_zero);
+  }
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += NT) {
       if (dgamma) dgamma[c] = red[C + c];
@@ -423,9 +443,25 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = A[j] * g[j] + Bc[j] * vx[j] + Cc[j];
-      ((uint4*)dx)[k] = pack8(o);
+      const uint4 packed = pack8(o);
+      ((uint4*)dx)[k] = packed;
+      if (amax_out) {
+        float q[8];
+        unpack8(packed, q);  // quantise the stored bf16 values
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vmax = fmaxf(vmax, fabsf(q[j]));
+        if (emit8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) q[j] = fminf(fmaxf(q[j] * inv8, -57344.f), 57344.f);
+          uint2 w;
+          w.x = e5m2x4(q[0], q[1], q[2], q[3]);
+          w.y = e5m2x4(q[4], q[5], q[6], q[7]);
+          ((uint2*)dx8)[k] = w;
+        }
+      }
     }
   }
+  if (amax_out) amax_publish(amax_out, vmax);
 }
 
 __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
@@ -507,7 +543,8 @@ void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, co
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,
-                         hipStream_t st) {
+                         hipStream_t st, uint8_t* dx8, const float* amax_prev, float* scale_out,
+                         float* amax_out, float* amax_zero) {
   const long n = M * C;
   if (C % 8 == 0) {
     static const int u = env_int("TDL_BN_BWD_U", 2);
@@ -517,7 +554,8 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                                                                      : bwd_apply_vec_kernel<true, 1>)
                    : bwd_apply_vec_kernel<false, 1>;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
-                       dbeta, n / 8, C, 1.f / count, relu);
+                       dbeta, n / 8, C, 1.f / count, relu, dx8, amax_prev, scale_out, amax_out,
+                       amax_zero);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu);

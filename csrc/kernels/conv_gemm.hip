@@ -31,6 +31,7 @@
 // 16-B fp32 vector stores.  Epilogue: bias, ReLU, and per-channel Σy / Σy² of the stored bf16
 // values (BatchNorm statistics) reduced lanes → waves (LDS) → one contiguous atomic row per tile.
 #include "conv_common.h"
+#include <stdexcept>
 
 namespace tdl {
 
@@ -829,6 +830,8 @@ void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   if (ncls == 0) return;
   a.ncls = ncls;
   if (!masked && conv_dgrad_glds(a, Mmax * ncls, st)) return;
+  if (a.fp8) throw std::runtime_error("fp8 dgrad: LDS-DMA kernel not eligible (K % 128, C % 8, "
+                                      "stride with dilation)");
   int bm, bn;
   pick_tile(Mmax * ncls, a.Ng, bm, bn);
   a.cls_tile0[0] = 0;

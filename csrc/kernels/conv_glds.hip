@@ -85,16 +85,20 @@ __device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
 template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, bool FASTK,
           bool FP8 = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
-  // FP8 (FWD only): operands are OCP e4m3 bytes, a K-step is 128 deep (one 128-B LDS row per
-  // tile row, as for bf16), fragments are 32 B and feed v_mfma_scale_f32_16x16x128_f8f6f4 with
-  // unit E8M0 block scales; the per-tensor scales s_x·s_w are applied in the epilogue.
-  static_assert(!FP8 || MODE == FWD, "fp8 forward only");
+  // FP8: operands are OCP fp8 bytes, a K-step is 128 deep (one 128-B LDS row per tile row, as
+  // for bf16), fragments are 32 B and feed v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0
+  // block scales; the per-tensor scales are applied in the epilogue.  FWD: x e4m3 × W e4m3.
+  // DGRAD: dy e5m2 (gradients: wider range) × W^T e4m3 — the weight copy is stored transposed
+  // ([R][S][C][K], ops/fp8.py) so both operands are K-contiguous rows (KC LDS images, no
+  // transposed LDS reads); FASTK only (K % 128 == 0: a K-step is one tap, 128 output channels).
+  static_assert(!FP8 || MODE != WGRAD, "fp8 forward / dgrad only");
+  static_assert(!FP8 || MODE != DGRAD || FASTK, "fp8 dgrad needs K % 128 == 0");
   constexpr int ESZ = FP8 ? 1 : 2;         // bytes per element
   constexpr int EPC = 16 / ESZ;            // elements per 16-B chunk
   constexpr int KSTEP = 128 / ESZ;         // GEMM K per step (one 128-B LDS row)
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
-  constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE != FWD);
+  constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE == WGRAD) || (MODE == DGRAD && !FP8);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int IA = A_BYTES / (1024 * NW), IB = B_BYTES / (1024 * NW);
   static_assert(IA * 1024 * NW == A_BYTES && IB * 1024 * NW == B_BYTES, "tile / wave mismatch");
@@ -184,8 +188,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
-        const int ci = T.bn0 + mc_col(j, BN, mc_krow(j, BN));
-        b_base[j] = ci < a.Ng ? ci : -1;
+        if constexpr (FP8) {  // KC rows of W^T [R][S][C][K]: row ci of tap (r, s) at (r·S+s)·C·K + ci·K
+          const int ci = T.bn0 + kc_row(j);
+          b_base[j] = ci < a.Ng ? ci * a.K : -1;
+        } else {
+          const int ci = T.bn0 + mc_col(j, BN, mc_krow(j, BN));
+          b_base[j] = ci < a.Ng ? ci : -1;
+        }
       }
     } else {  // WGRAD
 #pragma unroll
@@ -254,7 +263,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
       for (int j = 0; j < IA; ++j) {
         const int lc = kc_lchunk(j);
-        int th = pos_r, tw = pos_s, co = co0 + lc * 8;
+        int th = pos_r, tw = pos_s, co = co0 + lc * EPC;
         bool kv = kb < T.Kgc;
         if constexpr (!FASTK) {
           const int k = kb + lc * 8;
@@ -266,10 +275,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
         const int ho = a_p0[j] - th * step_h, wo = a_p1[j] - tw * step_w;
         const bool v = kv && (unsigned)ho < (unsigned)a.Ho && (unsigned)wo < (unsigned)a.Wo;
-        const uint32_t off = (uint32_t)(a_base[j] + (ho * a.Wo + wo) * a.K + co) * 2u;
+        const uint32_t off = (uint32_t)(a_base[j] + (ho * a.Wo + wo) * a.K + co) * (uint32_t)ESZ;
         dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
       }
       const int r0 = a.cls_r0[c], s0 = a.cls_s0[c];
+      if constexpr (FP8) {  // W^T rows: tap (r, s) of this class, output channels co0 … +127
+        const int r = r0 + a.sh * pos_r, s = s0 + a.sw * pos_s;
+        const int toff = (r * a.S + s) * a.C * a.K + co0;
+#pragma unroll
+        for (int j = 0; j < IB; ++j) {
+          const bool v = kb < T.Kgc && b_base[j] >= 0;
+          dma16(rb_src, Bs + (j * NW + wid) * 1024,
+                v ? (uint32_t)(b_base[j] + toff + kc_lchunk(j) * EPC) : OOB);
+        }
+      } else
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
         const int kk = kb + mc_krow(j, BN);
@@ -630,8 +649,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       for (int rm = 0; rm < RM; ++rm)
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn)
-          acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b8[rn], a8[rm], acc[rm][rn],
-                                                                         0, 0, 0, 127, 0, 127);
+          // operand formats: first (B tile: weights) e4m3 = 0; second (A tile) e4m3 = 0 for
+          // FWD activations, e5m2 (bf8) = 1 for DGRAD output gradients
+          acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              b8[rn], a8[rm], acc[rm][rn], 0, MODE == DGRAD ? 1 : 0, 0, 127, 0, 127);
       slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;
       --inflight;
       if (ckt + 1 >= CT.kt1) {
@@ -845,13 +866,17 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
 // register-staged kernel should run instead.
 bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
   const int mode = conv_glds_mode();
-  if (mode == 0 || a0.C % 8 || a0.K % 8 || a0.dg_masked) return false;
-  if (mode == 1 && (Mmax_total < 4096 || a0.Ng < 128)) return false;
+  if (a0.fp8) {  // fp8 operands exist only for this kernel
+    if (a0.C % 8 || a0.K % 128 || a0.dg_masked) return false;
+  } else {
+    if (mode == 0 || a0.C % 8 || a0.K % 8 || a0.dg_masked) return false;
+    if (mode == 1 && (Mmax_total < 4096 || a0.Ng < 128)) return false;
+  }
   ConvArgs a = a0;
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
   int cfg = a.Ng <= 64 ? 1 : 0;
-  cfg = env_int("TDL_GLDS_CFG_DGRAD", cfg);
+  if (!a.fp8) cfg = env_int("TDL_GLDS_CFG_DGRAD", cfg);
   const GCfg& g = cfg_of(cfg);
   a.cls_tile0[0] = 0;
   for (int c = 0; c < a.ncls; ++c) {
@@ -863,7 +888,12 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
   a.tpb = persistent_tpb(tiles);
   a.splits = 1;
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
-  if (a.K % 64 == 0)
+  if (a.fp8) {
+    if (cfg == 1)
+      launch_g<DGRAD, 256, 64, 4, 1, 3, false, false, true, true>(a, blocks, st);
+    else
+      launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, true, true>(a, blocks, st);
+  } else if (a.K % 64 == 0)
     launch_gcfg<DGRAD, false, false, true>(a, cfg, blocks, st);
   else
     launch_gcfg<DGRAD, false, false, false>(a, cfg, blocks, st);

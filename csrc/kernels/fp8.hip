@@ -36,6 +36,77 @@ __device__ __forceinline__ uint32_t pack4_e4m3(float a, float b, float c, float 
   return (uint32_t)v;
 }
 
+constexpr float E5M2_MAX = 57344.f;
+
+__device__ __forceinline__ uint32_t pack4_e5m2(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+// e5m2 flavour of quantize_kernel (same delayed-scaling slots)
+__global__ void __launch_bounds__(NT) quantize_e5m2_kernel(const bf16_t* __restrict__ x, long n16,
+                                                           const float* __restrict__ prev,
+                                                           float* __restrict__ meas,
+                                                           float* __restrict__ clr,
+                                                           float* __restrict__ scale_out,
+                                                           uint8_t* __restrict__ y) {
+  const float am = fmaxf(amax_read(prev), 1e-30f);
+  const float inv = E5M2_MAX / am;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = am / E5M2_MAX;
+  if (clr) amax_clear(clr);
+  float m = 0.f;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n16; i += (long)gridDim.x * NT) {
+    float v[16];
+    unpack8(((const uint4*)x)[2 * i], v);
+    unpack8(((const uint4*)x)[2 * i + 1], v + 8);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      m = fmaxf(m, fabsf(v[j]));
+      v[j] = fminf(fmaxf(v[j] * inv, -E5M2_MAX), E5M2_MAX);
+    }
+    uint4 o;
+    o.x = pack4_e5m2(v[0], v[1], v[2], v[3]);
+    o.y = pack4_e5m2(v[4], v[5], v[6], v[7]);
+    o.z = pack4_e5m2(v[8], v[9], v[10], v[11]);
+    o.w = pack4_e5m2(v[12], v[13], v[14], v[15]);
+    ((uint4*)y)[i] = o;
+  }
+  if (meas) amax_publish(meas, m);
+}
+
+// one 64×64 byte tile per workgroup: 16-B row loads → LDS (padded rows) → 16-B column stores
+__global__ void __launch_bounds__(256) multi_transpose_kernel(const uint8_t* __restrict__ src,
+                                                              uint8_t* __restrict__ dst,
+                                                              const long* __restrict__ tiles) {
+  __shared__ uint8_t t[64][64 + 16];
+  const long* d = tiles + 4 * (long)blockIdx.x;
+  const long off = d[0], rows = d[1], cols = d[2], id = d[3];
+  const long tcols = (cols + 63) / 64;
+  const long r0 = (id / tcols) * 64, c0 = (id % tcols) * 64;
+  const int tr = threadIdx.x >> 2, tc = (threadIdx.x & 3) * 16;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (r0 + tr < rows && c0 + tc < cols) v = *(const uint4*)(src + off + (r0 + tr) * cols + c0 + tc);
+  *(uint4*)&t[tr][tc] = v;
+  __syncthreads();
+  // output row = source column c0 + tr, 16 consecutive source rows r0 + tc … +15
+  if (c0 + tr < cols && r0 + tc < rows) {
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      w[q] = (uint32_t)t[tc + 4 * q][tr] | ((uint32_t)t[tc + 4 * q + 1][tr] << 8) |
+             ((uint32_t)t[tc + 4 * q + 2][tr] << 16) | ((uint32_t)t[tc + 4 * q + 3][tr] << 24);
+    *(uint4*)(dst + off + (c0 + tr) * rows + r0 + tc) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+__global__ void dequantize_e5m2_kernel(const uint8_t* __restrict__ y, long n,
+                                       const float* __restrict__ scale, float* __restrict__ out) {
+  const float s = *scale;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = __builtin_amdgcn_cvt_f32_bf8((int)y[i], 0) * s;
+}
+
 // 16 elements per thread: two 16-B bf16 vectors in, one 16-B e4m3 vector out.  scale = amax(slot
 // `prev`)/448; with `meas` the |x|max of this call is accumulated into `meas` (the next call's
 // scale: delayed scaling) and `clr` is cleared for the call after.
@@ -151,6 +222,24 @@ void fp8_multi_quantize_launch(const bf16_t* src, uint8_t* dst, const long* chun
   if (nchunks <= 0) return;
   hipLaunchKernelGGL(multi_quantize_kernel, dim3(nchunks), dim3(NT), 0, st, src, dst, chunks, rings,
                      scales, phase, prime ? 1 : 0);
+}
+
+void fp8_quantize_e5m2_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,
+                              float* scale_out, uint8_t* y, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(quantize_e5m2_kernel, dim3(grid_for(n / 16)), dim3(NT), 0, st, x, n / 16, prev,
+                     meas, clr, scale_out, y);
+}
+
+void fp8_dequantize_e5m2_launch(const uint8_t* y, long n, const float* scale, float* out,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(dequantize_e5m2_kernel, dim3(grid_for(n)), dim3(NT), 0, st, y, n, scale, out);
+}
+
+void fp8_multi_transpose_launch(const uint8_t* src, uint8_t* dst, const long* tiles, int ntiles,
+                                hipStream_t st) {
+  if (ntiles <= 0) return;
+  hipLaunchKernelGGL(multi_transpose_kernel, dim3(ntiles), dim3(256), 0, st, src, dst, tiles);
 }
 
 void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st) {

@@ -46,6 +46,8 @@ struct ConvArgs {
   const float* scale_x;  // fp8 FWD: per-tensor scales of x and w (device scalars)
   const float* scale_w;
   int beta;          // DGRAD: 1 = accumulate into the existing dx (residual-gradient join)
+  int fp8;           // DGRAD: dy is e5m2 (a.dy), the weight e4m3 transposed [R][S][C][K] (a.w),
+                     // per-tensor scales a.scale_x (dy) and a.scale_w (LDS-DMA kernel, K % 128 == 0)
   const uint8_t* mask;  // DGRAD: optional ReLU bit mask of dx (1 bit per element, NHWC order):
                         // dx = ([dx +] dgrad)·[bit] — the consumers of a block output apply the
                         // mask of its ReLU, so the producer BN's backward reads no mask
@@ -93,6 +95,16 @@ void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas
 void fp8_multi_quantize_launch(const bf16_t* src, uint8_t* dst, const long* chunks, int nchunks,
                                float* rings, float* scales, int phase, bool prime, hipStream_t st);
 void fp8_dequantize_launch(const uint8_t* y, long n, const float* scale, float* out, hipStream_t st);
+// OCP e5m2 (bf8) flavour of fp8_quantize_launch (scale = amax / 57344) — output gradients
+void fp8_quantize_e5m2_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,
+                              float* scale_out, uint8_t* y, hipStream_t st);
+void fp8_dequantize_e5m2_launch(const uint8_t* y, long n, const float* scale, float* out,
+                                hipStream_t st);
+// byte-matrix transposes in one launch: tiles int64 [ntiles][4] = (offset, rows, cols, tile id);
+// dst[offset + c·rows + r] = src[offset + r·cols + c] (rows, cols % 16 == 0) — the fp8 dgrad's
+// transposed weight copies [R][S][C][K] of every fp8 conv weight [K][R·S·C]
+void fp8_multi_transpose_launch(const uint8_t* src, uint8_t* dst, const long* tiles, int ntiles,
+                                hipStream_t st);
 // bias gradient: out[K] (+)= column sums of x[P][K]; part = fp32 scratch of colsum_blocks(P, K)·K
 int colsum_blocks(long P, int K);
 void colsum_launch(const bf16_t* x, float* out, float* part, long P, int K, bool accumulate,
@@ -110,10 +122,15 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
                      uint8_t* mask = nullptr);  // mask: 1 bit per element of y > 0 (C % 8 == 0)
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                           float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0, 3 bit mask (y = uint8 mask, C % 8 == 0, C <= 2048)
+// optional e5m2 side output of dx (fp8 dgrad of the producing conv), delayed scaling as
+// bn_apply's e4m3 one: dx8 = e5m2(sat(dx·57344/amax_prev)), scale_out = amax_prev/57344,
+// this call's |dx|max into amax_out, amax_zero cleared (C % 8 == 0 only)
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,
-                         hipStream_t st);
+                         hipStream_t st, uint8_t* dx8 = nullptr, const float* amax_prev = nullptr,
+                         float* scale_out = nullptr, float* amax_out = nullptr,
+                         float* amax_zero = nullptr);
 
 // elementwise --------------------------------------------------------------------------------
 void relu_bwd_launch(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t st);

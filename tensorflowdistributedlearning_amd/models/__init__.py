@@ -16,12 +16,19 @@ _REGISTRY = {
 }
 
 
-def enable_fp8(model, fuse_bn=True):
-    """fp8 (e4m3) forward GEMMs for every bias-free conv whose input channels are a multiple of 16
-    (the 3-channel stem and biased heads stay bf16); backward stays bf16.  With ``fuse_bn`` the BN
-    layers write the e4m3 copy of their output in the same pass (scale from the previous step's
-    |y|max), so those conv inputs need no separate quantisation pass.  Returns the conv count."""
-    from .layers import Conv2d, BatchNorm
+def enable_fp8(model, fuse_bn=True, dgrad=None):
+    """fp8 GEMMs for every bias-free conv whose input channels are a multiple of 16 (the
+    3-channel stem and biased heads stay bf16): the forward on e4m3 activations × e4m3 weights
+    and — with ``dgrad`` — the input gradient on e5m2 output gradients × e4m3 weights (convs with
+    K % 128 == 0 output channels that feed a BN; the weight gradient stays bf16).  With
+    ``fuse_bn`` the BN layers write the e4m3 copy of their output in the same pass (scale from the
+    previous step's |y|max), so those conv inputs need no separate quantisation pass; the BN after
+    an fp8 conv likewise writes the e5m2 copy of its input gradient in the backward apply.
+    Returns the conv count."""
+    import os
+    from .layers import Conv2d, BatchNorm, ConvBN
+    if dgrad is None:
+        dgrad = os.environ.get("TDL_FP8_DGRAD", "1") == "1"
     n = 0
     for m in model.modules():
         if isinstance(m, Conv2d) and m.bias is None and m._cin_store % 16 == 0:
@@ -29,6 +36,10 @@ def enable_fp8(model, fuse_bn=True):
             n += 1
         elif isinstance(m, BatchNorm) and fuse_bn:
             m.emit_fp8 = True  # conv inputs arrive pre-quantised (delayed scaling, ops/bn.py)
+    if dgrad:
+        for m in model.modules():
+            if isinstance(m, ConvBN) and getattr(m.conv, "fp8", False):
+                m.bn.emit_fp8_bwd = True  # e5m2 dy for the conv's fp8 dgrad (ops/conv.py)
     return n
 
 

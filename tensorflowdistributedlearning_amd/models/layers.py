@@ -17,7 +17,7 @@ from ..ops.bn import batch_norm_act
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
 from ..ops.common import compute_weight, flat_view
-from ..ops.fp8 import DelayedScaler, flat_weights_for
+from ..ops.fp8 import DelayedScaler, flat_weights_for, transpose_weight
 from . import params as _params
 
 
@@ -189,6 +189,22 @@ class Conv2d(nn.Module):
             self.__dict__["_fp8_cache"] = cache
         return cache[1], cache[2]
 
+    def fp8_weight_t(self, w_lowp):
+        """Transposed e4m3 weight [R, S, C, K] + scale for the fp8 dgrad (same quantisation as
+        :meth:`fp8_weight`, refreshed once per optimizer step)."""
+        v = _params.version()
+        if not self.grad_needs_unpad():
+            fw = flat_weights_for(self.weight)
+            got = fw.get_t(self.weight, v) if fw is not None else None
+            if got is not None:
+                return got
+        cache = self.__dict__.get("_fp8_t_cache")
+        if cache is None or cache[0] != v or cache[1].device != w_lowp.device:
+            w8, sw = self.fp8_weight(w_lowp)
+            cache = (v, transpose_weight(w8), sw)
+            self.__dict__["_fp8_t_cache"] = cache
+        return cache[1], cache[2]
+
     def fp8_input(self, x):
         """e4m3 copy of an input no BN pre-quantised (delayed scaling, per layer)."""
         sc = self.__dict__.get("_fp8_x")
@@ -249,6 +265,18 @@ class BatchNorm(nn.Module):
         sc = self.__dict__.get("_fp8")
         if sc is None:
             sc = self.__dict__["_fp8"] = DelayedScaler()
+        return sc.bn_args(x)
+
+    emit_fp8_bwd = False  # set by models.enable_fp8: e5m2 copy of dx for the fp8 dgrad
+
+    def fp8_bwd_state(self, x):
+        """(amax ring, phase, scale, emit) for the e5m2 side output of the backward apply (the
+        producing conv's fp8 dgrad needs K % 128 == 0), or None where it does not apply."""
+        if not (x.is_cuda and self.c_phys % 128 == 0):
+            return None
+        sc = self.__dict__.get("_fp8_bwd")
+        if sc is None:
+            sc = self.__dict__["_fp8_bwd"] = DelayedScaler()
         return sc.bn_args(x)
 
     def forward(self, x, stats=None, residual=None, relu=False, res_join=None):

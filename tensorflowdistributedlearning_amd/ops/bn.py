@@ -127,15 +127,28 @@ def bn_bwd_reduce(dy, y, x, coef, relu):
     return torch.stack([g.sum(0), (g * xhat).sum(0)])
 
 
-def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None, dbeta=None):
+def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None, dbeta=None,
+                 fp8=None):
     """dx (same dtype as x) and optionally the masked gradient g for the residual branch.
-    On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch."""
+    On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch.
+    ``fp8`` = (amax_ring, phase, scale, emit): also write an e5m2 copy of dx with delayed scaling
+    (4× headroom over the previous call's |dx|max) — attached as ``dx._tdl_fp8`` = (dx8, scale)
+    for the fp8 dgrad of the producing conv."""
     C = x.shape[-1]
     if on_gpu(dy):
         dx = torch.empty_like(x)
         dres = torch.empty_like(dy) if want_dres else None
+        if fp8 is None:
+            ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
+                               int(relu))
+            return dx, dres
+        ring, phase, scale, emit = fp8
+        dx8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e5m2) if emit else None
         ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
-                           int(relu))
+                           int(relu), dx8.view(torch.uint8) if emit else None, ring, int(phase),
+                           scale)
+        if emit:
+            dx._tdl_fp8 = (dx8, scale)
         return dx, dres
     g = dy.float().reshape(-1, C)
     if relu:
@@ -221,9 +234,10 @@ class _BatchNormActFn(torch.autograd.Function):
         direct_b = on_gpu(dy) and bt is not None and bfresh
         gp, _ = _phys_params(ctx.bn, gamma, beta)
         count = ctx.count if ctx.training else float("inf")  # frozen BN: dx = γ·invstd·g
+        fp8 = ctx.bn.fp8_bwd_state(x) if getattr(ctx.bn, "emit_fp8_bwd", False) else None
         dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, count, relu,
                                 ctx.has_res and not premasked,
-                                gt if direct_g else None, bt if direct_b else None)
+                                gt if direct_g else None, bt if direct_b else None, fp8=fp8)
         if premasked and ctx.has_res:
             dres = dy
         if want_g:

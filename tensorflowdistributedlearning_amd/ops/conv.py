@@ -175,6 +175,37 @@ def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
     return cover > 0
 
 
+def conv_dgrad_fp8(dy8, sdy, w8t, sw, x_shape, geom: ConvGeom, out=None, accumulate=False,
+                   mask=None):
+    """dx from fp8 operands: ``dy8`` e5m2 [N,Ho,Wo,K] with scale ``sdy``, ``w8t`` the e4m3 weight
+    transposed to [R,S,C,K] with scale ``sw`` (ops/fp8.py).  GPU: the LDS-DMA dgrad on
+    v_mfma_scale_f32_16x16x128_f8f6f4 (K % 128 == 0); join accumulate / ReLU mask as
+    :func:`conv_dgrad`.  CPU: fp32 on the dequantised operands."""
+    if on_gpu(dy8):
+        dx = out if out is not None else torch.empty(x_shape, device=dy8.device,
+                                                     dtype=torch.bfloat16)
+        ext().conv_dgrad_fp8(dy8.view(torch.uint8), w8t.view(torch.uint8), dx, sdy, sw,
+                             geom.stride[0], geom.stride[1], geom.padding[0], geom.padding[2],
+                             geom.dilation[0], geom.dilation[1],
+                             bool(accumulate and out is not None), mask)
+        return dx
+    w = (w8t.float() * sw).permute(3, 0, 1, 2).contiguous()
+    return conv_dgrad(dy8.float() * sdy, w, x_shape, geom, out=out, accumulate=accumulate,
+                      mask=mask, out_dtype=torch.bfloat16)
+
+
+def fp8_dgrad_eligible(layer, dy, geom: ConvGeom, w_shape):
+    """Can this conv's dgrad run on fp8 operands?  An fp8 layer whose output gradient arrived
+    with an e5m2 copy (the BN backward's side output), K % 128 == 0 (one tap per 128-deep K-step)
+    and no stride-with-dilation (masked-class dgrad)."""
+    if layer is None or not getattr(layer, "fp8", False) or getattr(dy, "_tdl_fp8", None) is None:
+        return False
+    K, R, S, C = w_shape
+    (sh, sw), (dh, dw) = geom.stride, geom.dilation
+    masked = (sh > 1 and dh > 1) or (sw > 1 and dw > 1)
+    return K % 128 == 0 and C % 8 == 0 and not masked and not layer.grad_needs_unpad()
+
+
 def dgrad_covers_input(geom: ConvGeom, R, S):
     """Does the dgrad of this conv write every input pixel (no empty stride parity class)?"""
     (sh, sw), (dh, dw) = geom.stride, geom.dilation
@@ -266,17 +297,29 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
                 compute_weight(weight, dy.dtype)
+            if fp8_dgrad_eligible(ctx.layer, dy, geom, tuple(w.shape)):
+                # fp8 dgrad: e5m2 dy (the BN backward's side output) × e4m3 W^T
+                dy8, sdy = dy._tdl_fp8
+                w8t, sw8 = ctx.layer.fp8_weight_t(w)
+
+                def dgrad(out=None, accumulate=False, mask=None):
+                    return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
+                                          accumulate=accumulate, mask=mask)
+            else:
+                def dgrad(out=None, accumulate=False, mask=None):
+                    return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,
+                                      mask=mask)
             join = ctx.join
             if join is None:
-                dx = conv_dgrad(dy, w, ctx.x_shape, geom)
+                dx = dgrad()
             else:  # residual-gradient join: first consumer writes, later ones accumulate
                 # pre-masked join (ops/gradjoin.py); the epilogue reads 64-channel mask slabs
                 mask = join.mask if on_gpu(dy) and ctx.x_shape[-1] % 64 == 0 else None
                 if join.buf is None:
-                    join.buf = conv_dgrad(dy, w, ctx.x_shape, geom, mask=mask)
+                    join.buf = dgrad(mask=mask)
                     join.note(mask is not None)
                 else:
-                    conv_dgrad(dy, w, ctx.x_shape, geom, out=join.buf, accumulate=True, mask=mask)
+                    dgrad(out=join.buf, accumulate=True, mask=mask)
                     join.note(mask is not None, dgrad_covers_input(geom, w.shape[1], w.shape[2]))
                 dx = join.take()
         if side is None:

@@ -13,6 +13,8 @@ from .common import on_gpu, ext
 
 E4M3 = torch.float8_e4m3fn
 E4M3_MAX = 448.0
+E5M2 = torch.float8_e5m2
+E5M2_MAX = 57344.0
 
 
 AMAX_SLOT = 1024  # fp32 partial maxima per amax slot (csrc/kernels/kernels.h AMAX_SLOT)
@@ -37,6 +39,30 @@ def quantize_e4m3(x):
     scale = (amax / E4M3_MAX).reshape(1)
     y8 = (xf / scale).clamp(-E4M3_MAX, E4M3_MAX).to(E4M3)
     return y8, scale
+
+
+def quantize_e5m2(x):
+    """Just-in-time e5m2 (OCP bf8) quantisation — output gradients of the fp8 dgrad."""
+    if on_gpu(x):
+        ring = _new_ring(x.device)
+        scale = torch.empty(1, device=x.device, dtype=torch.float32)
+        y8 = torch.empty(x.shape, device=x.device, dtype=E5M2)
+        xc = x.contiguous()
+        ext().fp8_amax(xc, ring, 0)
+        ext().fp8_quantize_e5m2(xc, ring, 0, False, scale, y8.view(torch.uint8))
+        return y8, scale
+    xf = x.float()
+    amax = xf.abs().max().clamp_min(1e-30)
+    scale = (amax / E5M2_MAX).reshape(1)
+    y8 = (xf / scale).clamp(-E5M2_MAX, E5M2_MAX).to(E5M2)
+    return y8, scale
+
+
+def transpose_weight(w8):
+    """[K, R, S, C] fp8 → [R, S, C, K] (the fp8 dgrad's B operand layout)."""
+    K = w8.shape[0]
+    t = w8.view(torch.uint8).reshape(K, -1).t().contiguous()
+    return t.view(w8.dtype).reshape(*w8.shape[1:], K)
 
 
 class DelayedScaler:
@@ -102,6 +128,9 @@ class FlatFp8Weights:
     def __init__(self, flat_lowp):
         self.flat = flat_lowp
         self.w8 = torch.empty(flat_lowp.numel(), device=flat_lowp.device, dtype=E4M3)
+        # transposed copies [R][S][C][K] for the fp8 dgrad, refreshed by one transpose launch
+        self.w8t = torch.zeros(flat_lowp.numel(), device=flat_lowp.device, dtype=E4M3)
+        self.tviews = {}
         self.views = {}     # id(param) -> (w8 view, scale view), valid for the buffers' lifetime
         self.pending = {}   # id(param) -> (offset, numel, shape)
         self.spans = []     # segment -> (offset, numel, shape)
@@ -125,6 +154,19 @@ class FlatFp8Weights:
         self.scales = torch.zeros(len(self.spans), device=dev)
         self.views = {k: (self.w8[off:off + n].view(shape), self.scales[seg:seg + 1])
                       for seg, (k, (off, n, shape)) in enumerate(zip(keys, self.spans))}
+        trows = []
+        self.tviews = {}
+        for seg, (k, (off, n, shape)) in enumerate(zip(keys, self.spans)):
+            K = shape[0]
+            cols = n // K
+            if len(shape) == 4 and K % 16 == 0 and cols % 16 == 0:
+                tiles = ((K + 63) // 64) * ((cols + 63) // 64)
+                trows += [(off, K, cols, t) for t in range(tiles)]
+                self.tviews[k] = (self.w8t[off:off + n].view(*shape[1:], K),
+                                  self.scales[seg:seg + 1])
+        self.tiles = torch.tensor(trows if trows else [(0, 16, 16, 0)],
+                                  dtype=torch.int64).to(dev)
+        self.ntiles = len(trows)
         self.phase = 0
         ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
                                  self.scales, self.phase, True)  # prime: exact first scales
@@ -136,14 +178,28 @@ class FlatFp8Weights:
         if k not in self.views and k not in self.pending:
             self.pending[k] = (p._flat_offset, p.numel(), tuple(p.shape))
             return None
+        self._refresh(version)
+        return self.views.get(k)  # None: joined during this version
+
+    def _refresh(self, version):
         if self.version != version:
             if self.pending:
                 self._rebuild()
             ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
                                      self.scales, self.phase, False)
+            if self.ntiles:
+                ext().fp8_multi_transpose(self.w8.view(torch.uint8), self.w8t.view(torch.uint8),
+                                          self.tiles)
             self.phase = (self.phase + 1) % 3
             self.version = version
-        return self.views.get(k)  # None: joined during this version
+
+    def get_t(self, p, version):
+        """(W^T [R, S, C, K] e4m3, scale) of parameter ``p`` for the fp8 dgrad, or None if ``p``
+        has no flat copy yet (it joins at its first forward)."""
+        if id(p) not in self.tviews:
+            return None
+        self._refresh(version)
+        return self.tviews.get(id(p))
 
 
 def flat_weights_for(p):
@@ -156,6 +212,14 @@ def flat_weights_for(p):
     if fw is None:
         fw = flat._tdl_fp8w = FlatFp8Weights(flat)
     return fw
+
+
+def dequantize_e5m2(y8, scale):
+    if on_gpu(y8):
+        out = torch.empty(y8.shape, device=y8.device, dtype=torch.float32)
+        ext().fp8_dequantize_e5m2(y8.contiguous().view(torch.uint8), scale, out)
+        return out
+    return y8.float() * scale
 
 
 def dequantize(y8, scale):

@@ -498,6 +498,84 @@ def test_conv_fwd_fp8(gpu, shape):
     assert rel_err(y, C.ref_conv_fwd(x.float(), w.float(), g)) < 0.08
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 3, 1, 1),     # 3x3, Ng 64 (256x64 tiles)
+                                   (4, 15, 15, 256, 128, 1, 1, 2, 0),   # 1x1/s2: empty classes
+                                   (8, 28, 28, 128, 256, 3, 3, 2, 1),   # 3x3/s2: 4 parity classes
+                                   (16, 14, 14, 512, 256, 1, 1, 1, 0)])  # 1x1, many tiles
+def test_conv_dgrad_fp8(gpu, shape, accumulate):
+    """fp8 dgrad (e5m2 dy × e4m3 W^T on the f8f6f4 MFMA, LDS-DMA kernel) vs the fp32 dgrad of the
+    same dequantised operands; with accumulate, the join's dx += … plus the ReLU bit mask."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8, bn as BN
+    N, H, W, Cin, K, R, S, st, p = shape
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
+    torch.manual_seed(17)
+    Ho, Wo = g.out_hw(H, W, R, S)
+    dy = torch.randn(N, Ho, Wo, K).bfloat16()
+    w = (torch.randn(K, R, S, Cin) / math.sqrt(R * S * K)).bfloat16()
+    dy8, sdy = F8.quantize_e5m2(dy.to(gpu))
+    w8, sw = F8.quantize_e4m3(w.to(gpu))
+    w8t = F8.transpose_weight(w8)
+    assert w8t.shape == (R, S, Cin, K)
+    ref = C.ref_conv_dgrad(F8.dequantize_e5m2(dy8, sdy).cpu(), F8.dequantize(w8, sw).cpu(),
+                           (N, H, W, Cin), g)
+    prev = torch.randn(N, H, W, Cin).bfloat16()
+    mask = None
+    if accumulate:
+        keep = torch.rand(N, H, W, Cin) > 0.3
+        bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)
+        mask = bits.sum(1).to(torch.uint8)
+        touched = C._dgrad_touched(w.shape, (N, H, W, Cin), g)
+        ref = (ref + prev.float()) * (keep | ~touched)
+    out = prev.to(gpu) if accumulate else None
+    dx = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, out=out, accumulate=accumulate,
+                          mask=None if mask is None else mask.to(gpu))
+    assert dx.dtype == torch.bfloat16 and dx.shape == ref.shape
+    assert rel_err(dx, ref) < 2e-2
+    if not accumulate:  # vs the bf16 dgrad of the unquantised data: quantisation error only
+        assert rel_err(dx, C.ref_conv_dgrad(dy.float(), w.float(), (N, H, W, Cin), g)) < 0.15
+
+
+def test_fp8_e5m2_quantize_and_transpose(gpu):
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    torch.manual_seed(19)
+    x = (torch.randn(3, 5, 7, 32) * 40).bfloat16()
+    y8, s = F8.quantize_e5m2(x.to(gpu))
+    yc, sc = F8.quantize_e5m2(x)
+    torch.testing.assert_close(s.cpu(), sc, rtol=1e-6, atol=0)
+    deq = F8.dequantize_e5m2(y8, s).cpu()
+    assert rel_err(deq, yc.float() * sc) < 1e-6     # same e5m2 codes as torch's RNE conversion
+    assert rel_err(deq, x.float()) < 0.13           # 2 mantissa bits
+    w8, _ = F8.quantize_e4m3(torch.randn(128, 3, 3, 64, device=gpu).bfloat16())
+    torch.testing.assert_close(F8.transpose_weight(w8).view(torch.uint8).cpu(),
+                               w8.view(torch.uint8).cpu().permute(1, 2, 3, 0).contiguous())
+
+
+def test_bn_bwd_apply_e5m2_side_output(gpu):
+    """BN backward apply's e5m2 copy of dx (delayed scaling: the first call only measures, the
+    second quantises with the first call's |dx|max)."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    torch.manual_seed(21)
+    M, Cc = 2 * 9 * 11, 128
+    x = (torch.randn(2, 9, 11, Cc) * 2 + 0.5).bfloat16().to(gpu)
+    dy = torch.randn(2, 9, 11, Cc).bfloat16().to(gpu)
+    st = B.bn_stats(x)
+    coef = B.bn_finalize(st, M, torch.ones(Cc, device=gpu), torch.zeros(Cc, device=gpu),
+                         torch.zeros(Cc, device=gpu), torch.ones(Cc, device=gpu), 0.9, 1e-3, True)
+    red = B.bn_bwd_reduce(dy, None, x, coef, 2)
+    sc = F8.DelayedScaler()
+    dx0, _ = B.bn_bwd_apply(dy, None, x, coef, red, torch.ones(Cc, device=gpu), M, 2, False,
+                            fp8=sc.bn_args(x))
+    assert getattr(dx0, "_tdl_fp8", None) is None       # first call: measure only
+    dx1, _ = B.bn_bwd_apply(dy, None, x, coef, red, torch.ones(Cc, device=gpu), M, 2, False,
+                            fp8=sc.bn_args(x))
+    dx8, s = dx1._tdl_fp8
+    assert dx8.dtype == torch.float8_e5m2
+    torch.testing.assert_close(float(s), 4 * float(dx0.float().abs().max()) / F8.E5M2_MAX,
+                               rtol=1e-6, atol=0)  # 4× headroom over the previous |dx|max
+    assert rel_err(F8.dequantize_e5m2(dx8, s), dx1) < 0.13
+
+
 def test_fp8_flat_weights_one_launch(gpu):
     """All fp8 weights of a flat buffer re-quantised by one launch per parameter version; the
     first version is exact (primed), later versions use the previous amax."""

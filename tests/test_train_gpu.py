@@ -193,6 +193,40 @@ def test_resnet_fp8_forward_trains(gpu, fuse_bn):
     assert min(losses[-3:]) < losses[0], losses
 
 
+@pytest.mark.parametrize("depth", [18, 50])
+def test_resnet_fp8_dgrad_trains(gpu, depth, monkeypatch):
+    """fp8 forward + fp8 dgrad (e5m2 output gradients from the BN backward, e4m3 transposed
+    weights): the fp8 dgrad runs for every eligible conv (K % 128 == 0) after the delayed
+    scaling has its first measurement, and the loss stays finite and falls (numerics of the
+    kernel: tests/test_kernels_gpu.py::test_conv_dgrad_fp8)."""
+    from tensorflowdistributedlearning_amd.ops import conv as C
+    calls = []
+    orig = C.conv_dgrad_fp8
+
+    def spy(*a, **k):
+        calls.append(a[0].shape)
+        return orig(*a, **k)
+    monkeypatch.setattr(C, "conv_dgrad_fp8", spy)
+    torch.manual_seed(0)
+    net = models.build(f"resnet{depth}", num_classes=10)
+    models.enable_fp8(net)
+    # ResNet-50 from random init on one 64-px batch diverges in bf16 too at lr 0.01
+    # (tools/fp8_train_curve.py): a smaller step for it
+    tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01 if depth == 18 else 0.001,
+                                                            momentum=0.9, weight_decay=0.0))
+    x, y = imagenet_batch(32, 64, num_classes=10, device=gpu)
+    losses = []
+    for i in range(8):
+        calls.clear()
+        losses.append(float(tr.train_step(x, y)[0]))
+        if i == 0:
+            assert not calls  # first step: the e5m2 scalers only measure
+    eligible = sum(1 for m in net.modules() if getattr(m, "fp8", False)
+                   and m.__class__.__name__ == "Conv2d" and m.cout % 128 == 0)
+    assert len(calls) == eligible > 4, (len(calls), eligible)
+    assert all(l == l for l in losses) and min(losses[-3:]) < losses[0], losses
+
+
 def test_deeplab_channel_padding_gpu_matches_unpadded(gpu):
     """The reference preset with its 258-wide block2 carried as 264 physical channels (LDS-DMA
     kernels, flat-buffer slack for γ/β/bias) vs the unpadded generic-kernel path: same logits and
@@ -357,7 +391,11 @@ def test_side_stream_wgrad_matches_serial(gpu, model):
     torch.cuda.synchronize()
     assert torch.isfinite(masters[0]).all()
     assert not torch.equal(masters[0], start)  # the steps really updated the parameters
-    torch.testing.assert_close(masters[1], masters[0], rtol=1e-4, atol=1e-7)
+    # the two trajectories differ only by the BN backward's fp32 atomic summation order, which
+    # this unnormalised frozen-BN net amplifies over the steps; a missing join reads stale or
+    # zero gradients and moves the update by O(1) (tools/race_negative_control.py)
+    u0, u1 = masters[0] - start, masters[1] - start
+    assert ((u1 - u0).norm() / u0.norm()).item() < 1e-2
 
 
 def test_plain_backward_joins_side_stream(gpu):
@@ -389,7 +427,7 @@ def test_plain_backward_joins_side_stream(gpu):
         streams.set_enabled(old)
     # equal up to the BN backward's fp32 atomic summation order; a read before the stalled side
     # stream finished would see stale gradients (tools/race_negative_control.py)
-    torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-7)
+    assert ((outs[1] - outs[0]).norm() / outs[0].norm()).item() < 1e-3
 
 
 @pytest.mark.parametrize("early", [True, False])
