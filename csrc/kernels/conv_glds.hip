@@ -727,6 +727,8 @@ constexpr GCfg G256x128{256, 128, 4, 2, 3};
 constexpr GCfg G256x64{256, 64, 4, 1, 3};
 constexpr GCfg G128x128{128, 128, 2, 2, 4};
 constexpr GCfg G128x128s2{128, 128, 2, 2, 2};  // 66 KB LDS: two workgroups per CU
+constexpr GCfg G256x64w8{256, 64, 8, 1, 3};    // 64-wide N with 8 waves (32-row wave tiles)
+constexpr GCfg G128x64{128, 64, 4, 1, 4};      // 64-wide N, 4 stages, 96 KB LDS
 
 constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
   return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
@@ -753,12 +755,23 @@ void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
     launch_g<MODE, 256, 64, 4, 1, 3, STATS, BIAS, FK>(a, blocks, st);
   else if (cfg == 2)
     launch_g<MODE, 128, 128, 2, 2, 4, STATS, BIAS, FK>(a, blocks, st);
-  else
+  else if (cfg == 3)
     launch_g<MODE, 128, 128, 2, 2, 2, STATS, BIAS, FK>(a, blocks, st);
+  else if (cfg == 4)
+    launch_g<MODE, 256, 64, 8, 1, 3, STATS, BIAS, FK>(a, blocks, st);
+  else
+    launch_g<MODE, 128, 64, 4, 1, 4, STATS, BIAS, FK>(a, blocks, st);
 }
 
 const GCfg& cfg_of(int c) {
-  return c == 0 ? G256x128 : (c == 1 ? G256x64 : (c == 2 ? G128x128 : G128x128s2));
+  switch (c) {
+    case 0: return G256x128;
+    case 1: return G256x64;
+    case 2: return G128x128;
+    case 3: return G128x128s2;
+    case 4: return G256x64w8;
+    default: return G128x64;
+  }
 }
 
 void set_fastdivs(ConvArgs& a) {

@@ -168,6 +168,7 @@ class Trainer:
             step_count, global_step = self.optimizer.step_count, self.global_step
             _params.bump_version()  # derived weight copies (channel padding) refresh in-graph
             g = torch.cuda.CUDAGraph()
+            cap_stream = None
             try:
                 # thread_local: the native communicator's watchdog thread keeps polling its
                 # eager collectives' events during the capture (a global-mode capture would be
@@ -175,9 +176,10 @@ class Trainer:
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     # wgrads fork onto the side stream inside the capture and are joined back
                     # after backward (ops/streams.py), as in eager steps
+                    cap_stream = torch.cuda.current_stream(self.device)
                     self.graph_out = self._step(self.static_x, self.static_y)
             finally:
-                streams.end_capture()
+                streams.end_capture(cap_stream)
         # capture records without executing: the host-side counters did not really advance
         self.optimizer.step_count, self.global_step = step_count, global_step
         self.graph = g

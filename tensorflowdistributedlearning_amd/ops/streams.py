@@ -89,9 +89,13 @@ def origin(device):
     return _ORIGIN.get(torch.device(device), torch.cuda.current_stream(device))
 
 
-def end_capture():
-    """Forget the capture's forked side streams (call once the capture has ended)."""
+def end_capture(capture_stream=None):
+    """Forget the capture's forked side streams and the tensors its side-stream work read (call
+    once the capture has ended: the graph's private pool keeps their memory for its replays)."""
     _FORKED.clear()
+    if capture_stream is not None:
+        for key in [k for k in _KEEP if k[1] == capture_stream.stream_id]:
+            del _KEEP[key]
 
 
 _JOIN_QUEUED: dict = {}  # device -> autograd graph-task id whose final callback joins it
