@@ -38,7 +38,8 @@ bf16_t* optbw(const c10::optional<Tensor>& t) { return const_cast<bf16_t*>(optb(
 
 uint32_t nbytes32(const Tensor& t) {
   const int64_t n = t.numel() * t.element_size();
-  TORCH_CHECK(n < (int64_t(1) << 32) - 64, "tensor too large for 32-bit buffer addressing");
+  // < 3.75 GiB: the conv epilogues push invalid rows to byte offset 0xF0000000 (ROW_OOB)
+  TORCH_CHECK(n < int64_t(0xF0000000), "tensor too large for 32-bit buffer addressing");
   return (uint32_t)n;
 }
 

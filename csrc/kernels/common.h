@@ -23,6 +23,23 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, h);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// two floats → packed bf16 pair (round-to-nearest-even) in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  const bf16x2 h = __builtin_convertvector((f32x2){a, b}, bf16x2);
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+// ReLU of a packed bf16 pair in one v_pk_max_i16: a bf16 is negative iff its int16 bit pattern
+// is (−0 → +0; a NaN with the sign bit set → 0)
+__device__ __forceinline__ uint32_t relu_pk_bf16(uint32_t v) {
+  const s16x2 x = __builtin_bit_cast(s16x2, v);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, (s16x2){0, 0}));
+}
+
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

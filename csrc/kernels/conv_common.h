@@ -48,6 +48,9 @@ __device__ __forceinline__ bf16x8 read_mc(const char* tile, int krow, int col) {
 // and is dropped on store, so padding / ragged edges need no branch (a per-element branch around
 // a load makes hipcc wait vmcnt(0) per element and serialises the staging pipeline).
 constexpr uint32_t OOB = 0xFFFFFFF0u;
+// byte offset of an invalid output row: row + column offsets (< 64 KiB) stay past any buffer the
+// 32-bit range-checked descriptors address (hosts check out_bytes < ROW_OOB) without wrapping
+constexpr uint32_t ROW_OOB = 0xF0000000u;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
@@ -188,6 +191,24 @@ __device__ __forceinline__ long out_row(const ConvArgs& a, const Tile& T, int m)
   }
 }
 
+// out_row with the prepared fast divisions and 32-bit arithmetic (LDS-DMA kernel epilogue; no
+// dg_masked classes there)
+template <int MODE>
+__device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& T, int m) {
+  if constexpr (MODE == DGRAD) {
+    const int c = T.cls;
+    const uint32_t Hc = a.cls_Hc[c], Wc = a.cls_Wc[c];
+    const uint32_t n = fdiv((uint32_t)m, a.cls_fdHW[c]);
+    const uint32_t rem = (uint32_t)m - n * Hc * Wc;
+    const uint32_t i = fdiv(rem, a.cls_fdW[c]);
+    const uint32_t j = rem - i * Wc;
+    const uint32_t h = (uint32_t)a.cls_a[c] + (uint32_t)a.sh * i;
+    const uint32_t w = (uint32_t)a.cls_b[c] + (uint32_t)a.sw * j;
+    return (n * (uint32_t)a.H + h) * (uint32_t)a.W + w;
+  } else {
+    return (uint32_t)m;
+  }
+}
 
 }  // namespace convk
 }  // namespace tdl

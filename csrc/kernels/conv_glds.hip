@@ -39,6 +39,24 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+constexpr int vm63(int v) { return v < 63 ? v : 63; }  // 6-bit vmcnt field: a smaller count only waits longer
+
+// s_waitcnt vmcnt(LPS·ahead + (E or E/2)·ne) with the immediates the ring can need
+template <int LPS, int E, int ST>
+__device__ __forceinline__ void wait_ring(int ahead, int ne, bool half) {
+#define TDL_W(A, NE)                                              \
+  if (ahead == A && ne == NE) {                                   \
+    if (half) wait_vmcnt<vm63(LPS * A + (E / 2) * NE)>();         \
+    else wait_vmcnt<vm63(LPS * A + E * NE)>();                    \
+    return;                                                       \
+  }
+  TDL_W(0, 0) TDL_W(0, 1)
+  if constexpr (ST >= 3) { TDL_W(0, 2) TDL_W(1, 0) TDL_W(1, 1) TDL_W(1, 2) }
+  if constexpr (ST >= 4) { TDL_W(0, 3) TDL_W(1, 3) TDL_W(2, 0) TDL_W(2, 1) TDL_W(2, 2) TDL_W(2, 3) }
+#undef TDL_W
+  wait_vmcnt<0>();
+}
+
 typedef __attribute__((address_space(3))) char lds_char_t;
 
 // Fragment reads are inline asm: hipcc cannot order LDS reads against in-flight LDS-DMA and
@@ -360,6 +378,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   };
   const bool no_mfma = a.dbg & 2;
   const bool no_epi_mem = a.dbg & 128;  // timing-only: epilogue issues no global loads / stores
+  const bool wide_store = !(a.dbg & 256);  // 16-B epilogue stores (dbg 256: 8-B, for A/B)
   auto mfmas = [&](const bf16x8(&af)[RM], const bf16x8(&bfg)[RN]) {
     if (no_mfma) {
 #pragma unroll
@@ -400,102 +419,146 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
       }
     } else {
-      const rsrc_t rbias = make_rsrc(a.bias, a.bias ? (uint32_t)a.Ng * 4u : 0u);
-      const rsrc_t rmask = make_rsrc(a.mask, a.mask ? a.out_bytes / 16u : 0u);
-      // Phase 1: every load the epilogue needs (bias, the DGRAD join's previous dx, the ReLU
-      // mask) is issued before any is used — one memory round trip per tile.  Interleaved
-      // load → use per fragment made hipcc wait vmcnt(0) RM·RN times per tile, draining the
-      // next tile's in-flight operand DMA each time (the accumulating join dgrads ran 2-3x slower
-      // than the same GEMM without them).
-      long orow[RM];
-      bool mv[RM];
+      // Row byte offsets are 32-bit with invalid rows pushed past the buffer (ROW_OOB): a
+      // fragment's store offset is then row base + a compile-time constant.  Rows past the GEMM's
+      // M hold zeros (their A rows were fetched out of range), so the statistics need no mask.
+      uint32_t rbase[RM];
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm) {
         const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-        mv[rm] = m < T.Mc;
-        orow[rm] = mv[rm] ? out_row<MODE>(a, T, m) : 0;
+        rbase[rm] = m < T.Mc ? out_row_fast<MODE>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
       }
+      const int c0 = T.bn0 + wn * TN + (lane >> 4) * 4;  // this lane's column in fragment rn = 0
+      const bool cols_ok = T.bn0 + wn * TN + TN <= a.Ng;   // wave-uniform: no ragged columns
+      // Per fragment: two v_cvt_pk_bf16_f32, the ReLU as one packed int16 max per pair (a bf16
+      // is negative iff its int16 pattern is), one 16-B store per fragment pair.  The earlier
+      // per-element epilogue (64-bit row math, integer divisions, per-fragment validity selects,
+      // runtime mask / join / ReLU tests on every value) cost ≈1,200 VALU instructions per wave
+      // per tile — at 4 cycles per wave64 VALU op that, not HBM, paced the 1–4-K-step tiles of
+      // 1×1 convs (tools/dgrad_ablate.py: 129 µs for a 1×1 dgrad with no memory traffic).
       v4u32 bias_v[RN];
       if constexpr (BIAS) {
+        const rsrc_t rbias = make_rsrc(a.bias, (uint32_t)a.Ng * 4u);
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
-          const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
+          const int n0 = c0 + rn * 16;
           bias_v[rn] = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
         }
       }
-      // DGRAD ReLU mask (pre-masked join): a row's TN mask bits of the wave's columns in one 4- /
-      // 8-byte load (ldc % 64 == 0: byte-aligned slab), reused by every rn fragment
-      uint64_t mrow[RM];
+      // DGRAD residual join (dx += this dgrad: the previous dx is read back) and ReLU bit mask
+      // (pre-masked join: a row's TN mask bits of the wave's columns in one 4- / 8-byte load,
+      // ldc % 64 == 0).  Every load is issued before any is used — one memory round trip per
+      // tile; interleaved load → use made hipcc wait vmcnt(0) per fragment, draining the next
+      // tile's in-flight operand DMA each time.
+      bool join_prev = false, join_mask = false;
+      if constexpr (MODE == DGRAD) {
+        join_prev = a.beta && !no_epi_mem;
+        join_mask = a.mask && !no_epi_mem;
+      }
+      uint32_t mrow[RM][2];
       v2u32 pv[RM][RN];
+      if constexpr (MODE == DGRAD) {
+        if (join_mask) {
+          const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
 #pragma unroll
-      for (int rm = 0; rm < RM; ++rm) {
-        mrow[rm] = ~0ull;
-        if constexpr (MODE == DGRAD) {
-          if (a.mask && !no_epi_mem) {
-            const uint32_t boff = (uint32_t)((orow[rm] * a.ldc + T.bn0 + wn * TN) >> 3);
+          for (int rm = 0; rm < RM; ++rm) {
+            const uint32_t boff = (rbase[rm] / 2u + (uint32_t)(T.bn0 + wn * TN)) >> 3;
+            const uint32_t o = rbase[rm] != ROW_OOB ? boff : OOB;
             if constexpr (TN == 64) {
-              const v2u32 mv2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, mv[rm] ? boff : OOB, 0, 0);
-              mrow[rm] = (uint64_t)mv2[0] | ((uint64_t)mv2[1] << 32);
+              const v2u32 m2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, o, 0, 0);
+              mrow[rm][0] = m2[0];
+              mrow[rm][1] = m2[1];
             } else {
               static_assert(TN == 32, "mask slab of 4 or 8 bytes");
-              mrow[rm] = __builtin_amdgcn_raw_buffer_load_b32(rmask, mv[rm] ? boff : OOB, 0, 0);
-            }
-          }
-          if (a.beta && !no_epi_mem) {  // residual-gradient join: dx += this conv's dgrad
-#pragma unroll
-            for (int rn = 0; rn < RN; ++rn) {
-              const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
-              const uint32_t poff = (uint32_t)(orow[rm] * a.ldc + n0) * 2u;
-              pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(rout, (mv[rm] && n0 < a.Ng) ? poff : OOB, 0, 0);
+              mrow[rm][0] = __builtin_amdgcn_raw_buffer_load_b32(rmask, o, 0, 0);
+              mrow[rm][1] = 0;
             }
           }
         }
+        if (join_prev) {
+#pragma unroll
+          for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn) {
+              const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+              pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
+                  rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+            }
+        }
       }
-      // Phase 2: combine and store
+      const bool relu = a.relu;
+      const bool wide = wide_store && cols_ok;
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm) {
+        v2u32 pk[RN];
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
-          const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
-          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          f32x4 t = acc[rm][rn];
+          if constexpr (FP8) t = t * out_scale;
           if constexpr (BIAS) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) bv[i] = __uint_as_float(bias_v[rn][i]);
+            for (int i = 0; i < 4; ++i) t[i] += __uint_as_float(bias_v[rn][i]);
           }
-          bf16_t h[4];
-          float v[4];
-          float prev[4] = {0.f, 0.f, 0.f, 0.f};
-          uint32_t mbits = 0xFu;
           if constexpr (MODE == DGRAD) {
-            if (a.mask) mbits = (uint32_t)(mrow[rm] >> (rn * 16 + (lane >> 4) * 4)) & 0xFu;
-            if (a.beta && !no_epi_mem) {
-              prev[0] = __uint_as_float(pv[rm][rn][0] << 16);
-              prev[1] = __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
-              prev[2] = __uint_as_float(pv[rm][rn][1] << 16);
-              prev[3] = __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
+            if (join_prev) {
+              t[0] += __uint_as_float(pv[rm][rn][0] << 16);
+              t[1] += __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
+              t[2] += __uint_as_float(pv[rm][rn][1] << 16);
+              t[3] += __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
+            }
+            if (join_mask) {
+              // bit (rn·16 + group·4 + i) of the wave's TN-column slab; v_bfe_i32 → 0 / ~0
+              const int sh = (rn & 1) * 16 + (lane >> 4) * 4;
+              const uint32_t w = mrow[rm][rn >> 1];
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                t[i] = __uint_as_float(__float_as_uint(t[i]) &
+                                       (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + i, 1));
             }
           }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float t = acc[rm][rn][i] * out_scale + bv[i] + prev[i];
-            if (!((mbits >> i) & 1u)) t = 0.f;
-            if (a.relu) t = fmaxf(t, 0.f);
-            h[i] = f2bf(t);
-            v[i] = bf2f(h[i]);
+          pk[rn][0] = cvt_pk_bf16(t[0], t[1]);
+          pk[rn][1] = cvt_pk_bf16(t[2], t[3]);
+          if (relu) {
+            pk[rn][0] = relu_pk_bf16(pk[rn][0]);
+            pk[rn][1] = relu_pk_bf16(pk[rn][1]);
           }
-          const bool v_ok = mv[rm] && n0 < a.Ng;
-          const uint32_t off = (uint32_t)(orow[rm] * a.ldc + n0) * 2u;
-          v2u32 pk;
-          pk[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-          pk[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-          if (!no_epi_mem) __builtin_amdgcn_raw_buffer_store_b64(pk, rout, v_ok ? off : OOB, 0, 0);
+          // ragged column tiles: columns ≥ Ng hold zeros (B rows fetched out of range) and must
+          // not be stored (they would land in the next row)
+          const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+          if (!no_epi_mem && !wide)
+            __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
           if constexpr (STATS) {
-            const float msk = v_ok ? 1.f : 0.f;
+            // statistics of the stored bf16 values; rows past M are zero unless a bias was added
+            const float rv = (!BIAS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
+            const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;
+            const float v2 = __uint_as_float(pk[rn][1] << 16) * rv, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rv;
+            s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
+            s_sq[rn][0] = fmaf(v0, v0, s_sq[rn][0]);
+            s_sq[rn][1] = fmaf(v1, v1, s_sq[rn][1]);
+            s_sq[rn][2] = fmaf(v2, v2, s_sq[rn][2]);
+            s_sq[rn][3] = fmaf(v3, v3, s_sq[rn][3]);
+          }
+        }
+        if (!no_epi_mem && wide) {
+          // 16-B stores: lanes l and l^16 (column groups 2j, 2j+1 of the same row) trade one
+          // 8-B half so each holds 8 consecutive columns of one 16-column block — an instruction
+          // then writes 16 rows × 64 B instead of 16 rows × 32 B (half the write requests:
+          // −20 % on the 1×1 dgrads, profiles/r02_dgrad_ablation.txt)
+          const bool odd = (lane >> 4) & 1;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              s_sum[rn][i] += msk * v[i];
-              s_sq[rn][i] += msk * v[i] * v[i];
+          for (int p = 0; p < RN; p += 2) {
+            const v2u32 send = odd ? pk[p] : pk[p + 1];
+            v2u32 recv;
+            recv[0] = (uint32_t)__shfl_xor((int)send[0], 16, 64);
+            recv[1] = (uint32_t)__shfl_xor((int)send[1], 16, 64);
+            v4u32 q;
+            if (odd) {
+              q[0] = recv[0]; q[1] = recv[1]; q[2] = pk[p + 1][0]; q[3] = pk[p + 1][1];
+            } else {
+              q[0] = pk[p][0]; q[1] = pk[p][1]; q[2] = recv[0]; q[3] = recv[1];
             }
+            const int col = T.bn0 + wn * TN + (odd ? p + 1 : p) * 16 + ((lane >> 4) & ~1) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + (uint32_t)col * 2u, 0, 0);
           }
         }
       }
@@ -597,8 +660,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   Tile CT = LT;
   int ckt = CT.kt0;
   int inflight = 0;  // steps issued and not yet fully computed
-  constexpr int E = RM * RN;  // epilogue stores per lane
-  bool epi = false;
+  constexpr int E = RM * RN;  // epilogue stores per lane (E / 2 with 16-B stores)
+  const bool half_e = wide_store && MODE != WGRAD;
+  // bit i: the epilogue of the i-th previous K-step issued its stores
+  uint32_t ehist = 0;
   int slot_load = 0, slot_comp = 0;
   auto issue_next = [&]() {
     if (!no_dma) issue_step(LT, lkt, slot_load);
@@ -607,25 +672,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     advance_load();
   };
   // Retire the DMAs of the step about to be read while `ahead` younger steps stay in flight,
-  // then make them visible to every wave.  vmcnt retires in issue order; right after an epilogue
-  // its E stores are the youngest VMEM ops.
+  // then make them visible to every wave.  vmcnt retires in issue order, so the count must
+  // include every younger VMEM op: the `ahead` DMA steps and the stores of each epilogue since
+  // the awaited step was issued (STAGES − 1 K-steps ago).  Counting only the last epilogue's
+  // stores forced the previous tile's stores to complete one K-step after they were issued —
+  // store-completion latency then paced the memory-bound (one-K-step) tiles.
   auto ring_wait_barrier = [&](int ahead) {
-    if (epi) {
-      if (STAGES >= 4 && ahead >= 2)
-        wait_vmcnt<2 * LPS + E>();
-      else if (ahead >= 1)
-        wait_vmcnt<LPS + E>();
-      else
-        wait_vmcnt<E>();
-    } else {
-      if (STAGES >= 4 && ahead >= 2)
-        wait_vmcnt<2 * LPS>();
-      else if (ahead >= 1)
-        wait_vmcnt<LPS>();
-      else
-        wait_vmcnt<0>();
-    }
-    epi = false;
+    const int ne = __builtin_popcount(ehist & ((1u << (STAGES - 1)) - 1u));
+    wait_ring<LPS, E, STAGES>(ahead, ne, half_e);
     if (!no_barrier) raw_barrier();
   };
 
@@ -637,6 +691,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     zero_acc();
     while (inflight > 0) {
       ring_wait_barrier(inflight - 1);
+      ehist <<= 1;
       if (lmore) issue_next();
       const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;
       i32x8 a8[RM], b8[RN];
@@ -657,7 +712,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       --inflight;
       if (ckt + 1 >= CT.kt1) {
         epilogue(CT);
-        epi = true;
+        ehist |= 1u;
         zero_acc();
         if (inflight > 0) {
           ++ct;
@@ -700,9 +755,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     }
     mfmas(f1a, f1b);
     --inflight;
+    ehist <<= 1;
     if (ckt + 1 >= CT.kt1) {
       epilogue(CT);
-      epi = true;
+      ehist |= 1u;
       zero_acc();
       if (inflight > 0) {
         ++ct;

@@ -24,6 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default=";".join(SHAPES))
+    ap.add_argument("--cfgs", action="store_true", help="also the 128x128 configurations")
+    ap.add_argument("--dbg", default="", help="extra TDL_CONV_DBG values for plain dgrad, e.g. 1,64,129")
     a = ap.parse_args()
     dev = torch.device("cuda")
     ext().conv_set_glds_mode(-1)
@@ -34,6 +36,7 @@ def main():
         dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
         w = torch.randn(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16) * 0.05
         prev = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
+        xin = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
         mask = torch.randint(0, 256, (N * H * H * Cin // 8,), device=dev, dtype=torch.uint8)
         flop = 2.0 * N * Ho * Wo * Cout * Cin * k * k
         xs = (N, H, H, Cin)
@@ -45,11 +48,34 @@ def main():
                                                           mask=mask)),
             ("plain nomfma", 2, lambda: C.conv_dgrad(dy, w, xs, g)),
             ("plain noepimem", 128, lambda: C.conv_dgrad(dy, w, xs, g)),
+            ("plain narrow", 256, lambda: C.conv_dgrad(dy, w, xs, g)),
+            ("acc+mask narrow", 256, lambda: C.conv_dgrad(dy, w, xs, g, out=prev, accumulate=True,
+                                                    mask=mask)),
+            ("fwd", 0, lambda: C.conv_fwd(xin, w, g)),
+            ("fwd narrow", 256, lambda: C.conv_fwd(xin, w, g)),
         ]
-        variants += [("plain cfg3x512", "cfg3", lambda: C.conv_dgrad(dy, w, xs, g)),
+        for d in [int(v) for v in a.dbg.split(",") if v]:
+            variants.append((f"plain dbg{d}", d, lambda: C.conv_dgrad(dy, w, xs, g)))
+        if not a.cfgs:
+            variants = [v for v in variants if v[0] != "plain nomfma"]
+        variants += [] if not a.cfgs else [("plain cfg3x512", "cfg3", lambda: C.conv_dgrad(dy, w, xs, g)),
                      ("acc+mask cfg3x512", "cfg3", lambda: C.conv_dgrad(dy, w, xs, g, out=prev,
                                                                      accumulate=True, mask=mask)),
                      ("plain cfg2x512", "cfg2", lambda: C.conv_dgrad(dy, w, xs, g))]
+        # the 8-B store epilogue (TDL_CONV_DBG=256) must write the same bits as the default 16-B one
+        for fn in (lambda: C.conv_dgrad(dy, w, xs, g), lambda: C.conv_fwd(xin, w, g)):
+            os.environ["TDL_CONV_DBG"] = "0"
+            r0 = fn().clone()
+            os.environ["TDL_CONV_DBG"] = "256"
+            r1 = fn()
+            assert torch.equal(r0, r1), ("store-width mismatch", shp)
+        p0 = prev.clone()
+        os.environ["TDL_CONV_DBG"] = "0"
+        C.conv_dgrad(dy, w, xs, g, out=p0, accumulate=True, mask=mask)
+        p1 = prev.clone()
+        os.environ["TDL_CONV_DBG"] = "256"
+        C.conv_dgrad(dy, w, xs, g, out=p1, accumulate=True, mask=mask)
+        assert torch.equal(p0, p1), ("store-width join mismatch", shp)
         res = {v[0]: [] for v in variants}
         for _ in range(a.rounds):
             for name, dbg, fn in variants:
@@ -63,10 +89,17 @@ def main():
                 os.environ["TDL_CONV_DBG"] = str(dbg)
                 fn()
                 torch.cuda.synchronize()
+                # 10 calls captured as one graph: device time only (the Python/host path of a
+                # call is ~100 us and would otherwise floor every fast variant)
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    for _ in range(10):
+                        fn()
+                gr.replay()
+                torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
                 e0.record()
-                for _ in range(10):
-                    fn()
+                gr.replay()
                 e1.record()
                 torch.cuda.synchronize()
                 res[name].append(e0.elapsed_time(e1) / 10 * 1e3)
