@@ -898,13 +898,15 @@ void conv_set_glds_mode(int mode) { g_glds_override = mode; }
 bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int mode = conv_glds_mode();
   if (mode == 0 || a0.C % 8 || a0.K % 8) return false;
-  // default selection (conv_bench, ResNet-50 b256): faster for ≥ 128 output channels; the
-  // 4-wave 256×64 configuration loses to the register-staged kernel
-  if (mode == 1 && ((long)a0.M < 4096 || a0.Ng < 128)) return false;
+  // default selection (ResNet-50 b256, tools/n64_configs.py): ≥ 128 output channels, and 1×1
+  // filters with 64 (the 8-wave 256×64 tiles: 35 vs 53 µs on 56×56 64→64); 3×3 filters with 64
+  // output channels stay on the register-staged kernel
+  const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
+  if (mode == 1 && ((long)a0.M < 4096 || (a0.Ng < 128 && !n64_1x1))) return false;
   ConvArgs a = a0;
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
-  int cfg = a.Ng <= 64 ? 1 : 0;
+  int cfg = a.Ng <= 64 ? 4 : 0;
   cfg = env_int("TDL_GLDS_CFG_FWD", cfg);
   const GCfg& g = cfg_of(cfg);
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
@@ -939,12 +941,15 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
     if (a0.C % 8 || a0.K % 128 || a0.dg_masked) return false;
   } else {
     if (mode == 0 || a0.C % 8 || a0.K % 8 || a0.dg_masked) return false;
-    if (mode == 1 && (Mmax_total < 4096 || a0.Ng < 128)) return false;
+    // 1×1 filters with 64 input channels (dx width): 8-wave 256×64 tiles (49 vs 88 µs on
+    // ResNet-50 56×56 64→64, tools/n64_configs.py)
+    const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
+    if (mode == 1 && (Mmax_total < 4096 || (a0.Ng < 128 && !n64_1x1))) return false;
   }
   ConvArgs a = a0;
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
-  int cfg = a.Ng <= 64 ? 1 : 0;
+  int cfg = a.Ng <= 64 ? (a.fp8 ? 1 : 4) : 0;
   if (!a.fp8) cfg = env_int("TDL_GLDS_CFG_DGRAD", cfg);
   const GCfg& g = cfg_of(cfg);
   a.cls_tile0[0] = 0;
