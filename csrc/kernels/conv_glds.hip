@@ -41,18 +41,23 @@ __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "me
 
 constexpr int vm63(int v) { return v < 63 ? v : 63; }  // 6-bit vmcnt field: a smaller count only waits longer
 
-// s_waitcnt vmcnt(LPS·ahead + (E or E/2)·ne) with the immediates the ring can need
+// s_waitcnt vmcnt(LPS·ahead + E·ne) with the immediates the ring can need.  The steady states
+// come first — long-K tiles (ahead = ST−2, no epilogue in the window) and one-K-step tiles (an
+// epilogue every step) — so the usual wait is two scalar compares, not a branch tree.
 template <int LPS, int E, int ST>
-__device__ __forceinline__ void wait_ring(int ahead, int ne, bool half) {
-#define TDL_W(A, NE)                                              \
-  if (ahead == A && ne == NE) {                                   \
-    if (half) wait_vmcnt<vm63(LPS * A + (E / 2) * NE)>();         \
-    else wait_vmcnt<vm63(LPS * A + E * NE)>();                    \
-    return;                                                       \
+__device__ __forceinline__ void wait_ring(int ahead, int ne) {
+  if (ahead == ST - 2) {
+    if (ne == 0) { wait_vmcnt<vm63(LPS * (ST - 2))>(); return; }
+    if (ne == ST - 1) { wait_vmcnt<vm63(LPS * (ST - 2) + E * (ST - 1))>(); return; }
+  }
+#define TDL_W(A, NE)                                  \
+  if (ahead == A && ne == NE) {                       \
+    wait_vmcnt<vm63(LPS * A + E * NE)>();             \
+    return;                                           \
   }
   TDL_W(0, 0) TDL_W(0, 1)
-  if constexpr (ST >= 3) { TDL_W(0, 2) TDL_W(1, 0) TDL_W(1, 1) TDL_W(1, 2) }
-  if constexpr (ST >= 4) { TDL_W(0, 3) TDL_W(1, 3) TDL_W(2, 0) TDL_W(2, 1) TDL_W(2, 2) TDL_W(2, 3) }
+  if constexpr (ST >= 3) { TDL_W(0, 2) TDL_W(1, 1) }
+  if constexpr (ST >= 4) { TDL_W(0, 3) TDL_W(1, 0) TDL_W(1, 2) TDL_W(1, 3) TDL_W(2, 1) TDL_W(2, 2) }
 #undef TDL_W
   wait_vmcnt<0>();
 }
@@ -378,7 +383,6 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   };
   const bool no_mfma = a.dbg & 2;
   const bool no_epi_mem = a.dbg & 128;  // timing-only: epilogue issues no global loads / stores
-  const bool wide_store = !(a.dbg & 256);  // 16-B epilogue stores (dbg 256: 8-B, for A/B)
   auto mfmas = [&](const bf16x8(&af)[RM], const bf16x8(&bfg)[RN]) {
     if (no_mfma) {
 #pragma unroll
@@ -487,7 +491,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
       }
       const bool relu = a.relu;
-      const bool wide = wide_store && cols_ok;
+      const bool wide = cols_ok;
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm) {
         v2u32 pk[RN];
@@ -540,25 +544,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           }
         }
         if (!no_epi_mem && wide) {
-          // 16-B stores: lanes l and l^16 (column groups 2j, 2j+1 of the same row) trade one
-          // 8-B half so each holds 8 consecutive columns of one 16-column block — an instruction
-          // then writes 16 rows × 64 B instead of 16 rows × 32 B (half the write requests:
-          // −20 % on the 1×1 dgrads, profiles/r02_dgrad_ablation.txt)
-          const bool odd = (lane >> 4) & 1;
+          // 16-B stores: v_permlane16_swap trades the odd 16-lane rows of fragment p with the
+          // even rows of fragment p+1, so lanes l and l^16 (column groups 2j, 2j+1 of one row)
+          // each end up with 8 consecutive columns — even lanes of block p, odd lanes of block
+          // p+1 — and an instruction writes 16 rows × 64 B instead of 16 rows × 32 B (half the
+          // write requests: −20 % on the 1×1 dgrads, profiles/r02_dgrad_ablation.txt)
+          const int g = lane >> 4;
+          const uint32_t lcol = (uint32_t)(T.bn0 + wn * TN + (g & 1) * 16 + (g & ~1) * 4) * 2u;
 #pragma unroll
           for (int p = 0; p < RN; p += 2) {
-            const v2u32 send = odd ? pk[p] : pk[p + 1];
-            v2u32 recv;
-            recv[0] = (uint32_t)__shfl_xor((int)send[0], 16, 64);
-            recv[1] = (uint32_t)__shfl_xor((int)send[1], 16, 64);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(pk[p][0], pk[p + 1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(pk[p][1], pk[p + 1][1], false, false);
             v4u32 q;
-            if (odd) {
-              q[0] = recv[0]; q[1] = recv[1]; q[2] = pk[p + 1][0]; q[3] = pk[p + 1][1];
-            } else {
-              q[0] = pk[p][0]; q[1] = pk[p][1]; q[2] = recv[0]; q[3] = recv[1];
-            }
-            const int col = T.bn0 + wn * TN + (odd ? p + 1 : p) * 16 + ((lane >> 4) & ~1) * 4;
-            __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + (uint32_t)col * 2u, 0, 0);
+            q[0] = s0[0]; q[1] = s1[0]; q[2] = s0[1]; q[3] = s1[1];
+            __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, 0);
           }
         }
       }
@@ -660,8 +659,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   Tile CT = LT;
   int ckt = CT.kt0;
   int inflight = 0;  // steps issued and not yet fully computed
-  constexpr int E = RM * RN;  // epilogue stores per lane (E / 2 with 16-B stores)
-  const bool half_e = wide_store && MODE != WGRAD;
+  // epilogue stores per lane: RM·RN/2 16-B stores (FWD / DGRAD; a ragged column tile issues
+  // RM·RN 8-B ones — more than counted, so its stores are only waited for sooner), RM·RN (WGRAD)
+  constexpr int E = MODE == WGRAD ? RM * RN : RM * RN / 2;
   // bit i: the epilogue of the i-th previous K-step issued its stores
   uint32_t ehist = 0;
   int slot_load = 0, slot_comp = 0;
@@ -679,7 +679,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   // store-completion latency then paced the memory-bound (one-K-step) tiles.
   auto ring_wait_barrier = [&](int ahead) {
     const int ne = __builtin_popcount(ehist & ((1u << (STAGES - 1)) - 1u));
-    wait_ring<LPS, E, STAGES>(ahead, ne, half_e);
+    wait_ring<LPS, E, STAGES>(ahead, ne);
     if (!no_barrier) raw_barrier();
   };
 
