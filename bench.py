@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=None,
-                    help="per-GPU batch (default 512 for the ImageNet models, 64/N for deeplab_ref)")
+                    help="per-GPU batch (default 1024 for the ImageNet models, 64/N for deeplab_ref)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
@@ -89,9 +89,10 @@ def main():
                "wgrad_side_stream": streams.enabled()}
         base = REF_DEEPLAB_2GPU / 2 * n
     else:
-        # 512 images per GPU by default (≈60 GB of the 288 GB HBM for ResNet-50): +6.5 % img/s over
-        # 256 on the same box (bigger GEMM M, fixed per-layer costs amortised; profiles/r02_*)
-        per_gpu = args.batch or 512
+        # 1024 images per GPU by default (ResNet-50: 49 GiB reserved of the 288 GB HBM): +2.9 %
+        # img/s over 512 and +15 % over 256 on the same box (bigger GEMM M, fixed per-layer costs
+        # amortised; profiles/r02_resnet50_batch_sweep.txt)
+        per_gpu = args.batch or 1024
         model = models.build(args.model, num_classes=1000)
         if args.fp8:
             models.enable_fp8(model)
