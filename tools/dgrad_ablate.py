@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Interleaved A/B timing of the LDS-DMA dgrad on ResNet-50 join shapes: plain overwrite, the
+"""Needs a TDL_CONV_ABLATION=1 build of the extension (TDL_CONV_ABLATION=1 python build_ext.py
+--force): production builds compile the TDL_CONV_DBG flags out.
+Interleaved A/B timing of the LDS-DMA dgrad on ResNet-50 join shapes: plain overwrite, the
 residual-join accumulate (dx += …), + the ReLU bit mask, and TDL_CONV_DBG ablations
 (2 = skip MFMA, 128 = epilogue without global loads / stores).
 
