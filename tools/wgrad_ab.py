@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
 
-# (H, Cin, Cout, k, stride, pad) of the conv whose weight gradient is taken (input H×H×Cin)
+# (H, Cin, Cout, k, stride, pad[, dilation]) of the conv whose weight gradient is taken (input H×H×Cin)
 SHAPES = ["56,64,64,3,1,1", "28,128,128,3,1,1", "56,128,128,3,2,1", "14,256,256,3,1,1",
           "28,256,256,3,2,1", "7,512,512,3,1,1", "14,512,512,3,2,1", "56,64,64,1,1,0",
           "56,256,64,1,1,0", "56,64,256,1,1,0"]
@@ -41,8 +41,10 @@ def main():
     names = a.variants.split(",")
     keys = sorted({k for _, e in variants.values() for k in e})
     for shp in a.shapes.split(";"):
-        H, Cin, Cout, k, s, p = [int(v) for v in shp.split(",")]
-        g = C.ConvGeom((s, s), (p, p, p, p), (1, 1))
+        v = [int(t) for t in shp.split(",")]
+        H, Cin, Cout, k, s, p = v[:6]
+        d = v[6] if len(v) > 6 else 1
+        g = C.ConvGeom((s, s), (p, p, p, p), (d, d))
         Ho, Wo = g.out_hw(H, H, k, k)
         x = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
         dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
