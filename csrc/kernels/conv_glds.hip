@@ -172,6 +172,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 
   // ---- per-tile load state ----
   int a_base[IA], a_p0[IA], a_p1[IA];  // KC A: pixel base / spatial origin; MC A: column
+  int a_row[IA];                       // FASTK FWD / DGRAD: row offset at tap (0, 0)
   int b_base[IB], b_f2[IB], b_f3[IB];  // KC B: row base; MC B: column / tap offsets
   // load-cursor position inside the filter (FWD: tap r, s and channel c0; DGRAD: class tap
   // th, tw and output channel c0) — FWD / DGRAD tiles always start at K-step 0
@@ -193,6 +194,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           a_p0[j] = -(1 << 28);
           a_p1[j] = 0;
         }
+        // FASTK: the row's element offset at tap (0, 0), channel chunk included — a K-step then
+        // adds one wave-uniform term (no per-DMA multiplies)
+        if constexpr (FASTK) a_row[j] = m < T.Mc ? a_base[j] + (a_p0[j] * a.W + a_p1[j]) * a.C + kc_lchunk(j) * EPC : 0;
       }
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
@@ -219,6 +223,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           a_p0[j] = -(1 << 28);
           a_p1[j] = -(1 << 28);
         }
+        if constexpr (FASTK) a_row[j] = m < T.Mc ? a_base[j] + (a_p0[j] * a.Wo + a_p1[j]) * a.K + kc_lchunk(j) * EPC : 0;
       }
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
@@ -264,6 +269,15 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       // pos_c0 … +63, advanced incrementally by advance_load (no division in the loop)
       const int tap_r = pos_r, tap_s = pos_s, c0 = pos_c0;
       const int kbase = kb;
+      if constexpr (FASTK) {
+        const int rdh = tap_r * a.dh, sdw = tap_s * a.dw;
+        const int tuni = (rdh * a.W + sdw) * a.C + c0;  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < IA; ++j) {
+          const bool v = (unsigned)(a_p0[j] + rdh) < (unsigned)a.H && (unsigned)(a_p1[j] + sdw) < (unsigned)a.W;
+          dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+        }
+      } else
 #pragma unroll
       for (int j = 0; j < IA; ++j) {
         const int lc = kc_lchunk(j);
@@ -294,6 +308,15 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       const int step_h = a.sh == 1 ? a.dh : 1, step_w = a.sw == 1 ? a.dw : 1;
       // FASTK (K % 64 == 0): one tap (pos_r = th, pos_s = tw) per K-step, channels pos_c0 … +63
       const int co0 = pos_c0;
+      if constexpr (FASTK) {
+        const int dth = pos_r * step_h, dtw = pos_s * step_w;
+        const int tuni = co0 - (dth * a.Wo + dtw) * a.K;  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < IA; ++j) {
+          const bool v = (unsigned)(a_p0[j] - dth) < (unsigned)a.Ho && (unsigned)(a_p1[j] - dtw) < (unsigned)a.Wo;
+          dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+        }
+      } else
 #pragma unroll
       for (int j = 0; j < IA; ++j) {
         const int lc = kc_lchunk(j);
