@@ -202,6 +202,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       for (int j = 0; j < IB; ++j) {
         const int n = T.bn0 + kc_row(j);
         b_base[j] = n < a.Ng ? n * a.Kg : -1;
+        if constexpr (FASTK) b_f2[j] = b_base[j] + kc_lchunk(j) * EPC;
       }
     } else if constexpr (MODE == DGRAD) {
       const int c = T.cls;
@@ -233,6 +234,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         } else {
           const int ci = T.bn0 + mc_col(j, BN, mc_krow(j, BN));
           b_base[j] = ci < a.Ng ? ci : -1;
+          // FASTK: W [K][R][S][C] row co0 + krow of tap (r, s) = this part + a wave-uniform part
+          if constexpr (FASTK) b_f2[j] = mc_krow(j, BN) * a.R * a.S * a.C + b_base[j];
         }
       }
     } else {  // WGRAD
@@ -296,6 +299,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         const uint32_t off = (uint32_t)(a_base[j] + (hi * a.W + wi) * a.C + c) * (uint32_t)ESZ;
         dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
       }
+      if constexpr (FASTK) {  // every K-step of a FASTK tile is inside Kg
+#pragma unroll
+        for (int j = 0; j < IB; ++j)
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, b_base[j] >= 0 ? (uint32_t)(b_f2[j] + kbase) * (uint32_t)ESZ : OOB);
+      } else
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
         const int k = kbase + kc_lchunk(j) * EPC;
@@ -345,6 +353,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           dma16(rb_src, Bs + (j * NW + wid) * 1024,
                 v ? (uint32_t)(b_base[j] + toff + kc_lchunk(j) * EPC) : OOB);
         }
+      } else if constexpr (FASTK) {
+        const int r = r0 + a.sh * pos_r, s = s0 + a.sw * pos_s;
+        const int buni = (co0 * a.R * a.S + r * a.S + s) * a.C;  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < IB; ++j)
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, b_base[j] >= 0 ? (uint32_t)(b_f2[j] + buni) * 2u : OOB);
       } else
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
