@@ -191,8 +191,21 @@ __device__ __forceinline__ long out_row(const ConvArgs& a, const Tile& T, int m)
   }
 }
 
-// out_row with the prepared fast divisions and 32-bit arithmetic (LDS-DMA kernel epilogue; no
-// dg_masked classes there)
+// magic-number divisors of the geometry (host side; every conv kernel's row / tap arithmetic)
+inline void set_fastdivs(ConvArgs& a) {
+  a.fd_sh = make_fastdiv((uint32_t)std::max(1, a.sh));
+  a.fd_sw = make_fastdiv((uint32_t)std::max(1, a.sw));
+  for (int c = 0; c < MAX_DG_CLASSES; ++c) {
+    a.cls_fdHW[c] = make_fastdiv((uint32_t)std::max(1, a.cls_Hc[c] * a.cls_Wc[c]));
+    a.cls_fdW[c] = make_fastdiv((uint32_t)std::max(1, a.cls_Wc[c]));
+  }
+  a.fd_HoWo = make_fastdiv((uint32_t)std::max(1, a.Ho * a.Wo));
+  a.fd_Wo = make_fastdiv((uint32_t)std::max(1, a.Wo));
+  a.fd_C = make_fastdiv((uint32_t)std::max(1, a.C));
+  a.fd_S = make_fastdiv((uint32_t)std::max(1, a.S));
+}
+
+// out_row with the prepared fast divisions (set_fastdivs) and 32-bit arithmetic
 template <int MODE>
 __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& T, int m) {
   if constexpr (MODE == DGRAD) {
@@ -202,8 +215,9 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
     const uint32_t rem = (uint32_t)m - n * Hc * Wc;
     const uint32_t i = fdiv(rem, a.cls_fdW[c]);
     const uint32_t j = rem - i * Wc;
-    const uint32_t h = (uint32_t)a.cls_a[c] + (uint32_t)a.sh * i;
-    const uint32_t w = (uint32_t)a.cls_b[c] + (uint32_t)a.sw * j;
+    const uint32_t psh = a.dg_masked ? 1u : (uint32_t)a.sh, psw = a.dg_masked ? 1u : (uint32_t)a.sw;
+    const uint32_t h = (uint32_t)a.cls_a[c] + psh * i;
+    const uint32_t w = (uint32_t)a.cls_b[c] + psw * j;
     return (n * (uint32_t)a.H + h) * (uint32_t)a.W + w;
   } else {
     return (uint32_t)m;

@@ -878,18 +878,6 @@ const GCfg& cfg_of(int c) {
   }
 }
 
-void set_fastdivs(ConvArgs& a) {
-  a.fd_sh = make_fastdiv((uint32_t)std::max(1, a.sh));
-  a.fd_sw = make_fastdiv((uint32_t)std::max(1, a.sw));
-  for (int c = 0; c < MAX_DG_CLASSES; ++c) {
-    a.cls_fdHW[c] = make_fastdiv((uint32_t)std::max(1, a.cls_Hc[c] * a.cls_Wc[c]));
-    a.cls_fdW[c] = make_fastdiv((uint32_t)std::max(1, a.cls_Wc[c]));
-  }
-  a.fd_HoWo = make_fastdiv((uint32_t)std::max(1, a.Ho * a.Wo));
-  a.fd_Wo = make_fastdiv((uint32_t)std::max(1, a.Wo));
-  a.fd_C = make_fastdiv((uint32_t)std::max(1, a.C));
-  a.fd_S = make_fastdiv((uint32_t)std::max(1, a.S));
-}
 
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
