@@ -277,7 +277,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         const int tuni = (rdh * a.W + sdw) * a.C + c0;  // wave-uniform
 #pragma unroll
         for (int j = 0; j < IA; ++j) {
-          const bool v = (unsigned)(a_p0[j] + rdh) < (unsigned)a.H && (unsigned)(a_p1[j] + sdw) < (unsigned)a.W;
+          bool v = (unsigned)(a_p0[j] + rdh) < (unsigned)a.H && (unsigned)(a_p1[j] + sdw) < (unsigned)a.W;
+          if (a.kragged) v = v && c0 + kc_lchunk(j) * EPC < a.C;
           dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
         }
       } else
@@ -299,10 +300,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         const uint32_t off = (uint32_t)(a_base[j] + (hi * a.W + wi) * a.C + c) * (uint32_t)ESZ;
         dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
       }
-      if constexpr (FASTK) {  // every K-step of a FASTK tile is inside Kg
+      if constexpr (FASTK) {  // every K-step of a FASTK tile is inside Kg (ragged: its chunks)
 #pragma unroll
-        for (int j = 0; j < IB; ++j)
-          dma16(rb_src, Bs + (j * NW + wid) * 1024, b_base[j] >= 0 ? (uint32_t)(b_f2[j] + kbase) * (uint32_t)ESZ : OOB);
+        for (int j = 0; j < IB; ++j) {
+          bool v = b_base[j] >= 0;
+          if (a.kragged) v = v && kbase + kc_lchunk(j) * EPC < a.Kg;
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_f2[j] + kbase) * (uint32_t)ESZ : OOB);
+        }
       } else
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
@@ -321,7 +325,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         const int tuni = co0 - (dth * a.Wo + dtw) * a.K;  // wave-uniform
 #pragma unroll
         for (int j = 0; j < IA; ++j) {
-          const bool v = (unsigned)(a_p0[j] - dth) < (unsigned)a.Ho && (unsigned)(a_p1[j] - dtw) < (unsigned)a.Wo;
+          bool v = (unsigned)(a_p0[j] - dth) < (unsigned)a.Ho && (unsigned)(a_p1[j] - dtw) < (unsigned)a.Wo;
+          if (a.kragged) v = v && co0 + kc_lchunk(j) * EPC < a.K;
           dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
         }
       } else
@@ -357,8 +362,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         const int r = r0 + a.sh * pos_r, s = s0 + a.sw * pos_s;
         const int buni = (co0 * a.R * a.S + r * a.S + s) * a.C;  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < IB; ++j)
-          dma16(rb_src, Bs + (j * NW + wid) * 1024, b_base[j] >= 0 ? (uint32_t)(b_f2[j] + buni) * 2u : OOB);
+        for (int j = 0; j < IB; ++j) {
+          bool v = b_base[j] >= 0;
+          if (a.kragged) v = v && co0 + mc_krow(j, BN) < a.K;
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_f2[j] + buni) * 2u : OOB);
+        }
       } else
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
@@ -955,7 +963,10 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int blocks = (int)(groups * ntn);
   a.cls_tile0[0] = 0;
   a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
-  const bool fk = a.C % 64 == 0;
+  // FASTK: a K-step is one filter tap × 64 channels; 1×1 filters with C % 64 != 0 take it too,
+  // with the row's last channel chunk range-checked (Xception's 728-channel pointwise convs)
+  a.kragged = a.C % 64 != 0 && a.R * a.S == 1;
+  const bool fk = a.C % 64 == 0 || a.kragged;
   const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
 #define TDL_G(ST, BI, FK) launch_gcfg<FWD, ST, BI, FK>(a, cfg, blocks, st)
   if (fk) {
@@ -1003,8 +1014,10 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
       launch_g<DGRAD, 256, 64, 4, 1, 3, false, false, true, true>(a, blocks, st);
     else
       launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, true, true>(a, blocks, st);
-  } else if (a.K % 64 == 0)
+  } else if (a.K % 64 == 0 || (a.R * a.S == 1 && a.ncls == 1)) {
+    a.kragged = a.K % 64 != 0;
     launch_gcfg<DGRAD, false, false, true>(a, cfg, blocks, st);
+  }
   else
     launch_gcfg<DGRAD, false, false, false>(a, cfg, blocks, st);
   return true;

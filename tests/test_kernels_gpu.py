@@ -51,6 +51,8 @@ CONV_SHAPES = [
     (8, 29, 27, 128, 192, 3, 3, 2, (1, 1, 1, 1), 1),    # ragged rows / cols, 4 parity classes
     (8, 20, 20, 40, 24, 3, 3, 1, (1, 1, 1, 1), 1),      # C, K % 64 != 0 (tap-crossing K-steps)
     (4, 33, 33, 256, 512, 1, 1, 2, (0, 0, 0, 0), 1),    # 1x1 s2, zero parity classes
+    (2, 15, 15, 728, 200, 1, 1, 1, (0, 0, 0, 0), 1),    # 1x1, C and K % 64 != 0 (ragged FASTK)
+    (2, 16, 16, 200, 328, 1, 1, 2, (0, 0, 0, 0), 1),    # 1x1 s2, ragged FASTK dgrad class
 ]
 
 CONV_IMPLS = ["reg", "glds"]
