@@ -954,6 +954,10 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   cfg = env_int("TDL_GLDS_CFG_FWD", cfg);
   const GCfg& g = cfg_of(cfg);
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
+  // fewer than half a tile per CU: the register-staged kernel's smaller tiles and two workgroups
+  // per CU win (reference DeepLab preset, 13×13×1024→256 at batch 64: 20.6 vs 25.0 µs;
+  // tools/cfg_ab.py)
+  if (mode == 1 && ntm * ntn < 128) return false;
   a.ncls = 1;
   a.splits = 1;
   // FWD tile order (tile_of): a workgroup owns one column tile and tpb consecutive row tiles
@@ -1006,6 +1010,7 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
   }
   const long tiles = a.cls_tile0[a.ncls];
   if (tiles == 0) return true;
+  if (mode == 1 && !a.fp8 && tiles < 128) return false;  // see conv_fwd_glds
   a.tpb = persistent_tpb(tiles);
   a.splits = 1;
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
