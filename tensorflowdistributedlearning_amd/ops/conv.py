@@ -293,7 +293,7 @@ class _Conv2dFn(torch.autograd.Function):
         side = streams.side(dy.device) if (weight.requires_grad or
                                             (bias is not None and bias.requires_grad)) else None
         if side is not None and streams.EARLY_WAIT:  # dy is ready: wgrad may overlap this dgrad
-            side.wait_stream(torch.cuda.current_stream(dy.device))
+            side.wait_stream(streams.current(dy.device))
         if ctx.needs_input_grad[0]:
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
                 compute_weight(weight, dy.dtype)
@@ -326,8 +326,8 @@ class _Conv2dFn(torch.autograd.Function):
             _conv_param_grads(ctx, dy, x, weight, bias)
         else:  # weight / bias gradients on the side stream, concurrent with the dgrad chain
             if not streams.EARLY_WAIT:
-                side.wait_stream(torch.cuda.current_stream(dy.device))
-            with torch.cuda.stream(side):
+                side.wait_stream(streams.current(dy.device))
+            with streams.on(side):
                 _conv_param_grads(ctx, dy, x, weight, bias)
             streams.keep_alive(dy.device, dy, x)  # until the next join (no record_stream)
             streams.join_at_backward_end(dy.device)  # backward() returns joined

@@ -32,12 +32,46 @@ _KEEP: dict = {}
 KEEP_ALIVE = os.environ.get("TDL_SIDE_KEEPALIVE", "1") == "1"
 
 
+def current(device):
+    """``torch.cuda.current_stream(device)`` without its Python-level device normalisation (this
+    runs several times per conv backward; the public helper cost ≈5 µs per call, ≈1.4 ms of host
+    time per step of the reference DeepLab preset — tools/host_overhead.py)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    sid, di, dt = torch._C._cuda_getCurrentStream(idx)
+    return torch.cuda.Stream(stream_id=sid, device_index=di, device_type=dt)
+
+
+def capturing() -> bool:
+    """Is the current stream capturing a HIP graph (raw query, no lazy-init wrapper)?"""
+    return torch._C._cuda_isCurrentStreamCapturing()
+
+
+class on:
+    """``with on(stream):`` — make ``stream`` current on its device, restore the previous one on
+    exit (a lean ``torch.cuda.stream`` for the per-conv side-stream switch)."""
+    __slots__ = ("s", "prev")
+
+    def __init__(self, stream):
+        self.s = stream
+
+    def __enter__(self):
+        self.prev = torch._C._cuda_getCurrentStream(self.s.device_index)
+        torch._C._cuda_setStream(stream_id=self.s.stream_id, device_index=self.s.device_index,
+                                 device_type=self.s.device_type)
+        return self.s
+
+    def __exit__(self, *exc):
+        sid, di, dt = self.prev
+        torch._C._cuda_setStream(stream_id=sid, device_index=di, device_type=dt)
+        return False
+
+
 def keep_alive(device, *tensors):
     """Keep ``tensors`` (read by side-stream work; allocated on the caller's stream) alive until
     the caller's stream next joins the side stream (:func:`join`)."""
     if KEEP_ALIVE:
         dev = torch.device(device)
-        cur = torch.cuda.current_stream(dev)
+        cur = current(dev)
         _KEEP.setdefault((dev, cur.stream_id), []).extend(tensors)
     else:
         s = _SIDE[torch.device(device)]
@@ -65,14 +99,14 @@ def side(device):
     back."""
     if not _ENABLED or device.type != "cuda":
         return None
-    if torch.cuda.is_current_stream_capturing():
+    if capturing():
         if not IN_GRAPH:
             return None
         _FORKED.add(torch.device(device))
     s = _SIDE.get(device)
     if s is None:
         s = _SIDE[device] = torch.cuda.Stream(device=device)
-    cur = torch.cuda.current_stream(device)
+    cur = current(device)
     if cur != s:
         _ORIGIN[torch.device(device)] = cur
     return s
@@ -86,7 +120,7 @@ def is_side(stream, device) -> bool:
 
 def origin(device):
     """The stream that forks work onto the side stream (the compute / capturing stream)."""
-    return _ORIGIN.get(torch.device(device), torch.cuda.current_stream(device))
+    return _ORIGIN.get(torch.device(device), current(torch.device(device)))
 
 
 def end_capture(capture_stream=None):
@@ -133,13 +167,13 @@ def join(device=None):
     """Make the current stream wait for all work queued on the side stream(s).  While a HIP graph
     is being captured only side streams forked into that capture are joined (a wait on an event
     of a stream outside the capture must not enter the graph)."""
-    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    cap = torch.cuda.is_available() and capturing()
     for dev, s in _SIDE.items():
         if device is None or dev == torch.device(device):
-            if capturing and dev not in _FORKED:
+            if cap and dev not in _FORKED:
                 continue
-            cur = torch.cuda.current_stream(dev)
+            cur = current(dev)
             cur.wait_stream(s)
-            if cur != s and not capturing:
+            if cur != s and not cap:
                 # everything queued on `cur` from here on runs after the side stream's reads
                 _KEEP.pop((dev, cur.stream_id), None)
