@@ -302,124 +302,11 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
 
   // lane holds C[m = bm0 + wm*TM + rm*16 + (lane&15)][n = bn0 + wn*TN + rn*16 + (lane>>4)*4 + i]
   //
-  // bf16 epilogue for vector-aligned outputs (Ng, ldc % 4 == 0) — the same lean form as the
-  // LDS-DMA kernel's (conv_glds.hip): 32-bit row offsets with invalid rows pushed out of the
-  // buffer, packed conversions, packed-int16 ReLU, the join / mask under uniform branches,
-  // 16-B stores built by v_permlane16_swap
+  // bf16 epilogue for vector-aligned outputs (Ng, ldc % 4 == 0): the shared lean form
+  // (conv_common.h store_tile_bf16)
   auto lean_epilogue = [&](const Tile& T) {
-    uint32_t rbase[RM];
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-      rbase[rm] = m < T.Mc ? out_row_fast<MODE>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
-    }
-    const int c0 = T.bn0 + wn * TN + (lane >> 4) * 4;
-    const bool cols_ok = T.bn0 + wn * TN + TN <= a.Ng;
-    v4u32 bias_v[RN];
-    if constexpr (BIAS) {
-      const rsrc_t rbias = make_rsrc(a.bias, (uint32_t)a.Ng * 4u);
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) {
-        const int n0 = c0 + rn * 16;
-        bias_v[rn] = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
-      }
-    }
-    bool join_prev = false, join_mask = false;
-    if constexpr (MODE == DGRAD) {
-      join_prev = a.beta;
-      join_mask = a.mask;
-    }
-    uint32_t mrow[RM][2];
-    v2u32 pv[RM][RN];
-    if constexpr (MODE == DGRAD) {
-      if (join_mask) {
-        const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
-#pragma unroll
-        for (int rm = 0; rm < RM; ++rm) {
-          const uint32_t boff = (rbase[rm] / 2u + (uint32_t)(T.bn0 + wn * TN)) >> 3;
-          const uint32_t o = rbase[rm] != ROW_OOB ? boff : OOB;
-          if constexpr (TN == 64) {
-            const v2u32 m2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, o, 0, 0);
-            mrow[rm][0] = m2[0];
-            mrow[rm][1] = m2[1];
-          } else {
-            static_assert(TN == 32, "mask slab of 4 or 8 bytes");
-            mrow[rm][0] = __builtin_amdgcn_raw_buffer_load_b32(rmask, o, 0, 0);
-            mrow[rm][1] = 0;
-          }
-        }
-      }
-      if (join_prev) {
-#pragma unroll
-        for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-          for (int rn = 0; rn < RN; ++rn) {
-            const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-            pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
-                rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-          }
-      }
-    }
-    const bool relu = a.relu;
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      v2u32 pk[RN];
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) {
-        f32x4 t = acc[rm][rn];
-        if constexpr (BIAS) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) t[i] += __uint_as_float(bias_v[rn][i]);
-        }
-        if constexpr (MODE == DGRAD) {
-          if (join_prev) {
-            t[0] += __uint_as_float(pv[rm][rn][0] << 16);
-            t[1] += __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
-            t[2] += __uint_as_float(pv[rm][rn][1] << 16);
-            t[3] += __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
-          }
-          if (join_mask) {
-            const int sh = (rn & 1) * 16 + (lane >> 4) * 4;
-            const uint32_t w = mrow[rm][rn >> 1];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              t[i] = __uint_as_float(__float_as_uint(t[i]) &
-                                     (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + i, 1));
-          }
-        }
-        pk[rn][0] = cvt_pk_bf16(t[0], t[1]);
-        pk[rn][1] = cvt_pk_bf16(t[2], t[3]);
-        if (relu) {
-          pk[rn][0] = relu_pk_bf16(pk[rn][0]);
-          pk[rn][1] = relu_pk_bf16(pk[rn][1]);
-        }
-        const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-        if (!cols_ok)
-          __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-        if constexpr (STATS) {
-          const float rv = (!BIAS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
-          const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;
-          const float v2 = __uint_as_float(pk[rn][1] << 16) * rv, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rv;
-          s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
-          s_sq[rn][0] = fmaf(v0, v0, s_sq[rn][0]);
-          s_sq[rn][1] = fmaf(v1, v1, s_sq[rn][1]);
-          s_sq[rn][2] = fmaf(v2, v2, s_sq[rn][2]);
-          s_sq[rn][3] = fmaf(v3, v3, s_sq[rn][3]);
-        }
-      }
-      if (cols_ok) {
-        const int g = lane >> 4;
-        const uint32_t lcol = (uint32_t)(T.bn0 + wn * TN + (g & 1) * 16 + (g & ~1) * 4) * 2u;
-#pragma unroll
-        for (int p = 0; p < RN; p += 2) {
-          const auto s0 = __builtin_amdgcn_permlane16_swap(pk[p][0], pk[p + 1][0], false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(pk[p][1], pk[p + 1][1], false, false);
-          v4u32 q;
-          q[0] = s0[0]; q[1] = s1[0]; q[2] = s0[1]; q[3] = s1[1];
-          __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, 0);
-        }
-      }
-    }
+    store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, false>(a, T, acc, wm, wn, lane, rout, 1.f,
+                                                             false, s_sum, s_sq);
   };
 
   auto epilogue = [&](const Tile& T) {

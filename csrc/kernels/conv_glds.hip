@@ -479,144 +479,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
       }
     } else {
-      // Row byte offsets are 32-bit with invalid rows pushed past the buffer (ROW_OOB): a
-      // fragment's store offset is then row base + a compile-time constant.  Rows past the GEMM's
-      // M hold zeros (their A rows were fetched out of range), so the statistics need no mask.
-      uint32_t rbase[RM];
-#pragma unroll
-      for (int rm = 0; rm < RM; ++rm) {
-        const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-        rbase[rm] = m < T.Mc ? out_row_fast<MODE>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
-      }
-      const int c0 = T.bn0 + wn * TN + (lane >> 4) * 4;  // this lane's column in fragment rn = 0
-      const bool cols_ok = T.bn0 + wn * TN + TN <= a.Ng;   // wave-uniform: no ragged columns
-      // Per fragment: two v_cvt_pk_bf16_f32, the ReLU as one packed int16 max per pair (a bf16
-      // is negative iff its int16 pattern is), one 16-B store per fragment pair.  The earlier
-      // per-element epilogue (64-bit row math, integer divisions, per-fragment validity selects,
-      // runtime mask / join / ReLU tests on every value) cost ≈1,200 VALU instructions per wave
-      // per tile — at 4 cycles per wave64 VALU op that, not HBM, paced the 1–4-K-step tiles of
-      // 1×1 convs (tools/dgrad_ablate.py: 129 µs for a 1×1 dgrad with no memory traffic).
-      v4u32 bias_v[RN];
-      if constexpr (BIAS) {
-        const rsrc_t rbias = make_rsrc(a.bias, (uint32_t)a.Ng * 4u);
-#pragma unroll
-        for (int rn = 0; rn < RN; ++rn) {
-          const int n0 = c0 + rn * 16;
-          bias_v[rn] = __builtin_amdgcn_raw_buffer_load_b128(rbias, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
-        }
-      }
-      // DGRAD residual join (dx += this dgrad: the previous dx is read back) and ReLU bit mask
-      // (pre-masked join: a row's TN mask bits of the wave's columns in one 4- / 8-byte load,
-      // ldc % 64 == 0).  Every load is issued before any is used — one memory round trip per
-      // tile; interleaved load → use made hipcc wait vmcnt(0) per fragment, draining the next
-      // tile's in-flight operand DMA each time.
-      bool join_prev = false, join_mask = false;
-      if constexpr (MODE == DGRAD) {
-        join_prev = a.beta && !no_epi_mem;
-        join_mask = a.mask && !no_epi_mem;
-      }
-      uint32_t mrow[RM][2];
-      v2u32 pv[RM][RN];
-      if constexpr (MODE == DGRAD) {
-        if (join_mask) {
-          const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
-#pragma unroll
-          for (int rm = 0; rm < RM; ++rm) {
-            const uint32_t boff = (rbase[rm] / 2u + (uint32_t)(T.bn0 + wn * TN)) >> 3;
-            const uint32_t o = rbase[rm] != ROW_OOB ? boff : OOB;
-            if constexpr (TN == 64) {
-              const v2u32 m2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, o, 0, 0);
-              mrow[rm][0] = m2[0];
-              mrow[rm][1] = m2[1];
-            } else {
-              static_assert(TN == 32, "mask slab of 4 or 8 bytes");
-              mrow[rm][0] = __builtin_amdgcn_raw_buffer_load_b32(rmask, o, 0, 0);
-              mrow[rm][1] = 0;
-            }
-          }
-        }
-        if (join_prev) {
-#pragma unroll
-          for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-            for (int rn = 0; rn < RN; ++rn) {
-              const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-              pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
-                  rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-            }
-        }
-      }
-      const bool relu = a.relu;
-      const bool wide = cols_ok;
-#pragma unroll
-      for (int rm = 0; rm < RM; ++rm) {
-        v2u32 pk[RN];
-#pragma unroll
-        for (int rn = 0; rn < RN; ++rn) {
-          f32x4 t = acc[rm][rn];
-          if constexpr (FP8) t = t * out_scale;
-          if constexpr (BIAS) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) t[i] += __uint_as_float(bias_v[rn][i]);
-          }
-          if constexpr (MODE == DGRAD) {
-            if (join_prev) {
-              t[0] += __uint_as_float(pv[rm][rn][0] << 16);
-              t[1] += __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
-              t[2] += __uint_as_float(pv[rm][rn][1] << 16);
-              t[3] += __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
-            }
-            if (join_mask) {
-              // bit (rn·16 + group·4 + i) of the wave's TN-column slab; v_bfe_i32 → 0 / ~0
-              const int sh = (rn & 1) * 16 + (lane >> 4) * 4;
-              const uint32_t w = mrow[rm][rn >> 1];
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                t[i] = __uint_as_float(__float_as_uint(t[i]) &
-                                       (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + i, 1));
-            }
-          }
-          pk[rn][0] = cvt_pk_bf16(t[0], t[1]);
-          pk[rn][1] = cvt_pk_bf16(t[2], t[3]);
-          if (relu) {
-            pk[rn][0] = relu_pk_bf16(pk[rn][0]);
-            pk[rn][1] = relu_pk_bf16(pk[rn][1]);
-          }
-          // ragged column tiles: columns ≥ Ng hold zeros (B rows fetched out of range) and must
-          // not be stored (they would land in the next row)
-          const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-          if (!no_epi_mem && !wide)
-            __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-          if constexpr (STATS) {
-            // statistics of the stored bf16 values; rows past M are zero unless a bias was added
-            const float rv = (!BIAS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
-            const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;
-            const float v2 = __uint_as_float(pk[rn][1] << 16) * rv, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rv;
-            s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
-            s_sq[rn][0] = fmaf(v0, v0, s_sq[rn][0]);
-            s_sq[rn][1] = fmaf(v1, v1, s_sq[rn][1]);
-            s_sq[rn][2] = fmaf(v2, v2, s_sq[rn][2]);
-            s_sq[rn][3] = fmaf(v3, v3, s_sq[rn][3]);
-          }
-        }
-        if (!no_epi_mem && wide) {
-          // 16-B stores: v_permlane16_swap trades the odd 16-lane rows of fragment p with the
-          // even rows of fragment p+1, so lanes l and l^16 (column groups 2j, 2j+1 of one row)
-          // each end up with 8 consecutive columns — even lanes of block p, odd lanes of block
-          // p+1 — and an instruction writes 16 rows × 64 B instead of 16 rows × 32 B (half the
-          // write requests: −20 % on the 1×1 dgrads, profiles/r02_dgrad_ablation.txt)
-          const int g = lane >> 4;
-          const uint32_t lcol = (uint32_t)(T.bn0 + wn * TN + (g & 1) * 16 + (g & ~1) * 4) * 2u;
-#pragma unroll
-          for (int p = 0; p < RN; p += 2) {
-            const auto s0 = __builtin_amdgcn_permlane16_swap(pk[p][0], pk[p + 1][0], false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(pk[p][1], pk[p + 1][1], false, false);
-            v4u32 q;
-            q[0] = s0[0]; q[1] = s1[0]; q[2] = s0[1]; q[3] = s1[1];
-            __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, 0);
-          }
-        }
-      }
+      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8>(a, T, acc, wm, wn, lane, rout, out_scale,
+                                                             no_epi_mem, s_sum, s_sq);
     }
   };
 

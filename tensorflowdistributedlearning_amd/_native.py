@@ -36,7 +36,9 @@ def load():
         return _EXT
     if _EXT_ERR is not None:
         raise _EXT_ERR
-    so = _find_so("_C")
+    # TDL_EXT_SO: load another build of the same extension (same-box A/B of kernel changes,
+    # tools/ab_build.sh); the module name stays tensorflowdistributedlearning_amd._C
+    so = os.environ.get("TDL_EXT_SO") or _find_so("_C")
     if so is None:
         _EXT_ERR = ImportError(
             "native extension _C.so not built; run `python build_ext.py` (hipcc --offload-arch=gfx950)")
