@@ -206,7 +206,9 @@ inline void set_fastdivs(ConvArgs& a) {
 }
 
 // out_row with the prepared fast divisions (set_fastdivs) and 32-bit arithmetic
-template <int MODE>
+// DGM: the kernel may run dg_masked problems (the register-staged kernel; the LDS-DMA kernel
+// never does, and the extra uniform select cost it a scratch spill)
+template <int MODE, bool DGM = false>
 __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& T, int m) {
   if constexpr (MODE == DGRAD) {
     const int c = T.cls;
@@ -215,7 +217,8 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
     const uint32_t rem = (uint32_t)m - n * Hc * Wc;
     const uint32_t i = fdiv(rem, a.cls_fdW[c]);
     const uint32_t j = rem - i * Wc;
-    const uint32_t psh = a.dg_masked ? 1u : (uint32_t)a.sh, psw = a.dg_masked ? 1u : (uint32_t)a.sw;
+    const uint32_t psh = DGM && a.dg_masked ? 1u : (uint32_t)a.sh;
+    const uint32_t psw = DGM && a.dg_masked ? 1u : (uint32_t)a.sw;
     const uint32_t h = (uint32_t)a.cls_a[c] + psh * i;
     const uint32_t w = (uint32_t)a.cls_b[c] + psw * j;
     return (n * (uint32_t)a.H + h) * (uint32_t)a.W + w;
@@ -231,7 +234,7 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 // lane holds C[m = bm0 + wm*TM + rm*16 + (lane&15)][n = bn0 + wn*TN + rn*16 + (lane>>4)*4 + i].
 // SCALE: multiply by `scale` first (fp8 GEMMs: the per-tensor operand scales); `no_mem`: issue no
 // loads / stores (timing ablation).
-template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE>
+template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
@@ -243,7 +246,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
 #pragma unroll
   for (int rm = 0; rm < RM; ++rm) {
     const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-    rbase[rm] = m < T.Mc ? out_row_fast<MODE>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
+    rbase[rm] = m < T.Mc ? out_row_fast<MODE, DGM>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
   }
   const int c0 = T.bn0 + wn * TN + (lane >> 4) * 4;  // this lane's column in fragment rn = 0
   const bool cols_ok = T.bn0 + wn * TN + TN <= a.Ng;   // wave-uniform: no ragged columns

@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
   // bf16 epilogue for vector-aligned outputs (Ng, ldc % 4 == 0): the shared lean form
   // (conv_common.h store_tile_bf16)
   auto lean_epilogue = [&](const Tile& T) {
-    store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, false>(a, T, acc, wm, wn, lane, rout, 1.f,
+    store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, false, true>(a, T, acc, wm, wn, lane, rout, 1.f,
                                                              false, s_sum, s_sq);
   };
 

@@ -105,9 +105,13 @@ __device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_base, 16, voff, 0, 0, 0);
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, bool FASTK,
+template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, int FK,
           bool FP8 = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  // FK: 0 = generic K decomposition; 1 = FASTK (a K-step is one filter tap × 64 (fp8: 128)
+  // channels); 2 = FASTK on a 1×1 filter whose channel count is not a multiple of 64 — the row's
+  // last channel chunk is range-checked (compile time: a runtime test per DMA cost 10–20 %)
+  constexpr bool FASTK = FK != 0, RAG = FK == 2;
   // FP8: operands are OCP fp8 bytes, a K-step is 128 deep (one 128-B LDS row per tile row, as
   // for bf16), fragments are 32 B and feed v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0
   // block scales; the per-tensor scales are applied in the epilogue.  FWD: x e4m3 × W e4m3.
@@ -278,7 +282,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
         for (int j = 0; j < IA; ++j) {
           bool v = (unsigned)(a_p0[j] + rdh) < (unsigned)a.H && (unsigned)(a_p1[j] + sdw) < (unsigned)a.W;
-          if (a.kragged) v = v && c0 + kc_lchunk(j) * EPC < a.C;
+          if constexpr (RAG) v = v && c0 + kc_lchunk(j) * EPC < a.C;
           dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
         }
       } else
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
         for (int j = 0; j < IB; ++j) {
           bool v = b_base[j] >= 0;
-          if (a.kragged) v = v && kbase + kc_lchunk(j) * EPC < a.Kg;
+          if constexpr (RAG) v = v && kbase + kc_lchunk(j) * EPC < a.Kg;
           dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_f2[j] + kbase) * (uint32_t)ESZ : OOB);
         }
       } else
@@ -326,7 +330,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
         for (int j = 0; j < IA; ++j) {
           bool v = (unsigned)(a_p0[j] - dth) < (unsigned)a.Ho && (unsigned)(a_p1[j] - dtw) < (unsigned)a.Wo;
-          if (a.kragged) v = v && co0 + kc_lchunk(j) * EPC < a.K;
+          if constexpr (RAG) v = v && co0 + kc_lchunk(j) * EPC < a.K;
           dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
         }
       } else
@@ -364,7 +368,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 #pragma unroll
         for (int j = 0; j < IB; ++j) {
           bool v = b_base[j] >= 0;
-          if (a.kragged) v = v && co0 + mc_krow(j, BN) < a.K;
+          if constexpr (RAG) v = v && co0 + mc_krow(j, BN) < a.K;
           dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(b_f2[j] + buni) * 2u : OOB);
         }
       } else
@@ -710,7 +714,7 @@ constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
   return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, bool FK,
+template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, int FK,
           bool F8 = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
   auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8>;
@@ -723,7 +727,7 @@ void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), lds, st, a);
 }
 
-template <int MODE, bool STATS, bool BIAS, bool FK>
+template <int MODE, bool STATS, bool BIAS, int FK>
 void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
   if (cfg == 0)
     launch_g<MODE, 256, 128, 4, 2, 3, STATS, BIAS, FK>(a, blocks, st);
@@ -787,9 +791,9 @@ void conv_fwd_fp8_launch(const ConvArgs& a0, hipStream_t st) {
     else launch_g<FWD, 256, 64, 4, 1, 3, ST, false, FK, true>(a, blocks, st);       \
   } while (0)
   if (fk) {
-    if (stats) TDL_F8(true, true); else TDL_F8(false, true);
+    if (stats) TDL_F8(true, 1); else TDL_F8(false, 1);
   } else {
-    if (stats) TDL_F8(true, false); else TDL_F8(false, false);
+    if (stats) TDL_F8(true, 0); else TDL_F8(false, 0);
   }
 #undef TDL_F8
 }
@@ -831,19 +835,24 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int blocks = (int)(groups * ntn);
   a.cls_tile0[0] = 0;
   a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
-  // FASTK: a K-step is one filter tap × 64 channels; 1×1 filters with C % 64 != 0 take it too,
-  // with the row's last channel chunk range-checked (Xception's 728-channel pointwise convs)
-  a.kragged = a.C % 64 != 0 && a.R * a.S == 1;
-  const bool fk = a.C % 64 == 0 || a.kragged;
+  // FASTK (FK 1): a K-step is one filter tap × 64 channels; 1×1 filters with C % 64 != 0 take
+  // it with the row's last channel chunk range-checked (FK 2: Xception's 728-channel pointwise
+  // convs); otherwise the generic K decomposition (FK 0)
+  const int fk = a.C % 64 == 0 ? 1 : (a.R * a.S == 1 ? 2 : 0);
   const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
-#define TDL_G(ST, BI, FK) launch_gcfg<FWD, ST, BI, FK>(a, cfg, blocks, st)
-  if (fk) {
-    if (bias) { if (stats) TDL_G(true, true, true); else TDL_G(false, true, true); }
-    else { if (stats) TDL_G(true, false, true); else TDL_G(false, false, true); }
-  } else {
-    if (bias) { if (stats) TDL_G(true, true, false); else TDL_G(false, true, false); }
-    else { if (stats) TDL_G(true, false, false); else TDL_G(false, false, false); }
-  }
+#define TDL_G(FK)                                                            \
+  do {                                                                       \
+    if (bias) {                                                              \
+      if (stats) launch_gcfg<FWD, true, true, FK>(a, cfg, blocks, st);       \
+      else launch_gcfg<FWD, false, true, FK>(a, cfg, blocks, st);            \
+    } else {                                                                 \
+      if (stats) launch_gcfg<FWD, true, false, FK>(a, cfg, blocks, st);      \
+      else launch_gcfg<FWD, false, false, FK>(a, cfg, blocks, st);           \
+    }                                                                        \
+  } while (0)
+  if (fk == 1) TDL_G(1);
+  else if (fk == 2) TDL_G(2);
+  else TDL_G(0);
 #undef TDL_G
   return true;
 }
@@ -880,15 +889,16 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
   if (a.fp8) {
     if (cfg == 1)
-      launch_g<DGRAD, 256, 64, 4, 1, 3, false, false, true, true>(a, blocks, st);
+      launch_g<DGRAD, 256, 64, 4, 1, 3, false, false, 1, true>(a, blocks, st);
     else
-      launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, true, true>(a, blocks, st);
-  } else if (a.K % 64 == 0 || (a.R * a.S == 1 && a.ncls == 1)) {
-    a.kragged = a.K % 64 != 0;
-    launch_gcfg<DGRAD, false, false, true>(a, cfg, blocks, st);
+      launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, 1, true>(a, blocks, st);
+  } else if (a.K % 64 == 0) {
+    launch_gcfg<DGRAD, false, false, 1>(a, cfg, blocks, st);
+  } else if (a.R * a.S == 1 && a.ncls == 1) {  // ragged FASTK (see conv_fwd_glds)
+    launch_gcfg<DGRAD, false, false, 2>(a, cfg, blocks, st);
+  } else {
+    launch_gcfg<DGRAD, false, false, 0>(a, cfg, blocks, st);
   }
-  else
-    launch_gcfg<DGRAD, false, false, false>(a, cfg, blocks, st);
   return true;
 }
 
@@ -928,7 +938,7 @@ void conv_wgrad_glds_kernel_launch(const ConvArgs& a0, const WgradPlan& p, hipSt
   a.cls_tile0[1] = (int)tiles;
   a.tpb = persistent_tpb(tiles);
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
-  launch_gcfg<WGRAD, false, false, true>(a, p.cfg, blocks, st);
+  launch_gcfg<WGRAD, false, false, 1>(a, p.cfg, blocks, st);
 }
 
 }  // namespace tdl

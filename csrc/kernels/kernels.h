@@ -58,8 +58,6 @@ struct ConvArgs {
   FastDiv fd_HoWo, fd_Wo, fd_C, fd_S, fd_sh, fd_sw;  // magic divisors (LDS-DMA launchers)
   FastDiv cls_fdHW[16], cls_fdW[16];                 // DGRAD per-class pixel decomposition
   int dbg;           // ablation flags (TDL_CONV_DBG, diagnostics only): 1 drop operand loads, 2 skip MFMA
-  int kragged;       // LDS-DMA FASTK path on a 1×1 filter whose channel count (FWD: C, DGRAD: K) is
-                     // not a multiple of 64: the last channel chunk of a row is range-checked
   // DGRAD parity classes (stride s: s_h·s_w classes of input pixels, each with its exact taps)
   int ncls;
   int dg_masked;     // 1: stride>1 with dilation>1 — single class, divisibility-masked taps
