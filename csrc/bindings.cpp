@@ -151,7 +151,8 @@ void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
 }
 
 void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask) {
+                int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask,
+                c10::optional<Tensor> w_t) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -168,6 +169,14 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
                 mask->numel() * 8 == dx.numel() && dx.size(3) % 64 == 0,
                 "conv_dgrad mask: uint8 [numel(dx)/8], C % 64 == 0");
     a.mask = (const uint8_t*)mask->data_ptr();
+  }
+  a.w_t = nullptr;
+  if (w_t.has_value() && w_t->defined()) {  // [R,S,C,K] copy of w (the LDS-DMA kernel's KC path)
+    CHECK_T(*w_t, torch::kBFloat16);
+    TORCH_CHECK(w_t->dim() == 4 && w_t->size(0) == a.R && w_t->size(1) == a.S &&
+                w_t->size(2) == a.C && w_t->size(3) == a.K && w_t->is_contiguous(),
+                "conv_dgrad w_t must be the [R,S,C,K] transpose of w");
+    a.w_t = BF(*w_t);
   }
   if (a.M == 0) return;
   conv_dgrad_launch(a, stream());
@@ -708,7 +717,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
-        py::arg("accumulate") = false, py::arg("mask") = py::none());
+        py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
   m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dy8"), py::arg("w8t"), py::arg("dx"),

@@ -111,7 +111,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   // FK: 0 = generic K decomposition; 1 = FASTK (a K-step is one filter tap × 64 (fp8: 128)
   // channels); 2 = FASTK on a 1×1 filter whose channel count is not a multiple of 64 — the row's
   // last channel chunk is range-checked (compile time: a runtime test per DMA cost 10–20 %)
-  constexpr bool FASTK = FK != 0, RAG = FK == 2;
+  // FK 3 (DGRAD, bf16): FASTK with the weights given transposed ([R][S][C][K], a.w_t) so both
+  // operands are K-contiguous rows read with ds_read_b128, as in the forward and the fp8 dgrad
+  constexpr bool FASTK = FK != 0, RAG = FK == 2, WT = FP8 || FK == 3;
   // FP8: operands are OCP fp8 bytes, a K-step is 128 deep (one 128-B LDS row per tile row, as
   // for bf16), fragments are 32 B and feed v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0
   // block scales; the per-tensor scales are applied in the epilogue.  FWD: x e4m3 × W e4m3.
@@ -125,7 +127,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   constexpr int KSTEP = 128 / ESZ;         // GEMM K per step (one 128-B LDS row)
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
-  constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE == WGRAD) || (MODE == DGRAD && !FP8);
+  constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE == WGRAD) || (MODE == DGRAD && !WT);
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int IA = A_BYTES / (1024 * NW), IB = B_BYTES / (1024 * NW);
   static_assert(IA * 1024 * NW == A_BYTES && IB * 1024 * NW == B_BYTES, "tile / wave mismatch");
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
-        if constexpr (FP8) {  // KC rows of W^T [R][S][C][K]: row ci of tap (r, s) at (r·S+s)·C·K + ci·K
+        if constexpr (WT) {  // KC rows of W^T [R][S][C][K]: row ci of tap (r, s) at (r·S+s)·C·K + ci·K
           const int ci = T.bn0 + kc_row(j);
           b_base[j] = ci < a.Ng ? ci * a.K : -1;
         } else {
@@ -353,14 +355,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         dma16(ra_src, As + (j * NW + wid) * 1024, v ? off : OOB);
       }
       const int r0 = a.cls_r0[c], s0 = a.cls_s0[c];
-      if constexpr (FP8) {  // W^T rows: tap (r, s) of this class, output channels co0 … +127
+      if constexpr (WT) {  // W^T rows: tap (r, s) of this class, output channels co0 … +KSTEP−1
         const int r = r0 + a.sh * pos_r, s = s0 + a.sw * pos_s;
         const int toff = (r * a.S + s) * a.C * a.K + co0;
 #pragma unroll
         for (int j = 0; j < IB; ++j) {
           const bool v = kb < T.Kgc && b_base[j] >= 0;
           dma16(rb_src, Bs + (j * NW + wid) * 1024,
-                v ? (uint32_t)(b_base[j] + toff + kc_lchunk(j) * EPC) : OOB);
+                v ? (uint32_t)(b_base[j] + toff + kc_lchunk(j) * EPC) * (uint32_t)ESZ : OOB);
         }
       } else if constexpr (FASTK) {
         const int r = r0 + a.sh * pos_r, s = s0 + a.sw * pos_s;
@@ -892,6 +894,9 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
       launch_g<DGRAD, 256, 64, 4, 1, 3, false, false, 1, true>(a, blocks, st);
     else
       launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, 1, true>(a, blocks, st);
+  } else if (a.K % 64 == 0 && a.w_t) {  // transposed weights: KC B operand
+    a.w = a.w_t;
+    launch_gcfg<DGRAD, false, false, 3>(a, cfg, blocks, st);
   } else if (a.K % 64 == 0) {
     launch_gcfg<DGRAD, false, false, 1>(a, cfg, blocks, st);
   } else if (a.R * a.S == 1 && a.ncls == 1) {  // ragged FASTK (see conv_fwd_glds)

@@ -48,6 +48,8 @@ struct ConvArgs {
   int beta;          // DGRAD: 1 = accumulate into the existing dx (residual-gradient join)
   int fp8;           // DGRAD: dy is e5m2 (a.dy), the weight e4m3 transposed [R][S][C][K] (a.w),
                      // per-tensor scales a.scale_x (dy) and a.scale_w (LDS-DMA kernel, K % 128 == 0)
+  const bf16_t* w_t;    // DGRAD (bf16): optional copy of the weights transposed to [R][S][C][K];
+                        // the LDS-DMA kernel then reads both operands as K-contiguous rows
   const uint8_t* mask;  // DGRAD: optional ReLU bit mask of dx (1 bit per element, NHWC order):
                         // dx = ([dx +] dgrad)·[bit] — the consumers of a block output apply the
                         // mask of its ReLU, so the producer BN's backward reads no mask

@@ -138,16 +138,18 @@ def conv_fwd_fp8(x8, sx, w8, sw, geom: ConvGeom, relu=False, stats=None):
 
 
 def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumulate=False,
-               mask=None):
+               mask=None, w_t=None):
     """dx.  With ``out`` the result is written there (``accumulate``: dx += …, fused in the GEMM
     epilogue — used by the residual-gradient join, ops/gradjoin.py).  ``mask`` (uint8, 1 bit per
-    element of dx, GPU): dx = ([dx +] dgrad)·[bit] for the elements this dgrad writes."""
+    element of dx, GPU): dx = ([dx +] dgrad)·[bit] for the elements this dgrad writes.  ``w_t``
+    (GPU, optional): the same weights transposed to [R,S,C,K]; the LDS-DMA kernel then reads both
+    operands as K-contiguous rows (same result)."""
     if on_gpu(dy):
         dx = out if out is not None else torch.empty(x_shape, device=dy.device,
                                                      dtype=out_dtype or dy.dtype)
         ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
                          geom.padding[2], geom.dilation[0], geom.dilation[1],
-                         bool(accumulate and out is not None), mask)
+                         bool(accumulate and out is not None), mask, w_t)
         return dx
     r = ref_conv_dgrad(dy, w, x_shape, geom)
     if mask is not None:

@@ -635,3 +635,23 @@ def test_batchnorm_bitmask_relu(gpu, C_):
     dx1, dr1 = B.bn_bwd_apply(dy, y, x, coef, red1, gamma, M, 1, True)
     dx3, dr3 = B.bn_bwd_apply(dy, mask, x, coef, red1, gamma, M, 3, True)
     assert torch.equal(dx1, dx3) and torch.equal(dr1, dr3)
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 1, (1, 1, 1, 1)),
+                                   (8, 16, 16, 128, 64, 1, 2, (0, 0, 0, 0))])
+def test_conv_dgrad_transposed_weights(gpu, shape):
+    """conv_dgrad(w_t=[R,S,C,K] copy): the LDS-DMA kernel's K-contiguous B-operand variant gives
+    the same bits as the transposed-LDS-read path (same products, same order)."""
+    N, H, Cin, K, k, s, pad = shape
+    g = C.ConvGeom((s, s), pad, (1, 1))
+    torch.manual_seed(5)
+    w = (torch.randn(K, k, k, Cin) * 0.05).bfloat16().to(gpu)
+    Ho, Wo = g.out_hw(H, H, k, k)
+    dy = torch.randn(N, Ho, Wo, K).bfloat16().to(gpu)
+    ext().conv_set_glds_mode(2)
+    try:
+        r0 = C.conv_dgrad(dy, w, (N, H, H, Cin), g)
+        r1 = C.conv_dgrad(dy, w, (N, H, H, Cin), g, w_t=w.permute(1, 2, 3, 0).contiguous())
+    finally:
+        ext().conv_set_glds_mode(-1)
+    assert torch.equal(r0, r1)
