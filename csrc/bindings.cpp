@@ -150,9 +150,14 @@ void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
                         out.data_ptr<float>(), stream());
 }
 
-void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+// bn_x / bn_red (optional, together): also accumulate the BN-backward sums (Σg, Σg·x) of the
+// stored dx into bn_red fp32 [2, C] (zeroed by the caller), x = bn_x the input of the BN whose
+// output this conv consumed.  Returns whether they were computed (stride-1 problems on the
+// LDS-DMA kernel); otherwise bn_red is untouched and the BN backward reduces itself.
+bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                 int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask,
-                c10::optional<Tensor> w_t) {
+                c10::optional<Tensor> w_t, c10::optional<Tensor> bn_x,
+                c10::optional<Tensor> bn_red) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -178,8 +183,19 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
                 "conv_dgrad w_t must be the [R,S,C,K] transpose of w");
     a.w_t = BF(*w_t);
   }
-  if (a.M == 0) return;
-  conv_dgrad_launch(a, stream());
+  a.stats = nullptr;
+  a.bn_x = nullptr;
+  if (bn_x.has_value() && bn_x->defined()) {
+    TORCH_CHECK(bn_red.has_value() && bn_red->defined(), "conv_dgrad: bn_x needs bn_red");
+    CHECK_T(*bn_x, torch::kBFloat16);
+    CHECK_T(*bn_red, torch::kFloat32);
+    TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_red->numel() == 2 * dx.size(3) &&
+                bn_red->is_contiguous(), "conv_dgrad bn_x: shape of dx, bn_red fp32 [2, C]");
+    a.bn_x = BF(*bn_x);
+    a.stats = bn_red->data_ptr<float>();
+  }
+  if (a.M == 0) return false;
+  return conv_dgrad_launch(a, stream());
 }
 
 // fp8 dgrad: dy8 e5m2 [N,Ho,Wo,K], w8t e4m3 transposed weights [R,S,C,K] (ops/fp8.py), dx bf16
@@ -339,7 +355,7 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
                   c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres,
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
                   int64_t relu, c10::optional<Tensor> dx8, c10::optional<Tensor> amax_ring,
-                  int64_t phase, c10::optional<Tensor> scale_out) {
+                  int64_t phase, c10::optional<Tensor> scale_out, bool red_raw) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -358,7 +374,8 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
   }
   bn_bwd_apply_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
                       optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
-                      C, (float)count, (int)relu, stream(), d8, prev, optfw(scale_out), out, zero);
+                      C, (float)count, (int)relu, stream(), d8, prev, optfw(scale_out), out, zero,
+                      red_raw);
 }
 
 // ---------------------------------------------------------------------------------- elementwise
@@ -717,7 +734,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
-        py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none());
+        py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none(),
+        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
   m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dy8"), py::arg("w8t"), py::arg("dx"),
@@ -737,7 +755,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("coef"),
         py::arg("red"), py::arg("gamma"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("count"), py::arg("relu"), py::arg("dx8") = py::none(),
-        py::arg("amax_ring") = py::none(), py::arg("phase") = 0, py::arg("scale_out") = py::none());
+        py::arg("amax_ring") = py::none(), py::arg("phase") = 0, py::arg("scale_out") = py::none(),
+        py::arg("red_raw") = false);
   m.def("fp8_quantize_e5m2", [](Tensor x, Tensor ring, int64_t phase, bool measure, Tensor scale,
                                 Tensor y8) {
     CHECK_T(x, torch::kBFloat16);

@@ -360,7 +360,9 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dgamma,
     float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu,
     uint8_t* __restrict__ dx8, const float* __restrict__ amax_prev, float* __restrict__ scale_out,
-    float* __restrict__ amax_out, float* __restrict__ amax_zero) {
+    float* __restrict__ amax_out, float* __restrict__ amax_zero, int red_raw) {
+  // red_raw: red = (Σg, Σg·x) accumulated by the producing dgrad's epilogue (conv_common.h);
+  // Σg·x̂ = invstd·(Σg·x − mean·Σg) here
   // optional e5m2 side output of dx (fp8 dgrad of the producing conv; delayed scaling with 4×
   // headroom over the previous call's |dx|max: gradients can grow step to step, e5m2 has 30
   // binades to spare, a clipped gradient biases the update)
@@ -375,7 +377,8 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
   }
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += NT) {
-      if (dgamma) dgamma[c] = red[C + c];
+      if (dgamma)
+        dgamma[c] = red_raw ? coef[3 * C + c] * (red[C + c] - coef[2 * C + c] * red[c]) : red[C + c];
       if (dbeta) dbeta[c] = red[c];
     }
   }
@@ -391,6 +394,10 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     load8f(coef + 3 * C + cv * 8, inv);
     load8f(red + cv * 8, s0);
     load8f(red + C + cv * 8, s1);
+    if (red_raw) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s1[j] = inv[j] * (s1[j] - mean[j] * s0[j]);
+    }
     if (gamma) {
       load8f(gamma + cv * 8, gm);
     } else {
@@ -470,10 +477,13 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
                                         const float* __restrict__ gamma, bf16_t* __restrict__ dx,
                                         bf16_t* __restrict__ dres, float* __restrict__ dgamma,
                                         float* __restrict__ dbeta, long n, int C, float inv_count,
-                                        int relu) {
+                                        int relu, int red_raw) {
+  auto s1_of = [&](int c) {
+    return red_raw ? coef[3 * C + c] * (red[C + c] - coef[2 * C + c] * red[c]) : red[C + c];
+  };
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      if (dgamma) dgamma[c] = red[C + c];
+      if (dgamma) dgamma[c] = s1_of(c);
       if (dbeta) dbeta[c] = red[c];
     }
   }
@@ -486,7 +496,7 @@ __global__ void bwd_apply_scalar_kernel(const bf16_t* __restrict__ dy, const bf1
     const float mean = coef[2 * C + c], inv = coef[3 * C + c];
     const float k = (gamma ? gamma[c] : 1.f) * inv;
     const float xh = (bf2f(x[i]) - mean) * inv;
-    dx[i] = f2bf(k * (g - red[c] * inv_count - xh * red[C + c] * inv_count));
+    dx[i] = f2bf(k * (g - red[c] * inv_count - xh * s1_of(c) * inv_count));
   }
 }
 
@@ -544,7 +554,7 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,
                          hipStream_t st, uint8_t* dx8, const float* amax_prev, float* scale_out,
-                         float* amax_out, float* amax_zero) {
+                         float* amax_out, float* amax_zero, bool red_raw) {
   const long n = M * C;
   if (C % 8 == 0) {
     static const int u = env_int("TDL_BN_BWD_U", 2);
@@ -555,10 +565,11 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                    : bwd_apply_vec_kernel<false, 1>;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
                        dbeta, n / 8, C, 1.f / count, relu, dx8, amax_prev, scale_out, amax_out,
-                       amax_zero);
+                       amax_zero, red_raw ? 1 : 0);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
-                       red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu);
+                       red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu,
+                       red_raw ? 1 : 0);
   }
 }
 

@@ -77,7 +77,9 @@ struct Tile {
   int split;      // WGRAD split index
 };
 
-template <int MODE, int BM, int BN, int KS = BK>
+// COLG: column-grouped order (FWD always; DGRAD with fused BN statistics, single class): a
+// workgroup's tiles share one column tile, so its statistics flush once
+template <int MODE, int BM, int BN, int KS = BK, bool COLG = (MODE == FWD)>
 __device__ __forceinline__ Tile tile_of(const ConvArgs& a, int t) {
   Tile T;
   const int ntn = (a.Ng + BN - 1) / BN;
@@ -99,7 +101,7 @@ __device__ __forceinline__ Tile tile_of(const ConvArgs& a, int t) {
     T.split = t / nt;
     local = t - T.split * nt;
   }
-  if constexpr (MODE == FWD) {
+  if constexpr (COLG) {
     // workgroup b owns column tile (b % ntn) and row tiles [(b / ntn)·tpb, +tpb): its tiles share
     // bn0 (BN statistics accumulate in registers, one flush per workgroup) and the ntn workgroups
     // of a row group run together, re-reading the same A tiles from L2
@@ -229,12 +231,15 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 
 // ---------------------------------------------------------------------------------------------
 // bf16 output tile epilogue of both conv kernels (FWD y / DGRAD dx): bias, the DGRAD residual
-// join (dx += …) and ReLU bit mask, ReLU, BN Σ/Σ² of the stored values, 16-B stores.
+// join (dx += …) and ReLU bit mask, ReLU, BN Σ/Σ² of the stored values (FWD) or the BN-backward
+// sums Σg, Σg·x (DGRAD, x = a.bn_x), 16-B stores.
 // ---------------------------------------------------------------------------------------------
 // lane holds C[m = bm0 + wm*TM + rm*16 + (lane&15)][n = bn0 + wn*TN + rn*16 + (lane>>4)*4 + i].
 // SCALE: multiply by `scale` first (fp8 GEMMs: the per-tensor operand scales); `no_mem`: issue no
 // loads / stores (timing ablation).
-template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false>
+// NJ: compile-time "no residual join" (its previous-dx registers are not allocated)
+template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false,
+          bool NJ = false>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
@@ -272,11 +277,25 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
   // tile's in-flight operand DMA each time.
   bool join_prev = false, join_mask = false;
   if constexpr (MODE == DGRAD) {
-    join_prev = a.beta && !no_mem;
+    join_prev = !NJ && a.beta && !no_mem;
     join_mask = a.mask && !no_mem;
   }
   uint32_t mrow[RM][2];
   v2u32 pv[RM][RN];
+  // DGRAD BN-backward statistics (STATS): the BN input x at the stored positions — Σg·x with g
+  // the stored (masked) dx; the BN backward converts to Σg·x̂ (bn.hip, red_raw)
+  v2u32 xv[RM][RN];
+  if constexpr (MODE == DGRAD && STATS) {
+    const rsrc_t rbx = make_rsrc(a.bn_x, no_mem ? 0u : a.out_bytes);
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) {
+        const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+        xv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
+            rbx, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+      }
+  }
   if constexpr (MODE == DGRAD) {
     if (join_mask) {
       const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
@@ -347,7 +366,16 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
       const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
       if (!no_mem && !wide)
         __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-      if constexpr (STATS) {
+      if constexpr (STATS && MODE == DGRAD) {
+        // (Σg, Σg·x) of the stored bf16 g; rows past M store zeros (x reads there return 0)
+        const float v0 = __uint_as_float(pk[rn][0] << 16), v1 = __uint_as_float(pk[rn][0] & 0xffff0000u);
+        const float v2 = __uint_as_float(pk[rn][1] << 16), v3 = __uint_as_float(pk[rn][1] & 0xffff0000u);
+        s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
+        s_sq[rn][0] = fmaf(v0, __uint_as_float(xv[rm][rn][0] << 16), s_sq[rn][0]);
+        s_sq[rn][1] = fmaf(v1, __uint_as_float(xv[rm][rn][0] & 0xffff0000u), s_sq[rn][1]);
+        s_sq[rn][2] = fmaf(v2, __uint_as_float(xv[rm][rn][1] << 16), s_sq[rn][2]);
+        s_sq[rn][3] = fmaf(v3, __uint_as_float(xv[rm][rn][1] & 0xffff0000u), s_sq[rn][3]);
+      } else if constexpr (STATS) {
         // statistics of the stored bf16 values; rows past M are zero unless a bias was added
         const float rv = (!BIAS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
         const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;

@@ -787,7 +787,7 @@ static void zero_fill(void* p, uint32_t bytes, hipStream_t st) {
   hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)p, n4);
 }
 
-void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
+bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   const bool masked = (a.sh > 1 && a.dh > 1) || (a.sw > 1 && a.dw > 1) ||
                       a.sh * a.sw > MAX_DG_CLASSES;
@@ -846,9 +846,10 @@ void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   // (when accumulating into an existing dx the zero classes simply keep their values)
   if (nz < ncls && !a.beta) zero_fill(a.out, a.out_bytes, st);
   ncls = nz;
-  if (ncls == 0) return;
+  if (ncls == 0) return false;
   a.ncls = ncls;
-  if (!masked && conv_dgrad_glds(a, Mmax * ncls, st)) return;
+  bool fused = false;
+  if (!masked && conv_dgrad_glds(a, Mmax * ncls, st, &fused)) return fused;
   if (a.fp8) throw std::runtime_error("fp8 dgrad: LDS-DMA kernel not eligible (K % 128, C % 8, "
                                       "stride with dilation)");
   convk::set_fastdivs(a);
@@ -863,13 +864,14 @@ void conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
     maxkt = std::max(maxkt, cdiv((long)a.cls_Th[c] * a.cls_Tw[c] * a.K, BK));
   }
   const long tiles = a.cls_tile0[ncls];
-  if (tiles == 0) return;
+  if (tiles == 0) return false;
   a.tpb = pick_tpb(tiles, maxkt);
   a.splits = 1;
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
   const bool al = (a.C % 8 == 0) && (a.K % 8 == 0) && !masked;
   if (al) launch_cfg<DGRAD, true, false>(a, bm, bn, blocks, st);
   else launch_cfg<DGRAD, false, false>(a, bm, bn, blocks, st);
+  return false;  // the register-staged kernel does not fuse BN-backward statistics
 }
 
 void conv_wgrad_plan(const ConvArgs& a, WgradPlan* p) {

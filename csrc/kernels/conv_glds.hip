@@ -106,14 +106,20 @@ __device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, int FK,
-          bool FP8 = false>
+          bool FP8 = false, bool NJ = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  // NJ (DGRAD): no residual join (a.beta == 0) — the epilogue's previous-dx registers are not
+  // allocated (the fused-statistics dgrad needs them for the BN input x instead)
   // FK: 0 = generic K decomposition; 1 = FASTK (a K-step is one filter tap × 64 (fp8: 128)
   // channels); 2 = FASTK on a 1×1 filter whose channel count is not a multiple of 64 — the row's
   // last channel chunk is range-checked (compile time: a runtime test per DMA cost 10–20 %)
   // FK 3 (DGRAD, bf16): FASTK with the weights given transposed ([R][S][C][K], a.w_t) so both
   // operands are K-contiguous rows read with ds_read_b128, as in the forward and the fp8 dgrad
   constexpr bool FASTK = FK != 0, RAG = FK == 2, WT = FP8 || FK == 3;
+  // STATS: FWD — BN Σy, Σy² of the output; DGRAD — BN-backward Σg, Σg·x of dx (a.bn_x), tiles in
+  // column-grouped order (one class) so a workgroup's sums flush once
+  static_assert(!STATS || MODE != WGRAD, "no statistics for weight gradients");
+  constexpr bool COLG = MODE == FWD || (MODE == DGRAD && STATS);
   // FP8: operands are OCP fp8 bytes, a K-step is 128 deep (one 128-B LDS row per tile row, as
   // for bf16), fragments are 32 B and feed v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0
   // block scales; the per-tensor scales are applied in the epilogue.  FWD: x e4m3 × W e4m3.
@@ -485,8 +491,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
       }
     } else {
-      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8>(a, T, acc, wm, wn, lane, rout, out_scale,
-                                                             no_epi_mem, s_sum, s_sq);
+      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ>(
+          a, T, acc, wm, wn, lane, rout, out_scale, no_epi_mem, s_sum, s_sq);
     }
   };
 
@@ -532,14 +538,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   // split, and fall back to tile_of at a class or split boundary.
   const int ntn_c = (a.Ng + BN - 1) / BN;
   auto next_tile = [&](Tile& T, int t) {
-    if constexpr (MODE == FWD) {
+    if constexpr (COLG) {
       T.bm0 += BM;
     } else {
       T.bn0 += BN;
       if (T.bn0 >= a.Ng) {
         T.bn0 = 0;
         T.bm0 += BM;
-        if (T.bm0 >= T.Mc) T = tile_of<MODE, BM, BN, KSTEP>(a, t);
+        if (T.bm0 >= T.Mc) T = tile_of<MODE, BM, BN, KSTEP, COLG>(a, t);
       }
     }
     (void)ntn_c;
@@ -547,7 +553,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
 
   // ---- flat (tile, K-step) pipeline over this workgroup's tiles ----
   int lt = tile_begin;
-  Tile LT = tile_of<MODE, BM, BN, KSTEP>(a, lt);
+  Tile LT = tile_of<MODE, BM, BN, KSTEP, COLG>(a, lt);
   int lkt = LT.kt0;
   bool lmore = LT.bm0 < LT.Mc;
   if (!lmore) return;
@@ -711,15 +717,16 @@ constexpr GCfg G128x128{128, 128, 2, 2, 4};
 constexpr GCfg G128x128s2{128, 128, 2, 2, 2};  // 66 KB LDS: two workgroups per CU
 constexpr GCfg G256x64w8{256, 64, 8, 1, 3};    // 64-wide N with 8 waves (32-row wave tiles)
 constexpr GCfg G128x64{128, 64, 4, 1, 4};      // 64-wide N, 4 stages, 96 KB LDS
+constexpr GCfg G128x128w8{128, 128, 4, 2, 4};  // 8 waves of 32×64 (half the accumulators)
 
 constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
   return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, int FK,
-          bool F8 = false>
+          bool F8 = false, bool NJ = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8>;
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ>;
   constexpr int lds = lds_bytes(BM, BN, WM, ST);
   static bool attr = false;
   if (!attr) {
@@ -729,20 +736,22 @@ void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), lds, st, a);
 }
 
-template <int MODE, bool STATS, bool BIAS, int FK>
+template <int MODE, bool STATS, bool BIAS, int FK, bool NJ = false>
 void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
   if (cfg == 0)
-    launch_g<MODE, 256, 128, 4, 2, 3, STATS, BIAS, FK>(a, blocks, st);
+    launch_g<MODE, 256, 128, 4, 2, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else if (cfg == 1)
-    launch_g<MODE, 256, 64, 4, 1, 3, STATS, BIAS, FK>(a, blocks, st);
+    launch_g<MODE, 256, 64, 4, 1, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else if (cfg == 2)
-    launch_g<MODE, 128, 128, 2, 2, 4, STATS, BIAS, FK>(a, blocks, st);
+    launch_g<MODE, 128, 128, 2, 2, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else if (cfg == 3)
-    launch_g<MODE, 128, 128, 2, 2, 2, STATS, BIAS, FK>(a, blocks, st);
+    launch_g<MODE, 128, 128, 2, 2, 2, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else if (cfg == 4)
-    launch_g<MODE, 256, 64, 8, 1, 3, STATS, BIAS, FK>(a, blocks, st);
+    launch_g<MODE, 256, 64, 8, 1, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
+  else if (cfg == 6 && MODE == DGRAD && STATS)  // fused-statistics dgrads only
+    launch_g<MODE, 128, 128, 4, 2, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else
-    launch_g<MODE, 128, 64, 4, 1, 4, STATS, BIAS, FK>(a, blocks, st);
+    launch_g<MODE, 128, 64, 4, 1, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
 }
 
 const GCfg& cfg_of(int c) {
@@ -752,6 +761,7 @@ const GCfg& cfg_of(int c) {
     case 2: return G128x128;
     case 3: return G128x128s2;
     case 4: return G256x64w8;
+    case 6: return G128x128w8;
     default: return G128x64;
   }
 }
@@ -861,7 +871,8 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
 
 // DGRAD with prepared parity classes (conv_dgrad_launch builds them); returns false when the
 // register-staged kernel should run instead.
-bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
+bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* fused) {
+  if (fused) *fused = false;
   const int mode = conv_glds_mode();
   if (a0.fp8) {  // fp8 operands exist only for this kernel
     if (a0.C % 8 || a0.K % 128 || a0.dg_masked) return false;
@@ -886,6 +897,31 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st) {
   const long tiles = a.cls_tile0[a.ncls];
   if (tiles == 0) return true;
   if (mode == 1 && !a.fp8 && tiles < 128) return false;  // see conv_fwd_glds
+  // BN-backward statistics in the epilogue (a.stats, a.bn_x): stride 1 (one class covering
+  // every pixel), FASTK; tiles in the forward's column-grouped order (tile_of COLG) so each
+  // workgroup flushes its column sums once
+  const bool bn_stats = a.stats && a.bn_x && !a.fp8 && a.ncls == 1 && a.sh == 1 && a.sw == 1 &&
+                        a.K % 64 == 0;
+  if (bn_stats) {
+    // tile config (tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
+    // tiles (NJ: no previous-dx registers); with the join's previous-dx loads as well they spill,
+    // so 8 waves of 32×64 (cfg 6); 64-wide dx: the 8-wave 256×64 tiles
+    const int scfg = env_int(a.beta ? "TDL_GLDS_CFG_DGSTAT_J" : "TDL_GLDS_CFG_DGSTAT",
+                             a.Ng <= 64 ? 4 : (a.beta ? 6 : 0));
+    const GCfg& g = cfg_of(scfg);
+    const long ntm = cdiv((long)a.N * a.cls_Hc[0] * a.cls_Wc[0], g.bm), ntn = cdiv(a.Ng, g.bn);
+    a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm * ntn)), ntm);
+    const long groups = (ntm + a.tpb - 1) / a.tpb;
+    a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+    a.splits = 1;
+    if (a.beta)
+      launch_gcfg<DGRAD, true, false, 1>(a, scfg, (int)(groups * ntn), st);
+    else
+      launch_gcfg<DGRAD, true, false, 1, true>(a, scfg, (int)(groups * ntn), st);
+    if (fused) *fused = true;
+    return true;
+  }
+  a.stats = nullptr;
   a.tpb = persistent_tpb(tiles);
   a.splits = 1;
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);

@@ -37,7 +37,11 @@ struct ConvArgs {
   const bf16_t* dy;  // DGRAD / WGRAD: output gradient [N,Ho,Wo,K]
   void* out;         // FWD: y bf16 [M][ldc]; DGRAD: dx bf16 [M][ldc]; WGRAD: fp32 split slabs
   const float* bias; // FWD: optional bias [K]
-  float* stats;      // FWD: optional BN statistics [2][K] (Σy, Σy²), accumulated
+  float* stats;      // FWD: optional BN statistics [2][K] (Σy, Σy²), accumulated.
+                     // DGRAD: BN-backward statistics of the BN whose output is this conv's input
+                     // ((Σg, Σg·x) with g the stored dx and x = a.bn_x, the BN's input; LDS-DMA
+                     // kernel, stride-1 only) — the BN backward then needs no reduce pass
+  const bf16_t* bn_x;  // DGRAD with stats: the BN input [N,H,W,C] (same layout as dx)
   int N, H, W, C, K, R, S, Ho, Wo;
   int sh, sw, ph, pw, dh, dw;
   int M, Ng, Kg;     // GEMM dims
@@ -70,7 +74,9 @@ struct ConvArgs {
 constexpr int MAX_DG_CLASSES = 16;
 
 void conv_fwd_launch(const ConvArgs& a, hipStream_t st);
-void conv_dgrad_launch(const ConvArgs& a, hipStream_t st);
+// returns true when a.stats was filled (DGRAD BN-backward statistics fused into the epilogue);
+// a.stats is ignored (false) when the problem does not run on the LDS-DMA kernel
+bool conv_dgrad_launch(const ConvArgs& a, hipStream_t st);
 // WGRAD plan: impl 0 = register-staged kernel (bm × bn tiles), 1 = LDS-DMA kernel (config cfg);
 // the caller allocates splits·M·Ng fp32 slab floats and passes them in a.out.
 struct WgradPlan {
@@ -83,7 +89,8 @@ void conv_wgrad_launch(const ConvArgs& a, const WgradPlan& p, float* out, bool a
 int conv_glds_mode();
 void conv_set_glds_mode(int mode);  // -1: environment / default
 bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
-bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st);
+// *fused: set to whether a.stats was filled (stride-1 FASTK problems only)
+bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st, bool* fused = nullptr);
 bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);
 void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 // fp8 (OCP e4m3) forward conv: a.x / a.w point at e4m3 bytes, a.scale_x / a.scale_w at their fp32 scales
@@ -132,7 +139,8 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,
                          hipStream_t st, uint8_t* dx8 = nullptr, const float* amax_prev = nullptr,
                          float* scale_out = nullptr, float* amax_out = nullptr,
-                         float* amax_zero = nullptr);
+                         float* amax_zero = nullptr,
+                         bool red_raw = false);  // red = (Σg, Σg·x) from a fused dgrad epilogue
 
 // elementwise --------------------------------------------------------------------------------
 void relu_bwd_launch(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t st);

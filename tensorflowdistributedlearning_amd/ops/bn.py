@@ -6,7 +6,8 @@ GPU kernels (``csrc/kernels/bn.hip``):
                        accumulate them in its epilogue — see ``conv2d(want_stats=True)``);
   * ``bn_finalize``    mean / invstd / scale / shift + moving-average update in one tiny launch;
   * ``bn_apply``       y = act(x·scale + shift [+ residual]) — one vectorised pass;
-  * ``bn_bwd_reduce``  Σg, Σg·x̂ with g = dy·[y>0];
+  * ``bn_bwd_reduce``  Σg, Σg·x̂ with g = dy·[y>0] — skipped when the consumer conv's dgrad
+                       epilogue already accumulated (Σg, Σg·x) (ops/gradjoin.py, fused statistics);
   * ``bn_bwd_apply``   dx = γ·invstd·(g − Σg/M − x̂·Σg·x̂/M), plus g for the residual branch.
 
 Reference parity: ``slim.batch_norm`` under ``resnet_arg_scope`` (core/resnet.py:357-395,71,126,242)
@@ -127,10 +128,17 @@ def bn_bwd_reduce(dy, y, x, coef, relu):
     return torch.stack([g.sum(0), (g * xhat).sum(0)])
 
 
+def bn_red_xhat(red, coef):
+    """(Σg, Σg·x̂) from the raw (Σg, Σg·x) a fused dgrad epilogue accumulated:
+    Σg·x̂ = invstd·(Σg·x − mean·Σg)."""
+    return torch.stack([red[0], coef[3] * (red[1] - coef[2] * red[0])])
+
+
 def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None, dbeta=None,
-                 fp8=None):
+                 fp8=None, red_raw=False):
     """dx (same dtype as x) and optionally the masked gradient g for the residual branch.
     On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch.
+    ``red_raw``: ``red`` holds (Σg, Σg·x) from a fused dgrad epilogue (:func:`bn_red_xhat`).
     ``fp8`` = (amax_ring, phase, scale, emit): also write an e5m2 copy of dx with delayed scaling
     (4× headroom over the previous call's |dx|max) — attached as ``dx._tdl_fp8`` = (dx8, scale)
     for the fp8 dgrad of the producing conv."""
@@ -140,16 +148,18 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
         dres = torch.empty_like(dy) if want_dres else None
         if fp8 is None:
             ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
-                               int(relu))
+                               int(relu), red_raw=bool(red_raw))
             return dx, dres
         ring, phase, scale, emit = fp8
         dx8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e5m2) if emit else None
         ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
                            int(relu), dx8.view(torch.uint8) if emit else None, ring, int(phase),
-                           scale)
+                           scale, red_raw=bool(red_raw))
         if emit:
             dx._tdl_fp8 = (dx8, scale)
         return dx, dres
+    if red_raw:
+        red = bn_red_xhat(red, coef)
     g = dy.float().reshape(-1, C)
     if relu:
         g = g * _relu_mask(relu, y, x, coef, C)
@@ -181,18 +191,22 @@ class _BatchNormActFn(torch.autograd.Function):
         # nothing saved); with one, the forward writes it as 1 bit per element (mode 3: the two
         # backward kernels read 1/16 of y's bytes instead of y itself)
         mask = None
-        if relu and residual is not None and need_grad and on_gpu(x) and C % 8 == 0 and C <= 2048:
+        if relu and need_grad and on_gpu(x) and C % 8 == 0 and C <= 2048 and (
+                residual is not None or (C % 64 == 0 and gradjoin.STATS_ENABLED
+                                         and gradjoin.MASK_ENABLED)):
+            # without a residual only for the fused-statistics path: the consuming conv's dgrad
+            # applies the mask and accumulates this BN's backward sums (ops/gradjoin.py)
             mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8)
         y = bn_apply(x, coef, residual, relu, fp8, mask)
         ctx.mask_token = None
         if mask is not None:  # the consumers' dgrads may apply it for us (ops/gradjoin.py)
-            ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask)
+            ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask, x)
         ctx.count = count
         ctx.bn = bn
         ctx.training = training
         ctx.has_res = residual is not None
         ctx.res_join = res_join if residual is not None else None
-        ctx.relu = 0 if not relu else (2 if residual is None else (3 if mask is not None else 1))
+        ctx.relu = 0 if not relu else (3 if mask is not None else (2 if residual is None else 1))
         ctx.save_for_backward(x, mask if ctx.relu == 3 else (y if ctx.relu == 1 else None), coef,
                               gamma, beta)
         return y
@@ -225,7 +239,11 @@ class _BatchNormActFn(torch.autograd.Function):
         # (ops/gradjoin.py) — no mask reads, and dy itself is the residual gradient
         if premasked:
             relu, y = 0, None
-        red = bn_bwd_reduce(dy, y, x, coef, relu)
+        # (Σg, Σg·x) fused into the last writer's dgrad epilogue, else a reduce pass
+        red = ctx.mask_token.red if premasked else None
+        red_raw = red is not None
+        if red is None:
+            red = bn_bwd_reduce(dy, y, x, coef, relu)
         want_g = gamma is not None and gamma.requires_grad
         want_b = beta.requires_grad
         gt, gfresh = _grad_target_phys(gamma, C) if want_g else (None, False)
@@ -237,9 +255,12 @@ class _BatchNormActFn(torch.autograd.Function):
         fp8 = ctx.bn.fp8_bwd_state(x) if getattr(ctx.bn, "emit_fp8_bwd", False) else None
         dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, count, relu,
                                 ctx.has_res and not premasked,
-                                gt if direct_g else None, bt if direct_b else None, fp8=fp8)
+                                gt if direct_g else None, bt if direct_b else None, fp8=fp8,
+                                red_raw=red_raw)
         if premasked and ctx.has_res:
             dres = dy
+        if red_raw and want_g and not direct_g:
+            red = bn_red_xhat(red, coef)
         if want_g:
             deliver_grad(gamma, None if direct_g else red[1][:c], written=direct_g)
         if want_b:

@@ -24,6 +24,7 @@ import torch.nn.functional as F
 from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view
 from . import workspace
 from . import streams
+from . import gradjoin
 
 
 @dataclass(frozen=True)
@@ -167,6 +168,30 @@ def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumul
     return out
 
 
+def conv_dgrad_bnstat(dy, w, x_shape, geom: ConvGeom, bn_x, out=None, accumulate=False,
+                      mask=None):
+    """:func:`conv_dgrad` that also returns the BN-backward sums of the stored dx: fp32 [2, C] =
+    (Σg, Σg·x) with g = dx (as stored, after the join accumulate / ReLU mask) and x = ``bn_x``,
+    the input of the BN whose output this conv consumed — the BN backward then skips its reduce
+    pass (``bn_bwd_apply(red_raw=True)`` turns Σg·x into Σg·x̂).  Returns ``(dx, red)``; ``red`` is
+    None when the kernel could not fuse them (strided dgrads, problems that run on the
+    register-staged kernel): the BN then reduces as usual."""
+    if on_gpu(dy):
+        dx = out if out is not None else torch.empty(x_shape, device=dy.device, dtype=dy.dtype)
+        red = workspace.zeros((2, x_shape[-1]), dy.device)
+        fused = ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
+                                 geom.padding[2], geom.dilation[0], geom.dilation[1],
+                                 bool(accumulate and out is not None), mask, None, bn_x, red)
+        return dx, (red if fused else None)
+    dx = conv_dgrad(dy, w, x_shape, geom, out=out, accumulate=accumulate, mask=mask)
+    if geom.stride != (1, 1):
+        return dx, None
+    C = x_shape[-1]
+    g = dx.float().reshape(-1, C)
+    red = torch.stack([g.sum(0), (g * bn_x.float().reshape(-1, C)).sum(0)])
+    return dx, red
+
+
 def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
     """[N, H, W, 1] bool: input pixels the dgrad writes (a strided conv with taps of fewer than
     ``stride`` rows / columns leaves whole parity classes untouched)."""
@@ -273,6 +298,9 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.layer = layer
         ctx.join = join
         ctx.x_shape = tuple(x.shape)
+        # the ReLU-mask token of the BN that produced x (ops/gradjoin.py): a single-consumer conv
+        # applies the mask in its dgrad and may fuse that BN's backward statistics
+        ctx.bn_tok = getattr(x, "_tdl_mask_token", None) if join is None else None
         ctx.save_for_backward(x, weight, bias, y if relu else None)
         if stats is None:
             stats = torch.empty(0, device=x.device)
@@ -299,7 +327,8 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
                 compute_weight(weight, dy.dtype)
-            if fp8_dgrad_eligible(ctx.layer, dy, geom, tuple(w.shape)):
+            fp8_dg = fp8_dgrad_eligible(ctx.layer, dy, geom, tuple(w.shape))
+            if fp8_dg:
                 # fp8 dgrad: e5m2 dy (the BN backward's side output) × e4m3 W^T
                 dy8, sdy = dy._tdl_fp8
                 w8t, sw8 = ctx.layer.fp8_weight_t(w)
@@ -312,14 +341,33 @@ class _Conv2dFn(torch.autograd.Function):
                     return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,
                                       mask=mask)
             join = ctx.join
+            masks_ok = on_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
+            stats_ok = masks_ok and not fp8_dg and geom.stride == (1, 1)
             if join is None:
-                dx = dgrad()
+                tok = ctx.bn_tok
+                if tok is not None and masks_ok:
+                    # sole consumer of a masked BN output: apply the mask here, and fuse the BN's
+                    # backward statistics when the kernel can (ops/gradjoin.py)
+                    if stats_ok and tok.x is not None and gradjoin.STATS_SINGLE:
+                        dx, red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, tok.x,
+                                                    mask=tok.mask)
+                    else:
+                        dx, red = dgrad(mask=tok.mask), None
+                    tok.mark(dx, red)
+                else:
+                    dx = dgrad()
             else:  # residual-gradient join: first consumer writes, later ones accumulate
-                # pre-masked join (ops/gradjoin.py); the epilogue reads 64-channel mask slabs
-                mask = join.mask if on_gpu(dy) and ctx.x_shape[-1] % 64 == 0 else None
+                # pre-masked join (ops/gradjoin.py)
+                mask = join.mask if masks_ok else None
                 if join.buf is None:
                     join.buf = dgrad(mask=mask)
                     join.note(mask is not None)
+                elif join.last and mask is not None and stats_ok and join.stats_x is not None:
+                    # the final contribution writes every pixel through the mask: its epilogue
+                    # sees the finished gradient and can fuse the BN statistics
+                    _, join.red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, join.stats_x,
+                                                    out=join.buf, accumulate=True, mask=mask)
+                    join.note(True)
                 else:
                     dgrad(out=join.buf, accumulate=True, mask=mask)
                     join.note(mask is not None, dgrad_covers_input(geom, w.shape[1], w.shape[2]))

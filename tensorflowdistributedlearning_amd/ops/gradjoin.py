@@ -21,6 +21,13 @@ mask and returns the incoming gradient itself as the residual gradient instead o
 (ResNet-50 b256: one full activation write and the mask reads of 16 residual BN backwards).
 Anything that breaks the protocol (an unmasked contribution last, autograd summing another
 gradient into the buffer) leaves the token unset, and the BN applies the mask itself as before.
+
+Fused BN-backward statistics: the token also carries the BN's input x.  A stride-1 dgrad that
+writes the final gradient (the only consumer, or the join's last contribution) accumulates
+(Σg, Σg·x) of what it stores in its epilogue (``conv_dgrad_bnstat``); the token records them with
+the pre-masked stamp and the BN backward skips its reduce pass (a read of dy and x).  Non-residual
+ReLU BNs (bottleneck conv1 / conv2 outputs) write the 1-bit mask too so their single consumer
+conv can take the same path.
 """
 from __future__ import annotations
 
@@ -30,23 +37,45 @@ ENABLED = True
 
 
 MASK_ENABLED = os.environ.get("TDL_PREMASK", "1") == "1"  # 0: the BN applies its mask
+# TDL_BNSTAT_FUSE: 0 — the BN backward always runs its own reduce pass; 1 — statistics fused into
+# the last writer's dgrad epilogue, residual joins included; 2 (default) — only for
+# single-consumer convs; 3 — only for residual joins.  ResNet-50 b1024 same-box A/B
+# (profiles/r02_bnstat_fuse_ab.txt): 0 11993 / 11999, 1 11994 / 11984, 2 12029 / 12012,
+# 3 11882 / 11840 img/s — the join variant's smaller tiles (the 256×128 ones spill with both the
+# previous-dx and the x loads) lose next to the side-stream weight gradients
+_FUSE = os.environ.get("TDL_BNSTAT_FUSE", "2")
+STATS_ENABLED = _FUSE != "0"
+STATS_SINGLE = _FUSE in ("1", "2")
+STATS_JOIN = _FUSE in ("1", "3")
 
 
 class MaskToken:
-    """The ReLU bit mask of a residual BN output, and (after backward) which gradient buffer the
-    consumers handed back already masked: ``(data_ptr, version)`` of that tensor."""
-    __slots__ = ("mask", "premasked")
+    """The ReLU bit mask of a BN output, the BN's input ``x`` (for fused statistics), and (after
+    backward) which gradient buffer the consumers handed back already masked:
+    ``(data_ptr, version)`` of that tensor, plus its (Σg, Σg·x) when the last writer fused them."""
+    __slots__ = ("mask", "premasked", "x", "red")
 
-    def __init__(self, mask):
+    def __init__(self, mask, x=None):
         self.mask = mask
         self.premasked = None
+        self.x = x if STATS_ENABLED else None
+        self.red = None
 
     def is_premasked(self, g):
         return self.premasked is not None and self.premasked == (g.data_ptr(), g._version)
 
+    def mark(self, g, red=None):
+        """``g`` is the finished, masked gradient; ``red`` its fused (Σg, Σg·x) or None."""
+        self.premasked = (g.data_ptr(), g._version)
+        self.red = red
+
+    def stats_for(self, g):
+        """The fused (Σg, Σg·x) of ``g`` if its last writer produced them, else None."""
+        return self.red if self.is_premasked(g) else None
+
 
 class GradJoin:
-    __slots__ = ("n", "count", "buf", "mask_token", "unmasked")
+    __slots__ = ("n", "count", "buf", "mask_token", "unmasked", "red")
 
     def __init__(self, n, mask_token=None):
         self.n = n
@@ -54,6 +83,18 @@ class GradJoin:
         self.buf = None
         self.mask_token = mask_token
         self.unmasked = False  # some element of buf holds a contribution not yet masked
+        self.red = None        # (Σg, Σg·x) fused by the last contribution (conv_dgrad_bnstat)
+
+    @property
+    def last(self):
+        """The next contribution is the last one."""
+        return self.count + 1 == self.n
+
+    @property
+    def stats_x(self):
+        """The BN input to fuse statistics against (None: not applicable)."""
+        t = self.mask_token
+        return t.x if t is not None and STATS_JOIN else None
 
     @property
     def mask(self):
@@ -74,7 +115,7 @@ class GradJoin:
         if self.count != self.n:
             return None
         if self.mask_token is not None and not self.unmasked and self.buf is not None:
-            self.mask_token.premasked = (self.buf.data_ptr(), self.buf._version)
+            self.mask_token.mark(self.buf, self.red)
         return self.buf
 
 

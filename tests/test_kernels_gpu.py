@@ -416,6 +416,54 @@ def test_conv_dgrad_relu_mask(gpu, conv_impl, shape, accumulate):
     assert (dx.float().cpu()[~keep] == 0).all()  # masked elements exactly zero
 
 
+@pytest.mark.parametrize("shape", [(8, 28, 28, 128, 256, 1, 1, False),   # 1x1, 8-wave 128x128
+                                   (8, 28, 28, 64, 256, 1, 1, False),    # 64-wide dx (cfg 4)
+                                   (8, 14, 14, 128, 128, 3, 1, False),   # 3x3
+                                   (8, 28, 28, 256, 64, 1, 1, True),     # join accumulate
+                                   (8, 30, 30, 192, 128, 1, 1, False),   # ragged column tiles
+                                   (8, 28, 28, 128, 128, 3, 2, False)])  # strided: not fused
+def test_conv_dgrad_bnstat(gpu, shape):
+    """BN-backward statistics fused into the LDS-DMA dgrad epilogue (ops/gradjoin.py): dx is
+    bit-identical to the plain masked dgrad, and (Σg, Σg·x) of the stored dx match an fp32
+    reduction; strided dgrads report no statistics.  bn_bwd_apply(red_raw=True) on them equals
+    the reduce-pass path."""
+    N, H, W, Cin, K, k, st, join = shape
+    p = (k - 1) // 2
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
+    torch.manual_seed(21)
+    w = (torch.randn(K, k, k, Cin) / math.sqrt(k * k * Cin)).bfloat16().to(gpu)
+    Ho, Wo = g.out_hw(H, W, k, k)
+    dy = torch.randn(N, Ho, Wo, K).bfloat16().to(gpu)
+    x = (torch.randn(N, H, W, Cin) * 1.3 + 0.4).bfloat16().to(gpu)
+    gam, bet = torch.rand(Cin, device=gpu) + 0.5, torch.randn(Cin, device=gpu) * 0.3
+    M = N * H * W
+    coef = B.bn_finalize(B.bn_stats(x), M, gam, bet, torch.zeros(Cin, device=gpu),
+                         torch.ones(Cin, device=gpu), 0.9, 1e-3, True)
+    mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+    B.bn_apply(x, coef, None, True, mask=mask)
+    prev = torch.randn(N, H, W, Cin).bfloat16().to(gpu) if join else None
+    ext().conv_set_glds_mode(2)  # the LDS-DMA kernel for these small problems too
+    try:
+        ref = C.conv_dgrad(dy, w, x.shape, g, mask=mask,
+                           out=prev.clone() if join else None, accumulate=join)
+        dx, red = C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask,
+                                      out=prev.clone() if join else None, accumulate=join)
+    finally:
+        ext().conv_set_glds_mode(-1)
+    assert torch.equal(dx, ref)
+    if st != 1:
+        assert red is None
+        return
+    assert red is not None
+    gf, xf = dx.float().reshape(-1, Cin), x.float().reshape(-1, Cin)
+    want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
+    assert rel_err(red, want) < 1e-4
+    d0, _ = B.bn_bwd_apply(dx, None, x, coef, B.bn_bwd_reduce(dx, None, x, coef, 0), gam, M, 0,
+                           False)
+    d1, _ = B.bn_bwd_apply(dx, None, x, coef, red, gam, M, 0, False, red_raw=True)
+    assert rel_err(d1, d0) < 1e-2
+
+
 def test_fp8_quantize_matches_cpu(gpu):
     from tensorflowdistributedlearning_amd.ops import fp8 as F8
     torch.manual_seed(12)
@@ -642,7 +690,7 @@ def test_batchnorm_bitmask_relu(gpu, C_):
 def test_conv_dgrad_transposed_weights(gpu, shape):
     """conv_dgrad(w_t=[R,S,C,K] copy): the LDS-DMA kernel's K-contiguous B-operand variant gives
     the same bits as the transposed-LDS-read path (same products, same order)."""
-    N, H, Cin, K, k, s, pad = shape
+    N, H, _, Cin, K, k, s, pad = shape
     g = C.ConvGeom((s, s), pad, (1, 1))
     torch.manual_seed(5)
     w = (torch.randn(K, k, k, Cin) * 0.05).bfloat16().to(gpu)

@@ -286,3 +286,29 @@ def test_depthwise_relu_in_matches_explicit_relu_cpu():
             r = pw.bn(pw.conv(r), relu=False)
         ref = r + xi
         torch.testing.assert_close(m(xi), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_conv_dgrad_bnstat_cpu_oracle():
+    """CPU oracle of the fused BN-backward statistics: (Σg, Σg·x) of the stored dx, and
+    bn_bwd_apply(red_raw=True) — Σg·x̂ = invstd·(Σg·x − mean·Σg) — equals the reduce path."""
+    torch.manual_seed(3)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    x = torch.randn(2, 9, 9, 16) * 1.2 + 0.5
+    w = torch.randn(24, 3, 3, 16) * 0.1
+    dy = torch.randn(2, 9, 9, 24)
+    dx, red = C.conv_dgrad_bnstat(dy, w, x.shape, g, x)
+    assert torch.allclose(dx, C.conv_dgrad(dy, w, x.shape, g))
+    gf, xf = dx.reshape(-1, 16), x.reshape(-1, 16)
+    assert torch.allclose(red, torch.stack([gf.sum(0), (gf * xf).sum(0)]), atol=1e-4)
+    st = B.bn_stats(x)
+    coef = B.bn_finalize(st, 162, torch.ones(16), torch.zeros(16), torch.zeros(16),
+                         torch.ones(16), 0.9, 1e-3, True)
+    want = B.bn_bwd_reduce(dx, None, x, coef, 0)
+    assert torch.allclose(B.bn_red_xhat(red, coef), want, rtol=1e-4, atol=1e-4)
+    gam = torch.rand(16) + 0.5
+    d0, _ = B.bn_bwd_apply(dx, None, x, coef, want, gam, 162, 0, False)
+    d1, _ = B.bn_bwd_apply(dx, None, x, coef, red, gam, 162, 0, False, red_raw=True)
+    assert torch.allclose(d0, d1, rtol=1e-4, atol=1e-5)
+    # strided dgrads do not fuse
+    _, r2 = C.conv_dgrad_bnstat(dy[:, ::2, ::2], w, x.shape, C.ConvGeom((2, 2), (1, 1, 1, 1)), x)
+    assert r2 is None

@@ -156,6 +156,9 @@ def test_premasked_join_matches_bn_masking(gpu, depth, monkeypatch):
         return r
 
     monkeypatch.setattr(gradjoin.MaskToken, "is_premasked", spy)
+    # residual joins only (no non-residual BN masks for fused statistics: see
+    # test_fused_bn_stats_match_reduce_pass)
+    monkeypatch.setattr(gradjoin, "STATS_ENABLED", False)
     nblocks = sum(1 for mod in m.modules()
                   if mod.__class__.__name__ in ("Bottleneck", "BasicBlock"))
     outs = []
@@ -175,6 +178,62 @@ def test_premasked_join_matches_bn_masking(gpu, depth, monkeypatch):
             gradjoin.MASK_ENABLED = True
     cos = torch.nn.functional.cosine_similarity(outs[0], outs[1], dim=0).item()
     assert cos > 0.9999, cos
+
+
+@pytest.mark.parametrize("frozen", [True, False])
+def test_fused_bn_stats_match_reduce_pass(gpu, monkeypatch, frozen):
+    """BN-backward statistics fused into the consumer dgrads (ops/gradjoin.py: bottleneck conv1 /
+    conv2 outputs and the block outputs whose last gradient writer is a stride-1 dgrad) vs every
+    BN running its reduce pass: the fused path is taken for most BNs and gives the same
+    gradients.  Frozen BN (moving statistics): dx needs no batch sums, so dγ/dβ compare the fused
+    sums directly; batch statistics: compared against the run-to-run spread of the plain path
+    (fp32 atomic order).  Exact kernel semantics: test_kernels_gpu.py::test_conv_dgrad_bnstat."""
+    from tensorflowdistributedlearning_amd.ops import gradjoin
+    from tensorflowdistributedlearning_amd.ops import bn as BN
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    torch.manual_seed(11)
+    m = models.build("resnet50", num_classes=10).to(gpu)
+    m.train()
+    if frozen:
+        for mod in m.modules():
+            if mod.__class__.__name__ == "BatchNorm":
+                mod.train(False)
+    x = torch.randn(32, 128, 128, 8, device=gpu, dtype=torch.bfloat16)
+    used = []
+    orig = BN.bn_bwd_reduce
+
+    def spy(*a, **k):
+        used.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(BN, "bn_bwd_reduce", spy)
+    monkeypatch.setattr(gradjoin, "STATS_ENABLED", True)
+    outs, calls = [], []
+    ext().conv_set_glds_mode(2)  # the LDS-DMA kernels also for this test's small problems
+    try:
+        for enabled in (False, False, True):
+            gradjoin.STATS_ENABLED = enabled
+            used.clear()
+            for p in m.parameters():
+                p.grad = None
+            y = m(x)
+            (y.float() * torch.linspace(-1, 1, 10, device=gpu)).sum().backward()
+            torch.cuda.synchronize()
+            outs.append(torch.cat([p.grad.float().flatten() for p in m.parameters()
+                                   if p.grad is not None]))
+            calls.append(len(used))
+    finally:
+        gradjoin.STATS_ENABLED = True
+        ext().conv_set_glds_mode(-1)
+    assert calls[0] - calls[2] >= 20, calls  # most BN backwards skipped their reduce pass
+    cs = torch.nn.functional.cosine_similarity
+    noise = cs(outs[0], outs[1], dim=0).item()
+    cos = cs(outs[0], outs[2], dim=0).item()
+    print(f"cos plain/plain {noise:.6f} plain/fused {cos:.6f}")
+    if frozen:
+        assert cos > 0.9999, (cos, noise)
+    else:
+        assert cos > noise - 0.02, (cos, noise)
 
 
 @pytest.mark.parametrize("fuse_bn", [False, True])

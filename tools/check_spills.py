@@ -15,7 +15,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the instantiations the default selection runs (mode, tile, waves, stages, STATS, BIAS, FK, FP8)
-DEFAULT = [r"ILi0ELi256ELi128ELi4ELi2ELi3ELb[01]ELb[01]ELi1ELb0E", r"ILi1ELi256ELi128ELi4ELi2ELi3ELb0ELb0ELi1ELb0E",
+DEFAULT = [r"ILi0ELi256ELi128ELi4ELi2ELi3ELb[01]ELb[01]ELi1ELb0E", r"ILi1ELi256ELi128ELi4ELi2ELi3ELb0ELb0ELi1ELb0E", r"ILi1ELi128ELi128ELi4ELi2ELi4ELb1E", r"ILi1ELi256ELi128ELi4ELi2ELi3ELb1ELb0ELi1ELb0ELb1E",
            r"ILi2ELi256ELi128ELi4ELi2ELi3ELb0ELb0ELi1ELb0E", r"ILi[01]ELi256ELi64ELi8ELi1ELi3E",
            r"ILi[01]ELi256ELi128ELi4ELi2ELi3ELb[01]ELb0ELi1ELb1E"]
 
