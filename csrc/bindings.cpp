@@ -379,6 +379,16 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
 }
 
 // ---------------------------------------------------------------------------------- elementwise
+void row_pack(Tensor x, Tensor t, int64_t creal, int64_t S, int64_t sw, int64_t pl) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(t, torch::kBFloat16);
+  TORCH_CHECK(x.dim() == 4 && t.dim() == 4 && t.size(0) == x.size(0) && t.size(1) == x.size(1) &&
+              t.size(3) % 8 == 0 && t.size(3) >= S * creal && creal <= x.size(3),
+              "row_pack: x [N,H,W,Cx], t [N,H,Wo,Cp] with Cp % 8 == 0, Cp >= S*creal");
+  row_pack_launch(BF(x), BFW(t), x.size(0), x.size(1), x.size(2), x.size(3), creal, S, sw, pl,
+                  t.size(2), t.size(3), stream());
+}
+
 void relu_bwd(Tensor dy, Tensor y, Tensor dx) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -784,6 +794,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                tiles.data_ptr<int64_t>(), (int)tiles.size(0), stream());
   });
   m.def("relu_bwd", &relu_bwd);
+  m.def("row_pack", &row_pack);
   m.def("add_act", &add_act);
   m.def("scale_by_scalar", &scale_by_scalar);
   m.def("sigmoid_threshold", &sigmoid_threshold);

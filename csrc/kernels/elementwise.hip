@@ -79,7 +79,91 @@ __global__ void sigmoid_threshold_kernel(const void* __restrict__ x, int bf16,
   }
 }
 
+// Row packing of a few-channel image for its k×k stem conv (ops/conv.py row_pack): t[n][h][wo] =
+// the S·Cr values x[n][h][wo·sw − pl + s][c] (s < S, c < Cr; zero outside the row) followed by zero
+// padding to Cp.  The k×k conv over x is then a k×1 conv over t whose GEMM K is R·Cp (168 for the
+// 7×7 RGB stem) instead of R·S·8 (392 with the channels padded to 8).  One thread per 16-B chunk.
+__global__ void row_pack_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ t, long chunks,
+                                int H, int W, int Cx, int Cr, int S, int sw, int pl, int Wo, int Cp) {
+  const int cpc = Cp >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < chunks;
+       i += (long)gridDim.x * blockDim.x) {
+    const long row = i / cpc;  // (n, h, wo)
+    const int q = (int)(i - row * cpc);
+    const int wo = (int)(row % Wo);
+    const long nh = row / Wo;  // n·H + h
+    const int w0 = wo * sw - pl;
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint32_t pair = 0;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int e = q * 8 + j + h2, s = e / Cr, c = e - s * Cr, wi = w0 + s;
+        uint32_t b = 0;
+        if (s < S && (unsigned)wi < (unsigned)W) b = x[(nh * W + wi) * Cx + c];
+        pair |= b << (16 * h2);
+      }
+      v[j >> 1] = pair;
+    }
+    *(uint4*)(t + i * 8) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// the RGB stem's case (input padded to 8 channels, 7 taps × 3 channels → 24): one thread per
+// output row — seven 16-B pixel loads (neighbouring rows share them through the caches), three
+// 16-B stores; the generic kernel's per-element 2-byte loads ran at ~2.6 TB/s
+template <int S, int CR, int CP>
+__global__ void row_pack_px8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ t, long rows,
+                                    int W, int sw, int pl, int Wo) {
+  for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < rows;
+       r += (long)gridDim.x * blockDim.x) {
+    const int wo = (int)(r % Wo);
+    const long nh = r / Wo;
+    const int w0 = wo * sw - pl;
+    uint4 px[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int wi = w0 + s;
+      px[s] = (unsigned)wi < (unsigned)W ? *(const uint4*)(x + (nh * W + wi) * 8)
+                                         : make_uint4(0, 0, 0, 0);
+    }
+    uint32_t o[CP / 2];
+#pragma unroll
+    for (int j = 0; j < CP / 2; ++j) o[j] = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const uint32_t w4[4] = {px[s].x, px[s].y, px[s].z, px[s].w};
+#pragma unroll
+      for (int c = 0; c < CR; ++c) {
+        const int e = s * CR + c;
+        const uint32_t v = (w4[c >> 1] >> (16 * (c & 1))) & 0xffffu;
+        o[e >> 1] |= v << (16 * (e & 1));
+      }
+    }
+    uint4* dst = (uint4*)(t + r * CP);
+#pragma unroll
+    for (int q = 0; q < CP / 8; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
+}
+
 }  // namespace
+
+void row_pack_launch(const bf16_t* x, bf16_t* t, int N, int H, int W, int Cx, int Cr, int S,
+                     int sw, int pl, int Wo, int Cp, hipStream_t st) {
+  const long chunks = (long)N * H * Wo * (Cp / 8);
+  if (chunks == 0) return;
+  if (Cx == 8 && Cr == 3 && S == 7 && Cp == 24) {
+    const long rows = (long)N * H * Wo;
+    const int blocks = (int)std::min<long>(16384, (rows + 255) / 256);
+    hipLaunchKernelGGL((row_pack_px8_kernel<7, 3, 24>), dim3(blocks), dim3(256), 0, st, x, t, rows, W,
+                       sw, pl, Wo);
+    return;
+  }
+  const int blocks = (int)std::min<long>(8192, (chunks + 255) / 256);
+  hipLaunchKernelGGL(row_pack_kernel, dim3(blocks), dim3(256), 0, st, x, t, chunks, H, W, Cx, Cr,
+                     S, sw, pl, Wo, Cp);
+}
 
 void relu_bwd_launch(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t st) {
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(blocks_for(n / 8 + 1)), dim3(NT), 0, st, dy, y, dx, n);

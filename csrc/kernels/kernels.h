@@ -143,6 +143,10 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          bool red_raw = false);  // red = (Σg, Σg·x) from a fused dgrad epilogue
 
 // elementwise --------------------------------------------------------------------------------
+// t [N][H][Wo][Cp] = row-packed x [N][H][W][Cx] for a k×k stem conv (first Cr channels, S taps of
+// stride sw from column wo·sw − pl; zeros past the row / after S·Cr); Cp % 8 == 0
+void row_pack_launch(const bf16_t* x, bf16_t* t, int N, int H, int W, int Cx, int Cr, int S,
+                     int sw, int pl, int Wo, int Cp, hipStream_t st);
 void relu_bwd_launch(const bf16_t* dy, const bf16_t* y, bf16_t* dx, long n, hipStream_t st);
 void add_act_launch(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, bool relu,
                     hipStream_t st);

@@ -12,7 +12,7 @@ import math
 import torch
 import torch.nn as nn
 
-from ..ops.conv import ConvGeom, conv2d, same_padding, symmetric_padding
+from ..ops.conv import ConvGeom, conv2d, same_padding, symmetric_padding, row_pack
 from ..ops.bn import batch_norm_act
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
@@ -222,6 +222,64 @@ class Conv2d(nn.Module):
                 f"pad={self.padding}, bias={self.bias is not None}, relu={self.relu}")
 
 
+class RowPackedConv2d(Conv2d):
+    """k×k conv on a few-channel image (the 7×7 RGB stem) computed as a k×1 conv over the
+    row-packed input (:func:`ops.conv.row_pack`: each output column's k taps × C channels become
+    one contiguous channel vector, padded to a multiple of 8).  Same math as :class:`Conv2d` with
+    the input padded to 8 channels, but the GEMM K is k·⌈k·C/8⌉·8 instead of k·k·8 (168 vs 392
+    for 7×7×3: 2.3× fewer MFMA FLOPs in the stem's forward and weight gradient).  The parameter
+    keeps its [Cout, k, k, C] shape (checkpoints, optimizer); the compute copy is re-laid to
+    [Cout, k, 1, Cp] once per parameter version and the weight gradient folded back.  The input
+    gets no gradient (an image)."""
+
+    def __init__(self, cin, cout, k, stride=1, padding="sym", **kw):
+        super().__init__(cin, cout, k, stride, padding, **kw)
+        assert self.k[0] == self.k[1] and self.dilation == (1, 1)
+        self._cp = _round_up(self.k[1] * cin, 8)
+        self._packed = None
+        self._packed_version = -1
+        self._pgeom = {}
+
+    def grad_needs_unpad(self):
+        return True
+
+    def padded_weight_shape(self):
+        return (self._cout_store, self.k[0], 1, self._cp)
+
+    def unpad_grad(self, dw):
+        k = self.k[1]
+        return dw[: self.cout, :, 0, : k * self.cin].reshape(self.cout, self.k[0], k, self.cin)
+
+    def compute_weight(self, dtype):
+        w = compute_weight(self.weight, dtype)
+        if (self._packed is None or self._packed.dtype != dtype
+                or self._packed.device != w.device):
+            self._packed = torch.zeros(self.padded_weight_shape(), dtype=dtype, device=w.device)
+            self._packed_version = -1
+        v = _params.version()
+        if self._packed_version != v:
+            k = self.k[1]
+            self._packed[: self.cout, :, 0, : k * self.cin].copy_(
+                w.reshape(self.cout, self.k[0], k * self.cin))
+            self._packed_version = v
+        return self._packed
+
+    def forward(self, x, want_stats=False, join=None):
+        if x.requires_grad:
+            raise ValueError("RowPackedConv2d: the packed stem propagates no input gradient")
+        H, W = x.shape[1], x.shape[2]
+        pg = self._pgeom.get((H, W))
+        if pg is None:
+            pt, pb, pl, pr = resolve_padding(self.padding, H, W, self.k[0], self.k[1],
+                                             self.stride, self.dilation)
+            Wo = (W + pl + pr - self.k[1]) // self.stride[1] + 1
+            pg = self._pgeom[(H, W)] = (ConvGeom((self.stride[0], 1), (pt, pb, 0, 0)), pl, Wo)
+        g, pl, Wo = pg
+        t = row_pack(x, self.cin, self.k[1], self.stride[1], pl, Wo, self._cp)
+        y, stats = conv2d(t, self.weight, self.bias, g, self.relu, want_stats, self, join)
+        return (y, stats) if want_stats else y
+
+
 class BatchNorm(nn.Module):
     """BN over the channel (last) axis with TF-style moving averages
     (``m ← decay·m + (1−decay)·batch``).  ``scale=False`` drops γ (slim ``scale`` flag).
@@ -289,11 +347,11 @@ class ConvBN(nn.Module):
 
     def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, relu=True,
                  bn_decay=0.997, bn_eps=1e-5, bn_scale=True, zero_init_gamma=False, init="he_tf",
-                 init_std=None, pad_cin_to=None, pad_cout_to=None):
+                 init_std=None, pad_cin_to=None, pad_cout_to=None, conv_cls=None):
         super().__init__()
-        self.conv = Conv2d(cin, cout, k, stride, padding, dilation, bias=False, relu=False,
-                           init=init, init_std=init_std, pad_cin_to=pad_cin_to,
-                           pad_cout_to=pad_cout_to)
+        self.conv = (conv_cls or Conv2d)(cin, cout, k, stride, padding, dilation=dilation,
+                                         bias=False, relu=False, init=init, init_std=init_std,
+                                         pad_cin_to=pad_cin_to, pad_cout_to=pad_cout_to)
         self.bn = BatchNorm(cout, bn_decay, bn_eps, bn_scale, zero_init_gamma,
                             c_phys=self.conv._cout_store)
         self.relu = relu

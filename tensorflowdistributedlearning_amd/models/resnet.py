@@ -8,12 +8,14 @@ bottleneck's last BN, the residual add and the ReLU are a single fused kernel pa
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops import gradjoin
 
-from .layers import ConvBN, MaxPool, GlobalAvgPool, Linear
+from .layers import ConvBN, MaxPool, GlobalAvgPool, Linear, RowPackedConv2d
 
 _CFG = {
     18: ("basic", (2, 2, 2, 2)),
@@ -85,8 +87,11 @@ class ResNet(nn.Module):
         bn_kw = dict(bn_decay=bn_decay, bn_eps=bn_eps)
         self.depth = depth
         self.in_channels = in_channels
+        # 7×7/s2 stem on the row-packed image (K = 7·24 instead of 7·7·8, RowPackedConv2d);
+        # TDL_STEM_PACK=0: the plain conv on the 8-channel padded input
+        packed = in_channels * 7 <= 64 and os.environ.get("TDL_STEM_PACK", "1") == "1"
         self.stem = ConvBN(in_channels, width, 7, 2, "sym", relu=True, init="kaiming_fan_out",
-                           pad_cin_to=8, **bn_kw)
+                           pad_cin_to=8, conv_cls=RowPackedConv2d if packed else None, **bn_kw)
         self.pool = MaxPool(3, 2, "sym")
         stages = []
         cin = width

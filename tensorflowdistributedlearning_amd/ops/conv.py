@@ -263,6 +263,23 @@ def conv_wgrad(dy, x, w_shape, geom: ConvGeom, out=None, accumulate=False, bias_
     return out
 
 
+def row_pack(x, creal, S, sw, pl, Wo, Cp):
+    """Row packing of a few-channel image for its S-wide stem conv: t [N, H, Wo, Cp] with
+    t[n, h, wo, s·creal + c] = x[n, h, wo·sw − pl + s, c] (zero outside the row, zero after
+    S·creal).  A k×k conv over x equals a k×1 conv over t with the weight re-laid to
+    [K, k, 1, Cp] (models.layers.RowPackedConv2d) — its GEMM K shrinks from k·k·8 (input padded to
+    8 channels) to k·Cp (7×7 RGB stem: 392 → 168).  GPU: one HIP gather pass."""
+    N, H, W, Cx = x.shape
+    if on_gpu(x):
+        t = torch.empty((N, H, Wo, Cp), device=x.device, dtype=x.dtype)
+        ext().row_pack(x, t, int(creal), int(S), int(sw), int(pl))
+        return t
+    xp = F.pad(x[..., :creal], (0, 0, pl, max(0, (Wo - 1) * sw + S - W - pl)))
+    cols = xp.unfold(2, S, sw)[:, :, :Wo]               # [N, H, Wo, creal, S]
+    t = cols.permute(0, 1, 2, 4, 3).reshape(N, H, Wo, S * creal)
+    return F.pad(t, (0, Cp - S * creal)).contiguous()
+
+
 def relu_bwd(dy, y):
     """dy * (y > 0) — GPU: fused elementwise kernel."""
     if on_gpu(dy):

@@ -703,3 +703,28 @@ def test_conv_dgrad_transposed_weights(gpu, shape):
     finally:
         ext().conv_set_glds_mode(-1)
     assert torch.equal(r0, r1)
+
+
+def test_row_packed_stem_gpu(gpu):
+    """The row-pack HIP kernel = its CPU oracle (bitwise), and the packed 7×7/s2 stem
+    (RowPackedConv2d) = the plain conv on the 8-channel padded input: forward and dW on the GPU."""
+    from tensorflowdistributedlearning_amd.models.layers import Conv2d, RowPackedConv2d
+    torch.manual_seed(6)
+    x = torch.randn(4, 45, 50, 8).bfloat16()
+    x[..., 3:] = 0
+    for sw, pl, Wo in ((2, 3, 25), (1, 3, 50)):
+        ref = C.row_pack(x, 3, 7, sw, pl, Wo, 24)
+        got = C.row_pack(x.to(gpu), 3, 7, sw, pl, Wo, 24)
+        assert torch.equal(got.cpu(), ref)
+    plain = Conv2d(3, 64, 7, 2, "sym", pad_cin_to=8).to(gpu)
+    packed = RowPackedConv2d(3, 64, 7, 2, "sym", pad_cin_to=8).to(gpu)
+    packed.weight.data.copy_(plain.weight.data)
+    xg = torch.randn(8, 64, 64, 8, device=gpu).bfloat16()
+    xg[..., 3:] = 0
+    y0, y1 = plain(xg), packed(xg)
+    assert rel_err(y1, y0) < 1e-2
+    g = torch.randn_like(y0)
+    (y0.float() * g.float()).sum().backward()
+    (y1.float() * g.float()).sum().backward()
+    torch.cuda.synchronize()
+    assert rel_err(packed.weight.grad, plain.weight.grad) < 1e-2

@@ -312,3 +312,27 @@ def test_conv_dgrad_bnstat_cpu_oracle():
     # strided dgrads do not fuse
     _, r2 = C.conv_dgrad_bnstat(dy[:, ::2, ::2], w, x.shape, C.ConvGeom((2, 2), (1, 1, 1, 1)), x)
     assert r2 is None
+
+
+def test_row_packed_stem_matches_conv():
+    """RowPackedConv2d (7×7/s2 stem as a 7×1 conv over the row-packed image) = the plain conv on
+    the 8-channel padded input: forward and weight gradient (CPU oracle path)."""
+    from tensorflowdistributedlearning_amd.models.layers import Conv2d, RowPackedConv2d
+    torch.manual_seed(4)
+    plain = Conv2d(3, 16, 7, 2, "sym", pad_cin_to=8)
+    packed = RowPackedConv2d(3, 16, 7, 2, "sym", pad_cin_to=8)
+    packed.weight.data.copy_(plain.weight.data)
+    for H, W in ((32, 32), (29, 35)):
+        x = torch.randn(2, H, W, 8)
+        x[..., 3:] = 0
+        y0 = plain(x)
+        y1 = packed(x)
+        assert y1.shape == y0.shape
+        assert torch.allclose(y0, y1, atol=1e-4, rtol=1e-4)
+        g = torch.randn_like(y0)
+        plain.weight.grad = packed.weight.grad = None
+        (y0 * g).sum().backward()
+        (y1 * g).sum().backward()
+        assert torch.allclose(plain.weight.grad, packed.weight.grad, atol=1e-3, rtol=1e-4)
+    t = C.row_pack(x, 3, 7, 2, 3, 18, 24)
+    assert t.shape == (2, 29, 18, 24) and float(t[..., 21:].abs().sum()) == 0.0
