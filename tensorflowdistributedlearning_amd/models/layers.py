@@ -229,8 +229,8 @@ class RowPackedConv2d(Conv2d):
     the input padded to 8 channels, but the GEMM K is k·⌈k·C/8⌉·8 instead of k·k·8 (168 vs 392
     for 7×7×3: 2.3× fewer MFMA FLOPs in the stem's forward and weight gradient).  The parameter
     keeps its [Cout, k, k, C] shape (checkpoints, optimizer); the compute copy is re-laid to
-    [Cout, k, 1, Cp] once per parameter version and the weight gradient folded back.  The input
-    gets no gradient (an image)."""
+    [Cout, k, 1, Cp] once per parameter version and the weight gradient folded back.  An input
+    gradient (rare for an image) flows through the packing's transposed gather."""
 
     def __init__(self, cin, cout, k, stride=1, padding="sym", **kw):
         super().__init__(cin, cout, k, stride, padding, **kw)
@@ -265,8 +265,6 @@ class RowPackedConv2d(Conv2d):
         return self._packed
 
     def forward(self, x, want_stats=False, join=None):
-        if x.requires_grad:
-            raise ValueError("RowPackedConv2d: the packed stem propagates no input gradient")
         H, W = x.shape[1], x.shape[2]
         pg = self._pgeom.get((H, W))
         if pg is None:

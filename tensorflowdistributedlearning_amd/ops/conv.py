@@ -263,7 +263,36 @@ def conv_wgrad(dy, x, w_shape, geom: ConvGeom, out=None, accumulate=False, bias_
     return out
 
 
+class _RowPackFn(torch.autograd.Function):
+    """Differentiable :func:`row_pack` (the input gradient — rare for an image — is the
+    transposed gather: S strided slice-adds)."""
+
+    @staticmethod
+    def forward(ctx, x, creal, S, sw, pl, Wo, Cp):
+        ctx.args = (tuple(x.shape), creal, S, sw, pl, Wo)
+        return _row_pack(x, creal, S, sw, pl, Wo, Cp)
+
+    @staticmethod
+    def backward(ctx, dt):
+        (N, H, W, Cx), creal, S, sw, pl, Wo = ctx.args
+        g = dt[..., : S * creal].float().reshape(N, H, Wo, S, creal)
+        span = (Wo - 1) * sw + S
+        dxp = torch.zeros(N, H, max(span, pl + W), creal, device=dt.device)
+        for s in range(S):
+            dxp[:, :, s: s + (Wo - 1) * sw + 1: sw] += g[:, :, :, s]
+        dx = torch.zeros(N, H, W, Cx, device=dt.device, dtype=dt.dtype)
+        dx[..., :creal] = dxp[:, :, pl: pl + W].to(dt.dtype)
+        return dx, None, None, None, None, None, None
+
+
 def row_pack(x, creal, S, sw, pl, Wo, Cp):
+    """See :func:`_row_pack`; differentiable when ``x`` requires a gradient."""
+    if x.requires_grad and torch.is_grad_enabled():
+        return _RowPackFn.apply(x, creal, S, sw, pl, Wo, Cp)
+    return _row_pack(x, creal, S, sw, pl, Wo, Cp)
+
+
+def _row_pack(x, creal, S, sw, pl, Wo, Cp):
     """Row packing of a few-channel image for its S-wide stem conv: t [N, H, Wo, Cp] with
     t[n, h, wo, s·creal + c] = x[n, h, wo·sw − pl + s, c] (zero outside the row, zero after
     S·creal).  A k×k conv over x equals a k×1 conv over t with the weight re-laid to

@@ -336,3 +336,19 @@ def test_row_packed_stem_matches_conv():
         assert torch.allclose(plain.weight.grad, packed.weight.grad, atol=1e-3, rtol=1e-4)
     t = C.row_pack(x, 3, 7, 2, 3, 18, 24)
     assert t.shape == (2, 29, 18, 24) and float(t[..., 21:].abs().sum()) == 0.0
+
+
+def test_row_pack_input_gradient():
+    """The packed stem's input gradient (the row-pack's transposed gather) = the plain conv's."""
+    from tensorflowdistributedlearning_amd.models.layers import Conv2d, RowPackedConv2d
+    torch.manual_seed(8)
+    plain = Conv2d(3, 8, 7, 2, "sym", pad_cin_to=8)
+    packed = RowPackedConv2d(3, 8, 7, 2, "sym", pad_cin_to=8)
+    packed.weight.data.copy_(plain.weight.data)
+    x = torch.randn(2, 21, 23, 8)
+    x[..., 3:] = 0
+    x0, x1 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    g = torch.randn(2, 11, 12, 8)
+    (plain(x0) * g).sum().backward()
+    (packed(x1) * g).sum().backward()
+    assert torch.allclose(x0.grad[..., :3], x1.grad[..., :3], atol=1e-4, rtol=1e-4)
