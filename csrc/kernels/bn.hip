@@ -172,7 +172,12 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     static const int cap = env_int("TDL_BN_RED_BLOCKS", 1024);
     static const int u = env_int("TDL_BN_RED_U", 4);
     static const int minr = env_int("TDL_BN_RED_MINR", 8);
-    long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * minr)));
+    // optional cap on the atomics per launch (every workgroup adds 2C partial sums): measured
+    // (tools/bn_micro.py) 1 Mi: b256 reduce total 2.92 -> 2.85 ms but b1024 8.43 -> 8.86 ms —
+    // fewer workgroups cost more bandwidth than the atomics save; off by default
+    static const long atom = env_int("TDL_BN_RED_ATOM", 1 << 30);
+    const long cap_atom = std::max<long>(128, atom / (2L * C));
+    long blocks = std::min<long>(std::min<long>(cap, cap_atom), std::max<long>(1, M / (rpp * minr)));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
     if (u == 8)
