@@ -541,19 +541,20 @@ def test_bucket_launch_sees_complete_gradients(gpu, early, monkeypatch):
         streams.set_enabled(old)
 
 
-def test_large_batch_matches_split_batches(gpu):
-    """Large per-GPU batches (the bench runs 512 images per MI355X): with frozen BN every sample is
-    independent, so a 768-image forward/backward must give the same logits as three 256-image
-    passes and the sum of their parameter gradients — catches 32-bit index / offset overflow and
-    tiling bugs that only appear at large M = N·H·W."""
+@pytest.mark.parametrize("batch", [768, 1024])
+def test_large_batch_matches_split_batches(gpu, batch):
+    """Large per-GPU batches (the bench runs 1024 images per MI355X): with frozen BN every sample
+    is independent, so a big forward/backward must give the same logits as 256-image passes and
+    the sum of their parameter gradients — catches 32-bit index / offset overflow and tiling bugs
+    that only appear at large M = N·H·W."""
     torch.manual_seed(13)
     m = models.resnet50(num_classes=10).to(gpu)
     m.train()
     for mod in m.modules():
         if mod.__class__.__name__ == "BatchNorm":
             mod.train(False)
-    x = torch.randn(768, 224, 224, 3, device=gpu, dtype=torch.bfloat16)
-    w = torch.randn(768, 10, device=gpu)
+    x = torch.randn(batch, 224, 224, 3, device=gpu, dtype=torch.bfloat16)
+    w = torch.randn(batch, 10, device=gpu)
 
     def run(xs, ws):
         for p in m.parameters():
@@ -563,7 +564,7 @@ def test_large_batch_matches_split_batches(gpu):
         return y.float(), torch.cat([p.grad.float().flatten() for p in m.parameters()])
     y_big, g_big = run(x, w)
     ys, gsum = [], 0
-    for i in range(3):
+    for i in range(batch // 256):
         y, g = run(x[256 * i:256 * (i + 1)], w[256 * i:256 * (i + 1)])
         ys.append(y)
         gsum = gsum + g
