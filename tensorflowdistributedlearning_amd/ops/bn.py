@@ -265,6 +265,8 @@ class _BatchNormActFn(torch.autograd.Function):
             deliver_grad(gamma, None if direct_g else red[1][:c], written=direct_g)
         if want_b:
             deliver_grad(beta, None if direct_b else red[0][:c], written=direct_b)
+        if ctx.mask_token is not None:
+            ctx.mask_token.release()
         return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None
 
 

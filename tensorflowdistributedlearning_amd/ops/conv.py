@@ -400,6 +400,7 @@ class _Conv2dFn(torch.autograd.Function):
                     else:
                         dx, red = dgrad(mask=tok.mask), None
                     tok.mark(dx, red)
+                    ctx.bn_tok = None
                 else:
                     dx = dgrad()
             else:  # residual-gradient join: first consumer writes, later ones accumulate

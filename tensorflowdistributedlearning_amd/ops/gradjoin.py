@@ -73,6 +73,13 @@ class MaskToken:
         """The fused (Σg, Σg·x) of ``g`` if its last writer produced them, else None."""
         return self.red if self.is_premasked(g) else None
 
+    def release(self):
+        """Drop the tensors once the BN backward has used them (the token is reachable from
+        autograd nodes that live until the whole backward ends: it must not pin x)."""
+        self.x = None
+        self.red = None
+        self.mask = None
+
 
 class GradJoin:
     __slots__ = ("n", "count", "buf", "mask_token", "unmasked", "red")
@@ -116,7 +123,8 @@ class GradJoin:
             return None
         if self.mask_token is not None and not self.unmasked and self.buf is not None:
             self.mask_token.mark(self.buf, self.red)
-        return self.buf
+        buf, self.buf = self.buf, None  # autograd owns it now: the join (kept by the graph
+        return buf                       # nodes until backward ends) must not pin it
 
 
 def make(n, x):
