@@ -186,8 +186,8 @@ def test_fused_bn_stats_match_reduce_pass(gpu, monkeypatch, frozen):
     conv2 outputs and the block outputs whose last gradient writer is a stride-1 dgrad) vs every
     BN running its reduce pass: the fused path is taken for most BNs and gives the same
     gradients.  Frozen BN (moving statistics): dx needs no batch sums, so dγ/dβ compare the fused
-    sums directly (cos > 0.9999); with batch statistics only the path and finiteness are checked
-    (see below).  Exact kernel semantics: test_kernels_gpu.py::test_conv_dgrad_bnstat."""
+    sums directly (cos > 0.9999); with batch statistics the path is checked (see below).
+    Exact kernel semantics: test_kernels_gpu.py::test_conv_dgrad_bnstat."""
     from tensorflowdistributedlearning_amd.ops import gradjoin
     from tensorflowdistributedlearning_amd.ops import bn as BN
     from tensorflowdistributedlearning_amd.ops.common import ext
@@ -199,6 +199,9 @@ def test_fused_bn_stats_match_reduce_pass(gpu, monkeypatch, frozen):
             if mod.__class__.__name__ == "BatchNorm":
                 mod.train(False)
     x = torch.randn(32, 128, 128, 8, device=gpu, dtype=torch.bfloat16)
+    # per-sample loss weights: a loss gradient identical for every sample is exactly what a
+    # batch-statistics BN backward subtracts out (g − mean g), leaving only rounding noise below
+    wts = torch.randn(32, 10, device=gpu)
     used = []
     orig = BN.bn_bwd_reduce
 
@@ -217,7 +220,7 @@ def test_fused_bn_stats_match_reduce_pass(gpu, monkeypatch, frozen):
             for p in m.parameters():
                 p.grad = None
             y = m(x)
-            (y.float() * torch.linspace(-1, 1, 10, device=gpu)).sum().backward()
+            (y.float() * wts).sum().backward()
             torch.cuda.synchronize()
             outs.append(torch.cat([p.grad.float().flatten() for p in m.parameters()
                                    if p.grad is not None]))
@@ -233,8 +236,10 @@ def test_fused_bn_stats_match_reduce_pass(gpu, monkeypatch, frozen):
     assert torch.isfinite(outs[2]).all()
     if frozen:
         assert cos > 0.9999, (cos, noise)
-    # batch statistics: two runs of the plain path already differ at cos ≈ 0.4–0.5 (fp32 atomic
-    # order amplified through 50 random-init BN layers), so no comparison is meaningful there
+    # With batch statistics two runs of the plain path already differ at cos ≈ 0.4–0.5: a deep
+    # random-init BN net amplifies the fp32 atomic-order differences of its batch sums
+    # exponentially with depth (BN's gradient explosion at initialisation), so only the path and
+    # finiteness are checked here; test_conv_dgrad_bnstat pins the sums themselves.
 
 
 @pytest.mark.parametrize("fuse_bn", [False, True])
