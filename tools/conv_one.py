@@ -19,7 +19,8 @@ from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", type=int, default=1)
-    ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--op", default="fwd", choices=["fwd", "dgrad", "wgrad", "dgrad_bnstat",
+                                                    "dgrad_reduce"])
     ap.add_argument("--shape", default="256,14,512,512,3,2,1")
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
@@ -31,6 +32,24 @@ def main():
     Ho, Wo = g.out_hw(H, H, k, k)
     dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
     ext().conv_set_glds_mode(a.mode)
+    if a.op in ("dgrad_bnstat", "dgrad_reduce"):
+        # BN-backward statistics: fused into the dgrad epilogue vs dgrad + the BN reduce pass
+        # (x plays the BN input; its ReLU bit mask and coefficients from a real BN forward)
+        from tensorflowdistributedlearning_amd.ops import bn as B
+        Cc = Cin
+        coef = B.bn_finalize(B.bn_stats(x), x.numel() // Cc, torch.ones(Cc, device=dev),
+                             torch.zeros(Cc, device=dev), torch.zeros(Cc, device=dev),
+                             torch.ones(Cc, device=dev), 0.9, 1e-5, True)
+        mask = torch.empty(x.numel() // 8, device=dev, dtype=torch.uint8)
+        yb = B.bn_apply(x, coef, None, True, mask=mask)
+        for _ in range(a.iters):
+            if a.op == "dgrad_bnstat":
+                C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask)
+            else:
+                B.bn_bwd_reduce(C.conv_dgrad(dy, w, x.shape, g), yb, x, coef, 2)
+        torch.cuda.synchronize()
+        print("done", a.mode, a.op, a.shape)
+        return
     for _ in range(a.iters):
         if a.op == "fwd":
             C.conv_fwd(x, w, g)
