@@ -432,6 +432,24 @@ void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t
                      dx.size(3), dy.size(1), dy.size(2), k, s, pt, pl, stream());
 }
 
+// maxpool backward with the producing BN's ReLU mask applied and its backward sums (Σg, Σg·x)
+// accumulated into bn_red fp32 [2, C] (zeroed by the caller); returns false (nothing launched)
+// when the channel count does not fit the kernel
+bool maxpool_bwd_stats(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t pt,
+                       int64_t pl, Tensor bn_x, Tensor mask, Tensor bn_red) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  CHECK_T(bn_x, torch::kBFloat16);
+  CHECK_T(bn_red, torch::kFloat32);
+  TORCH_CHECK(bn_x.sizes() == dx.sizes() && mask.is_cuda() && mask.scalar_type() == torch::kUInt8 &&
+              mask.numel() * 8 == dx.numel() && bn_red.numel() == 2 * dx.size(3),
+              "maxpool_bwd_stats: bn_x like dx, 1-bit mask, bn_red [2, C]");
+  return maxpool_bwd_stats_launch(BF(dy), idx.data_ptr<uint8_t>(), BFW(dx), BF(bn_x),
+                                  mask.data_ptr<uint8_t>(), bn_red.data_ptr<float>(), dx.size(0),
+                                  dx.size(1), dx.size(2), dx.size(3), dy.size(1), dy.size(2), k, s,
+                                  pt, pl, stream());
+}
+
 void avgpool_fwd(Tensor x, Tensor y) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -800,6 +818,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sigmoid_threshold", &sigmoid_threshold);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("maxpool_bwd_stats", &maxpool_bwd_stats);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("softmax_xent", &softmax_xent);

@@ -158,6 +158,12 @@ void sigmoid_threshold_launch(const void* x, bool x_bf16, float* prob, float* pr
 // pooling ------------------------------------------------------------------------------------
 void maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
                         int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
+// maxpool backward that also applies the producing BN's ReLU bit mask to dx and accumulates the
+// BN-backward sums (Σg, Σg·x) of the stored dx into red [2][C] (x = bx, the BN input); false (and
+// nothing launched) unless C % 8 == 0 and 256 % (C / 8) == 0
+bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, const bf16_t* bx,
+                              const uint8_t* mask, float* red, int N, int H, int W, int C, int Ho,
+                              int Wo, int k, int s, int pt, int pl, hipStream_t st);
 void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
 void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);

@@ -117,6 +117,80 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
   }
 }
 
+// maxpool backward + the BN-backward statistics of the BN (+ReLU) that produced the pool input
+// (ops/gradjoin.py fused statistics): dx = gathered dy · [ReLU bit], and (Σg, Σg·x) of the stored
+// dx with x = that BN's input — the BN backward then skips its reduce pass.  8-channel vectors;
+// NT % (C/8) == 0 so each thread's channel vector is fixed over the grid-stride loop.
+__global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
+    const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
+    const bf16_t* __restrict__ bx, const uint8_t* __restrict__ mask, float* __restrict__ red, int N,
+    int H, int W, int C, int Ho, int Wo, int k, int s, int pt, int pl) {
+  __shared__ float lds[2][NT][9];  // +1 pad against bank conflicts
+  const int cv = C / 8;
+  const long total = (long)N * H * W * cv;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * 8;
+    long p = t / cv;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const int n = (int)(p / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int hh = h + pt, ww = w + pl;
+    const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
+    const int ho_hi = min(Ho - 1, hh / s);
+    const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
+    const int wo_hi = min(Wo - 1, ww / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int r = hh - ho * s;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int want = r * k + (ww - wo * s);
+        const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+        float g[8];
+        unpack8(*(const uint4*)(dy + o), g);
+        const uint2 packed = *(const uint2*)(idx + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t word = j < 4 ? packed.x : packed.y;
+          if ((int)((word >> ((j & 3) * 8)) & 0xff) == want) acc[j] += g[j];
+        }
+      }
+    }
+    const long off = (((long)n * H + h) * W + w) * C + c;
+    const uint32_t mb = mask[off >> 3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = (mb >> j) & 1u ? acc[j] : 0.f;
+    const uint4 st = pack8(acc);
+    *(uint4*)(dx + off) = st;
+    float q[8], xv[8];
+    unpack8(st, q);  // statistics of the stored bf16 values
+    unpack8(*(const uint4*)(bx + off), xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s0[j] += q[j];
+      s1[j] = fmaf(q[j], xv[j], s1[j]);
+    }
+  }
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lds[0][tid][j] = s0[j];
+    lds[1][tid][j] = s1[j];
+  }
+  __syncthreads();
+  for (int o = tid; o < 2 * C; o += NT) {  // threads tid ≡ v (mod cv) hold channel vector v
+    const int which = o / C, c = o - which * C, v = c >> 3, j = c & 7;
+    float sum = 0.f;
+    for (int r = v; r < NT; r += cv) sum += lds[which][r][j];
+    atomicAdd(red + which * C + c, sum);
+  }
+}
+
 // global average pool: one thread per (n, channel vector), loop over HW
 __global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
                                    int HW, int C) {
@@ -197,6 +271,15 @@ void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N,
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<1>, dim3(blocks_for((long)N * H * W * C)), dim3(NT), 0, st,
                        dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+}
+
+bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, const bf16_t* bx,
+                              const uint8_t* mask, float* red, int N, int H, int W, int C, int Ho,
+                              int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+  if (C % 8 || NT % (C / 8)) return false;
+  hipLaunchKernelGGL(maxpool_bwd_stats_kernel, dim3(blocks_for((long)N * H * W * C / 8)), dim3(NT), 0,
+                     st, dy, idx, dx, bx, mask, red, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  return true;
 }
 
 void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {

@@ -16,6 +16,12 @@ import torch
 import torch.nn.functional as F
 
 from .common import on_gpu, ext
+from . import gradjoin
+from . import workspace
+
+import os
+
+POOL_STATS = os.environ.get("TDL_POOL_BNSTAT", "1") == "1"  # 0: the stem BN reduces itself
 
 
 def _out(size, k, s, pb, pa):
@@ -37,6 +43,9 @@ class _MaxPoolFn(torch.autograd.Function):
         Ho = _out(H, k, s, pad[0], pad[1])
         Wo = _out(W, k, s, pad[2], pad[3])
         ctx.k, ctx.s, ctx.pad, ctx.x_shape = k, s, pad, tuple(x.shape)
+        # ReLU-mask token of the producing BN (ops/gradjoin.py): the backward applies the mask
+        # and fuses that BN's backward sums (the ResNet stem: BN+ReLU → max-pool)
+        ctx.bn_tok = getattr(x, "_tdl_mask_token", None)
         if on_gpu(x):
             y = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
             idx = torch.empty((N, Ho, Wo, C), device=x.device, dtype=torch.uint8)
@@ -55,6 +64,14 @@ class _MaxPoolFn(torch.autograd.Function):
         if on_gpu(dy):
             (idx,) = ctx.saved_tensors
             dx = torch.empty(ctx.x_shape, device=dy.device, dtype=dy.dtype)
+            tok, ctx.bn_tok = ctx.bn_tok, None
+            if (tok is not None and tok.x is not None and tok.mask is not None
+                    and gradjoin.STATS_SINGLE and POOL_STATS):
+                red = workspace.zeros((2, ctx.x_shape[-1]), dy.device)
+                if ext().maxpool_bwd_stats(dy, idx, dx, ctx.k, ctx.s, ctx.pad[0], ctx.pad[2],
+                                           tok.x, tok.mask, red):
+                    tok.mark(dx, red)
+                    return dx, None, None, None
             ext().maxpool_bwd(dy, idx, dx, ctx.k, ctx.s, ctx.pad[0], ctx.pad[2])
             return dx, None, None, None
         xr, yr = ctx.saved_tensors

@@ -728,3 +728,30 @@ def test_row_packed_stem_gpu(gpu):
     (y1.float() * g.float()).sum().backward()
     torch.cuda.synchronize()
     assert rel_err(packed.weight.grad, plain.weight.grad) < 1e-2
+
+
+def test_maxpool_bwd_bnstat(gpu):
+    """Max-pool backward with the producing BN's ReLU mask and its backward sums fused
+    (maxpool_bwd_stats): dx = plain gathered dx · [bit] exactly, (Σg, Σg·x) vs fp32."""
+    torch.manual_seed(23)
+    N, H, W, Cc = 4, 30, 30, 64
+    x = (torch.randn(N, H, W, Cc) * 1.2 + 0.2).bfloat16().to(gpu)  # BN input
+    coef = B.bn_finalize(B.bn_stats(x), N * H * W, torch.ones(Cc, device=gpu),
+                         torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu),
+                         torch.ones(Cc, device=gpu), 0.9, 1e-3, True)
+    mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+    y = B.bn_apply(x, coef, None, True, mask=mask)
+    pad = (1, 1, 1, 1)
+    pooled = P.max_pool2d(y, 3, 2, pad)
+    dy = torch.randn_like(pooled)
+    idx = torch.empty(pooled.shape, device=gpu, dtype=torch.uint8)
+    ext().maxpool_fwd(y, torch.empty_like(pooled), idx, 3, 2, 1, 1)
+    plain = torch.empty_like(y)
+    ext().maxpool_bwd(dy, idx, plain, 3, 2, 1, 1)
+    keep = B.unpack_relu_mask(mask, Cc).reshape(y.shape)
+    dx = torch.empty_like(y)
+    red = torch.zeros(2, Cc, device=gpu)
+    assert ext().maxpool_bwd_stats(dy, idx, dx, 3, 2, 1, 1, x, mask, red)
+    assert torch.equal(dx, (plain.float() * keep).bfloat16())
+    gf, xf = dx.float().reshape(-1, Cc), x.float().reshape(-1, Cc)
+    assert rel_err(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-4
