@@ -881,7 +881,13 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
     // 1×1 filters with 64 input channels (dx width): 8-wave 256×64 tiles (49 vs 88 µs on
     // ResNet-50 56×56 64→64, tools/n64_configs.py)
     const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
-    if (mode == 1 && (Mmax_total < 4096 || (a0.Ng < 128 && !n64_1x1))) return false;
+    // with fused BN statistics the 64-wide 3×3 dgrads too (ResNet-50 layer1 conv2: the LDS-DMA
+    // 8-wave 256×64 dgrad is within 5 % of the register-staged one, and the fusion saves the BN's
+    // reduce pass; TDL_DGSTAT_N64=0 turns it off)
+    static const bool n64_stats_on = env_int("TDL_DGSTAT_N64", 1) != 0;
+    const bool n64_stats = n64_stats_on && a0.stats && a0.bn_x && a0.Ng > 48 && a0.Ng <= 64 &&
+                           a0.ncls == 1 && a0.sh == 1 && a0.sw == 1 && a0.K % 64 == 0;
+    if (mode == 1 && (Mmax_total < 4096 || (a0.Ng < 128 && !n64_1x1 && !n64_stats))) return false;
   }
   ConvArgs a = a0;
   a.dbg = env_int("TDL_CONV_DBG", 0);
