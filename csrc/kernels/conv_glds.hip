@@ -906,8 +906,11 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   // BN-backward statistics in the epilogue (a.stats, a.bn_x): stride 1 (one class covering
   // every pixel), FASTK; tiles in the forward's column-grouped order (tile_of COLG) so each
   // workgroup flushes its column sums once
-  const bool bn_stats = a.stats && a.bn_x && !a.fp8 && a.ncls == 1 && a.sh == 1 && a.sw == 1 &&
-                        a.K % 64 == 0;
+  // (strided dgrads: every parity class in the same order, each class's tiles padded to whole
+  // workgroups so none straddles two classes; a class without taps was zero-filled and adds 0;
+  // joins need stride 1 — an accumulate leaves the pixels of such a class unmasked)
+  const bool bn_stats = a.stats && a.bn_x && !a.fp8 && a.K % 64 == 0 &&
+                        (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1));
   if (bn_stats) {
     // tile config (tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
     // tiles (NJ: no previous-dx registers); with the join's previous-dx loads as well they spill,
@@ -915,15 +918,25 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
     const int scfg = env_int(a.beta ? "TDL_GLDS_CFG_DGSTAT_J" : "TDL_GLDS_CFG_DGSTAT",
                              a.Ng <= 64 ? 4 : (a.beta ? 6 : 0));
     const GCfg& g = cfg_of(scfg);
-    const long ntm = cdiv((long)a.N * a.cls_Hc[0] * a.cls_Wc[0], g.bm), ntn = cdiv(a.Ng, g.bn);
-    a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm * ntn)), ntm);
-    const long groups = (ntm + a.tpb - 1) / a.tpb;
-    a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+    const long ntn = cdiv(a.Ng, g.bn);
+    long ntm_all = 0, ntm_max = 1;
+    for (int c = 0; c < a.ncls; ++c) {
+      const long ntm_c = cdiv((long)a.N * a.cls_Hc[c] * a.cls_Wc[c], g.bm);
+      ntm_all += ntm_c;
+      ntm_max = std::max(ntm_max, ntm_c);
+    }
+    a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm_all * ntn)), ntm_max);
+    a.cls_tile0[0] = 0;
+    for (int c = 0; c < a.ncls; ++c) {
+      const long groups_c = cdiv(cdiv((long)a.N * a.cls_Hc[c] * a.cls_Wc[c], g.bm), a.tpb);
+      a.cls_tile0[c + 1] = a.cls_tile0[c] + (int)(groups_c * ntn * a.tpb);
+    }
+    const int blocks = a.cls_tile0[a.ncls] / a.tpb;
     a.splits = 1;
     if (a.beta)
-      launch_gcfg<DGRAD, true, false, 1>(a, scfg, (int)(groups * ntn), st);
+      launch_gcfg<DGRAD, true, false, 1>(a, scfg, blocks, st);
     else
-      launch_gcfg<DGRAD, true, false, 1, true>(a, scfg, (int)(groups * ntn), st);
+      launch_gcfg<DGRAD, true, false, 1, true>(a, scfg, blocks, st);
     if (fused) *fused = true;
     return true;
   }

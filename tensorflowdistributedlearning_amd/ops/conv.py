@@ -184,8 +184,8 @@ def conv_dgrad_bnstat(dy, w, x_shape, geom: ConvGeom, bn_x, out=None, accumulate
                                  bool(accumulate and out is not None), mask, None, bn_x, red)
         return dx, (red if fused else None)
     dx = conv_dgrad(dy, w, x_shape, geom, out=out, accumulate=accumulate, mask=mask)
-    if geom.stride != (1, 1):
-        return dx, None
+    if accumulate and out is not None and geom.stride != (1, 1):
+        return dx, None  # a strided accumulate leaves untouched pixels unmasked
     C = x_shape[-1]
     g = dx.float().reshape(-1, C)
     red = torch.stack([g.sum(0), (g * bn_x.float().reshape(-1, C)).sum(0)])
@@ -388,7 +388,7 @@ class _Conv2dFn(torch.autograd.Function):
                                       mask=mask)
             join = ctx.join
             masks_ok = on_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
-            stats_ok = masks_ok and not fp8_dg and geom.stride == (1, 1)
+            stats_ok = masks_ok and not fp8_dg  # (the kernel decides; strided: parity classes)
             if join is None:
                 tok = ctx.bn_tok
                 if tok is not None and masks_ok:
@@ -409,7 +409,8 @@ class _Conv2dFn(torch.autograd.Function):
                 if join.buf is None:
                     join.buf = dgrad(mask=mask)
                     join.note(mask is not None)
-                elif join.last and mask is not None and stats_ok and join.stats_x is not None:
+                elif (join.last and mask is not None and stats_ok and geom.stride == (1, 1)
+                      and join.stats_x is not None):
                     # the final contribution writes every pixel through the mask: its epilogue
                     # sees the finished gradient and can fuse the BN statistics
                     _, join.red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, join.stats_x,

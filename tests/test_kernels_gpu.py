@@ -421,7 +421,9 @@ def test_conv_dgrad_relu_mask(gpu, conv_impl, shape, accumulate):
                                    (8, 14, 14, 128, 128, 3, 1, False),   # 3x3
                                    (8, 28, 28, 256, 64, 1, 1, True),     # join accumulate
                                    (8, 30, 30, 192, 128, 1, 1, False),   # ragged column tiles
-                                   (8, 28, 28, 128, 128, 3, 2, False)])  # strided: not fused
+                                   (8, 28, 28, 128, 128, 3, 2, False),   # strided: 4 classes
+                                   (8, 28, 28, 128, 256, 1, 2, False),   # 1x1/s2: zero classes
+                                   (8, 28, 28, 256, 128, 1, 2, True)])   # strided join: no
 def test_conv_dgrad_bnstat(gpu, shape):
     """BN-backward statistics fused into the LDS-DMA dgrad epilogue (ops/gradjoin.py): dx is
     bit-identical to the plain masked dgrad, and (Σg, Σg·x) of the stored dx match an fp32
@@ -451,7 +453,7 @@ def test_conv_dgrad_bnstat(gpu, shape):
     finally:
         ext().conv_set_glds_mode(-1)
     assert torch.equal(dx, ref)
-    if st != 1:
+    if st != 1 and join:
         assert red is None
         return
     assert red is not None

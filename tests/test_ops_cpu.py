@@ -309,9 +309,13 @@ def test_conv_dgrad_bnstat_cpu_oracle():
     d0, _ = B.bn_bwd_apply(dx, None, x, coef, want, gam, 162, 0, False)
     d1, _ = B.bn_bwd_apply(dx, None, x, coef, red, gam, 162, 0, False, red_raw=True)
     assert torch.allclose(d0, d1, rtol=1e-4, atol=1e-5)
-    # strided dgrads do not fuse
-    _, r2 = C.conv_dgrad_bnstat(dy[:, ::2, ::2], w, x.shape, C.ConvGeom((2, 2), (1, 1, 1, 1)), x)
-    assert r2 is None
+    # strided dgrads fuse (parity classes) unless they accumulate into a join
+    g2 = C.ConvGeom((2, 2), (1, 1, 1, 1))
+    dx2, r2 = C.conv_dgrad_bnstat(dy[:, ::2, ::2].contiguous(), w, x.shape, g2, x)
+    assert r2 is not None and torch.allclose(r2[0], dx2.reshape(-1, 16).sum(0), atol=1e-4)
+    _, r3 = C.conv_dgrad_bnstat(dy[:, ::2, ::2].contiguous(), w, x.shape, g2, x, out=dx2.clone(),
+                                accumulate=True)
+    assert r3 is None
 
 
 def test_row_packed_stem_matches_conv():
