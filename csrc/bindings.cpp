@@ -351,6 +351,19 @@ void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Te
                        red.data_ptr<float>(), x.numel() / C, C, (int)relu, stream());
 }
 
+bool bn_bwd_reduce2(Tensor dy, Tensor x, Tensor x2, Tensor coef, Tensor red, Tensor red2) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(x2, torch::kBFloat16);
+  CHECK_T(red, torch::kFloat32);
+  CHECK_T(red2, torch::kFloat32);
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(x2.sizes() == x.sizes() && dy.sizes() == x.sizes() && red.numel() == 2 * C &&
+              red2.numel() == 2 * C, "bn_bwd_reduce2: dy, x, x2 of one shape, red / red2 [2, C]");
+  return bn_bwd_reduce2_launch(BF(dy), BF(x), BF(x2), coef.data_ptr<float>(), red.data_ptr<float>(),
+                               red2.data_ptr<float>(), x.numel() / C, C, stream());
+}
+
 void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red,
                   c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres,
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
@@ -780,6 +793,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_ring") = py::none(),
         py::arg("phase") = 0, py::arg("scale_out") = py::none(), py::arg("mask") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_reduce2", &bn_bwd_reduce2);
   m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("coef"),
         py::arg("red"), py::arg("gamma"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("count"), py::arg("relu"), py::arg("dx8") = py::none(),

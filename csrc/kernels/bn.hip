@@ -161,6 +161,83 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
   }
 }
 
+// Backward sums of two BNs fed the same gradient g = dy (no ReLU mask left: the residual BN of a
+// downsampling bottleneck and its shortcut BN, whose output the residual BN adds): one pass reads
+// dy once for both — out = (Σg, Σg·x̂) of x (coef), out2 = (Σg, Σg·x2) raw (bn_bwd_apply
+// red_raw).  Same thread layout as reduce_vec_kernel (C % 8 == 0, C / 8 <= NT).
+template <int U>
+__global__ void __launch_bounds__(NT) reduce2_vec_kernel(const bf16_t* __restrict__ a,
+                                                         const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ x2,
+                                                         const float* __restrict__ coef,
+                                                         float* __restrict__ out,
+                                                         float* __restrict__ out2, long M, int C,
+                                                         long rows_per_block) {
+  __shared__ float red[3][NT][9];
+  const int cvecs = C >> 3;
+  const int rpp = NT / cvecs;
+  const int t = threadIdx.x;
+  const int cv = t % cvecs, rl = t / cvecs;
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s0[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = s2[j] = 0.f;
+  if (rl < rpp) {
+    float mean[8], inv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mean[j] = coef[2 * C + cv * 8 + j];
+      inv[j] = coef[3 * C + cv * 8 + j];
+    }
+    for (long r = r0 + rl; r < r1; r += U * rpp) {
+      uint4 la[U], lx[U], lx2[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long rr = r + u * rpp;
+        const long off = (rr < r1 ? rr : r) * C + cv * 8;
+        la[u] = *(const uint4*)(a + off);
+        lx[u] = *(const uint4*)(x + off);
+        lx2[u] = *(const uint4*)(x2 + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + u * rpp >= r1) break;
+        float va[8], vx[8], vx2[8];
+        unpack(la[u], va);
+        unpack(lx[u], vx);
+        unpack(lx2[u], vx2);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s0[j] += va[j];
+          s1[j] += va[j] * ((vx[j] - mean[j]) * inv[j]);
+          s2[j] = fmaf(va[j], vx2[j], s2[j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][t][j] = s0[j];
+    red[1][t][j] = s1[j];
+    red[2][t][j] = s2[j];
+  }
+  __syncthreads();
+  for (int o = t; o < 3 * C; o += NT) {
+    const int which = o / C, c = o - which * C;
+    const int v = c >> 3, j = c & 7;
+    float sum = 0.f;
+    for (int r = 0; r < rpp; ++r) sum += red[which][r * cvecs + v][j];
+    if (which == 0) {
+      atomicAdd(out + c, sum);
+      atomicAdd(out2 + c, sum);
+    } else if (which == 1) {
+      atomicAdd(out + C + c, sum);
+    } else {
+      atomicAdd(out2 + C + c, sum);
+    }
+  }
+}
+
 template <int KIND>
 void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const float* coef, float* out,
                    long M, int C, int relu, hipStream_t st) {
@@ -553,6 +630,19 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                           float* red, long M, int C, int relu, hipStream_t st) {
   reduce_launch<1>(dy, y, x, coef, red, M, C, relu, st);
+}
+
+bool bn_bwd_reduce2_launch(const bf16_t* dy, const bf16_t* x, const bf16_t* x2, const float* coef,
+                           float* red, float* red2, long M, int C, hipStream_t st) {
+  if (M <= 0 || C % 8 || C / 8 > NT) return false;
+  const int cvecs = C / 8, rpp = NT / cvecs;
+  static const int cap = env_int("TDL_BN_RED_BLOCKS", 1024);
+  long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * 8)));
+  const long rpb = (M + blocks - 1) / blocks;
+  blocks = (M + rpb - 1) / rpb;
+  hipLaunchKernelGGL((reduce2_vec_kernel<4>), dim3(blocks), dim3(NT), 0, st, dy, x, x2, coef, red, red2,
+                     M, C, rpb);
+  return true;
 }
 
 void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,

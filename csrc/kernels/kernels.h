@@ -131,6 +131,10 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
                      uint8_t* mask = nullptr);  // mask: 1 bit per element of y > 0 (C % 8 == 0)
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
                           float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0, 3 bit mask (y = uint8 mask, C % 8 == 0, C <= 2048)
+// two BNs fed the same (unmasked) gradient dy: red = (Σdy, Σdy·x̂) of x (coef), red2 = (Σdy,
+// Σdy·x2) raw; false (nothing launched) unless C % 8 == 0 and C <= 2048
+bool bn_bwd_reduce2_launch(const bf16_t* dy, const bf16_t* x, const bf16_t* x2, const float* coef,
+                           float* red, float* red2, long M, int C, hipStream_t st);
 // optional e5m2 side output of dx (fp8 dgrad of the producing conv), delayed scaling as
 // bn_apply's e4m3 one: dx8 = e5m2(sat(dx·57344/amax_prev)), scale_out = amax_prev/57344,
 // this call's |dx|max into amax_out, amax_zero cleared (C % 8 == 0 only)

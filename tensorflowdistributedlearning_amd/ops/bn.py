@@ -17,6 +17,8 @@ with ``UPDATE_OPS`` moving averages (model.py:465-467) — TF FusedBatchNorm/Fus
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .common import on_gpu, ext, deliver_grad, grad_target, flat_view
@@ -128,6 +130,26 @@ def bn_bwd_reduce(dy, y, x, coef, relu):
     return torch.stack([g.sum(0), (g * xhat).sum(0)])
 
 
+PAIR_STATS = os.environ.get("TDL_BNSTAT_PAIR", "1") == "1"
+
+
+def bn_bwd_reduce2(dy, x, coef, x2):
+    """Backward sums of two BNs fed the same gradient ``dy`` (no mask): ((Σdy, Σdy·x̂) of ``x``,
+    (Σdy, Σdy·x2) raw) — the residual BN of a downsampling bottleneck and its shortcut BN, in
+    one pass that reads dy once.  None when the kernel does not take the shape."""
+    C = x.shape[-1]
+    if on_gpu(dy):
+        red = workspace.zeros((2, C), dy.device)
+        red2 = workspace.zeros((2, C), dy.device)
+        if not ext().bn_bwd_reduce2(dy, x, x2, coef, red, red2):
+            return None
+        return red, red2
+    g = dy.float().reshape(-1, C)
+    xhat = (x.float().reshape(-1, C) - coef[2]) * coef[3]
+    return (torch.stack([g.sum(0), (g * xhat).sum(0)]),
+            torch.stack([g.sum(0), (g * x2.float().reshape(-1, C)).sum(0)]))
+
+
 def bn_red_xhat(red, coef):
     """(Σg, Σg·x̂) from the raw (Σg, Σg·x) a fused dgrad epilogue accumulated:
     Σg·x̂ = invstd·(Σg·x − mean·Σg)."""
@@ -201,6 +223,16 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.mask_token = None
         if mask is not None:  # the consumers' dgrads may apply it for us (ops/gradjoin.py)
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask, x)
+        elif (not relu and residual is None and need_grad and on_gpu(x) and PAIR_STATS
+              and gradjoin.STATS_ENABLED):
+            # no ReLU: a statistics-only token — the residual BN this output feeds (a shortcut
+            # BN) computes both BNs' backward sums in one pass over the shared gradient
+            ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(None, x)
+        ctx.res_tok = None
+        if residual is not None:
+            rt = getattr(residual, "_tdl_mask_token", None)
+            if rt is not None and rt.mask is None and rt.x is not None:
+                ctx.res_tok = rt
         ctx.count = count
         ctx.bn = bn
         ctx.training = training
@@ -242,6 +274,14 @@ class _BatchNormActFn(torch.autograd.Function):
         # (Σg, Σg·x) fused into the last writer's dgrad epilogue, else a reduce pass
         red = ctx.mask_token.red if premasked else None
         red_raw = red is not None
+        rt, ctx.res_tok = ctx.res_tok, None
+        if red is None and premasked and rt is not None and rt.x is not None \
+                and tuple(rt.x.shape) == tuple(x.shape):
+            # the shortcut BN gets this same gradient (dres = dy): both sums in one pass
+            pair = bn_bwd_reduce2(dy, x, coef, rt.x)
+            if pair is not None:
+                red = pair[0]
+                rt.mark(dy, pair[1])
         if red is None:
             red = bn_bwd_reduce(dy, y, x, coef, relu)
         want_g = gamma is not None and gamma.requires_grad

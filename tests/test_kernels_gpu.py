@@ -757,3 +757,22 @@ def test_maxpool_bwd_bnstat(gpu):
     assert torch.equal(dx, (plain.float() * keep).bfloat16())
     gf, xf = dx.float().reshape(-1, Cc), x.float().reshape(-1, Cc)
     assert rel_err(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-4
+
+
+def test_bn_bwd_reduce2_matches_two_reduces(gpu):
+    """One pass for the two BNs of a downsampling bottleneck (residual BN + shortcut BN, same
+    gradient): (Σg, Σg·x̂) of x and raw (Σg, Σg·x2) = two separate reduce passes."""
+    torch.manual_seed(29)
+    Cc = 256
+    x = (torch.randn(8, 14, 14, Cc) + 0.3).bfloat16().to(gpu)
+    x2 = (torch.randn(8, 14, 14, Cc) * 0.7 - 0.2).bfloat16().to(gpu)
+    dy = torch.randn(8, 14, 14, Cc).bfloat16().to(gpu)
+    M = 8 * 14 * 14
+    mk = lambda t: B.bn_finalize(B.bn_stats(t), M, torch.ones(Cc, device=gpu),  # noqa: E731
+                                 torch.zeros(Cc, device=gpu), torch.zeros(Cc, device=gpu),
+                                 torch.ones(Cc, device=gpu), 0.9, 1e-3, True)
+    c1, c2 = mk(x), mk(x2)
+    red, red2 = B.bn_bwd_reduce2(dy, x, c1, x2)
+    torch.testing.assert_close(red, B.bn_bwd_reduce(dy, None, x, c1, 0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(B.bn_red_xhat(red2, c2), B.bn_bwd_reduce(dy, None, x2, c2, 0),
+                               rtol=1e-3, atol=1e-2)
