@@ -3,8 +3,16 @@
 data-parallel over N MI355X GPUs (one process per GPU, RCCL all-reduce overlapped with backward).
 
   python bench.py --gpus 1 --steps 20 --warmup 5
+  python bench.py --gpus 8                 # self-launches 8 worker processes (one per GPU)
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
       --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+With ``--gpus N > 1`` and no launcher environment (WORLD_SIZE unset) the process starts N fresh
+worker processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 set and
+relays their exit status; it never touches the GPU itself.  Under torchrun it is one of the
+workers.  Every GPU rank count > 1 runs its collectives on the native RCCL communicator, and the
+run fails unless RCCL itself (``ncclCommCount``) reports N ranks; the JSON line carries that
+count as ``config.rccl_ranks``.
 
 Metric (BASELINE.json): images/sec for the whole node (weak scaling: per-GPU batch fixed).
 Timing: W untimed warmup steps, then barrier + device sync, K timed steps, device sync + barrier;
@@ -22,20 +30,65 @@ import os
 import sys
 import time
 
-import torch
+import signal
+import socket
+import subprocess
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown  # noqa: E402
-from tensorflowdistributedlearning_amd.ops import streams  # noqa: E402
-from tensorflowdistributedlearning_amd.engine.trainer import Trainer  # noqa: E402
-from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy, lovasz_hinge  # noqa: E402
-from tensorflowdistributedlearning_amd.data.synthetic import imagenet_batch, segmentation_batch  # noqa: E402
-from tensorflowdistributedlearning_amd import models  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 METRIC = "images/sec (whole node), ResNet-50 224x224 bf16 at 1/2/4/8 MI355X"
 REF_PER_GPU_DERIVED = 86.0   # ResNet-50-equivalent at the reference's FLOP rate
 REF_DEEPLAB_2GPU = 90.7      # measured, 2 GPUs, global batch 64
+
+
+def launch_workers(n: int, argv) -> int:
+    """Start ``n`` worker processes of this script (one per GPU) and relay their exit status.
+
+    The parent imports nothing that touches the GPU.  Rank 0's stdout (the JSON line) and every
+    rank's stderr are inherited.  If any worker fails, the others are terminated (SIGTERM, then
+    SIGKILL after 15 s) so a dead rank cannot leave its peers blocked in a collective."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env, cwd=os.getcwd(), start_new_session=False))
+    def forward(sig, _frame):  # a signal to the launcher (e.g. `timeout`) reaches every worker
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(sig)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                print(f"[bench] worker pid {p.pid} exited with {r}; stopping the others",
+                      file=sys.stderr, flush=True)
+                for q in alive:
+                    q.send_signal(signal.SIGTERM)
+                t0 = time.time()
+                while any(q.poll() is None for q in alive) and time.time() - t0 < 15:
+                    time.sleep(0.2)
+                for q in alive:
+                    if q.poll() is None:
+                        q.kill()
+                        q.wait()
+                alive = []
+        time.sleep(0.05)
+    return rc
 
 
 def main():
@@ -50,13 +103,12 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--first-bucket-mb", type=float, default=4.0)
     ap.add_argument("--lr", type=float, default=0.1)
-    ap.add_argument("--comm", choices=["torch", "rccl"], default=os.environ.get("TDL_COMM", "torch"),
-                    help="gradient all-reduce backend: torch.distributed ProcessGroupNCCL (RCCL) or "
-                         "the native RCCL communicator with watchdog (parallel/rccl.py)")
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 GEMMs on the CDNA4 16x16x128 f8f6f4 MFMA for every eligible conv: "
-                         "forward e4m3 x e4m3, input gradient e5m2 x e4m3 (TDL_FP8_DGRAD=0: "
-                         "forward only); weight gradients stay bf16")
+                         "forward e4m3 activations x e4m3 weights; weight and input gradients "
+                         "stay bf16")
+    ap.add_argument("--fp8-dgrad", action="store_true",
+                    help="with --fp8: also the input gradients on fp8 (e5m2 x e4m3; experimental)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step as a HIP graph and replay it (removes "
                          "host launch overhead in launch-bound configs; with N>1 the bucketed "
@@ -66,25 +118,45 @@ def main():
                          "device events) to stderr")
     args = ap.parse_args()
 
-    if args.graph and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        args.comm = "rccl"  # collectives inside the captured step: native RCCL communicator
-    ctx = init_distributed(comm=args.comm)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
+
+    import torch
+    from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown
+    from tensorflowdistributedlearning_amd.ops import streams
+    from tensorflowdistributedlearning_amd.engine.trainer import Trainer
+    from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy, lovasz_hinge
+    from tensorflowdistributedlearning_amd.data.synthetic import imagenet_batch, segmentation_batch
+    from tensorflowdistributedlearning_amd import models
+
+    ctx = init_distributed()
     n = ctx.world_size
-    if n != args.gpus and ctx.is_main:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}", file=sys.stderr)
+    if n != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {n}")
     dev = ctx.device
+    rccl_ranks = ctx.rccl_ranks
+    if dev.type == "cuda" and n > 1 and os.environ.get("TDL_SHARE_GPU") != "1" \
+            and rccl_ranks != args.gpus:
+        raise SystemExit(f"RCCL reports {rccl_ranks} ranks, --gpus {args.gpus}")
+    comm = "rccl" if ctx.native is not None else ("gloo" if n > 1 else "none")
+    # CPU (plumbing runs, tests): fp32 storage, the PyTorch reference ops
+    lowp = torch.bfloat16 if dev.type == "cuda" else None
+    ddt = torch.bfloat16 if dev.type == "cuda" else torch.float32
     torch.manual_seed(1234)
+    fp8_desc = None
+    if args.model == "deeplab_ref" and args.fp8:
+        raise SystemExit("--fp8 is for the ImageNet models")
 
     if args.model == "deeplab_ref":
         per_gpu = args.batch or max(64 // n, 1)
         model = models.DeepLabResNet(model_name="model", input_shape=(101, 101))
         tr = Trainer(model, lovasz_hinge, dev, "adam", dict(lr=1e-3), ctx=ctx,
                      bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
-                     profile_phases=args.profile_phases)
-        x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank)
+                     profile_phases=args.profile_phases, lowp_dtype=lowp)
+        x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank, dtype=ddt)
         metric = "images/sec (whole node), reference DeepLab-ResNet 101x101x2 bf16"
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
-               "image": "101x101x2", "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "adam",
+               "image": "101x101x2", "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks, "optimizer": "adam",
                "loss": "lovasz_hinge", "hip_graph": args.graph,
                "wgrad_side_stream": streams.enabled()}
         base = REF_DEEPLAB_2GPU / 2 * n
@@ -95,18 +167,22 @@ def main():
         per_gpu = args.batch or 1024
         model = models.build(args.model, num_classes=1000)
         if args.fp8:
-            models.enable_fp8(model)
+            models.enable_fp8(model, dgrad=args.fp8_dgrad or None)
+            fp8_desc = ("fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad + BN)"
+                        if args.fp8_dgrad else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / "
+                        "wgrad + BN)")
         tr = Trainer(model, softmax_cross_entropy, dev, "sgd",
                      dict(lr=args.lr, momentum=0.9, weight_decay=5e-5), ctx=ctx,
                      bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
-                     profile_phases=args.profile_phases)
-        x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank)
+                     profile_phases=args.profile_phases, lowp_dtype=lowp)
+        x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank, dtype=ddt)
         metric = METRIC if args.model == "resnet50" and args.image_size == 224 and not args.fp8 \
             else (f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} "
-                  f"{'fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad)' if args.fp8 else 'bf16'}")
+                  f"{fp8_desc if args.fp8 else 'bf16' if dev.type == 'cuda' else 'fp32'}")
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
-               "parallelism": f"dp{n}", "comm": args.comm, "optimizer": "sgd_momentum",
+               "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks,
+               "optimizer": "sgd_momentum",
                "loss": "softmax_ce", "hip_graph": args.graph,
                "wgrad_side_stream": streams.enabled()}
         base = REF_PER_GPU_DERIVED * n
@@ -156,7 +232,8 @@ def main():
             "baseline": ("BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
                          "ResNet-50 number)" if args.model != "deeplab_ref" else
                          "BASELINE.md measured 90.7 img/s on 2 GPUs, scaled per GPU"),
-            "dtype": "fp8 (e4m3 fwd / e5m2 dgrad, bf16 wgrad + BN)" if args.fp8 else "bf16",
+            "dtype": (fp8_desc if args.fp8 else
+                      "bf16" if dev.type == "cuda" else "fp32 (CPU plumbing run)"),
             "data": "synthetic (device-resident random batch, random-init weights)",
             "config": cfg}), flush=True)
     shutdown()

@@ -692,6 +692,9 @@ struct PyComm {
     debug_spin_launch(ms, cs.stream());
     return track ? (int64_t)c->track("debug_delay", cs.stream()) : 0;
   }
+  // watch the work queued so far on the current (compute) stream like a collective — a HIP-graph
+  // replay whose captured collectives hang is then timed out by the watchdog as well
+  int64_t track_current(const std::string& name) { return (int64_t)c->track(name.c_str(), stream()); }
 };
 
 struct PyLoader {
@@ -868,6 +871,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("wait", &PyComm::wait)
       .def("synchronize", &PyComm::synchronize)
       .def("debug_delay", &PyComm::debug_delay, py::arg("ms"), py::arg("track") = false)
+      .def("track_current", &PyComm::track_current, py::arg("name") = "graph_replay")
+      .def_property_readonly("rccl_count", [](PyComm& p) { return p.c->rccl_count(); })
+      .def_property_readonly("rccl_rank", [](PyComm& p) { return p.c->rccl_rank(); })
+      .def_property_readonly("rccl_device", [](PyComm& p) { return p.c->rccl_device(); })
       .def("abort", [](PyComm& p, const std::string& why) { p.c->abort(why); })
       .def_property_readonly("error", [](PyComm& p) { return p.c->error(); })
       .def_property_readonly("ok", [](PyComm& p) { return p.c->ok(); })

@@ -331,9 +331,12 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
   float inv8 = 0.f, vmax = 0.f;
   bool emit8 = false;
   if (amax_out) {
-    const float ap = amax_read(amax_prev);
-    emit8 = y8 != nullptr && ap > 0.f;
-    inv8 = ap > 0.f ? 448.f / ap : 0.f;
+    // a zero (or never-set) previous |y|max falls back to unit scale: the e4m3 copy is always
+    // written when requested, so a consumer never reads uninitialised bytes
+    const float ap0 = amax_read(amax_prev);
+    const float ap = ap0 > 0.f ? ap0 : 448.f;
+    emit8 = y8 != nullptr;
+    inv8 = 448.f / ap;
     if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = ap / 448.f;
     amax_clear(amax_zero);  // the slot the next call accumulates into
   }
@@ -451,9 +454,13 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
   float inv8 = 0.f, vmax = 0.f;
   bool emit8 = false;
   if (amax_out) {
-    const float ap = amax_read(amax_prev) * 4.f;
-    emit8 = dx8 != nullptr && ap > 0.f;
-    inv8 = ap > 0.f ? 57344.f / ap : 0.f;
+    // a zero previous |dx|max (e.g. a step whose loss gradient was exactly zero) falls back to
+    // unit scale: dx8 is always written when requested (values clamped to ±57344), never left
+    // as uninitialised bytes behind a zero scale
+    const float ap0 = amax_read(amax_prev) * 4.f;
+    const float ap = ap0 > 0.f ? ap0 : 57344.f;
+    emit8 = dx8 != nullptr;
+    inv8 = 57344.f / ap;
     if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = ap / 57344.f;
     amax_clear(amax_zero);
   }

@@ -230,6 +230,30 @@ std::string Communicator::error() const {
   return error_;
 }
 
+int Communicator::rccl_count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!comm_) throw std::runtime_error("RCCL communicator failed: " + error_);
+  int n = 0;
+  check_nccl(ncclCommCount((ncclComm_t)comm_, &n), "ncclCommCount");
+  return n;
+}
+
+int Communicator::rccl_rank() const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!comm_) throw std::runtime_error("RCCL communicator failed: " + error_);
+  int r = -1;
+  check_nccl(ncclCommUserRank((ncclComm_t)comm_, &r), "ncclCommUserRank");
+  return r;
+}
+
+int Communicator::rccl_device() const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!comm_) throw std::runtime_error("RCCL communicator failed: " + error_);
+  int d = -1;
+  check_nccl(ncclCommCuDevice((ncclComm_t)comm_, &d), "ncclCommCuDevice");
+  return d;
+}
+
 size_t Communicator::outstanding() const {
   std::lock_guard<std::mutex> g(mu_);
   return works_.size();

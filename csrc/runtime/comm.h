@@ -65,6 +65,11 @@ class Communicator {
   void abort(const std::string& why);
   int rank() const { return rank_; }
   int world() const { return world_; }
+  // what RCCL itself reports for this communicator (ncclCommCount / ncclCommUserRank /
+  // ncclCommCuDevice) — the bench cross-checks the rank count against its --gpus
+  int rccl_count() const;
+  int rccl_rank() const;
+  int rccl_device() const;
   size_t outstanding() const;
 
  private:

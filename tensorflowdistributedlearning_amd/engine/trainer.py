@@ -141,15 +141,16 @@ class Trainer:
         The step must be host-synchronisation-free (it is: losses stay on the device) and its
         Python-side choices static across steps; the learning rate moves to a device scalar
         (optimizer ``set_device_lr``).  Data parallel: with the native RCCL communicator
-        (``init_distributed(comm="rccl")``) the bucketed all-reduces are captured into the graph
-        too (csrc/runtime/comm.cpp forks its comm stream into the capture) and overlap backward
-        at every replay; ProcessGroupNCCL collectives stay eager-only.
+        (every GPU run with world > 1) the bucketed all-reduces are captured into the graph too
+        (csrc/runtime/comm.cpp forks its comm stream into the capture) and overlap backward at
+        every replay; each replay is registered with the communicator's watchdog, so a replay
+        whose collectives hang is timed out like an eager collective.
         The fp8 delayed-scaling state rotates on the host, so fp8 models are not capturable."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs a GPU")
         if self.bucketer is not None and getattr(self.ctx, "native", None) is None:
             raise RuntimeError("data-parallel graph capture needs the native RCCL communicator "
-                               "(init_distributed(comm='rccl'))")
+                               "(GPU ranks; not the TDL_SHARE_GPU gloo rehearsal)")
         if any(getattr(m, "fp8", False) or getattr(m, "emit_fp8", False)
                for m in self.model.modules()):
             raise RuntimeError("fp8 delayed scaling keeps host-side state: not capturable")
@@ -195,6 +196,9 @@ class Trainer:
             self.static_y.copy_(y, non_blocking=True)
         self.optimizer.prepare_replay()
         self.graph.replay()
+        nc = getattr(self.ctx, "native", None)
+        if nc is not None and hasattr(nc, "track_current"):
+            nc.track_current("graph_replay")  # watchdog covers the captured collectives
         self.optimizer.step_count += 1
         self.global_step += 1
         _params.bump_version()

@@ -285,7 +285,7 @@ class Model:
                                  loss.double() * n, torch.tensor(float(n), dtype=torch.float64,
                                                                  device=device)])
         if ctx.is_distributed:
-            s = sums.to(ctx.device) if ctx.backend == "nccl" else sums.cpu()
+            s = sums.to(ctx.device) if ctx.native is not None else sums.cpu()
             ctx.all_reduce_sum_(s)
             sums = s
         sums = sums.cpu()

@@ -79,6 +79,9 @@ class MaskToken:
         self.x = None
         self.red = None
         self.mask = None
+        # a second backward over the same graph (retain_graph) must not see this backward's
+        # stamp: a fresh unmasked gradient can reuse the address at version 0
+        self.premasked = None
 
 
 class GradJoin:
@@ -119,6 +122,10 @@ class GradJoin:
     def take(self):
         """Register one consumer's contribution; returns the buffer for the last one, else None."""
         self.count += 1
+        if self.count > self.n:
+            raise RuntimeError(
+                "fused residual-gradient join reached more than once per forward (a second "
+                "backward over a retained graph?): run the forward again for every backward")
         if self.count != self.n:
             return None
         if self.mask_token is not None and not self.unmasked and self.buf is not None:

@@ -7,9 +7,10 @@ The reference concatenates ALL gradients into one NCCL pack after the full backw
   bucket is just a contiguous slice — no pack/unpack copies;
 * buckets are cut walking the parameters *backwards* (the order backward produces them); each of
   our autograd Functions calls ``p._grad_hook(p)`` right after its wgrad kernel is enqueued; when
-  the last parameter of a bucket lands, the bucket's all-reduce is issued immediately
-  (``async_op=True``; ProcessGroupNCCL orders it after the producing kernels with an event and
-  runs it on RCCL's own stream, so it overlaps the rest of backward on the compute stream);
+  the last parameter of a bucket lands, the bucket's all-reduce is issued immediately on the
+  native RCCL communicator (parallel/rccl.py orders it after the producing kernels with an event
+  and runs it on its own high-priority comm stream, so it overlaps the rest of backward on the
+  compute stream; the optimizer's stream waits on the bucket's completion event only);
 * buckets are always launched in index order (identical on every rank, as RCCL requires);
 * the first-issued bucket is kept small so communication starts early, later ones are large
   (``bucket_mb``, default 32 MB) — fewer, larger collectives suit xGMI's per-link ring bandwidth

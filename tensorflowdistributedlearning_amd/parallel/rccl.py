@@ -11,8 +11,8 @@ model.py:114-116, Test.ipynb:197-200) with the failure detection of §5.3.
   older than ``timeout_s`` or an async RCCL error aborts the communicator and every later call
   raises :class:`CommError` (fail fast instead of hanging the job).
 
-Select it with ``init_distributed(comm="rccl")`` / ``bench.py --comm rccl``; the default DP path
-uses ProcessGroupNCCL (also RCCL) through torch.distributed.
+This is the only GPU collective path: ``init_distributed`` creates it for every GPU run with
+world > 1 (torch.distributed runs gloo beside it for the rendezvous store and host barriers only).
 """
 from __future__ import annotations
 
@@ -110,6 +110,25 @@ class NativeComm:
     @property
     def outstanding(self):
         return self._c.outstanding
+
+    @property
+    def rccl_count(self):
+        """Rank count as RCCL reports it (``ncclCommCount``)."""
+        return self._c.rccl_count
+
+    @property
+    def rccl_rank(self):
+        return self._c.rccl_rank
+
+    @property
+    def rccl_device(self):
+        return self._c.rccl_device
+
+    def track_current(self, name="graph_replay"):
+        """Watch everything queued so far on the current stream like a collective (the watchdog
+        times it out): a HIP-graph replay's captured collectives are covered this way."""
+        self._check()
+        return Work(self, self._c.track_current(name))
 
     def abort(self, why="aborted by user"):
         self._c.abort(why)

@@ -274,7 +274,7 @@ def test_resnet_fp8_dgrad_trains(gpu, depth, monkeypatch):
     monkeypatch.setattr(C, "conv_dgrad_fp8", spy)
     torch.manual_seed(0)
     net = models.build(f"resnet{depth}", num_classes=10)
-    models.enable_fp8(net)
+    models.enable_fp8(net, dgrad=True)
     # ResNet-50 from random init on one 64-px batch diverges in bf16 too at lr 0.01
     # (tools/fp8_train_curve.py): a smaller step for it
     tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01 if depth == 18 else 0.001,
@@ -290,6 +290,116 @@ def test_resnet_fp8_dgrad_trains(gpu, depth, monkeypatch):
                    and m.__class__.__name__ == "Conv2d" and m.cout % 128 == 0)
     assert len(calls) == eligible > 4, (len(calls), eligible)
     assert all(l == l for l in losses) and min(losses[-3:]) < losses[0], losses
+
+
+def test_fp8_dgrad_after_zero_gradient_step_is_finite(gpu):
+    """A step whose loss gradient is exactly zero leaves |dx|max = 0 for the e5m2 delayed scaling;
+    the next step's fp8 dgrad must still read a fully written dx8 (unit fallback scale), not
+    uninitialised bytes behind a zero scale."""
+    torch.manual_seed(0)
+    net = models.resnet18(num_classes=10)
+    models.enable_fp8(net, dgrad=True)
+    scale = {"w": 1.0}
+    tr = Trainer(net, lambda out, y: softmax_cross_entropy(out, y) * scale["w"], gpu, "sgd",
+                 dict(lr=0.01, momentum=0.9, weight_decay=0.0))
+    x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
+    tr.train_step(x, y)               # scalers measure
+    scale["w"] = 0.0
+    for _ in range(2):                # zero loss gradient: every |dx|max becomes 0
+        tr.train_step(x, y)
+    scale["w"] = 1.0
+    for _ in range(2):                # fp8 dgrad with the fallback scale, then re-measured
+        l = float(tr.train_step(x, y)[0])
+    torch.cuda.synchronize()
+    assert l == l and torch.isfinite(tr.flat.master).all() and torch.isfinite(tr.flat.grad).all()
+
+
+def _loss_curve(depth, fp8, steps, dgrad=False, batch=32, size=64, lr=0.002):
+    torch.manual_seed(0)
+    net = models.build(f"resnet{depth}", num_classes=10)
+    if fp8:
+        models.enable_fp8(net, dgrad=dgrad)
+    tr = Trainer(net, softmax_cross_entropy, torch.device("cuda", 0), "sgd",
+                 dict(lr=lr, momentum=0.9, weight_decay=0.0))
+    data = [imagenet_batch(batch, size, num_classes=10, device="cuda", seed=s) for s in range(4)]
+    return [float(tr.train_step(*data[i % 4])[0]) for i in range(steps)]
+
+
+@pytest.mark.timeout(300)
+def test_fp8_loss_curve_tracks_bf16(gpu):
+    """ResNet-50, 60 steps over 4 fixed synthetic batches (memorisation task), identical init and
+    data: the fp8 forward (e4m3 × e4m3 GEMMs, delayed scaling) loss curve stays within a bounded
+    relative gap of the bf16 curve, and both learn.  fp8 + fp8 dgrad is reported and must stay
+    finite and learn (its default is off, models.enable_fp8)."""
+    n = 80
+    ref = _loss_curve(50, False, n, lr=0.003)
+    f8 = _loss_curve(50, True, n, lr=0.003)
+    f8d = _loss_curve(50, True, n, dgrad=True, lr=0.003)
+    tail = lambda c: sum(c[-10:]) / 10
+    print("bf16", [round(v, 3) for v in ref[::6]], tail(ref))
+    print("fp8 ", [round(v, 3) for v in f8[::6]], tail(f8))
+    print("fp8d", [round(v, 3) for v in f8d[::6]], tail(f8d))
+    assert all(v == v for v in ref + f8 + f8d)
+    assert tail(ref) < 0.7 * ref[0]                  # the task is learnable in bf16
+    assert tail(f8) < 0.8 * f8[0]
+    assert abs(f8[0] - ref[0]) < 0.05 * ref[0]      # same function at step 0
+    gap = max(abs(a - b) for a, b in zip(ref[:20], f8[:20])) / ref[0]
+    assert gap < 0.15, gap                          # early trajectory tracks bf16
+    assert abs(tail(f8) - tail(ref)) < 0.2 * ref[0]  # bounded gap at the end of the run
+    assert tail(f8d) < 0.85 * f8d[0]
+
+
+@pytest.mark.timeout(300)
+def test_resnet152_fp8_large_batch_step(gpu):
+    """ResNet-152 with fp8 forward GEMMs at the large-batch bench shape (224², 256 per GPU):
+    finite loss and parameters after a few steps."""
+    torch.manual_seed(0)
+    net = models.resnet152(num_classes=1000)
+    n = models.enable_fp8(net)
+    assert n > 100
+    tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01, momentum=0.9,
+                                                            weight_decay=5e-5))
+    x, y = imagenet_batch(256, 224, device=gpu)
+    for _ in range(3):
+        l = float(tr.train_step(x, y)[0])
+    torch.cuda.synchronize()
+    assert l == l and torch.isfinite(tr.flat.master).all()
+    del tr, net, x, y
+    torch.cuda.empty_cache()
+
+
+def _oracle_compare(model_fn, gpu, x, y, lossf, cos_min=0.99):
+    """GPU native step vs the CPU fp32 oracle on identical bf16-rounded weights and input, frozen
+    BN (moving statistics): logits, loss and the full gradient."""
+    tc, tg, (lc, oc), (lg, og) = _paired(model_fn, gpu, x, y, lossf, train_mode=False)
+    cs = torch.nn.functional.cosine_similarity
+    co = cs(oc.flatten().float(), og.cpu().flatten().float(), dim=0).item()
+    cg = cs(tc.flat.grad, tg.flat.grad.cpu(), dim=0).item()
+    print(f"logits cos {co:.5f} loss {float(lc):.5f} / {float(lg):.5f} grad cos {cg:.5f}")
+    assert co > cos_min, co
+    assert abs(float(lc) - float(lg)) < 0.03 * max(1.0, abs(float(lc)))
+    assert cg > cos_min, cg
+    return co, cg
+
+
+@pytest.mark.timeout(300)
+def test_xception41_matches_cpu_oracle(gpu):
+    """Xception-41 (depthwise-separable HIP path: depthwise fwd/dgrad/wgrad, fused pre-ReLU,
+    pointwise LDS-DMA convs) vs the CPU fp32 oracle."""
+    torch.manual_seed(5)
+    x, y = imagenet_batch(4, 64, num_classes=10, dtype=torch.float32)
+    _oracle_compare(lambda: models.xception_41(num_classes=10), gpu, x, y, softmax_cross_entropy)
+
+
+@pytest.mark.timeout(300)
+def test_deeplab_preset_matches_cpu_oracle(gpu):
+    """The reference DeepLab ResNet-v2-beta preset (101×101×2, ASPP with separable atrous convs,
+    image pooling, TF1 bilinear upsampling, decoder, 258-wide block2 padded to 264, Lovász hinge
+    on the GPU) vs the CPU fp32 oracle."""
+    torch.manual_seed(6)
+    x, y = segmentation_batch(2, dtype=torch.float32)
+    _oracle_compare(lambda: models.DeepLabResNet(model_name="m", input_shape=(101, 101)), gpu,
+                    x, y, lovasz_hinge)
 
 
 def test_deeplab_channel_padding_gpu_matches_unpadded(gpu):
