@@ -504,9 +504,18 @@ void lovasz_hinge(Tensor logits, Tensor labels, Tensor loss, Tensor grad) {
   const bool bf = logits.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32);
   const int64_t B = logits.size(0), P = logits.numel() / B;
-  TORCH_CHECK(P <= 16384, "lovasz kernel supports up to 16384 pixels per image");
-  lovasz_hinge_launch(logits.data_ptr(), bf, labels.data_ptr(), label_kind(labels),
-                      loss.data_ptr<float>(), grad.data_ptr<float>(), B, P, stream());
+  TORCH_CHECK(P < (1 << 30), "lovasz: too many pixels per image");
+  if (P <= 16384) {  // one workgroup per image, sort in LDS
+    lovasz_hinge_launch(logits.data_ptr(), bf, labels.data_ptr(), label_kind(labels),
+                        loss.data_ptr<float>(), grad.data_ptr<float>(), B, P, stream());
+    return;
+  }
+  const int64_t Pp = lovasz_padded_len((int)P);
+  auto opt = logits.options().dtype(torch::kFloat32);
+  Tensor key = torch::empty({B, Pp}, opt), idx = torch::empty({B, Pp}, opt.dtype(torch::kInt32));
+  lovasz_hinge_large_launch(logits.data_ptr(), bf, labels.data_ptr(), label_kind(labels),
+                            loss.data_ptr<float>(), grad.data_ptr<float>(), key.data_ptr<float>(),
+                            idx.data_ptr<int>(), B, P, stream());
 }
 
 void seg_metrics(Tensor labels, Tensor pred, Tensor score, Tensor acc, bool kaggle) {
@@ -703,11 +712,25 @@ struct PyLoader {
   bool pin;
   PyLoader(std::vector<std::string> images, std::vector<std::string> masks, int batch, bool augment,
            bool shuffle, bool repeat, int64_t seed, int threads, int prefetch, int channels,
-           int transformation, bool pin_memory)
+           int transformation, bool pin_memory, py::dict aug)
       : has_masks(!masks.empty()), pin(pin_memory) {
+    tdl_rt::AugConfig cfg;
+    for (auto item : aug) {
+      const std::string k = py::str(item.first);
+      if (k == "horizontal_flip") cfg.horizontal_flip = item.second.cast<bool>();
+      else if (k == "vertical_flip") cfg.vertical_flip = item.second.cast<bool>();
+      else if (k == "rotate_range") cfg.rotate_range = item.second.cast<double>();
+      else if (k == "crop_probability") cfg.crop_probability = item.second.cast<double>();
+      else if (k == "crop_min_percent") cfg.crop_min_percent = item.second.cast<double>();
+      else if (k == "crop_max_percent") cfg.crop_max_percent = item.second.cast<double>();
+      else if (k == "height_shift_range") cfg.height_shift_range = item.second.cast<double>();
+      else if (k == "width_shift_range") cfg.width_shift_range = item.second.cast<double>();
+      else if (k == "brightness_range") cfg.brightness_range = item.second.cast<double>();
+      else throw std::invalid_argument("unknown augmentation option: " + k);
+    }
     impl.reset(new tdl_rt::BatchLoader(images, masks, batch, augment, shuffle, repeat,
                                        (uint64_t)seed, threads, prefetch, channels,
-                                       transformation, 0.0));
+                                       transformation, cfg));
   }
   py::object next() {
     tdl_rt::Batch b;
@@ -739,7 +762,8 @@ Tensor png_decode_gray(const std::string& path) {
 }
 
 py::tuple augment_one(Tensor img, c10::optional<Tensor> mask, bool transpose, bool hflip, bool vflip,
-                      double angle, double tx, double ty, int64_t pad) {
+                      double angle, double tx, double ty, int64_t pad, double brightness,
+                      bool crop, double crop_pct, double crop_left, double crop_top) {
   TORCH_CHECK(img.dim() == 2 && img.scalar_type() == torch::kFloat32 && img.is_contiguous());
   tdl_rt::GrayImage gi;
   gi.h = img.size(0);
@@ -754,6 +778,8 @@ py::tuple augment_one(Tensor img, c10::optional<Tensor> mask, bool transpose, bo
   }
   tdl_rt::AugParams p;
   p.transpose = transpose; p.hflip = hflip; p.vflip = vflip; p.angle = angle; p.tx = tx; p.ty = ty;
+  p.brightness = brightness; p.crop = crop; p.crop_pct = crop_pct; p.crop_left = crop_left;
+  p.crop_top = crop_top;
   Tensor oi = torch::empty_like(img), om = torch::empty_like(img);
   tdl_rt::augment_sample(gi, hm ? &gm : nullptr, p, (int)pad, oi.data_ptr<float>(),
                          hm ? om.data_ptr<float>() : nullptr);
@@ -763,9 +789,11 @@ py::tuple augment_one(Tensor img, c10::optional<Tensor> mask, bool transpose, bo
 }
 
 std::vector<double> transform_matrix(bool hflip, bool vflip, double angle, double tx, double ty,
-                                     int64_t H, int64_t W) {
+                                     int64_t H, int64_t W, bool crop, double crop_pct,
+                                     double crop_left, double crop_top) {
   tdl_rt::AugParams p;
   p.hflip = hflip; p.vflip = vflip; p.angle = angle; p.tx = tx; p.ty = ty;
+  p.crop = crop; p.crop_pct = crop_pct; p.crop_left = crop_left; p.crop_top = crop_top;
   double t[8];
   tdl_rt::make_transform(p, (int)H, (int)W, t);
   return std::vector<double>(t, t + 8);
@@ -883,16 +911,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("world", [](PyComm& p) { return p.c->world(); });
   py::class_<PyLoader>(m, "BatchLoader")
       .def(py::init<std::vector<std::string>, std::vector<std::string>, int, bool, bool, bool,
-                    int64_t, int, int, int, int, bool>(),
+                    int64_t, int, int, int, int, bool, py::dict>(),
            py::arg("images"), py::arg("masks"), py::arg("batch"), py::arg("augment"),
            py::arg("shuffle"), py::arg("repeat"), py::arg("seed"), py::arg("threads"),
            py::arg("prefetch"), py::arg("channels"), py::arg("transformation"),
-           py::arg("pin_memory") = false)
+           py::arg("pin_memory") = false, py::arg("aug") = py::dict())
       .def("next", &PyLoader::next)
       .def_property_readonly("num_batches", [](PyLoader& l) { return l.impl->num_batches(); })
       .def_property_readonly("height", [](PyLoader& l) { return l.impl->height(); })
       .def_property_readonly("width", [](PyLoader& l) { return l.impl->width(); });
   m.def("png_decode_gray", &png_decode_gray);
-  m.def("augment_one", &augment_one);
-  m.def("transform_matrix", &transform_matrix);
+  m.def("augment_one", &augment_one, py::arg("img"), py::arg("mask"), py::arg("transpose"),
+        py::arg("hflip"), py::arg("vflip"), py::arg("angle"), py::arg("tx"), py::arg("ty"),
+        py::arg("pad"), py::arg("brightness") = 0.0, py::arg("crop") = false,
+        py::arg("crop_pct") = 1.0, py::arg("crop_left") = 0.0, py::arg("crop_top") = 0.0);
+  m.def("transform_matrix", &transform_matrix, py::arg("hflip"), py::arg("vflip"),
+        py::arg("angle"), py::arg("tx"), py::arg("ty"), py::arg("H"), py::arg("W"),
+        py::arg("crop") = false, py::arg("crop_pct") = 1.0, py::arg("crop_left") = 0.0,
+        py::arg("crop_top") = 0.0);
 }

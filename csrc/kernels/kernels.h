@@ -178,6 +178,11 @@ void softmax_xent_launch(const void* logits, bool bf16, const int64_t* labels, f
                          void* grad, int N, int K, float smoothing, hipStream_t st);
 void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* labels, int label_kind,
                          float* loss, float* grad, int B, int P, hipStream_t st);
+// P > 16384 pixels per image: multi-pass global bitonic sort; key / idx hold B × padded_len(P)
+int lovasz_padded_len(int P);
+void lovasz_hinge_large_launch(const void* logits, bool logits_bf16, const void* labels,
+                               int label_kind, float* loss, float* grad, float* key, int* idx, int B,
+                               int P, hipStream_t st);
 void seg_metrics_launch(const void* labels, int label_kind, const float* pred, float* score,
                         float* acc, int B, int P, bool kaggle, hipStream_t st);
 

@@ -5,6 +5,11 @@
 //    image: errors → LDS bitonic sort (descending, index tie-break like tf.nn.top_k) of up to
 //    16384 (key, index) pairs (96 KB of the 160 KB LDS) → gather labels → block scans for the
 //    Jaccard gradient → loss and ∂loss/∂logit scattered back to pixel order;
+//    Images above 16384 pixels (any input_shape beyond 128×128) take the multi-pass path: the
+//    same bitonic network over the whole padded row in global memory — a local LDS pass sorts
+//    16384-element chunks, each later merge stage runs its strides ≥ 16384 as global
+//    compare-exchange passes and the rest in one LDS pass per chunk — then one workgroup per
+//    image walks the sorted row in 4096-element chunks with a carried block scan;
 //  * segmentation metrics per image (reference core/metric.py): TP/FP/FN/TN block counts → IoU
 //    threshold score and pixel accuracy.
 #include "common.h"
@@ -204,6 +209,158 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_kernel(const void* __restri
   if (tid == 0) atomicAdd(loss, tot / (float)B);
 }
 
+// ---- multi-pass Lovász hinge for P > LV_MAXP ------------------------------------------------
+constexpr int LVG_CHUNK = 16384;  // elements per LDS pass (1024 threads, 128 KB of LDS)
+
+__device__ __forceinline__ bool lv_before(float ka, int ia, float kb, int ib) {
+  return (ka > kb) || (ka == kb && ia < ib);  // descending key, ascending index on ties
+}
+
+__global__ void __launch_bounds__(256) lovasz_init_kernel(const void* __restrict__ logits, int bf,
+                                                          const void* __restrict__ labels,
+                                                          int lkind, float* __restrict__ key,
+                                                          int* __restrict__ idx, int P, int Pp) {
+  const long img = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Pp) return;
+  float k = -INFINITY;
+  if (i < P) {
+    const float lab = ld_label(labels, lkind, img * P + i);
+    const float sgn = lab > 0.5f ? 1.f : -1.f;
+    k = 1.f - ld(logits, bf, img * P + i) * sgn;
+  }
+  key[img * Pp + i] = k;
+  idx[img * Pp + i] = i;
+}
+
+// one (size, stride) step of the bitonic network, stride ≥ LVG_CHUNK: one pair per thread
+__global__ void __launch_bounds__(256) lovasz_bitonic_global_kernel(float* __restrict__ key,
+                                                                    int* __restrict__ idx, int Pp,
+                                                                    int size, int stride) {
+  const long row = (long)blockIdx.y * Pp;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= Pp / 2) return;
+  const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+  const bool desc = (lo & size) == 0;
+  const float ka = key[row + lo], kb = key[row + hi];
+  const int ia = idx[row + lo], ib = idx[row + hi];
+  const bool a_first = lv_before(ka, ia, kb, ib);
+  if (desc ? !a_first : a_first) {
+    key[row + lo] = kb;
+    key[row + hi] = ka;
+    idx[row + lo] = ib;
+    idx[row + hi] = ia;
+  }
+}
+
+// every step with stride < LVG_CHUNK of the merge stages size_lo … size_hi (doubling), on one
+// LDS-resident chunk; the direction of a pair follows its position in the whole row
+__global__ void __launch_bounds__(LV_THREADS) lovasz_bitonic_local_kernel(float* __restrict__ key,
+                                                                          int* __restrict__ idx,
+                                                                          int Pp, int size_lo,
+                                                                          int size_hi) {
+  extern __shared__ __attribute__((aligned(16))) char lsm[];
+  float* k = (float*)lsm;
+  int* ix = (int*)(k + LVG_CHUNK);
+  const long row = (long)blockIdx.y * Pp;
+  const int c0 = blockIdx.x * LVG_CHUNK;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < LVG_CHUNK; i += LV_THREADS) {
+    k[i] = key[row + c0 + i];
+    ix[i] = idx[row + c0 + i];
+  }
+  __syncthreads();
+  for (int size = size_lo; size <= size_hi; size <<= 1) {
+    for (int stride = min(size, LVG_CHUNK) >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < LVG_CHUNK / 2; t += LV_THREADS) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const bool desc = ((c0 + lo) & size) == 0;
+        const float ka = k[lo], kb = k[hi];
+        const int ia = ix[lo], ib = ix[hi];
+        const bool a_first = lv_before(ka, ia, kb, ib);
+        if (desc ? !a_first : a_first) {
+          k[lo] = kb;
+          k[hi] = ka;
+          ix[lo] = ib;
+          ix[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < LVG_CHUNK; i += LV_THREADS) {
+    key[row + c0 + i] = k[i];
+    idx[row + c0 + i] = ix[i];
+  }
+}
+
+// Jaccard-gradient walk over the sorted row: 4096-element chunks (4 per thread), block scan of
+// the ground-truth counts with a carry between chunks
+__global__ void __launch_bounds__(LV_THREADS) lovasz_scan_kernel(const void* __restrict__ labels,
+                                                                 int lkind,
+                                                                 const float* __restrict__ key,
+                                                                 const int* __restrict__ idx,
+                                                                 float* __restrict__ loss,
+                                                                 float* __restrict__ grad, int B,
+                                                                 int P, int Pp) {
+  __shared__ float wtot[LV_THREADS / 64];
+  __shared__ float red[LV_THREADS / 64 + 4];
+  const long img = blockIdx.x;
+  const long lbase = img * P, kbase = img * Pp;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int PER = 4, STEP = LV_THREADS * PER;
+  float gl = 0.f;
+  for (int i = tid; i < P; i += LV_THREADS) gl += ld_label(labels, lkind, lbase + i) > 0.5f ? 1.f : 0.f;
+  const float gts = block_sum<LV_THREADS>(gl, red);
+  float carry = 0.f, loss_local = 0.f;
+  for (int start = 0; start < P; start += STEP) {
+    const int i0 = start + tid * PER;
+    float g[PER];
+    int pix[PER];
+    float mine = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = i0 + j;
+      pix[j] = i < P ? idx[kbase + i] : 0;
+      g[j] = i < P && ld_label(labels, lkind, lbase + pix[j]) > 0.5f ? 1.f : 0.f;
+      mine += g[j];
+    }
+    float incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    __syncthreads();  // wtot reuse across chunks
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    float before = 0.f, all = 0.f;
+#pragma unroll
+    for (int q = 0; q < LV_THREADS / 64; ++q) {
+      const float t = wtot[q];
+      if (q < w) before += t;
+      all += t;
+    }
+    float cum = carry + before + incl - mine;  // inclusive count before element i0
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = i0 + j;
+      if (i >= P) break;
+      const float cprev = cum;
+      cum += g[j];
+      const float jac = 1.f - (gts - cum) / (gts + ((float)(i + 1) - cum));
+      float gr = jac;
+      if (i > 0) gr -= 1.f - (gts - cprev) / (gts + ((float)i - cprev));
+      const float e = key[kbase + i];
+      if (e > 0.f) loss_local += e * gr;
+      grad[lbase + pix[j]] = (e > 0.f ? -(2.f * g[j] - 1.f) * gr : 0.f) / (float)B;
+    }
+    carry += all;
+  }
+  const float tot = block_sum<LV_THREADS>(loss_local, red);
+  if (tid == 0) atomicAdd(loss, tot / (float)B);
+}
+
 __global__ void __launch_bounds__(256) seg_metrics_kernel(const void* __restrict__ labels, int lkind,
                                                           const float* __restrict__ pred,
                                                           float* __restrict__ score,
@@ -257,6 +414,39 @@ void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* label
   }
   hipLaunchKernelGGL(lovasz_kernel, dim3(B), dim3(LV_THREADS), lds, st, logits,
                      logits_bf16 ? 1 : 0, labels, label_kind, loss, grad, B, P);
+}
+
+int lovasz_padded_len(int P) {
+  int Pp = LVG_CHUNK;
+  while (Pp < P) Pp <<= 1;
+  return Pp;
+}
+
+void lovasz_hinge_large_launch(const void* logits, bool logits_bf16, const void* labels,
+                               int label_kind, float* loss, float* grad, float* key, int* idx, int B,
+                               int P, hipStream_t st) {
+  const int Pp = lovasz_padded_len(P);
+  const size_t lds = (size_t)LVG_CHUNK * 8;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)lovasz_bitonic_local_kernel,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(lovasz_init_kernel, dim3(Pp / 256, B), dim3(256), 0, st, logits,
+                     logits_bf16 ? 1 : 0, labels, label_kind, key, idx, P, Pp);
+  const dim3 lgrid(Pp / LVG_CHUNK, B), ggrid(Pp / 2 / 256, B);
+  hipLaunchKernelGGL(lovasz_bitonic_local_kernel, lgrid, dim3(LV_THREADS), lds, st, key, idx, Pp,
+                     2, LVG_CHUNK);
+  for (int size = 2 * LVG_CHUNK; size <= Pp; size <<= 1) {
+    for (int stride = size >> 1; stride >= LVG_CHUNK; stride >>= 1)
+      hipLaunchKernelGGL(lovasz_bitonic_global_kernel, ggrid, dim3(256), 0, st, key, idx, Pp, size,
+                         stride);
+    hipLaunchKernelGGL(lovasz_bitonic_local_kernel, lgrid, dim3(LV_THREADS), lds, st, key, idx, Pp,
+                       size, size);
+  }
+  hipLaunchKernelGGL(lovasz_scan_kernel, dim3(B), dim3(LV_THREADS), 0, st, labels, label_kind, key,
+                     idx, loss, grad, B, P, Pp);
 }
 
 void seg_metrics_launch(const void* labels, int label_kind, const float* pred, float* score,

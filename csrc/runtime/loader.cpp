@@ -7,7 +7,8 @@
 //  * reference augmentation per sample: (x−MEAN)/STD → REFLECT pad 40 → random transpose →
 //    H-flip / V-flip projective matrices (the reference's [-1,0,width,...] form) → rotation ±10°
 //    about the centre (angles_to_projective_transforms) → translation ±20% drawn PER SAMPLE
-//    (defect D13 fixed; the reference drew it once at graph construction) → composed transform
+//    (defect D13 fixed; the reference drew it once at graph construction) → optional random crop
+//    (crop_probability, crop_min/max_percent) and brightness delta → composed transform
 //    (M = T1·T2·…, output→input mapping as tf.contrib.image.transform) → bilinear (image) /
 //    nearest (mask) sampling with zero fill → central crop → 3×3 Laplacian channel (SAME, zero pad);
 //  * a worker-thread pool assembles whole batches ahead of the consumer (prefetch queue), shuffling
@@ -181,8 +182,38 @@ void make_transform(const AugParams& p, int H, int W, double out[8]) {
   M = mul(M, from_flat(rot));
   const double tr[8] = {1, 0, p.tx, 0, 1, p.ty, 0, 0};
   M = mul(M, from_flat(tr));
+  if (p.crop) {
+    // the reference's crop transform, offsets as written there (top in the x row, left in the
+    // y row: preprocessing.py:219-221)
+    const double cr[8] = {p.crop_pct, 0, p.crop_top, 0, p.crop_pct, p.crop_left, 0, 0};
+    M = mul(M, from_flat(cr));
+  }
   for (int i = 0; i < 8; ++i) out[i] = M.m[i] / M.m[8];
 }
+
+template <class RNG>
+AugParams draw_aug(const AugConfig& cfg, int H, int W, RNG& rng) {
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  AugParams p;
+  p.transpose = U(rng) > 0.5;
+  if (cfg.brightness_range > 0) p.brightness = (2 * U(rng) - 1) * cfg.brightness_range;
+  if (cfg.horizontal_flip) p.hflip = U(rng) < 0.5;
+  if (cfg.vertical_flip) p.vflip = U(rng) < 0.5;
+  const double ar = cfg.rotate_range / 180.0 * M_PI;
+  p.angle = -ar + 2 * ar * U(rng);
+  // both shifts scale with the height in the reference (preprocessing.py:196-203); drawn per
+  // sample here (defect D13 fixed)
+  p.tx = cfg.width_shift_range ? (2 * U(rng) - 1) * cfg.width_shift_range * H : 0.0;
+  p.ty = cfg.height_shift_range ? (2 * U(rng) - 1) * cfg.height_shift_range * H : 0.0;
+  if (cfg.crop_probability > 0) {
+    p.crop_pct = cfg.crop_min_percent + (cfg.crop_max_percent - cfg.crop_min_percent) * U(rng);
+    p.crop_left = U(rng) * W * (1 - p.crop_pct);
+    p.crop_top = U(rng) * H * (1 - p.crop_pct);
+    p.crop = U(rng) < cfg.crop_probability;
+  }
+  return p;
+}
+template AugParams draw_aug<std::mt19937_64>(const AugConfig&, int, int, std::mt19937_64&);
 
 // tf.contrib.image.transform: output (x, y) samples input at (a0x+a1y+a2, b0x+b1y+b2)/(c0x+c1y+1)
 void projective_warp(const float* in, int H, int W, const double t[8], bool nearest, float* out) {
@@ -232,7 +263,7 @@ void augment_sample(const GrayImage& img, const GrayImage* mask, const AugParams
     for (int x = 0; x < PW; ++x) {
       int sy = reflect_idx(y - pad, H), sx = reflect_idx(x - pad, W);
       if (p.transpose) std::swap(sy, sx);  // transpose_image (square images)
-      pi[(size_t)y * PW + x] = (img.px[(size_t)sy * W + sx] - MEAN) / STD;
+      pi[(size_t)y * PW + x] = (img.px[(size_t)sy * W + sx] - MEAN) / STD + (float)p.brightness;
       if (mask) pm[(size_t)y * PW + x] = mask->px[(size_t)sy * W + sx];
     }
   double t[8];
@@ -273,10 +304,13 @@ static inline uint16_t f2bf(float f) {
 BatchLoader::BatchLoader(const std::vector<std::string>& images,
                          const std::vector<std::string>& masks, int batch, bool augment,
                          bool shuffle, bool repeat, uint64_t seed, int threads, int prefetch,
-                         int channels, int transformation, double crop_probability)
+                         int channels, int transformation, const AugConfig& aug)
     : images_(images), masks_(masks), batch_(batch), augment_(augment), shuffle_(shuffle),
-      repeat_(repeat), seed_(seed), channels_(channels), transformation_(transformation) {
-  (void)crop_probability;
+      repeat_(repeat), seed_(seed), channels_(channels), transformation_(transformation),
+      aug_(aug) {
+  if (aug_.crop_probability < 0 || aug_.crop_probability > 1 || aug_.brightness_range < 0 ||
+      aug_.crop_min_percent <= 0 || aug_.crop_max_percent < aug_.crop_min_percent)
+    throw std::runtime_error("invalid augmentation parameters");
   if (!masks_.empty() && masks_.size() != images_.size())
     throw std::runtime_error("images and masks differ in length");
   if (images_.empty()) throw std::runtime_error("empty dataset");
@@ -374,16 +408,7 @@ void BatchLoader::build(long b, Batch& out) {
     const GrayImage* gm = masks_.empty() ? nullptr : &get(cache_mask_, masks_, idx[i]);
     if (augment_) {
       std::mt19937_64 rng(seed_ * 7919ull + (uint64_t)b * 104729ull + i);
-      std::uniform_real_distribution<double> U(0.0, 1.0);
-      AugParams p;
-      p.transpose = U(rng) > 0.5;
-      p.hflip = U(rng) < 0.5;
-      p.vflip = U(rng) < 0.5;
-      const double ar = 10.0 / 180.0 * M_PI;
-      p.angle = -ar + 2 * ar * U(rng);
-      const int PH = H_ + 80;
-      p.tx = (-0.2 + 0.4 * U(rng)) * PH;  // reference scales both shifts by height
-      p.ty = (-0.2 + 0.4 * U(rng)) * PH;
+      const AugParams p = draw_aug(aug_, H_ + 80, W_ + 80, rng);
       augment_sample(gi, gm, p, 40, img.data(), gm ? msk.data() : nullptr);
     } else {
       for (int k = 0; k < HW; ++k) img[k] = (gi.px[k] - MEAN) / STD;

@@ -22,10 +22,28 @@ struct GrayImage {
 GrayImage decode_png_gray(const std::vector<uint8_t>& file);
 GrayImage load_png_gray(const std::string& path);
 
+// one sample's draw of the reference augmentation (preprocessing.py:112-246)
 struct AugParams {
   bool transpose = false, hflip = false, vflip = false;
   double angle = 0.0, tx = 0.0, ty = 0.0;
+  double brightness = 0.0;                        // tf.image.random_brightness delta (image only)
+  bool crop = false;                              // random-crop transform applied
+  double crop_pct = 1.0, crop_left = 0.0, crop_top = 0.0;
 };
+
+// the knobs of read_and_preprocess (preprocessing.py:112-123), same names and defaults
+struct AugConfig {
+  bool horizontal_flip = true, vertical_flip = true;
+  double rotate_range = 10.0;                     // degrees
+  double crop_probability = 0.5, crop_min_percent = 0.9, crop_max_percent = 1.1;
+  double height_shift_range = 0.2, width_shift_range = 0.2;
+  double brightness_range = 0.0;
+};
+
+// draw one sample's parameters from `cfg` (padded image size H×W) — the reference's draw order:
+// transpose, brightness, H-flip, V-flip, angle, shifts, crop
+template <class RNG>
+AugParams draw_aug(const AugConfig& cfg, int H, int W, RNG& rng);
 
 void make_transform(const AugParams& p, int H, int W, double out[8]);
 void projective_warp(const float* in, int H, int W, const double t[8], bool nearest, float* out);
@@ -46,7 +64,7 @@ class BatchLoader {
  public:
   BatchLoader(const std::vector<std::string>& images, const std::vector<std::string>& masks,
               int batch, bool augment, bool shuffle, bool repeat, uint64_t seed, int threads,
-              int prefetch, int channels, int transformation, double crop_probability);
+              int prefetch, int channels, int transformation, const AugConfig& aug = AugConfig());
   ~BatchLoader();
   bool next(Batch& out);
   int height() const { return H_; }
@@ -67,6 +85,7 @@ class BatchLoader {
   bool augment_, shuffle_, repeat_;
   uint64_t seed_;
   int channels_, transformation_;
+  AugConfig aug_;
   int H_ = 0, W_ = 0, prefetch_ = 2;
   long n_batches_ = -1;
   std::vector<GrayImage> cache_img_, cache_mask_;

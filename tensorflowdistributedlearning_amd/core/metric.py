@@ -1,8 +1,11 @@
 """core.metric — reference API (core/metric.py:3-71).
 
-``mIOU`` / ``mean_accuracy`` return ``(value, update)`` like ``tf.metrics.mean``: ``update`` is a
-callable that folds the current batch into a device-resident streaming mean stored under
-``name`` (tf's local metric variables); ``value`` is the running mean *after* this batch.
+``mIOU`` / ``mean_accuracy`` return ``(value, update)`` with ``tf.metrics.mean`` semantics
+(core/metric.py:42-50): the streaming state (total, count) lives on the device under ``name``
+(tf's local metric variables); ``value`` reads the running mean as it stands — creating the metric
+does not fold the batch in — and ``update()`` (the update op) folds this batch's per-image scores
+into the state and returns the new mean.  Calling ``update()`` twice folds the batch twice, as
+running the update op twice would; the mean of an empty state is 0 (tf's ``div_no_nan``).
 Per-image scores come from the fused seg-metrics kernel on the GPU.
 """
 from __future__ import annotations
@@ -28,14 +31,19 @@ def reset(name=None):
 
 
 def _metric(y_true, y_pred, which, name, kaggle=False):
-    score, acc = seg_scores(y_true, y_pred, kaggle)
-    vals = score if which == "iou" else acc
-    s = _stream(name, vals.device)
-    value = s.update(vals)
+    s = _stream(name, y_pred.device)
+    value = s.result()  # the current state: this batch is not folded in yet
 
     def update():
-        return s.result()
+        score, acc = seg_scores(y_true, y_pred, kaggle)
+        return s.update(score if which == "iou" else acc)
     return value, update
+
+
+def result(name):
+    """The running mean of metric ``name`` (0 when empty)."""
+    s = _STATE.get(name)
+    return None if s is None else s.result()
 
 
 def mIOU(y_true, y_pred, metrics_collections=None, updates_collections=None, name="iou",
@@ -58,4 +66,4 @@ def mean_accuracy(y_true, y_pred, metrics_collections=None, updates_collections=
     return v, u
 
 
-__all__ = ["IOU_THRESHOLDS", "mIOU", "mean_accuracy", "reset"]
+__all__ = ["IOU_THRESHOLDS", "mIOU", "mean_accuracy", "reset", "result"]

@@ -8,7 +8,7 @@ import collections
 
 import torch.nn.functional as F
 
-from ..models.xception import Xception41, XceptionModule, SeparableConvBN, _fixed_pad
+from ..models.xception import Xception, Xception41, XceptionModule, SeparableConvBN, _fixed_pad
 from ..models.deeplab import SplitSeparableConv  # noqa: F401  (split_separable_conv2d lives in core.layers)
 from .layers import split_separable_conv2d  # noqa: F401
 from ._scope import get_or_create, to_nhwc, from_nhwc, device_of
@@ -89,13 +89,43 @@ def stack_blocks_dense(in_channels, blocks, output_stride=None):
     return units, cin
 
 
+def _block_specs(blocks):
+    """xception_block specs (Block namedtuples, core/xception.py:367-402) → the model's
+    (scope, depth_list, skip, num_units, stride, unit_rate_list, act) rows."""
+    rows = []
+    for b in blocks:
+        # xception_block repeats one unit dict num_units times with the block stride in every
+        # unit; the reference stack applies each unit's own stride (stack_blocks_dense, :270-290)
+        for a in b.args:
+            rows.append((b.scope, list(a["depth_list"]), a["skip_connection_type"], 1,
+                         a["stride"], list(a.get("unit_rate_list") or [1, 1, 1]),
+                         bool(a["activation_fn_in_separable_conv"])))
+    return rows
+
+
 def xception(inputs, blocks=None, num_classes=None, is_training=True, global_pool=True,
              keep_prob=0.5, output_stride=None, reuse=None, scope=None, data_format="NHWC"):
-    """Generic Xception generator (core/xception.py:295-402) over the Xception-41 block specs;
-    the 41-layer configuration is :func:`xception_41`."""
-    return xception_41(inputs, is_training=is_training, keep_prob=keep_prob,
-                       output_stride=output_stride, scope=scope or "xception",
-                       num_classes=num_classes, data_format=data_format)
+    """Generic Xception generator (core/xception.py:295-364): the root block, then
+    ``stack_blocks_dense`` over ``blocks`` (a list of :func:`xception_block` specs; default: the
+    Xception-41 blocks) with atrous output-stride control, and — with ``num_classes`` — global
+    pooling + logits.  Builds (or reuses, per ``scope``) the module; returns (net, end_points)
+    with one end point per unit ('<scope>/<block>/unit_<i>')."""
+    scope = scope or "xception"
+    if blocks is None:
+        return xception_41(inputs, is_training=is_training, keep_prob=keep_prob,
+                           output_stride=output_stride, scope=scope, num_classes=num_classes,
+                           data_format=data_format)
+    rows = _block_specs(blocks)
+    x = to_nhwc(inputs, data_format)
+    key = ("xception", scope, output_stride, num_classes, x.shape[-1],
+           tuple((r[0], tuple(r[1]), r[2], r[4], tuple(r[5]), r[6]) for r in rows))
+    m = get_or_create(key, lambda: Xception(rows, num_classes=num_classes or 0,
+                                            in_channels=min(x.shape[-1], 8),
+                                            output_stride=output_stride), device_of(x))
+    m.train(bool(is_training))
+    y, ep = m(x, return_end_points=True)
+    ep = {f"{scope}/{k}": v for k, v in ep.items()}
+    return (from_nhwc(y, data_format) if y.dim() == 4 else y), ep
 
 
 def xception_41(inputs, is_training=True, keep_prob=0.5, output_stride=None,

@@ -26,9 +26,18 @@ def fold_files(model_dir, mode, fold):
     return images, masks
 
 
+# what the reference's training input_fn maps: read_and_preprocess(augment, crop_probability=0)
+# (model.py:315-317) with the function's other defaults (preprocessing.py:112-123)
+TRAIN_AUG = {"crop_probability": 0.0}
+
+
 class SegmentationPipeline:
+    """``aug``: read_and_preprocess knobs for the native augmentation (horizontal_flip,
+    vertical_flip, rotate_range, crop_probability, crop_min_percent, crop_max_percent,
+    height_shift_range, width_shift_range, brightness_range); default :data:`TRAIN_AUG`."""
+
     def __init__(self, images, masks, batch_size, augment, shuffle, repeat=True, seed=0,
-                 device="cpu", rank=0, world=1, threads=4, prefetch=4, channels=8):
+                 device="cpu", rank=0, world=1, threads=4, prefetch=4, channels=8, aug=None):
         if world > 1:
             images = images[rank::world]
             masks = masks[rank::world] if masks else masks
@@ -41,7 +50,7 @@ class SegmentationPipeline:
         self._loader = _native.load().BatchLoader(
             list(images), list(masks or []), int(batch_size), bool(augment), bool(shuffle),
             bool(repeat), int(seed) * 1000 + rank, int(threads), int(prefetch), int(channels), 0,
-            self.device.type == "cuda")
+            self.device.type == "cuda", dict(TRAIN_AUG if aug is None else aug))
 
     def __iter__(self):
         return self

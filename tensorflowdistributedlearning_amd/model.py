@@ -44,7 +44,7 @@ from .ops.loss import lovasz_hinge
 from .ops.metrics import seg_scores, StreamingMean
 from .ops.optim import exponential_decay
 from .preprocessing.preprocessing import _prepare_directory, create_symlinks, TRAIN, EVAL
-from .data.pipeline import SegmentationPipeline, TestPipeline, fold_files
+from .data.pipeline import SegmentationPipeline, TestPipeline, fold_files, TRAIN_AUG
 from .utils import metric_comparisson, get_available_gpus
 
 WEIGHT_DECAY = 0.001
@@ -93,6 +93,9 @@ class Model:
         self.use_regularization = kwargs.get("use_regularization", False)  # D5: opt-in
         self.kaggle_metric = kwargs.get("kaggle_metric", False)  # D16: reference formula default
         self.loader_threads = kwargs.get("loader_threads", 4)
+        # read_and_preprocess knobs of the training input (model.py:315-317: crop_probability=0,
+        # the function's other defaults); e.g. augmentation={"brightness_range": 0.1}
+        self.augmentation = dict(TRAIN_AUG, **kwargs.get("augmentation", {}))
         self.device = kwargs.get("device", None)
         self.backend = kwargs.get("backend", None)
 
@@ -208,7 +211,7 @@ class Model:
         pipe = SegmentationPipeline(tr_imgs, tr_masks, batch, augment=True, shuffle=True,
                                     repeat=True, seed=self.seed + 7919 * fold + start,
                                     device=device, rank=ctx.rank, world=ctx.world_size,
-                                    threads=self.loader_threads)
+                                    threads=self.loader_threads, aug=self.augmentation)
         main = ctx.is_main
         tw = SummaryWriter(os.path.join(fold_dir, "train"), enabled=main)
         ew = SummaryWriter(os.path.join(fold_dir, "eval"), enabled=main)
@@ -364,7 +367,7 @@ class Model:
             return SegmentationPipeline(imgs, masks, batch_size, augment=augment, shuffle=shuffle,
                                         repeat=(mode == TRAIN), seed=self.seed + fold,
                                         device=device, rank=rank, world=world,
-                                        threads=self.loader_threads)
+                                        threads=self.loader_threads, aug=self.augmentation)
         return input_fn
 
     def _make_test_input(self, batch_size, test_directory, tti="none", device="cpu"):

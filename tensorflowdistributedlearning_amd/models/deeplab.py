@@ -188,7 +188,9 @@ class DeepLabResNet(nn.Module):
         self.decoder_conv_3x3 = Conv2d(2 * base_depth, 1, 3, 1, "SAME", bias=True,
                                        pad_cout_to=channel_align)
 
-    def forward(self, x, return_end_points=False):
+    def forward_encoder(self, x):
+        """The ResNet-v2-beta encoder alone (``resnet_v2_beta`` without the ASPP / decoder,
+        core/resnet.py:171-257): returns (block4 features, end_points)."""
         if x.shape[-1] != self.conv1_1.conv._cin_store:
             x = nn.functional.pad(x, (0, self.conv1_1.conv._cin_store - x.shape[-1]))
         end_points = {}
@@ -199,6 +201,11 @@ class DeepLabResNet(nn.Module):
             for ui, unit in enumerate(mods):
                 net = unit(net, end_points, f"{root}/{bname}/unit_{ui + 1}")
             end_points[f"{root}/{bname}"] = _logical(net, mods[-1].out_channels)
+        return end_points[f"{root}/block4"], end_points
+
+    def forward(self, x, return_end_points=False):
+        root = f"{self.model_name}/resnet_v2"
+        _, end_points = self.forward_encoder(x)
         atrous = end_points[f"{root}/block4"].contiguous()  # a copy only for unaligned widths
         size = (atrous.shape[1], atrous.shape[2])
         a1 = self.assp_conv_1x1(atrous)

@@ -78,23 +78,32 @@ class XceptionModule(nn.Module):
         return r
 
 
-class Xception41(nn.Module):
-    def __init__(self, num_classes=1000, in_channels=3, output_stride=None, multi_grid=None,
-                 bn_decay=0.9997, bn_eps=1e-3):
+# Xception-41 (core/xception.py:405-465): (block scope, depth_list, skip, num_units, stride,
+# unit_rate_list, activation inside the separable convs)
+XCEPTION41_BLOCKS = [
+    ("entry_flow/block1", [128, 128, 128], "conv", 1, 2, [1, 1, 1], False),
+    ("entry_flow/block2", [256, 256, 256], "conv", 1, 2, [1, 1, 1], False),
+    ("entry_flow/block3", [728, 728, 728], "conv", 1, 2, [1, 1, 1], False),
+    ("middle_flow/block1", [728, 728, 728], "sum", 8, 1, [1, 1, 1], False),
+    ("exit_flow/block1", [728, 1024, 1024], "conv", 1, 2, [1, 1, 1], False),
+    ("exit_flow/block2", [1536, 1536, 2048], "none", 1, 1, None, True),
+]
+
+
+class Xception(nn.Module):
+    """The generic Xception generator (core/xception.py:295-364): the root (3×3/s2 32 → 3×3 64,
+    conv+BN+ReLU) then ``stack_blocks_dense`` over ``blocks`` — a list of (scope, depth_list,
+    skip_connection_type, num_units, stride, unit_rate_list, activation_fn_in_separable_conv);
+    the stride of a block is in its last unit — with atrous output-stride control, and an
+    optional global-pool + logits head."""
+
+    def __init__(self, blocks, num_classes=0, in_channels=3, output_stride=None, bn_decay=0.9997,
+                 bn_eps=1e-3):
         super().__init__()
         bn_kw = dict(bn_decay=bn_decay, bn_eps=bn_eps)
         self.conv1_1 = ConvBN(in_channels, 32, 3, 2, _fixed_pad(3, 1), relu=True, pad_cin_to=8,
                               **bn_kw)
         self.conv1_2 = ConvBN(32, 64, 3, 1, "SAME", relu=True, **bn_kw)
-        mg = list(multi_grid) if multi_grid else [1, 1, 1]
-        spec = [
-            ("entry_flow/block1", [128, 128, 128], "conv", 1, 2, [1, 1, 1], False),
-            ("entry_flow/block2", [256, 256, 256], "conv", 1, 2, [1, 1, 1], False),
-            ("entry_flow/block3", [728, 728, 728], "conv", 1, 2, [1, 1, 1], False),
-            ("middle_flow/block1", [728, 728, 728], "sum", 8, 1, [1, 1, 1], False),
-            ("exit_flow/block1", [728, 1024, 1024], "conv", 1, 2, [1, 1, 1], False),
-            ("exit_flow/block2", [1536, 1536, 2048], "none", 1, 1, mg, True),
-        ]
         target = None if output_stride is None else output_stride // 2
         if output_stride is not None and output_stride % 2 != 0:
             raise ValueError("The output_stride needs to be a multiple of 2.")
@@ -102,32 +111,53 @@ class Xception41(nn.Module):
         self.units = nn.ModuleList()
         self.unit_names = []
         cin = 64
-        for name, depths, skip, n, stride, urates, act in spec:
+        seen = {}
+        for name, depths, skip, n, stride, urates, act in blocks:
+            urates = list(urates) if urates else [1, 1, 1]
+            if len(depths) != 3 or len(urates) != 3:
+                raise ValueError("Expect three elements in depth_list and unit_rate_list.")
+            if skip not in ("conv", "sum", "none"):
+                raise ValueError("Unsupported skip connection type.")
             for u in range(n):
+                s = stride if u == n - 1 else 1
+                if target is not None and current > target:
+                    raise ValueError("The target output_stride cannot be reached.")
                 if target is not None and current == target:
                     m = XceptionModule(cin, depths, skip, 1, rate, urates, act, bn_kw)
-                    rate *= stride
+                    rate *= s
                 else:
-                    m = XceptionModule(cin, depths, skip, stride, 1, urates, act, bn_kw)
-                    current *= stride
+                    m = XceptionModule(cin, depths, skip, s, 1, urates, act, bn_kw)
+                    current *= s
                 cin = m.out_channels
                 self.units.append(m)
-                self.unit_names.append(f"{name}/unit_{u + 1}")
+                seen[name] = seen.get(name, 0) + 1
+                self.unit_names.append(f"{name}/unit_{seen[name]}")
         if target is not None and current != target:
             raise ValueError("The target output_stride cannot be reached.")
         self.num_features = cin
         self.gap = GlobalAvgPool() if num_classes else None
         self.fc = Linear(cin, num_classes) if num_classes else None
 
-    def forward(self, x):
+    def forward(self, x, return_end_points=False):
         if x.shape[-1] != self.conv1_1.conv._cin_store:
             x = nn.functional.pad(x, (0, self.conv1_1.conv._cin_store - x.shape[-1]))
         x = self.conv1_2(self.conv1_1(x))
-        for u in self.units:
+        ep = {}
+        for name, u in zip(self.unit_names, self.units):
             x = u(x)
+            if return_end_points:
+                ep[name] = x
         if self.fc is not None:
             x = self.fc(self.gap(x))
-        return x
+        return (x, ep) if return_end_points else x
+
+
+class Xception41(Xception):
+    def __init__(self, num_classes=1000, in_channels=3, output_stride=None, multi_grid=None,
+                 bn_decay=0.9997, bn_eps=1e-3):
+        blocks = [b if b[5] is not None else b[:5] + (list(multi_grid or [1, 1, 1]),) + b[6:]
+                  for b in XCEPTION41_BLOCKS]
+        super().__init__(blocks, num_classes, in_channels, output_stride, bn_decay, bn_eps)
 
 
 def xception_41(num_classes=1000, **kw):

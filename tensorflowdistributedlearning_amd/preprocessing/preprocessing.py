@@ -122,23 +122,42 @@ def read_and_preprocess(X, y, augment=False, horizontal_flip=True, vertical_flip
                         rotate_range=10, crop_probability=0.5, crop_min_percent=0.9,
                         crop_max_percent=1.1, height_shift_range=0.2, width_shift_range=0.2,
                         brightness_range=0.0, rng=None):
-    """Per-sample version of the reference's augmentation (the batched hot path is the native
-    loader).  Returns ({'images': [H,W,2]}, mask [H,W,1]).  Random crop (crop_probability) and
-    brightness are accepted for signature parity; the reference trains with crop_probability=0
-    (model.py:316) and brightness_range=0."""
+    """Per-sample version of the reference's augmentation (preprocessing.py:112-246; the batched
+    hot path is the native loader, data/pipeline.py, with the same knobs).  Returns
+    ({'images': [H,W,2]}, mask [H,W,1]).  Draw order as the reference: transpose, brightness
+    (``tf.image.random_brightness``: a uniform delta in ±brightness_range added to the normalised
+    image), H-flip, V-flip, rotation, shifts (per sample: D13 fixed), random crop (scale
+    uniform in [crop_min_percent, crop_max_percent], offsets as the reference's crop transform,
+    applied with probability ``crop_probability``)."""
+    if not 0 <= crop_probability <= 1 or brightness_range < 0:
+        raise ValueError("crop_probability must be in [0, 1] and brightness_range >= 0")
     rng = rng or np.random.default_rng()
     image = _parse_image(X)[..., 0].contiguous()
     mask = _parse_image(y)[..., 0].contiguous()
     C = _native.load()
     if augment:
         H = image.shape[0] + 80
+        W = image.shape[1] + 80
         ang = rotate_range / 180 * math.pi
-        img, msk, lap = C.augment_one(
-            image, mask, bool(rng.uniform() > 0.5),
-            bool(horizontal_flip and rng.uniform() < 0.5),
-            bool(vertical_flip and rng.uniform() < 0.5), float(rng.uniform(-ang, ang)),
-            float(rng.uniform(-width_shift_range, width_shift_range) * H),
-            float(rng.uniform(-height_shift_range, height_shift_range) * H), 40)
+        transpose = bool(rng.uniform() > 0.5)
+        bright = float(rng.uniform(-brightness_range, brightness_range)) if brightness_range > 0 \
+            else 0.0
+        hf = bool(horizontal_flip and rng.uniform() < 0.5)
+        vf = bool(vertical_flip and rng.uniform() < 0.5)
+        angle = float(rng.uniform(-ang, ang))
+        tx = float(rng.uniform(-width_shift_range, width_shift_range) * H) if width_shift_range \
+            else 0.0
+        ty = float(rng.uniform(-height_shift_range, height_shift_range) * H) \
+            if height_shift_range else 0.0
+        crop, pct, left, top = False, 1.0, 0.0, 0.0
+        if crop_probability > 0:
+            pct = float(rng.uniform(crop_min_percent, crop_max_percent))
+            left = float(rng.uniform() * W * (1 - pct))
+            top = float(rng.uniform() * H * (1 - pct))
+            crop = bool(rng.uniform() < crop_probability)
+        img, msk, lap = C.augment_one(image, mask, transpose, hf, vf, angle, tx, ty, 40,
+                                      brightness=bright, crop=crop, crop_pct=pct,
+                                      crop_left=left, crop_top=top)
     else:
         img = (image - MEAN) / STD
         msk = mask

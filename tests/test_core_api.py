@@ -45,12 +45,46 @@ def test_resnet_v2_specs_and_helpers():
         resnet.channel_dimension((2, None), "NHWC")
     sc = resnet.resnet_arg_scope(weight_decay=1e-4)
     assert sc["weight_decay"] == 1e-4 and sc["max_pool_padding"] == "SAME"
+    with resnet.arg_scope(resnet.resnet_arg_scope(batch_norm_decay=0.5, batch_norm_epsilon=0.1)):
+        u = resnet.bottleneck(64, 256, 64, 1)
+        with resnet.resnet_arg_scope(batch_norm_decay=0.25):  # the innermost scope wins
+            u2 = resnet.basic_block(64, 64, 64, 1)
+    u3 = resnet.bottleneck(64, 256, 64, 1)
+    assert u.preact.bn.decay == 0.5 and u.preact.bn.eps == 0.1
+    assert u2.preact.bn.decay == 0.25 and u2.preact.bn.eps == 1e-5  # a full scope, as slim
+    assert u3.preact.bn.decay == 0.997
     u = resnet.bottleneck(64, 256, 64, 2)
     assert u(torch.randn(1, 8, 8, 64)).shape == (1, 4, 4, 256)
     b = resnet.basic_block(64, 64, 64, 1, rate=2)
     assert b(torch.randn(1, 8, 8, 64)).shape == (1, 8, 8, 64)
     root = resnet.root_block_fn_for_beta_variant(2)
     assert root(torch.randn(1, 16, 16, 8)).shape == (1, 8, 8, 128)
+
+
+def test_resnet_v2_classification_head():
+    """num_classes + global_pool (core/resnet.py:246-256): pool5 mean, 1×1 'logits' conv with
+    bias, softmax predictions."""
+    x = torch.randn(2, 2, 32, 32)
+    net, ep = resnet.resnet_v2(x, n_blocks=(1, 1, 1), num_classes=5, global_pool=True,
+                               output_stride=8, scope="cls", data_format="NCHW", is_training=False)
+    assert net.shape == (2, 5, 1, 1)
+    p = ep["predictions"]
+    assert p.shape == (2, 1, 1, 5)
+    torch.testing.assert_close(p.sum(-1), torch.ones(2, 1, 1))
+    feat = ep["cls/resnet_v2/block4"]
+    pooled = ep["cls/resnet_v2/pool5"]
+    torch.testing.assert_close(pooled, feat.mean(dim=(1, 2), keepdim=True), rtol=1e-4, atol=1e-5)
+    m = _scope._CACHE[next(iter(_scope._CACHE))]
+    w, b = m.logits.weight, m.logits.bias
+    ref = torch.einsum("nhwc,kc->nhwk", pooled, w.reshape(5, -1)) + b
+    torch.testing.assert_close(ep["cls/resnet_v2/logits"], ref, rtol=1e-4, atol=1e-4)
+    # dense features without the head; global pool alone
+    f, _ = resnet.resnet_v2(x.permute(0, 2, 3, 1), n_blocks=(1, 1, 1), output_stride=8,
+                            scope="feat")
+    assert f.shape == (2, 4, 4, 1024)
+    g, _ = resnet.resnet_v2(x.permute(0, 2, 3, 1), n_blocks=(1, 1, 1), output_stride=8,
+                            global_pool=True, scope="gp")
+    assert g.shape == (2, 1, 1, 1024)
 
 
 def test_fixed_padding_matches_numpy():
@@ -105,21 +139,30 @@ def test_lovasz_facade_matches_reference():
 
 
 def test_streaming_metrics():
+    """tf.metrics.mean semantics: value = the state as it stands, update() folds the batch."""
     lab = torch.zeros(2, 8, 8, 1)
     lab[0, :4] = 1
     pred = lab.clone()
     v, upd = metric.mIOU(lab, pred, name="iou")
-    assert float(v) == pytest.approx(np.mean([1.0 * (1.0 > t) for t in metric.IOU_THRESHOLDS]))
+    assert float(v) == 0.0  # nothing folded yet (div_no_nan)
+    s_full = np.mean([1.0 * (1.0 > t) for t in metric.IOU_THRESHOLDS])
+    assert float(upd()) == pytest.approx(s_full)
     pred2 = torch.zeros_like(lab)
     pred2[0, :2] = 1  # IoU 0.5 on image 0; image 1 empty/empty → 1
-    v2, _ = metric.mIOU(lab, pred2, name="iou")
+    v2, upd2 = metric.mIOU(lab, pred2, name="iou")
+    assert float(v2) == pytest.approx(s_full)  # the first batch only
     s0 = np.mean([0.5 * (0.5 > t) for t in metric.IOU_THRESHOLDS])
-    assert float(v2) == pytest.approx((2 + s0 + 1) / 4)
-    assert float(upd()) == pytest.approx(float(v2))
-    a, _ = metric.mean_accuracy(lab, pred2, name="acc")
-    assert float(a) == pytest.approx(np.mean([1 - 16 / 64, 1.0]))
-    k, _ = metric.mIOU(lab, pred2, name="kag", kaggle=True)
-    assert float(k) == pytest.approx((0.0 + 1) / 2)  # IoU 0.5 passes no threshold (strict >)
+    assert float(upd2()) == pytest.approx((2 * s_full + s0 + 1) / 4)
+    assert float(metric.result("iou")) == pytest.approx((2 * s_full + s0 + 1) / 4)
+    upd2()  # running the update op again folds the batch again
+    assert float(metric.result("iou")) == pytest.approx((2 * s_full + 2 * s0 + 2) / 6)
+    a, ua = metric.mean_accuracy(lab, pred2, name="acc")
+    assert float(a) == 0.0
+    assert float(ua()) == pytest.approx(np.mean([1 - 16 / 64, 1.0]))
+    coll_v, coll_u = [], []
+    k, uk = metric.mIOU(lab, pred2, coll_v, coll_u, name="kag", kaggle=True)
+    assert coll_v == [k] and coll_u == [uk]
+    assert float(uk()) == pytest.approx((0.0 + 1) / 2)  # IoU 0.5 passes no threshold (strict >)
 
 
 def test_xception_facade():
@@ -137,6 +180,29 @@ def test_xception_facade():
     assert len(b.args) == 2
     s = xception.separable_conv2d_same(32, 64, stride=2)
     assert s(torch.randn(1, 8, 8, 32)).shape == (1, 4, 4, 64)
+
+
+def test_xception_generic_blocks():
+    """xception(inputs, blocks) honours the given block specs (core/xception.py:295-364), with
+    per-unit strides as the reference's stack_blocks_dense applies them."""
+    b = [xception.xception_block("entry_flow/block1", [16, 16, 16], "conv", False, False, 1, 2),
+         xception.xception_block("middle_flow/block1", [16, 16, 16], "sum", False, False, 3, 1),
+         xception.xception_block("exit_flow/block1", [32, 32, 48], "none", True, False, 1, 1,
+                                 [1, 2, 1])]
+    y, ep = xception.xception(torch.randn(2, 32, 32, 3), blocks=b, num_classes=7, scope="xs")
+    assert y.shape == (2, 7)
+    assert sorted(ep) == ["xs/entry_flow/block1/unit_1", "xs/exit_flow/block1/unit_1",
+                          "xs/middle_flow/block1/unit_1", "xs/middle_flow/block1/unit_2",
+                          "xs/middle_flow/block1/unit_3"]
+    assert ep["xs/exit_flow/block1/unit_1"].shape == (2, 8, 8, 48)
+    y2, _ = xception.xception(torch.randn(2, 32, 32, 3), blocks=b, output_stride=4, scope="xs2")
+    assert y2.shape == (2, 8, 8, 48)
+    with pytest.raises(ValueError):
+        xception.xception(torch.randn(1, 32, 32, 3), blocks=b, output_stride=64, scope="xs3")
+    # two stride-2 units in one block: both stride (reference semantics)
+    b2 = [xception.xception_block("entry_flow/block1", [8, 8, 8], "conv", False, False, 2, 2)]
+    y3, _ = xception.xception(torch.randn(1, 32, 32, 3), blocks=b2, scope="xs4")
+    assert y3.shape == (1, 4, 4, 8)
 
 
 def test_xception_stack_blocks_dense():

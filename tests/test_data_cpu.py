@@ -41,9 +41,11 @@ def np_laplace(x):
     return out
 
 
-def np_transform(hflip, vflip, angle, tx, ty, H, W):
+def np_transform(hflip, vflip, angle, tx, ty, H, W, crop=None):
     """tf.contrib.image.compose_transforms(hflip, vflip, angles_to_projective_transforms,
-    translations_to_projective_transforms) as a flat 8-vector."""
+    translations_to_projective_transforms[, crop]) as a flat 8-vector; ``crop`` = (pct, left,
+    top) is the reference's crop transform [pct, 0, top, 0, pct, left, 0, 0]
+    (preprocessing.py:213-228)."""
     def m(t):
         return np.array([[t[0], t[1], t[2]], [t[3], t[4], t[5]], [t[6], t[7], 1.0]])
     ident = [1, 0, 0, 0, 1, 0, 0, 0]
@@ -55,6 +57,9 @@ def np_transform(hflip, vflip, angle, tx, ty, H, W):
     rot = [c, -s, xo, s, c, yo, 0, 0]
     tr = [1, 0, tx, 0, 1, ty, 0, 0]
     M = m(hf) @ m(vf) @ m(rot) @ m(tr)
+    if crop is not None:
+        pct, left, top = crop
+        M = M @ m([pct, 0, top, 0, pct, left, 0, 0])
     return (M / M[2, 2]).reshape(-1)[:8]
 
 
@@ -77,14 +82,14 @@ def np_warp(img, t, nearest):
             + ay * ((1 - ax) * at(y0 + 1, x0) + ax * at(y0 + 1, x0 + 1)))
 
 
-def np_augment(img, mask, transpose, hflip, vflip, angle, tx, ty, pad):
-    x = (img.astype(np.float64) - MEAN) / STD
+def np_augment(img, mask, transpose, hflip, vflip, angle, tx, ty, pad, bright=0.0, crop=None):
+    x = (img.astype(np.float64) - MEAN) / STD + bright
     x = np.pad(x, pad, mode="reflect")
     mk = np.pad(mask.astype(np.float64), pad, mode="reflect")
     if transpose:
         x, mk = x.T, mk.T
     H, W = x.shape
-    t = np_transform(hflip, vflip, angle, tx, ty, H, W)
+    t = np_transform(hflip, vflip, angle, tx, ty, H, W, crop)
     wi, wm = np_warp(x, t, False), np_warp(mk, t, True)
     h, w = img.shape
     return wi[pad:pad + h, pad:pad + w], wm[pad:pad + h, pad:pad + w]
@@ -131,6 +136,83 @@ def test_augment_matches_numpy_oracle(seed):
     # nearest sampling: allow a handful of exact-half rounding ties to differ
     assert (np.abs(om.numpy() - rm) > 1e-6).mean() < 0.01
     np.testing.assert_allclose(lap.numpy(), np_laplace(oi.numpy()), atol=1e-4)
+
+
+@pytest.mark.parametrize("pct,left,top", [(0.9, 5.0, 12.0), (1.1, -3.0, -7.5), (1.0, 0.0, 0.0)])
+def test_crop_transform_matrix(pct, left, top):
+    got = np.array(C.transform_matrix(True, False, 0.1, 3.0, -2.0, 181, 181, crop=True,
+                                      crop_pct=pct, crop_left=left, crop_top=top))
+    np.testing.assert_allclose(got, np_transform(True, False, 0.1, 3.0, -2.0, 181, 181,
+                                                 (pct, left, top)), rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_augment_crop_brightness_matches_numpy_oracle(seed):
+    """Random crop (scale / offset transform) and brightness delta, composed with the rest."""
+    rng = np.random.default_rng(100 + seed)
+    img = rng.random((21, 21)).astype(np.float32)
+    mask = (rng.random((21, 21)) > 0.5).astype(np.float32)
+    tp, hf, vf = bool(rng.random() > 0.5), bool(rng.random() < 0.5), bool(rng.random() < 0.5)
+    ang = float(rng.uniform(-0.17, 0.17))
+    tx, ty = float(rng.uniform(-8, 8)), float(rng.uniform(-8, 8))
+    pct = float(rng.uniform(0.9, 1.1))
+    left, top = float(rng.random() * 41 * (1 - pct)), float(rng.random() * 41 * (1 - pct))
+    br = float(rng.uniform(-0.3, 0.3))
+    oi, om, _ = C.augment_one(torch.from_numpy(img), torch.from_numpy(mask), tp, hf, vf, ang,
+                              tx, ty, 10, brightness=br, crop=True, crop_pct=pct,
+                              crop_left=left, crop_top=top)
+    ri, rm = np_augment(img, mask, tp, hf, vf, ang, tx, ty, 10, br, (pct, left, top))
+    np.testing.assert_allclose(oi.numpy(), ri, atol=2e-4)
+    assert (np.abs(om.numpy() - rm) > 1e-6).mean() < 0.01
+    # brightness only (identity geometry): the normalised image shifted by the delta
+    oi, _, _ = C.augment_one(torch.from_numpy(img), None, False, False, False, 0.0, 0.0, 0.0, 10,
+                             brightness=0.25)
+    np.testing.assert_allclose(oi.numpy(), (img - MEAN) / STD + 0.25, atol=1e-5)
+
+
+def test_loader_augmentation_options(tmp_path):
+    """The loader honours read_and_preprocess's knobs (crop_probability, brightness_range, flips,
+    rotation, shifts) and rejects invalid ones instead of dropping them."""
+    imgs, masks, _ = _write(str(tmp_path), n=4)
+    none = dict(horizontal_flip=False, vertical_flip=False, rotate_range=0.0,
+                crop_probability=0.0, height_shift_range=0.0, width_shift_range=0.0)
+
+    def first(aug):
+        L = C.BatchLoader(imgs, masks, 4, True, False, False, 3, 2, 2, 8, 0, False, aug)
+        x, y, _, _ = L.next()
+        return x.float(), y
+
+    base = first(none)
+    crop = first(dict(none, crop_probability=1.0, crop_min_percent=0.8, crop_max_percent=0.8))
+    bright = first(dict(none, brightness_range=0.5))
+    assert not torch.equal(base[0], crop[0]) and not torch.equal(base[1], crop[1])
+    d = (bright[0][..., 0] - base[0][..., 0]).reshape(4, -1)
+    # one delta per sample (bf16 storage rounding aside), |delta| <= 0.5
+    assert (d.max(1).values - d.min(1).values).abs().max() < 0.05
+    assert d.abs().max() <= 0.5 + 0.05 and d.abs().mean() > 1e-3
+    with pytest.raises(Exception):
+        C.BatchLoader(imgs, masks, 4, True, False, False, 3, 2, 2, 8, 0, False,
+                      dict(crop_probability=1.5))
+    with pytest.raises(Exception):
+        C.BatchLoader(imgs, masks, 4, True, False, False, 3, 2, 2, 8, 0, False,
+                      dict(no_such_knob=1))
+
+
+def test_read_and_preprocess_crop_and_brightness(tmp_path):
+    from tensorflowdistributedlearning_amd.preprocessing import preprocessing as P
+    imgs, masks, _ = _write(str(tmp_path), n=1, hw=21)
+    kw = dict(horizontal_flip=False, vertical_flip=False, rotate_range=0, height_shift_range=0,
+              width_shift_range=0)
+    a = P.read_and_preprocess(imgs[0], masks[0], True, crop_probability=0.0, **kw,
+                              rng=np.random.default_rng(0))
+    b = P.read_and_preprocess(imgs[0], masks[0], True, crop_probability=1.0,
+                              crop_min_percent=0.7, crop_max_percent=0.7, **kw,
+                              rng=np.random.default_rng(0))
+    assert not torch.equal(a[0]["images"], b[0]["images"])
+    with pytest.raises(ValueError):
+        P.read_and_preprocess(imgs[0], masks[0], True, crop_probability=2.0)
+    with pytest.raises(ValueError):
+        P.read_and_preprocess(imgs[0], masks[0], True, brightness_range=-1.0)
 
 
 def test_loader_eval_batches_exact(tmp_path):

@@ -224,8 +224,10 @@ def test_softmax_xent(gpu, dtype, smooth):
     assert rel_err(lg.grad, g_ref) < 2e-2
 
 
-@pytest.mark.parametrize("P_", [101 * 101, 64, 1000])
+@pytest.mark.parametrize("P_", [101 * 101, 64, 1000, 16385, 256 * 256, 300 * 300])
 def test_lovasz(gpu, P_):
+    """One-workgroup LDS sort up to 16384 px, the multi-pass global bitonic path above (any
+    input_shape beyond 128×128, as the reference's full top_k sort: core/losses.py:48-56)."""
     torch.manual_seed(7)
     Bn = 4
     logits = torch.randn(Bn, P_) * 2
@@ -237,6 +239,18 @@ def test_lovasz(gpu, P_):
     assert abs(loss.item() - l_ref.item()) < 1e-4 * max(1.0, abs(l_ref.item()))
     loss.backward()
     assert rel_err(lg.grad, g_ref) < 1e-3
+
+
+@pytest.mark.parametrize("P_", [5000, 200 * 200])
+def test_lovasz_ties(gpu, P_):
+    """Heavily tied errors: the loss is order-independent within a tie (Σ over a tied run of
+    e·Δjaccard telescopes), so it must match whatever tie order the reference sort picks."""
+    torch.manual_seed(9)
+    logits = torch.randint(-4, 5, (3, P_)).float() * 0.5
+    labels = (torch.rand(3, P_) > 0.5).float()
+    l_ref, _ = L.ref_lovasz_hinge(logits, labels)
+    loss = L.lovasz_hinge(logits.to(gpu), labels.to(gpu))
+    assert abs(loss.item() - l_ref.item()) < 1e-4 * max(1.0, abs(l_ref.item()))
 
 
 def test_seg_metrics(gpu):

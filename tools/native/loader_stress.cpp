@@ -19,10 +19,13 @@ int main(int argc, char** argv) {
   const std::vector<std::string> im = {d + "/i0.png", d + "/i1.png"}, mk = {d + "/m0.png", d + "/m1.png"};
   long batches = 0;
   for (int it = 0; it < iters; ++it) {
-    tdl_rt::BatchLoader L(im, mk, 4, true, true, true, (uint64_t)it, 8, 8, 8, 0, 0.0);
+    tdl_rt::AugConfig aug;  // every knob on: crop and brightness paths under the sanitizers too
+    aug.crop_probability = 0.5;
+    aug.brightness_range = 0.2;
+    tdl_rt::BatchLoader L(im, mk, 4, true, true, true, (uint64_t)it, 8, 8, 8, 0, aug);
     tdl_rt::Batch b;
     for (int k = 0; k < 3; ++k) batches += L.next(b) ? 1 : 0;
-    tdl_rt::BatchLoader E(im, mk, 3, false, false, false, 0, 4, 2, 8, 1, 0.0);  // eval + TTA
+    tdl_rt::BatchLoader E(im, mk, 3, false, false, false, 0, 4, 2, 8, 1);  // eval + TTA
     while (E.next(b)) ++batches;
   }
   std::printf("ok %ld batches\n", batches);
