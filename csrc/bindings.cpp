@@ -106,6 +106,13 @@ float* ring_slot(const Tensor& ring, int64_t k) {
   return ring.data_ptr<float>() + ((k % 3) + 3) % 3 * AMAX_SLOT;
 }
 
+// ptrs: int64 [n] device table of ring base addresses
+void fp8_roll(Tensor ptrs) {
+  TORCH_CHECK(ptrs.is_cuda() && ptrs.scalar_type() == torch::kInt64 && ptrs.is_contiguous(),
+              "fp8_roll: int64 device pointer table");
+  fp8_roll_launch((const unsigned long long*)ptrs.data_ptr<int64_t>(), (int)ptrs.numel(), stream());
+}
+
 void fp8_amax(Tensor x, Tensor ring, int64_t slot) {
   CHECK_T(x, torch::kBFloat16);
   TORCH_CHECK(x.numel() % 8 == 0, "numel % 8");
@@ -815,6 +822,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dh"), py::arg("dw"), py::arg("accumulate") = false, py::arg("mask") = py::none());
   m.attr("AMAX_SLOT") = AMAX_SLOT;
   m.def("fp8_amax", &fp8_amax);
+  m.def("fp8_roll", &fp8_roll);
   m.def("fp8_quantize", &fp8_quantize);
   m.def("fp8_multi_quantize", &fp8_multi_quantize);
   m.def("fp8_dequantize", &fp8_dequantize);

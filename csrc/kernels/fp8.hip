@@ -201,9 +201,25 @@ __global__ void dequantize_kernel(const uint8_t* __restrict__ y, long n, const f
   }
 }
 
+// End-of-step roll of every delayed-scaling amax ring (graph-capturable: the slot roles are fixed,
+// the data moves): slot 0 (read by the next call) ← slot 1 (accumulated by this step's call),
+// slot 1 ← 0.  rings: n ring base addresses (fp32 [3][AMAX_SLOT] each)
+__global__ void __launch_bounds__(NT) roll_kernel(const unsigned long long* __restrict__ rings) {
+  float* r = (float*)rings[blockIdx.x];
+  for (int t = threadIdx.x; t < AMAX_SLOT; t += NT) {
+    r[t] = r[AMAX_SLOT + t];
+    r[AMAX_SLOT + t] = 0.f;
+  }
+}
+
 inline int grid_for(long n) { return (int)std::min<long>(4096, std::max<long>(1, (n + NT - 1) / NT)); }
 
 }  // namespace
+
+void fp8_roll_launch(const unsigned long long* rings, int n, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(roll_kernel, dim3(n), dim3(NT), 0, st, rings);
+}
 
 void fp8_amax_launch(const bf16_t* x, long n, float* slot, hipStream_t st) {
   if (n <= 0) return;

@@ -96,6 +96,8 @@ void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStr
 // fp8 (OCP e4m3) forward conv: a.x / a.w point at e4m3 bytes, a.scale_x / a.scale_w at their fp32 scales
 void conv_fwd_fp8_launch(const ConvArgs& a, hipStream_t st);
 void fp8_amax_launch(const bf16_t* x, long n, float* slot, hipStream_t st);
+// end-of-step roll of n amax rings (device pointer table): slot0 ← slot1, slot1 ← 0
+void fp8_roll_launch(const unsigned long long* rings, int n, hipStream_t st);
 // prev: amax slot giving the scale; meas (optional): slot accumulating |x|max; clr (optional):
 // slot cleared for the next call
 void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,

@@ -17,6 +17,7 @@ from ..parallel.bucketer import GradBucketer
 from ..parallel.dist import get_context
 from .optimizer import build_optimizer
 from ..ops import workspace, streams
+from ..ops.fp8 import RingRoller
 
 
 class PhaseTimer:
@@ -84,6 +85,9 @@ class Trainer:
         self.train_mode = True  # False: BN uses moving statistics while training (frozen BN)
         self.timer = PhaseTimer(self.device) if profile_phases else None
         self.graph = None  # HIP graph of one whole step (capture / replay)
+        # fp8 delayed scaling: one end-of-step device roll of every amax ring (ops/fp8.py)
+        # (a no-op until the model's first fp8 scaler exists)
+        self.fp8_roller = RingRoller(self.model)
 
     # ------------------------------------------------------------------------------------------
     def broadcast_state(self):
@@ -125,6 +129,7 @@ class Trainer:
         if t:
             t.mark("comm_wait")
         self.optimizer.step(grad_scale=1.0 / world)
+        self.fp8_roller.roll(self.device)
         if t:
             t.mark("optimizer")
             t.end_step()
@@ -144,16 +149,14 @@ class Trainer:
         (every GPU run with world > 1) the bucketed all-reduces are captured into the graph too
         (csrc/runtime/comm.cpp forks its comm stream into the capture) and overlap backward at
         every replay; each replay is registered with the communicator's watchdog, so a replay
-        whose collectives hang is timed out like an eager collective.
-        The fp8 delayed-scaling state rotates on the host, so fp8 models are not capturable."""
+        whose collectives hang is timed out like an eager collective.  fp8 models capture too:
+        their delayed-scaling state has fixed slot roles and is rolled on the device once per
+        step (ops/fp8.RingRoller), so no kernel argument changes between steps."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs a GPU")
         if self.bucketer is not None and getattr(self.ctx, "native", None) is None:
             raise RuntimeError("data-parallel graph capture needs the native RCCL communicator "
                                "(GPU ranks; not the TDL_SHARE_GPU gloo rehearsal)")
-        if any(getattr(m, "fp8", False) or getattr(m, "emit_fp8", False)
-               for m in self.model.modules()):
-            raise RuntimeError("fp8 delayed scaling keeps host-side state: not capturable")
         self.timer = None
         self.static_x = x.detach().clone()
         self.static_y = y.detach().clone()

@@ -24,6 +24,67 @@ def _new_ring(device):
     return torch.zeros(3, AMAX_SLOT, device=device, dtype=torch.float32)
 
 
+# ---- device-side rotation of the delayed-scaling state (graph-capturable) --------------------
+# Every delayed-scaling ring keeps fixed slot roles: slot 0 = the previous call's |x|max (scale
+# source), slot 1 = accumulates this call's.  The data moves instead of the roles: ONE launch per
+# training step rolls every ring of the model (slot 0 ← slot 1, slot 1 ← 0; fp8_roll), issued by
+# the Trainer after the optimizer — so no kernel argument changes from step to step and the whole
+# fp8 step can be captured as a HIP graph.  A scaler called twice with no roll in between (direct
+# use outside a Trainer) rolls its own ring first, which keeps the per-call delayed semantics.
+_STATE = {"rolls": 0, "rings_made": 0}
+
+
+def _rolls(device=None):
+    return _STATE["rolls"]
+
+
+def _self_roll(table):
+    ext().fp8_roll(table)
+
+
+class RingRoller:
+    """The end-of-step roll of every delayed-scaling ring of ``model`` (its DelayedScalers and
+    the FlatFp8Weights of its flat parameter buffer): one launch over a device pointer table,
+    rebuilt only when scalers were created since (they appear lazily in the first forwards)."""
+
+    def __init__(self, model):
+        self.model = model
+        self.table = None
+        self.keep = []
+        self.built_at = -1
+
+    def _scan(self):
+        rings = []
+        seen = set()
+        for m in self.model.modules():
+            for k in ("_fp8_w", "_fp8_x", "_fp8", "_fp8_bwd"):
+                sc = m.__dict__.get(k)
+                if isinstance(sc, DelayedScaler) and sc.ring is not None:
+                    rings.append((sc.ring, 0))
+            for prm in m.parameters(recurse=False):
+                flat = getattr(prm, "_flat_lowp", None)
+                fw = getattr(flat, "_tdl_fp8w", None) if flat is not None else None
+                if fw is not None and id(fw) not in seen and getattr(fw, "rings", None) is not None:
+                    seen.add(id(fw))
+                    for seg in range(fw.rings.shape[0]):
+                        rings.append((fw.rings, seg * 3 * AMAX_SLOT * 4))
+        return rings
+
+    def roll(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            return
+        if self.built_at != _STATE["rings_made"]:
+            rings = self._scan()
+            self.keep = [t for t, _ in rings]
+            self.table = (torch.tensor([t.data_ptr() + o for t, o in rings], dtype=torch.int64)
+                          .to(device) if rings else None)
+            self.built_at = _STATE["rings_made"]
+        if self.table is not None:
+            ext().fp8_roll(self.table)
+            _STATE["rolls"] += 1
+
+
 def quantize_e4m3(x):
     """Just-in-time scaling: scale from this tensor's own amax (amax pass + quantise pass)."""
     if on_gpu(x):
@@ -67,52 +128,55 @@ def transpose_weight(w8):
 
 class DelayedScaler:
     """Per-tensor delayed scaling (the fp8 training recipe): call t quantises with the |x|max
-    measured by call t−1 while measuring its own — one pass over x, no host sync, no memset
-    (a 3-slot amax ring: read p, accumulate p+1, clear p+2).  The very first call primes the
-    ring with an amax pass, so it is exact.  Values beyond the previous amax saturate at ±448.
-    ``bn_args`` hands the same state to the BN apply kernel's fused e4m3 side output
-    (ops/bn.py), whose first call only measures.
-
-    The scale each call produces lives in one of 3 preallocated slots rotating with the phase: a
-    consumer kernel of call t is stream-ordered before call t+3 rewrites the slot, and no
-    allocation or view is created per call (this state is touched once per layer per step, so its
-    host cost is on the critical path of launch-bound steps)."""
+    measured by call t−1 while measuring its own — one pass over x, no host sync, no memset.
+    The ring's slot 0 holds the previous |x|max, slot 1 accumulates this call's; the end-of-step
+    :func:`roll_all` moves slot 1 into slot 0 on the device (a self-roll covers back-to-back
+    calls without a Trainer step in between), so the kernel arguments never change and the step
+    is graph-capturable.  The very first call primes the ring with an amax pass, so it is exact.
+    Values beyond the previous amax saturate at ±448.  ``bn_args`` hands the same state to the BN
+    apply kernel's fused e4m3 side output (ops/bn.py), whose first call only measures.  The
+    scale a call produces lives in one preallocated slot: its consumers (the conv of the same
+    step) are stream-ordered before the next call rewrites it."""
 
     def __init__(self):
         self.ring = None
-        self.scale_slots = None
-        self.phase = 0
+        self.scale = None
         self.calls = 0
+        self.last_roll = None
 
     def _ensure(self, device):
         if self.ring is None or self.ring.device != device:
             self.ring = _new_ring(device)
-            slots = torch.zeros(3, 1, device=device, dtype=torch.float32)
-            self.scale_slots = [slots[i] for i in range(3)]
-            self.phase = 0
+            self.scale = torch.zeros(1, device=device, dtype=torch.float32)
+            self.self_table = torch.tensor([self.ring.data_ptr()], dtype=torch.int64).to(device)
+            _STATE["rings_made"] += 1
             self.calls = 0
+            self.last_roll = None
 
-    def _advance(self):
-        self.phase = (self.phase + 1) % 3
-        self.calls += 1
+    def _begin(self, device):
+        rolls = _rolls()
+        if self.calls > 0 and self.last_roll == rolls:
+            _self_roll(self.self_table)  # second call since the last step roll
+        self.last_roll = rolls
 
     def quantize(self, x):
         if not on_gpu(x):
             return quantize_e4m3(x)
         self._ensure(x.device)
+        self._begin(x.device)
         xc = x.contiguous()
         if self.calls == 0:
-            ext().fp8_amax(xc, self.ring, self.phase)
+            ext().fp8_amax(xc, self.ring, 0)
         y8 = torch.empty(x.shape, device=x.device, dtype=E4M3)
-        scale = self.scale_slots[self.phase]
-        ext().fp8_quantize(xc, self.ring, self.phase, True, scale, y8.view(torch.uint8))
-        self._advance()
-        return y8, scale
+        ext().fp8_quantize(xc, self.ring, 0, True, self.scale, y8.view(torch.uint8))
+        self.calls += 1
+        return y8, self.scale
 
     def bn_args(self, x):
         self._ensure(x.device)
-        out = (self.ring, self.phase, self.scale_slots[self.phase], self.calls > 0)
-        self._advance()
+        self._begin(x.device)
+        out = (self.ring, 0, self.scale, self.calls > 0)
+        self.calls += 1
         return out
 
 
@@ -135,7 +199,8 @@ class FlatFp8Weights:
         self.pending = {}   # id(param) -> (offset, numel, shape)
         self.spans = []     # segment -> (offset, numel, shape)
         self.version = None
-        self.phase = 0
+        self.last_roll = None
+        self.rings = None
 
     def _rebuild(self):
         keys = list(self.views) + list(self.pending)
@@ -151,6 +216,10 @@ class FlatFp8Weights:
         dev = self.flat.device
         self.chunks = torch.tensor(rows, dtype=torch.int64).to(dev)
         self.rings = torch.zeros(len(self.spans), 3, AMAX_SLOT, device=dev)
+        _STATE["rings_made"] += 1  # rolled with the model's other rings (RingRoller)
+        self.self_table = torch.tensor([self.rings.data_ptr() + seg * 3 * AMAX_SLOT * 4
+                                        for seg in range(len(self.spans))],
+                                       dtype=torch.int64).to(dev)
         self.scales = torch.zeros(len(self.spans), device=dev)
         self.views = {k: (self.w8[off:off + n].view(shape), self.scales[seg:seg + 1])
                       for seg, (k, (off, n, shape)) in enumerate(zip(keys, self.spans))}
@@ -167,9 +236,9 @@ class FlatFp8Weights:
         self.tiles = torch.tensor(trows if trows else [(0, 16, 16, 0)],
                                   dtype=torch.int64).to(dev)
         self.ntiles = len(trows)
-        self.phase = 0
+        self.last_roll = None
         ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
-                                 self.scales, self.phase, True)  # prime: exact first scales
+                                 self.scales, 0, True)  # prime: exact first scales
 
     def get(self, p, version):
         """(w8, scale) for parameter ``p`` at parameter version ``version``, or None the first
@@ -185,12 +254,15 @@ class FlatFp8Weights:
         if self.version != version:
             if self.pending:
                 self._rebuild()
+            rolls = _rolls()
+            if self.last_roll == rolls:
+                _self_roll(self.self_table)  # refreshed twice with no step roll in between
+            self.last_roll = rolls
             ext().fp8_multi_quantize(self.flat, self.w8.view(torch.uint8), self.chunks, self.rings,
-                                     self.scales, self.phase, False)
+                                     self.scales, 0, False)
             if self.ntiles:
                 ext().fp8_multi_transpose(self.w8.view(torch.uint8), self.w8t.view(torch.uint8),
                                           self.tiles)
-            self.phase = (self.phase + 1) % 3
             self.version = version
 
     def get_t(self, p, version):

@@ -690,3 +690,55 @@ def test_large_batch_matches_split_batches(gpu, batch):
     cos = torch.nn.functional.cosine_similarity(g_big, gsum, dim=0).item()
     assert cos > 0.999, cos
     assert ((g_big - gsum).norm() / gsum.norm()).item() < 0.03
+
+
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_fp8_graph_replay_matches_eager(gpu, dgrad):
+    """fp8 models are graph-capturable: the delayed-scaling amax rings keep fixed slot roles and
+    are rolled on the device once per step (ops/fp8.RingRoller), so a captured fp8 step follows
+    the eager fp8 trajectory (frozen BN; tolerance for the BN backward's fp32 atomic order)."""
+    torch.manual_seed(8)
+    nets = [models.resnet18(num_classes=10) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    for n in nets:
+        assert models.enable_fp8(n, dgrad=dgrad) > 10
+    ta, tb = [Trainer(n, softmax_cross_entropy, gpu, "sgd", dict(lr=0.02, momentum=0.9))
+              for n in nets]
+    ta.train_mode = tb.train_mode = False
+    x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
+    tb.capture(x, y, warmup=3)
+    for _ in range(3):
+        ta.train_step(x, y)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(ta.flat.master, tb.flat.master, rtol=1e-4, atol=1e-6)
+    m0 = ta.flat.master.clone()
+    la_l, lb_l = [], []
+    for _ in range(4):
+        la, _ = ta.train_step(x, y)
+        lb, _ = tb.replay()
+        la_l.append(float(la))
+        lb_l.append(float(lb))
+    torch.cuda.synchronize()
+    ua, ub = ta.flat.master - m0, tb.flat.master - m0
+    assert ua.norm() > 0 and torch.isfinite(ub).all()
+    cos = torch.nn.functional.cosine_similarity(ua, ub, dim=0).item()
+    assert cos > 0.995, cos
+    for a_, b_ in zip(la_l, lb_l):  # the losses move step to step and agree
+        assert abs(a_ - b_) < 2e-3 * max(1.0, abs(a_)), (la_l, lb_l)
+    assert len(set(round(v, 5) for v in lb_l)) > 1, lb_l
+
+
+def test_fp8_delayed_scaling_rolls_on_device(gpu):
+    """The scale a DelayedScaler uses at call t is the |x|max of call t−1 (device-side roll by
+    the Trainer's RingRoller, self-roll for back-to-back direct calls)."""
+    from tensorflowdistributedlearning_amd.ops.fp8 import DelayedScaler, E4M3_MAX
+    sc = DelayedScaler()
+    xs = [torch.randn(4096, device=gpu, dtype=torch.bfloat16) * s for s in (1.0, 3.0, 0.5, 2.0)]
+    scales = []
+    for x in xs:
+        _, s = sc.quantize(x)
+        scales.append(float(s))
+    am = [float(x.float().abs().max()) for x in xs]
+    assert abs(scales[0] - am[0] / E4M3_MAX) < 1e-6 * am[0]  # first call primes (exact)
+    for t in (1, 2, 3):
+        assert abs(scales[t] - am[t - 1] / E4M3_MAX) < 1e-6 * max(am), (t, scales, am)
