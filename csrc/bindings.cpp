@@ -21,7 +21,26 @@ hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
   TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype ", (t).scalar_type())
 
 #define BF(t) reinterpret_cast<const bf16_t*>((t).data_ptr())
+// NHWC bf16 tensor that is contiguous or a channel slice [..., c0:c0+C] of a contiguous NHWC
+// buffer (the concat-free ASPP / decoder): returns the pixel stride in elements
+static int64_t nhwc_ld(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16, what, ": bf16 HIP tensor");
+  if (t.is_contiguous()) return t.size(-1);
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.stride(2) >= t.size(3) &&
+                  t.stride(1) == t.stride(2) * t.size(2) && t.stride(0) == t.stride(1) * t.size(1),
+              what, ": must be contiguous NHWC or a channel slice of a contiguous NHWC buffer");
+  return t.stride(2);
+}
 #define BFW(t) reinterpret_cast<bf16_t*>((t).data_ptr())
+// row stride of a strided operand of the vector BN kernels (8-element vectors, 16-byte aligned)
+static int64_t bn_vec_ld(const at::Tensor& t, int64_t C, const char* what) {
+  const int64_t ld = nhwc_ld(t, what);
+  if (ld != C)
+    TORCH_CHECK(C % 8 == 0 && C <= 2048 && ld % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+                what, ": a channel slice needs C % 8 == 0, C <= 2048, 8-aligned offset and stride");
+  return ld;
+}
 
 const float* optf(const c10::optional<Tensor>& t) {
   if (!t.has_value() || !t->defined()) return nullptr;
@@ -307,9 +326,11 @@ void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool r
               c10::optional<Tensor> y8, c10::optional<Tensor> amax_ring, int64_t phase,
               c10::optional<Tensor> scale_out, c10::optional<Tensor> mask) {
   CHECK_T(x, torch::kBFloat16);
-  CHECK_T(y, torch::kBFloat16);
   CHECK_T(coef, torch::kFloat32);
   const int64_t C = x.size(-1);
+  // y may be a channel slice of a wider NHWC buffer (concat-free ASPP / decoder)
+  const int64_t ldy = bn_vec_ld(y, C, "bn_apply y");
+  TORCH_CHECK(y.numel() == x.numel(), "bn_apply: y and x sizes");
   uint8_t* y8p = nullptr;
   float *prev = nullptr, *out = nullptr, *zero = nullptr;
   if (amax_ring.has_value() && amax_ring->defined()) {
@@ -334,7 +355,7 @@ void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool r
     maskp = (uint8_t*)mask->data_ptr();
   }
   bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu,
-                  stream(), y8p, prev, optfw(scale_out), out, zero, maskp);
+                  stream(), y8p, prev, optfw(scale_out), out, zero, maskp, ldy);
 }
 
 // relu mode 3: `y` is the uint8 bit mask bn_apply wrote (vector kernels only: C % 8 == 0 and
@@ -349,13 +370,14 @@ const bf16_t* mask_or_y(const c10::optional<Tensor>& y, const Tensor& x, int64_t
 }
 
 void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, int64_t relu) {
-  CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(red, torch::kFloat32);
   const int64_t C = x.size(-1);
+  const int64_t ldd = bn_vec_ld(dy, C, "bn_bwd_reduce dy");  // dy: contiguous or channel slice
+  TORCH_CHECK(dy.numel() == x.numel(), "bn_bwd_reduce: dy and x sizes");
   TORCH_CHECK(relu != 1 || (y.has_value() && y->defined()), "relu mask mode 1 needs y");
   bn_bwd_reduce_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(),
-                       red.data_ptr<float>(), x.numel() / C, C, (int)relu, stream());
+                       red.data_ptr<float>(), x.numel() / C, C, (int)relu, stream(), ldd);
 }
 
 bool bn_bwd_reduce2(Tensor dy, Tensor x, Tensor x2, Tensor coef, Tensor red, Tensor red2) {
@@ -376,10 +398,11 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
                   int64_t relu, c10::optional<Tensor> dx8, c10::optional<Tensor> amax_ring,
                   int64_t phase, c10::optional<Tensor> scale_out, bool red_raw) {
-  CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   const int64_t C = x.size(-1);
+  const int64_t ldd = bn_vec_ld(dy, C, "bn_bwd_apply dy");  // dy: contiguous or channel slice
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn_bwd_apply: dy, x, dx sizes");
   uint8_t* d8 = nullptr;
   float *prev = nullptr, *out = nullptr, *zero = nullptr;
   if (amax_ring.has_value() && amax_ring->defined()) {  // e5m2 side output (fp8 dgrad)
@@ -395,7 +418,7 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
   bn_bwd_apply_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
                       optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
                       C, (float)count, (int)relu, stream(), d8, prev, optfw(scale_out), out, zero,
-                      red_raw);
+                      red_raw, ldd);
 }
 
 // ---------------------------------------------------------------------------------- elementwise
@@ -612,20 +635,19 @@ void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int
 // ------------------------------------------------------------------------------------- upsample
 void upsample_fwd(Tensor x, Tensor y, Tensor ih, Tensor wh, Tensor iw, Tensor ww) {
   CHECK_T(x, torch::kBFloat16);
-  CHECK_T(y, torch::kBFloat16);
+  const int64_t ldy = nhwc_ld(y, "upsample y");
   upsample_fwd_launch(BF(x), BFW(y), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
                       ww.data_ptr<float>(), x.size(0), x.size(1), x.size(2), x.size(3), y.size(1),
-                      y.size(2), stream());
+                      y.size(2), stream(), (int)ldy);
 }
 
 void upsample_bwd(Tensor dy, Tensor dx, Tensor ih, Tensor wh, Tensor iw, Tensor ww) {
-  CHECK_T(dy, torch::kBFloat16);
+  const int64_t ldd = nhwc_ld(dy, "upsample dy");
   CHECK_T(dx, torch::kBFloat16);
   upsample_bwd_launch(BF(dy), BFW(dx), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
-                      ww.data_ptr<float>(), dx.size(0), dx.size(1), dx.size(2), dx.size(3),
-                      dy.size(1), dy.size(2), stream());
+                      ww.data_ptr<float>(), dx.size(0), dx.size(1), dx.size(2), dx.size(3), dy.size(1),
+                      dy.size(2), stream(), (int)ldd);
 }
-
 
 // --------------------------------------------------------------------------- native data loader
 // ------------------------------------------------------------------------- native RCCL comm

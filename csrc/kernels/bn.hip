@@ -74,7 +74,8 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ x,
                                                         const float* __restrict__ coef,
                                                         float* __restrict__ out, long M, int C,
-                                                        long rows_per_block, int relu) {
+                                                        long rows_per_block, int relu, long lda) {
+  // lda: row stride (elements) of `a` (C, or wider for a channel slice of a concat gradient)
   __shared__ float red[2][NT][9];  // +1 pad against bank conflicts
   const int cvecs = C >> 3;
   const int rpp = NT / cvecs;  // rows per pass
@@ -103,8 +104,9 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long rr = r + u * rpp;
-        const long off = (rr < r1 ? rr : r) * C + cv * 8;
-        la[u] = *(const uint4*)(a + off);
+        const long row = rr < r1 ? rr : r;
+        const long off = row * C + cv * 8;
+        la[u] = *(const uint4*)(a + row * lda + cv * 8);
         if (KIND == 1) lx[u] = *(const uint4*)(x + off);
         if (KIND == 1 && relu == 1) ly[u] = *(const uint4*)(y + off);
         if (KIND == 1 && relu == 3) lm[u] = ((const uint8_t*)y)[off >> 3];
@@ -240,7 +242,8 @@ __global__ void __launch_bounds__(NT) reduce2_vec_kernel(const bf16_t* __restric
 
 template <int KIND>
 void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const float* coef, float* out,
-                   long M, int C, int relu, hipStream_t st) {
+                   long M, int C, int relu, hipStream_t st, long lda = 0) {
+  if (lda <= 0) lda = C;
   if (M <= 0) return;
   if (C % 8 == 0 && C / 8 <= NT) {
     // ≈ one or two workgroups per CU, ≥ 16 rows per thread: few atomics per output address
@@ -259,13 +262,13 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     blocks = (M + rpb - 1) / rpb;
     if (u == 8)
       hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                         out, M, C, rpb, relu);
+                         out, M, C, rpb, relu, lda);
     else if (u == 2)
       hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                         out, M, C, rpb, relu);
+                         out, M, C, rpb, relu, lda);
     else
       hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                         out, M, C, rpb, relu);
+                         out, M, C, rpb, relu, lda);
   } else {
     long blocks = std::min<long>(512, std::max<long>(1, M / 64));
     long rpb = (M + blocks - 1) / blocks;
@@ -327,7 +330,9 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
                                                        float* __restrict__ scale_out,
                                                        float* __restrict__ amax_out,
                                                        float* __restrict__ amax_zero,
-                                                       uint8_t* __restrict__ mask) {
+                                                       uint8_t* __restrict__ mask, int ldy_v) {
+  // ldy_v: y's row stride in 8-element vectors (C/8 contiguous; wider when y is a channel slice
+  // of a concat buffer — the concat-free ASPP / decoder)
   float inv8 = 0.f, vmax = 0.f;
   bool emit8 = false;
   if (amax_out) {
@@ -382,7 +387,7 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
     const uint4 packed = pack8(v);
-    ((uint4*)y)[k] = packed;
+    ((uint4*)y)[ldy_v == cvecs ? k : (k / cvecs) * ldy_v + k % cvecs] = packed;
     if (mask) {  // ReLU mask of the stored bf16 values, one bit per element (backward relu mode 3)
       float q[8];
       unpack8(packed, q);
@@ -445,7 +450,8 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dgamma,
     float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu,
     uint8_t* __restrict__ dx8, const float* __restrict__ amax_prev, float* __restrict__ scale_out,
-    float* __restrict__ amax_out, float* __restrict__ amax_zero, int red_raw) {
+    float* __restrict__ amax_out, float* __restrict__ amax_zero, int red_raw, int ldd_v) {
+  // ldd_v: dy's row stride in 8-element vectors (a channel slice of a concat gradient when > C/8)
   // red_raw: red = (Σg, Σg·x) accumulated by the producing dgrad's epilogue (conv_common.h);
   // Σg·x̂ = invstd·(Σg·x − mean·Σg) here
   // optional e5m2 side output of dx (fp8 dgrad of the producing conv; delayed scaling with 4×
@@ -510,7 +516,7 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long k = i + u * stride < nvec ? i + u * stride : i;
-      lg[u] = ((const uint4*)dy)[k];
+      lg[u] = ((const uint4*)dy)[ldd_v == cvecs ? k : (k / cvecs) * ldd_v + k % cvecs];
       lx[u] = ((const uint4*)x)[k];
       if (relu == 1) ly[u] = ((const uint4*)y)[k];
       if (relu == 3) lm[u] = ((const uint8_t*)y)[k];
@@ -621,13 +627,16 @@ void bn_finalize_launch(const float* stats, float* coef, const float* gamma, con
 
 void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16_t* y, long M,
                      int C, bool relu, hipStream_t st, uint8_t* y8, const float* amax_prev,
-                     float* scale_out, float* amax_out, float* amax_zero, uint8_t* mask) {
+                     float* scale_out, float* amax_out, float* amax_zero, uint8_t* mask,
+                     long ldy) {
   const long n = M * C;
+  if (ldy <= 0) ldy = C;
   if (C % 8 == 0) {
     static const int u = env_int("TDL_BN_APPLY_U", 1);
     auto k = u == 2 ? apply_vec_kernel<2> : u == 4 ? apply_vec_kernel<4> : apply_vec_kernel<1>;
     hipLaunchKernelGGL(k, dim3(ew_blocks(n / 8, C / 8, u)), dim3(NT), 0, st, x, coef, res, y, n / 8, C,
-                       relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask);
+                       relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask,
+                       (int)(ldy / 8));
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
                        C, relu ? 1 : 0);
@@ -635,8 +644,8 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
 }
 
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                          float* red, long M, int C, int relu, hipStream_t st) {
-  reduce_launch<1>(dy, y, x, coef, red, M, C, relu, st);
+                          float* red, long M, int C, int relu, hipStream_t st, long ldd) {
+  reduce_launch<1>(dy, y, x, coef, red, M, C, relu, st, ldd);
 }
 
 bool bn_bwd_reduce2_launch(const bf16_t* dy, const bf16_t* x, const bf16_t* x2, const float* coef,
@@ -656,8 +665,9 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,
                          hipStream_t st, uint8_t* dx8, const float* amax_prev, float* scale_out,
-                         float* amax_out, float* amax_zero, bool red_raw) {
+                         float* amax_out, float* amax_zero, bool red_raw, long ldd) {
   const long n = M * C;
+  if (ldd <= 0) ldd = C;
   if (C % 8 == 0) {
     static const int u = env_int("TDL_BN_BWD_U", 2);
     const int blocks = ew_blocks(n / 8, C / 8, u);
@@ -667,7 +677,7 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                    : bwd_apply_vec_kernel<false, 1>;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
                        dbeta, n / 8, C, 1.f / count, relu, dx8, amax_prev, scale_out, amax_out,
-                       amax_zero, red_raw ? 1 : 0);
+                       amax_zero, red_raw ? 1 : 0, (int)(ldd / 8));
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu,

@@ -130,9 +130,11 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
                      int C, bool relu, hipStream_t st, uint8_t* y8 = nullptr,
                      const float* amax_prev = nullptr, float* scale_out = nullptr,
                      float* amax_out = nullptr, float* amax_zero = nullptr,
-                     uint8_t* mask = nullptr);  // mask: 1 bit per element of y > 0 (C % 8 == 0)
+                     uint8_t* mask = nullptr,  // mask: 1 bit per element of y > 0 (C % 8 == 0)
+                     long ldy = 0);  // y row stride (elements; 0 = C): y a channel slice of a concat buffer
 void bn_bwd_reduce_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* coef,
-                          float* red, long M, int C, int relu, hipStream_t st);  // relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0, 3 bit mask (y = uint8 mask, C % 8 == 0, C <= 2048)
+                          float* red, long M, int C, int relu, hipStream_t st,
+                          long ldd = 0);  // ldd: dy row stride (0 = C; C % 8 == 0, C <= 2048) relu: 0 none, 1 mask y>0, 2 mask x·scale+shift>0, 3 bit mask (y = uint8 mask, C % 8 == 0, C <= 2048)
 // two BNs fed the same (unmasked) gradient dy: red = (Σdy, Σdy·x̂) of x (coef), red2 = (Σdy,
 // Σdy·x2) raw; false (nothing launched) unless C % 8 == 0 and C <= 2048
 bool bn_bwd_reduce2_launch(const bf16_t* dy, const bf16_t* x, const bf16_t* x2, const float* coef,
@@ -146,7 +148,8 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          hipStream_t st, uint8_t* dx8 = nullptr, const float* amax_prev = nullptr,
                          float* scale_out = nullptr, float* amax_out = nullptr,
                          float* amax_zero = nullptr,
-                         bool red_raw = false);  // red = (Σg, Σg·x) from a fused dgrad epilogue
+                         bool red_raw = false,  // red = (Σg, Σg·x) from a fused dgrad epilogue
+                         long ldd = 0);  // dy row stride (elements; 0 = C)
 
 // elementwise --------------------------------------------------------------------------------
 // t [N][H][Wo][Cp] = row-packed x [N][H][W][Cx] for a k×k stem conv (first Cr channels, S taps of
@@ -223,12 +226,14 @@ void splitk_reduce_launch(const float* slab, float* out, long n, int splits, boo
                           hipStream_t st);
 
 // upsample (TF1 legacy bilinear with symmetric pad) -----------------------------------------
+// ldy / ldd: pixel stride (elements) of y / dy — C, or wider for a channel slice of a concat
+// buffer (concat-free ASPP / decoder); <= 0 means C
 void upsample_fwd_launch(const bf16_t* x, bf16_t* y, const int* ih, const float* wh,
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
-                         int Wo, hipStream_t st);
+                         int Wo, hipStream_t st, int ldy = 0);
 void upsample_bwd_launch(const bf16_t* dy, bf16_t* dx, const int* ih, const float* wh,
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
-                         int Wo, hipStream_t st);
+                         int Wo, hipStream_t st, int ldd = 0);
 
 // fault injection: a 1-lane kernel that spins `ms` milliseconds (≤ 60 s) on stream st
 void debug_spin_launch(double ms, hipStream_t st);

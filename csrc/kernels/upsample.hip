@@ -16,7 +16,8 @@ template <int V>
 __global__ void up_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                               const int* __restrict__ ih, const float* __restrict__ wh,
                               const int* __restrict__ iw, const float* __restrict__ ww, int N, int H,
-                              int W, int C, int Ho, int Wo) {
+                              int W, int C, int Ho, int Wo, int ldy) {
+  // ldy: pixel stride of y in elements (C, or wider: y is a channel slice of a concat buffer)
   const int cv = C / V;
   const long total = (long)N * Ho * Wo * cv;
   for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
@@ -49,7 +50,7 @@ __global__ void up_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__
 #pragma unroll
         for (int k = 0; k < V; ++k) acc[k] += wgt * v[k];
       }
-    bf16_t* dst = y + (((long)n * Ho + i) * Wo + j) * C + c;
+    bf16_t* dst = y + (((long)n * Ho + i) * Wo + j) * ldy + c;
     if constexpr (V == 8) *(uint4*)dst = pack8(acc);
     else *dst = f2bf(acc[0]);
   }
@@ -59,7 +60,8 @@ template <int V>
 __global__ void up_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
                               const int* __restrict__ ih, const float* __restrict__ wh,
                               const int* __restrict__ iw, const float* __restrict__ ww, int N, int H,
-                              int W, int C, int Ho, int Wo) {
+                              int W, int C, int Ho, int Wo, int ldd) {
+  // ldd: pixel stride of dy in elements (a channel slice of a concat buffer's gradient)
   const int cv = C / V;
   const long total = (long)N * H * W * cv;
   for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
@@ -80,7 +82,7 @@ __global__ void up_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict_
       for (int j = jlo; j <= jhi; ++j) {
         const float wj = (iw[j] == b ? ww[j] : 0.f) + (iw[Wo + j] == b ? ww[Wo + j] : 0.f);
         if (wj == 0.f) continue;
-        const bf16_t* src = dy + (((long)n * Ho + i) * Wo + j) * C + c;
+        const bf16_t* src = dy + (((long)n * Ho + i) * Wo + j) * ldd + c;
         float v[V];
         if constexpr (V == 8) unpack8(*(const uint4*)src, v);
         else v[0] = bf2f(*src);
@@ -99,26 +101,28 @@ __global__ void up_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict_
 
 void upsample_fwd_launch(const bf16_t* x, bf16_t* y, const int* ih, const float* wh, const int* iw,
                          const float* ww, int N, int H, int W, int C, int Ho, int Wo,
-                         hipStream_t st) {
+                         hipStream_t st, int ldy) {
   const long n = (long)N * Ho * Wo * C;
-  if (C % 8 == 0)
+  if (ldy <= 0) ldy = C;
+  if (C % 8 == 0 && ldy % 8 == 0)
     hipLaunchKernelGGL(up_fwd_kernel<8>, dim3(blocks_for(n / 8)), dim3(NT), 0, st, x, y, ih, wh, iw, ww,
-                       N, H, W, C, Ho, Wo);
+                       N, H, W, C, Ho, Wo, ldy);
   else
     hipLaunchKernelGGL(up_fwd_kernel<1>, dim3(blocks_for(n)), dim3(NT), 0, st, x, y, ih, wh, iw, ww, N,
-                       H, W, C, Ho, Wo);
+                       H, W, C, Ho, Wo, ldy);
 }
 
 void upsample_bwd_launch(const bf16_t* dy, bf16_t* dx, const int* ih, const float* wh,
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho, int Wo,
-                         hipStream_t st) {
+                         hipStream_t st, int ldd) {
   const long n = (long)N * H * W * C;
-  if (C % 8 == 0)
+  if (ldd <= 0) ldd = C;
+  if (C % 8 == 0 && ldd % 8 == 0)
     hipLaunchKernelGGL(up_bwd_kernel<8>, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, dx, ih, wh, iw,
-                       ww, N, H, W, C, Ho, Wo);
+                       ww, N, H, W, C, Ho, Wo, ldd);
   else
     hipLaunchKernelGGL(up_bwd_kernel<1>, dim3(blocks_for(n)), dim3(NT), 0, st, dy, dx, ih, wh, iw, ww,
-                       N, H, W, C, Ho, Wo);
+                       N, H, W, C, Ho, Wo, ldd);
 }
 
 }  // namespace tdl

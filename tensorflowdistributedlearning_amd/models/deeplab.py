@@ -21,13 +21,16 @@ so checkpoints use the reference layout.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from .layers import ConvBN, Conv2d, BNAct, MaxPool, DepthwiseConv2d, BatchNorm
 from ..ops.pool import max_pool2d, global_avg_pool
-from ..ops.upsample import upsample
+from ..ops.upsample import upsample, upsample_into
 from ..ops.elementwise import add_relu
+from ..ops import gradjoin
 
 
 class _Subsample(nn.Module):
@@ -76,8 +79,15 @@ class BetaUnit(nn.Module):
 
     def forward(self, x, end_points=None, name=None):
         preact = self.preact(x)
-        sc = self.subsample(x) if self.shortcut is None else self.shortcut(preact)
-        r = self.conv1(preact)
+        if self.shortcut is None:
+            sc, join = self.subsample(x), None
+        else:
+            # preact feeds the projection shortcut and conv1: both dgrads write one gradient
+            # buffer (the second accumulates in its epilogue and applies the preact BN's ReLU
+            # mask, ops/gradjoin.py) instead of autograd summing two tensors
+            join = gradjoin.make(2, preact) if self.training else None
+            sc = self.shortcut(preact, join=join)
+        r = self.conv1(preact, join=join)
         if self.conv2 is not None:
             r = self.conv2(r)
         r = self.conv3(r)
@@ -108,8 +118,8 @@ class SplitSeparableConv(nn.Module):
                                 init_std=0.06, bn_decay=bn_kw["decay"], bn_eps=bn_kw["eps"],
                                 bn_scale=bn_kw["scale"])
 
-    def forward(self, x):
-        return self.pointwise(self.depthwise(x))
+    def forward(self, x, into=None):
+        return self.pointwise(self.depthwise(x), into=into)
 
 
 class DeepLabResNet(nn.Module):
@@ -203,10 +213,21 @@ class DeepLabResNet(nn.Module):
             end_points[f"{root}/{bname}"] = _logical(net, mods[-1].out_channels)
         return end_points[f"{root}/block4"], end_points
 
+    # ASPP / decoder concatenations written in place: every branch's BN(+ReLU) apply (and the
+    # upsample of the pooled / ASPP features) stores straight into its channel slice of the
+    # consumer conv's input, and each backward reads its slice of the concat gradient in place
+    # (ops/bn.batch_norm_act_into, ops/upsample.upsample_into) — no torch.cat / split passes
+    concat_free = os.environ.get("TDL_CONCAT_FREE", "1") == "1"
+
     def forward(self, x, return_end_points=False):
         root = f"{self.model_name}/resnet_v2"
         _, end_points = self.forward_encoder(x)
         atrous = end_points[f"{root}/block4"].contiguous()  # a copy only for unaligned widths
+        last = 3 if self.block_type == "bottleneck" else 2
+        b1 = end_points[f"{root}/block1/unit_1/bottleneck_v2/conv{last}"].contiguous()
+        if self.concat_free and self._concat_free_ok(atrous):
+            out = self._head_concat_free(atrous, b1)
+            return (out, end_points) if return_end_points else out
         size = (atrous.shape[1], atrous.shape[2])
         a1 = self.assp_conv_1x1(atrous)
         a2 = self.assp_conv_3x3_1(atrous)
@@ -216,14 +237,40 @@ class DeepLabResNet(nn.Module):
         a5 = self.assp_pool_conv(a5)
         a5 = upsample(a5, size)
         assp = self.assp_out(torch.cat([a1, a2, a3, a4, a5], dim=-1))
-        last = 3 if self.block_type == "bottleneck" else 2
-        b1 = end_points[f"{root}/block1/unit_1/bottleneck_v2/conv{last}"].contiguous()
         assp_up = upsample(assp, (b1.shape[1], b1.shape[2]))
         dec = self.decoder_conv_1x1(b1)
         dec = torch.cat([dec, assp_up], dim=-1)
         dec = _logical(self.decoder_conv_3x3(dec), 1).contiguous()
         out = upsample(dec, self.input_shape)
         return (out, end_points) if return_end_points else out
+
+    def _concat_free_ok(self, atrous):
+        """Every writer's output is exactly its logical slice (no channel padding) and the
+        consumers read the concatenation unpadded."""
+        d = self.assp_out.bn.c
+        writers = (self.assp_conv_1x1, self.assp_conv_3x3_1.pointwise,
+                   self.assp_conv_3x3_2.pointwise, self.assp_conv_3x3_3.pointwise,
+                   self.assp_pool_conv, self.decoder_conv_1x1)
+        return (d % 8 == 0 and all(m.conv._cout_store == d for m in writers) and
+                self.assp_out.conv._cin_store == 5 * d and
+                self.decoder_conv_3x3._cin_store == 2 * d)
+
+    def _head_concat_free(self, atrous, b1):
+        d = self.assp_out.bn.c
+        N, h, w = atrous.shape[:3]
+        cat = atrous.new_empty((N, h, w, 5 * d))
+        cat = self.assp_conv_1x1(atrous, into=(cat, 0))
+        cat = self.assp_conv_3x3_1(atrous, into=(cat, d))
+        cat = self.assp_conv_3x3_2(atrous, into=(cat, 2 * d))
+        cat = self.assp_conv_3x3_3(atrous, into=(cat, 3 * d))
+        a5 = self.assp_pool_conv(global_avg_pool(atrous, keepdims=True))
+        cat = upsample_into(cat, 4 * d, a5)
+        assp = self.assp_out(cat)
+        dec = b1.new_empty((b1.shape[0], b1.shape[1], b1.shape[2], 2 * d))
+        dec = self.decoder_conv_1x1(b1, into=(dec, 0))
+        dec = upsample_into(dec, d, assp)
+        dec = _logical(self.decoder_conv_3x3(dec), 1).contiguous()
+        return upsample(dec, self.input_shape)
 
     # ------------------------------------------------------------------------------------------
     def tf_names(self):

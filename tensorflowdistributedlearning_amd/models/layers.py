@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import ConvGeom, conv2d, same_padding, symmetric_padding, row_pack
-from ..ops.bn import batch_norm_act
+from ..ops.bn import batch_norm_act, batch_norm_act_into
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
 from ..ops.common import compute_weight, flat_view
@@ -354,12 +354,19 @@ class ConvBN(nn.Module):
                             c_phys=self.conv._cout_store)
         self.relu = relu
 
-    def forward(self, x, residual=None, join=None, res_join=None):
-        """``join``: gradient join for x (ops/gradjoin.py); ``res_join``: for the residual."""
+    def forward(self, x, residual=None, join=None, res_join=None, into=None):
+        """``join``: gradient join for x (ops/gradjoin.py); ``res_join``: for the residual.
+        ``into`` = (buf, c0): write act(BN(conv(x))) into ``buf[..., c0:c0+C]`` (a concat
+        buffer, ops/bn.batch_norm_act_into) and return ``buf``."""
         if self.training:
             y, stats = self.conv(x, want_stats=True, join=join)
         else:
             y, stats = self.conv(x, join=join), None
+        if into is not None:
+            if residual is not None:
+                raise ValueError("ConvBN: no residual with into=")
+            return batch_norm_act_into(into[0], into[1], y, self.bn, stats, self.relu,
+                                       self.bn.training)
         return self.bn(y, stats=stats, residual=residual, relu=self.relu, res_join=res_join)
 
 

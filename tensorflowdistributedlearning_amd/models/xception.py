@@ -16,7 +16,6 @@ import torch
 import torch.nn as nn
 
 from .layers import ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear
-from ..ops.elementwise import add as add_op
 
 
 def _fixed_pad(k, rate):
@@ -41,10 +40,10 @@ class SeparableConvBN(nn.Module):
                                 init="trunc_normal", init_std=0.06, **bn_kw)
         self.act_inside = act_inside
 
-    def forward(self, x, relu_in=False):
+    def forward(self, x, relu_in=False, residual=None):
         y = self.depthwise(x, relu_in=relu_in)
         y = self.dw_bn(y, relu=self.act_inside)
-        return self.pointwise(y)
+        return self.pointwise(y, residual=residual)
 
 
 class XceptionModule(nn.Module):
@@ -70,11 +69,14 @@ class XceptionModule(nn.Module):
 
     def forward(self, x):
         r = self.convs[0](x, relu_in=not self.act_inside)
-        r = self.convs[2](self.convs[1](r))
+        r = self.convs[1](r)
+        if self.skip == "sum":
+            # identity skip: the add is folded into the last pointwise BN's apply (one pass,
+            # one bf16 rounding of BN(y) + x instead of two)
+            return self.convs[2](r, residual=x)
+        r = self.convs[2](r)
         if self.skip == "conv":
             return self.shortcut(x, residual=r)  # BN(shortcut) + residual, no act
-        if self.skip == "sum":
-            return add_op(r, x)
         return r
 
 

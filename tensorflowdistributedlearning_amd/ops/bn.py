@@ -71,13 +71,17 @@ def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps
     return torch.stack([scale, shift, mean, invstd])
 
 
-def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None):
-    """``fp8`` = (amax_ring fp32[3], phase, scale fp32[1], emit): also write an e4m3 copy of y
+def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None, out=None):
+    """``out``: write y there instead (e.g. a channel slice ``buf[..., c0:c0+C]`` of a wider
+    NHWC concat buffer — the kernel takes its pixel stride; no fp8 side output then).
+    ``fp8`` = (amax_ring fp32[3], phase, scale fp32[1], emit): also write an e4m3 copy of y
     scaled by the previous call's |y|max (delayed scaling) — returned as ``y._tdl_fp8`` =
     (y8, scale) for an fp8 consumer conv (ops/conv.py) when ``emit``.  ``mask`` (uint8
     [numel/8], GPU): also write the ReLU mask y > 0 as one bit per element (relu mode 3)."""
+    if out is not None and fp8 is not None:
+        raise ValueError("bn_apply: no fp8 side output into a strided destination")
     if on_gpu(x):
-        y = torch.empty_like(x)
+        y = torch.empty_like(x) if out is None else out
         if fp8 is None:
             ext().bn_apply(x, coef, residual, y, bool(relu), mask=mask)
             return y
@@ -94,6 +98,9 @@ def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None):
         y = y + residual.float()
     if relu:
         y = torch.relu(y)
+    if out is not None:
+        out.copy_(y)
+        return out
     return y.to(x.dtype)
 
 
@@ -294,11 +301,11 @@ class _BatchNormActFn(torch.autograd.Function):
         count = ctx.count if ctx.training else float("inf")  # frozen BN: dx = γ·invstd·g
         fp8 = ctx.bn.fp8_bwd_state(x) if getattr(ctx.bn, "emit_fp8_bwd", False) else None
         dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, count, relu,
-                                ctx.has_res and not premasked,
+                                ctx.has_res and not premasked and relu != 0,
                                 gt if direct_g else None, bt if direct_b else None, fp8=fp8,
                                 red_raw=red_raw)
-        if premasked and ctx.has_res:
-            dres = dy
+        if ctx.has_res and (premasked or relu == 0):
+            dres = dy  # no mask to apply: the residual gradient is the incoming one, no copy
         if red_raw and want_g and not direct_g:
             red = bn_red_xhat(red, coef)
         if want_g:
@@ -349,3 +356,68 @@ def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True, r
         x.requires_grad or (residual is not None and residual.requires_grad))
     return _BatchNormActFn.apply(x, stats, bn.gamma, bn.beta, residual, bn, relu, training,
                                  res_join, need_grad)
+
+
+# ----------------------------------------------------------------------------------------------
+# BN(+ReLU) written straight into a channel slice of a concat buffer (concat-free ASPP / decoder)
+# ----------------------------------------------------------------------------------------------
+
+class _BatchNormActIntoFn(torch.autograd.Function):
+    """``buf[..., c0:c0+C] = act(BN(x))`` in place, returning ``buf``: the DeepLab ASPP branches
+    and the decoder's low-level features land in the consumer conv's input without a
+    ``torch.cat`` pass (core/resnet.py:438-448,476-486 concatenate them).  The backward reads its
+    branch's gradient as a strided slice of the concat gradient — no split copy — and passes that
+    gradient on to the other writers.  The ReLU mask is recomputed from x (relu mode 2)."""
+
+    @staticmethod
+    def forward(ctx, buf, x, stats, gamma, beta, bn, c0, relu, training):
+        C = x.shape[-1]
+        count = x.numel() // C
+        if training and (stats is None or stats.numel() == 0):
+            stats = bn_stats(x)
+        gp, bp = _phys_params(bn, gamma, beta)
+        coef = bn_finalize(stats, count, gp, bp, bn.running_mean, bn.running_var,
+                           bn.decay, bn.eps, training)
+        bn_apply(x, coef, None, relu, out=buf[..., c0:c0 + C])
+        ctx.mark_dirty(buf)
+        ctx.count, ctx.bn, ctx.training, ctx.c0 = count, bn, training, c0
+        ctx.relu = 2 if relu else 0
+        ctx.save_for_backward(x, coef, gamma, beta)
+        return buf
+
+    @staticmethod
+    def backward(ctx, gbuf):
+        x, coef, gamma, beta = ctx.saved_tensors
+        if gbuf.stride(-1) != 1 or not gbuf.is_contiguous():
+            gbuf = gbuf.contiguous()
+        C = x.shape[-1]
+        dy = gbuf[..., ctx.c0:ctx.c0 + C]  # strided view: the kernels take the pixel stride
+        if not on_gpu(dy):
+            dy = dy.contiguous()
+        red = bn_bwd_reduce(dy, None, x, coef, ctx.relu)
+        want_g = gamma is not None and gamma.requires_grad
+        want_b = beta.requires_grad
+        gt, gfresh = _grad_target_phys(gamma, C) if want_g else (None, False)
+        bt, bfresh = _grad_target_phys(beta, C) if want_b else (None, False)
+        direct_g = on_gpu(dy) and gt is not None and gfresh
+        direct_b = on_gpu(dy) and bt is not None and bfresh
+        gp, _ = _phys_params(ctx.bn, gamma, beta)
+        count = ctx.count if ctx.training else float("inf")
+        dx, _ = bn_bwd_apply(dy, None, x, coef, red, gp, count, ctx.relu, False,
+                             gt if direct_g else None, bt if direct_b else None)
+        c = beta.numel()
+        if want_g:
+            deliver_grad(gamma, None if direct_g else red[1][:c], written=direct_g)
+        if want_b:
+            deliver_grad(beta, None if direct_b else red[0][:c], written=direct_b)
+        return gbuf, dx, None, None, None, None, None, None, None
+
+
+def batch_norm_act_into(buf, c0, x, bn, stats=None, relu=True, training=True):
+    """``buf[..., c0:c0+C] = act(BN(x))`` (in place; returns ``buf`` for the autograd chain).
+    ``x`` must not be channel-padded (its channels are the slice's channels)."""
+    C = x.shape[-1]
+    if C != bn.beta.numel() or buf.shape[:-1] != x.shape[:-1] or c0 + C > buf.shape[-1]:
+        raise ValueError(f"batch_norm_act_into: x {tuple(x.shape)} into buf {tuple(buf.shape)} "
+                         f"at channel {c0} (BN of {bn.beta.numel()} channels)")
+    return _BatchNormActIntoFn.apply(buf, x, stats, bn.gamma, bn.beta, bn, c0, relu, training)

@@ -117,3 +117,49 @@ class _UpsampleFn(torch.autograd.Function):
 def upsample(x, out_shape):
     """Reference ``_upsample(inputs, out_shape)``; ``out_shape`` = (H, W)."""
     return _UpsampleFn.apply(x, int(out_shape[0]), int(out_shape[1]))
+
+
+class _UpsampleIntoFn(torch.autograd.Function):
+    """``buf[..., c0:c0+C] = upsample(x)`` in place (the kernel takes the destination's pixel
+    stride), returning ``buf`` — the concat-free ASPP pooling branch and decoder input."""
+
+    @staticmethod
+    def forward(ctx, buf, x, c0):
+        N, H, W, C = x.shape
+        out_h, out_w = buf.shape[1], buf.shape[2]
+        ctx.x_shape, ctx.c0 = tuple(x.shape), c0
+        dst = buf[..., c0:c0 + C]
+        if on_gpu(x):
+            ih, wh = _tap_tensor(H, out_h, x.device)
+            iw, ww = _tap_tensor(W, out_w, x.device)
+            ext().upsample_fwd(x.contiguous(), dst, ih, wh, iw, ww)
+        else:
+            dst.copy_(torch.einsum("ia,jb,nabc->nijc", interp_matrix(H, out_h),
+                                   interp_matrix(W, out_w), x.float()).to(buf.dtype))
+        ctx.mark_dirty(buf)
+        ctx.out = (out_h, out_w)
+        return buf
+
+    @staticmethod
+    def backward(ctx, gbuf):
+        N, H, W, C = ctx.x_shape
+        out_h, out_w = ctx.out
+        if not gbuf.is_contiguous():
+            gbuf = gbuf.contiguous()
+        dy = gbuf[..., ctx.c0:ctx.c0 + C]
+        if on_gpu(dy):
+            ih, wh = _tap_tensor(H, out_h, dy.device)
+            iw, ww = _tap_tensor(W, out_w, dy.device)
+            dx = torch.empty(ctx.x_shape, device=dy.device, dtype=dy.dtype)
+            ext().upsample_bwd(dy, dx, ih, wh, iw, ww)
+        else:
+            dx = torch.einsum("ia,jb,nijc->nabc", interp_matrix(H, out_h),
+                              interp_matrix(W, out_w), dy.float()).to(dy.dtype)
+        return gbuf, dx, None
+
+
+def upsample_into(buf, c0, x):
+    """``buf[..., c0:c0+C] = upsample(x, buf.shape[1:3])`` in place; returns ``buf``."""
+    if buf.shape[0] != x.shape[0] or c0 + x.shape[-1] > buf.shape[-1]:
+        raise ValueError(f"upsample_into: x {tuple(x.shape)} into buf {tuple(buf.shape)} at {c0}")
+    return _UpsampleIntoFn.apply(buf, x, int(c0))

@@ -794,3 +794,46 @@ def test_bn_bwd_reduce2_matches_two_reduces(gpu):
     torch.testing.assert_close(red, B.bn_bwd_reduce(dy, None, x, c1, 0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(B.bn_red_xhat(red2, c2), B.bn_bwd_reduce(dy, None, x2, c2, 0),
                                rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("C,ld,c0", [(256, 1280, 512), (48, 304, 256), (728, 1456, 0)])
+def test_bn_and_upsample_channel_slice_io(gpu, C, ld, c0):
+    """The concat-free ASPP / decoder kernels: bn_apply writing into a channel slice of a wider
+    NHWC buffer, bn_bwd_reduce / bn_bwd_apply and upsample_bwd reading dy from one, and
+    upsample_fwd writing into one, are bitwise the contiguous kernels (other channels untouched)."""
+    torch.manual_seed(1)
+    N, H, W = 2, 13, 13
+    x = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    stats = B.bn_stats(x)
+    g = torch.rand(C, device=gpu) + 0.5
+    b = torch.randn(C, device=gpu) * 0.1
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    coef = B.bn_finalize(stats, N * H * W, g, b, rm, rv, 0.9, 1e-3, True)
+    y = B.bn_apply(x, coef, None, True)
+    buf = torch.full((N, H, W, ld), 7.0, device=gpu, dtype=torch.bfloat16)
+    B.bn_apply(x, coef, None, True, out=buf[..., c0:c0 + C])
+    torch.cuda.synchronize()
+    assert torch.equal(buf[..., c0:c0 + C], y)
+    rest = torch.cat([buf[..., :c0], buf[..., c0 + C:]], -1)
+    assert torch.all(rest == 7.0)
+    gbuf = torch.randn(N, H, W, ld, device=gpu).bfloat16()
+    dy = gbuf[..., c0:c0 + C]
+    for relu in (0, 2):
+        r1 = B.bn_bwd_reduce(dy.contiguous(), None, x, coef, relu)
+        r2 = B.bn_bwd_reduce(dy, None, x, coef, relu)
+        torch.testing.assert_close(r1, r2, rtol=1e-5, atol=1e-3)
+        d1, _ = B.bn_bwd_apply(dy.contiguous(), None, x, coef, r1, g, N * H * W, relu, False)
+        d2, _ = B.bn_bwd_apply(dy, None, x, coef, r1, g, N * H * W, relu, False)
+        assert torch.equal(d1, d2)
+    small = torch.randn(N, 5, 5, C, device=gpu).bfloat16()
+    up = U.upsample(small, (H, W))
+    buf2 = torch.zeros(N, H, W, ld, device=gpu, dtype=torch.bfloat16)
+    U.upsample_into(buf2, c0, small)
+    assert torch.equal(buf2[..., c0:c0 + C], up)
+    ih, wh = U._tap_tensor(5, H, gpu)
+    iw, ww = U._tap_tensor(5, W, gpu)
+    dx1 = torch.empty_like(small)
+    dx2 = torch.empty_like(small)
+    ext().upsample_bwd(dy.contiguous(), dx1, ih, wh, iw, ww)
+    ext().upsample_bwd(dy, dx2, ih, wh, iw, ww)
+    assert torch.equal(dx1, dx2)

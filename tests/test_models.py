@@ -159,3 +159,29 @@ def test_deeplab_channel_padding_is_exact(flat):
             end = o + (n + 63) // 64 * 64
             assert f.master[o + n:end].abs().max() == 0 if end > o + n else True
             assert f.grad[o + n:end].abs().max() == 0 if end > o + n else True
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_deeplab_concat_free_head_matches_cat(train):
+    """The ASPP / decoder concatenations written in place (each branch's BN+ReLU and the
+    upsamples store into their channel slice; backward reads slices of the concat gradient)
+    compute the same logits, parameter gradients and moving statistics as the torch.cat head."""
+    torch.manual_seed(3)
+    kw = dict(model_name="m", input_shape=(33, 33), n_blocks=(1, 1, 1), base_depth=16)
+    a = models.DeepLabResNet(**kw)
+    b = models.DeepLabResNet(**kw)
+    b.load_state_dict(a.state_dict())
+    a.concat_free, b.concat_free = False, True
+    x = torch.randn(2, 33, 33, 2)
+    res = []
+    for m in (a, b):
+        m.train(train)
+        out = m(x)
+        out.float().pow(2).mean().backward()
+        res.append((out, [p.grad.clone() for p in m.parameters()]))
+    assert b._concat_free_ok(torch.empty(1, 5, 5, 1024))
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-6)
+    for (name, _), ga, gb in zip(a.named_parameters(), res[0][1], res[1][1]):
+        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-6, msg=name)
+    for p, q in zip(a.buffers(), b.buffers()):
+        torch.testing.assert_close(p, q)

@@ -742,3 +742,30 @@ def test_fp8_delayed_scaling_rolls_on_device(gpu):
     assert abs(scales[0] - am[0] / E4M3_MAX) < 1e-6 * am[0]  # first call primes (exact)
     for t in (1, 2, 3):
         assert abs(scales[t] - am[t - 1] / E4M3_MAX) < 1e-6 * max(am), (t, scales, am)
+
+
+@pytest.mark.timeout(300)
+def test_deeplab_concat_free_head_gpu_matches_cat(gpu):
+    """The reference preset's ASPP / decoder written in place into the concat buffers (strided
+    BN apply / backward and upsample kernels) vs the torch.cat head on the GPU: same logits and
+    gradients (frozen BN; with batch statistics one training step's moving statistics)."""
+    torch.manual_seed(8)
+    kw = dict(model_name="m", input_shape=(101, 101))
+    a = models.DeepLabResNet(**kw)
+    b = models.DeepLabResNet(**kw)
+    b.load_state_dict(a.state_dict())
+    a.concat_free, b.concat_free = False, True
+    ta = Trainer(a, lovasz_hinge, gpu, "adam", dict(lr=0.0))
+    tb = Trainer(b, lovasz_hinge, gpu, "adam", dict(lr=0.0))
+    x, y = segmentation_batch(4, device=gpu)
+    ta.train_mode = tb.train_mode = False
+    la, oa = ta.train_step(x, y)
+    lb, ob = tb.train_step(x, y)
+    assert torch.equal(oa, ob)
+    gcos = torch.nn.functional.cosine_similarity(ta.flat.grad, tb.flat.grad, dim=0).item()
+    assert gcos > 0.9999, gcos
+    ta.train_mode = tb.train_mode = True
+    ta.train_step(x, y)
+    tb.train_step(x, y)
+    for (n, ra), rb in zip(a.named_buffers(), b.buffers()):
+        torch.testing.assert_close(ra, rb, rtol=1e-2, atol=1e-3, msg=n)
