@@ -589,8 +589,11 @@ DwArgs dw_args(const Tensor& x_like, const Tensor& w, int64_t Ho, int64_t Wo, in
   return a;
 }
 
-void dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t sh, int64_t sw,
-                int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu, bool relu_in) {
+// stats (optional fp32 [2, C], zeroed by the caller): BN sums of y fused into the kernel;
+// returns whether they were written (stride-1 3×3 tile kernel only)
+bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t sh, int64_t sw,
+                int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu, bool relu_in,
+                c10::optional<Tensor> stats) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -598,11 +601,18 @@ void dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_
   a.x = BF(x); a.w = BF(w); a.bias = optf(bias); a.out = BFW(y); a.relu = relu;
   TORCH_CHECK(!relu_in || (a.C % 8 == 0 && a.R * a.S == 9), "fused input ReLU: 3x3, C % 8 == 0");
   a.relu_in = relu_in;
-  dwconv_fwd_launch(a, stream());
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->numel() == 2 * a.C, "dwconv_fwd stats: fp32 [2, C]");
+    a.stats = optfw(stats);
+  }
+  return dwconv_fwd_launch(a, stream());
 }
 
-void dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-                  int64_t dh, int64_t dw, c10::optional<Tensor> mask_x) {
+// bn_x / bn_red (optional, together): also accumulate the BN-backward sums (Σg, Σg·bn_x) of the
+// stored dx (stride-1 3×3 tile kernel only; returns whether they were written)
+bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                  int64_t dh, int64_t dw, c10::optional<Tensor> mask_x,
+                  c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_red) {
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -613,7 +623,15 @@ void dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
     TORCH_CHECK(mask_x->sizes() == dx.sizes(), "mask_x must be shaped like dx");
     TORCH_CHECK(a.C % 8 == 0 && a.R * a.S == 9, "fused input ReLU: 3x3, C % 8 == 0");
   }
-  dwconv_dgrad_launch(a, stream());
+  if (bn_x.has_value() && bn_x->defined()) {
+    TORCH_CHECK(bn_red.has_value() && bn_red->defined(), "dwconv_dgrad: bn_x needs bn_red");
+    CHECK_T(*bn_x, torch::kBFloat16);
+    TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_red->numel() == 2 * a.C,
+                "dwconv_dgrad bn_x: shape of dx, bn_red fp32 [2, C]");
+    a.bn_x = BF(*bn_x);
+    a.stats = optfw(bn_red);
+  }
+  return dwconv_dgrad_launch(a, stream());
 }
 
 void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int64_t sh, int64_t sw,
@@ -905,8 +923,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lowp"),
         py::arg("flags"), py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
         py::arg("wd"), py::arg("gs"), py::arg("lr_scale") = py::none());
-  m.def("dwconv_fwd", &dwconv_fwd);
-  m.def("dwconv_dgrad", &dwconv_dgrad);
+  m.def("dwconv_fwd", &dwconv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"),
+        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
+        py::arg("relu"), py::arg("relu_in"), py::arg("stats") = py::none());
+  m.def("dwconv_dgrad", &dwconv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
+        py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
+        py::arg("mask_x") = py::none(), py::arg("bn_x") = py::none(),
+        py::arg("bn_red") = py::none());
   m.def("dwconv_wgrad", &dwconv_wgrad);
   m.def("upsample_fwd", &upsample_fwd);
   m.def("upsample_bwd", &upsample_bwd);

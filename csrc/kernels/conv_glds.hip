@@ -718,6 +718,7 @@ constexpr GCfg G128x128s2{128, 128, 2, 2, 2};  // 66 KB LDS: two workgroups per 
 constexpr GCfg G256x64w8{256, 64, 8, 1, 3};    // 64-wide N with 8 waves (32-row wave tiles)
 constexpr GCfg G128x64{128, 64, 4, 1, 4};      // 64-wide N, 4 stages, 96 KB LDS
 constexpr GCfg G128x128w8{128, 128, 4, 2, 4};  // 8 waves of 32×64 (half the accumulators)
+constexpr GCfg G64x256{64, 256, 1, 4, 3};      // WGRAD, ≤ 64 output channels, 129–256 columns
 
 constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
   return stages * (bm + bn) * BK * 2 + 2 * wm * bn * 4;
@@ -750,7 +751,9 @@ void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
     launch_g<MODE, 256, 64, 8, 1, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else if (cfg == 6 && MODE == DGRAD && STATS)  // fused-statistics dgrads only
     launch_g<MODE, 128, 128, 4, 2, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
-  else
+  else if (cfg == 7) {  // weight gradients of few-output-channel convs only (the ResNet stem)
+    if constexpr (MODE == WGRAD) launch_g<MODE, 64, 256, 1, 4, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
+  } else
     launch_g<MODE, 128, 64, 4, 1, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
 }
 
@@ -762,6 +765,7 @@ const GCfg& cfg_of(int c) {
     case 3: return G128x128s2;
     case 4: return G256x64w8;
     case 6: return G128x128w8;
+    case 7: return G64x256;
     default: return G128x64;
   }
 }
@@ -909,7 +913,9 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   // (strided dgrads: every parity class in the same order, each class's tiles padded to whole
   // workgroups so none straddles two classes; a class without taps was zero-filled and adds 0;
   // joins need stride 1 — an accumulate leaves the pixels of such a class unmasked)
-  const bool bn_stats = a.stats && a.bn_x && !a.fp8 && a.K % 64 == 0 &&
+  // K % 64 != 0 (Xception's 728-channel pointwise convs): the ragged FASTK form for 1×1 filters
+  const bool rag_stats = a.K % 64 != 0 && a.R * a.S == 1 && a.ncls == 1 && a.K % 8 == 0;
+  const bool bn_stats = a.stats && a.bn_x && !a.fp8 && (a.K % 64 == 0 || rag_stats) &&
                         (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1));
   if (bn_stats) {
     // tile config (tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
@@ -933,10 +939,16 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
     }
     const int blocks = a.cls_tile0[a.ncls] / a.tpb;
     a.splits = 1;
-    if (a.beta)
+    if (rag_stats) {
+      if (a.beta)
+        launch_gcfg<DGRAD, true, false, 2>(a, scfg, blocks, st);
+      else
+        launch_gcfg<DGRAD, true, false, 2, true>(a, scfg, blocks, st);
+    } else if (a.beta) {
       launch_gcfg<DGRAD, true, false, 1>(a, scfg, blocks, st);
-    else
+    } else {
       launch_gcfg<DGRAD, true, false, 1, true>(a, scfg, blocks, st);
+    }
     if (fused) *fused = true;
     return true;
   }
@@ -966,9 +978,16 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
 bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
   const int mode = conv_glds_mode();
   if (mode == 0 || a.C % 8 || a.K % 8) return false;
+  // the ResNet stem (64 output channels × 168 row-packed columns, K = every output pixel): one
+  // 64×256 tile column reads dy once, where the register-staged kernel's 64×128 tiles read it twice
+  // — measured slower on the row-packed stem at b1024 (1120 vs 1040 us, tools/stem_ab.py: the x
+  // gather, not the dy re-read, bounds it), so opt-in (TDL_GLDS_STEM_WGRAD=1)
+  const char* stem_env = getenv("TDL_GLDS_STEM_WGRAD");
+  const bool stem = (stem_env ? atoi(stem_env) : 0) != 0 && a.M <= 64 && a.Ng > 128 &&
+                    a.Ng <= 256 && (long)a.Kg >= 65536;
   // default: 1×1 filters with ≥ 256 output channels (3×3 gathers of x favour the other kernel)
-  if (mode == 1 && ((long)a.Kg < 4096 || a.M < 256 || a.R * a.S != 1)) return false;
-  int cfg = a.M <= 128 ? 2 : 0;
+  if (mode == 1 && !stem && ((long)a.Kg < 4096 || a.M < 256 || a.R * a.S != 1)) return false;
+  int cfg = stem ? 7 : a.M <= 128 ? 2 : 0;
   cfg = env_int("TDL_GLDS_CFG_WGRAD", cfg);
   const GCfg& g = cfg_of(cfg);
   const long tiles = (long)cdiv(a.M, g.bm) * cdiv(a.Ng, g.bn);

@@ -563,7 +563,13 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
                                                      int Ho, int Wo, int C, int Ph, int Pw,
                                                      int relu, int tr, int tw, int rg, int tiles_h,
                                                      int tiles_w, int relu_in,
-                                                     const bf16_t* __restrict__ mask_x) {
+                                                     const bf16_t* __restrict__ mask_x,
+                                                     float* __restrict__ stats,
+                                                     const bf16_t* __restrict__ bn_x) {
+  // stats (optional, fp32 [2][C], accumulated): BN sums of the stored bf16 outputs — (Σy, Σy²)
+  // for the BN that normalises this forward's output, or (Σg, Σg·bn_x) with bn_x the input of
+  // the BN whose output gradient this dgrad produces (bn.hip red_raw) — so that BN skips its
+  // separate reduce pass
   // tile: tr × tw output pixels (runtime, ≤ DT_TR × DT_TW, balanced splits of Ho / Wo); lanes:
   // 8 channel lanes × tw column lanes × rg row groups (each slides over ⌈tr / rg⌉ rows)
   __shared__ uint4 tile[DT_CHUNKS];
@@ -592,7 +598,11 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
   const int w = w0 + pw, c = cg0 + cl * 8;
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
   const int r1 = min(min(tr, r0 + rpg), Ho - h0);
-  if (g >= rg || w >= Wo || c >= C || r0 >= r1) return;
+  const bool active = !(g >= rg || w >= Wo || c >= C || r0 >= r1);
+  float ss[8], sq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss[j] = sq[j] = 0.f;
+  if (active) {
   f32x2 wv[9][4], bb[4];
 #pragma unroll
   for (int k = 0; k < 9; ++k) unpack8x2(*(const uint4*)(wt + (long)(FLIP ? 8 - k : k) * C + c), wv[k]);
@@ -634,7 +644,47 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
     }
     const long op = (((long)n * Ho + h0 + h) * Wo + w) * C + c;
     if (mask_x) mask_pos(o, mask_x + op);
-    *(uint4*)(out + op) = pack8(o);
+    const uint4 packed = pack8(o);
+    *(uint4*)(out + op) = packed;
+    if (stats) {
+      float q[8];
+      unpack8(packed, q);  // the stored bf16 values
+      if (bn_x) {
+        float xv[8];
+        unpack8(*(const uint4*)(bn_x + op), xv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ss[j] += q[j];
+          sq[j] = fmaf(q[j], xv[j], sq[j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ss[j] += q[j];
+          sq[j] = fmaf(q[j], q[j], sq[j]);
+        }
+      }
+    }
+  }
+  }
+  if (stats) {
+    // workgroup reduction over the lanes of each of the 64 channels (the LDS tile is free now),
+    // then one atomic pair per channel
+    __syncthreads();
+    float* red = (float*)tile;
+    const int L = blockDim.x >> 3;  // lanes per channel lane (≤ 32)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(cl * 8 + j) * L + rest] = ss[j];
+      red[(64 + cl * 8 + j) * L + rest] = sq[j];
+    }
+    __syncthreads();
+    if (t < 128) {
+      const int which = t >> 6, ch = t & 63;
+      float v = 0.f;
+      for (int i = 0; i < L; ++i) v += red[(which * 64 + ch) * L + i];
+      if (cg0 + ch < C) atomicAdd(stats + which * C + cg0 + ch, v);
+    }
   }
 }
 
@@ -833,14 +883,15 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 }  // namespace
 
-void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
+bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
   if (slide_ok(a) && dw_tile()) {
     const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
     dim3 grid((unsigned)(a.N * g.th * g.twn), (unsigned)cdiv(a.C, DT_CH));
     hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
-                       g.twn, a.relu_in, (const bf16_t*)nullptr);
+                       g.twn, a.relu_in, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr);
+    return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {
     const Slide4Geom g = slide4_geom(a.C / 4, a.Wo);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
@@ -862,16 +913,18 @@ void dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   } else {
     hipLaunchKernelGGL(dw_fwd_kernel<1>, dim3(blocks_for(outs)), dim3(NT), 0, st, a);
   }
+  return false;
 }
 
-void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
+bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
   if (slide_ok(a) && dw_tile()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const DwTileGeom g = dw_tile_geom(a.H, a.W);
     dim3 grid((unsigned)(a.N * g.th * g.twn), (unsigned)cdiv(a.C, DT_CH));
     hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
-                       g.twn, 0, a.mask_x);
+                       g.twn, 0, a.mask_x, a.stats, a.bn_x);
+    return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const Slide4Geom g = slide4_geom(a.C / 4, a.W);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
@@ -893,6 +946,7 @@ void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   } else {
     hipLaunchKernelGGL(dw_dgrad_kernel<1>, dim3(blocks_for(ins)), dim3(NT), 0, st, a);
   }
+  return false;
 }
 
 // slab rows for the row-oriented wgrad (0: generic atomic kernel)

@@ -214,10 +214,14 @@ struct DwArgs {
   // fused pre-activation ReLU of the input (Xception's relu → separable conv): fwd / wgrad read
   // max(x, 0); dgrad zeroes dx where mask_x ≤ 0 (mask_x = the un-rectified x).  3×3, C % 8 == 0.
   int relu_in = 0;
+  // optional fused BN sums (fp32 [2][C], accumulated; stride-1 3×3 tile kernels only — the
+  // launchers return whether they were written): fwd (Σy, Σy²); dgrad (Σg, Σg·bn_x)
+  float* stats = nullptr;
+  const bf16_t* bn_x = nullptr;
   const bf16_t* mask_x = nullptr;
 };
-void dwconv_fwd_launch(const DwArgs& a, hipStream_t st);
-void dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);
+bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st);  // true: a.stats written
+bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);  // true: a.stats written
 int dwconv_wgrad_slabs(const DwArgs& a);  // row-slab count of the fast wgrad (0: generic)
 // adds dW / db into a.dw / a.db; ws: slabs·(R·S + 1)·C floats when dwconv_wgrad_slabs(a) > 0
 void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st);

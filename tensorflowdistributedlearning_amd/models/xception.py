@@ -41,8 +41,13 @@ class SeparableConvBN(nn.Module):
         self.act_inside = act_inside
 
     def forward(self, x, relu_in=False, residual=None):
-        y = self.depthwise(x, relu_in=relu_in)
-        y = self.dw_bn(y, relu=self.act_inside)
+        # training: the depthwise kernel accumulates the BN statistics of its output in its
+        # epilogue (no separate reduce pass over y)
+        if self.training:
+            y, stats = self.depthwise(x, relu_in=relu_in, want_stats=True)
+        else:
+            y, stats = self.depthwise(x, relu_in=relu_in), None
+        y = self.dw_bn(y, stats=stats, relu=self.act_inside)
         return self.pointwise(y, residual=residual)
 
 

@@ -233,12 +233,17 @@ class _BatchNormActFn(torch.autograd.Function):
         elif (not relu and residual is None and need_grad and on_gpu(x) and PAIR_STATS
               and gradjoin.STATS_ENABLED):
             # no ReLU: a statistics-only token — the residual BN this output feeds (a shortcut
-            # BN) computes both BNs' backward sums in one pass over the shared gradient
+            # BN) computes both BNs' backward sums in one pass over the shared gradient, or the
+            # consuming conv's dgrad fuses them
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(None, x)
+        elif relu and residual is None and need_grad and on_gpu(x) and C % 8 == 0 \
+                and gradjoin.STATS_ENABLED:
+            # ReLU without a bit mask: a consuming depthwise dgrad masks by y > 0 itself
+            ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(None, x, relu_y=True)
         ctx.res_tok = None
         if residual is not None:
             rt = getattr(residual, "_tdl_mask_token", None)
-            if rt is not None and rt.mask is None and rt.x is not None:
+            if rt is not None and rt.mask is None and not rt.relu_y and rt.x is not None:
                 ctx.res_tok = rt
         ctx.count = count
         ctx.bn = bn

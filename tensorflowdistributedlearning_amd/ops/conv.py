@@ -391,10 +391,14 @@ class _Conv2dFn(torch.autograd.Function):
             stats_ok = masks_ok and not fp8_dg  # (the kernel decides; strided: parity classes)
             if join is None:
                 tok = ctx.bn_tok
-                if tok is not None and masks_ok:
+                # a statistics-only token (BN without ReLU) needs no 64-channel mask slabs
+                if tok is not None and tok.relu_y:
+                    tok = None  # a ReLU without bit mask: only the depthwise dgrad applies it
+                if tok is not None and (masks_ok or (on_gpu(dy) and tok.mask is None)):
                     # sole consumer of a masked BN output: apply the mask here, and fuse the BN's
                     # backward statistics when the kernel can (ops/gradjoin.py)
-                    if stats_ok and tok.x is not None and gradjoin.STATS_SINGLE:
+                    if (stats_ok or tok.mask is None) and not fp8_dg and tok.x is not None \
+                            and gradjoin.STATS_SINGLE:
                         dx, red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, tok.x,
                                                     mask=tok.mask)
                     else:

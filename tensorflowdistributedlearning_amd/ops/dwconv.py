@@ -14,6 +14,8 @@ import torch
 import torch.nn.functional as F
 
 from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+from .bn import bn_stats
+from . import gradjoin
 from . import workspace
 from .conv import ConvGeom
 
@@ -35,30 +37,45 @@ def _fusable_relu_in(x, R, S):
 
 class _DwConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, relu, relu_in):
+    def forward(ctx, x, weight, bias, geom, relu, relu_in, want_stats):
         w = compute_weight(weight, x.dtype)
         N, H, W, C = x.shape
         R, S, _ = w.shape
         Ho, Wo = geom.out_hw(H, W, R, S)
+        stats = workspace.zeros((2, C), x.device) if want_stats else None
         if on_gpu(x):
             y = torch.empty((N, Ho, Wo, C), device=x.device, dtype=x.dtype)
-            ext().dwconv_fwd(x, w, None if bias is None else bias.detach(), y, geom.stride[0],
-                             geom.stride[1], geom.padding[0], geom.padding[2], geom.dilation[0],
-                             geom.dilation[1], bool(relu), bool(relu_in))
+            fused = ext().dwconv_fwd(x, w, None if bias is None else bias.detach(), y,
+                                     geom.stride[0], geom.stride[1], geom.padding[0],
+                                     geom.padding[2], geom.dilation[0], geom.dilation[1],
+                                     bool(relu), bool(relu_in), stats)
+            if want_stats and not fused:  # strided / dilated row kernels: a reduce pass
+                bn_stats(y, stats)
         else:
             y = ref_dw_fwd(torch.relu(x) if relu_in else x, w, geom,
                            None if bias is None else bias.detach())
             if relu:
                 y = torch.relu(y)
             y = y.to(x.dtype)
+            if want_stats:
+                bn_stats(y, stats)
         ctx.geom, ctx.relu, ctx.relu_in = geom, relu, relu_in
+        # the mask token of the BN that produced x (ops/gradjoin.py): this dgrad may mask by
+        # x > 0 and fuse that BN's backward statistics
+        ctx.bn_tok = getattr(x, "_tdl_mask_token", None)
         ctx.save_for_backward(x, weight, bias, y if relu else None)
-        return y
+        if stats is None:
+            stats = torch.empty(0, device=x.device)
+        ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
+        return y, stats
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dstats):
         x, weight, bias, y = ctx.saved_tensors
         geom = ctx.geom
+        if dy is None:
+            return (None,) * 7
         dy = dy.contiguous()
         if on_gpu(dy):
             if ctx.relu:
@@ -70,9 +87,21 @@ class _DwConvFn(torch.autograd.Function):
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.empty_like(x)
-                ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
-                                   geom.padding[2], geom.dilation[0], geom.dilation[1],
-                                   x if ctx.relu_in else None)
+                R, S = weight.shape[0], weight.shape[1]
+                tok, ctx.bn_tok = ctx.bn_tok, None
+                # x is a BN output: its ReLU mask is x > 0 (the stored y), so this dgrad can apply
+                # it through the relu_in mask path, and the tile kernel can accumulate that BN's
+                # backward sums (Σg, Σg·x_bn) in its epilogue (ops/gradjoin.py)
+                use_tok = (tok is not None and tok.x is not None and gradjoin.STATS_SINGLE
+                           and _fusable_relu_in(x, R, S))
+                masked = ctx.relu_in or (use_tok and (tok.relu_y or tok.mask is not None))
+                red = workspace.zeros((2, x.shape[-1]), dy.device) if use_tok else None
+                fused = ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1],
+                                           geom.padding[0], geom.padding[2], geom.dilation[0],
+                                           geom.dilation[1], x if masked else None,
+                                           tok.x if use_tok else None, red)
+                if use_tok:
+                    tok.mark(dx, red if fused else None)
             # accumulated by the kernels: pre-zeroed slices of the per-step arena (one fill per
             # step instead of one per layer); deliver_grad copies them out
             dw = workspace.zeros(tuple(weight.shape), dy.device)
@@ -97,17 +126,20 @@ class _DwConvFn(torch.autograd.Function):
             deliver_grad(weight, dw)
         if bias is not None and bias.requires_grad:
             deliver_grad(bias, db)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
 def depthwise_conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False,
-                     relu_in=False):
+                     relu_in=False, want_stats=False):
     """``relu_in``: convolve max(x, 0) without materialising it (Xception's pre-activation ReLU
-    in front of each separable conv, core/xception.py:90-110); the backward masks dx by x > 0."""
+    in front of each separable conv, core/xception.py:90-110); the backward masks dx by x > 0.
+    ``want_stats``: also return fp32 [2, C] = (Σy, Σy²) of the stored output for the BN that
+    normalises it (fused into the stride-1 tile kernel's epilogue) — returns ``(y, stats)``."""
     if relu_in and on_gpu(x) and not _fusable_relu_in(x, weight.shape[0], weight.shape[1]):
         from .elementwise import relu as relu_op
         x, relu_in = relu_op(x), False
-    return _DwConvFn.apply(x, weight, bias, geom, relu, relu_in)
+    y, stats = _DwConvFn.apply(x, weight, bias, geom, relu, relu_in, bool(want_stats))
+    return (y, stats) if want_stats else y
 
 
 def laplace(x):

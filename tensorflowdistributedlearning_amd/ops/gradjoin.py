@@ -53,13 +53,18 @@ class MaskToken:
     """The ReLU bit mask of a BN output, the BN's input ``x`` (for fused statistics), and (after
     backward) which gradient buffer the consumers handed back already masked:
     ``(data_ptr, version)`` of that tensor, plus its (Σg, Σg·x) when the last writer fused them."""
-    __slots__ = ("mask", "premasked", "x", "red")
+    __slots__ = ("mask", "premasked", "x", "red", "relu_y")
 
-    def __init__(self, mask, x=None):
+    def __init__(self, mask, x=None, relu_y=False):
         self.mask = mask
         self.premasked = None
         self.x = x if STATS_ENABLED else None
         self.red = None
+        # relu_y: the BN output is ReLU'd but no bit mask was written (channel counts that do
+        # not fill the 64-channel mask slabs): a consumer may apply the mask as "its input > 0"
+        # (the depthwise dgrad's relu_in path); the conv dgrads, which only take bit masks,
+        # leave such tokens alone
+        self.relu_y = relu_y
 
     def is_premasked(self, g):
         return self.premasked is not None and self.premasked == (g.data_ptr(), g._version)

@@ -837,3 +837,61 @@ def test_bn_and_upsample_channel_slice_io(gpu, C, ld, c0):
     ext().upsample_bwd(dy.contiguous(), dx1, ih, wh, iw, ww)
     ext().upsample_bwd(dy, dx2, ih, wh, iw, ww)
     assert torch.equal(dx1, dx2)
+
+
+@pytest.mark.parametrize("shape", [(8, 19, 19, 728, 728), (4, 19, 19, 1024, 728),
+                                   (4, 10, 10, 728, 1024)])
+def test_conv_dgrad_bnstat_ragged_k(gpu, shape):
+    """Fused BN-backward statistics on the ragged-K (K % 64 != 0) 1×1 LDS-DMA dgrad — Xception's
+    728-channel pointwise convs with a statistics-only token (no ReLU mask): dx bit-identical to
+    the plain dgrad, (Σg, Σg·x) vs an fp32 reduction."""
+    N, H, W, Cin, K = shape
+    g = C.ConvGeom((1, 1), (0, 0, 0, 0), (1, 1))
+    torch.manual_seed(23)
+    w = (torch.randn(K, 1, 1, Cin) / math.sqrt(Cin)).bfloat16().to(gpu)
+    dy = torch.randn(N, H, W, K).bfloat16().to(gpu)
+    x = (torch.randn(N, H, W, Cin) * 1.3 + 0.4).bfloat16().to(gpu)
+    ext().conv_set_glds_mode(2)
+    try:
+        ref = C.conv_dgrad(dy, w, x.shape, g)
+        dx, red = C.conv_dgrad_bnstat(dy, w, x.shape, g, x)
+    finally:
+        ext().conv_set_glds_mode(-1)
+    assert torch.equal(dx, ref)
+    assert red is not None
+    gf, xf = dx.float().reshape(-1, Cin), x.float().reshape(-1, Cin)
+    want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
+    assert rel_err(red, want) < 1e-4
+
+
+@pytest.mark.parametrize("Cn,stride", [(728, 1), (128, 1), (64, 2), (200, 1)])
+def test_depthwise_fused_bn_stats(gpu, Cn, stride):
+    """The depthwise kernels' fused BN sums: forward (Σy, Σy²) of the stored output (tile kernel;
+    the strided row kernels fall back to a reduce pass inside the op), and the dgrad's
+    (Σg, Σg·x_bn) of the stored, x>0-masked dx — vs fp32 reductions; dx bit-identical to the
+    unfused dgrad."""
+    torch.manual_seed(24)
+    from tensorflowdistributedlearning_amd.models.layers import resolve_padding
+    H = 19
+    pad = resolve_padding("SAME", H, H, 3, 3, (stride, stride), (1, 1))
+    g = C.ConvGeom((stride, stride), pad, (1, 1))
+    x = torch.randn(4, H, H, Cn, device=gpu).bfloat16()
+    w = (torch.randn(3, 3, Cn, device=gpu) * 0.3).bfloat16()
+    wp = torch.nn.Parameter(w.float())
+    wp._lowp = w
+    y, st = D.depthwise_conv2d(x, wp, None, g, False, want_stats=True)
+    yf = y.float().reshape(-1, Cn)
+    assert rel_err(st, torch.stack([yf.sum(0), (yf * yf).sum(0)])) < 1e-4
+    Ho = y.shape[1]
+    dy = torch.randn(4, Ho, Ho, Cn, device=gpu).bfloat16()
+    bn_x = (torch.randn(4, H, H, Cn, device=gpu) + 0.3).bfloat16()
+    dx0 = torch.empty_like(x)
+    ext().dwconv_dgrad(dy, w, dx0, stride, stride, pad[0], pad[2], 1, 1, x)
+    dx1 = torch.empty_like(x)
+    red = torch.zeros(2, Cn, device=gpu)
+    fused = ext().dwconv_dgrad(dy, w, dx1, stride, stride, pad[0], pad[2], 1, 1, x, bn_x, red)
+    assert torch.equal(dx0, dx1)
+    assert fused == (stride == 1 and Cn % 8 == 0)
+    if fused:
+        gf, xf = dx1.float().reshape(-1, Cn), bn_x.float().reshape(-1, Cn)
+        assert rel_err(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-4

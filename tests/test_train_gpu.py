@@ -769,3 +769,73 @@ def test_deeplab_concat_free_head_gpu_matches_cat(gpu):
     tb.train_step(x, y)
     for (n, ra), rb in zip(a.named_buffers(), b.buffers()):
         torch.testing.assert_close(ra, rb, rtol=1e-2, atol=1e-3, msg=n)
+
+
+@pytest.mark.timeout(400)
+def test_deeplab_bf16_training_curve_tracks_fp32_oracle(gpu):
+    """Precision parity of the reference preset (the reference trains it in fp32, the GPU path is
+    bf16): 40 Adam steps with batch statistics on one fixed batch from identical weights, native
+    bf16 GPU vs the CPU fp32 oracle — the loss curves must track (same step-0 loss, bounded gap,
+    both fit the batch)."""
+    torch.manual_seed(11)
+    mc = models.DeepLabResNet(model_name="m", input_shape=(101, 101))
+    mg = models.DeepLabResNet(model_name="m", input_shape=(101, 101))
+    mg.load_state_dict(mc.state_dict())
+    opt = dict(lr=5e-4)
+    tc = Trainer(mc, lovasz_hinge, "cpu", "adam", opt, lowp_dtype=None)
+    with torch.no_grad():
+        tc.flat.master.copy_(tc.flat.master.bfloat16().float())
+        tc.flat.sync_lowp()
+    tg = Trainer(mg, lovasz_hinge, gpu, "adam", opt)
+    with torch.no_grad():
+        tg.flat.master.copy_(tc.flat.master.to(gpu))
+        tg.flat.sync_lowp()
+    x, y = segmentation_batch(8, dtype=torch.float32, seed=3)
+    x = x.bfloat16().float()
+    xg, yg = x.to(gpu, torch.bfloat16), y.to(gpu)
+    fc, fg = [], []
+    for _ in range(40):
+        fc.append(float(tc.train_step(x, y)[0]))
+        fg.append(float(tg.train_step(xg, yg)[0]))
+    tail = lambda v: sum(v[-8:]) / 8
+    print("fp32 cpu", [round(v, 3) for v in fc[::4]], round(tail(fc), 4))
+    print("bf16 gpu", [round(v, 3) for v in fg[::4]], round(tail(fg), 4))
+    assert abs(fc[0] - fg[0]) < 0.03 * fc[0]
+    assert tail(fc) < 0.8 * fc[0] and tail(fg) < 0.8 * fg[0]
+    assert abs(tail(fg) - tail(fc)) < 0.25 * fc[0], (tail(fg), tail(fc))
+
+
+@pytest.mark.timeout(300)
+def test_xception_fused_bn_statistics_match_reduce_passes(gpu, monkeypatch):
+    """Xception-41 training step (batch statistics) with the separable path's BN sums fused into
+    the depthwise forward / dgrad and the ragged pointwise dgrad epilogues vs the same step with
+    every BN running its own reduce passes: same loss, gradients and moving statistics."""
+    from tensorflowdistributedlearning_amd.ops import gradjoin
+    torch.manual_seed(9)
+    x, y = imagenet_batch(8, 64, num_classes=10, device=gpu)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(gradjoin, "STATS_ENABLED", fused)
+        torch.manual_seed(9)
+        m = models.xception_41(num_classes=10)
+        if not fused:  # no depthwise forward statistics either
+            for mod in m.modules():
+                if type(mod).__name__ == "SeparableConvBN":
+                    mod.forward = _unfused_sep_forward(mod)
+        tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.0))
+        loss = float(tr.train_step(x, y)[0])
+        torch.cuda.synchronize()
+        res.append((loss, tr.flat.grad.clone(), [b.clone() for b in m.buffers()]))
+    assert abs(res[0][0] - res[1][0]) < 1e-3 * max(1.0, abs(res[1][0]))
+    cos = torch.nn.functional.cosine_similarity(res[0][1], res[1][1], dim=0).item()
+    assert cos > 0.999, cos
+    for a, b in zip(res[0][2], res[1][2]):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3)
+
+
+def _unfused_sep_forward(mod):
+    def fwd(x, relu_in=False, residual=None):
+        yy = mod.depthwise(x, relu_in=relu_in)
+        yy = mod.dw_bn(yy, relu=mod.act_inside)
+        return mod.pointwise(yy, residual=residual)
+    return fwd

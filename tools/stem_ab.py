@@ -48,6 +48,17 @@ def main():
                   f"({flop / tw / 1e6:4.0f} TF)  err {err:.2e}", flush=True)
             os.environ.pop("TDL_GLDS_CFG_FWD", None)
     ext().conv_set_glds_mode(-1)
+    # weight gradient: register-staged 64x128 tiles (dy read twice) vs the LDS-DMA 64x256 tile
+    for v in ("0", "1", "0", "1"):
+        os.environ["TDL_GLDS_STEM_WGRAD"] = v
+        dw = C.conv_wgrad(dy, t, tuple(w.shape), g)
+        tw = timeit(lambda: C.conv_wgrad(dy, t, tuple(w.shape), g))
+        if v == "0":
+            dw0 = dw.float()
+        err = ((dw.float() - dw0).abs().max() / dw0.abs().max()).item()
+        print(f"stem wgrad TDL_GLDS_STEM_WGRAD={v}: {tw:7.1f} us ({flop / tw / 1e6:4.0f} TF) "
+              f"err vs register-staged {err:.2e}", flush=True)
+    os.environ.pop("TDL_GLDS_STEM_WGRAD", None)
 
 
 if __name__ == "__main__":
