@@ -74,8 +74,12 @@ ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_
 }
 
 // ------------------------------------------------------------------------------------------ conv
-void conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::optional<Tensor> stats,
-              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu) {
+// res (optional, shaped like y): y = act(conv + bias + res) in the LDS-DMA epilogue; returns
+// false — nothing launched — when that kernel does not take the problem (the caller then adds
+// the residual itself)
+bool conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::optional<Tensor> stats,
+              int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu,
+              c10::optional<Tensor> res) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -90,8 +94,16 @@ void conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::opt
   a.stats = optfw(stats);
   if (a.stats) TORCH_CHECK(stats->numel() == 2 * a.K, "stats must be [2, K]");
   a.M = a.N * a.Ho * a.Wo; a.Ng = a.K; a.Kg = a.R * a.S * a.C; a.ldc = a.K; a.relu = relu;
-  if (a.M == 0) return;
+  if (res.has_value() && res->defined()) {
+    CHECK_T(*res, torch::kBFloat16);
+    TORCH_CHECK(res->sizes() == y.sizes(), "conv_fwd res: shaped like y");
+    a.res = BF(*res);
+    if (a.M == 0) return true;
+    return conv_fwd_res_launch(a, stream());
+  }
+  if (a.M == 0) return true;
   conv_fwd_launch(a, stream());
+  return true;
 }
 
 // fp8 (e4m3) forward conv: x8 [N,H,W,C] and w8 [K,R,S,C] as 1-byte tensors, sx / sw fp32 [1]
@@ -850,7 +862,9 @@ std::vector<double> transform_matrix(bool hflip, bool vflip, double angle, doubl
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "tensorflowdistributedlearning_amd native gfx950 kernels";
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"),
+        py::arg("stats"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("res") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
         py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none(),

@@ -238,8 +238,11 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 // SCALE: multiply by `scale` first (fp8 GEMMs: the per-tensor operand scales); `no_mem`: issue no
 // loads / stores (timing ablation).
 // NJ: compile-time "no residual join" (its previous-dx registers are not allocated)
+// FRES (FWD): add the residual a.res (laid out like the output) before the ReLU — the
+// DeepLab unit's relu(conv3 + bias + shortcut) in one pass (the statistics then are those of
+// the next unit's pre-activation BN input)
 template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false,
-          bool NJ = false>
+          bool NJ = false, bool FRES = false>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
@@ -279,6 +282,8 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
   if constexpr (MODE == DGRAD) {
     join_prev = !NJ && a.beta && !no_mem;
     join_mask = a.mask && !no_mem;
+  } else if constexpr (MODE == FWD && FRES) {
+    join_prev = !no_mem;
   }
   uint32_t mrow[RM][2];
   v2u32 pv[RM][RN];
@@ -314,14 +319,18 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
         }
       }
     }
+  }
+  if constexpr ((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) {
     if (join_prev) {
+      // DGRAD: the previous dx of the output buffer itself; FWD: the residual tensor
+      const rsrc_t rprev = MODE == FWD ? make_rsrc(a.res, a.out_bytes) : rout;
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm)
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
           const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
           pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
-              rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+              rprev, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
         }
     }
   }
@@ -338,13 +347,15 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
 #pragma unroll
         for (int i = 0; i < 4; ++i) t[i] += __uint_as_float(bias_v[rn][i]);
       }
-      if constexpr (MODE == DGRAD) {
+      if constexpr ((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) {
         if (join_prev) {
           t[0] += __uint_as_float(pv[rm][rn][0] << 16);
           t[1] += __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
           t[2] += __uint_as_float(pv[rm][rn][1] << 16);
           t[3] += __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
         }
+      }
+      if constexpr (MODE == DGRAD) {
         if (join_mask) {
           // bit (rn·16 + group·4 + i) of the wave's TN-column slab; v_bfe_i32 → 0 / ~0
           const int sh = (rn & 1) * 16 + (lane >> 4) * 4;

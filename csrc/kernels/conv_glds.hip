@@ -106,8 +106,9 @@ __device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, int FK,
-          bool FP8 = false, bool NJ = false>
+          bool FP8 = false, bool NJ = false, bool FRES = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  // FRES (FWD): residual a.res added in the epilogue before the ReLU (conv_common.h)
   // NJ (DGRAD): no residual join (a.beta == 0) — the epilogue's previous-dx registers are not
   // allocated (the fused-statistics dgrad needs them for the BN input x instead)
   // FK: 0 = generic K decomposition; 1 = FASTK (a K-step is one filter tap × 64 (fp8: 128)
@@ -491,7 +492,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
       }
     } else {
-      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ>(
+      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES>(
           a, T, acc, wm, wn, lane, rout, out_scale, no_epi_mem, s_sum, s_sq);
     }
   };
@@ -725,9 +726,9 @@ constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, int FK,
-          bool F8 = false, bool NJ = false>
+          bool F8 = false, bool NJ = false, bool FRES = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ>;
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES>;
   constexpr int lds = lds_bytes(BM, BN, WM, ST);
   static bool attr = false;
   if (!attr) {
@@ -826,6 +827,7 @@ void conv_set_glds_mode(int mode) { g_glds_override = mode; }
 bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int mode = conv_glds_mode();
   if (mode == 0 || a0.C % 8 || a0.K % 8) return false;
+  if (a0.res && !a0.bias) return false;  // residual epilogue instantiated with bias only
   // default selection (ResNet-50 b256, tools/n64_configs.py): ≥ 128 output channels, and 1×1
   // filters with 64 (the 8-wave 256×64 tiles: 35 vs 53 µs on 56×56 64→64); 3×3 filters with 64
   // output channels stay on the register-staged kernel
@@ -866,12 +868,33 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
       else launch_gcfg<FWD, false, false, FK>(a, cfg, blocks, st);           \
     }                                                                        \
   } while (0)
+  if (a.res) {
+    // residual epilogue (DeepLab units): the default FWD tile configs, bias, ± statistics
+#define TDL_R(FK)                                                                            \
+  do {                                                                                       \
+    if (cfg == 4) {                                                                          \
+      if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, true, FK, false, false, true>(a, blocks, st);   \
+      else launch_g<FWD, 256, 64, 8, 1, 3, false, true, FK, false, false, true>(a, blocks, st);        \
+    } else {                                                                                 \
+      if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, true, FK, false, false, true>(a, blocks, st);  \
+      else launch_g<FWD, 256, 128, 4, 2, 3, false, true, FK, false, false, true>(a, blocks, st);       \
+    }                                                                                        \
+  } while (0)
+    if (cfg != 0 && cfg != 4) return false;
+    if (fk == 1) TDL_R(1);
+    else if (fk == 2) TDL_R(2);
+    else TDL_R(0);
+#undef TDL_R
+    return true;
+  }
   if (fk == 1) TDL_G(1);
   else if (fk == 2) TDL_G(2);
   else TDL_G(0);
 #undef TDL_G
   return true;
 }
+
+bool conv_fwd_res_launch(const ConvArgs& a, hipStream_t st) { return conv_fwd_glds(a, st); }
 
 // DGRAD with prepared parity classes (conv_dgrad_launch builds them); returns false when the
 // register-staged kernel should run instead.

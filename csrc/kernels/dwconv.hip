@@ -565,21 +565,29 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
                                                      int tiles_w, int relu_in,
                                                      const bf16_t* __restrict__ mask_x,
                                                      float* __restrict__ stats,
-                                                     const bf16_t* __restrict__ bn_x) {
+                                                     const bf16_t* __restrict__ bn_x, int ntiles) {
   // stats (optional, fp32 [2][C], accumulated): BN sums of the stored bf16 outputs — (Σy, Σy²)
   // for the BN that normalises this forward's output, or (Σg, Σg·bn_x) with bn_x the input of
   // the BN whose output gradient this dgrad produces (bn.hip red_raw) — so that BN skips its
   // separate reduce pass
   // tile: tr × tw output pixels (runtime, ≤ DT_TR × DT_TW, balanced splits of Ho / Wo); lanes:
   // 8 channel lanes × tw column lanes × rg row groups (each slides over ⌈tr / rg⌉ rows)
+  // A workgroup walks tiles blockIdx.x, +gridDim.x, … < ntiles (one tile per workgroup unless
+  // the launcher caps the grid — with statistics, so each workgroup flushes its sums once).
   __shared__ uint4 tile[DT_CHUNKS];
   const int t = threadIdx.x;
-  int b = blockIdx.x;
+  const int cl = t & 7, rest = t >> 3, cg0 = blockIdx.y * DT_CH;
+  float ss[8], sq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss[j] = sq[j] = 0.f;
+  for (int tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+  if (tb != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+  int b = tb;
   const int tx = b % tiles_w;
   b /= tiles_w;
   const int ty = b % tiles_h;
   const int n = b / tiles_h;
-  const int h0 = ty * tr, w0 = tx * tw, cg0 = blockIdx.y * DT_CH;
+  const int h0 = ty * tr, w0 = tx * tw;
   const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
   const bf16_t* src = in + (long)n * Hi * Wi * C;
   for (int i = t; i < chunks; i += blockDim.x) {
@@ -594,14 +602,11 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
     tile[i] = v;
   }
   __syncthreads();
-  const int cl = t & 7, rest = t >> 3, pw = rest % tw, g = rest / tw;
+  const int pw = rest % tw, g = rest / tw;
   const int w = w0 + pw, c = cg0 + cl * 8;
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
   const int r1 = min(min(tr, r0 + rpg), Ho - h0);
   const bool active = !(g >= rg || w >= Wo || c >= C || r0 >= r1);
-  float ss[8], sq[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ss[j] = sq[j] = 0.f;
   if (active) {
   f32x2 wv[9][4], bb[4];
 #pragma unroll
@@ -667,6 +672,7 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
     }
   }
   }
+  }  // tiles
   if (stats) {
     // workgroup reduction over the lanes of each of the 64 channels (the LDS tile is free now),
     // then one atomic pair per channel
@@ -679,13 +685,26 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
       red[(64 + cl * 8 + j) * L + rest] = sq[j];
     }
     __syncthreads();
-    if (t < 128) {
-      const int which = t >> 6, ch = t & 63;
+    for (int o = t; o < 128; o += blockDim.x) {  // (64-thread workgroups for tiny images)
+      const int which = o >> 6, ch = o & 63;
       float v = 0.f;
       for (int i = 0; i < L; ++i) v += red[(which * 64 + ch) * L + i];
       if (cg0 + ch < C) atomicAdd(stats + which * C + cg0 + ch, v);
     }
   }
+}
+
+// tile-kernel grid (x): every tile its own workgroup, except with fused statistics — then
+// ≈ TDL_DW_STAT_WG workgroups in all, each walking several tiles and flushing its sums once
+// (one atomic pair per channel per workgroup instead of per tile)
+int dw_tile_grid(int ntiles, int C, bool stats) {
+  if (!stats) return ntiles;
+  static const int target = [] {
+    const char* e = getenv("TDL_DW_STAT_WG");
+    return e ? std::max(1, atoi(e)) : 2048;
+  }();
+  const int cg = cdiv(C, DT_CH);
+  return std::max(1, std::min(ntiles, cdiv(target, cg)));
 }
 
 // balanced tiling of an Ho × Wo output: tw ≤ 32 columns, tr ≤ 8 rows, rg = 32 / tw row groups
@@ -887,10 +906,12 @@ bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
   if (slide_ok(a) && dw_tile()) {
     const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
-    dim3 grid((unsigned)(a.N * g.th * g.twn), (unsigned)cdiv(a.C, DT_CH));
+    const int ntiles = a.N * g.th * g.twn;
+    dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
     hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
-                       g.twn, a.relu_in, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr);
+                       g.twn, a.relu_in, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
+                       ntiles);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {
     const Slide4Geom g = slide4_geom(a.C / 4, a.Wo);
@@ -920,10 +941,11 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
   if (slide_ok(a) && dw_tile()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const DwTileGeom g = dw_tile_geom(a.H, a.W);
-    dim3 grid((unsigned)(a.N * g.th * g.twn), (unsigned)cdiv(a.C, DT_CH));
+    const int ntiles = a.N * g.th * g.twn;
+    dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
     hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
-                       g.twn, 0, a.mask_x, a.stats, a.bn_x);
+                       g.twn, 0, a.mask_x, a.stats, a.bn_x, ntiles);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const Slide4Geom g = slide4_geom(a.C / 4, a.W);

@@ -42,6 +42,8 @@ struct ConvArgs {
                      // ((Σg, Σg·x) with g the stored dx and x = a.bn_x, the BN's input; LDS-DMA
                      // kernel, stride-1 only) — the BN backward then needs no reduce pass
   const bf16_t* bn_x;  // DGRAD with stats: the BN input [N,H,W,C] (same layout as dx)
+  const bf16_t* res;   // FWD (LDS-DMA kernel, with bias): residual added before the ReLU, laid
+                       // out like the output
   int N, H, W, C, K, R, S, Ho, Wo;
   int sh, sw, ph, pw, dh, dw;
   int M, Ng, Kg;     // GEMM dims
@@ -74,6 +76,8 @@ struct ConvArgs {
 constexpr int MAX_DG_CLASSES = 16;
 
 void conv_fwd_launch(const ConvArgs& a, hipStream_t st);
+// FWD with a.res: false (nothing launched) when the LDS-DMA kernel does not take the problem
+bool conv_fwd_res_launch(const ConvArgs& a, hipStream_t st);
 // returns true when a.stats was filled (DGRAD BN-backward statistics fused into the epilogue);
 // a.stats is ignored (false) when the problem does not run on the LDS-DMA kernel
 bool conv_dgrad_launch(const ConvArgs& a, hipStream_t st);

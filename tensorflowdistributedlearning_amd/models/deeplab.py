@@ -78,7 +78,17 @@ class BetaUnit(nn.Module):
                                 **pad)
 
     def forward(self, x, end_points=None, name=None):
-        preact = self.preact(x)
+        return self._run(x, end_points, name, None, False)[0]
+
+    def forward_fused(self, x, stats=None):
+        """The unit with its output ``relu(conv3 + bias + shortcut)`` computed in conv3's
+        epilogue, which also accumulates the BN sums of that output for the next unit's
+        pre-activation BN (training).  ``stats``: those sums for this unit's input.  Returns
+        ``(y, stats_of_y)``; the conv3 end point (the pre-add conv3 output) is not produced."""
+        return self._run(x, None, None, stats, True)
+
+    def _run(self, x, end_points, name, stats, fuse_out):
+        preact = self.preact(x, stats=stats)
         if self.shortcut is None:
             sc, join = self.subsample(x), None
         else:
@@ -90,11 +100,15 @@ class BetaUnit(nn.Module):
         r = self.conv1(preact, join=join)
         if self.conv2 is not None:
             r = self.conv2(r)
+        if fuse_out:
+            if self.training:
+                return self.conv3(r, want_stats=True, residual=sc, relu=True)
+            return self.conv3(r, residual=sc, relu=True), None
         r = self.conv3(r)
         if end_points is not None and name is not None:
             last = "conv3" if self.block_type == "bottleneck" else "conv2"
             end_points[f"{name}/bottleneck_v2/{last}"] = _logical(r, self.out_channels)
-        return add_relu(sc, r)
+        return add_relu(sc, r), None
 
 
 def _round_up(c, multiple):
@@ -198,18 +212,31 @@ class DeepLabResNet(nn.Module):
         self.decoder_conv_3x3 = Conv2d(2 * base_depth, 1, 3, 1, "SAME", bias=True,
                                        pad_cout_to=channel_align)
 
-    def forward_encoder(self, x):
+    # residual add + ReLU of every unit in its conv3 epilogue, with the next unit's pre-activation
+    # BN statistics accumulated there too (BetaUnit.forward_fused) — not for units whose conv3 end
+    # point is wanted (the decoder's block1/unit_1; all of them with return_end_points)
+    fuse_residual = os.environ.get("TDL_DL_FUSE_RES", "1") == "1"
+
+    def forward_encoder(self, x, all_end_points=True):
         """The ResNet-v2-beta encoder alone (``resnet_v2_beta`` without the ASPP / decoder,
-        core/resnet.py:171-257): returns (block4 features, end_points)."""
+        core/resnet.py:171-257): returns (block4 features, end_points).  ``all_end_points``
+        False: only the block outputs and the decoder's block1/unit_1 conv end point (the other
+        units then run with the fused residual epilogue)."""
         if x.shape[-1] != self.conv1_1.conv._cin_store:
             x = nn.functional.pad(x, (0, self.conv1_1.conv._cin_store - x.shape[-1]))
         end_points = {}
         root = f"{self.model_name}/resnet_v2"
         net = self.conv1_3(self.conv1_2(self.conv1_1(x)))
         net = self.postnorm(self.pool1(net))
-        for bname, mods in zip(self.block_names, self.blocks):
+        fuse = self.fuse_residual and not all_end_points
+        st = None
+        for bi, (bname, mods) in enumerate(zip(self.block_names, self.blocks)):
             for ui, unit in enumerate(mods):
-                net = unit(net, end_points, f"{root}/{bname}/unit_{ui + 1}")
+                if fuse and not (bi == 0 and ui == 0):
+                    net, st = unit.forward_fused(net, st)
+                else:
+                    net, st = unit._run(net, end_points, f"{root}/{bname}/unit_{ui + 1}", st,
+                                        False)
             end_points[f"{root}/{bname}"] = _logical(net, mods[-1].out_channels)
         return end_points[f"{root}/block4"], end_points
 
@@ -221,7 +248,7 @@ class DeepLabResNet(nn.Module):
 
     def forward(self, x, return_end_points=False):
         root = f"{self.model_name}/resnet_v2"
-        _, end_points = self.forward_encoder(x)
+        _, end_points = self.forward_encoder(x, all_end_points=return_end_points)
         atrous = end_points[f"{root}/block4"].contiguous()  # a copy only for unaligned widths
         last = 3 if self.block_type == "bottleneck" else 2
         b1 = end_points[f"{root}/block1/unit_1/bottleneck_v2/conv{last}"].contiguous()

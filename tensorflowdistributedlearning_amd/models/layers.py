@@ -212,9 +212,12 @@ class Conv2d(nn.Module):
             sc = self.__dict__["_fp8_x"] = DelayedScaler()
         return sc.quantize(x)
 
-    def forward(self, x, want_stats=False, join=None):
+    def forward(self, x, want_stats=False, join=None, residual=None, relu=None):
+        """``residual``: y = act(conv(x) + bias + residual) (the epilogue adds it); ``relu``
+        overrides the layer's activation for this call."""
         g = self.geom(x.shape[1], x.shape[2])
-        y, stats = conv2d(x, self.weight, self.bias, g, self.relu, want_stats, self, join)
+        y, stats = conv2d(x, self.weight, self.bias, g, self.relu if relu is None else relu,
+                          want_stats, self, join, residual)
         return (y, stats) if want_stats else y
 
     def extra_repr(self):
@@ -378,8 +381,9 @@ class BNAct(nn.Module):
         self.bn = BatchNorm(c, decay, eps, scale, c_phys=c_phys)
         self.relu = relu
 
-    def forward(self, x):
-        return self.bn(x, relu=self.relu)
+    def forward(self, x, stats=None):
+        """``stats``: the input's BN sums (Σx, Σx²) if its producer already accumulated them."""
+        return self.bn(x, stats=stats, relu=self.relu)
 
 
 class MaxPool(nn.Module):

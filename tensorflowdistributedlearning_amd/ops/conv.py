@@ -92,19 +92,36 @@ def ref_conv_wgrad(dy, x, w_shape, geom: ConvGeom):
 # raw ops (dispatch)
 # ----------------------------------------------------------------------------------------------
 
-def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out_dtype=None):
-    """y = conv(x, w) (+bias) (relu).  If ``stats`` (fp32 [2, K]) is given, per-channel sum and
-    sum of squares of the *stored* output are accumulated into it (BN statistics epilogue)."""
+def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out_dtype=None,
+             residual=None):
+    """y = conv(x, w) (+bias) (+residual) (relu).  If ``stats`` (fp32 [2, K]) is given,
+    per-channel sum and sum of squares of the *stored* output are accumulated into it (BN
+    statistics epilogue).  ``residual`` (shaped like y) is added in the LDS-DMA kernel's epilogue
+    before the ReLU (with a bias); problems that kernel does not take add it in one elementwise
+    pass afterwards."""
     N, H, W, C = x.shape
     K, R, S, Cw = w.shape
     assert C == Cw, f"channel mismatch {C} vs {Cw}"
     Ho, Wo = geom.out_hw(H, W, R, S)
     if on_gpu(x):
         y = torch.empty((N, Ho, Wo, K), device=x.device, dtype=out_dtype or x.dtype)
-        ext().conv_fwd(x, w, y, bias, stats, geom.stride[0], geom.stride[1], geom.padding[0],
-                       geom.padding[2], geom.dilation[0], geom.dilation[1], bool(relu))
-        return y
+        args = (geom.stride[0], geom.stride[1], geom.padding[0], geom.padding[2],
+                geom.dilation[0], geom.dilation[1])
+        if residual is None:
+            ext().conv_fwd(x, w, y, bias, stats, *args, bool(relu))
+            return y
+        if bias is not None and ext().conv_fwd(x, w, y, bias, stats, *args, bool(relu),
+                                               residual.contiguous()):
+            return y
+        ext().conv_fwd(x, w, y, bias, None, *args, False)
+        out = torch.empty_like(y)
+        ext().add_act(y, residual.contiguous(), out, bool(relu))
+        if stats is not None:
+            ext().bn_stats(out, stats)
+        return out
     y = ref_conv_fwd(x, w, geom, bias)
+    if residual is not None:
+        y = y + residual.float()
     if relu:
         y = torch.relu(y)
     y = y.to(out_dtype or x.dtype)
@@ -324,21 +341,23 @@ def relu_bwd(dy, y):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer, join):
+    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer, join, residual=None):
         w = layer.compute_weight(x.dtype) if layer is not None else compute_weight(weight, x.dtype)
         stats = None
         if want_stats:
             stats = workspace.zeros((2, w.shape[0]), x.device)
         b = None if bias is None else (layer.compute_bias() if layer is not None
                                        else bias.detach())
-        if layer is not None and getattr(layer, "fp8", False) and b is None and on_gpu(x):
+        if layer is not None and getattr(layer, "fp8", False) and b is None and on_gpu(x) \
+                and residual is None:
             # fp8 forward (weights + activations e4m3, per-tensor scales); backward stays bf16
             pre = getattr(x, "_tdl_fp8", None)  # e4m3 copy emitted by the producing BN
             x8, sx = pre if pre is not None else layer.fp8_input(x)
             w8, sw = layer.fp8_weight(w)
             y = conv_fwd_fp8(x8, sx, w8, sw, geom, relu=relu, stats=stats)
         else:
-            y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats)
+            y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats, residual=residual)
+        ctx.has_res = residual is not None
         ctx.geom = geom
         ctx.relu = relu
         ctx.layer = layer
@@ -361,10 +380,14 @@ class _Conv2dFn(torch.autograd.Function):
         x, weight, bias, y = ctx.saved_tensors
         geom = ctx.geom
         if dy is None:
-            return (None,) * 8
+            return (None,) * 9
         dy = dy.contiguous()
         if ctx.relu:
             dy = relu_bwd(dy, y)
+        # the residual's gradient is the (masked) output gradient itself; it stays referenced by
+        # the side-stream weight gradient's keep-alive list, so autograd never sums into it in
+        # place while that kernel reads it
+        dres = dy if ctx.has_res and ctx.needs_input_grad[8] else None
         dx = None
         side = streams.side(dy.device) if (weight.requires_grad or
                                             (bias is not None and bias.requires_grad)) else None
@@ -433,7 +456,7 @@ class _Conv2dFn(torch.autograd.Function):
                 _conv_param_grads(ctx, dy, x, weight, bias)
             streams.keep_alive(dy.device, dy, x)  # until the next join (no record_stream)
             streams.join_at_backward_end(dy.device)  # backward() returns joined
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, dres
 
 
 def _conv_param_grads(ctx, dy, x, weight, bias):
@@ -471,8 +494,8 @@ def _conv_param_grads(ctx, dy, x, weight, bias):
 
 
 def conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False, want_stats=False,
-           layer=None, join=None):
+           layer=None, join=None, residual=None):
     """Differentiable NHWC conv. Returns (y, stats) where stats is fp32 [2, K] (sum, sumsq of y)
     when ``want_stats`` else an empty tensor.  ``join`` (ops.gradjoin.GradJoin) makes dx share one
-    buffer with the other consumers of ``x``."""
-    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer, join)
+    buffer with the other consumers of ``x``.  ``residual``: y = act(conv + bias + residual)."""
+    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer, join, residual)

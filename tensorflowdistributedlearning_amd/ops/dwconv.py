@@ -10,6 +10,8 @@ core/xception.py:90-110) and the fixed Laplacian of preprocessing.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -30,6 +32,14 @@ def ref_dw_fwd(x, w, geom: ConvGeom, bias=None):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
+# TDL_DW_STATS=1: the depthwise tile kernels fuse the neighbouring BNs' statistics (forward
+# Σy, Σy²; dgrad Σg, Σg·x_bn with the ReLU mask applied as x > 0).  Off by default: on
+# Xception-41 b128 (same box, two alternating rounds, scripts/r3_dwab.sh) 2578 / 2577 img/s on vs
+# 2595 / 2604 off — the epilogue's extra x read, LDS reduction and atomics cost what the BNs'
+# reduce passes did (the per-kernel checks stay in tests/test_kernels_gpu.py)
+DW_STATS = os.environ.get("TDL_DW_STATS", "0") == "1"
+
+
 def _fusable_relu_in(x, R, S):
     """The kernels fold an input ReLU into their loads for 3×3 filters on 8-channel vectors."""
     return x.shape[-1] % 8 == 0 and R * S == 9
@@ -48,7 +58,7 @@ class _DwConvFn(torch.autograd.Function):
             fused = ext().dwconv_fwd(x, w, None if bias is None else bias.detach(), y,
                                      geom.stride[0], geom.stride[1], geom.padding[0],
                                      geom.padding[2], geom.dilation[0], geom.dilation[1],
-                                     bool(relu), bool(relu_in), stats)
+                                     bool(relu), bool(relu_in), stats if DW_STATS else None)
             if want_stats and not fused:  # strided / dilated row kernels: a reduce pass
                 bn_stats(y, stats)
         else:
@@ -92,8 +102,8 @@ class _DwConvFn(torch.autograd.Function):
                 # x is a BN output: its ReLU mask is x > 0 (the stored y), so this dgrad can apply
                 # it through the relu_in mask path, and the tile kernel can accumulate that BN's
                 # backward sums (Σg, Σg·x_bn) in its epilogue (ops/gradjoin.py)
-                use_tok = (tok is not None and tok.x is not None and gradjoin.STATS_SINGLE
-                           and _fusable_relu_in(x, R, S))
+                use_tok = (DW_STATS and tok is not None and tok.x is not None
+                           and gradjoin.STATS_SINGLE and _fusable_relu_in(x, R, S))
                 masked = ctx.relu_in or (use_tok and (tok.relu_y or tok.mask is not None))
                 red = workspace.zeros((2, x.shape[-1]), dy.device) if use_tok else None
                 fused = ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1],

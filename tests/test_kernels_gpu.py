@@ -864,22 +864,26 @@ def test_conv_dgrad_bnstat_ragged_k(gpu, shape):
     assert rel_err(red, want) < 1e-4
 
 
-@pytest.mark.parametrize("Cn,stride", [(728, 1), (128, 1), (64, 2), (200, 1)])
-def test_depthwise_fused_bn_stats(gpu, Cn, stride):
+@pytest.mark.parametrize("Cn,stride,H", [(728, 1, 19), (128, 1, 19), (64, 2, 19), (200, 1, 19),
+                                        (1536, 1, 2), (728, 1, 4), (256, 1, 7)])
+def test_depthwise_fused_bn_stats(gpu, Cn, stride, H):
     """The depthwise kernels' fused BN sums: forward (Σy, Σy²) of the stored output (tile kernel;
     the strided row kernels fall back to a reduce pass inside the op), and the dgrad's
     (Σg, Σg·x_bn) of the stored, x>0-masked dx — vs fp32 reductions; dx bit-identical to the
     unfused dgrad."""
     torch.manual_seed(24)
     from tensorflowdistributedlearning_amd.models.layers import resolve_padding
-    H = 19
     pad = resolve_padding("SAME", H, H, 3, 3, (stride, stride), (1, 1))
     g = C.ConvGeom((stride, stride), pad, (1, 1))
     x = torch.randn(4, H, H, Cn, device=gpu).bfloat16()
     w = (torch.randn(3, 3, Cn, device=gpu) * 0.3).bfloat16()
     wp = torch.nn.Parameter(w.float())
     wp._lowp = w
-    y, st = D.depthwise_conv2d(x, wp, None, g, False, want_stats=True)
+    D.DW_STATS = True
+    try:
+        y, st = D.depthwise_conv2d(x, wp, None, g, False, want_stats=True)
+    finally:
+        D.DW_STATS = False
     yf = y.float().reshape(-1, Cn)
     assert rel_err(st, torch.stack([yf.sum(0), (yf * yf).sum(0)])) < 1e-4
     Ho = y.shape[1]

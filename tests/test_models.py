@@ -185,3 +185,28 @@ def test_deeplab_concat_free_head_matches_cat(train):
         torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-6, msg=name)
     for p, q in zip(a.buffers(), b.buffers()):
         torch.testing.assert_close(p, q)
+
+
+@pytest.mark.parametrize("block_type", ["bottleneck", "basic_block"])
+def test_deeplab_fused_residual_units_match(block_type):
+    """Units with relu(conv3 + bias + shortcut) in conv3's epilogue (plus the next pre-activation
+    BN's statistics) vs the unfused units: same logits, gradients and moving statistics."""
+    torch.manual_seed(4)
+    kw = dict(model_name="m", input_shape=(33, 33), n_blocks=(2, 2, 1), base_depth=16,
+              block_type=block_type)
+    a = models.DeepLabResNet(**kw)
+    b = models.DeepLabResNet(**kw)
+    b.load_state_dict(a.state_dict())
+    a.fuse_residual, b.fuse_residual = False, True
+    x = torch.randn(2, 33, 33, 2)
+    res = []
+    for m in (a, b):
+        m.train()
+        out = m(x)
+        out.float().pow(2).mean().backward()
+        res.append((out, [p.grad.clone() for p in m.parameters()]))
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=1e-5, atol=1e-6)
+    for (name, _), ga, gb in zip(a.named_parameters(), res[0][1], res[1][1]):
+        torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-6, msg=name)
+    for p, q in zip(a.buffers(), b.buffers()):
+        torch.testing.assert_close(p, q)
