@@ -409,9 +409,17 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
                   c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dres,
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
                   int64_t relu, c10::optional<Tensor> dx8, c10::optional<Tensor> amax_ring,
-                  int64_t phase, c10::optional<Tensor> scale_out, bool red_raw) {
+                  int64_t phase, c10::optional<Tensor> scale_out, bool red_raw,
+                  c10::optional<Tensor> dadd) {
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
+  const bf16_t* addp = nullptr;
+  if (dadd.has_value() && dadd->defined()) {
+    CHECK_T(*dadd, torch::kBFloat16);
+    TORCH_CHECK(dadd->sizes() == dx.sizes() && x.size(-1) % 8 == 0,
+                "bn_bwd_apply dadd: shaped like dx, C % 8 == 0");
+    addp = BF(*dadd);
+  }
   const int64_t C = x.size(-1);
   const int64_t ldd = bn_vec_ld(dy, C, "bn_bwd_apply dy");  // dy: contiguous or channel slice
   TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn_bwd_apply: dy, x, dx sizes");
@@ -430,7 +438,7 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
   bn_bwd_apply_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
                       optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
                       C, (float)count, (int)relu, stream(), d8, prev, optfw(scale_out), out, zero,
-                      red_raw, ldd);
+                      red_raw, ldd, addp);
 }
 
 // ---------------------------------------------------------------------------------- elementwise
@@ -891,7 +899,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("red"), py::arg("gamma"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("count"), py::arg("relu"), py::arg("dx8") = py::none(),
         py::arg("amax_ring") = py::none(), py::arg("phase") = 0, py::arg("scale_out") = py::none(),
-        py::arg("red_raw") = false);
+        py::arg("red_raw") = false, py::arg("dadd") = py::none());
   m.def("fp8_quantize_e5m2", [](Tensor x, Tensor ring, int64_t phase, bool measure, Tensor scale,
                                 Tensor y8) {
     CHECK_T(x, torch::kBFloat16);

@@ -450,7 +450,11 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, float* __restrict__ dgamma,
     float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu,
     uint8_t* __restrict__ dx8, const float* __restrict__ amax_prev, float* __restrict__ scale_out,
-    float* __restrict__ amax_out, float* __restrict__ amax_zero, int red_raw, int ldd_v) {
+    float* __restrict__ amax_out, float* __restrict__ amax_zero, int red_raw, int ldd_v,
+    const bf16_t* __restrict__ dadd) {
+  // dadd (optional, shaped like dx): another consumer's gradient of x added to dx in this pass
+  // (a DeepLab unit input feeds its pre-activation BN and, as the identity shortcut, the
+  // residual of conv3's epilogue) instead of autograd summing the two
   // ldd_v: dy's row stride in 8-element vectors (a channel slice of a concat gradient when > C/8)
   // red_raw: red = (Σg, Σg·x) accumulated by the producing dgrad's epilogue (conv_common.h);
   // Σg·x̂ = invstd·(Σg·x − mean·Σg) here
@@ -511,13 +515,14 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
   if (HOIST) load_coef((int)(i % cvecs));
   for (; i < nvec; i += U * stride) {
     // U vectors per thread in flight: every load of the group is issued before any use
-    uint4 lg[U], lx[U], ly[U];
+    uint4 lg[U], lx[U], ly[U], la[U];
     uint32_t lm[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long k = i + u * stride < nvec ? i + u * stride : i;
       lg[u] = ((const uint4*)dy)[ldd_v == cvecs ? k : (k / cvecs) * ldd_v + k % cvecs];
       lx[u] = ((const uint4*)x)[k];
+      if (dadd) la[u] = ((const uint4*)dadd)[k];
       if (relu == 1) ly[u] = ((const uint4*)y)[k];
       if (relu == 3) lm[u] = ((const uint8_t*)y)[k];
     }
@@ -545,6 +550,12 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = A[j] * g[j] + Bc[j] * vx[j] + Cc[j];
+      if (dadd) {
+        float va[8];
+        unpack(la[u], va);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += va[j];
+      }
       const uint4 packed = pack8(o);
       ((uint4*)dx)[k] = packed;
       if (amax_out) {
@@ -665,7 +676,8 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          const float* red, const float* gamma, bf16_t* dx, bf16_t* dres,
                          float* dgamma, float* dbeta, long M, int C, float count, int relu,
                          hipStream_t st, uint8_t* dx8, const float* amax_prev, float* scale_out,
-                         float* amax_out, float* amax_zero, bool red_raw, long ldd) {
+                         float* amax_out, float* amax_zero, bool red_raw, long ldd,
+                         const bf16_t* dadd) {
   const long n = M * C;
   if (ldd <= 0) ldd = C;
   if (C % 8 == 0) {
@@ -677,7 +689,7 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                    : bwd_apply_vec_kernel<false, 1>;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
                        dbeta, n / 8, C, 1.f / count, relu, dx8, amax_prev, scale_out, amax_out,
-                       amax_zero, red_raw ? 1 : 0, (int)(ldd / 8));
+                       amax_zero, red_raw ? 1 : 0, (int)(ldd / 8), dadd);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu,

@@ -153,7 +153,8 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                          float* scale_out = nullptr, float* amax_out = nullptr,
                          float* amax_zero = nullptr,
                          bool red_raw = false,  // red = (Σg, Σg·x) from a fused dgrad epilogue
-                         long ldd = 0);  // dy row stride (elements; 0 = C)
+                         long ldd = 0,  // dy row stride (elements; 0 = C)
+                         const bf16_t* dadd = nullptr);  // added to dx (C % 8 == 0)
 
 // elementwise --------------------------------------------------------------------------------
 // t [N][H][Wo][Cp] = row-packed x [N][H][W][Cx] for a k×k stem conv (first Cr channels, S taps of

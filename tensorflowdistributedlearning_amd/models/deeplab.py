@@ -31,6 +31,7 @@ from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.upsample import upsample, upsample_into
 from ..ops.elementwise import add_relu
 from ..ops import gradjoin
+from ..ops.bn import ResidualLink
 
 
 class _Subsample(nn.Module):
@@ -88,7 +89,11 @@ class BetaUnit(nn.Module):
         return self._run(x, None, None, stats, True)
 
     def _run(self, x, end_points, name, stats, fuse_out):
-        preact = self.preact(x, stats=stats)
+        # identity shortcut of a fused unit: x feeds the pre-activation BN and conv3's residual
+        # epilogue — the BN backward adds the residual gradient to its dx (ops/bn.ResidualLink)
+        link = (ResidualLink() if fuse_out and self.shortcut is None and self.stride == 1
+                and torch.is_grad_enabled() and x.requires_grad else None)
+        preact = self.preact(x, stats=stats, link=link)
         if self.shortcut is None:
             sc, join = self.subsample(x), None
         else:
@@ -102,8 +107,8 @@ class BetaUnit(nn.Module):
             r = self.conv2(r)
         if fuse_out:
             if self.training:
-                return self.conv3(r, want_stats=True, residual=sc, relu=True)
-            return self.conv3(r, residual=sc, relu=True), None
+                return self.conv3(r, want_stats=True, residual=sc, relu=True, res_link=link)
+            return self.conv3(r, residual=sc, relu=True, res_link=link), None
         r = self.conv3(r)
         if end_points is not None and name is not None:
             last = "conv3" if self.block_type == "bottleneck" else "conv2"

@@ -212,12 +212,13 @@ class Conv2d(nn.Module):
             sc = self.__dict__["_fp8_x"] = DelayedScaler()
         return sc.quantize(x)
 
-    def forward(self, x, want_stats=False, join=None, residual=None, relu=None):
+    def forward(self, x, want_stats=False, join=None, residual=None, relu=None, res_link=None):
         """``residual``: y = act(conv(x) + bias + residual) (the epilogue adds it); ``relu``
-        overrides the layer's activation for this call."""
+        overrides the layer's activation for this call; ``res_link`` (ops/bn.ResidualLink)
+        hands the residual's gradient to the BN that normalises it."""
         g = self.geom(x.shape[1], x.shape[2])
         y, stats = conv2d(x, self.weight, self.bias, g, self.relu if relu is None else relu,
-                          want_stats, self, join, residual)
+                          want_stats, self, join, residual, res_link)
         return (y, stats) if want_stats else y
 
     def extra_repr(self):
@@ -338,9 +339,9 @@ class BatchNorm(nn.Module):
             sc = self.__dict__["_fp8_bwd"] = DelayedScaler()
         return sc.bn_args(x)
 
-    def forward(self, x, stats=None, residual=None, relu=False, res_join=None):
+    def forward(self, x, stats=None, residual=None, relu=False, res_join=None, link=None):
         return batch_norm_act(x, self, stats=stats, residual=residual, relu=relu,
-                              training=self.training, res_join=res_join)
+                              training=self.training, res_join=res_join, link=link)
 
 
 class ConvBN(nn.Module):
@@ -381,9 +382,10 @@ class BNAct(nn.Module):
         self.bn = BatchNorm(c, decay, eps, scale, c_phys=c_phys)
         self.relu = relu
 
-    def forward(self, x, stats=None):
-        """``stats``: the input's BN sums (Σx, Σx²) if its producer already accumulated them."""
-        return self.bn(x, stats=stats, relu=self.relu)
+    def forward(self, x, stats=None, link=None):
+        """``stats``: the input's BN sums (Σx, Σx²) if its producer already accumulated them;
+        ``link``: ops/bn.ResidualLink of x's residual-path gradient."""
+        return self.bn(x, stats=stats, relu=self.relu, link=link)
 
 
 class MaxPool(nn.Module):

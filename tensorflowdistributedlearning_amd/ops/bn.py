@@ -164,26 +164,27 @@ def bn_red_xhat(red, coef):
 
 
 def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None, dbeta=None,
-                 fp8=None, red_raw=False):
+                 fp8=None, red_raw=False, dadd=None):
     """dx (same dtype as x) and optionally the masked gradient g for the residual branch.
     On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch.
     ``red_raw``: ``red`` holds (Σg, Σg·x) from a fused dgrad epilogue (:func:`bn_red_xhat`).
     ``fp8`` = (amax_ring, phase, scale, emit): also write an e5m2 copy of dx with delayed scaling
     (4× headroom over the previous call's |dx|max) — attached as ``dx._tdl_fp8`` = (dx8, scale)
-    for the fp8 dgrad of the producing conv."""
+    for the fp8 dgrad of the producing conv.  ``dadd`` (shaped like x): another gradient of x
+    added to dx in the same pass."""
     C = x.shape[-1]
     if on_gpu(dy):
         dx = torch.empty_like(x)
         dres = torch.empty_like(dy) if want_dres else None
         if fp8 is None:
             ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
-                               int(relu), red_raw=bool(red_raw))
+                               int(relu), red_raw=bool(red_raw), dadd=dadd)
             return dx, dres
         ring, phase, scale, emit = fp8
         dx8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e5m2) if emit else None
         ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
                            int(relu), dx8.view(torch.uint8) if emit else None, ring, int(phase),
-                           scale, red_raw=bool(red_raw))
+                           scale, red_raw=bool(red_raw), dadd=dadd)
         if emit:
             dx._tdl_fp8 = (dx8, scale)
         return dx, dres
@@ -196,6 +197,8 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
     gam = gamma.detach().float() if gamma is not None else torch.ones(C)
     k = gam * coef[3]
     dx = k * (g - red[0] / count - xhat * red[1] / count)
+    if dadd is not None:
+        dx = dx + dadd.float().reshape(-1, C)
     dres = g.reshape(dy.shape).to(dy.dtype) if want_dres else None
     return dx.reshape(x.shape).to(x.dtype), dres
 
@@ -204,9 +207,37 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
 # autograd
 # ----------------------------------------------------------------------------------------------
 
+class ResidualLink:
+    """Hands the residual-path gradient of a tensor x to the BN that normalises x, so the BN
+    backward adds it to its dx in the same pass (``bn_bwd_apply(dadd=…)``) instead of autograd
+    summing the two gradients (a DeepLab unit input feeds its pre-activation BN and, as the
+    identity shortcut, conv3's residual epilogue).  Order independent: whichever backward runs
+    second sees the other's state — a residual gradient arriving after the BN backward already
+    ran is returned to autograd as usual."""
+    __slots__ = ("g", "bn_done")
+
+    def __init__(self):
+        self.g = None
+        self.bn_done = False
+
+    def offer(self, g):
+        """Residual side: True if the BN will add ``g`` (return None to autograd then)."""
+        if self.bn_done:
+            return False
+        self.g = g
+        return True
+
+    def take(self):
+        """BN side: the residual gradient if it arrived first, else None (and mark done)."""
+        g, self.g = self.g, None
+        self.bn_done = True
+        return g
+
+
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training, res_join, need_grad):
+    def forward(ctx, x, stats, gamma, beta, residual, bn, relu, training, res_join, need_grad,
+                link=None):
         C = x.shape[-1]
         count = x.numel() // C
         if training:
@@ -248,6 +279,7 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.count = count
         ctx.bn = bn
         ctx.training = training
+        ctx.link = link
         ctx.has_res = residual is not None
         ctx.res_join = res_join if residual is not None else None
         ctx.relu = 0 if not relu else (3 if mask is not None else (2 if residual is None else 1))
@@ -278,7 +310,11 @@ class _BatchNormActFn(torch.autograd.Function):
             dres = None
             if ctx.has_res:
                 dres = dy if premasked else g.reshape(dy.shape).to(dy.dtype)
-            return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None
+            if ctx.link is not None:
+                extra = ctx.link.take()
+                if extra is not None:
+                    dx = (dx.float() + extra.float()).to(x.dtype)
+            return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None, None
         # pre-masked: the block output's consumers already applied this ReLU's mask to dy
         # (ops/gradjoin.py) — no mask reads, and dy itself is the residual gradient
         if premasked:
@@ -305,10 +341,15 @@ class _BatchNormActFn(torch.autograd.Function):
         gp, _ = _phys_params(ctx.bn, gamma, beta)
         count = ctx.count if ctx.training else float("inf")  # frozen BN: dx = γ·invstd·g
         fp8 = ctx.bn.fp8_bwd_state(x) if getattr(ctx.bn, "emit_fp8_bwd", False) else None
+        extra = ctx.link.take() if ctx.link is not None else None
+        fuse_add = extra is not None and tuple(extra.shape) == tuple(x.shape) and (
+            not on_gpu(dy) or C % 8 == 0)
         dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, count, relu,
                                 ctx.has_res and not premasked and relu != 0,
                                 gt if direct_g else None, bt if direct_b else None, fp8=fp8,
-                                red_raw=red_raw)
+                                red_raw=red_raw, dadd=extra.contiguous() if fuse_add else None)
+        if extra is not None and not fuse_add:
+            dx = dx + extra
         if ctx.has_res and (premasked or relu == 0):
             dres = dy  # no mask to apply: the residual gradient is the incoming one, no copy
         if red_raw and want_g and not direct_g:
@@ -319,7 +360,7 @@ class _BatchNormActFn(torch.autograd.Function):
             deliver_grad(beta, None if direct_b else red[0][:c], written=direct_b)
         if ctx.mask_token is not None:
             ctx.mask_token.release()
-        return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None
+        return dx, None, None, None, _join_res(ctx, dres), None, None, None, None, None, None
 
 
 def _phys_params(bn, gamma, beta):
@@ -352,15 +393,17 @@ def _join_res(ctx, dres):
     return join.take()
 
 
-def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True, res_join=None):
+def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True, res_join=None,
+                   link=None):
     """act(BN(x) [+ residual]).  ``bn`` is a :class:`models.layers.BatchNorm` (holds γ, β and the
     moving statistics).  ``stats`` may carry Σx, Σx² already accumulated by the producer conv.
-    ``res_join`` shares the residual's gradient buffer with its other consumers."""
+    ``res_join`` shares the residual's gradient buffer with its other consumers; ``link``
+    (:class:`ResidualLink`) adds x's residual-path gradient to dx in the backward pass."""
     # (grad mode is off inside Function.forward: decide here whether a backward will follow)
     need_grad = torch.is_grad_enabled() and (
         x.requires_grad or (residual is not None and residual.requires_grad))
     return _BatchNormActFn.apply(x, stats, bn.gamma, bn.beta, residual, bn, relu, training,
-                                 res_join, need_grad)
+                                 res_join, need_grad, link)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -341,7 +341,8 @@ def relu_bwd(dy, y):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer, join, residual=None):
+    def forward(ctx, x, weight, bias, geom, relu, want_stats, layer, join, residual=None,
+                res_link=None):
         w = layer.compute_weight(x.dtype) if layer is not None else compute_weight(weight, x.dtype)
         stats = None
         if want_stats:
@@ -358,6 +359,7 @@ class _Conv2dFn(torch.autograd.Function):
         else:
             y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats, residual=residual)
         ctx.has_res = residual is not None
+        ctx.res_link = res_link
         ctx.geom = geom
         ctx.relu = relu
         ctx.layer = layer
@@ -380,7 +382,7 @@ class _Conv2dFn(torch.autograd.Function):
         x, weight, bias, y = ctx.saved_tensors
         geom = ctx.geom
         if dy is None:
-            return (None,) * 9
+            return (None,) * 10
         dy = dy.contiguous()
         if ctx.relu:
             dy = relu_bwd(dy, y)
@@ -388,6 +390,9 @@ class _Conv2dFn(torch.autograd.Function):
         # the side-stream weight gradient's keep-alive list, so autograd never sums into it in
         # place while that kernel reads it
         dres = dy if ctx.has_res and ctx.needs_input_grad[8] else None
+        if dres is not None and ctx.res_link is not None and ctx.res_link.offer(dres):
+            dres = None  # the residual's BN adds it to its dx (ops/bn.py ResidualLink)
+        ctx.res_link = None
         dx = None
         side = streams.side(dy.device) if (weight.requires_grad or
                                             (bias is not None and bias.requires_grad)) else None
@@ -456,7 +461,7 @@ class _Conv2dFn(torch.autograd.Function):
                 _conv_param_grads(ctx, dy, x, weight, bias)
             streams.keep_alive(dy.device, dy, x)  # until the next join (no record_stream)
             streams.join_at_backward_end(dy.device)  # backward() returns joined
-        return dx, None, None, None, None, None, None, None, dres
+        return dx, None, None, None, None, None, None, None, dres, None
 
 
 def _conv_param_grads(ctx, dy, x, weight, bias):
@@ -494,8 +499,9 @@ def _conv_param_grads(ctx, dy, x, weight, bias):
 
 
 def conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False, want_stats=False,
-           layer=None, join=None, residual=None):
+           layer=None, join=None, residual=None, res_link=None):
     """Differentiable NHWC conv. Returns (y, stats) where stats is fp32 [2, K] (sum, sumsq of y)
     when ``want_stats`` else an empty tensor.  ``join`` (ops.gradjoin.GradJoin) makes dx share one
     buffer with the other consumers of ``x``.  ``residual``: y = act(conv + bias + residual)."""
-    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer, join, residual)
+    return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer, join, residual,
+                           res_link)

@@ -899,3 +899,20 @@ def test_depthwise_fused_bn_stats(gpu, Cn, stride, H):
     if fused:
         gf, xf = dx1.float().reshape(-1, Cn), bn_x.float().reshape(-1, Cn)
         assert rel_err(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-4
+
+
+def test_bn_bwd_apply_dadd(gpu):
+    """bn_bwd_apply(dadd=g2): dx + g2 in the same pass — equals the plain dx plus g2 (bf16
+    rounding of the sum once instead of twice)."""
+    torch.manual_seed(31)
+    M, Cn = 4 * 13 * 13, 1024
+    x = torch.randn(4, 13, 13, Cn, device=gpu).bfloat16()
+    dy = torch.randn_like(x)
+    g2 = torch.randn_like(x)
+    gam = torch.rand(Cn, device=gpu) + 0.5
+    coef = B.bn_finalize(B.bn_stats(x), M, gam, torch.zeros(Cn, device=gpu),
+                         torch.zeros(Cn, device=gpu), torch.ones(Cn, device=gpu), 0.9, 1e-3, True)
+    red = B.bn_bwd_reduce(dy, None, x, coef, 2)
+    d0, _ = B.bn_bwd_apply(dy, None, x, coef, red, gam, M, 2, False)
+    d1, _ = B.bn_bwd_apply(dy, None, x, coef, red, gam, M, 2, False, dadd=g2)
+    assert rel_err(d1, d0.float() + g2.float()) < 1e-2

@@ -764,11 +764,12 @@ def test_deeplab_concat_free_head_gpu_matches_cat(gpu):
     assert torch.equal(oa, ob)
     gcos = torch.nn.functional.cosine_similarity(ta.flat.grad, tb.flat.grad, dim=0).item()
     assert gcos > 0.9999, gcos
-    ta.train_mode = tb.train_mode = True
-    ta.train_step(x, y)
-    tb.train_step(x, y)
-    for (n, ra), rb in zip(a.named_buffers(), b.buffers()):
-        torch.testing.assert_close(ra, rb, rtol=1e-2, atol=1e-3, msg=n)
+    a2, b2, c = (models.DeepLabResNet(**kw) for _ in range(3))
+    b2.load_state_dict(a2.state_dict())
+    c.load_state_dict(a2.state_dict())
+    a2.concat_free = False
+    _moving_stats_within_noise(a2, b2, c, lambda m: Trainer(m, lovasz_hinge, gpu, "adam",
+                                                            dict(lr=0.0)), x, y)
 
 
 @pytest.mark.timeout(400)
@@ -872,8 +873,31 @@ def test_deeplab_fused_residual_gpu_matches_unfused(gpu):
     assert cos.item() > 0.9999, cos.item()
     gcos = torch.nn.functional.cosine_similarity(ta.flat.grad, tb.flat.grad, dim=0).item()
     assert gcos > 0.999, gcos
-    ta.train_mode = tb.train_mode = True
-    ta.train_step(x, y)
-    tb.train_step(x, y)
-    for (n, ra), rb in zip(a.named_buffers(), b.buffers()):
-        torch.testing.assert_close(ra, rb, rtol=2e-2, atol=2e-3, msg=n)
+    a2, b2, c = (models.DeepLabResNet(**kw) for _ in range(3))
+    b2.load_state_dict(a2.state_dict())
+    c.load_state_dict(a2.state_dict())
+    a2.fuse_residual, b2.fuse_residual, c.fuse_residual = False, True, True
+    _moving_stats_within_noise(a2, b2, c, lambda m: Trainer(m, lovasz_hinge, gpu, "adam",
+                                                            dict(lr=0.0)), x, y)
+
+
+def _moving_stats_within_noise(a, b, c, make_trainer, x, y):
+    """One training-mode step of models a, b and c (b and c identical): the moving statistics of
+    a vs b differ by no more than b vs c do.  Batch statistics are summed with float atomics
+    (non-deterministic order), and on a 4-image batch the last BNs of this 60-BN network move by
+    ~5 % run to run from that alone (tools/dbg_det.py), so a fixed tolerance is no test."""
+    trs = [make_trainer(m) for m in (a, b, c)]
+    for t in trs:
+        t.train_mode = True
+        t.train_step(x, y)
+    torch.cuda.synchronize()
+    bufs = [dict(m.named_buffers()) for m in (a, b, c)]
+    worst_ab = worst_bc = 0.0
+    for n in bufs[0]:
+        if "running" not in n:
+            continue
+        scale = bufs[1][n].abs().max().clamp_min(1e-6)
+        worst_ab = max(worst_ab, ((bufs[0][n] - bufs[1][n]).abs().max() / scale).item())
+        worst_bc = max(worst_bc, ((bufs[1][n] - bufs[2][n]).abs().max() / scale).item())
+    print("moving stats: a-b", worst_ab, "run-to-run b-c", worst_bc)
+    assert worst_ab <= 2.0 * worst_bc + 2e-3, (worst_ab, worst_bc)
