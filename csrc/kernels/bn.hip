@@ -67,8 +67,31 @@ __global__ void reduce_scalar_kernel(const bf16_t* __restrict__ a, const bf16_t*
 
 // ---------------------------------------------------------------------------------------------
 // vector path (C % 8 == 0, C/8 <= 256): thread = (row lane, channel vector)
+typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
+// 16-B global load / store, optionally non-temporal (streamed once: keep it out of the caches the
+// concurrent side-stream weight-gradient GEMMs reuse)
+template <bool NTM>
+__device__ __forceinline__ uint4 ld16(const void* p, long k) {
+  if constexpr (NTM) {
+    const nt_u32x4 v = __builtin_nontemporal_load((const nt_u32x4*)p + k);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+    return ((const uint4*)p)[k];
+  }
+}
+template <bool NTM>
+__device__ __forceinline__ void st16(void* p, long k, const uint4& v) {
+  if constexpr (NTM) {
+    nt_u32x4 w;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    __builtin_nontemporal_store(w, (nt_u32x4*)p + k);
+  } else {
+    ((uint4*)p)[k] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
-template <int KIND, int U>
+template <int KIND, int U, bool NTM = false>
 __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict__ a,
                                                         const bf16_t* __restrict__ y,
                                                         const bf16_t* __restrict__ x,
@@ -106,9 +129,9 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
         const long rr = r + u * rpp;
         const long row = rr < r1 ? rr : r;
         const long off = row * C + cv * 8;
-        la[u] = *(const uint4*)(a + row * lda + cv * 8);
-        if (KIND == 1) lx[u] = *(const uint4*)(x + off);
-        if (KIND == 1 && relu == 1) ly[u] = *(const uint4*)(y + off);
+        la[u] = ld16<NTM>(a + row * lda + cv * 8, 0);
+        if (KIND == 1) lx[u] = ld16<NTM>(x + off, 0);
+        if (KIND == 1 && relu == 1) ly[u] = ld16<NTM>(y + off, 0);
         if (KIND == 1 && relu == 3) lm[u] = ((const uint8_t*)y)[off >> 3];
       }
 #pragma unroll
@@ -167,7 +190,7 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
 // downsampling bottleneck and its shortcut BN, whose output the residual BN adds): one pass reads
 // dy once for both — out = (Σg, Σg·x̂) of x (coef), out2 = (Σg, Σg·x2) raw (bn_bwd_apply
 // red_raw).  Same thread layout as reduce_vec_kernel (C % 8 == 0, C / 8 <= NT).
-template <int U>
+template <int U, bool NTM = false>
 __global__ void __launch_bounds__(NT) reduce2_vec_kernel(const bf16_t* __restrict__ a,
                                                          const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ x2,
@@ -197,9 +220,9 @@ __global__ void __launch_bounds__(NT) reduce2_vec_kernel(const bf16_t* __restric
       for (int u = 0; u < U; ++u) {
         const long rr = r + u * rpp;
         const long off = (rr < r1 ? rr : r) * C + cv * 8;
-        la[u] = *(const uint4*)(a + off);
-        lx[u] = *(const uint4*)(x + off);
-        lx2[u] = *(const uint4*)(x2 + off);
+        la[u] = ld16<NTM>(a + off, 0);
+        lx[u] = ld16<NTM>(x + off, 0);
+        lx2[u] = ld16<NTM>(x2 + off, 0);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -252,6 +275,7 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     static const int cap = env_int("TDL_BN_RED_BLOCKS", 1024);
     static const int u = env_int("TDL_BN_RED_U", 4);
     static const int minr = env_int("TDL_BN_RED_MINR", 8);
+    static const bool ntm = env_int("TDL_BN_NT", 1) != 0;  // non-temporal streaming
     // optional cap on the atomics per launch (every workgroup adds 2C partial sums): measured
     // (tools/bn_micro.py) 1 Mi: b256 reduce total 2.92 -> 2.85 ms but b1024 8.43 -> 8.86 ms —
     // fewer workgroups cost more bandwidth than the atomics save; off by default
@@ -261,14 +285,26 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
     if (u == 8)
-      hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                         out, M, C, rpb, relu, lda);
+      if (ntm)
+        hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8, true>), dim3(blocks), dim3(NT), 0, st, a, y, x,
+                           coef, out, M, C, rpb, relu, lda);
+      else
+        hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
+                           out, M, C, rpb, relu, lda);
     else if (u == 2)
-      hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                         out, M, C, rpb, relu, lda);
+      if (ntm)
+        hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2, true>), dim3(blocks), dim3(NT), 0, st, a, y, x,
+                           coef, out, M, C, rpb, relu, lda);
+      else
+        hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
+                           out, M, C, rpb, relu, lda);
     else
-      hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                         out, M, C, rpb, relu, lda);
+      if (ntm)
+        hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4, true>), dim3(blocks), dim3(NT), 0, st, a, y, x,
+                           coef, out, M, C, rpb, relu, lda);
+      else
+        hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
+                           out, M, C, rpb, relu, lda);
   } else {
     long blocks = std::min<long>(512, std::max<long>(1, M / 64));
     long rpb = (M + blocks - 1) / blocks;
@@ -320,7 +356,7 @@ __device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) {
   return (uint32_t)v;
 }
 
-template <int U>
+template <int U, bool NTM = false>
 __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict__ x,
                                                        const float* __restrict__ coef,
                                                        const bf16_t* __restrict__ res,
@@ -364,8 +400,8 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long k = i + u * stride < nvec ? i + u * stride : i;
-      lx[u] = ((const uint4*)x)[k];
-      if (res) lr[u] = ((const uint4*)res)[k];
+      lx[u] = ld16<NTM>(x, k);
+      if (res) lr[u] = ld16<NTM>(res, k);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -387,7 +423,7 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
     const uint4 packed = pack8(v);
-    ((uint4*)y)[ldy_v == cvecs ? k : (k / cvecs) * ldy_v + k % cvecs] = packed;
+    st16<NTM>(y, ldy_v == cvecs ? k : (k / cvecs) * ldy_v + k % cvecs, packed);
     if (mask) {  // ReLU mask of the stored bf16 values, one bit per element (backward relu mode 3)
       float q[8];
       unpack8(packed, q);
@@ -443,7 +479,7 @@ __device__ __forceinline__ uint32_t e5m2x4(float a, float b, float c, float d) {
   return (uint32_t)v;
 }
 
-template <bool HOIST, int U>
+template <bool HOIST, int U, bool NTM = false>
 __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const bf16_t* __restrict__ x,
     const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
@@ -520,9 +556,9 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long k = i + u * stride < nvec ? i + u * stride : i;
-      lg[u] = ((const uint4*)dy)[ldd_v == cvecs ? k : (k / cvecs) * ldd_v + k % cvecs];
-      lx[u] = ((const uint4*)x)[k];
-      if (dadd) la[u] = ((const uint4*)dadd)[k];
+      lg[u] = ld16<NTM>(dy, ldd_v == cvecs ? k : (k / cvecs) * ldd_v + k % cvecs);
+      lx[u] = ld16<NTM>(x, k);
+      if (dadd) la[u] = ld16<NTM>(dadd, k);
       if (relu == 1) ly[u] = ((const uint4*)y)[k];
       if (relu == 3) lm[u] = ((const uint8_t*)y)[k];
     }
@@ -557,7 +593,7 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
         for (int j = 0; j < 8; ++j) o[j] += va[j];
       }
       const uint4 packed = pack8(o);
-      ((uint4*)dx)[k] = packed;
+      st16<NTM>(dx, k, packed);
       if (amax_out) {
         float q[8];
         unpack8(packed, q);  // quantise the stored bf16 values
@@ -644,7 +680,9 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
   if (ldy <= 0) ldy = C;
   if (C % 8 == 0) {
     static const int u = env_int("TDL_BN_APPLY_U", 1);
-    auto k = u == 2 ? apply_vec_kernel<2> : u == 4 ? apply_vec_kernel<4> : apply_vec_kernel<1>;
+    static const bool ntm = env_int("TDL_BN_NT", 1) != 0;  // non-temporal streaming
+    auto k = ntm ? apply_vec_kernel<1, true>
+                 : (u == 2 ? apply_vec_kernel<2> : u == 4 ? apply_vec_kernel<4> : apply_vec_kernel<1>);
     hipLaunchKernelGGL(k, dim3(ew_blocks(n / 8, C / 8, u)), dim3(NT), 0, st, x, coef, res, y, n / 8, C,
                        relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask,
                        (int)(ldy / 8));
@@ -667,8 +705,13 @@ bool bn_bwd_reduce2_launch(const bf16_t* dy, const bf16_t* x, const bf16_t* x2, 
   long blocks = std::min<long>(cap, std::max<long>(1, M / (rpp * 8)));
   const long rpb = (M + blocks - 1) / blocks;
   blocks = (M + rpb - 1) / rpb;
-  hipLaunchKernelGGL((reduce2_vec_kernel<4>), dim3(blocks), dim3(NT), 0, st, dy, x, x2, coef, red, red2,
-                     M, C, rpb);
+  static const bool ntm = env_int("TDL_BN_NT", 1) != 0;  // non-temporal streaming
+  if (ntm)
+    hipLaunchKernelGGL((reduce2_vec_kernel<4, true>), dim3(blocks), dim3(NT), 0, st, dy, x, x2, coef, red,
+                       red2, M, C, rpb);
+  else
+    hipLaunchKernelGGL((reduce2_vec_kernel<4>), dim3(blocks), dim3(NT), 0, st, dy, x, x2, coef, red, red2,
+                       M, C, rpb);
   return true;
 }
 
@@ -684,8 +727,10 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
     static const int u = env_int("TDL_BN_BWD_U", 2);
     const int blocks = ew_blocks(n / 8, C / 8, u);
     const bool hoist = ((long)blocks * NT) % (C / 8) == 0;
-    auto k = hoist ? (u == 2 ? bwd_apply_vec_kernel<true, 2> : u == 4 ? bwd_apply_vec_kernel<true, 4>
-                                                                     : bwd_apply_vec_kernel<true, 1>)
+    static const bool ntm = env_int("TDL_BN_NT", 1) != 0;  // non-temporal streaming
+    auto k = hoist ? (ntm ? bwd_apply_vec_kernel<true, 2, true>
+                          : u == 2 ? bwd_apply_vec_kernel<true, 2>
+                                   : u == 4 ? bwd_apply_vec_kernel<true, 4> : bwd_apply_vec_kernel<true, 1>)
                    : bwd_apply_vec_kernel<false, 1>;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
                        dbeta, n / 8, C, 1.f / count, relu, dx8, amax_prev, scale_out, amax_out,
