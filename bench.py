@@ -113,6 +113,10 @@ def main():
                     help="capture the whole training step as a HIP graph and replay it (removes "
                          "host launch overhead in launch-bound configs; with N>1 the bucketed "
                          "all-reduces are captured too, on the native RCCL communicator)")
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="GPU compute precision: bf16 (fused bf16 kernels, fp32 accumulation / "
+                         "master weights) or fp32 (fp32 operands on the fp32 MFMA end to end — the "
+                         "reference's own precision, for the like-for-like deeplab_ref comparison)")
     ap.add_argument("--profile-phases", action="store_true",
                     help="also print per-phase step times (forward/backward/comm_wait/optimizer, "
                          "device events) to stderr")
@@ -139,9 +143,14 @@ def main():
             and rccl_ranks != args.gpus:
         raise SystemExit(f"RCCL reports {rccl_ranks} ranks, --gpus {args.gpus}")
     comm = "rccl" if ctx.native is not None else ("gloo" if n > 1 else "none")
-    # CPU (plumbing runs, tests): fp32 storage, the PyTorch reference ops
-    lowp = torch.bfloat16 if dev.type == "cuda" else None
-    ddt = torch.bfloat16 if dev.type == "cuda" else torch.float32
+    # CPU (plumbing runs, tests): fp32 storage, the PyTorch reference ops; GPU --dtype fp32: fp32
+    # activations + the fp32 master weights read directly by the fp32 kernels (no compute copy)
+    gpu_bf16 = dev.type == "cuda" and args.dtype == "bf16"
+    lowp = torch.bfloat16 if gpu_bf16 else None
+    ddt = torch.bfloat16 if gpu_bf16 else torch.float32
+    dtype_name = "bf16" if gpu_bf16 else "fp32" if dev.type == "cuda" else "fp32 (CPU plumbing run)"
+    if args.fp8 and not gpu_bf16:
+        raise SystemExit("--fp8 runs on the bf16 GPU path")
     torch.manual_seed(1234)
     fp8_desc = None
     if args.model == "deeplab_ref" and args.fp8:
@@ -154,7 +163,8 @@ def main():
                      bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
                      profile_phases=args.profile_phases, lowp_dtype=lowp)
         x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank, dtype=ddt)
-        metric = "images/sec (whole node), reference DeepLab-ResNet 101x101x2 bf16"
+        metric = ("images/sec (whole node), reference DeepLab-ResNet 101x101x2 "
+                  + ("bf16" if gpu_bf16 else "fp32"))
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
                "image": "101x101x2", "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks, "optimizer": "adam",
                "loss": "lovasz_hinge", "hip_graph": args.graph,
@@ -176,9 +186,9 @@ def main():
                      bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
                      profile_phases=args.profile_phases, lowp_dtype=lowp)
         x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank, dtype=ddt)
-        metric = METRIC if args.model == "resnet50" and args.image_size == 224 and not args.fp8 \
+        metric = METRIC if args.model == "resnet50" and args.image_size == 224 and gpu_bf16 \
             else (f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} "
-                  f"{fp8_desc if args.fp8 else 'bf16' if dev.type == 'cuda' else 'fp32'}")
+                  f"{fp8_desc if args.fp8 else 'bf16' if gpu_bf16 else 'fp32'}")
         cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
                "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks,
@@ -232,8 +242,7 @@ def main():
             "baseline": ("BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
                          "ResNet-50 number)" if args.model != "deeplab_ref" else
                          "BASELINE.md measured 90.7 img/s on 2 GPUs, scaled per GPU"),
-            "dtype": (fp8_desc if args.fp8 else
-                      "bf16" if dev.type == "cuda" else "fp32 (CPU plumbing run)"),
+            "dtype": fp8_desc if args.fp8 else dtype_name,
             "data": "synthetic (device-resident random batch, random-init weights)",
             "config": cfg}), flush=True)
     shutdown()

@@ -73,6 +73,109 @@ ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_
   return a;
 }
 
+// ------------------------------------------------------------------------------- fp32 path (f32.hip)
+// Every entry point below dispatches on the activation dtype: fp32 tensors run the fp32 kernels
+// (the reference's precision), bf16 the fused bf16 kernels.  The fp32 path has no fused ReLU bit
+// masks, BN-backward-statistics epilogues or fp8 side outputs: requests for them return "not
+// fused" (the caller then runs the plain pass) or fail loudly.
+#define F32(t) ((t).data_ptr<float>())
+static bool is_f32(const Tensor& t) { return t.scalar_type() == torch::kFloat32; }
+
+static void check_c4(int64_t c, const char* what) {
+  TORCH_CHECK(c % 4 == 0, what, ": the fp32 kernels need channel counts % 4 == 0 (got ", c, ")");
+}
+
+// fp32 NHWC tensor, contiguous or a channel slice of a contiguous NHWC buffer: pixel stride
+static int64_t nhwc_ld_f32(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && is_f32(t), what, ": fp32 HIP tensor");
+  if (t.is_contiguous()) return t.size(-1);
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1 && t.stride(2) >= t.size(3) &&
+                  t.stride(1) == t.stride(2) * t.size(2) && t.stride(0) == t.stride(1) * t.size(1) &&
+                  t.stride(2) % 4 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              what, ": must be contiguous NHWC or a 4-aligned channel slice of one");
+  return t.stride(2);
+}
+
+static const float* opt_f32_like(const c10::optional<Tensor>& t, const Tensor& like,
+                                 const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_T(*t, torch::kFloat32);
+  TORCH_CHECK(t->sizes() == like.sizes(), what, ": shaped like ", like.sizes());
+  return F32(*t);
+}
+
+static ConvF32Args conv_f32_args(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t R,
+                                 int64_t S, int64_t Ho, int64_t Wo, int64_t sh, int64_t sw,
+                                 int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  check_c4(C, "conv input channels");
+  check_c4(K, "conv output channels");
+  TORCH_CHECK(N * std::max(H * W, Ho * Wo) < (1LL << 31) && K * R * S * C < (1LL << 31),
+              "fp32 conv: problem too large for 32-bit GEMM indices");
+  ConvF32Args a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.K = K; a.R = R; a.S = S; a.Ho = Ho; a.Wo = Wo;
+  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+  return a;
+}
+
+bool conv_fwd_f32(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias,
+                  c10::optional<Tensor> stats, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                  int64_t dh, int64_t dw, bool relu, c10::optional<Tensor> res) {
+  CHECK_T(x, torch::kFloat32);
+  CHECK_T(w, torch::kFloat32);
+  CHECK_T(y, torch::kFloat32);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && y.dim() == 4 && x.size(3) == w.size(3) &&
+                  y.size(0) == x.size(0) && y.size(3) == w.size(0), "conv_fwd fp32 shapes");
+  ConvF32Args a = conv_f32_args(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1),
+                                w.size(2), y.size(1), y.size(2), sh, sw, ph, pw, dh, dw);
+  a.x = F32(x); a.w = F32(w); a.out = F32(y);
+  a.bias = optf(bias);
+  if (a.bias) TORCH_CHECK(bias->numel() == a.K, "conv_fwd bias: [K]");
+  a.stats = optfw(stats);
+  if (a.stats) TORCH_CHECK(stats->numel() == 2 * a.K, "stats must be [2, K]");
+  a.res = opt_f32_like(res, y, "conv_fwd res");
+  a.relu = relu;
+  conv_f32_fwd_launch(a, stream());
+  return true;
+}
+
+bool conv_dgrad_f32(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                    int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask) {
+  CHECK_T(dy, torch::kFloat32);
+  CHECK_T(w, torch::kFloat32);
+  CHECK_T(dx, torch::kFloat32);
+  TORCH_CHECK(!(mask.has_value() && mask->defined()), "fp32 conv_dgrad: no fused ReLU mask");
+  TORCH_CHECK(dx.size(3) == w.size(3) && dy.size(3) == w.size(0) && dx.size(0) == dy.size(0),
+              "conv_dgrad fp32 shapes");
+  ConvF32Args a = conv_f32_args(dx.size(0), dx.size(1), dx.size(2), dx.size(3), w.size(0), w.size(1),
+                                w.size(2), dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
+  a.dy = F32(dy); a.w = F32(w); a.out = F32(dx);
+  a.accumulate = accumulate;
+  conv_f32_dgrad_launch(a, stream());
+  return false;  // BN-backward statistics never fused on this path
+}
+
+void conv_wgrad_f32(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad, int64_t sh,
+                    int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate) {
+  CHECK_T(dy, torch::kFloat32);
+  CHECK_T(x, torch::kFloat32);
+  CHECK_T(out, torch::kFloat32);
+  TORCH_CHECK(out.dim() == 4 && out.size(3) == x.size(3) && dy.size(3) == out.size(0) &&
+                  dy.size(0) == x.size(0), "conv_wgrad fp32 shapes (dW KRSC)");
+  ConvF32Args a = conv_f32_args(x.size(0), x.size(1), x.size(2), x.size(3), out.size(0),
+                                out.size(1), out.size(2), dy.size(1), dy.size(2), sh, sw, ph, pw,
+                                dh, dw);
+  a.dy = F32(dy); a.x = F32(x); a.out = F32(out);
+  a.accumulate = accumulate;
+  auto st = stream();
+  conv_f32_wgrad_launch(a, st);
+  if (bias_grad.has_value() && bias_grad->defined()) {
+    CHECK_T(*bias_grad, torch::kFloat32);
+    TORCH_CHECK(bias_grad->numel() == a.K, "bias_grad must have K elements");
+    (void)hipMemsetAsync(bias_grad->data_ptr(), 0, a.K * sizeof(float), st);
+    colsum_f32_launch(F32(dy), F32(*bias_grad), (long)dy.numel() / a.K, a.K, a.K, st);
+  }
+}
+
 // ------------------------------------------------------------------------------------------ conv
 // res (optional, shaped like y): y = act(conv + bias + res) in the LDS-DMA epilogue; returns
 // false — nothing launched — when that kernel does not take the problem (the caller then adds
@@ -80,6 +183,7 @@ ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_
 bool conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::optional<Tensor> stats,
               int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu,
               c10::optional<Tensor> res) {
+  if (is_f32(x)) return conv_fwd_f32(x, w, y, bias, stats, sh, sw, ph, pw, dh, dw, relu, res);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -196,6 +300,7 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
                 int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask,
                 c10::optional<Tensor> w_t, c10::optional<Tensor> bn_x,
                 c10::optional<Tensor> bn_red) {
+  if (is_f32(dy)) return conv_dgrad_f32(dy, w, dx, sh, sw, ph, pw, dh, dw, accumulate, mask);
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -277,6 +382,7 @@ void conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, i
 
 void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad, int64_t sh,
                 int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate) {
+  if (is_f32(dy)) return conv_wgrad_f32(dy, x, out, bias_grad, sh, sw, ph, pw, dh, dw, accumulate);
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(out, torch::kFloat32);
@@ -306,6 +412,13 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad
 
 // ------------------------------------------------------------------------------------------- bn
 void bn_stats(Tensor x, Tensor stats) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(stats, torch::kFloat32);
+    check_c4(x.size(-1), "bn_stats");
+    bn_stats_f32_launch(F32(x), F32(stats), x.numel() / x.size(-1), x.size(-1), stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(stats, torch::kFloat32);
   const int64_t C = x.size(-1);
@@ -337,6 +450,20 @@ void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor>
 void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu,
               c10::optional<Tensor> y8, c10::optional<Tensor> amax_ring, int64_t phase,
               c10::optional<Tensor> scale_out, c10::optional<Tensor> mask) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(coef, torch::kFloat32);
+    TORCH_CHECK(!(y8.has_value() && y8->defined()) && !(amax_ring.has_value() && amax_ring->defined()) &&
+                    !(mask.has_value() && mask->defined()),
+                "fp32 bn_apply: no fp8 side output / ReLU bit mask");
+    const int64_t C = x.size(-1);
+    check_c4(C, "bn_apply");
+    const int64_t ldy = nhwc_ld_f32(y, "bn_apply y");
+    TORCH_CHECK(y.numel() == x.numel(), "bn_apply: y and x sizes");
+    bn_apply_f32_launch(F32(x), F32(coef), opt_f32_like(res, x, "bn_apply res"), F32(y),
+                        x.numel() / C, C, relu, ldy, stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(coef, torch::kFloat32);
   const int64_t C = x.size(-1);
@@ -382,6 +509,20 @@ const bf16_t* mask_or_y(const c10::optional<Tensor>& y, const Tensor& x, int64_t
 }
 
 void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Tensor red, int64_t relu) {
+  if (is_f32(x)) {
+    CHECK_T(red, torch::kFloat32);
+    CHECK_T(coef, torch::kFloat32);
+    const int64_t C = x.size(-1);
+    check_c4(C, "bn_bwd_reduce");
+    TORCH_CHECK(relu >= 0 && relu <= 2, "fp32 bn_bwd_reduce: relu mode 0, 1 (y) or 2 (x)");
+    TORCH_CHECK(relu != 1 || (y.has_value() && y->defined()), "relu mask mode 1 needs y");
+    const int64_t ldd = nhwc_ld_f32(dy, "bn_bwd_reduce dy");
+    TORCH_CHECK(dy.numel() == x.numel() && x.is_contiguous(), "bn_bwd_reduce: dy and x sizes");
+    bn_bwd_reduce_f32_launch(F32(dy), relu == 1 ? opt_f32_like(y, x, "bn_bwd_reduce y") : nullptr,
+                             F32(x), F32(coef), F32(red), x.numel() / C, C, (int)relu, ldd,
+                             stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(red, torch::kFloat32);
   const int64_t C = x.size(-1);
@@ -393,6 +534,7 @@ void bn_bwd_reduce(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Te
 }
 
 bool bn_bwd_reduce2(Tensor dy, Tensor x, Tensor x2, Tensor coef, Tensor red, Tensor red2) {
+  if (is_f32(x)) return false;  // fp32: each BN reduces itself
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(x2, torch::kBFloat16);
@@ -411,6 +553,30 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
                   int64_t relu, c10::optional<Tensor> dx8, c10::optional<Tensor> amax_ring,
                   int64_t phase, c10::optional<Tensor> scale_out, bool red_raw,
                   c10::optional<Tensor> dadd) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(dx, torch::kFloat32);
+    CHECK_T(coef, torch::kFloat32);
+    CHECK_T(red, torch::kFloat32);
+    TORCH_CHECK(!red_raw && !(amax_ring.has_value() && amax_ring->defined()),
+                "fp32 bn_bwd_apply: no fused-dgrad statistics / fp8 side output");
+    TORCH_CHECK(relu >= 0 && relu <= 2, "fp32 bn_bwd_apply: relu mode 0, 1 (y) or 2 (x)");
+    const int64_t C = x.size(-1);
+    check_c4(C, "bn_bwd_apply");
+    const int64_t ldd = nhwc_ld_f32(dy, "bn_bwd_apply dy");
+    TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "bn_bwd_apply: dy, x, dx sizes");
+    float* dresp = nullptr;
+    if (dres.has_value() && dres->defined()) {
+      CHECK_T(*dres, torch::kFloat32);
+      TORCH_CHECK(dres->numel() == x.numel(), "dres size");
+      dresp = F32(*dres);
+    }
+    bn_bwd_apply_f32_launch(F32(dy), relu == 1 ? opt_f32_like(y, x, "bn_bwd_apply y") : nullptr,
+                            F32(x), F32(coef), F32(red), optf(gamma), F32(dx), dresp, optfw(dgamma),
+                            optfw(dbeta), opt_f32_like(dadd, x, "bn_bwd_apply dadd"), x.numel() / C,
+                            C, (float)count, (int)relu, ldd, stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   const bf16_t* addp = nullptr;
@@ -453,6 +619,14 @@ void row_pack(Tensor x, Tensor t, int64_t creal, int64_t S, int64_t sw, int64_t 
 }
 
 void relu_bwd(Tensor dy, Tensor y, Tensor dx) {
+  if (is_f32(dy)) {
+    CHECK_T(dy, torch::kFloat32);
+    CHECK_T(y, torch::kFloat32);
+    CHECK_T(dx, torch::kFloat32);
+    TORCH_CHECK(dy.numel() % 4 == 0 && y.numel() == dy.numel() && dx.numel() == dy.numel());
+    relu_bwd_f32_launch(F32(dy), F32(y), F32(dx), dy.numel(), stream());
+    return;
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -460,6 +634,13 @@ void relu_bwd(Tensor dy, Tensor y, Tensor dx) {
 }
 
 void add_act(Tensor a, c10::optional<Tensor> b, Tensor y, bool relu) {
+  if (is_f32(a)) {
+    CHECK_T(a, torch::kFloat32);
+    CHECK_T(y, torch::kFloat32);
+    TORCH_CHECK(a.numel() % 4 == 0 && y.numel() == a.numel());
+    add_act_f32_launch(F32(a), opt_f32_like(b, a, "add_act b"), F32(y), a.numel(), relu, stream());
+    return;
+  }
   CHECK_T(a, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   add_act_launch(BF(a), optb(b), BFW(y), a.numel(), relu, stream());
@@ -480,6 +661,15 @@ void sigmoid_threshold(Tensor x, Tensor prob, Tensor pred, double thr) {
 
 // -------------------------------------------------------------------------------------- pooling
 void maxpool_fwd(Tensor x, Tensor y, Tensor idx, int64_t k, int64_t s, int64_t pt, int64_t pl) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(y, torch::kFloat32);
+    CHECK_T(idx, torch::kUInt8);
+    TORCH_CHECK(k * k <= 255, "window too large for uint8 argmax");
+    maxpool_fwd_launch(F32(x), F32(y), idx.data_ptr<uint8_t>(), x.size(0), x.size(1), x.size(2),
+                       x.size(3), y.size(1), y.size(2), k, s, pt, pl, stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   CHECK_T(idx, torch::kUInt8);
@@ -489,6 +679,13 @@ void maxpool_fwd(Tensor x, Tensor y, Tensor idx, int64_t k, int64_t s, int64_t p
 }
 
 void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t pt, int64_t pl) {
+  if (is_f32(dy)) {
+    CHECK_T(dy, torch::kFloat32);
+    CHECK_T(dx, torch::kFloat32);
+    maxpool_bwd_launch(F32(dy), idx.data_ptr<uint8_t>(), F32(dx), dx.size(0), dx.size(1), dx.size(2),
+                       dx.size(3), dy.size(1), dy.size(2), k, s, pt, pl, stream());
+    return;
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   maxpool_bwd_launch(BF(dy), idx.data_ptr<uint8_t>(), BFW(dx), dx.size(0), dx.size(1), dx.size(2),
@@ -500,6 +697,7 @@ void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t
 // when the channel count does not fit the kernel
 bool maxpool_bwd_stats(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t pt,
                        int64_t pl, Tensor bn_x, Tensor mask, Tensor bn_red) {
+  if (is_f32(dy)) return false;  // fp32: no fused ReLU mask / BN statistics
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   CHECK_T(bn_x, torch::kBFloat16);
@@ -514,12 +712,24 @@ bool maxpool_bwd_stats(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, i
 }
 
 void avgpool_fwd(Tensor x, Tensor y) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(y, torch::kFloat32);
+    avgpool_fwd_launch(F32(x), F32(y), x.size(0), x.size(1) * x.size(2), x.size(3), stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   avgpool_fwd_launch(BF(x), BFW(y), x.size(0), x.size(1) * x.size(2), x.size(3), stream());
 }
 
 void avgpool_bwd(Tensor dy, Tensor dx) {
+  if (is_f32(dy)) {
+    CHECK_T(dy, torch::kFloat32);
+    CHECK_T(dx, torch::kFloat32);
+    avgpool_bwd_launch(F32(dy), F32(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream());
+    return;
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   avgpool_bwd_launch(BF(dy), BFW(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream());
@@ -609,11 +819,33 @@ DwArgs dw_args(const Tensor& x_like, const Tensor& w, int64_t Ho, int64_t Wo, in
   return a;
 }
 
+static DwF32Args dw_f32_args(const Tensor& x_like, const Tensor& w, int64_t Ho, int64_t Wo, int64_t sh,
+                             int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
+  DwF32Args a{};
+  a.N = x_like.size(0); a.H = x_like.size(1); a.W = x_like.size(2); a.C = x_like.size(3);
+  a.R = w.size(0); a.S = w.size(1); a.Ho = Ho; a.Wo = Wo;
+  a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dwl = dw;
+  TORCH_CHECK(w.dim() == 3 && w.size(2) == a.C, "depthwise weight must be [R,S,C]");
+  check_c4(a.C, "depthwise conv");
+  return a;
+}
+
 // stats (optional fp32 [2, C], zeroed by the caller): BN sums of y fused into the kernel;
 // returns whether they were written (stride-1 3×3 tile kernel only)
 bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t sh, int64_t sw,
                 int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu, bool relu_in,
                 c10::optional<Tensor> stats) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(w, torch::kFloat32);
+    CHECK_T(y, torch::kFloat32);
+    TORCH_CHECK(!relu_in, "fp32 depthwise: no fused input ReLU");
+    DwF32Args a = dw_f32_args(x, w, y.size(1), y.size(2), sh, sw, ph, pw, dh, dw);
+    a.x = F32(x); a.w = F32(w); a.bias = optf(bias); a.out = F32(y); a.relu = relu;
+    dwconv_f32_fwd_launch(a, stream());
+    return false;  // statistics never fused here: the caller runs bn_stats
+  }
+
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -633,6 +865,16 @@ bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_
 bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                   int64_t dh, int64_t dw, c10::optional<Tensor> mask_x,
                   c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_red) {
+  if (is_f32(dy)) {
+    CHECK_T(dy, torch::kFloat32);
+    CHECK_T(w, torch::kFloat32);
+    CHECK_T(dx, torch::kFloat32);
+    TORCH_CHECK(!(mask_x.has_value() && mask_x->defined()), "fp32 depthwise: no fused input ReLU");
+    DwF32Args a = dw_f32_args(dx, w, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
+    a.dy = F32(dy); a.w = F32(w); a.out = F32(dx);
+    dwconv_f32_dgrad_launch(a, stream());
+    return false;
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -656,6 +898,17 @@ bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
 
 void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int64_t sh, int64_t sw,
                   int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu_in) {
+  if (is_f32(dy)) {
+    CHECK_T(dy, torch::kFloat32);
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(dwt, torch::kFloat32);
+    TORCH_CHECK(!relu_in, "fp32 depthwise: no fused input ReLU");
+    TORCH_CHECK(dwt.size(0) * dwt.size(1) <= 9, "fp32 depthwise weight gradient: up to 3x3 taps");
+    DwF32Args a = dw_f32_args(x, dwt, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
+    a.dy = F32(dy); a.x = F32(x); a.dwt = F32(dwt); a.db = optfw(db);
+    dwconv_f32_wgrad_launch(a, stream());
+    return;
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(dwt, torch::kFloat32);
@@ -672,6 +925,14 @@ void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int
 
 // ------------------------------------------------------------------------------------- upsample
 void upsample_fwd(Tensor x, Tensor y, Tensor ih, Tensor wh, Tensor iw, Tensor ww) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    const int64_t ldy = nhwc_ld_f32(y, "upsample y");
+    upsample_fwd_launch(F32(x), F32(y), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
+                        ww.data_ptr<float>(), x.size(0), x.size(1), x.size(2), x.size(3), y.size(1),
+                        y.size(2), stream(), (int)ldy);
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   const int64_t ldy = nhwc_ld(y, "upsample y");
   upsample_fwd_launch(BF(x), BFW(y), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
@@ -680,6 +941,14 @@ void upsample_fwd(Tensor x, Tensor y, Tensor ih, Tensor wh, Tensor iw, Tensor ww
 }
 
 void upsample_bwd(Tensor dy, Tensor dx, Tensor ih, Tensor wh, Tensor iw, Tensor ww) {
+  if (is_f32(dy)) {
+    const int64_t ldd = nhwc_ld_f32(dy, "upsample dy");
+    CHECK_T(dx, torch::kFloat32);
+    upsample_bwd_launch(F32(dy), F32(dx), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),
+                        ww.data_ptr<float>(), dx.size(0), dx.size(1), dx.size(2), dx.size(3),
+                        dy.size(1), dy.size(2), stream(), (int)ldd);
+    return;
+  }
   const int64_t ldd = nhwc_ld(dy, "upsample dy");
   CHECK_T(dx, torch::kBFloat16);
   upsample_bwd_launch(BF(dy), BFW(dx), ih.data_ptr<int>(), wh.data_ptr<float>(), iw.data_ptr<int>(),

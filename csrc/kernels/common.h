@@ -57,6 +57,24 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
+// element-type-generic 8-vector / scalar access (bf16 storage or the fp32 path): kernels that are
+// pure data movement (pooling, upsample) are templated on the storage type through these
+__device__ __forceinline__ void load8(const bf16_t* p, float* f) { unpack8(*(const uint4*)p, f); }
+__device__ __forceinline__ void load8(const float* p, float* f) {
+  const float4 a = ((const float4*)p)[0], b = ((const float4*)p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* f) { *(uint4*)p = pack8(f); }
+__device__ __forceinline__ void store8(float* p, const float* f) {
+  ((float4*)p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  ((float4*)p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+__device__ __forceinline__ float load1(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float load1(const float* p) { return *p; }
+__device__ __forceinline__ void store1(bf16_t* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void store1(float* p, float v) { *p = v; }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

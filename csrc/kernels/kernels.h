@@ -244,6 +244,66 @@ void upsample_bwd_launch(const bf16_t* dy, bf16_t* dx, const int* ih, const floa
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
                          int Wo, hipStream_t st, int ldd = 0);
 
+// fp32 path (f32.hip; the reference's own precision) --------------------------------------------
+// NHWC fp32 activations, KRSC fp32 weights; every channel count (C, K) % 4 == 0 (host-checked)
+struct ConvF32Args {
+  const float* x;      // FWD / WGRAD input [N,H,W,C]
+  const float* w;      // FWD / DGRAD weights [K,R,S,C]
+  const float* dy;     // DGRAD / WGRAD output gradient [N,Ho,Wo,K]
+  float* out;          // FWD y [N,Ho,Wo,K]; DGRAD dx [N,H,W,C]; WGRAD dW [K,R,S,C]
+  const float* bias;   // FWD optional [K]
+  float* stats;        // FWD optional BN sums [2][K] (Σy, Σy² of the stored y), accumulated
+  const float* res;    // FWD optional residual shaped like y, added before the ReLU
+  int N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw;
+  int relu;            // FWD
+  int accumulate;      // DGRAD: dx += …; WGRAD: dW += … (else overwritten)
+};
+void conv_f32_fwd_launch(const ConvF32Args& a, hipStream_t st);
+void conv_f32_dgrad_launch(const ConvF32Args& a, hipStream_t st);
+void conv_f32_wgrad_launch(const ConvF32Args& a, hipStream_t st);
+// out[c] += Σ_m x[m·ldx + c] (the caller zeroes out for an overwrite)
+void colsum_f32_launch(const float* x, float* out, long M, int C, long ldx, hipStream_t st);
+void bn_stats_f32_launch(const float* x, float* stats, long M, int C, hipStream_t st);
+// relu: 0 none, 1 mask y > 0, 2 mask x·scale + shift > 0; ldd: dy row stride
+void bn_bwd_reduce_f32_launch(const float* dy, const float* y, const float* x, const float* coef,
+                              float* red, long M, int C, int relu, long ldd, hipStream_t st);
+void bn_apply_f32_launch(const float* x, const float* coef, const float* res, float* y, long M,
+                         int C, bool relu, long ldy, hipStream_t st);
+void bn_bwd_apply_f32_launch(const float* dy, const float* y, const float* x, const float* coef,
+                             const float* red, const float* gamma, float* dx, float* dres,
+                             float* dgamma, float* dbeta, const float* dadd, long M, int C,
+                             float count, int relu, long ldd, hipStream_t st);
+void relu_bwd_f32_launch(const float* dy, const float* y, float* dx, long n, hipStream_t st);
+void add_act_f32_launch(const float* a, const float* b, float* y, long n, bool relu,
+                        hipStream_t st);
+struct DwF32Args {
+  const float* x;
+  const float* w;      // [R,S,C]
+  const float* bias;   // [C] or null
+  const float* dy;
+  float* out;
+  float* dwt;          // fp32 [R,S,C], accumulated
+  float* db;           // fp32 [C], accumulated (optional)
+  int N, H, W, C, R, S, Ho, Wo, sh, sw, ph, pw, dh, dwl;
+  int relu;
+};
+void dwconv_f32_fwd_launch(const DwF32Args& a, hipStream_t st);
+void dwconv_f32_dgrad_launch(const DwF32Args& a, hipStream_t st);
+void dwconv_f32_wgrad_launch(const DwF32Args& a, hipStream_t st);  // R·S ≤ 9
+// fp32 instantiations of the type-generic pooling / upsample kernels
+void maxpool_fwd_launch(const float* x, float* y, uint8_t* idx, int N, int H, int W, int C,
+                        int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
+void maxpool_bwd_launch(const float* dy, const uint8_t* idx, float* dx, int N, int H, int W,
+                        int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
+void avgpool_fwd_launch(const float* x, float* y, int N, int HW, int C, hipStream_t st);
+void avgpool_bwd_launch(const float* dy, float* dx, int N, int HW, int C, hipStream_t st);
+void upsample_fwd_launch(const float* x, float* y, const int* ih, const float* wh,
+                         const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
+                         int Wo, hipStream_t st, int ldy = 0);
+void upsample_bwd_launch(const float* dy, float* dx, const int* ih, const float* wh,
+                         const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
+                         int Wo, hipStream_t st, int ldd = 0);
+
 // fault injection: a 1-lane kernel that spins `ms` milliseconds (≤ 60 s) on stream st
 void debug_spin_launch(double ms, hipStream_t st);
 

@@ -11,8 +11,8 @@ inline int blocks_for(long n) {
   return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT));
 }
 
-template <int V>  // V = 8 (vector) or 1 (scalar)
-__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+template <int V, typename T>  // V = 8 (vector) or 1 (scalar); T = bf16_t or float storage
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                    uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
                                    int Wo, int k, int s, int pt, int pl) {
   const int cv = C / V;
@@ -40,9 +40,9 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
         const long off = (((long)n * H + hi) * W + wi) * C + c;
         float v[V];
         if constexpr (V == 8) {
-          unpack8(*(const uint4*)(x + off), v);
+          load8(x + off, v);
         } else {
-          v[0] = bf2f(x[off]);
+          v[0] = load1(x + off);
         }
 #pragma unroll
         for (int j = 0; j < V; ++j)
@@ -54,21 +54,21 @@ __global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restr
     }
     const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
     if constexpr (V == 8) {
-      *(uint4*)(y + o) = pack8(best);
+      store8(y + o, best);
       uint2 packed;
       packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
       packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
       *(uint2*)(idx + o) = packed;
     } else {
-      y[o] = f2bf(best[0]);
+      store1(y + o, best[0]);
       idx[o] = (uint8_t)arg[0];
     }
   }
 }
 
-template <int V>
-__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
-                                   bf16_t* __restrict__ dx, int N, int H, int W, int C, int Ho,
+template <int V, typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                   T* __restrict__ dx, int N, int H, int W, int C, int Ho,
                                    int Wo, int k, int s, int pt, int pl) {
   const int cv = C / V;
   const long total = (long)N * H * W * cv;
@@ -96,7 +96,7 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
         const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
         if constexpr (V == 8) {
           float g[8];
-          unpack8(*(const uint4*)(dy + o), g);
+          load8(dy + o, g);
           const uint2 packed = *(const uint2*)(idx + o);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -105,15 +105,15 @@ __global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t*
             if (a == want) acc[j] += g[j];
           }
         } else {
-          if (idx[o] == want) acc[0] += bf2f(dy[o]);
+          if (idx[o] == want) acc[0] += load1(dy + o);
         }
       }
     }
     const long off = (((long)n * H + h) * W + w) * C + c;
     if constexpr (V == 8)
-      *(uint4*)(dx + off) = pack8(acc);
+      store8(dx + off, acc);
     else
-      dx[off] = f2bf(acc[0]);
+      store1(dx + off, acc[0]);
   }
 }
 
@@ -192,28 +192,30 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
 }
 
 // global average pool: one thread per (n, channel vector), loop over HW
-__global__ void avgpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+template <typename T>
+__global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N,
                                    int HW, int C) {
   const int cv = C / 8;
   const long total = (long)N * cv;
   for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
     const int n = (int)(t / cv), c = (int)(t % cv) * 8;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bf16_t* base = x + (long)n * HW * C + c;
+    const T* base = x + (long)n * HW * C + c;
     for (int i = 0; i < HW; ++i) {
       float v[8];
-      unpack8(*(const uint4*)(base + (long)i * C), v);
+      load8(base + (long)i * C, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += v[j];
     }
     const float inv = 1.f / HW;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= inv;
-    *(uint4*)(y + (long)n * C + c) = pack8(acc);
+    store8(y + (long)n * C + c, acc);
   }
 }
 
-__global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+template <typename T>
+__global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int N,
                                    int HW, int C) {
   const int cv = C / 8;
   const long total = (long)N * HW * cv;
@@ -223,53 +225,57 @@ __global__ void avgpool_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __rest
     const long p = t / cv;
     const int n = (int)(p / HW);
     float g[8];
-    unpack8(*(const uint4*)(dy + (long)n * C + c), g);
+    load8(dy + (long)n * C + c, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] *= inv;
-    *(uint4*)(dx + p * C + c) = pack8(g);
+    store8(dx + p * C + c, g);
   }
 }
 
-__global__ void avgpool_scalar_fwd(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+template <typename T>
+__global__ void avgpool_scalar_fwd(const T* __restrict__ x, T* __restrict__ y, int N,
                                    int HW, int C) {
   const long total = (long)N * C;
   for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
     const int n = (int)(t / C), c = (int)(t % C);
     float acc = 0.f;
-    for (int i = 0; i < HW; ++i) acc += bf2f(x[((long)n * HW + i) * C + c]);
-    y[t] = f2bf(acc / HW);
+    for (int i = 0; i < HW; ++i) acc += load1(x + ((long)n * HW + i) * C + c);
+    store1(y + t, acc / HW);
   }
 }
 
-__global__ void avgpool_scalar_bwd(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N,
+template <typename T>
+__global__ void avgpool_scalar_bwd(const T* __restrict__ dy, T* __restrict__ dx, int N,
                                    int HW, int C) {
   const long total = (long)N * HW * C;
   for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
     const int c = (int)(t % C);
     const int n = (int)(t / ((long)HW * C));
-    dx[t] = f2bf(bf2f(dy[(long)n * C + c]) / HW);
+    store1(dx + t, load1(dy + (long)n * C + c) / HW);
   }
 }
 
 }  // namespace
 
-void maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
+template <typename T>
+static void maxpool_fwd_impl(const T* x, T* y, uint8_t* idx, int N, int H, int W, int C,
                         int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
   if (C % 8 == 0)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<8>, dim3(blocks_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0,
+    hipLaunchKernelGGL((maxpool_fwd_kernel<8, T>), dim3(blocks_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0,
                        st, x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
   else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<1>, dim3(blocks_for((long)N * Ho * Wo * C)), dim3(NT), 0, st,
+    hipLaunchKernelGGL((maxpool_fwd_kernel<1, T>), dim3(blocks_for((long)N * Ho * Wo * C)), dim3(NT), 0, st,
                        x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
 }
 
-void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
+template <typename T>
+static void maxpool_bwd_impl(const T* dy, const uint8_t* idx, T* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
   if (C % 8 == 0)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<8>, dim3(blocks_for((long)N * H * W * C / 8)), dim3(NT), 0,
+    hipLaunchKernelGGL((maxpool_bwd_kernel<8, T>), dim3(blocks_for((long)N * H * W * C / 8)), dim3(NT), 0,
                        st, dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<1>, dim3(blocks_for((long)N * H * W * C)), dim3(NT), 0, st,
+    hipLaunchKernelGGL((maxpool_bwd_kernel<1, T>), dim3(blocks_for((long)N * H * W * C)), dim3(NT), 0, st,
                        dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
 }
 
@@ -282,22 +288,44 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
   return true;
 }
 
-void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
+template <typename T>
+static void avgpool_fwd_impl(const T* x, T* y, int N, int HW, int C, hipStream_t st) {
   if (C % 8 == 0)
-    hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(blocks_for((long)N * C / 8)), dim3(NT), 0, st, x, y, N,
+    hipLaunchKernelGGL(avgpool_fwd_kernel<T>, dim3(blocks_for((long)N * C / 8)), dim3(NT), 0, st, x, y, N,
                        HW, C);
   else
-    hipLaunchKernelGGL(avgpool_scalar_fwd, dim3(blocks_for((long)N * C)), dim3(NT), 0, st, x, y, N, HW,
+    hipLaunchKernelGGL(avgpool_scalar_fwd<T>, dim3(blocks_for((long)N * C)), dim3(NT), 0, st, x, y, N, HW,
                        C);
 }
 
-void avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
+template <typename T>
+static void avgpool_bwd_impl(const T* dy, T* dx, int N, int HW, int C, hipStream_t st) {
   if (C % 8 == 0)
-    hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(blocks_for((long)N * HW * C / 8)), dim3(NT), 0, st, dy,
+    hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(blocks_for((long)N * HW * C / 8)), dim3(NT), 0, st, dy,
                        dx, N, HW, C);
   else
-    hipLaunchKernelGGL(avgpool_scalar_bwd, dim3(blocks_for((long)N * HW * C)), dim3(NT), 0, st, dy, dx,
+    hipLaunchKernelGGL(avgpool_scalar_bwd<T>, dim3(blocks_for((long)N * HW * C)), dim3(NT), 0, st, dy, dx,
                        N, HW, C);
 }
+
+
+#define TDL_POOL_ENTRY(T)                                                                         \
+  void maxpool_fwd_launch(const T* x, T* y, uint8_t* idx, int N, int H, int W, int C, int Ho,       \
+                          int Wo, int k, int s, int pt, int pl, hipStream_t st) {                   \
+    maxpool_fwd_impl<T>(x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl, st);                           \
+  }                                                                                               \
+  void maxpool_bwd_launch(const T* dy, const uint8_t* idx, T* dx, int N, int H, int W, int C,      \
+                          int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {           \
+    maxpool_bwd_impl<T>(dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl, st);                         \
+  }                                                                                               \
+  void avgpool_fwd_launch(const T* x, T* y, int N, int HW, int C, hipStream_t st) {                 \
+    avgpool_fwd_impl<T>(x, y, N, HW, C, st);                                                      \
+  }                                                                                               \
+  void avgpool_bwd_launch(const T* dy, T* dx, int N, int HW, int C, hipStream_t st) {               \
+    avgpool_bwd_impl<T>(dy, dx, N, HW, C, st);                                                    \
+  }
+TDL_POOL_ENTRY(bf16_t)
+TDL_POOL_ENTRY(float)
+#undef TDL_POOL_ENTRY
 
 }  // namespace tdl

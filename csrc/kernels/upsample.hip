@@ -12,8 +12,8 @@ namespace {
 constexpr int NT = 256;
 inline int blocks_for(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT)); }
 
-template <int V>
-__global__ void up_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+template <int V, typename T>
+__global__ void up_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                               const int* __restrict__ ih, const float* __restrict__ wh,
                               const int* __restrict__ iw, const float* __restrict__ ww, int N, int H,
                               int W, int C, int Ho, int Wo, int ldy) {
@@ -43,21 +43,21 @@ __global__ void up_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const float wgt = wr[r] * wc[q];
-        const bf16_t* src = x + (((long)n * H + rows[r]) * W + cols[q]) * C + c;
+        const T* src = x + (((long)n * H + rows[r]) * W + cols[q]) * C + c;
         float v[V];
-        if constexpr (V == 8) unpack8(*(const uint4*)src, v);
-        else v[0] = bf2f(*src);
+        if constexpr (V == 8) load8(src, v);
+        else v[0] = load1(src);
 #pragma unroll
         for (int k = 0; k < V; ++k) acc[k] += wgt * v[k];
       }
-    bf16_t* dst = y + (((long)n * Ho + i) * Wo + j) * ldy + c;
-    if constexpr (V == 8) *(uint4*)dst = pack8(acc);
-    else *dst = f2bf(acc[0]);
+    T* dst = y + (((long)n * Ho + i) * Wo + j) * ldy + c;
+    if constexpr (V == 8) store8(dst, acc);
+    else store1(dst, acc[0]);
   }
 }
 
-template <int V>
-__global__ void up_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+template <int V, typename T>
+__global__ void up_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx,
                               const int* __restrict__ ih, const float* __restrict__ wh,
                               const int* __restrict__ iw, const float* __restrict__ ww, int N, int H,
                               int W, int C, int Ho, int Wo, int ldd) {
@@ -82,47 +82,65 @@ __global__ void up_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict_
       for (int j = jlo; j <= jhi; ++j) {
         const float wj = (iw[j] == b ? ww[j] : 0.f) + (iw[Wo + j] == b ? ww[Wo + j] : 0.f);
         if (wj == 0.f) continue;
-        const bf16_t* src = dy + (((long)n * Ho + i) * Wo + j) * ldd + c;
+        const T* src = dy + (((long)n * Ho + i) * Wo + j) * ldd + c;
         float v[V];
-        if constexpr (V == 8) unpack8(*(const uint4*)src, v);
-        else v[0] = bf2f(*src);
+        if constexpr (V == 8) load8(src, v);
+        else v[0] = load1(src);
         const float wgt = wi * wj;
 #pragma unroll
         for (int k = 0; k < V; ++k) acc[k] += wgt * v[k];
       }
     }
-    bf16_t* dst = dx + (((long)n * H + a) * W + b) * C + c;
-    if constexpr (V == 8) *(uint4*)dst = pack8(acc);
-    else *dst = f2bf(acc[0]);
+    T* dst = dx + (((long)n * H + a) * W + b) * C + c;
+    if constexpr (V == 8) store8(dst, acc);
+    else store1(dst, acc[0]);
   }
 }
 
 }  // namespace
 
-void upsample_fwd_launch(const bf16_t* x, bf16_t* y, const int* ih, const float* wh, const int* iw,
+template <typename T>
+static void upsample_fwd_impl(const T* x, T* y, const int* ih, const float* wh, const int* iw,
                          const float* ww, int N, int H, int W, int C, int Ho, int Wo,
                          hipStream_t st, int ldy) {
   const long n = (long)N * Ho * Wo * C;
   if (ldy <= 0) ldy = C;
   if (C % 8 == 0 && ldy % 8 == 0)
-    hipLaunchKernelGGL(up_fwd_kernel<8>, dim3(blocks_for(n / 8)), dim3(NT), 0, st, x, y, ih, wh, iw, ww,
+    hipLaunchKernelGGL((up_fwd_kernel<8, T>), dim3(blocks_for(n / 8)), dim3(NT), 0, st, x, y, ih, wh, iw, ww,
                        N, H, W, C, Ho, Wo, ldy);
   else
-    hipLaunchKernelGGL(up_fwd_kernel<1>, dim3(blocks_for(n)), dim3(NT), 0, st, x, y, ih, wh, iw, ww, N,
+    hipLaunchKernelGGL((up_fwd_kernel<1, T>), dim3(blocks_for(n)), dim3(NT), 0, st, x, y, ih, wh, iw, ww, N,
                        H, W, C, Ho, Wo, ldy);
 }
 
-void upsample_bwd_launch(const bf16_t* dy, bf16_t* dx, const int* ih, const float* wh,
+template <typename T>
+static void upsample_bwd_impl(const T* dy, T* dx, const int* ih, const float* wh,
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho, int Wo,
                          hipStream_t st, int ldd) {
   const long n = (long)N * H * W * C;
   if (ldd <= 0) ldd = C;
   if (C % 8 == 0 && ldd % 8 == 0)
-    hipLaunchKernelGGL(up_bwd_kernel<8>, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, dx, ih, wh, iw,
+    hipLaunchKernelGGL((up_bwd_kernel<8, T>), dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, dx, ih, wh, iw,
                        ww, N, H, W, C, Ho, Wo, ldd);
   else
-    hipLaunchKernelGGL(up_bwd_kernel<1>, dim3(blocks_for(n)), dim3(NT), 0, st, dy, dx, ih, wh, iw, ww,
+    hipLaunchKernelGGL((up_bwd_kernel<1, T>), dim3(blocks_for(n)), dim3(NT), 0, st, dy, dx, ih, wh, iw, ww,
                        N, H, W, C, Ho, Wo, ldd);
 }
+
+
+#define TDL_UP_ENTRY(T)                                                                           \
+  void upsample_fwd_launch(const T* x, T* y, const int* ih, const float* wh, const int* iw,       \
+                           const float* ww, int N, int H, int W, int C, int Ho, int Wo,           \
+                           hipStream_t st, int ldy) {                                             \
+    upsample_fwd_impl<T>(x, y, ih, wh, iw, ww, N, H, W, C, Ho, Wo, st, ldy);                       \
+  }                                                                                               \
+  void upsample_bwd_launch(const T* dy, T* dx, const int* ih, const float* wh, const int* iw,     \
+                           const float* ww, int N, int H, int W, int C, int Ho, int Wo,           \
+                           hipStream_t st, int ldd) {                                             \
+    upsample_bwd_impl<T>(dy, dx, ih, wh, iw, ww, N, H, W, C, Ho, Wo, st, ldd);                     \
+  }
+TDL_UP_ENTRY(bf16_t)
+TDL_UP_ENTRY(float)
+#undef TDL_UP_ENTRY
 
 }  // namespace tdl

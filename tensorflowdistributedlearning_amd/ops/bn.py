@@ -21,7 +21,7 @@ import os
 
 import torch
 
-from .common import on_gpu, ext, deliver_grad, grad_target, flat_view
+from .common import on_gpu, fused_gpu, ext, deliver_grad, grad_target, flat_view
 from . import workspace
 from . import gradjoin
 
@@ -251,7 +251,7 @@ class _BatchNormActFn(torch.autograd.Function):
         # nothing saved); with one, the forward writes it as 1 bit per element (mode 3: the two
         # backward kernels read 1/16 of y's bytes instead of y itself)
         mask = None
-        if relu and need_grad and on_gpu(x) and C % 8 == 0 and C <= 2048 and (
+        if relu and need_grad and fused_gpu(x) and C % 8 == 0 and C <= 2048 and (
                 residual is not None or (C % 64 == 0 and gradjoin.STATS_ENABLED
                                          and gradjoin.MASK_ENABLED)):
             # without a residual only for the fused-statistics path: the consuming conv's dgrad
@@ -261,13 +261,13 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.mask_token = None
         if mask is not None:  # the consumers' dgrads may apply it for us (ops/gradjoin.py)
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask, x)
-        elif (not relu and residual is None and need_grad and on_gpu(x) and PAIR_STATS
+        elif (not relu and residual is None and need_grad and fused_gpu(x) and PAIR_STATS
               and gradjoin.STATS_ENABLED):
             # no ReLU: a statistics-only token — the residual BN this output feeds (a shortcut
             # BN) computes both BNs' backward sums in one pass over the shared gradient, or the
             # consuming conv's dgrad fuses them
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(None, x)
-        elif relu and residual is None and need_grad and on_gpu(x) and C % 8 == 0 \
+        elif relu and residual is None and need_grad and fused_gpu(x) and C % 8 == 0 \
                 and gradjoin.STATS_ENABLED:
             # ReLU without a bit mask: a consuming depthwise dgrad masks by y > 0 itself
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(None, x, relu_y=True)

@@ -19,6 +19,14 @@ def on_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+def fused_gpu(t: torch.Tensor) -> bool:
+    """A GPU tensor on the bf16 fast path: the fused epilogue features (ReLU bit masks, BN-backward
+    statistics in the consumer's dgrad, fp8 side outputs) apply.  fp32 GPU tensors — the
+    reference-precision path (``--dtype fp32``) — run the plain fp32 kernels
+    (``csrc/kernels/f32.hip``), which take none of those fusions."""
+    return t.is_cuda and t.dtype != torch.float32
+
+
 def ext():
     return _native.ext()
 

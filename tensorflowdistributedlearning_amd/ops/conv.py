@@ -21,7 +21,7 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
-from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view
+from .common import on_gpu, fused_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view
 from . import workspace
 from . import streams
 from . import gradjoin
@@ -415,14 +415,14 @@ class _Conv2dFn(torch.autograd.Function):
                     return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,
                                       mask=mask)
             join = ctx.join
-            masks_ok = on_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
+            masks_ok = fused_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
             stats_ok = masks_ok and not fp8_dg  # (the kernel decides; strided: parity classes)
             if join is None:
                 tok = ctx.bn_tok
                 # a statistics-only token (BN without ReLU) needs no 64-channel mask slabs
                 if tok is not None and tok.relu_y:
                     tok = None  # a ReLU without bit mask: only the depthwise dgrad applies it
-                if tok is not None and (masks_ok or (on_gpu(dy) and tok.mask is None)):
+                if tok is not None and (masks_ok or (fused_gpu(dy) and tok.mask is None)):
                     # sole consumer of a masked BN output: apply the mask here, and fuse the BN's
                     # backward statistics when the kernel can (ops/gradjoin.py)
                     if (stats_ok or tok.mask is None) and not fp8_dg and tok.x is not None \

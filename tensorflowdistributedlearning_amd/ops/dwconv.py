@@ -41,8 +41,9 @@ DW_STATS = os.environ.get("TDL_DW_STATS", "0") == "1"
 
 
 def _fusable_relu_in(x, R, S):
-    """The kernels fold an input ReLU into their loads for 3×3 filters on 8-channel vectors."""
-    return x.shape[-1] % 8 == 0 and R * S == 9
+    """The bf16 kernels fold an input ReLU into their loads for 3×3 filters on 8-channel vectors
+    (the fp32 path applies it as a separate pass)."""
+    return x.shape[-1] % 8 == 0 and R * S == 9 and x.dtype != torch.float32
 
 
 class _DwConvFn(torch.autograd.Function):

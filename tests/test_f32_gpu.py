@@ -1,0 +1,256 @@
+"""The fp32 GPU path (``csrc/kernels/f32.hip`` + the fp32 instantiations of the pooling /
+upsample kernels): every kernel against a plain PyTorch fp32 reference of the same op, and the
+reference DeepLab preset trained in fp32 on the GPU against the CPU fp32 oracle.
+
+The reference trains in fp32 (no dtype option in /root/reference/model.py), so this is the path
+its published speed (Test.ipynb:212-213) is compared with; tolerances are fp32 summation-order
+tight, not bf16 loose."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tensorflowdistributedlearning_amd import models
+from tensorflowdistributedlearning_amd.engine.trainer import Trainer
+from tensorflowdistributedlearning_amd.ops import conv as C
+from tensorflowdistributedlearning_amd.ops import bn as B
+from tensorflowdistributedlearning_amd.ops import pool as P
+from tensorflowdistributedlearning_amd.ops import dwconv as D
+from tensorflowdistributedlearning_amd.ops import upsample as U
+from tensorflowdistributedlearning_amd.ops import lovasz_hinge
+from tensorflowdistributedlearning_amd.ops.common import ext
+from tensorflowdistributedlearning_amd.data.synthetic import segmentation_batch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+# (N, H, W, C, K, R, S, stride, pad(t,b,l,r), dil) — every channel count % 4 == 0
+F32_SHAPES = [
+    (2, 14, 14, 64, 64, 3, 3, 1, (1, 1, 1, 1), 1),
+    (2, 14, 14, 64, 256, 1, 1, 1, (0, 0, 0, 0), 1),
+    (2, 15, 15, 128, 132, 3, 3, 2, (1, 1, 1, 1), 1),      # odd size, K % 128 != 0
+    (2, 16, 16, 8, 64, 3, 3, 2, (0, 1, 0, 1), 1),         # TF SAME asymmetric s2, 8-ch stem
+    (2, 13, 13, 64, 36, 3, 3, 1, (4, 4, 4, 4), 4),        # dilated r4
+    (3, 1, 1, 200, 100, 1, 1, 1, (0, 0, 0, 0), 1),        # pooled-branch shape, ragged tiles
+    (2, 13, 13, 264, 264, 3, 3, 1, (1, 1, 1, 1), 1),      # preset block2 (258 padded to 264)
+    (2, 9, 9, 40, 8, 3, 3, 1, (1, 1, 1, 1), 1),           # decoder logit conv (1 padded to 8)
+    (2, 13, 13, 24, 16, 3, 3, 2, (2, 2, 2, 2), 2),        # stride 2 + dilation 2
+    (2, 11, 12, 16, 20, 1, 1, 2, (0, 0, 0, 0), 1),        # 1x1 s2 on odd/even sizes
+    (16, 26, 26, 128, 128, 3, 3, 1, (1, 1, 1, 1), 1),     # many tiles + split-K wgrad
+]
+
+
+@pytest.mark.parametrize("shape", F32_SHAPES)
+def test_conv_f32_fwd_dgrad_wgrad(gpu, shape):
+    N, H, W, Ci, K, R, S, st, pad, dil = shape
+    g = C.ConvGeom((st, st), pad, (dil, dil))
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, Ci)
+    w = torch.randn(K, R, S, Ci) / (R * S * Ci) ** 0.5
+    Ho, Wo = g.out_hw(H, W, R, S)
+    dy = torch.randn(N, Ho, Wo, K)
+    xg, wg, dyg = x.to(gpu), w.to(gpu), dy.to(gpu)
+    y = C.conv_fwd(xg, wg, g)
+    assert y.dtype == torch.float32
+    assert rel_err(y, C.ref_conv_fwd(x, w, g)) < TOL
+    dx = C.conv_dgrad(dyg, wg, tuple(x.shape), g)
+    assert rel_err(dx, C.ref_conv_dgrad(dy, w, tuple(x.shape), g)) < TOL
+    dw = C.conv_wgrad(dyg, xg, tuple(w.shape), g)
+    assert rel_err(dw, C.ref_conv_wgrad(dy, x, tuple(w.shape), g)) < TOL
+
+
+def test_conv_f32_epilogues(gpu):
+    """bias + residual + ReLU + BN statistics in the forward epilogue; dgrad accumulate (join);
+    wgrad accumulate + bias gradient."""
+    torch.manual_seed(1)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    x = torch.randn(4, 13, 13, 64)
+    w = torch.randn(128, 3, 3, 64) * 0.05
+    b = torch.randn(128)
+    res = torch.randn(4, 13, 13, 128)
+    stats = torch.zeros(2, 128, device=gpu)
+    y = C.conv_fwd(x.to(gpu), w.to(gpu), g, bias=b.to(gpu), relu=True, stats=stats,
+                   residual=res.to(gpu))
+    ref = torch.relu(C.ref_conv_fwd(x, w, g, b) + res)
+    assert rel_err(y, ref) < TOL
+    rf = ref.reshape(-1, 128)
+    assert rel_err(stats[0], rf.sum(0)) < 1e-4 and rel_err(stats[1], (rf * rf).sum(0)) < 1e-4
+    dy = torch.randn(4, 13, 13, 128)
+    prev = torch.randn(4, 13, 13, 64)
+    out = prev.to(gpu)
+    C.conv_dgrad(dy.to(gpu), w.to(gpu), tuple(x.shape), g, out=out, accumulate=True)
+    assert rel_err(out, prev + C.ref_conv_dgrad(dy, w, tuple(x.shape), g)) < TOL
+    dw0 = torch.randn(128, 3, 3, 64)
+    dwg = dw0.to(gpu)
+    bg = torch.full((128,), 7.0, device=gpu)
+    C.conv_wgrad(dy.to(gpu), x.to(gpu), tuple(w.shape), g, out=dwg, accumulate=True, bias_grad=bg)
+    assert rel_err(dwg, dw0 + C.ref_conv_wgrad(dy, x, tuple(w.shape), g)) < TOL
+    assert rel_err(bg, dy.reshape(-1, 128).sum(0)) < 1e-5
+
+
+def _coef(C_, dev):
+    torch.manual_seed(2)
+    scale = torch.rand(C_) + 0.5
+    shift = torch.randn(C_) * 0.1
+    mean = torch.randn(C_) * 0.1
+    inv = torch.rand(C_) + 0.5
+    return torch.stack([scale, shift, mean, inv]).to(dev)
+
+
+@pytest.mark.parametrize("Cn", [8, 64, 264, 1024])
+def test_bn_f32_kernels(gpu, Cn):
+    torch.manual_seed(3)
+    x = torch.randn(3, 9, 11, Cn)
+    st = B.bn_stats(x.to(gpu))
+    xf = x.reshape(-1, Cn)
+    assert rel_err(st[0], xf.sum(0)) < 1e-4 and rel_err(st[1], (xf * xf).sum(0)) < 1e-4
+    coef = _coef(Cn, gpu)
+    cc = coef.cpu()
+    res = torch.randn_like(x)
+    y = B.bn_apply(x.to(gpu), coef, res.to(gpu), relu=True)
+    assert rel_err(y, B.bn_apply(x, cc, res, relu=True)) < TOL
+    # strided destination (a channel slice of a wider concat buffer)
+    buf = torch.zeros(3, 9, 11, 2 * Cn, device=gpu)
+    B.bn_apply(x.to(gpu), coef, None, relu=True, out=buf[..., Cn:])
+    assert rel_err(buf[..., Cn:], B.bn_apply(x, cc, None, relu=True)) < TOL
+    assert float(buf[..., :Cn].abs().max()) == 0.0
+    dy = torch.randn_like(x)
+    yc = B.bn_apply(x, cc, None, relu=True)
+    for relu in (0, 1, 2):
+        yy = yc if relu == 1 else None
+        red = B.bn_bwd_reduce(dy.to(gpu), None if yy is None else yy.to(gpu), x.to(gpu), coef,
+                              relu)
+        rc = B.bn_bwd_reduce(dy, yy, x, cc, relu)
+        assert rel_err(red, rc) < 1e-4, relu
+        gam = torch.rand(Cn) + 0.5
+        dadd = torch.randn_like(x)
+        dg = torch.zeros(Cn, device=gpu)
+        db = torch.zeros(Cn, device=gpu)
+        dx, dres = B.bn_bwd_apply(dy.to(gpu), None if yy is None else yy.to(gpu), x.to(gpu),
+                                  coef, rc.to(gpu), gam.to(gpu), 40.0, relu, True, dg, db,
+                                  dadd=dadd.to(gpu))
+        dxc, dresc = B.bn_bwd_apply(dy, yy, x, cc, rc, gam, 40.0, relu, True, dadd=dadd)
+        assert rel_err(dx, dxc) < TOL and rel_err(dres, dresc) < TOL, relu
+        assert rel_err(dg, rc[1]) < 1e-6 and rel_err(db, rc[0]) < 1e-6
+    # strided dy (the concat-free head's slice of the concat gradient)
+    gb = torch.randn(3, 9, 11, 2 * Cn)
+    dys = gb[..., :Cn]
+    red = B.bn_bwd_reduce(gb.to(gpu)[..., :Cn], None, x.to(gpu), coef, 2)
+    rc = B.bn_bwd_reduce(dys.contiguous(), None, x, cc, 2)
+    assert rel_err(red, rc) < 1e-4
+
+
+def test_pool_upsample_dw_f32(gpu):
+    torch.manual_seed(4)
+    x = torch.randn(2, 15, 17, 64)
+    pad = (0, 1, 1, 1)
+    xg = x.to(gpu).requires_grad_(True)
+    xc = x.clone().requires_grad_(True)
+    yg = P.max_pool2d(xg, 3, 2, pad)
+    yc = P.max_pool2d(xc, 3, 2, pad)
+    assert yg.dtype == torch.float32 and rel_err(yg, yc) == 0.0
+    dy = torch.randn_like(yc)
+    yg.backward(dy.to(gpu))
+    yc.backward(dy)
+    assert rel_err(xg.grad, xc.grad) < TOL
+    a = P.global_avg_pool(x.to(gpu), keepdims=True)
+    assert rel_err(a, x.mean(dim=(1, 2), keepdim=True)) < 1e-5
+    # upsample into a channel slice + backward
+    s = torch.randn(2, 5, 6, 16)
+    sg = s.to(gpu).requires_grad_(True)
+    sc = s.clone().requires_grad_(True)
+    ug, uc = U.upsample(sg, (13, 11)), U.upsample(sc, (13, 11))
+    assert rel_err(ug, uc) < TOL
+    du = torch.randn_like(uc)
+    ug.backward(du.to(gpu))
+    uc.backward(du)
+    assert rel_err(sg.grad, sc.grad) < TOL
+    # depthwise 3x3, dilation 2, bias + ReLU: forward, dgrad, wgrad
+    w = torch.randn(3, 3, 64) * 0.3
+    b = torch.randn(64) * 0.1
+    g = C.ConvGeom((1, 1), (2, 2, 2, 2), (2, 2))
+    wg_ = w.to(gpu).requires_grad_(True)
+    bg_ = b.to(gpu).requires_grad_(True)
+    wc_ = w.clone().requires_grad_(True)
+    bc_ = b.clone().requires_grad_(True)
+    xg = x.to(gpu).requires_grad_(True)
+    xc = x.clone().requires_grad_(True)
+    dg = D.depthwise_conv2d(xg, wg_, bg_, g, relu=True)
+    dc = D.depthwise_conv2d(xc, wc_, bc_, g, relu=True)
+    assert rel_err(dg, dc) < TOL
+    dd = torch.randn_like(dc)
+    dg.backward(dd.to(gpu))
+    dc.backward(dd)
+    assert rel_err(xg.grad, xc.grad) < TOL
+    assert rel_err(wg_.grad, wc_.grad) < 1e-4 and rel_err(bg_.grad, bc_.grad) < 1e-4
+
+
+def _deeplab_pair(gpu, train_mode, lr=0.0):
+    mc = models.DeepLabResNet(model_name="m", input_shape=(101, 101))
+    mg = models.DeepLabResNet(model_name="m", input_shape=(101, 101))
+    mg.load_state_dict(mc.state_dict())
+    tc = Trainer(mc, lovasz_hinge, "cpu", "adam", dict(lr=lr), lowp_dtype=None)
+    tg = Trainer(mg, lovasz_hinge, gpu, "adam", dict(lr=lr), lowp_dtype=None)
+    with torch.no_grad():
+        tg.flat.master.copy_(tc.flat.master.to(gpu))
+    tc.train_mode = tg.train_mode = train_mode
+    return tc, tg
+
+
+@pytest.mark.timeout(300)
+def test_deeplab_fp32_gpu_matches_cpu_oracle(gpu):
+    """The reference preset in fp32 on the GPU (every op on the fp32 kernels) vs the CPU fp32
+    oracle, frozen BN: logits, loss and the full gradient agree to fp32 summation order."""
+    torch.manual_seed(6)
+    tc, tg = _deeplab_pair(gpu, train_mode=False)
+    x, y = segmentation_batch(2, dtype=torch.float32)
+    lc, oc = tc.train_step(x, y)
+    lg, og = tg.train_step(x.to(gpu), y.to(gpu))
+    assert og.dtype == torch.float32
+    cs = torch.nn.functional.cosine_similarity
+    co = cs(oc.flatten().double(), og.cpu().flatten().double(), dim=0).item()
+    cg = cs(tc.flat.grad.double(), tg.flat.grad.cpu().double(), dim=0).item()
+    print(f"fp32: logits cos {co:.7f} rel {rel_err(og, oc):.2e} loss {float(lc):.6f} / "
+          f"{float(lg):.6f} grad cos {cg:.7f}")
+    assert rel_err(og, oc) < 1e-3
+    assert abs(float(lc) - float(lg)) < 1e-4 * max(1.0, abs(float(lc)))
+    assert cg > 0.9999, cg
+
+
+@pytest.mark.timeout(400)
+def test_deeplab_fp32_training_curve_matches_oracle(gpu):
+    """20 Adam steps with batch statistics on one fixed batch, fp32 GPU vs fp32 CPU from
+    identical weights: the curves coincide (no bf16 rounding on either side)."""
+    torch.manual_seed(11)
+    tc, tg = _deeplab_pair(gpu, train_mode=True, lr=5e-4)
+    x, y = segmentation_batch(8, dtype=torch.float32, seed=3)
+    xg, yg = x.to(gpu), y.to(gpu)
+    fc, fg = [], []
+    for _ in range(20):
+        fc.append(float(tc.train_step(x, y)[0]))
+        fg.append(float(tg.train_step(xg, yg)[0]))
+    print("fp32 cpu", [round(v, 4) for v in fc[::2]])
+    print("fp32 gpu", [round(v, 4) for v in fg[::2]])
+    assert abs(fc[0] - fg[0]) < 1e-4 * fc[0]
+    assert fg[-1] < 0.9 * fg[0]
+    assert max(abs(a - b) for a, b in zip(fc[:10], fg[:10])) < 0.02 * fc[0]
+
+
+def test_fp32_rejects_fused_requests(gpu):
+    """fp32 tensors never reach a bf16-only fusion silently: the BN forward writes no bit mask /
+    token, and a fused request fails loudly in the binding."""
+    x = torch.randn(2, 4, 4, 64, device=gpu)
+    mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+    coef = _coef(64, gpu)
+    with pytest.raises(RuntimeError):
+        ext().bn_apply(x, coef, None, torch.empty_like(x), True, mask=mask)
+    with pytest.raises(RuntimeError):
+        ext().conv_fwd(x, torch.randn(64, 1, 1, 62, device=gpu), torch.empty(2, 4, 4, 64, device=gpu),
+                       None, None, 1, 1, 0, 0, 1, 1, False)
