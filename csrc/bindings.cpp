@@ -609,6 +609,15 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
 
 // ---------------------------------------------------------------------------------- elementwise
 void row_pack(Tensor x, Tensor t, int64_t creal, int64_t S, int64_t sw, int64_t pl) {
+  if (is_f32(x)) {
+    CHECK_T(x, torch::kFloat32);
+    CHECK_T(t, torch::kFloat32);
+    TORCH_CHECK(x.dim() == 4 && t.dim() == 4 && t.size(0) == x.size(0) && t.size(1) == x.size(1) &&
+                t.size(3) >= S * creal && creal <= x.size(3), "row_pack: x [N,H,W,Cx], t [N,H,Wo,Cp]");
+    row_pack_f32_launch(F32(x), F32(t), x.size(0), x.size(1), x.size(2), x.size(3), creal, S, sw, pl,
+                        t.size(2), t.size(3), stream());
+    return;
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(t, torch::kBFloat16);
   TORCH_CHECK(x.dim() == 4 && t.dim() == 4 && t.size(0) == x.size(0) && t.size(1) == x.size(1) &&
@@ -1228,6 +1237,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "conv kernel selection: 0 register-staged only, 1 LDS-DMA for large problems (default), "
         "2 LDS-DMA whenever aligned, -1 environment (TDL_CONV_GLDS)");
   m.def("conv_glds_mode", &conv_glds_mode);
+  m.def("conv_set_m32", &conv_set_m32, "32x32x16-MFMA K loop for KC-operand LDS-DMA convs (-1: env)");
+  m.def("conv_m32", &conv_m32);
   m.def("fastdiv", [](uint32_t d) { auto f = make_fastdiv(d); return py::make_tuple(f.m, f.s); },
         "magic (m, s) with n / d == (n * m) >> s for 0 <= n < 2^31");
   m.def("rccl_unique_id", []() { return py::bytes(comm::get_unique_id()); });

@@ -105,9 +105,38 @@ __device__ __forceinline__ void dma16(rsrc_t r, char* lds_base, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_base, 16, voff, 0, 0, 0);
 }
 
+// 32×32 accumulator blocks (v_mfma_f32_32x32x16_bf16, operands swapped like the 16×16 form:
+// row = output column n, col = output row m) → the 16×16 layout the shared epilogue takes.
+// Lane l of a 32×32 block holds m = l&31, n = 8g + 4(l>>5) + i in register 4g + i; the 16×16
+// sub-block (mm, nn) wants lane 16q + p to hold m = 16mm + p, n = 16nn + 4q + i, i.e. register
+// 8nn + 4(q>>1) + i of lane 32(q&1) + 16mm + p.  Per register pair (8nn + i, 8nn + 4 + i) one
+// v_permlane32_swap then one v_permlane16_swap produce the two target fragments (mm = 0, 1).
+template <int QM, int QN>
+__device__ __forceinline__ void acc32_to_16(const f32x16 (&c)[QM][QN], f32x4 (&acc)[2 * QM][2 * QN]) {
+#pragma unroll
+  for (int qm = 0; qm < QM; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < QN; ++qn)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(c[qm][qn][8 * nn + i]),
+                                                          __float_as_uint(c[qm][qn][8 * nn + 4 + i]),
+                                                          false, false);
+          const auto u = __builtin_amdgcn_permlane16_swap(t[0], t[1], false, false);
+          acc[2 * qm][2 * qn + nn][i] = __uint_as_float(u[0]);
+          acc[2 * qm + 1][2 * qn + nn][i] = __uint_as_float(u[1]);
+        }
+}
+
 template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, int FK,
-          bool FP8 = false, bool NJ = false, bool FRES = false>
+          bool FP8 = false, bool NJ = false, bool FRES = false, bool M32 = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  // M32: the K loop runs v_mfma_f32_32x32x16_bf16 on 32×32 blocks (half the MFMA instructions
+  // and half the vector-issue hold per FLOP of the 16×16×32 form); accumulators are re-laid to
+  // the 16×16 fragment layout (acc32_to_16) before the shared epilogue.  Both operands must be
+  // K-contiguous (KC) LDS images: FWD, and DGRAD with transposed weights.
   // FRES (FWD): residual a.res added in the epilogue before the ReLU (conv_common.h)
   // NJ (DGRAD): no residual join (a.beta == 0) — the epilogue's previous-dx registers are not
   // allocated (the fused-statistics dgrad needs them for the BN input x instead)
@@ -135,6 +164,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   constexpr int NW = WM * WN, NT = 64 * NW;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
   constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE == WGRAD) || (MODE == DGRAD && !WT);
+  static_assert(!M32 || (!A_MC && !B_MC && !FP8), "32x32 blocks: KC operands, bf16");
+  constexpr int QM = (BM / WM) / 32 > 0 ? (BM / WM) / 32 : 1, QN = (BN / WN) / 32 > 0 ? (BN / WN) / 32 : 1;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int IA = A_BYTES / (1024 * NW), IB = B_BYTES / (1024 * NW);
   static_assert(IA * 1024 * NW == A_BYTES && IB * 1024 * NW == B_BYTES, "tile / wave mismatch");
@@ -422,17 +453,42 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   };
 
   f32x4 acc[RM][RN];
+  f32x16 acc32[QM][QN];
   auto zero_acc = [&]() {
+    if constexpr (M32) {
 #pragma unroll
-    for (int i = 0; i < RM; ++i)
+      for (int i = 0; i < QM; ++i)
 #pragma unroll
-      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < QN; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc32[i][j][v] = 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   };
 
   const uint32_t smem_lds = (uint32_t)(size_t)(lds_char_t*)smem;
   const bool no_reads = DBG & 16, no_barrier = DBG & 32, no_dma = DBG & 64;
   auto load_frags = [&](uint32_t As, uint32_t Bs, int kk, bf16x8(&af)[RM], bf16x8(&bfg)[RN]) {
     if (no_reads) return;
+    if constexpr (M32) {
+      // half-step kk = 16-deep slices 2kk, 2kk+1; lane l reads k-chunk 4kk + 2s + (l>>5) of row
+      // l&31 (A and B alike: any k permutation shared by both operands is exact)
+#pragma unroll
+      for (int q = 0; q < QM; ++q)
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl)
+          af[2 * q + sl] = lds_read_kc(As, wm * TM + q * 32 + (lane & 31), kk * 4 + sl * 2 + (lane >> 5));
+#pragma unroll
+      for (int q = 0; q < QN; ++q)
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl)
+          bfg[2 * q + sl] = lds_read_kc(Bs, wn * TN + q * 32 + (lane & 31), kk * 4 + sl * 2 + (lane >> 5));
+      return;
+    }
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm) {
       const int row = wm * TM + rm * 16;
@@ -458,6 +514,17 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       for (int rm = 0; rm < RM; ++rm) asm volatile("" ::"v"(af[rm]));
 #pragma unroll
       for (int rn = 0; rn < RN; ++rn) asm volatile("" ::"v"(bfg[rn]));
+      return;
+    }
+    if constexpr (M32) {
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+        for (int qm = 0; qm < QM; ++qm)
+#pragma unroll
+          for (int qn = 0; qn < QN; ++qn)
+            acc32[qm][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[2 * qn + sl], af[2 * qm + sl],
+                                                                    acc32[qm][qn], 0, 0, 0);
       return;
     }
 #pragma unroll
@@ -492,6 +559,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         }
       }
     } else {
+      if constexpr (M32) acc32_to_16<QM, QN>(acc32, acc);
       store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES>(
           a, T, acc, wm, wn, lane, rout, out_scale, no_epi_mem, s_sum, s_sq);
     }
@@ -726,9 +794,9 @@ constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, int FK,
-          bool F8 = false, bool NJ = false, bool FRES = false>
+          bool F8 = false, bool NJ = false, bool FRES = false, bool M32 = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES>;
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES, M32>;
   constexpr int lds = lds_bytes(BM, BN, WM, ST);
   static bool attr = false;
   if (!attr) {
@@ -823,6 +891,12 @@ int conv_glds_mode() {
   return g_glds_override >= 0 ? g_glds_override : m;
 }
 void conv_set_glds_mode(int mode) { g_glds_override = mode; }
+static int g_m32_override = -1;
+int conv_m32() {
+  static int m = env_int("TDL_M32", 0);
+  return g_m32_override >= 0 ? g_m32_override : m;
+}
+void conv_set_m32(int on) { g_m32_override = on; }
 
 bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int mode = conv_glds_mode();
@@ -885,6 +959,17 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
     else if (fk == 2) TDL_R(2);
     else TDL_R(0);
 #undef TDL_R
+    return true;
+  }
+  // TDL_M32=1: the 256×128 FASTK forward on 32×32×16 MFMA blocks (A/B: tools/m32_ab.py)
+  if (conv_m32() && fk == 1 && cfg == 0) {
+    if (bias) {
+      if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, true, 1, false, false, false, true>(a, blocks, st);
+      else launch_g<FWD, 256, 128, 4, 2, 3, false, true, 1, false, false, false, true>(a, blocks, st);
+    } else {
+      if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, false, false, true>(a, blocks, st);
+      else launch_g<FWD, 256, 128, 4, 2, 3, false, false, 1, false, false, false, true>(a, blocks, st);
+    }
     return true;
   }
   if (fk == 1) TDL_G(1);
@@ -986,7 +1071,10 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
       launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, 1, true>(a, blocks, st);
   } else if (a.K % 64 == 0 && a.w_t) {  // transposed weights: KC B operand
     a.w = a.w_t;
-    launch_gcfg<DGRAD, false, false, 3>(a, cfg, blocks, st);
+    if (conv_m32() && cfg == 0)
+      launch_g<DGRAD, 256, 128, 4, 2, 3, false, false, 3, false, false, false, true>(a, blocks, st);
+    else
+      launch_gcfg<DGRAD, false, false, 3>(a, cfg, blocks, st);
   } else if (a.K % 64 == 0) {
     launch_gcfg<DGRAD, false, false, 1>(a, cfg, blocks, st);
   } else if (a.R * a.S == 1 && a.ncls == 1) {  // ragged FASTK (see conv_fwd_glds)

@@ -24,8 +24,6 @@
 namespace tdl {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
 constexpr int CT = 256;             // conv workgroup: 4 waves in a 2×2 grid, 64×64 outputs each
 constexpr int BM = 128, BN = 128, BK = 16;
 constexpr int LDP = 128 + 4;        // LDS row = one k: rows k and k+8 land 32 banks apart
@@ -539,9 +537,30 @@ __global__ void __launch_bounds__(256) dw_wgrad_f32(DwF32Args a, int cvb) {
   }
 }
 
+// row packing of a few-channel image for its k×k stem conv (elementwise.hip row_pack_kernel's
+// fp32 form): t[n][h][wo][e] = x[n][h][wo·sw − pl + e / Cr][e % Cr] for e < S·Cr, zero elsewhere
+__global__ void __launch_bounds__(256) row_pack_f32(const float* __restrict__ x,
+                                                    float* __restrict__ t, long n, int W, int Cx,
+                                                    int Cr, int S, int sw, int pl, int Wo, int Cp) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long row = i / Cp;
+    const int e = (int)(i - row * Cp);
+    const int wo = (int)(row % Wo);
+    const long nh = row / Wo;
+    const int s = e / Cr, c = e - s * Cr, wi = wo * sw - pl + s;
+    t[i] = s < S && (unsigned)wi < (unsigned)W ? x[(nh * W + wi) * Cx + c] : 0.f;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------ launchers
+void row_pack_f32_launch(const float* x, float* t, int N, int H, int W, int Cx, int Cr, int S,
+                         int sw, int pl, int Wo, int Cp, hipStream_t st) {
+  const long n = (long)N * H * Wo * Cp;
+  hipLaunchKernelGGL(row_pack_f32, dim3(eblocks(n)), dim3(256), 0, st, x, t, n, W, Cx, Cr, S, sw, pl,
+                     Wo, Cp);
+}
 static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
   int M, Ng, nq, cch = 1;
   if (mode == C_FWD) {

@@ -92,6 +92,10 @@ void conv_wgrad_launch(const ConvArgs& a, const WgradPlan& p, float* out, bool a
 // LDS-DMA pipelined kernels (conv_glds.hip); false / 0 = not eligible, use the register-staged one
 int conv_glds_mode();
 void conv_set_glds_mode(int mode);  // -1: environment / default
+// 32×32×16-MFMA K loop for the KC-operand LDS-DMA convs (FWD FASTK, DGRAD with W^T): TDL_M32 /
+// override (-1: environment)
+int conv_m32();
+void conv_set_m32(int on);
 bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
 // *fused: set to whether a.stats was filled (stride-1 FASTK problems only)
 bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st, bool* fused = nullptr);
@@ -273,6 +277,8 @@ void bn_bwd_apply_f32_launch(const float* dy, const float* y, const float* x, co
                              const float* red, const float* gamma, float* dx, float* dres,
                              float* dgamma, float* dbeta, const float* dadd, long M, int C,
                              float count, int relu, long ldd, hipStream_t st);
+void row_pack_f32_launch(const float* x, float* t, int N, int H, int W, int Cx, int Cr, int S,
+                         int sw, int pl, int Wo, int Cp, hipStream_t st);
 void relu_bwd_f32_launch(const float* dy, const float* y, float* dx, long n, hipStream_t st);
 void add_act_f32_launch(const float* a, const float* b, float* y, long n, bool relu,
                         hipStream_t st);

@@ -725,6 +725,43 @@ def test_conv_dgrad_transposed_weights(gpu, shape):
     assert torch.equal(r0, r1)
 
 
+@pytest.mark.parametrize("shape", [(8, 14, 14, 256, 256, 3, 1, (1, 1, 1, 1)),
+                                   (16, 14, 14, 1024, 256, 1, 1, (0, 0, 0, 0)),
+                                   (8, 15, 15, 128, 192, 3, 2, (1, 1, 1, 1))])
+def test_conv_m32_kloop(gpu, shape):
+    """The 32×32×16-MFMA K loop (TDL_M32, conv_glds_kernel M32: accumulators re-laid to the
+    16×16 fragment layout before the shared epilogue) vs the default 16×16×32 loop: forward with
+    bias + BN statistics and the transposed-weight dgrad.  The 16×16×32 instruction sums its 32
+    products in two 16-deep passes, so the two loops round identically: the outputs are equal."""
+    N, H, _, Cin, K, k, s, pad = shape
+    g = C.ConvGeom((s, s), pad, (1, 1))
+    torch.manual_seed(8)
+    x = torch.randn(N, H, H, Cin).bfloat16().to(gpu)
+    w = (torch.randn(K, k, k, Cin) * 0.05).bfloat16().to(gpu)
+    b = torch.randn(K, device=gpu)
+    Ho, Wo = g.out_hw(H, H, k, k)
+    dy = torch.randn(N, Ho, Wo, K).bfloat16().to(gpu)
+    wt = w.permute(1, 2, 3, 0).contiguous()
+    outs = []
+    ext().conv_set_glds_mode(2)
+    try:
+        for m32 in (0, 1):
+            ext().conv_set_m32(m32)
+            st = torch.zeros(2, K, device=gpu)
+            y = C.conv_fwd(x, w, g, bias=b, relu=True, stats=st)
+            dx = C.conv_dgrad(dy, w, (N, H, H, Cin), g, w_t=wt)
+            outs.append((y, st, dx))
+    finally:
+        ext().conv_set_m32(-1)
+        ext().conv_set_glds_mode(-1)
+    (y0, s0, d0), (y1, s1, d1) = outs
+    ref = torch.relu(C.ref_conv_fwd(x.cpu(), w.cpu(), g, b.cpu()))
+    assert rel_err(y1, ref) < 1e-2
+    assert rel_err(d1, C.ref_conv_dgrad(dy.cpu(), w.cpu(), (N, H, H, Cin), g)) < 1e-2
+    assert torch.equal(y0, y1) and torch.equal(d0, d1)
+    assert rel_err(s1, s0) < 1e-5
+
+
 def test_row_packed_stem_gpu(gpu):
     """The row-pack HIP kernel = its CPU oracle (bitwise), and the packed 7×7/s2 stem
     (RowPackedConv2d) = the plain conv on the 8-channel padded input: forward and dW on the GPU."""
