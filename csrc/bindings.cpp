@@ -107,8 +107,7 @@ static const float* opt_f32_like(const c10::optional<Tensor>& t, const Tensor& l
 static ConvF32Args conv_f32_args(int64_t N, int64_t H, int64_t W, int64_t C, int64_t K, int64_t R,
                                  int64_t S, int64_t Ho, int64_t Wo, int64_t sh, int64_t sw,
                                  int64_t ph, int64_t pw, int64_t dh, int64_t dw) {
-  check_c4(C, "conv input channels");
-  check_c4(K, "conv output channels");
+  check_c4(C, "conv input channels");  // (any output channel count)
   TORCH_CHECK(N * std::max(H * W, Ho * Wo) < (1LL << 31) && K * R * S * C < (1LL << 31),
               "fp32 conv: problem too large for 32-bit GEMM indices");
   ConvF32Args a{};

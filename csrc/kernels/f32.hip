@@ -32,6 +32,15 @@ enum { C_FWD = 0, C_DGRAD = 1, C_WGRAD = 2 };
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
+// 4 consecutive floats p[0..3] of which the first n are valid (n ≤ 0: none).  vec: the row
+// length is a multiple of 4 (aligned float4 loads); otherwise element loads (classifier heads
+// with a class count that is not a multiple of 4)
+__device__ __forceinline__ float4 ld4(const float* p, int n, bool vec) {
+  if (n <= 0) return f4zero();
+  if (vec) return *(const float4*)p;
+  return make_float4(p[0], n > 1 ? p[1] : 0.f, n > 2 ? p[2] : 0.f, n > 3 ? p[3] : 0.f);
+}
+
 // GEMM views (m = output row, n = output column, reduction in 16-deep K-steps q):
 //   FWD   m = output pixel, n = output channel, q = (tap r,s) × 16-channel chunk of C
 //   DGRAD m = input pixel,  n = input channel,  q = (tap r,s) × 16-channel chunk of K
@@ -102,8 +111,9 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
       const bool pv = a_ok && ho >= 0 && wo >= 0 && ho * a.sh == hn && wo * a.sw == wn_ &&
                       ho < Ho && wo < Wo;
       const float* src = a.dy + (((long)pa_n * Ho + ho) * Wo + wo) * K + k;
-      ra0 = pv && k < K ? *(const float4*)src : f4zero();
-      ra1 = pv && k + 8 < K ? *(const float4*)(src + 8) : f4zero();
+      const bool kv = (K & 3) == 0;
+      ra0 = pv ? ld4(src, K - k, kv) : f4zero();
+      ra1 = pv ? ld4(src + 8, K - k - 8, kv) : f4zero();
       const int kb = cq * BK + kr;
       const float* wsrc = a.w + (((long)kb * a.R + r) * S + s) * C + n0 + c4;
       const long kstride = (long)a.R * S * C * 8;
@@ -112,8 +122,9 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
     } else {
       const long P = (long)a.N * Ho * Wo;
       const long p0 = (long)q * BK + kr, p1 = p0 + 8;
-      ra0 = a_ok && p0 < P ? *(const float4*)(a.dy + p0 * K + m0 + c4) : f4zero();
-      ra1 = a_ok && p1 < P ? *(const float4*)(a.dy + p1 * K + m0 + c4) : f4zero();
+      const bool kv = (K & 3) == 0;
+      ra0 = p0 < P ? ld4(a.dy + p0 * K + m0 + c4, K - m0 - c4, kv) : f4zero();
+      ra1 = p1 < P ? ld4(a.dy + p1 * K + m0 + c4, K - m0 - c4, kv) : f4zero();
       const int HoWo = Ho * Wo;
       auto gather = [&](long p) -> float4 {
         if (!b_ok || p >= P) return f4zero();
@@ -314,6 +325,21 @@ void chan_reduce_launch(int mode, const float* a, const float* x, const float* y
   else
     hipLaunchKernelGGL(chan_reduce_f32<2>, grid, dim3(RT), 0, st, a, x, y, coef, out, M, C, lda, relu,
                        cvb);
+}
+
+// column sums for any column count: 64 columns × 4 row lanes per block, one atomic per column
+__global__ void __launch_bounds__(256) colsum_scalar_f32(const float* __restrict__ x,
+                                                         float* __restrict__ out, long M, int C,
+                                                         long ldx) {
+  __shared__ float red[256];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + tx;
+  float s = 0.f;
+  if (c < C)
+    for (long m = (long)blockIdx.x * 4 + ty; m < M; m += (long)gridDim.x * 4) s += x[m * ldx + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) unsafeAtomicAdd(out + c, s + red[64 + tx] + red[128 + tx] + red[192 + tx]);
 }
 
 inline int eblocks(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + 255) / 256)); }
@@ -600,7 +626,14 @@ void conv_f32_wgrad_launch(const ConvF32Args& a, hipStream_t st) {
 }
 
 void colsum_f32_launch(const float* x, float* out, long M, int C, long ldx, hipStream_t st) {
-  chan_reduce_launch(1, x, nullptr, nullptr, nullptr, out, M, C, ldx, 0, st);
+  if (C % 4 == 0 && ldx % 4 == 0) {
+    chan_reduce_launch(1, x, nullptr, nullptr, nullptr, out, M, C, ldx, 0, st);
+    return;
+  }
+  const int gy = (C + 63) / 64;
+  const long gx = std::max<long>(1, std::min<long>((M + 63) / 64, 256 / gy));
+  hipLaunchKernelGGL(colsum_scalar_f32, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, x, out, M,
+                     C, ldx);
 }
 void bn_stats_f32_launch(const float* x, float* stats, long M, int C, hipStream_t st) {
   chan_reduce_launch(0, x, nullptr, nullptr, nullptr, stats, M, C, C, 0, st);
