@@ -870,9 +870,12 @@ bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_
 
 // bn_x / bn_red (optional, together): also accumulate the BN-backward sums (Σg, Σg·bn_x) of the
 // stored dx (stride-1 3×3 tile kernel only; returns whether they were written)
+// dadd (optional, shaped like dx, may be dx itself): dx = dgrad + dadd — the residual-gradient
+// join (ops/gradjoin.py) of a tensor whose other consumer wrote its gradient first
 bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                   int64_t dh, int64_t dw, c10::optional<Tensor> mask_x,
-                  c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_red) {
+                  c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_red,
+                  c10::optional<Tensor> dadd) {
   if (is_f32(dy)) {
     CHECK_T(dy, torch::kFloat32);
     CHECK_T(w, torch::kFloat32);
@@ -880,6 +883,7 @@ bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
     TORCH_CHECK(!(mask_x.has_value() && mask_x->defined()), "fp32 depthwise: no fused input ReLU");
     DwF32Args a = dw_f32_args(dx, w, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
     a.dy = F32(dy); a.w = F32(w); a.out = F32(dx);
+    a.dadd = opt_f32_like(dadd, dx, "dwconv_dgrad dadd");
     dwconv_f32_dgrad_launch(a, stream());
     return false;
   }
@@ -889,6 +893,11 @@ bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
   DwArgs a = dw_args(dx, w, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
   a.dy = BF(dy); a.w = BF(w); a.out = BFW(dx);
   a.mask_x = optb(mask_x);
+  if (dadd.has_value() && dadd->defined()) {
+    CHECK_T(*dadd, torch::kBFloat16);
+    TORCH_CHECK(dadd->sizes() == dx.sizes(), "dwconv_dgrad dadd must be shaped like dx");
+    a.dadd = BF(*dadd);
+  }
   if (a.mask_x) {
     TORCH_CHECK(mask_x->sizes() == dx.sizes(), "mask_x must be shaped like dx");
     TORCH_CHECK(a.C % 8 == 0 && a.R * a.S == 9, "fused input ReLU: 3x3, C % 8 == 0");
@@ -905,7 +914,7 @@ bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
 }
 
 void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int64_t sh, int64_t sw,
-                  int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu_in) {
+                  int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu_in, bool accumulate) {
   if (is_f32(dy)) {
     CHECK_T(dy, torch::kFloat32);
     CHECK_T(x, torch::kFloat32);
@@ -914,6 +923,10 @@ void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int
     TORCH_CHECK(dwt.size(0) * dwt.size(1) <= 9, "fp32 depthwise weight gradient: up to 3x3 taps");
     DwF32Args a = dw_f32_args(x, dwt, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
     a.dy = F32(dy); a.x = F32(x); a.dwt = F32(dwt); a.db = optfw(db);
+    if (!accumulate) {
+      (void)hipMemsetAsync(a.dwt, 0, dwt.numel() * sizeof(float), stream());
+      if (a.db) (void)hipMemsetAsync(a.db, 0, a.C * sizeof(float), stream());
+    }
     dwconv_f32_wgrad_launch(a, stream());
     return;
   }
@@ -923,6 +936,7 @@ void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int
   TORCH_CHECK(dwt.size(0) * dwt.size(1) <= 49, "depthwise kernel up to 7x7");
   DwArgs a = dw_args(x, dwt, dy.size(1), dy.size(2), sh, sw, ph, pw, dh, dw);
   a.dy = BF(dy); a.x = BF(x); a.dw = dwt.data_ptr<float>(); a.db = optfw(db);
+  a.accum = accumulate;
   TORCH_CHECK(!relu_in || (a.C % 8 == 0 && a.R * a.S == 9), "fused input ReLU: 3x3, C % 8 == 0");
   a.relu_in = relu_in;
   const int slabs = dwconv_wgrad_slabs(a);
@@ -1228,8 +1242,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dwconv_dgrad", &dwconv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
         py::arg("mask_x") = py::none(), py::arg("bn_x") = py::none(),
-        py::arg("bn_red") = py::none());
-  m.def("dwconv_wgrad", &dwconv_wgrad);
+        py::arg("bn_red") = py::none(), py::arg("dadd") = py::none());
+  m.def("dwconv_wgrad", &dwconv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("db"),
+        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dwl"),
+        py::arg("relu_in"), py::arg("accumulate") = true);
   m.def("upsample_fwd", &upsample_fwd);
   m.def("upsample_bwd", &upsample_bwd);
   m.def("conv_set_glds_mode", &conv_set_glds_mode,

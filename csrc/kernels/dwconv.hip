@@ -27,6 +27,14 @@ __device__ __forceinline__ void mask_pos(float* acc, const bf16_t* xp) {
   for (int j = 0; j < 8; ++j) acc[j] = xv[j] > 0.f ? acc[j] : 0.f;
 }
 
+// residual-gradient join: acc += dadd (8 channels)
+__device__ __forceinline__ void add8(float* acc, const bf16_t* p) {
+  float v[8];
+  unpack8(*(const uint4*)p, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] += v[j];
+}
+
 template <int V>
 __device__ __forceinline__ void ldv(const bf16_t* p, float* f) {
   if constexpr (V == 8) unpack8(*(const uint4*)p, f);
@@ -105,7 +113,14 @@ __global__ void dw_dgrad_kernel(DwArgs a) {
         for (int j = 0; j < V; ++j) acc[j] += gv[j] * wv[j];
       }
     }
-    stv<V>(a.out + (((long)n * a.H + h) * a.W + w) * a.C + c, acc);
+    const long o = (((long)n * a.H + h) * a.W + w) * a.C + c;
+    if (a.dadd) {
+      float d[V];
+      ldv<V>(a.dadd + o, d);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += d[j];
+    }
+    stv<V>(a.out + o, acc);
   }
 }
 
@@ -271,6 +286,7 @@ __global__ void __launch_bounds__(NT) dw_dgrad_rows(DwArgs a, int lanes_c, int r
       for (int j = 0; j < 8; ++j) acc[j] += gv[j] * wv[k][j];
     }
     if (a.mask_x) mask_pos(acc, a.mask_x + ((long)row * a.W + w) * a.C + c);
+    if (a.dadd) add8(acc, a.dadd + ((long)row * a.W + w) * a.C + c);
     *(uint4*)(xrow + (long)w * a.C) = pack8(acc);
   }
 }
@@ -362,7 +378,8 @@ __global__ void __launch_bounds__(NT) dw_slide_kernel(const bf16_t* __restrict__
                                                       int Ho, int Wo, int C, int Ph, int Pw,
                                                       int relu, int lanes_c, int rpp, int seg,
                                                       int relu_in,
-                                                      const bf16_t* __restrict__ mask_x) {
+                                                      const bf16_t* __restrict__ mask_x,
+                                                      const bf16_t* __restrict__ dadd) {
   const int cv = C / 8;
   const int t = threadIdx.x, lc = t % lanes_c, pl = t / lanes_c;
   const int cvi = lc + blockIdx.y * lanes_c;
@@ -422,6 +439,7 @@ __global__ void __launch_bounds__(NT) dw_slide_kernel(const bf16_t* __restrict__
       for (int j = 0; j < 8; ++j) acc[j] = fmaxf(acc[j], 0.f);
     }
     if (mask_x) mask_pos(acc, mask_x + ((long)row * Wo + w) * C + c);
+    if (dadd) add8(acc, dadd + ((long)row * Wo + w) * C + c);
     *(uint4*)(orow + (long)w * C) = pack8(acc);
   }
 }
@@ -454,7 +472,8 @@ __global__ void __launch_bounds__(NT) dw_slide4_kernel(const bf16_t* __restrict_
                                                        int Ho, int Wo, int C, int Ph, int Pw,
                                                        int relu, int lanes_c, int rpp, int seg,
                                                        int relu_in,
-                                                       const bf16_t* __restrict__ mask_x) {
+                                                       const bf16_t* __restrict__ mask_x,
+                                                       const bf16_t* __restrict__ dadd) {
   // The window is kept unpacked (fp32 pairs), so a step converts only its new column, and the
   // FMAs run as packed fp32 pairs (v_pk_fma_f32).  (Measured alternatives, Xception-41 b128:
   // columns prefetched in blocks of 4 — 141 VGPRs, 3 waves — 2394 img/s; XCD-aware row order
@@ -536,6 +555,14 @@ __global__ void __launch_bounds__(NT) dw_slide4_kernel(const bf16_t* __restrict_
       o[2] = m1.x > 0.f ? o[2] : 0.f;
       o[3] = m1.y > 0.f ? o[3] : 0.f;
     }
+    if (dadd) {
+      const uint2 d = *(const uint2*)(dadd + ((long)row * Wo + w) * C + c);
+      const f32x2 d0 = lo_hi(d.x), d1 = lo_hi(d.y);
+      o[0] += d0.x;
+      o[1] += d0.y;
+      o[2] += d1.x;
+      o[3] += d1.y;
+    }
     *(uint2*)(orow + (long)w * C) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
   }
 }
@@ -565,7 +592,8 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
                                                      int tiles_w, int relu_in,
                                                      const bf16_t* __restrict__ mask_x,
                                                      float* __restrict__ stats,
-                                                     const bf16_t* __restrict__ bn_x, int ntiles) {
+                                                     const bf16_t* __restrict__ bn_x, int ntiles,
+                                                     const bf16_t* __restrict__ dadd) {
   // stats (optional, fp32 [2][C], accumulated): BN sums of the stored bf16 outputs — (Σy, Σy²)
   // for the BN that normalises this forward's output, or (Σg, Σg·bn_x) with bn_x the input of
   // the BN whose output gradient this dgrad produces (bn.hip red_raw) — so that BN skips its
@@ -649,6 +677,7 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
     }
     const long op = (((long)n * Ho + h0 + h) * Wo + w) * C + c;
     if (mask_x) mask_pos(o, mask_x + op);
+    if (dadd) add8(o, dadd + op);
     const uint4 packed = pack8(o);
     *(uint4*)(out + op) = packed;
     if (stats) {
@@ -911,20 +940,20 @@ bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
                        g.twn, a.relu_in, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
-                       ntiles);
+                       ntiles, (const bf16_t*)nullptr);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {
     const Slide4Geom g = slide4_geom(a.C / 4, a.Wo);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
     hipLaunchKernelGGL(dw_slide4_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.lanes_c, g.rpp, g.seg,
-                       a.relu_in, (const bf16_t*)nullptr);
+                       a.relu_in, (const bf16_t*)nullptr, (const bf16_t*)nullptr);
   } else if (slide_ok(a)) {
     const SlideGeom g = slide_geom(a.C / 8, a.Wo);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
     hipLaunchKernelGGL(dw_slide_kernel<false>, grid, dim3(NT), 0, st, a.x, a.w, a.bias, a.out, a.H,
                        a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.lanes_c, g.rpp, g.seg, a.relu_in,
-                       (const bf16_t*)nullptr);
+                       (const bf16_t*)nullptr, (const bf16_t*)nullptr);
   } else if (a.C % 8 == 0 && a.R * a.S == 9) {
     const RowGeom g = row_geom(a.C / 8);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
@@ -945,20 +974,20 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
     hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
-                       g.twn, 0, a.mask_x, a.stats, a.bn_x, ntiles);
+                       g.twn, 0, a.mask_x, a.stats, a.bn_x, ntiles, a.dadd);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const Slide4Geom g = slide4_geom(a.C / 4, a.W);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 4, g.lanes_c), (unsigned)g.gz);
     hipLaunchKernelGGL(dw_slide4_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.lanes_c, g.rpp, g.seg,
-                       0, a.mask_x);
+                       0, a.mask_x, a.dadd);
   } else if (slide_ok(a)) {  // stride-1 dgrad = forward of dy with the rotated filter, padding 2 − p
     const SlideGeom g = slide_geom(a.C / 8, a.W);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));
     hipLaunchKernelGGL(dw_slide_kernel<true>, grid, dim3(NT), 0, st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.lanes_c, g.rpp, g.seg, 0,
-                       a.mask_x);
+                       a.mask_x, a.dadd);
   } else if (a.C % 8 == 0 && a.R * a.S == 9) {
     const RowGeom g = row_geom(a.C / 8);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));
@@ -1000,9 +1029,13 @@ void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st) {
       hipLaunchKernelGGL(dw_wgrad_rows<9>, grid, dim3(NT), 0, st, a, g.lanes_c, g.rpp, rpb, ws_w,
                          ws_b);
     }
-    splitk_reduce_launch(ws_w, a.dw, 9L * a.C, slabs, true, st);
-    if (a.db) splitk_reduce_launch(ws_b, a.db, a.C, slabs, true, st);
+    splitk_reduce_launch(ws_w, a.dw, 9L * a.C, slabs, a.accum != 0, st);
+    if (a.db) splitk_reduce_launch(ws_b, a.db, a.C, slabs, a.accum != 0, st);
     return;
+  }
+  if (!a.accum) {  // the atomic kernels accumulate: overwrite = clear first
+    (void)hipMemsetAsync(a.dw, 0, sizeof(float) * a.R * a.S * a.C, st);
+    if (a.db) (void)hipMemsetAsync(a.db, 0, sizeof(float) * a.C, st);
   }
   if (a.C % 8 == 0 && (a.R * a.S == 9 || a.R * a.S == 1))
     wgrad_dispatch<8>(a, st);

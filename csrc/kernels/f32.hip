@@ -48,27 +48,33 @@ __device__ __forceinline__ float4 ld4(const float* p, int n, bool vec) {
 // Operand staging patterns (per K-step, 256 threads, 2 float4 loads per operand per thread):
 //   "row" operands (FWD A/B, DGRAD A): thread owns row t&127, loads k (t>>7)*4 and +8
 //   "col" operands (DGRAD B, WGRAD A/B): thread owns columns (t&31)*4..+3, loads k t>>5 and +8
-template <int MODE>
+// TBM: workgroup rows (128, or 64 for FWD / DGRAD problems with fewer than two 128-row tiles per
+// CU — the reference preset's 13×13 maps at batch 64 fill only 170 of 256 CUs with 128-row tiles)
+template <int MODE, int TBM = BM>
 __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int Ng, int nq,
                                                       int cch, int qps, int tiles_n) {
+  static_assert(TBM == 128 || (TBM == 64 && MODE != C_WGRAD), "row tile 128, or 64 (FWD / DGRAD)");
+  constexpr int FM = TBM / 64;  // 32×32 blocks per wave along M
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int l31 = lane & 31, hk = lane >> 5;
   const int tile = blockIdx.x;
-  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int m0 = (tile / tiles_n) * TBM, n0 = (tile % tiles_n) * BN;
   const int q0 = blockIdx.y * qps, q1 = min(nq, q0 + qps);
   const int H = a.H, W = a.W, C = a.C, K = a.K, S = a.S, Ho = a.Ho, Wo = a.Wo;
 
   // ---- per-thread loader state (fixed over the K loop)
   const int ri = t & 127, k4 = (t >> 7) * 4;       // "row" pattern
+  // the A operand's row pattern: TBM rows × 16 k (TBM 64: one float4 per thread, k 0/4/8/12)
+  const int ri_a = t & (TBM - 1), k4a = (t / TBM) * 4;
   const int kr = t >> 5, c4 = (t & 31) * 4;        // "col" pattern
   int pa_n = 0, pa_h = 0, pa_w = 0;                // A row pixel (FWD: output, DGRAD: input)
   bool a_ok = false, b_ok = false;
   int wr_r = 0, wr_s = 0, wr_c = 0;                // WGRAD: this thread's dW column (r, s, c)
   if (MODE == C_FWD || MODE == C_DGRAD) {
-    const int m = m0 + ri;
+    const int m = m0 + ri_a;
     a_ok = m < M;
     const int PW = MODE == C_FWD ? Wo : W, PH = MODE == C_FWD ? Ho : H;
     const int mm = a_ok ? m : 0;
@@ -93,19 +99,19 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
     if (MODE == C_FWD) {
       const int tap = q / cch, cq = q - tap * cch;
       const int r = tap / S, s = tap - r * S;
-      const int c = cq * BK + k4;
+      const int c = cq * BK + k4, ca = cq * BK + k4a;
       const int hi = pa_h * a.sh - a.ph + r * a.dh, wi = pa_w * a.sw - a.pw + s * a.dw;
       const bool pv = a_ok && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-      const float* src = a.x + (((long)pa_n * H + hi) * W + wi) * C + c;
-      ra0 = pv && c < C ? *(const float4*)src : f4zero();
-      ra1 = pv && c + 8 < C ? *(const float4*)(src + 8) : f4zero();
+      const float* src = a.x + (((long)pa_n * H + hi) * W + wi) * C + ca;
+      ra0 = pv && ca < C ? *(const float4*)src : f4zero();
+      if (TBM == 128) ra1 = pv && ca + 8 < C ? *(const float4*)(src + 8) : f4zero();
       const float* wsrc = a.w + (((long)(n0 + ri) * a.R + r) * S + s) * C + c;
       rb0 = b_ok && c < C ? *(const float4*)wsrc : f4zero();
       rb1 = b_ok && c + 8 < C ? *(const float4*)(wsrc + 8) : f4zero();
     } else if (MODE == C_DGRAD) {
       const int tap = q / cch, cq = q - tap * cch;
       const int r = tap / S, s = tap - r * S;
-      const int k = cq * BK + k4;
+      const int k = cq * BK + k4a;
       const int hn = pa_h + a.ph - r * a.dh, wn_ = pa_w + a.pw - s * a.dw;
       const int ho = hn >= 0 ? hn / a.sh : -1, wo = wn_ >= 0 ? wn_ / a.sw : -1;
       const bool pv = a_ok && ho >= 0 && wo >= 0 && ho * a.sh == hn && wo * a.sw == wn_ &&
@@ -113,7 +119,7 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
       const float* src = a.dy + (((long)pa_n * Ho + ho) * Wo + wo) * K + k;
       const bool kv = (K & 3) == 0;
       ra0 = pv ? ld4(src, K - k, kv) : f4zero();
-      ra1 = pv ? ld4(src + 8, K - k - 8, kv) : f4zero();
+      if (TBM == 128) ra1 = pv ? ld4(src + 8, K - k - 8, kv) : f4zero();
       const int kb = cq * BK + kr;
       const float* wsrc = a.w + (((long)kb * a.R + r) * S + s) * C + n0 + c4;
       const long kstride = (long)a.R * S * C * 8;
@@ -140,10 +146,12 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
   };
   auto store = [&](int buf) {
     if (MODE == C_FWD || MODE == C_DGRAD) {
-      As[buf][k4 + 0][ri] = ra0.x; As[buf][k4 + 1][ri] = ra0.y;
-      As[buf][k4 + 2][ri] = ra0.z; As[buf][k4 + 3][ri] = ra0.w;
-      As[buf][k4 + 8][ri] = ra1.x; As[buf][k4 + 9][ri] = ra1.y;
-      As[buf][k4 + 10][ri] = ra1.z; As[buf][k4 + 11][ri] = ra1.w;
+      As[buf][k4a + 0][ri_a] = ra0.x; As[buf][k4a + 1][ri_a] = ra0.y;
+      As[buf][k4a + 2][ri_a] = ra0.z; As[buf][k4a + 3][ri_a] = ra0.w;
+      if (TBM == 128) {
+        As[buf][k4a + 8][ri_a] = ra1.x; As[buf][k4a + 9][ri_a] = ra1.y;
+        As[buf][k4a + 10][ri_a] = ra1.z; As[buf][k4a + 11][ri_a] = ra1.w;
+      }
     } else {
       *(float4*)&As[buf][kr][c4] = ra0;
       *(float4*)&As[buf][kr + 8][c4] = ra1;
@@ -159,9 +167,9 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[FM][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -178,13 +186,15 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         // MFMA k-slot hk of step kk reads LDS row 8·hk + kk (same permutation for A and B)
-        const float* ar = &As[buf][8 * hk + kk][wm * 64 + l31];
+        const float* ar = &As[buf][8 * hk + kk][wm * (TBM / 2) + l31];
         const float* br = &Bs[buf][8 * hk + kk][wn * 64 + l31];
-        const float a0 = ar[0], a1 = ar[32], b0 = br[0], b1 = br[32];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        const float b0 = br[0], b1 = br[32];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+          const float av = ar[32 * fm];
+          acc[fm][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc[fm][0], 0, 0, 0);
+          acc[fm][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc[fm][1], 0, 0, 0);
+        }
       }
       if (more) store(buf ^ 1);
       __syncthreads();
@@ -199,10 +209,10 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
     float bias = 0.f;
     if (MODE == C_FWD && a.bias && col < K) bias = a.bias[col];
 #pragma unroll
-    for (int fm = 0; fm < 2; ++fm) {
+    for (int fm = 0; fm < FM; ++fm) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int row = m0 + wm * 64 + fm * 32 + (v & 3) + 8 * (v >> 2) + 4 * hk;
+        const int row = m0 + wm * (TBM / 2) + fm * 32 + (v & 3) + 8 * (v >> 2) + 4 * hk;
         float val = acc[fm][fn][v];
         if (MODE == C_FWD) {
           if (row < M && col < K) {
@@ -503,6 +513,10 @@ __global__ void __launch_bounds__(256) dw_dgrad_f32(DwF32Args a) {
         acc.x += g.x * wv.x; acc.y += g.y * wv.y; acc.z += g.z * wv.z; acc.w += g.w * wv.w;
       }
     }
+    if (a.dadd) {
+      const float4 d = ((const float4*)a.dadd)[i];
+      acc.x += d.x; acc.y += d.y; acc.z += d.z; acc.w += d.w;
+    }
     ((float4*)a.out)[i] = acc;
   }
 }
@@ -532,7 +546,7 @@ __global__ void __launch_bounds__(256) dw_wgrad_f32(DwF32Args a, int cvb) {
       acc[DW_MAXT].x += g.x; acc[DW_MAXT].y += g.y; acc[DW_MAXT].z += g.z; acc[DW_MAXT].w += g.w;
 #pragma unroll
       for (int j = 0; j < DW_MAXT; ++j) {
-        if (j >= T) break;
+        if (j >= T) continue;  // (no break: the loop must unroll or acc[] goes to scratch)
         const int r = j / a.S, s = j - r * a.S;
         const int hi = ho * a.sh - a.ph + r * a.dh, wi = wo * a.sw - a.pw + s * a.dwl;
         if ((unsigned)hi >= (unsigned)a.H || (unsigned)wi >= (unsigned)a.W) continue;
@@ -597,7 +611,13 @@ static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
     M = a.K; Ng = a.R * a.S * a.C; nq = (int)(((long)a.N * a.Ho * a.Wo + BK - 1) / BK);
   }
   if (M <= 0 || Ng <= 0 || nq <= 0) return;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (Ng + BN - 1) / BN;
+  int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = (Ng + BN - 1) / BN;
+  // fewer than two 128-row tiles per CU: 64-row tiles (twice the workgroups, each with half the
+  // work) — TDL_F32_BM64=0 turns it off
+  static const bool bm64_on = getenv("TDL_F32_BM64") == nullptr || atoi(getenv("TDL_F32_BM64"));
+  const bool bm64 = mode != C_WGRAD && bm64_on && (long)tiles_m * tiles_n < 512;
+  if (bm64) tiles_m = (M + 63) / 64;
   const long tiles = (long)tiles_m * tiles_n;
   int qps = nq, splits = 1;
   if (mode == C_WGRAD) {
@@ -607,8 +627,14 @@ static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
     splits = (nq + qps - 1) / qps;
   }
   const dim3 grid((unsigned)tiles, (unsigned)splits);
-  if (mode == C_FWD)
+  if (mode == C_FWD && bm64)
+    hipLaunchKernelGGL((conv_f32_kernel<C_FWD, 64>), grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
+                       tiles_n);
+  else if (mode == C_FWD)
     hipLaunchKernelGGL(conv_f32_kernel<C_FWD>, grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps, tiles_n);
+  else if (mode == C_DGRAD && bm64)
+    hipLaunchKernelGGL((conv_f32_kernel<C_DGRAD, 64>), grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
+                       tiles_n);
   else if (mode == C_DGRAD)
     hipLaunchKernelGGL(conv_f32_kernel<C_DGRAD>, grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
                        tiles_n);

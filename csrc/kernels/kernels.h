@@ -228,11 +228,16 @@ struct DwArgs {
   float* stats = nullptr;
   const bf16_t* bn_x = nullptr;
   const bf16_t* mask_x = nullptr;
+  int accum = 1;  // wgrad: 1 = add into a.dw / a.db, 0 = overwrite them
+  // dgrad: dx = (masked) dgrad + dadd (shaped like dx; may alias a.out) — the residual-gradient
+  // join of a tensor whose other consumer's gradient is already in the buffer (ops/gradjoin.py)
+  const bf16_t* dadd = nullptr;
 };
 bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st);  // true: a.stats written
 bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);  // true: a.stats written
 int dwconv_wgrad_slabs(const DwArgs& a);  // row-slab count of the fast wgrad (0: generic)
-// adds dW / db into a.dw / a.db; ws: slabs·(R·S + 1)·C floats when dwconv_wgrad_slabs(a) > 0
+// adds dW / db into a.dw / a.db (a.accum = 0: overwrites them); ws: slabs·(R·S + 1)·C floats when
+// dwconv_wgrad_slabs(a) > 0
 void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st);
 // out[i] (+)= Σ_z slab[z·n + i]  (split-K / slab reduction, conv_gemm.hip)
 void splitk_reduce_launch(const float* slab, float* out, long n, int splits, bool accumulate,
@@ -292,6 +297,7 @@ struct DwF32Args {
   float* db;           // fp32 [C], accumulated (optional)
   int N, H, W, C, R, S, Ho, Wo, sh, sw, ph, pw, dh, dwl;
   int relu;
+  const float* dadd;   // dgrad: added to dx (residual-gradient join; may alias out)
 };
 void dwconv_f32_fwd_launch(const DwF32Args& a, hipStream_t st);
 void dwconv_f32_dgrad_launch(const DwF32Args& a, hipStream_t st);

@@ -444,10 +444,11 @@ class DepthwiseConv2d(nn.Module):
         else:
             self.bias = None
 
-    def forward(self, x, relu_in=False, want_stats=False):
-        """``want_stats``: returns ``(y, stats)`` with the BN sums (Σy, Σy²) of y."""
+    def forward(self, x, relu_in=False, want_stats=False, join=None):
+        """``want_stats``: returns ``(y, stats)`` with the BN sums (Σy, Σy²) of y.  ``join``:
+        residual-gradient join for x (ops/gradjoin.py; see ops.dwconv.joinable)."""
         pad = resolve_padding(self.padding, x.shape[1], x.shape[2], self.k, self.k, self.stride,
                               self.dilation)
         return depthwise_conv2d(x, self.weight, self.bias, ConvGeom(self.stride, pad,
                                                                     self.dilation), self.relu,
-                                relu_in, want_stats)
+                                relu_in, want_stats, join)

@@ -12,10 +12,14 @@ GEMM kernels with BN statistics fused into their epilogue.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from .layers import ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear
+from ..ops import gradjoin
+from ..ops.dwconv import joinable
 
 
 def _fixed_pad(k, rate):
@@ -40,15 +44,17 @@ class SeparableConvBN(nn.Module):
                                 init="trunc_normal", init_std=0.06, **bn_kw)
         self.act_inside = act_inside
 
-    def forward(self, x, relu_in=False, residual=None):
+    def forward(self, x, relu_in=False, residual=None, join=None, res_join=None):
+        """``join``: gradient join of x (its depthwise dgrad accumulates onto the other
+        consumer's contribution); ``res_join``: gradient join of the residual."""
         # training: the depthwise kernel accumulates the BN statistics of its output in its
         # epilogue (no separate reduce pass over y)
         if self.training:
-            y, stats = self.depthwise(x, relu_in=relu_in, want_stats=True)
+            y, stats = self.depthwise(x, relu_in=relu_in, want_stats=True, join=join)
         else:
-            y, stats = self.depthwise(x, relu_in=relu_in), None
+            y, stats = self.depthwise(x, relu_in=relu_in, join=join), None
         y = self.dw_bn(y, stats=stats, relu=self.act_inside)
-        return self.pointwise(y, residual=residual)
+        return self.pointwise(y, residual=residual, res_join=res_join)
 
 
 class XceptionModule(nn.Module):
@@ -72,16 +78,27 @@ class XceptionModule(nn.Module):
                          if skip == "conv" else None)
         self.out_channels = depth_list[-1]
 
+    # x feeds the first separable conv and the skip: their gradients meet in one buffer — the
+    # skip's contribution (the residual BN's dres, or the 1×1 shortcut's dgrad) is written first
+    # and the depthwise dgrad adds its own in its epilogue (ops/gradjoin.py) instead of autograd
+    # summing two tensors (TDL_XC_JOIN=0: autograd add)
+    grad_join = os.environ.get("TDL_XC_JOIN", "1") == "1"
+
     def forward(self, x):
-        r = self.convs[0](x, relu_in=not self.act_inside)
+        relu_in = not self.act_inside
+        join = None
+        if (self.grad_join and self.skip in ("sum", "conv") and torch.is_grad_enabled()
+                and x.requires_grad and joinable(x, relu_in)):
+            join = gradjoin.GradJoin(2)
+        r = self.convs[0](x, relu_in=relu_in, join=join)
         r = self.convs[1](r)
         if self.skip == "sum":
             # identity skip: the add is folded into the last pointwise BN's apply (one pass,
             # one bf16 rounding of BN(y) + x instead of two)
-            return self.convs[2](r, residual=x)
+            return self.convs[2](r, residual=x, res_join=join)
         r = self.convs[2](r)
         if self.skip == "conv":
-            return self.shortcut(x, residual=r)  # BN(shortcut) + residual, no act
+            return self.shortcut(x, residual=r, join=join)  # BN(shortcut) + residual, no act
         return r
 
 

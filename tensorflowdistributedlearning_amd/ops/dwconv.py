@@ -46,9 +46,16 @@ def _fusable_relu_in(x, R, S):
     return x.shape[-1] % 8 == 0 and R * S == 9 and x.dtype != torch.float32
 
 
+def joinable(x, relu_in, R=3, S=3):
+    """Can the depthwise backward take part in a residual-gradient join on ``x`` (ops/gradjoin.py:
+    its dgrad adds the join buffer's earlier contribution in its epilogue)?  Not when an input
+    ReLU it cannot fuse turns ``x`` into a separate tensor first."""
+    return not relu_in or not on_gpu(x) or _fusable_relu_in(x, R, S)
+
+
 class _DwConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, geom, relu, relu_in, want_stats):
+    def forward(ctx, x, weight, bias, geom, relu, relu_in, want_stats, join=None):
         w = compute_weight(weight, x.dtype)
         N, H, W, C = x.shape
         R, S, _ = w.shape
@@ -71,6 +78,7 @@ class _DwConvFn(torch.autograd.Function):
             if want_stats:
                 bn_stats(y, stats)
         ctx.geom, ctx.relu, ctx.relu_in = geom, relu, relu_in
+        ctx.join = join
         # the mask token of the BN that produced x (ops/gradjoin.py): this dgrad may mask by
         # x > 0 and fuse that BN's backward statistics
         ctx.bn_tok = getattr(x, "_tdl_mask_token", None)
@@ -86,7 +94,7 @@ class _DwConvFn(torch.autograd.Function):
         x, weight, bias, y = ctx.saved_tensors
         geom = ctx.geom
         if dy is None:
-            return (None,) * 7
+            return (None,) * 8
         dy = dy.contiguous()
         if on_gpu(dy):
             if ctx.relu:
@@ -97,29 +105,52 @@ class _DwConvFn(torch.autograd.Function):
             w = compute_weight(weight, dy.dtype)
             dx = None
             if ctx.needs_input_grad[0]:
-                dx = torch.empty_like(x)
+                join, ctx.join = ctx.join, None
+                # residual-gradient join: the other consumer of x already wrote its gradient —
+                # accumulate onto it in place (the kernel adds it in its epilogue)
+                dadd = join.buf if join is not None else None
+                dx = dadd if dadd is not None else torch.empty_like(x)
                 R, S = weight.shape[0], weight.shape[1]
                 tok, ctx.bn_tok = ctx.bn_tok, None
                 # x is a BN output: its ReLU mask is x > 0 (the stored y), so this dgrad can apply
                 # it through the relu_in mask path, and the tile kernel can accumulate that BN's
                 # backward sums (Σg, Σg·x_bn) in its epilogue (ops/gradjoin.py)
-                use_tok = (DW_STATS and tok is not None and tok.x is not None
+                use_tok = (DW_STATS and tok is not None and tok.x is not None and join is None
                            and gradjoin.STATS_SINGLE and _fusable_relu_in(x, R, S))
                 masked = ctx.relu_in or (use_tok and (tok.relu_y or tok.mask is not None))
                 red = workspace.zeros((2, x.shape[-1]), dy.device) if use_tok else None
                 fused = ext().dwconv_dgrad(g, w, dx, geom.stride[0], geom.stride[1],
                                            geom.padding[0], geom.padding[2], geom.dilation[0],
                                            geom.dilation[1], x if masked else None,
-                                           tok.x if use_tok else None, red)
+                                           tok.x if use_tok else None, red, dadd=dadd)
                 if use_tok:
                     tok.mark(dx, red if fused else None)
-            # accumulated by the kernels: pre-zeroed slices of the per-step arena (one fill per
-            # step instead of one per layer); deliver_grad copies them out
-            dw = workspace.zeros(tuple(weight.shape), dy.device)
-            db = workspace.zeros((x.shape[-1],), dy.device) if bias is not None else None
+                if join is not None:
+                    if join.buf is None:
+                        join.buf = dx
+                    join.note(False)
+                    dx = join.take()
+            # straight into the flat gradient buffer (overwrite on the step's first contribution)
+            # when the parameters are flat-backed; otherwise pre-zeroed slices of the per-step
+            # arena (one fill per step) that deliver_grad copies out
+            want_b = bias is not None and bias.requires_grad
+            wt, wfresh = grad_target(weight) if weight.requires_grad else (None, False)
+            bt, bfresh = grad_target(bias) if want_b else (None, wfresh)
+            direct = (wt is not None and (not want_b or (bt is not None and bfresh == wfresh))
+                      and (bias is None or want_b))
+            if direct:
+                dw, db = wt, (bt if want_b else None)
+            else:
+                dw = workspace.zeros(tuple(weight.shape), dy.device)
+                db = workspace.zeros((x.shape[-1],), dy.device) if bias is not None else None
             ext().dwconv_wgrad(g, x, dw, db, geom.stride[0], geom.stride[1], geom.padding[0],
                                geom.padding[2], geom.dilation[0], geom.dilation[1],
-                               bool(ctx.relu_in))
+                               bool(ctx.relu_in), not (direct and wfresh))
+            if direct:
+                deliver_grad(weight, written=True)
+                if want_b:
+                    deliver_grad(bias, written=True)
+                return dx, None, None, None, None, None, None, None
         else:
             xr = x.detach().float().requires_grad_(True)
             wr = weight.detach().float().requires_grad_(True)
@@ -133,23 +164,34 @@ class _DwConvFn(torch.autograd.Function):
             dx = grads[0].to(x.dtype)
             dw = grads[1]
             db = grads[2] if br is not None else None
+            join, ctx.join = ctx.join, None
+            if join is not None:
+                if join.buf is None:
+                    join.buf = dx
+                else:
+                    join.buf += dx
+                join.note(False)
+                dx = join.take()
         if weight.requires_grad:
             deliver_grad(weight, dw)
         if bias is not None and bias.requires_grad:
             deliver_grad(bias, db)
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
 def depthwise_conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False,
-                     relu_in=False, want_stats=False):
+                     relu_in=False, want_stats=False, join=None):
     """``relu_in``: convolve max(x, 0) without materialising it (Xception's pre-activation ReLU
     in front of each separable conv, core/xception.py:90-110); the backward masks dx by x > 0.
     ``want_stats``: also return fp32 [2, C] = (Σy, Σy²) of the stored output for the BN that
     normalises it (fused into the stride-1 tile kernel's epilogue) — returns ``(y, stats)``."""
     if relu_in and on_gpu(x) and not _fusable_relu_in(x, weight.shape[0], weight.shape[1]):
+        if join is not None:
+            raise ValueError("depthwise_conv2d: a join on x needs the fused input ReLU "
+                             "(see joinable())")
         from .elementwise import relu as relu_op
         x, relu_in = relu_op(x), False
-    y, stats = _DwConvFn.apply(x, weight, bias, geom, relu, relu_in, bool(want_stats))
+    y, stats = _DwConvFn.apply(x, weight, bias, geom, relu, relu_in, bool(want_stats), join)
     return (y, stats) if want_stats else y
 
 

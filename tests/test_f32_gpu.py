@@ -43,7 +43,9 @@ F32_SHAPES = [
     (2, 9, 9, 40, 8, 3, 3, 1, (1, 1, 1, 1), 1),           # decoder logit conv (1 padded to 8)
     (2, 13, 13, 24, 16, 3, 3, 2, (2, 2, 2, 2), 2),        # stride 2 + dilation 2
     (2, 11, 12, 16, 20, 1, 1, 2, (0, 0, 0, 0), 1),        # 1x1 s2 on odd/even sizes
-    (16, 26, 26, 128, 128, 3, 3, 1, (1, 1, 1, 1), 1),     # many tiles + split-K wgrad
+    (16, 26, 26, 128, 128, 3, 3, 1, (1, 1, 1, 1), 1),     # 64-row tiles + split-K wgrad
+    (32, 32, 32, 64, 256, 1, 1, 1, (0, 0, 0, 0), 1),      # ≥ 512 tiles: 128-row tiles
+    (32, 32, 32, 128, 256, 3, 3, 1, (1, 1, 1, 1), 1),     # 128-row tiles, 3×3
 ]
 
 

@@ -210,3 +210,26 @@ def test_deeplab_fused_residual_units_match(block_type):
         torch.testing.assert_close(ga, gb, rtol=1e-4, atol=1e-6, msg=name)
     for p, q in zip(a.buffers(), b.buffers()):
         torch.testing.assert_close(p, q)
+
+
+def test_xception_gradient_join_matches_autograd():
+    """Xception modules: the skip's gradient and the first separable conv's depthwise dgrad meet
+    in one buffer (the depthwise backward adds onto it) — same gradients as autograd's sum."""
+    from tensorflowdistributedlearning_amd.models.xception import XceptionModule
+    torch.manual_seed(0)
+    m = models.xception_41(num_classes=5)
+    x = torch.randn(2, 64, 64, 3)
+    grads = []
+    for enabled in (False, True):
+        XceptionModule.grad_join = enabled
+        try:
+            m.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            m.train()
+            out = m(xi)
+            out.float().pow(2).sum().backward()
+            grads.append([xi.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+        finally:
+            XceptionModule.grad_join = True
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)

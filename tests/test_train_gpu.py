@@ -845,10 +845,10 @@ def test_xception_fused_bn_statistics_match_reduce_passes(gpu, monkeypatch):
 
 
 def _unfused_sep_forward(mod):
-    def fwd(x, relu_in=False, residual=None):
-        yy = mod.depthwise(x, relu_in=relu_in)
+    def fwd(x, relu_in=False, residual=None, join=None, res_join=None):
+        yy = mod.depthwise(x, relu_in=relu_in, join=join)
         yy = mod.dw_bn(yy, relu=mod.act_inside)
-        return mod.pointwise(yy, residual=residual)
+        return mod.pointwise(yy, residual=residual, res_join=res_join)
     return fwd
 
 
@@ -901,3 +901,28 @@ def _moving_stats_within_noise(a, b, c, make_trainer, x, y):
         worst_bc = max(worst_bc, ((bufs[1][n] - bufs[2][n]).abs().max() / scale).item())
     print("moving stats: a-b", worst_ab, "run-to-run b-c", worst_bc)
     assert worst_ab <= 2.0 * worst_bc + 2e-3, (worst_ab, worst_bc)
+
+
+@pytest.mark.timeout(300)
+def test_xception_depthwise_join_matches_autograd_sum(gpu):
+    """Xception module inputs: the depthwise dgrad adds the skip's gradient in its epilogue
+    (dwconv_dgrad dadd, one buffer per join) instead of autograd summing two tensors — same
+    gradients on the GPU within bf16 rounding of one add, and depthwise weight gradients written
+    straight into the flat gradient buffer."""
+    from tensorflowdistributedlearning_amd.models.xception import XceptionModule
+    torch.manual_seed(12)
+    x, y = imagenet_batch(4, 64, num_classes=10, dtype=torch.float32)
+    grads = []
+    for enabled in (False, True):
+        XceptionModule.grad_join = enabled
+        try:
+            torch.manual_seed(13)
+            m = models.xception_41(num_classes=10)
+            tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.0, momentum=0.0))
+            tr.train_mode = False
+            tr.train_step(x.to(gpu, torch.bfloat16), y.to(gpu))
+            grads.append(tr.flat.grad.clone())
+        finally:
+            XceptionModule.grad_join = True
+    cos = torch.nn.functional.cosine_similarity(grads[0], grads[1], dim=0).item()
+    assert cos > 0.9999, cos
