@@ -107,6 +107,8 @@ def main(argv=None):
         p.add_argument("--seed", type=int)
         p.add_argument("--device")
         p.add_argument("--block-type", dest="block_type")
+        p.add_argument("--precision", choices=("bf16", "fp32"),
+                       help="GPU compute precision (fp32: the reference's own precision)")
         p.add_argument("--batch-size", dest="batch_size", type=int, default=64)
 
     t = sub.add_parser("train")

@@ -47,6 +47,9 @@ class ModelConfig:
     kaggle_metric: bool = False       # D16: reference formula by default
     loader_threads: int = 4
     device: Optional[str] = None
+    # GPU compute precision: "bf16" (fused bf16 kernels, fp32 accumulation / master weights) or
+    # "fp32" (the reference's own precision: fp32 operands on the fp32 kernels end to end)
+    precision: str = "bf16"
 
     def validate(self):
         if self.data_format not in ("NCHW", "NHWC"):
@@ -57,6 +60,8 @@ class ModelConfig:
             raise ValueError("Expect n_blocks to have length 3.")
         if self.block_type not in ("bottleneck", "basic_block"):
             raise ValueError(f"unknown block_type {self.block_type}")
+        if self.precision not in ("bf16", "fp32"):
+            raise ValueError(f"unknown precision {self.precision} (bf16 or fp32)")
         return self
 
     def model_kwargs(self):

@@ -98,6 +98,12 @@ class Model:
         self.augmentation = dict(TRAIN_AUG, **kwargs.get("augmentation", {}))
         self.device = kwargs.get("device", None)
         self.backend = kwargs.get("backend", None)
+        # GPU compute precision: bf16 (default; fp32 accumulation, statistics, optimizer state and
+        # master weights) or fp32 (the reference's precision — no dtype option exists in
+        # /root/reference/model.py: every op on fp32 operands, csrc/kernels/f32.hip)
+        self.precision = kwargs.get("precision", "bf16")
+        if self.precision not in ("bf16", "fp32"):
+            raise ValueError(f"unknown precision {self.precision} (bf16 or fp32)")
 
         self.model_name = model_dir.rstrip("/").split("/")[-1]
         self.model_dir = model_dir
@@ -118,7 +124,7 @@ class Model:
                 "batch_norm_scale": self.batch_norm_scale, "output_stride": self.output_stride,
                 "base_depth": self.base_depth, "input_shape": list(self.input_shape),
                 "n_blocks": list(self.n_blocks), "block_type": self.block_type,
-                "lr": self.lr, "seed": self.seed}
+                "lr": self.lr, "seed": self.seed, "precision": self.precision}
 
     def build_network(self):
         return DeepLabResNet(model_name=self.model_name, in_channels=2,
@@ -128,6 +134,10 @@ class Model:
                              batch_norm_epsilon=self.batch_norm_epsilon,
                              batch_norm_scale=self.batch_norm_scale,
                              weight_decay=self.weight_decay)
+
+    def _cast(self, x):
+        """The network input in the compute precision (the loaders deliver bf16 images)."""
+        return x.float() if self.precision == "fp32" and x.dtype != torch.float32 else x
 
     def _world(self):
         """Processes to launch: one per GPU when enough GPUs exist; ``device='cpu'`` with
@@ -198,7 +208,8 @@ class Model:
         extra = ((lambda m: m.regularization_loss()) if self.use_regularization else None)
         trainer = Trainer(net, lambda out, yy: lovasz_hinge(out, yy), device, optimizer="adam",
                           opt_kwargs=dict(lr=self.lr, lr_schedule=schedule), ctx=ctx,
-                          extra_loss_fn=extra)
+                          extra_loss_fn=extra,
+                          lowp_dtype=None if self.precision == "fp32" else torch.bfloat16)
         start = 0
         latest = ckpt.latest_checkpoint(fold_dir)
         if latest is not None:
@@ -230,6 +241,7 @@ class Model:
         t0 = time.time()
         while step < steps:
             x, yy = next(pipe)
+            x = self._cast(x)
             loss, out = trainer.train_step(x, yy)
             step = trainer.global_step
             pred = (out.float() > _logit(self.threshold)).float()
@@ -276,6 +288,7 @@ class Model:
         sums = torch.zeros(4, dtype=torch.float64, device=device)  # iou, acc, loss, count
         first = True
         for x, yy in pipe:
+            x = self._cast(x)
             out = net(x)
             if first and writer is not None:
                 _image_summaries(writer, "eval", x, yy, out, self.threshold, step)
@@ -320,7 +333,7 @@ class Model:
                 probs, fold_ids = [], []
                 for x, b_ids in TestPipeline(images, batch_size, tf, device=device,
                                              threads=self.loader_threads):
-                    p = torch.sigmoid(net(x).float())
+                    p = torch.sigmoid(net(self._cast(x)).float())
                     probs.append(_undo_transform(p, tf)[..., 0].cpu())
                     fold_ids += b_ids
                 p = torch.cat(probs)
@@ -352,7 +365,8 @@ class Model:
                                              decay_rate=0.5, staircase=False)
                 spec["trainer"] = Trainer(net, loss_fn, device, optimizer="adam",
                                           opt_kwargs=dict(lr=self.lr, lr_schedule=schedule),
-                                          ctx=ctx)
+                                          ctx=ctx, lowp_dtype=None if self.precision == "fp32"
+                                          else torch.bfloat16)
             else:
                 net.to(device).eval()
             return spec

@@ -124,6 +124,28 @@ def test_model_train_predict_on_gpu(tmp_path, gpu):
     assert out["probabilities"].shape == (8, 101, 101)
 
 
+@pytest.mark.gpu
+def test_model_train_predict_fp32_on_gpu(tmp_path, gpu):
+    """``Model(precision="fp32")``: the reference's own precision — fp32 master weights read
+    directly by the fp32 kernels (no bf16 compute copy), fp32 activations end to end."""
+    X, y = _dataset(str(tmp_path / "data"), n=8, hw=101, seed=4)
+    md = str(tmp_path / "runs" / "gpu32")
+    kw = dict(SMALL, device=None, input_shape=(101, 101), save_checkpoints_steps=3)
+    m = Model(md, str(tmp_path / "data"), n_gpus=1, n_fold=2, save_best=1, precision="fp32", **kw)
+    res = m.train(X, y, batch_size=4, steps=3)
+    assert all(np.isfinite(r["eval"]["loss/lovasz_loss"]) for r in res)
+    out = m.predict(os.path.join(str(tmp_path / "data"), "images"), batch_size=4)
+    assert out["probabilities"].shape == (8, 101, 101)
+
+
+def test_model_precision_option(tmp_path):
+    with pytest.raises(ValueError):
+        Model(str(tmp_path / "m"), str(tmp_path), precision="fp16", **SMALL)
+    m = Model(str(tmp_path / "m"), str(tmp_path), precision="fp32", **SMALL)
+    assert m.config()["precision"] == "fp32"
+    assert m._cast(torch.zeros(2, dtype=torch.bfloat16)).dtype == torch.float32
+
+
 def test_model_reference_surface_helpers(tmp_path):
     """build_model_fn_optimizer / _make_input_fn / _make_test_input (model.py:257-505)."""
     X, y = _dataset(str(tmp_path / "data"), n=4)
