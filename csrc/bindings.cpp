@@ -731,16 +731,24 @@ void avgpool_fwd(Tensor x, Tensor y) {
   avgpool_fwd_launch(BF(x), BFW(y), x.size(0), x.size(1) * x.size(2), x.size(3), stream());
 }
 
-void avgpool_bwd(Tensor dy, Tensor dx) {
+// dadd (optional, shaped like dx, may be dx itself; C % 8 == 0): dx = dy/HW + dadd
+void avgpool_bwd(Tensor dy, Tensor dx, c10::optional<Tensor> dadd) {
+  const bool has_add = dadd.has_value() && dadd->defined();
+  if (has_add)
+    TORCH_CHECK(dadd->sizes() == dx.sizes() && dadd->is_contiguous() &&
+                    dadd->scalar_type() == dx.scalar_type() && dx.size(3) % 8 == 0,
+                "avgpool_bwd dadd: shaped like dx, C % 8 == 0");
   if (is_f32(dy)) {
     CHECK_T(dy, torch::kFloat32);
     CHECK_T(dx, torch::kFloat32);
-    avgpool_bwd_launch(F32(dy), F32(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream());
+    avgpool_bwd_launch(F32(dy), F32(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream(),
+                       has_add ? F32(*dadd) : nullptr);
     return;
   }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
-  avgpool_bwd_launch(BF(dy), BFW(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream());
+  avgpool_bwd_launch(BF(dy), BFW(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), stream(),
+                     has_add ? BF(*dadd) : nullptr);
 }
 
 // --------------------------------------------------------------------------------------- losses
@@ -1226,7 +1234,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("maxpool_bwd_stats", &maxpool_bwd_stats);
   m.def("avgpool_fwd", &avgpool_fwd);
-  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("avgpool_bwd", &avgpool_bwd, py::arg("dy"), py::arg("dx"), py::arg("dadd") = py::none());
   m.def("softmax_xent", &softmax_xent);
   m.def("lovasz_hinge", &lovasz_hinge);
   m.def("seg_metrics", &seg_metrics);

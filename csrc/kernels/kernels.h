@@ -185,7 +185,9 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
 void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
 void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
-void avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
+// dadd (optional, C % 8 == 0, may alias dx): dx = dy/HW + dadd (residual-gradient join)
+void avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st,
+                        const bf16_t* dadd = nullptr);
 
 // losses -------------------------------------------------------------------------------------
 void softmax_xent_launch(const void* logits, bool bf16, const int64_t* labels, float* loss,
@@ -308,7 +310,8 @@ void maxpool_fwd_launch(const float* x, float* y, uint8_t* idx, int N, int H, in
 void maxpool_bwd_launch(const float* dy, const uint8_t* idx, float* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
 void avgpool_fwd_launch(const float* x, float* y, int N, int HW, int C, hipStream_t st);
-void avgpool_bwd_launch(const float* dy, float* dx, int N, int HW, int C, hipStream_t st);
+void avgpool_bwd_launch(const float* dy, float* dx, int N, int HW, int C, hipStream_t st,
+                        const float* dadd = nullptr);
 void upsample_fwd_launch(const float* x, float* y, const int* ih, const float* wh,
                          const int* iw, const float* ww, int N, int H, int W, int C, int Ho,
                          int Wo, hipStream_t st, int ldy = 0);

@@ -216,7 +216,8 @@ __global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, i
 
 template <typename T>
 __global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int N,
-                                   int HW, int C) {
+                                   int HW, int C, const T* __restrict__ dadd) {
+  // dadd (optional, may alias dx): the residual-gradient join's earlier contribution
   const int cv = C / 8;
   const long total = (long)N * HW * cv;
   const float inv = 1.f / HW;
@@ -228,6 +229,12 @@ __global__ void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx,
     load8(dy + (long)n * C + c, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] *= inv;
+    if (dadd) {
+      float d[8];
+      load8(dadd + p * C + c, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] += d[j];
+    }
     store8(dx + p * C + c, g);
   }
 }
@@ -299,10 +306,13 @@ static void avgpool_fwd_impl(const T* x, T* y, int N, int HW, int C, hipStream_t
 }
 
 template <typename T>
-static void avgpool_bwd_impl(const T* dy, T* dx, int N, int HW, int C, hipStream_t st) {
+static void avgpool_bwd_impl(const T* dy, T* dx, int N, int HW, int C, hipStream_t st,
+                             const T* dadd = nullptr) {
   if (C % 8 == 0)
     hipLaunchKernelGGL(avgpool_bwd_kernel<T>, dim3(blocks_for((long)N * HW * C / 8)), dim3(NT), 0, st, dy,
-                       dx, N, HW, C);
+                       dx, N, HW, C, dadd);
+  else if (dadd)
+    __builtin_trap();  // host-checked: a join needs C % 8 == 0
   else
     hipLaunchKernelGGL(avgpool_scalar_bwd<T>, dim3(blocks_for((long)N * HW * C)), dim3(NT), 0, st, dy, dx,
                        N, HW, C);
@@ -321,8 +331,9 @@ static void avgpool_bwd_impl(const T* dy, T* dx, int N, int HW, int C, hipStream
   void avgpool_fwd_launch(const T* x, T* y, int N, int HW, int C, hipStream_t st) {                 \
     avgpool_fwd_impl<T>(x, y, N, HW, C, st);                                                      \
   }                                                                                               \
-  void avgpool_bwd_launch(const T* dy, T* dx, int N, int HW, int C, hipStream_t st) {               \
-    avgpool_bwd_impl<T>(dy, dx, N, HW, C, st);                                                    \
+  void avgpool_bwd_launch(const T* dy, T* dx, int N, int HW, int C, hipStream_t st,               \
+                          const T* dadd) {                                                        \
+    avgpool_bwd_impl<T>(dy, dx, N, HW, C, st, dadd);                                              \
   }
 TDL_POOL_ENTRY(bf16_t)
 TDL_POOL_ENTRY(float)

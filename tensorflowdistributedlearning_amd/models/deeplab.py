@@ -137,8 +137,8 @@ class SplitSeparableConv(nn.Module):
                                 init_std=0.06, bn_decay=bn_kw["decay"], bn_eps=bn_kw["eps"],
                                 bn_scale=bn_kw["scale"])
 
-    def forward(self, x, into=None):
-        return self.pointwise(self.depthwise(x), into=into)
+    def forward(self, x, into=None, join=None):
+        return self.pointwise(self.depthwise(x, join=join), into=into)
 
 
 class DeepLabResNet(nn.Module):
@@ -250,6 +250,7 @@ class DeepLabResNet(nn.Module):
     # consumer conv's input, and each backward reads its slice of the concat gradient in place
     # (ops/bn.batch_norm_act_into, ops/upsample.upsample_into) — no torch.cat / split passes
     concat_free = os.environ.get("TDL_CONCAT_FREE", "1") == "1"
+    aspp_join = os.environ.get("TDL_ASPP_JOIN", "1") == "1"
 
     def forward(self, x, return_end_points=False):
         root = f"{self.model_name}/resnet_v2"
@@ -290,12 +291,18 @@ class DeepLabResNet(nn.Module):
     def _head_concat_free(self, atrous, b1):
         d = self.assp_out.bn.c
         N, h, w = atrous.shape[:3]
+        # the five ASPP branches read the encoder output: their input gradients meet in one
+        # buffer (the first branch backward writes it, the others add in their epilogues —
+        # conv dgrad accumulate, depthwise / avg-pool dadd; ops/gradjoin.py) instead of four
+        # autograd adds
+        join = (gradjoin.GradJoin(5) if self.aspp_join and torch.is_grad_enabled()
+                and atrous.requires_grad and atrous.shape[-1] % 8 == 0 else None)
         cat = atrous.new_empty((N, h, w, 5 * d))
-        cat = self.assp_conv_1x1(atrous, into=(cat, 0))
-        cat = self.assp_conv_3x3_1(atrous, into=(cat, d))
-        cat = self.assp_conv_3x3_2(atrous, into=(cat, 2 * d))
-        cat = self.assp_conv_3x3_3(atrous, into=(cat, 3 * d))
-        a5 = self.assp_pool_conv(global_avg_pool(atrous, keepdims=True))
+        cat = self.assp_conv_1x1(atrous, into=(cat, 0), join=join)
+        cat = self.assp_conv_3x3_1(atrous, into=(cat, d), join=join)
+        cat = self.assp_conv_3x3_2(atrous, into=(cat, 2 * d), join=join)
+        cat = self.assp_conv_3x3_3(atrous, into=(cat, 3 * d), join=join)
+        a5 = self.assp_pool_conv(global_avg_pool(atrous, keepdims=True, join=join))
         cat = upsample_into(cat, 4 * d, a5)
         assp = self.assp_out(cat)
         dec = b1.new_empty((b1.shape[0], b1.shape[1], b1.shape[2], 2 * d))

@@ -85,10 +85,11 @@ def max_pool2d(x, k, s, pad):
 
 class _GAPFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, keepdims):
+    def forward(ctx, x, keepdims, join=None):
         N, H, W, C = x.shape
         ctx.x_shape = tuple(x.shape)
         ctx.keepdims = keepdims
+        ctx.join = join
         if on_gpu(x):
             y = torch.empty((N, C), device=x.device, dtype=x.dtype)
             ext().avgpool_fwd(x, y)
@@ -100,13 +101,28 @@ class _GAPFn(torch.autograd.Function):
     def backward(ctx, dy):
         N, H, W, C = ctx.x_shape
         dy = dy.reshape(N, C).contiguous()
+        join, ctx.join = ctx.join, None
         if on_gpu(dy):
-            dx = torch.empty(ctx.x_shape, device=dy.device, dtype=dy.dtype)
-            ext().avgpool_bwd(dy, dx)
-            return dx, None
-        dx = (dy.float() / (H * W)).view(N, 1, 1, C).expand(N, H, W, C).contiguous()
-        return dx.to(dy.dtype), None
+            # residual-gradient join (ops/gradjoin.py): add the earlier contributions in place
+            dadd = join.buf if join is not None else None
+            dx = dadd if dadd is not None else torch.empty(ctx.x_shape, device=dy.device,
+                                                           dtype=dy.dtype)
+            ext().avgpool_bwd(dy, dx, dadd)
+        else:
+            dx = (dy.float() / (H * W)).view(N, 1, 1, C).expand(N, H, W, C).to(dy.dtype)
+            if join is not None and join.buf is not None:
+                join.buf += dx
+                dx = join.buf
+            else:
+                dx = dx.contiguous()
+        if join is not None:
+            join.buf = dx
+            join.note(False)
+            dx = join.take()
+        return dx, None, None
 
 
-def global_avg_pool(x, keepdims=False):
-    return _GAPFn.apply(x, keepdims)
+def global_avg_pool(x, keepdims=False, join=None):
+    """Mean over H, W.  ``join``: gradient join of x (ops/gradjoin.py; the backward adds the
+    join buffer's earlier contributions, C % 8 == 0 on the GPU)."""
+    return _GAPFn.apply(x, keepdims, join)
