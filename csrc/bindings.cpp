@@ -166,6 +166,12 @@ void conv_wgrad_f32(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_
   a.dy = F32(dy); a.x = F32(x); a.out = F32(out);
   a.accumulate = accumulate;
   auto st = stream();
+  const int splits = conv_f32_wgrad_splits(a);
+  Tensor slab;
+  if (splits > 1) {
+    slab = torch::empty({(int64_t)splits * out.numel()}, out.options());
+    a.slab = F32(slab);
+  }
   conv_f32_wgrad_launch(a, st);
   if (bias_grad.has_value() && bias_grad->defined()) {
     CHECK_T(*bias_grad, torch::kFloat32);

@@ -229,8 +229,12 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
             const long o = (long)row * C + col;
             a.out[o] = a.accumulate ? a.out[o] + val : val;
           }
-        } else {
-          if (row < K && col < Ng) unsafeAtomicAdd(a.out + (long)row * Ng + col, val);
+        } else if (row < K && col < Ng) {
+          const long o = (long)row * Ng + col;
+          if (a.slab)
+            a.slab[(long)blockIdx.y * K * Ng + o] = val;  // this split's partial slab
+          else
+            a.out[o] = a.accumulate ? a.out[o] + val : val;
         }
       }
     }
@@ -601,6 +605,22 @@ void row_pack_f32_launch(const float* x, float* t, int N, int H, int W, int Cx, 
   hipLaunchKernelGGL(row_pack_f32, dim3(eblocks(n)), dim3(256), 0, st, x, t, n, W, Cx, Cr, S, sw, pl,
                      Wo, Cp);
 }
+// WGRAD: split the pixel reduction until the grid holds ~4 workgroups per CU, ≥ 16 K-steps each
+static void wgrad_plan(const ConvF32Args& a, int* qps, int* splits) {
+  const int M = a.K, Ng = a.R * a.S * a.C;
+  const int nq = (int)(((long)a.N * a.Ho * a.Wo + BK - 1) / BK);
+  const long tiles = (long)((M + BM - 1) / BM) * ((Ng + BN - 1) / BN);
+  const long want = std::max<long>(1, 1024 / tiles);
+  *qps = (int)std::max<long>(16, (nq + want - 1) / want);
+  *splits = std::max(1, (nq + *qps - 1) / *qps);
+}
+
+int conv_f32_wgrad_splits(const ConvF32Args& a) {
+  int qps, splits;
+  wgrad_plan(a, &qps, &splits);
+  return splits;
+}
+
 static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
   int M, Ng, nq, cch = 1;
   if (mode == C_FWD) {
@@ -620,12 +640,7 @@ static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
   if (bm64) tiles_m = (M + 63) / 64;
   const long tiles = (long)tiles_m * tiles_n;
   int qps = nq, splits = 1;
-  if (mode == C_WGRAD) {
-    // split the pixel reduction until the grid holds ~4 workgroups per CU (8 K-steps minimum)
-    const long want = std::max<long>(1, 1024 / tiles);
-    qps = (int)std::max<long>(8, (nq + want - 1) / want);
-    splits = (nq + qps - 1) / qps;
-  }
+  if (mode == C_WGRAD) wgrad_plan(a, &qps, &splits);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (mode == C_FWD && bm64)
     hipLaunchKernelGGL((conv_f32_kernel<C_FWD, 64>), grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
@@ -645,10 +660,13 @@ static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
 
 void conv_f32_fwd_launch(const ConvF32Args& a, hipStream_t st) { conv_f32_launch(C_FWD, a, st); }
 void conv_f32_dgrad_launch(const ConvF32Args& a, hipStream_t st) { conv_f32_launch(C_DGRAD, a, st); }
-void conv_f32_wgrad_launch(const ConvF32Args& a, hipStream_t st) {
-  const long n = (long)a.K * a.R * a.S * a.C;
-  if (!a.accumulate) (void)hipMemsetAsync(a.out, 0, n * sizeof(float), st);
+void conv_f32_wgrad_launch(const ConvF32Args& a0, hipStream_t st) {
+  const long n = (long)a0.K * a0.R * a0.S * a0.C;
+  const int splits = conv_f32_wgrad_splits(a0);
+  ConvF32Args a = a0;
+  if (splits == 1) a.slab = nullptr;  // one split: dW written (or accumulated) directly
   conv_f32_launch(C_WGRAD, a, st);
+  if (splits > 1) splitk_reduce_launch(a.slab, a.out, n, splits, a.accumulate != 0, st);
 }
 
 void colsum_f32_launch(const float* x, float* out, long M, int C, long ldx, hipStream_t st) {

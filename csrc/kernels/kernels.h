@@ -268,9 +268,13 @@ struct ConvF32Args {
   int N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw;
   int relu;            // FWD
   int accumulate;      // DGRAD: dx += …; WGRAD: dW += … (else overwritten)
+  float* slab;         // WGRAD with conv_f32_wgrad_splits(a) > 1: fp32 scratch of splits·K·R·S·C
 };
 void conv_f32_fwd_launch(const ConvF32Args& a, hipStream_t st);
 void conv_f32_dgrad_launch(const ConvF32Args& a, hipStream_t st);
+// WGRAD splits the pixel reduction: each split writes its partial dW slab (plain stores), one
+// reduction pass sums the slabs into dW (no memset, no atomics)
+int conv_f32_wgrad_splits(const ConvF32Args& a);
 void conv_f32_wgrad_launch(const ConvF32Args& a, hipStream_t st);
 // out[c] += Σ_m x[m·ldx + c] (the caller zeroes out for an overwrite)
 void colsum_f32_launch(const float* x, float* out, long M, int C, long ldx, hipStream_t st);

@@ -953,3 +953,28 @@ def test_bn_bwd_apply_dadd(gpu):
     d0, _ = B.bn_bwd_apply(dy, None, x, coef, red, gam, M, 2, False)
     d1, _ = B.bn_bwd_apply(dy, None, x, coef, red, gam, M, 2, False, dadd=g2)
     assert rel_err(d1, d0.float() + g2.float()) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_join_dadd_kernels(gpu, dtype):
+    """Residual-gradient join inputs: the depthwise dgrad and the global-average-pool backward add
+    an earlier contribution (``dadd``, here in place: out is dadd) in their epilogues — equal to
+    the plain result plus that contribution."""
+    torch.manual_seed(9)
+    N, H, W, Cn = 2, 13, 13, 64
+    dy = torch.randn(N, H, W, Cn, device=gpu).to(dtype)
+    w = (torch.randn(3, 3, Cn, device=gpu) * 0.3).to(dtype)
+    prev = torch.randn(N, H, W, Cn, device=gpu).to(dtype)
+    for dil in (1, 2):
+        plain = torch.empty_like(prev)
+        ext().dwconv_dgrad(dy, w, plain, 1, 1, dil, dil, dil, dil)
+        buf = prev.clone()
+        ext().dwconv_dgrad(dy, w, buf, 1, 1, dil, dil, dil, dil, dadd=buf)
+        tol = 0 if dtype == torch.float32 else 1e-2
+        assert rel_err(buf, plain.float() + prev.float()) <= max(tol, 1e-6), dil
+    g = torch.randn(N, Cn, device=gpu).to(dtype)
+    plain = torch.empty_like(prev)
+    ext().avgpool_bwd(g, plain)
+    buf = prev.clone()
+    ext().avgpool_bwd(g, buf, buf)
+    assert rel_err(buf, plain.float() + prev.float()) <= (1e-6 if dtype == torch.float32 else 1e-2)
