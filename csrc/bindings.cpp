@@ -1268,6 +1268,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_glds_mode", &conv_glds_mode);
   m.def("conv_set_m32", &conv_set_m32, "32x32x16-MFMA K loop for KC-operand LDS-DMA convs (-1: env)");
   m.def("conv_m32", &conv_m32);
+  m.def("conv_f32_set_tile", &conv_f32_set_tile, "fp32 conv FWD/DGRAD tile override (0, 0: auto)");
   m.def("fastdiv", [](uint32_t d) { auto f = make_fastdiv(d); return py::make_tuple(f.m, f.s); },
         "magic (m, s) with n / d == (n * m) >> s for 0 <= n < 2^31");
   m.def("rccl_unique_id", []() { return py::bytes(comm::get_unique_id()); });

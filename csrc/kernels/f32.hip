@@ -45,36 +45,52 @@ __device__ __forceinline__ float4 ld4(const float* p, int n, bool vec) {
 //   FWD   m = output pixel, n = output channel, q = (tap r,s) × 16-channel chunk of C
 //   DGRAD m = input pixel,  n = input channel,  q = (tap r,s) × 16-channel chunk of K
 //   WGRAD m = output channel, n = (r,s,c) of dW [K][R][S][C], q = 16-pixel chunk of N·Ho·Wo
-// Operand staging patterns (per K-step, 256 threads, 2 float4 loads per operand per thread):
-//   "row" operands (FWD A/B, DGRAD A): thread owns row t&127, loads k (t>>7)*4 and +8
-//   "col" operands (DGRAD B, WGRAD A/B): thread owns columns (t&31)*4..+3, loads k t>>5 and +8
-// TBM: workgroup rows (128, or 64 for FWD / DGRAD problems with fewer than two 128-row tiles per
-// CU — the reference preset's 13×13 maps at batch 64 fill only 170 of 256 CUs with 128-row tiles)
-template <int MODE, int TBM = BM>
+// Workgroup tile TBM × TBN (64 or 128 each), 4 waves in a 2×2 grid, each wave (TBM/2) × (TBN/2) =
+// FM × FN blocks of 32×32.  Operand staging per K-step (an operand with R rows is R×16 floats =
+// R/64 float4 loads per thread; 256 % R == 0, so a thread keeps one row / column group):
+//   "row" operands (FWD A/B, DGRAD A): thread owns row t % R and k offsets 4·((t + 256j) / R)
+//   "col" operands (DGRAD B, WGRAD A/B): thread owns columns 4·(t % (R/4)) … +3 and k rows
+//   (t + 256j) / (R/4)
+// Small problems take smaller tiles (conv_f32_launch): the reference preset's 13×13 maps at batch
+// 64 are 170 workgroups of 128×128 — two thirds of the chip, one wave of work — but 676 of 64×64.
+template <int R>
+struct RowPat {  // "row" staging: row, and the k offset of load j
+  static constexpr int L = R / 64;
+  __device__ __forceinline__ static int row(int t) { return t % R; }
+  __device__ __forceinline__ static int k4(int t, int j) { return ((t + 256 * j) / R) * 4; }
+};
+template <int R>
+struct ColPat {  // "col" staging: first column, and the k row of load j
+  static constexpr int L = R / 64;
+  __device__ __forceinline__ static int col(int t) { return (t % (R / 4)) * 4; }
+  __device__ __forceinline__ static int kr(int t, int j) { return (t + 256 * j) / (R / 4); }
+};
+
+template <int MODE, int TBM = BM, int TBN = BN>
 __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int Ng, int nq,
                                                       int cch, int qps, int tiles_n) {
-  static_assert(TBM == 128 || (TBM == 64 && MODE != C_WGRAD), "row tile 128, or 64 (FWD / DGRAD)");
-  constexpr int FM = TBM / 64;  // 32×32 blocks per wave along M
+  static_assert((TBM == 64 || TBM == 128) && (TBN == 64 || TBN == 128), "tiles of 64 / 128");
+  constexpr int FM = TBM / 64, FN = TBN / 64;  // 32×32 blocks per wave
+  constexpr bool A_ROW = MODE != C_WGRAD, B_ROW = MODE == C_FWD;
+  constexpr int LA = TBM / 64, LB = TBN / 64;  // float4 loads per thread per operand
   __shared__ __attribute__((aligned(16))) float As[2][BK][LDP];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDP];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int l31 = lane & 31, hk = lane >> 5;
   const int tile = blockIdx.x;
-  const int m0 = (tile / tiles_n) * TBM, n0 = (tile % tiles_n) * BN;
+  const int m0 = (tile / tiles_n) * TBM, n0 = (tile % tiles_n) * TBN;
   const int q0 = blockIdx.y * qps, q1 = min(nq, q0 + qps);
   const int H = a.H, W = a.W, C = a.C, K = a.K, S = a.S, Ho = a.Ho, Wo = a.Wo;
 
   // ---- per-thread loader state (fixed over the K loop)
-  const int ri = t & 127, k4 = (t >> 7) * 4;       // "row" pattern
-  // the A operand's row pattern: TBM rows × 16 k (TBM 64: one float4 per thread, k 0/4/8/12)
-  const int ri_a = t & (TBM - 1), k4a = (t / TBM) * 4;
-  const int kr = t >> 5, c4 = (t & 31) * 4;        // "col" pattern
-  int pa_n = 0, pa_h = 0, pa_w = 0;                // A row pixel (FWD: output, DGRAD: input)
+  const int ra_ = A_ROW ? RowPat<TBM>::row(t) : ColPat<TBM>::col(t);  // A row / first column
+  const int rb_ = B_ROW ? RowPat<TBN>::row(t) : ColPat<TBN>::col(t);  // B row / first column
+  int pa_n = 0, pa_h = 0, pa_w = 0;  // A row pixel (FWD: output, DGRAD: input)
   bool a_ok = false, b_ok = false;
-  int wr_r = 0, wr_s = 0, wr_c = 0;                // WGRAD: this thread's dW column (r, s, c)
+  int wr_r = 0, wr_s = 0, wr_c = 0;  // WGRAD: this thread's dW columns (r, s, c)
   if (MODE == C_FWD || MODE == C_DGRAD) {
-    const int m = m0 + ri_a;
+    const int m = m0 + ra_;
     a_ok = m < M;
     const int PW = MODE == C_FWD ? Wo : W, PH = MODE == C_FWD ? Ho : H;
     const int mm = a_ok ? m : 0;
@@ -82,10 +98,9 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
     const int tq = mm / PW;
     pa_h = tq % PH;
     pa_n = tq / PH;
-    b_ok = MODE == C_FWD ? (n0 + ri < K) : (n0 + c4 < C);
+    b_ok = n0 + rb_ < (MODE == C_FWD ? K : C);
   } else {
-    a_ok = m0 + c4 < K;
-    const int n = n0 + c4;
+    const int n = n0 + rb_;
     b_ok = n < Ng;
     const int nn = b_ok ? n : 0;
     const int rs = nn / C;
@@ -94,84 +109,100 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
     wr_s = rs - wr_r * S;
   }
 
-  float4 ra0, ra1, rb0, rb1;
+  float4 ra[LA], rb[LB];
   auto load = [&](int q) {
     if (MODE == C_FWD) {
       const int tap = q / cch, cq = q - tap * cch;
       const int r = tap / S, s = tap - r * S;
-      const int c = cq * BK + k4, ca = cq * BK + k4a;
       const int hi = pa_h * a.sh - a.ph + r * a.dh, wi = pa_w * a.sw - a.pw + s * a.dw;
       const bool pv = a_ok && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-      const float* src = a.x + (((long)pa_n * H + hi) * W + wi) * C + ca;
-      ra0 = pv && ca < C ? *(const float4*)src : f4zero();
-      if (TBM == 128) ra1 = pv && ca + 8 < C ? *(const float4*)(src + 8) : f4zero();
-      const float* wsrc = a.w + (((long)(n0 + ri) * a.R + r) * S + s) * C + c;
-      rb0 = b_ok && c < C ? *(const float4*)wsrc : f4zero();
-      rb1 = b_ok && c + 8 < C ? *(const float4*)(wsrc + 8) : f4zero();
+      const float* src = a.x + (((long)pa_n * H + hi) * W + wi) * C + cq * BK;
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const int c = cq * BK + RowPat<TBM>::k4(t, j);
+        ra[j] = pv && c < C ? *(const float4*)(src + RowPat<TBM>::k4(t, j)) : f4zero();
+      }
+      const float* wsrc = a.w + (((long)(n0 + rb_) * a.R + r) * S + s) * C + cq * BK;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const int c = cq * BK + RowPat<TBN>::k4(t, j);
+        rb[j] = b_ok && c < C ? *(const float4*)(wsrc + RowPat<TBN>::k4(t, j)) : f4zero();
+      }
     } else if (MODE == C_DGRAD) {
       const int tap = q / cch, cq = q - tap * cch;
       const int r = tap / S, s = tap - r * S;
-      const int k = cq * BK + k4a;
       const int hn = pa_h + a.ph - r * a.dh, wn_ = pa_w + a.pw - s * a.dw;
       const int ho = hn >= 0 ? hn / a.sh : -1, wo = wn_ >= 0 ? wn_ / a.sw : -1;
       const bool pv = a_ok && ho >= 0 && wo >= 0 && ho * a.sh == hn && wo * a.sw == wn_ &&
                       ho < Ho && wo < Wo;
-      const float* src = a.dy + (((long)pa_n * Ho + ho) * Wo + wo) * K + k;
+      const float* src = a.dy + (((long)pa_n * Ho + ho) * Wo + wo) * K + cq * BK;
       const bool kv = (K & 3) == 0;
-      ra0 = pv ? ld4(src, K - k, kv) : f4zero();
-      if (TBM == 128) ra1 = pv ? ld4(src + 8, K - k - 8, kv) : f4zero();
-      const int kb = cq * BK + kr;
-      const float* wsrc = a.w + (((long)kb * a.R + r) * S + s) * C + n0 + c4;
-      const long kstride = (long)a.R * S * C * 8;
-      rb0 = b_ok && kb < K ? *(const float4*)wsrc : f4zero();
-      rb1 = b_ok && kb + 8 < K ? *(const float4*)(wsrc + kstride) : f4zero();
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const int kk = RowPat<TBM>::k4(t, j);
+        ra[j] = pv ? ld4(src + kk, K - cq * BK - kk, kv) : f4zero();
+      }
+      const long kstride = (long)a.R * S * C;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const int kb = cq * BK + ColPat<TBN>::kr(t, j);
+        rb[j] = b_ok && kb < K ? *(const float4*)(a.w + ((long)kb * a.R + r) * S * C + (long)s * C +
+                                                  n0 + rb_)
+                               : f4zero();
+      }
+      (void)kstride;
     } else {
       const long P = (long)a.N * Ho * Wo;
-      const long p0 = (long)q * BK + kr, p1 = p0 + 8;
       const bool kv = (K & 3) == 0;
-      ra0 = p0 < P ? ld4(a.dy + p0 * K + m0 + c4, K - m0 - c4, kv) : f4zero();
-      ra1 = p1 < P ? ld4(a.dy + p1 * K + m0 + c4, K - m0 - c4, kv) : f4zero();
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const long p = (long)q * BK + ColPat<TBM>::kr(t, j);
+        ra[j] = p < P ? ld4(a.dy + p * K + m0 + ra_, K - m0 - ra_, kv) : f4zero();
+      }
       const int HoWo = Ho * Wo;
-      auto gather = [&](long p) -> float4 {
-        if (!b_ok || p >= P) return f4zero();
-        const int pn = (int)(p / HoWo), rem = (int)(p - (long)pn * HoWo);
-        const int ho = rem / Wo, wo = rem - ho * Wo;
-        const int hi = ho * a.sh - a.ph + wr_r * a.dh, wi = wo * a.sw - a.pw + wr_s * a.dw;
-        if ((unsigned)hi >= (unsigned)H || (unsigned)wi >= (unsigned)W) return f4zero();
-        return *(const float4*)(a.x + (((long)pn * H + hi) * W + wi) * C + wr_c);
-      };
-      rb0 = gather(p0);
-      rb1 = gather(p1);
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        const long p = (long)q * BK + ColPat<TBN>::kr(t, j);
+        float4 v = f4zero();
+        if (b_ok && p < P) {
+          const int pn = (int)(p / HoWo), rem = (int)(p - (long)pn * HoWo);
+          const int ho = rem / Wo, wo = rem - ho * Wo;
+          const int hi = ho * a.sh - a.ph + wr_r * a.dh, wi = wo * a.sw - a.pw + wr_s * a.dw;
+          if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
+            v = *(const float4*)(a.x + (((long)pn * H + hi) * W + wi) * C + wr_c);
+        }
+        rb[j] = v;
+      }
     }
   };
   auto store = [&](int buf) {
-    if (MODE == C_FWD || MODE == C_DGRAD) {
-      As[buf][k4a + 0][ri_a] = ra0.x; As[buf][k4a + 1][ri_a] = ra0.y;
-      As[buf][k4a + 2][ri_a] = ra0.z; As[buf][k4a + 3][ri_a] = ra0.w;
-      if (TBM == 128) {
-        As[buf][k4a + 8][ri_a] = ra1.x; As[buf][k4a + 9][ri_a] = ra1.y;
-        As[buf][k4a + 10][ri_a] = ra1.z; As[buf][k4a + 11][ri_a] = ra1.w;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) {
+      if (A_ROW) {
+        const int k4 = RowPat<TBM>::k4(t, j);
+        As[buf][k4 + 0][ra_] = ra[j].x; As[buf][k4 + 1][ra_] = ra[j].y;
+        As[buf][k4 + 2][ra_] = ra[j].z; As[buf][k4 + 3][ra_] = ra[j].w;
+      } else {
+        *(float4*)&As[buf][ColPat<TBM>::kr(t, j)][ra_] = ra[j];
       }
-    } else {
-      *(float4*)&As[buf][kr][c4] = ra0;
-      *(float4*)&As[buf][kr + 8][c4] = ra1;
     }
-    if (MODE == C_FWD) {
-      Bs[buf][k4 + 0][ri] = rb0.x; Bs[buf][k4 + 1][ri] = rb0.y;
-      Bs[buf][k4 + 2][ri] = rb0.z; Bs[buf][k4 + 3][ri] = rb0.w;
-      Bs[buf][k4 + 8][ri] = rb1.x; Bs[buf][k4 + 9][ri] = rb1.y;
-      Bs[buf][k4 + 10][ri] = rb1.z; Bs[buf][k4 + 11][ri] = rb1.w;
-    } else {
-      *(float4*)&Bs[buf][kr][c4] = rb0;
-      *(float4*)&Bs[buf][kr + 8][c4] = rb1;
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      if (B_ROW) {
+        const int k4 = RowPat<TBN>::k4(t, j);
+        Bs[buf][k4 + 0][rb_] = rb[j].x; Bs[buf][k4 + 1][rb_] = rb[j].y;
+        Bs[buf][k4 + 2][rb_] = rb[j].z; Bs[buf][k4 + 3][rb_] = rb[j].w;
+      } else {
+        *(float4*)&Bs[buf][ColPat<TBN>::kr(t, j)][rb_] = rb[j];
+      }
     }
   };
 
-  f32x16 acc[FM][2];
+  f32x16 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
@@ -187,13 +218,16 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
       for (int kk = 0; kk < 8; ++kk) {
         // MFMA k-slot hk of step kk reads LDS row 8·hk + kk (same permutation for A and B)
         const float* ar = &As[buf][8 * hk + kk][wm * (TBM / 2) + l31];
-        const float* br = &Bs[buf][8 * hk + kk][wn * 64 + l31];
-        const float b0 = br[0], b1 = br[32];
+        const float* br = &Bs[buf][8 * hk + kk][wn * (TBN / 2) + l31];
+        float bv[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) bv[fn] = br[32 * fn];
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
           const float av = ar[32 * fm];
-          acc[fm][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b0, acc[fm][0], 0, 0, 0);
-          acc[fm][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b1, acc[fm][1], 0, 0, 0);
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[fn], acc[fm][fn], 0, 0, 0);
         }
       }
       if (more) store(buf ^ 1);
@@ -203,8 +237,8 @@ __global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int 
 
   // ---- epilogue: lane holds column l31 of each 32×32 block, rows (v&3) + 8(v>>2) + 4·hk
 #pragma unroll
-  for (int fn = 0; fn < 2; ++fn) {
-    const int col = n0 + wn * 64 + fn * 32 + l31;
+  for (int fn = 0; fn < FN; ++fn) {
+    const int col = n0 + wn * (TBN / 2) + fn * 32 + l31;
     float s0 = 0.f, s1 = 0.f;
     float bias = 0.f;
     if (MODE == C_FWD && a.bias && col < K) bias = a.bias[col];
@@ -621,6 +655,13 @@ int conv_f32_wgrad_splits(const ConvF32Args& a) {
   return splits;
 }
 
+static int g_f32_tile[2] = {0, 0};
+void conv_f32_set_tile(int tbm, int tbn) {
+  const bool ok = (tbm == 64 || tbm == 128) && (tbn == 64 || tbn == 128);
+  g_f32_tile[0] = ok ? tbm : 0;
+  g_f32_tile[1] = ok ? tbn : 0;
+}
+
 static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
   int M, Ng, nq, cch = 1;
   if (mode == C_FWD) {
@@ -631,31 +672,52 @@ static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
     M = a.K; Ng = a.R * a.S * a.C; nq = (int)(((long)a.N * a.Ho * a.Wo + BK - 1) / BK);
   }
   if (M <= 0 || Ng <= 0 || nq <= 0) return;
-  int tiles_m = (M + BM - 1) / BM;
-  const int tiles_n = (Ng + BN - 1) / BN;
-  // fewer than two 128-row tiles per CU: 64-row tiles (twice the workgroups, each with half the
-  // work) — TDL_F32_BM64=0 turns it off
-  static const bool bm64_on = getenv("TDL_F32_BM64") == nullptr || atoi(getenv("TDL_F32_BM64"));
-  const bool bm64 = mode != C_WGRAD && bm64_on && (long)tiles_m * tiles_n < 512;
-  if (bm64) tiles_m = (M + 63) / 64;
+  // tile: 128×128, unless that leaves the chip under-filled (FWD / DGRAD): then the shape among
+  // 128×128 / 64×128 / 128×64 / 64×64 whose workgroup count best fills whole waves of 256 CUs
+  // (ties: the bigger tile) — TDL_F32_TILE=0 keeps 128×128
+  static const bool small_on = getenv("TDL_F32_TILE") == nullptr || atoi(getenv("TDL_F32_TILE"));
+  int tbm = 128, tbn = 128;
+  if (mode != C_WGRAD && g_f32_tile[0] > 0) {  // forced (tests: every tile shape)
+    tbm = g_f32_tile[0];
+    tbn = g_f32_tile[1];
+  } else if (mode != C_WGRAD && small_on) {
+    const int cand[4][2] = {{128, 128}, {64, 128}, {128, 64}, {64, 64}};
+    double best = -1.0;
+    for (const auto& cdm : cand) {
+      const long nt = (long)((M + cdm[0] - 1) / cdm[0]) * ((Ng + cdm[1] - 1) / cdm[1]);
+      const long slots = 256L * ((nt + 255) / 256);
+      // fill of the last wave of workgroups; a bigger tile is worth ~10 % of fill
+      const double score = (double)nt / slots + (cdm[0] * cdm[1] == 128 * 128 ? 0.1 : cdm[0] * cdm[1] == 64 * 64 ? 0.0 : 0.05);
+      if (score > best + 1e-9) {
+        best = score;
+        tbm = cdm[0];
+        tbn = cdm[1];
+      }
+    }
+  }
+  const int tiles_m = (M + tbm - 1) / tbm;
+  const int tiles_n = (Ng + tbn - 1) / tbn;
   const long tiles = (long)tiles_m * tiles_n;
   int qps = nq, splits = 1;
   if (mode == C_WGRAD) wgrad_plan(a, &qps, &splits);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
-  if (mode == C_FWD && bm64)
-    hipLaunchKernelGGL((conv_f32_kernel<C_FWD, 64>), grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
-                       tiles_n);
-  else if (mode == C_FWD)
-    hipLaunchKernelGGL(conv_f32_kernel<C_FWD>, grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps, tiles_n);
-  else if (mode == C_DGRAD && bm64)
-    hipLaunchKernelGGL((conv_f32_kernel<C_DGRAD, 64>), grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
-                       tiles_n);
-  else if (mode == C_DGRAD)
-    hipLaunchKernelGGL(conv_f32_kernel<C_DGRAD>, grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
-                       tiles_n);
-  else
-    hipLaunchKernelGGL(conv_f32_kernel<C_WGRAD>, grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps,
-                       tiles_n);
+#define TDL_F32_LAUNCH(MODE_, TM_, TN_)                                                         \
+  hipLaunchKernelGGL((conv_f32_kernel<MODE_, TM_, TN_>), grid, dim3(CT), 0, st, a, M, Ng, nq, cch, qps, \
+                     tiles_n)
+  if (mode == C_WGRAD) {
+    TDL_F32_LAUNCH(C_WGRAD, 128, 128);
+  } else if (mode == C_FWD) {
+    if (tbm == 128 && tbn == 128) TDL_F32_LAUNCH(C_FWD, 128, 128);
+    else if (tbm == 64 && tbn == 128) TDL_F32_LAUNCH(C_FWD, 64, 128);
+    else if (tbm == 128) TDL_F32_LAUNCH(C_FWD, 128, 64);
+    else TDL_F32_LAUNCH(C_FWD, 64, 64);
+  } else {
+    if (tbm == 128 && tbn == 128) TDL_F32_LAUNCH(C_DGRAD, 128, 128);
+    else if (tbm == 64 && tbn == 128) TDL_F32_LAUNCH(C_DGRAD, 64, 128);
+    else if (tbm == 128) TDL_F32_LAUNCH(C_DGRAD, 128, 64);
+    else TDL_F32_LAUNCH(C_DGRAD, 64, 64);
+  }
+#undef TDL_F32_LAUNCH
 }
 
 void conv_f32_fwd_launch(const ConvF32Args& a, hipStream_t st) { conv_f32_launch(C_FWD, a, st); }

@@ -271,6 +271,8 @@ struct ConvF32Args {
   float* slab;         // WGRAD with conv_f32_wgrad_splits(a) > 1: fp32 scratch of splits·K·R·S·C
 };
 void conv_f32_fwd_launch(const ConvF32Args& a, hipStream_t st);
+// FWD / DGRAD workgroup tile override (64 or 128 each; anything else: automatic choice)
+void conv_f32_set_tile(int tbm, int tbn);
 void conv_f32_dgrad_launch(const ConvF32Args& a, hipStream_t st);
 // WGRAD splits the pixel reduction: each split writes its partial dW slab (plain stores), one
 // reduction pass sums the slabs into dW (no memset, no atomics)

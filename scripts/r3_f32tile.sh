@@ -1,0 +1,11 @@
+# round 3: fp32 conv tile shapes (tests + A/B on the reference preset)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_f32_gpu.py -x -q --timeout 400 --timeout-method thread > gpurun_out/pytest_f32.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -1 gpurun_out/pytest_f32.log
+[ $rc -ge 124 ] && exit $rc
+for v in 1 0 1 0; do
+  TDL_F32_TILE=$v timeout -k 10 300 python bench.py --model deeplab_ref --dtype fp32 --steps 30 --warmup 5 > gpurun_out/dlf32_t$v.log 2>&1 || exit $?
+  echo "tile auto=$v $(tail -1 gpurun_out/dlf32_t$v.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+done
+echo done

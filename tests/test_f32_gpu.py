@@ -68,6 +68,32 @@ def test_conv_f32_fwd_dgrad_wgrad(gpu, shape):
     assert rel_err(dw, C.ref_conv_wgrad(dy, x, tuple(w.shape), g)) < TOL
 
 
+@pytest.mark.parametrize("tile", [(128, 128), (64, 128), (128, 64), (64, 64)])
+def test_conv_f32_tile_shapes(gpu, tile):
+    """Every FWD / DGRAD workgroup tile shape of the fp32 conv kernel (forced) against PyTorch."""
+    ext().conv_f32_set_tile(*tile)
+    try:
+        for shape in [(3, 13, 13, 64, 136, 3, 3, 1, (2, 2, 2, 2), 2),
+                      (2, 15, 15, 24, 200, 1, 1, 2, (0, 0, 0, 0), 1)]:
+            N, H, W, Ci, K, R, S, st, pad, dil = shape
+            g = C.ConvGeom((st, st), pad, (dil, dil))
+            torch.manual_seed(1)
+            x = torch.randn(N, H, W, Ci)
+            w = torch.randn(K, R, S, Ci) / (R * S * Ci) ** 0.5
+            b = torch.randn(K)
+            Ho, Wo = g.out_hw(H, W, R, S)
+            dy = torch.randn(N, Ho, Wo, K)
+            st_ = torch.zeros(2, K, device=gpu)
+            y = C.conv_fwd(x.to(gpu), w.to(gpu), g, bias=b.to(gpu), relu=True, stats=st_)
+            ref = torch.relu(C.ref_conv_fwd(x, w, g, b))
+            assert rel_err(y, ref) < TOL, (tile, shape)
+            assert rel_err(st_[0], ref.reshape(-1, K).sum(0)) < 1e-4
+            dx = C.conv_dgrad(dy.to(gpu), w.to(gpu), tuple(x.shape), g)
+            assert rel_err(dx, C.ref_conv_dgrad(dy, w, tuple(x.shape), g)) < TOL, (tile, shape)
+    finally:
+        ext().conv_f32_set_tile(0, 0)
+
+
 def test_conv_f32_epilogues(gpu):
     """bias + residual + ReLU + BN statistics in the forward epilogue; dgrad accumulate (join);
     wgrad accumulate + bias gradient."""
