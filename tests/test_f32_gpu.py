@@ -333,3 +333,32 @@ def test_xception41_fp32_gpu_matches_cpu_oracle(gpu):
     cg = torch.nn.functional.cosine_similarity(tc.flat.grad.double(),
                                                tg.flat.grad.cpu().double(), dim=0).item()
     assert cg > 0.99999, cg
+
+
+@pytest.mark.timeout(300)
+def test_deeplab_fp32_graph_replay_matches_eager(gpu):
+    """The fp32 reference-preset step captured as one HIP graph (split-slab weight gradients,
+    side-stream wgrads, Adam) replays like the eager step."""
+    torch.manual_seed(21)
+    nets = [models.DeepLabResNet(model_name="m", input_shape=(101, 101)) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    ta, tb = [Trainer(n, lovasz_hinge, gpu, "adam", dict(lr=1e-4), lowp_dtype=None)
+              for n in nets]
+    with torch.no_grad():
+        tb.flat.master.copy_(ta.flat.master)
+    ta.train_mode = tb.train_mode = False
+    x, y = segmentation_batch(4, device=gpu, dtype=torch.float32, seed=5)
+    tb.capture(x, y, warmup=2)
+    for _ in range(2):
+        ta.train_step(x, y)
+    torch.cuda.synchronize()
+    m0 = ta.flat.master.clone()
+    for _ in range(3):
+        la, _ = ta.train_step(x, y)
+        lb, _ = tb.replay()
+    torch.cuda.synchronize()
+    ua, ub = ta.flat.master - m0, tb.flat.master - m0
+    assert ua.norm() > 0 and torch.isfinite(ub).all()
+    cos = torch.nn.functional.cosine_similarity(ua, ub, dim=0).item()
+    assert cos > 0.999, cos
+    torch.testing.assert_close(float(lb), float(la), rtol=1e-4, atol=1e-5)
