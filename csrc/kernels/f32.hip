@@ -66,8 +66,11 @@ struct ColPat {  // "col" staging: first column, and the k row of load j
   __device__ __forceinline__ static int kr(int t, int j) { return (t + 256 * j) / (R / 4); }
 };
 
+// (launch bounds: ≥ 2 waves per SIMD — without it hipcc parks the accumulators in AGPRs next to
+// ~140–200 VGPRs, 1–2 waves per SIMD; with it 106–139 VGPRs and no AGPRs: 3–4 waves per SIMD,
+// no scratch)
 template <int MODE, int TBM = BM, int TBN = BN>
-__global__ void __launch_bounds__(CT) conv_f32_kernel(ConvF32Args a, int M, int Ng, int nq,
+__global__ void __launch_bounds__(CT, 2) conv_f32_kernel(ConvF32Args a, int M, int Ng, int nq,
                                                       int cch, int qps, int tiles_n) {
   static_assert((TBM == 64 || TBM == 128) && (TBN == 64 || TBN == 128), "tiles of 64 / 128");
   constexpr int FM = TBM / 64, FN = TBN / 64;  // 32×32 blocks per wave
