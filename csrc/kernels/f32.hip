@@ -115,7 +115,9 @@ __global__ void __launch_bounds__(CT, 2) conv_f32_kernel(ConvF32Args a, int M, i
   float4 ra[LA], rb[LB];
   auto load = [&](int q) {
     if (MODE == C_FWD) {
-      const int tap = q / cch, cq = q - tap * cch;
+      // q is uniform: the tap / chunk decomposition stays in scalar registers
+      const int qu = __builtin_amdgcn_readfirstlane(q);
+      const int tap = qu / cch, cq = qu - tap * cch;
       const int r = tap / S, s = tap - r * S;
       const int hi = pa_h * a.sh - a.ph + r * a.dh, wi = pa_w * a.sw - a.pw + s * a.dw;
       const bool pv = a_ok && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
@@ -132,10 +134,13 @@ __global__ void __launch_bounds__(CT, 2) conv_f32_kernel(ConvF32Args a, int M, i
         rb[j] = b_ok && c < C ? *(const float4*)(wsrc + RowPat<TBN>::k4(t, j)) : f4zero();
       }
     } else if (MODE == C_DGRAD) {
-      const int tap = q / cch, cq = q - tap * cch;
+      const int qu = __builtin_amdgcn_readfirstlane(q);
+      const int tap = qu / cch, cq = qu - tap * cch;
       const int r = tap / S, s = tap - r * S;
       const int hn = pa_h + a.ph - r * a.dh, wn_ = pa_w + a.pw - s * a.dw;
-      const int ho = hn >= 0 ? hn / a.sh : -1, wo = wn_ >= 0 ? wn_ / a.sw : -1;
+      // (stride 1, the common case, needs no per-lane division; the branch is uniform)
+      const int ho = hn < 0 ? -1 : a.sh == 1 ? hn : hn / a.sh;
+      const int wo = wn_ < 0 ? -1 : a.sw == 1 ? wn_ : wn_ / a.sw;
       const bool pv = a_ok && ho >= 0 && wo >= 0 && ho * a.sh == hn && wo * a.sw == wn_ &&
                       ho < Ho && wo < Wo;
       const float* src = a.dy + (((long)pa_n * Ho + ho) * Wo + wo) * K + cq * BK;
@@ -168,8 +173,8 @@ __global__ void __launch_bounds__(CT, 2) conv_f32_kernel(ConvF32Args a, int M, i
         const long p = (long)q * BK + ColPat<TBN>::kr(t, j);
         float4 v = f4zero();
         if (b_ok && p < P) {
-          const int pn = (int)(p / HoWo), rem = (int)(p - (long)pn * HoWo);
-          const int ho = rem / Wo, wo = rem - ho * Wo;
+          const int pn = (int)fdiv((uint32_t)p, a.fd_HoWo), rem = (int)p - pn * HoWo;
+          const int ho = (int)fdiv((uint32_t)rem, a.fd_Wo), wo = rem - ho * Wo;
           const int hi = ho * a.sh - a.ph + wr_r * a.dh, wi = wo * a.sw - a.pw + wr_s * a.dw;
           if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
             v = *(const float4*)(a.x + (((long)pn * H + hi) * W + wi) * C + wr_c);
@@ -665,7 +670,10 @@ void conv_f32_set_tile(int tbm, int tbn) {
   g_f32_tile[1] = ok ? tbn : 0;
 }
 
-static void conv_f32_launch(int mode, const ConvF32Args& a, hipStream_t st) {
+static void conv_f32_launch(int mode, const ConvF32Args& a0, hipStream_t st) {
+  ConvF32Args a = a0;
+  a.fd_HoWo = make_fastdiv((uint32_t)std::max(1, a.Ho * a.Wo));
+  a.fd_Wo = make_fastdiv((uint32_t)std::max(1, a.Wo));
   int M, Ng, nq, cch = 1;
   if (mode == C_FWD) {
     M = a.N * a.Ho * a.Wo; Ng = a.K; cch = (a.C + BK - 1) / BK; nq = a.R * a.S * cch;

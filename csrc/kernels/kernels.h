@@ -269,6 +269,7 @@ struct ConvF32Args {
   int relu;            // FWD
   int accumulate;      // DGRAD: dx += …; WGRAD: dW += … (else overwritten)
   float* slab;         // WGRAD with conv_f32_wgrad_splits(a) > 1: fp32 scratch of splits·K·R·S·C
+  FastDiv fd_HoWo, fd_Wo;  // (launcher) magic divisors of the WGRAD pixel decomposition
 };
 void conv_f32_fwd_launch(const ConvF32Args& a, hipStream_t st);
 // FWD / DGRAD workgroup tile override (64 or 128 each; anything else: automatic choice)
