@@ -1,5 +1,6 @@
 """Data-parallel logic on the CPU (SURVEY §7.5 "Dist logic"): bucket layout, launch order with a
-fake communicator, and real multi-process gloo training equivalence (world_size 2)."""
+fake communicator, and real multi-process gloo training equivalence (world_size 2 and 4), and
+the driver's own ``torch.distributed.run`` launch of bench.py."""
 import os
 
 import pytest
@@ -82,7 +83,7 @@ def test_bucketer_reset_between_steps():
     assert log == list(range(len(b.buckets))) * 2
 
 
-def _dp_worker(rank, tmpdir):
+def _dp_worker(rank, tmpdir, world=2):
     import torch
     from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown
     from tensorflowdistributedlearning_amd.engine.trainer import Trainer
@@ -98,7 +99,8 @@ def _dp_worker(rank, tmpdir):
     g = torch.Generator().manual_seed(7)
     x = torch.randn(8, 8, 8, 8, generator=g)
     y = torch.randint(0, 5, (8,), generator=g)
-    xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+    per = 8 // world
+    xs, ys = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
     for _ in range(3):
         tr.train_step(xs, ys)
     torch.save(tr.flat.master.clone(), os.path.join(tmpdir, f"rank{rank}.pt"))
@@ -106,12 +108,14 @@ def _dp_worker(rank, tmpdir):
 
 
 @pytest.mark.timeout(240)
-def test_gloo_dp_equals_large_batch(tmp_path):
-    """2 ranks × batch 4 with mean-gradient all-reduce == 1 process × batch 8."""
-    launcher.spawn(_dp_worker, 2, args=(str(tmp_path),))
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_dp_equals_large_batch(tmp_path, world):
+    """W ranks × batch 8/W with mean-gradient all-reduce == 1 process × batch 8 (rank 0's
+    parameters broadcast at start: rank 1 starts from different weights)."""
+    launcher.spawn(_dp_worker, world, args=(str(tmp_path), world))
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
-    assert torch.equal(r0, r1)  # replicas stay identical
+    for r in range(1, world):  # replicas stay identical
+        assert torch.equal(r0, torch.load(tmp_path / f"rank{r}.pt", weights_only=True))
     from tensorflowdistributedlearning_amd.engine.trainer import Trainer
     from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy
     torch.manual_seed(123)
@@ -210,6 +214,34 @@ def test_bench_self_spawns_ranks_cpu(tmp_path):
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["comm"] == "gloo" and out["config"]["global_batch"] == 4
     assert out["value"] > 0 and out["steps"] == 1 and out["warmup"] == 1
+
+
+@pytest.mark.timeout(300)
+def test_bench_under_torchrun_driver_form_cpu(tmp_path):
+    """The driver's exact multi-GPU launch (`python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...`) with
+    N = 4 gloo ranks: bench.py takes the launcher's ranks (no self-spawn), the barrier-bracketed
+    timing covers every rank and only rank 0 prints the JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(launcher.free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "4", "--model", "resnet18",
+           "--image-size", "32", "--batch", "2", "--steps", "2", "--warmup", "1"]
+    env = _bench_env()
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4"
+    assert out["config"]["global_batch"] == 8 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert abs(out["value"] - 8 * 1e3 / out["ms_per_step"]) / out["value"] < 0.01
 
 
 @pytest.mark.timeout(300)

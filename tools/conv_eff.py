@@ -25,7 +25,9 @@ def conv_list(model, batch, image):
         fl = 2.0 * batch * Ho * Wo * K * C * mod.k[0] * mod.k[1]
         st = mod.stride[0] if isinstance(mod.stride, tuple) else mod.stride
         dl = mod.dilation[0]
-        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{st}" + (f" d{dl}" if dl > 1 else ""), fl))
+        # minimum HBM bytes (bf16): input + output activations + weights, each touched once
+        by = 2.0 * (batch * (H * W * C + Ho * Wo * K) + K * C * mod.k[0] * mod.k[1])
+        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{st}" + (f" d{dl}" if dl > 1 else ""), fl, by))
     for mod in m.modules():
         if isinstance(mod, Conv2d):
             mod.register_forward_hook(hook)
@@ -42,7 +44,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--marker", default="sgd_kernel", help="optimizer kernel delimiting steps")
+    ap.add_argument("--hbm", type=float, default=5.6, help="achievable HBM TB/s")
+    ap.add_argument("--mfma", type=float, default=2.3, help="achievable dense bf16 PFLOP/s")
     a = ap.parse_args()
+
+    def bound_us(fl, by):
+        return max(fl / (a.mfma * 1e15), by / (a.hbm * 1e12)) * 1e6
     convs = conv_list(a.model, a.batch, a.image)
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
@@ -56,25 +63,38 @@ def main():
     print(f"{len(convs)} convs; kernels fwd {len(by[0])} dgrad {len(by[1])} wgrad {len(by[2])}")
     fw = by[0]
     tot = {}
-    if len(fw) == len(convs):
-        print("forward:")
+    # forward in forward order; dgrad (no stem: its input is the image) and wgrad in reverse
+    lists = {0: convs, 1: [c for c in convs[1:]][::-1], 2: convs[::-1]}
+    grand = [0.0, 0.0]
+    for mode, nm in ((0, "forward"), (1, "dgrad"), (2, "wgrad")):
+        ks, cl = by[mode], lists[mode]
+        if len(ks) != len(cl):
+            agg = {}
+            for d, impl in ks:
+                e = agg.setdefault(impl, [0, 0.0])
+                e[0] += 1
+                e[1] += d
+            print(f"{nm}: count mismatch ({len(ks)} kernels, {len(cl)} convs): " +
+                  ", ".join(f"{impl} x{n} {d:.1f} us" for impl, (n, d) in sorted(agg.items())))
+            continue
+        print(f"{nm}:  (bound = max(FLOP / {a.mfma} PF, min bytes / {a.hbm} TB/s))")
         agg = {}
-        for (d, impl), (name, fl) in zip(fw, convs):
-            k = (name, impl)
-            e = agg.setdefault(k, [0, 0.0, fl])
+        for (d, impl), (name, fl, bts) in zip(ks, cl):
+            e = agg.setdefault((name, impl), [0, 0.0, fl, bts])
             e[0] += 1
             e[1] += d
-        for (name, impl), (n, d, fl) in sorted(agg.items(), key=lambda x: -x[1][1]):
-            print(f"  {name:32s} {impl:5s} x{n:2d} {d / n:7.1f} us  {fl / (d / n) / 1e6:7.1f} TF/s  total {d:7.1f} us")
-    else:
-        print("forward count mismatch")
-    for mode, nm in ((1, "dgrad"), (2, "wgrad")):
-        agg = {}
-        for d, impl in by[mode]:
-            e = agg.setdefault(impl, [0, 0.0])
-            e[0] += 1
-            e[1] += d
-        print(f"{nm}: " + ", ".join(f"{impl} x{n} {d:.1f} us" for impl, (n, d) in sorted(agg.items())))
+        tot = [0.0, 0.0]
+        for (name, impl), (n, d, fl, bts) in sorted(agg.items(), key=lambda x: -x[1][1]):
+            b = bound_us(fl, bts)
+            tot[0] += d
+            tot[1] += b * n
+            print(f"  {name:32s} {impl:5s} x{n:2d} {d / n:7.1f} us  {fl / (d / n) / 1e6:7.1f} TF/s "
+                  f"{bts / (d / n) / 1e6:5.2f} TB/s  bound {b:6.1f} us ({b / (d / n) * 100:3.0f} %)  total {d:7.1f} us")
+        print(f"  sum {tot[0] / 1e3:.2f} ms, bound {tot[1] / 1e3:.2f} ms ({tot[1] / tot[0] * 100:.0f} %)")
+        grand[0] += tot[0]
+        grand[1] += tot[1]
+    if grand[0]:
+        print(f"all matched convs: {grand[0] / 1e3:.2f} ms vs bound {grand[1] / 1e3:.2f} ms")
 
 
 if __name__ == "__main__":
