@@ -117,10 +117,18 @@ def main():
                     help="GPU compute precision: bf16 (fused bf16 kernels, fp32 accumulation / "
                          "master weights) or fp32 (fp32 operands on the fp32 MFMA end to end — the "
                          "reference's own precision, for the like-for-like deeplab_ref comparison)")
+    ap.add_argument("--mode", choices=("train", "infer"), default="train",
+                    help="train (the headline: full training step) or infer (serving: eval-mode "
+                         "forward under no_grad with every BatchNorm folded into its conv, "
+                         "models/layers.ConvBN; images/sec of forward passes)")
+    ap.add_argument("--no-fold", action="store_true",
+                    help="with --mode infer: keep the unfolded conv + BN-apply eval path (A/B)")
     ap.add_argument("--profile-phases", action="store_true",
                     help="also print per-phase step times (forward/backward/comm_wait/optimizer, "
                          "device events) to stderr")
     args = ap.parse_args()
+    if args.no_fold:
+        os.environ["TDL_BN_FOLD"] = "0"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_workers(args.gpus, sys.argv[1:]))
@@ -200,7 +208,35 @@ def main():
     def step():
         tr.train_step(x, y)
 
-    if args.graph:
+    if args.mode == "infer":
+        if args.model == "deeplab_ref" or args.fp8:
+            raise SystemExit("--mode infer: the ImageNet models, bf16 / fp32")
+        model.eval()
+        metric = ("inference images/sec (whole node), " + args.model
+                  + f" {args.image_size}x{args.image_size} " + ("bf16" if gpu_bf16 else "fp32")
+                  + (" (BN unfolded)" if args.no_fold else " (BN folded into the convs)"))
+        cfg.update(optimizer=None, loss=None, mode="infer", bn_folded=not args.no_fold)
+        base = None
+
+        @torch.no_grad()
+        def step():
+            model(x)
+
+    if args.graph and args.mode == "infer":
+        step()
+        torch.cuda.synchronize(dev)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        gr = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(gr):
+            model(x)
+        step = gr.replay
+        for _ in range(args.warmup):
+            step()
+    elif args.graph:
         tr.capture(x, y, warmup=args.warmup)  # W eager warm-up steps, then the capture
         step = tr.replay
         step()  # first replay (graph upload) stays untimed
@@ -239,7 +275,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
-            "baseline": ("BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
+            "baseline": (None if base is None else
+                         "BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
                          "ResNet-50 number)" if args.model != "deeplab_ref" else
                          "BASELINE.md measured 90.7 img/s on 2 GPUs, scaled per GPU"),
             "dtype": fp8_desc if args.fp8 else dtype_name,

@@ -12,7 +12,9 @@ import math
 import torch
 import torch.nn as nn
 
-from ..ops.conv import ConvGeom, conv2d, same_padding, symmetric_padding, row_pack
+import os
+
+from ..ops.conv import ConvGeom, conv2d, conv_fwd, same_padding, symmetric_padding, row_pack
 from ..ops.bn import batch_norm_act, batch_norm_act_into
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
@@ -221,6 +223,18 @@ class Conv2d(nn.Module):
                           want_stats, self, join, residual, res_link)
         return (y, stats) if want_stats else y
 
+    def _load_from_state_dict(self, *args, **kw):
+        # derived copies (channel-padded / row-packed weights, folded BN) key on the parameter
+        # version: a load outside the optimizer must refresh them too
+        _params.bump_version()
+        return super()._load_from_state_dict(*args, **kw)
+
+    def forward_folded(self, x, w, bias, relu, residual=None):
+        """Inference forward with a given compute weight and fp32 bias (ConvBN's folded BN):
+        act(conv(x, w) + bias [+ residual]) in the conv epilogue, no autograd record."""
+        return conv_fwd(x, w, self.geom(x.shape[1], x.shape[2]), bias=bias, relu=relu,
+                        residual=residual)
+
     def extra_repr(self):
         return (f"{self.cin}->{self.cout}, k={self.k}, s={self.stride}, d={self.dilation}, "
                 f"pad={self.padding}, bias={self.bias is not None}, relu={self.relu}")
@@ -268,18 +282,26 @@ class RowPackedConv2d(Conv2d):
             self._packed_version = v
         return self._packed
 
-    def forward(self, x, want_stats=False, join=None):
-        H, W = x.shape[1], x.shape[2]
+    def packed_geom(self, H, W):
+        """(k×1 conv geometry over the packed rows, left padding, output width)."""
         pg = self._pgeom.get((H, W))
         if pg is None:
             pt, pb, pl, pr = resolve_padding(self.padding, H, W, self.k[0], self.k[1],
                                              self.stride, self.dilation)
             Wo = (W + pl + pr - self.k[1]) // self.stride[1] + 1
             pg = self._pgeom[(H, W)] = (ConvGeom((self.stride[0], 1), (pt, pb, 0, 0)), pl, Wo)
-        g, pl, Wo = pg
+        return pg
+
+    def forward(self, x, want_stats=False, join=None):
+        g, pl, Wo = self.packed_geom(x.shape[1], x.shape[2])
         t = row_pack(x, self.cin, self.k[1], self.stride[1], pl, Wo, self._cp)
         y, stats = conv2d(t, self.weight, self.bias, g, self.relu, want_stats, self, join)
         return (y, stats) if want_stats else y
+
+    def forward_folded(self, x, w, bias, relu, residual=None):
+        g, pl, Wo = self.packed_geom(x.shape[1], x.shape[2])
+        t = row_pack(x, self.cin, self.k[1], self.stride[1], pl, Wo, self._cp)
+        return conv_fwd(t, w, g, bias=bias, relu=relu, residual=residual)
 
 
 class BatchNorm(nn.Module):
@@ -344,8 +366,35 @@ class BatchNorm(nn.Module):
                               training=self.training, res_join=res_join, link=link)
 
 
+def bn_fold_enabled():
+    """Inference BN folding (ConvBN, eval mode, no autograd): on unless TDL_BN_FOLD=0."""
+    return os.environ.get("TDL_BN_FOLD", "1") != "0"
+
+
+def fold_bn_affine(bn, device):
+    """(s, b') fp32 over ``bn.c_phys`` channels: eval-mode BN(y) = y·s + b' with
+    s = γ/√(σ²+ε), b' = β − μ·s (zero on padding channels)."""
+    gamma, beta = bn.phys_params()
+    s = torch.zeros(bn.c_phys, dtype=torch.float32, device=device)
+    sh = torch.zeros(bn.c_phys, dtype=torch.float32, device=device)
+    inv = torch.rsqrt(bn.running_var.float().to(device) + bn.eps)
+    if gamma is not None:
+        inv = inv * gamma[: bn.c].float().to(device)
+    s[: bn.c] = inv
+    sh[: bn.c] = beta[: bn.c].float().to(device) - bn.running_mean.float().to(device) * inv
+    return s, sh
+
+
 class ConvBN(nn.Module):
-    """conv → BN → [+residual] → [ReLU] with BN statistics accumulated in the conv epilogue."""
+    """conv → BN → [+residual] → [ReLU] with BN statistics accumulated in the conv epilogue.
+
+    Inference (eval mode under ``torch.no_grad``): the BN's moving statistics are folded into
+    the conv — W' = W·s, b' = β − μ·s with s = γ/√(σ²+ε) per output channel — so the layer is one
+    conv whose epilogue adds b' (+ the residual) and applies the ReLU: no BN pass at all (the
+    reference's eval graph runs slim.batch_norm(is_training=False) as separate ops,
+    core/resnet.py:373-386).  The folded weights are cached per parameter version and dropped on
+    every train()/eval() switch and state-dict load (the moving statistics change only in
+    training).  ``TDL_BN_FOLD=0`` keeps the unfolded conv + BN-apply path."""
 
     def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, relu=True,
                  bn_decay=0.997, bn_eps=1e-5, bn_scale=True, zero_init_gamma=False, init="he_tf",
@@ -358,10 +407,40 @@ class ConvBN(nn.Module):
                             c_phys=self.conv._cout_store)
         self.relu = relu
 
+    # inference BN folding ------------------------------------------------------------------------
+    def train(self, mode=True):
+        self.__dict__.pop("_fold", None)
+        return super().train(mode)
+
+    def _load_from_state_dict(self, *args, **kw):
+        self.__dict__.pop("_fold", None)
+        _params.bump_version()
+        return super()._load_from_state_dict(*args, **kw)
+
+    def folded_params(self, dtype, device):
+        """(W·s in the compute dtype, fp32 b') over the stored (padded) output channels."""
+        key = (_params.version(), dtype, device)
+        c = self.__dict__.get("_fold")
+        if c is not None and c[0] == key:
+            return c[1], c[2]
+        bn, conv = self.bn, self.conv
+        with torch.no_grad():
+            s, sh = fold_bn_affine(bn, device)
+            if conv.bias is not None:
+                sh += conv.compute_bias().float().to(device) * s
+            w = conv.compute_weight(dtype)
+            wf = (w.float() * s.view(-1, 1, 1, 1)).to(dtype).contiguous()
+        self.__dict__["_fold"] = (key, wf, sh.contiguous())
+        return wf, self.__dict__["_fold"][2]
+
     def forward(self, x, residual=None, join=None, res_join=None, into=None):
         """``join``: gradient join for x (ops/gradjoin.py); ``res_join``: for the residual.
         ``into`` = (buf, c0): write act(BN(conv(x))) into ``buf[..., c0:c0+C]`` (a concat
         buffer, ops/bn.batch_norm_act_into) and return ``buf``."""
+        if (not self.training and into is None and not torch.is_grad_enabled()
+                and bn_fold_enabled()):
+            wf, bf = self.folded_params(x.dtype, x.device)
+            return self.conv.forward_folded(x, wf, bf, self.relu, residual)
         if self.training:
             y, stats = self.conv(x, want_stats=True, join=join)
         else:
@@ -452,3 +531,11 @@ class DepthwiseConv2d(nn.Module):
         return depthwise_conv2d(x, self.weight, self.bias, ConvGeom(self.stride, pad,
                                                                     self.dilation), self.relu,
                                 relu_in, want_stats, join)
+
+    def forward_folded(self, x, w, bias, relu, relu_in=False):
+        """Inference forward with a given weight (x's dtype) and fp32 bias: a BN folded into
+        the depthwise conv (models/xception.SeparableConvBN), no autograd record."""
+        pad = resolve_padding(self.padding, x.shape[1], x.shape[2], self.k, self.k, self.stride,
+                              self.dilation)
+        return depthwise_conv2d(x, w, bias, ConvGeom(self.stride, pad, self.dilation), relu,
+                                relu_in)

@@ -17,7 +17,9 @@ import os
 import torch
 import torch.nn as nn
 
-from .layers import ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear
+from . import params as _params
+from .layers import (ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear, bn_fold_enabled,
+                     fold_bn_affine)
 from ..ops import gradjoin
 from ..ops.dwconv import joinable
 
@@ -44,9 +46,33 @@ class SeparableConvBN(nn.Module):
                                 init="trunc_normal", init_std=0.06, **bn_kw)
         self.act_inside = act_inside
 
+    def train(self, mode=True):
+        self.__dict__.pop("_fold", None)
+        return super().train(mode)
+
+    def _load_from_state_dict(self, *args, **kw):
+        self.__dict__.pop("_fold", None)
+        return super()._load_from_state_dict(*args, **kw)
+
+    def _dw_folded(self, dtype, device):
+        """depthwise weight × s and b' of the depthwise BN (inference; see layers.ConvBN)."""
+        key = (_params.version(), dtype, device)
+        c = self.__dict__.get("_fold")
+        if c is None or c[0] != key:
+            with torch.no_grad():
+                s, sh = fold_bn_affine(self.dw_bn, device)
+                w = self.depthwise.weight.detach().to(device).float() * s.view(1, 1, -1)
+                c = self.__dict__["_fold"] = (key, w.to(dtype).contiguous(), sh.contiguous())
+        return c[1], c[2]
+
     def forward(self, x, relu_in=False, residual=None, join=None, res_join=None):
         """``join``: gradient join of x (its depthwise dgrad accumulates onto the other
         consumer's contribution); ``res_join``: gradient join of the residual."""
+        if not self.training and not torch.is_grad_enabled() and bn_fold_enabled():
+            # inference: the depthwise BN (+ReLU) folded into the depthwise conv's bias epilogue
+            w, b = self._dw_folded(x.dtype, x.device)
+            y = self.depthwise.forward_folded(x, w, b, self.act_inside, relu_in)
+            return self.pointwise(y, residual=residual)
         # training: the depthwise kernel accumulates the BN statistics of its output in its
         # epilogue (no separate reduce pass over y)
         if self.training:
