@@ -209,11 +209,13 @@ def main():
         tr.train_step(x, y)
 
     if args.mode == "infer":
-        if args.model == "deeplab_ref" or args.fp8:
-            raise SystemExit("--mode infer: the ImageNet models, bf16 / fp32")
+        if args.fp8:
+            raise SystemExit("--mode infer: bf16 / fp32")
         model.eval()
-        metric = ("inference images/sec (whole node), " + args.model
-                  + f" {args.image_size}x{args.image_size} " + ("bf16" if gpu_bf16 else "fp32")
+        shape = ("101x101x2 (the reference's Model.predict workload)" if args.model == "deeplab_ref"
+                 else f"{args.image_size}x{args.image_size}")
+        metric = ("inference images/sec (whole node), " + args.model + f" {shape} "
+                  + ("bf16" if gpu_bf16 else "fp32")
                   + (" (BN unfolded)" if args.no_fold else " (BN folded into the convs)"))
         cfg.update(optimizer=None, loss=None, mode="infer", bn_folded=not args.no_fold)
         base = None
