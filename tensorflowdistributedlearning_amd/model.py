@@ -40,6 +40,7 @@ from .engine.summary import SummaryWriter
 from .engine.exporter import BestExporter
 from .engine.trainer import Trainer
 from .models.deeplab import DeepLabResNet
+from .models.params import FlatParams
 from .ops.loss import lovasz_hinge
 from .ops.metrics import seg_scores, StreamingMean
 from .ops.optim import exponential_decay
@@ -328,6 +329,10 @@ class Model:
                 continue
             net = self.build_network().to(device)
             ckpt.restore(path, net)
+            if device.type == "cuda" and self.precision != "fp32":
+                # bf16 compute copies of the weights once per fold (not per batch); in eval mode
+                # under no_grad every conv+BN runs BN-folded (models/layers.ConvBN)
+                FlatParams(net, device, lowp_dtype=torch.bfloat16)
             net.eval()
             for tf in transforms:
                 probs, fold_ids = [], []

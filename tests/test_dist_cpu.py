@@ -245,6 +245,27 @@ def test_bench_under_torchrun_driver_form_cpu(tmp_path):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("model", ["resnet18", "deeplab_ref"])
+def test_bench_infer_mode_cpu(tmp_path, model):
+    """`bench.py --mode infer` (eval forward, folded BN): one JSON line with no training
+    baseline attached."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--mode", "infer", "--model", model,
+           "--image-size", "32", "--batch", "2", "--steps", "1", "--warmup", "1"]
+    r = subprocess.run(cmd, env=_bench_env(), cwd=str(tmp_path), capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["metric"].startswith("inference images/sec") and "folded" in out["metric"]
+    assert out["config"]["mode"] == "infer" and out["vs_baseline"] is None and out["value"] > 0
+
+
+@pytest.mark.timeout(300)
 def test_bench_self_spawn_propagates_worker_failure(tmp_path):
     """A failing worker makes the launcher exit non-zero (and stops its peers)."""
     import subprocess
