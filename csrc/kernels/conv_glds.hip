@@ -192,6 +192,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   const int tile_end = min(a.cls_tile0[a.ncls], tile_begin + a.tpb);
   if (tile_begin >= tile_end) return;
   const int HoWo = a.Ho * a.Wo;
+  // 1×1 filter without padding (wave-uniform): the FASTK A-operand DMAs need only the row check
+  const bool pointwise = a.R == 1 && a.S == 1 && a.ph == 0 && a.pw == 0;
   const bool no_loads = DBG & 1;
   const rsrc_t rx = make_rsrc(a.x, no_loads ? 0u : a.x_bytes);
   const rsrc_t rw = make_rsrc(a.w, no_loads ? 0u : a.w_bytes);
@@ -319,11 +321,22 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       if constexpr (FASTK) {
         const int rdh = tap_r * a.dh, sdw = tap_s * a.dw;
         const int tuni = (rdh * a.W + sdw) * a.C + c0;  // wave-uniform
+        if (pointwise) {
+          // 1×1 filter, no padding: every tap of a valid row is in range (row validity only —
+          // loop-invariant, so the per-DMA cost is the offset add and the select)
 #pragma unroll
-        for (int j = 0; j < IA; ++j) {
-          bool v = (unsigned)(a_p0[j] + rdh) < (unsigned)a.H && (unsigned)(a_p1[j] + sdw) < (unsigned)a.W;
-          if constexpr (RAG) v = v && c0 + kc_lchunk(j) * EPC < a.C;
-          dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+          for (int j = 0; j < IA; ++j) {
+            bool v = a_p0[j] >= 0;
+            if constexpr (RAG) v = v && c0 + kc_lchunk(j) * EPC < a.C;
+            dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < IA; ++j) {
+            bool v = (unsigned)(a_p0[j] + rdh) < (unsigned)a.H && (unsigned)(a_p1[j] + sdw) < (unsigned)a.W;
+            if constexpr (RAG) v = v && c0 + kc_lchunk(j) * EPC < a.C;
+            dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+          }
         }
       } else
 #pragma unroll
@@ -367,11 +380,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       if constexpr (FASTK) {
         const int dth = pos_r * step_h, dtw = pos_s * step_w;
         const int tuni = co0 - (dth * a.Wo + dtw) * a.K;  // wave-uniform
+        if (pointwise) {  // as in FWD: a valid row's only tap is in range
 #pragma unroll
-        for (int j = 0; j < IA; ++j) {
-          bool v = (unsigned)(a_p0[j] - dth) < (unsigned)a.Ho && (unsigned)(a_p1[j] - dtw) < (unsigned)a.Wo;
-          if constexpr (RAG) v = v && co0 + kc_lchunk(j) * EPC < a.K;
-          dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+          for (int j = 0; j < IA; ++j) {
+            bool v = a_p0[j] >= 0;
+            if constexpr (RAG) v = v && co0 + kc_lchunk(j) * EPC < a.K;
+            dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < IA; ++j) {
+            bool v = (unsigned)(a_p0[j] - dth) < (unsigned)a.Ho && (unsigned)(a_p1[j] - dtw) < (unsigned)a.Wo;
+            if constexpr (RAG) v = v && co0 + kc_lchunk(j) * EPC < a.K;
+            dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(a_row[j] + tuni) * (uint32_t)ESZ : OOB);
+          }
         }
       } else
 #pragma unroll
@@ -741,36 +763,64 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   if (lmore) issue_next();
   load_frags(smem_lds + (uint32_t)(slot_comp * STAGE), smem_lds + (uint32_t)(slot_comp * STAGE + A_BYTES), 0, f0a, f0b);
   lgkm_wait0();
+  // One pipeline step.  FAST: the DMA issued in this step keeps the load cursor inside its tile
+  // (no prep_tile), so the per-lane load state is invariant across the inner loop below.  With a
+  // single loop whose issue might switch tiles, the compiler carried that state through phi
+  // copies: ≈28 v_mov per K-step on the vector-issue-bound path.
+#define TDL_GLDS_STEP(FAST)                                                                    \
+  do {                                                                                         \
+    const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;           \
+    load_frags(As, Bs, 1, f1a, f1b);                                                           \
+    mfmas(f0a, f0b);                                                                           \
+    lgkm_wait0();                                                                              \
+    const bool has_next = (FAST) || inflight > 1;                                              \
+    slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;                                   \
+    if (has_next) {                                                                            \
+      ring_wait_barrier(inflight - 2);                                                         \
+      if constexpr ((FAST)) {                                                                  \
+        if (!no_dma) issue_step(LT, lkt, slot_load);                                           \
+        slot_load = slot_load + 1 == STAGES ? 0 : slot_load + 1;                               \
+        ++inflight;                                                                            \
+        ++lkt; /* advance_load in-tile branch */                                              \
+        if constexpr (FASTK && MODE != WGRAD) {                                                \
+          pos_c0 += KSTEP;                                                                     \
+          if (pos_c0 >= pos_C) {                                                               \
+            pos_c0 = 0;                                                                        \
+            const int Sl = MODE == FWD ? a.S : a.cls_Tw[LT.cls];                               \
+            if (++pos_s == Sl) {                                                               \
+              pos_s = 0;                                                                       \
+              ++pos_r;                                                                         \
+            }                                                                                  \
+          }                                                                                    \
+        }                                                                                      \
+      } else {                                                                                 \
+        if (lmore) issue_next();                                                               \
+      }                                                                                        \
+      const uint32_t An = smem_lds + (uint32_t)(slot_comp * STAGE), Bn = An + A_BYTES;         \
+      load_frags(An, Bn, 0, f0a, f0b);                                                         \
+    }                                                                                          \
+    mfmas(f1a, f1b);                                                                           \
+    --inflight;                                                                                \
+    ehist <<= 1;                                                                               \
+    if (ckt + 1 >= CT.kt1) {                                                                   \
+      epilogue(CT);                                                                            \
+      ehist |= 1u;                                                                             \
+      zero_acc();                                                                              \
+      if (inflight > 0) {                                                                      \
+        ++ct;                                                                                  \
+        next_tile(CT, ct);                                                                     \
+        ckt = CT.kt0;                                                                          \
+      }                                                                                        \
+    } else {                                                                                   \
+      ++ckt;                                                                                   \
+    }                                                                                          \
+    if (has_next) lgkm_wait0();                                                                \
+  } while (0)
   while (inflight > 0) {
-    const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;
-    load_frags(As, Bs, 1, f1a, f1b);
-    mfmas(f0a, f0b);
-    lgkm_wait0();
-    const bool has_next = inflight > 1;
-    slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;
-    if (has_next) {
-      ring_wait_barrier(inflight - 2);
-      if (lmore) issue_next();
-      const uint32_t An = smem_lds + (uint32_t)(slot_comp * STAGE), Bn = An + A_BYTES;
-      load_frags(An, Bn, 0, f0a, f0b);
-    }
-    mfmas(f1a, f1b);
-    --inflight;
-    ehist <<= 1;
-    if (ckt + 1 >= CT.kt1) {
-      epilogue(CT);
-      ehist |= 1u;
-      zero_acc();
-      if (inflight > 0) {
-        ++ct;
-        next_tile(CT, ct);
-        ckt = CT.kt0;
-      }
-    } else {
-      ++ckt;
-    }
-    if (has_next) lgkm_wait0();
+    while (inflight > 1 && lmore && lkt + 1 < LT.kt1) TDL_GLDS_STEP(true);
+    TDL_GLDS_STEP(false);
   }
+#undef TDL_GLDS_STEP
   flush_stats(CT.bn0);
 }
 
