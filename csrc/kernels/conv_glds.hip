@@ -74,6 +74,18 @@ __device__ __forceinline__ bf16x8 lds_read_kc(uint32_t tile, int row, int chunk)
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(tile + (uint32_t)kc_off(row, chunk)) : "memory");
   return __builtin_bit_cast(bf16x8, v);
 }
+// I-th .. N-1-th 16-row fragment of a KC image column block: rows 16 apart are 2048 B apart
+// and share the swizzle ((row >> 1) & 7 only sees the low 4 row bits), so one base address per
+// block serves every fragment with ds_read immediate offsets (no per-fragment v_add)
+template <int N, int I = 0>
+__device__ __forceinline__ void lds_read_kc_rows(bf16x8 (&f)[N], uint32_t base) {
+  if constexpr (I < N) {
+    uint4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(I * 2048) : "memory");
+    f[I] = __builtin_bit_cast(bf16x8, v);
+    lds_read_kc_rows<N, I + 1>(f, base);
+  }
+}
 template <int COLS>
 __device__ __forceinline__ bf16x8 lds_read_mc(uint32_t tile, int krow, int col) {
   v2u32 lo, hi;
@@ -511,21 +523,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           bfg[2 * q + sl] = lds_read_kc(Bs, wn * TN + q * 32 + (lane & 31), kk * 4 + sl * 2 + (lane >> 5));
       return;
     }
+    static_assert(TM % 16 == 0 && TN % 16 == 0, "16-row fragment blocks");
+    if constexpr (A_MC) {
 #pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      const int row = wm * TM + rm * 16;
-      if constexpr (A_MC)
-        af[rm] = lds_read_mc<BM>(As, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), row + 4 * (lane & 3));
-      else
-        af[rm] = lds_read_kc(As, row + (lane & 15), kk * 4 + (lane >> 4));
+      for (int rm = 0; rm < RM; ++rm)
+        af[rm] = lds_read_mc<BM>(As, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), wm * TM + rm * 16 + 4 * (lane & 3));
+    } else {
+      lds_read_kc_rows<RM>(af, As + (uint32_t)kc_off(wm * TM + (lane & 15), kk * 4 + (lane >> 4)));
     }
+    if constexpr (B_MC) {
 #pragma unroll
-    for (int rn = 0; rn < RN; ++rn) {
-      const int row = wn * TN + rn * 16;
-      if constexpr (B_MC)
-        bfg[rn] = lds_read_mc<BN>(Bs, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), row + 4 * (lane & 3));
-      else
-        bfg[rn] = lds_read_kc(Bs, row + (lane & 15), kk * 4 + (lane >> 4));
+      for (int rn = 0; rn < RN; ++rn)
+        bfg[rn] = lds_read_mc<BN>(Bs, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), wn * TN + rn * 16 + 4 * (lane & 3));
+    } else {
+      lds_read_kc_rows<RN>(bfg, Bs + (uint32_t)kc_off(wn * TN + (lane & 15), kk * 4 + (lane >> 4)));
     }
   };
   const bool no_mfma = DBG & 2;
