@@ -86,6 +86,17 @@ __device__ __forceinline__ void lds_read_kc_rows(bf16x8 (&f)[N], uint32_t base) 
     lds_read_kc_rows<N, I + 1>(f, base);
   }
 }
+// MC fragment at (kk, col block): addr = tile + mc_off<COLS>(krow of kk = 0, col).  The k-rows
+// +4 (the fragment's second half) and +32 (kk = 1) keep the swizzle (krow's bits 0-1 and 3 are
+// unchanged), so both are immediate offsets of one base address per column block
+template <int COLS, int KK>
+__device__ __forceinline__ bf16x8 lds_read_mc_imm(uint32_t addr) {
+  v2u32 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "n"(KK * 64 * COLS) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "n"(KK * 64 * COLS + 8 * COLS) : "memory");
+  uint4 v = make_uint4(lo[0], lo[1], hi[0], hi[1]);
+  return __builtin_bit_cast(bf16x8, v);
+}
 template <int COLS>
 __device__ __forceinline__ bf16x8 lds_read_mc(uint32_t tile, int krow, int col) {
   v2u32 lo, hi;
@@ -472,16 +483,26 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
         const bool v = p < a.Kg && a_base[j] >= 0;
         dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.K + a_base[j]) * 2u : OOB);
       }
+      if (pointwise && a.sh == 1 && a.sw == 1) {
+        // 1×1, stride 1, no padding: x pixel = output pixel p (no per-DMA pixel divisions)
 #pragma unroll
-      for (int j = 0; j < IB; ++j) {
-        const int p = kb + mc_krow(j, BN);
-        const int ni = fdiv(p, a.fd_HoWo), rem = p - ni * HoWo;
-        const int ho = fdiv(rem, a.fd_Wo), wo = rem - ho * a.Wo;
-        const int hi = ho * a.sh + b_f2[j], wi = wo * a.sw + b_f3[j];
-        const bool v = p < a.Kg && b_base[j] >= 0 && (unsigned)hi < (unsigned)a.H &&
-                       (unsigned)wi < (unsigned)a.W;
-        const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_base[j]) * 2u;
-        dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? off : OOB);
+        for (int j = 0; j < IB; ++j) {
+          const int p = kb + mc_krow(j, BN);
+          const bool v = p < a.Kg && b_base[j] >= 0;
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.C + b_base[j]) * 2u : OOB);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < IB; ++j) {
+          const int p = kb + mc_krow(j, BN);
+          const int ni = fdiv(p, a.fd_HoWo), rem = p - ni * HoWo;
+          const int ho = fdiv(rem, a.fd_Wo), wo = rem - ho * a.Wo;
+          const int hi = ho * a.sh + b_f2[j], wi = wo * a.sw + b_f3[j];
+          const bool v = p < a.Kg && b_base[j] >= 0 && (unsigned)hi < (unsigned)a.H &&
+                         (unsigned)wi < (unsigned)a.W;
+          const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_base[j]) * 2u;
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? off : OOB);
+        }
       }
     }
   };
@@ -524,17 +545,22 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       return;
     }
     static_assert(TM % 16 == 0 && TN % 16 == 0, "16-row fragment blocks");
+    const int mck = 8 * (lane >> 4) + ((lane >> 2) & 3);  // MC fragment k-row at kk = 0
     if constexpr (A_MC) {
 #pragma unroll
-      for (int rm = 0; rm < RM; ++rm)
-        af[rm] = lds_read_mc<BM>(As, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), wm * TM + rm * 16 + 4 * (lane & 3));
+      for (int rm = 0; rm < RM; ++rm) {
+        const uint32_t ad = As + (uint32_t)mc_off<BM>(mck, wm * TM + rm * 16 + 4 * (lane & 3));
+        af[rm] = kk == 0 ? lds_read_mc_imm<BM, 0>(ad) : lds_read_mc_imm<BM, 1>(ad);
+      }
     } else {
       lds_read_kc_rows<RM>(af, As + (uint32_t)kc_off(wm * TM + (lane & 15), kk * 4 + (lane >> 4)));
     }
     if constexpr (B_MC) {
 #pragma unroll
-      for (int rn = 0; rn < RN; ++rn)
-        bfg[rn] = lds_read_mc<BN>(Bs, kk * 32 + 8 * (lane >> 4) + ((lane >> 2) & 3), wn * TN + rn * 16 + 4 * (lane & 3));
+      for (int rn = 0; rn < RN; ++rn) {
+        const uint32_t ad = Bs + (uint32_t)mc_off<BN>(mck, wn * TN + rn * 16 + 4 * (lane & 3));
+        bfg[rn] = kk == 0 ? lds_read_mc_imm<BN, 0>(ad) : lds_read_mc_imm<BN, 1>(ad);
+      }
     } else {
       lds_read_kc_rows<RN>(bfg, Bs + (uint32_t)kc_off(wn * TN + (lane & 15), kk * 4 + (lane >> 4)));
     }
@@ -723,40 +749,65 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     for (int s = 0; s < STAGES - 1; ++s)
       if (lmore) issue_next();
     zero_acc();
+    // as in the bf16 loop below: an in-tile fast step (loop-invariant load state) and the general one
+#define TDL_GLDS_STEP8(FAST)                                                                   \
+    do {                                                                                       \
+      ring_wait_barrier(inflight - 1);                                                         \
+      ehist <<= 1;                                                                             \
+      if constexpr ((FAST)) {                                                                  \
+        if (!no_dma) issue_step(LT, lkt, slot_load);                                           \
+        slot_load = slot_load + 1 == STAGES ? 0 : slot_load + 1;                               \
+        ++inflight;                                                                            \
+        ++lkt; /* advance_load in-tile branch */                                               \
+        if constexpr (FASTK && MODE != WGRAD) {                                                \
+          pos_c0 += KSTEP;                                                                     \
+          if (pos_c0 >= pos_C) {                                                               \
+            pos_c0 = 0;                                                                        \
+            const int Sl = MODE == FWD ? a.S : a.cls_Tw[LT.cls];                               \
+            if (++pos_s == Sl) {                                                               \
+              pos_s = 0;                                                                       \
+              ++pos_r;                                                                         \
+            }                                                                                  \
+          }                                                                                    \
+        }                                                                                      \
+      } else {                                                                                 \
+        if (lmore) issue_next();                                                               \
+      }                                                                                        \
+      const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;         \
+      i32x8 a8[RM], b8[RN];                                                                    \
+_Pragma("unroll")                                                                             \
+      for (int rm = 0; rm < RM; ++rm) a8[rm] = lds_read_kc_f8(As, wm * TM + rm * 16 + (lane & 15), lane >> 4);\
+_Pragma("unroll")                                                                             \
+      for (int rn = 0; rn < RN; ++rn) b8[rn] = lds_read_kc_f8(Bs, wn * TN + rn * 16 + (lane & 15), lane >> 4);\
+      lgkm_wait0();                                                                            \
+_Pragma("unroll")                                                                             \
+      for (int rm = 0; rm < RM; ++rm)                                                          \
+_Pragma("unroll")                                                                             \
+        for (int rn = 0; rn < RN; ++rn)                                                        \
+/* operand formats: first (B tile: weights) e4m3 = 0; second (A tile) e4m3 = 0 for */          \
+/* FWD activations, e5m2 (bf8) = 1 for DGRAD output gradients */                               \
+          acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(                      \
+              b8[rn], a8[rm], acc[rm][rn], 0, MODE == DGRAD ? 1 : 0, 0, 127, 0, 127);          \
+      slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;                                 \
+      --inflight;                                                                              \
+      if (ckt + 1 >= CT.kt1) {                                                                 \
+        epilogue(CT);                                                                          \
+        ehist |= 1u;                                                                           \
+        zero_acc();                                                                            \
+        if (inflight > 0) {                                                                    \
+          ++ct;                                                                                \
+          next_tile(CT, ct);                                                                   \
+          ckt = CT.kt0;                                                                        \
+        }                                                                                      \
+      } else {                                                                                 \
+        ++ckt;                                                                                 \
+      }                                                                                        \
+    } while (0)
     while (inflight > 0) {
-      ring_wait_barrier(inflight - 1);
-      ehist <<= 1;
-      if (lmore) issue_next();
-      const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;
-      i32x8 a8[RM], b8[RN];
-#pragma unroll
-      for (int rm = 0; rm < RM; ++rm) a8[rm] = lds_read_kc_f8(As, wm * TM + rm * 16 + (lane & 15), lane >> 4);
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) b8[rn] = lds_read_kc_f8(Bs, wn * TN + rn * 16 + (lane & 15), lane >> 4);
-      lgkm_wait0();
-#pragma unroll
-      for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-        for (int rn = 0; rn < RN; ++rn)
-          // operand formats: first (B tile: weights) e4m3 = 0; second (A tile) e4m3 = 0 for
-          // FWD activations, e5m2 (bf8) = 1 for DGRAD output gradients
-          acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              b8[rn], a8[rm], acc[rm][rn], 0, MODE == DGRAD ? 1 : 0, 0, 127, 0, 127);
-      slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;
-      --inflight;
-      if (ckt + 1 >= CT.kt1) {
-        epilogue(CT);
-        ehist |= 1u;
-        zero_acc();
-        if (inflight > 0) {
-          ++ct;
-          next_tile(CT, ct);
-          ckt = CT.kt0;
-        }
-      } else {
-        ++ckt;
-      }
+      while (inflight > 1 && lmore && lkt + 1 < LT.kt1) TDL_GLDS_STEP8(true);
+      TDL_GLDS_STEP8(false);
     }
+#undef TDL_GLDS_STEP8
     flush_stats(CT.bn0);
     return;
   }
