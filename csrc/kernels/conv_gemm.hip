@@ -80,7 +80,8 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       for (int i = 0; i < PA; ++i) {
         const int m = T.bm0 + (tid >> 3) + i * (NT / 8);
         if (m < T.Mc) {
-          const int n = m / HoWo, rem = m - n * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
+          const int n = (int)fdiv((uint32_t)m, a.fd_HoWo), rem = m - n * HoWo;
+          const int ho = (int)fdiv((uint32_t)rem, a.fd_Wo), wo = rem - ho * a.Wo;
           a_base[i] = n * a.H * a.W * a.C;
           a_p0[i] = ho * a.sh - a.ph;
           a_p1[i] = wo * a.sw - a.pw;
@@ -121,7 +122,8 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       a_fix = T.bm0 + (tid % A_CPR) * 8;  // co
       const int nn = T.bn0 + (tid % B_CPR) * 8;
       if (nn < a.Ng) {
-        const int ci = nn % a.C, rs = nn / a.C, r = rs / a.S, s = rs - r * a.S;
+        const int rs = (int)fdiv((uint32_t)nn, a.fd_C), ci = nn - rs * a.C;
+        const int r = (int)fdiv((uint32_t)rs, a.fd_S), s = rs - r * a.S;
         b_fix = ci;
         b_fix2 = r * a.dh - a.ph;
         b_fix3 = s * a.dw - a.pw;
@@ -140,7 +142,8 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
       if constexpr (MODE == FWD) {
         const int k = kt * BK + (tid & 7) * 8;
         const bool kv = k < a.Kg;
-        const int c = k % a.C, rs = k / a.C, r = rs / a.S, s = rs - r * a.S;
+        const int rs = (int)fdiv((uint32_t)k, a.fd_C), c = k - rs * a.C;
+        const int r = (int)fdiv((uint32_t)rs, a.fd_S), s = rs - r * a.S;
         const int ro = r * a.dh, so = s * a.dw;
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
@@ -189,7 +192,10 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
           const int p = kt * BK + tid / B_CPR + i * (NT / B_CPR);
-          const int ni = p / HoWo, rem = p - ni * HoWo, ho = rem / a.Wo, wo = rem - ho * a.Wo;
+          // magic-number divisions (set_fastdivs): `/` by a runtime divisor costs ~40 VALU each,
+          // twice per load, in the K-step loop
+          const int ni = (int)fdiv((uint32_t)p, a.fd_HoWo), rem = p - ni * HoWo;
+          const int ho = (int)fdiv((uint32_t)rem, a.fd_Wo), wo = rem - ho * a.Wo;
           const int hi = ho * a.sh + b_fix2, wi = wo * a.sw + b_fix3;
           const bool v = p < a.Kg && b_fix >= 0 && (unsigned)hi < (unsigned)a.H &&
                          (unsigned)wi < (unsigned)a.W;
@@ -905,6 +911,7 @@ void conv_wgrad_launch(const ConvArgs& a0, const WgradPlan& p, float* out, bool 
     a.tpb = 1;
     a.splits = splits;
     a.kps = p.kps;
+    convk::set_fastdivs(a);
     const bool al = (a.C % 8 == 0) && (a.K % 8 == 0);
     if (al) launch_cfg<WGRAD, true, false>(a, p.bm, p.bn, (int)tiles, st);
     else launch_cfg<WGRAD, false, false>(a, p.bm, p.bn, (int)tiles, st);
