@@ -91,18 +91,49 @@ def launch_workers(n: int, argv) -> int:
     return rc
 
 
+def _opt(name):
+    return "sgd" if name == "sgd_momentum" else name
+
+
+def _opt_kw(bc):
+    if bc.optimizer == "adam":
+        return dict(lr=bc.lr)
+    return dict(lr=bc.lr, momentum=bc.momentum, weight_decay=bc.weight_decay)
+
+
+def bench_config(args):
+    """The run's :class:`config.BenchConfig`: ``--config`` file (or the defaults), then every
+    flag that was given."""
+    from tensorflowdistributedlearning_amd.config import BenchConfig, load
+    cfg = load(args.config, BenchConfig) if args.config else BenchConfig()
+    over = {"arch": args.model, "batch": args.batch, "image_size": args.image_size,
+            "steps": args.steps, "warmup": args.warmup, "lr": args.lr,
+            "bucket_mb": args.bucket_mb, "first_bucket_mb": args.first_bucket_mb,
+            "optimizer": args.optimizer, "dtype": args.dtype}
+    for k, v in over.items():
+        if v is not None:
+            setattr(cfg, k, v)
+    if args.fp8:
+        cfg.dtype = "fp8"
+    cfg.fp8_dgrad = cfg.fp8_dgrad or args.fp8_dgrad
+    cfg.graph = cfg.graph or args.graph
+    return cfg.validate()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--config", help="BenchConfig JSON / YAML (config.BenchConfig); flags override")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 20)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default 5)")
+    ap.add_argument("--model", default=None, help="arch preset (default resnet50)")
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch (default 1024 for the ImageNet models, 64/N for deeplab_ref)")
-    ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--first-bucket-mb", type=float, default=4.0)
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--image-size", type=int, default=None)
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--first-bucket-mb", type=float, default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--optimizer", choices=("sgd_momentum", "adam"), default=None)
     ap.add_argument("--fp8", action="store_true",
                     help="fp8 GEMMs on the CDNA4 16x16x128 f8f6f4 MFMA for every eligible conv: "
                          "forward e4m3 activations x e4m3 weights; weight and input gradients "
@@ -113,7 +144,7 @@ def main():
                     help="capture the whole training step as a HIP graph and replay it (removes "
                          "host launch overhead in launch-bound configs; with N>1 the bucketed "
                          "all-reduces are captured too, on the native RCCL communicator)")
-    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default=None,
                     help="GPU compute precision: bf16 (fused bf16 kernels, fp32 accumulation / "
                          "master weights) or fp32 (fp32 operands on the fp32 MFMA end to end — the "
                          "reference's own precision, for the like-for-like deeplab_ref comparison)")
@@ -132,6 +163,7 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_workers(args.gpus, sys.argv[1:]))
+    bc = bench_config(args)  # in the workers: a bad preset fails a rank (launcher relays it)
 
     import torch
     from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown
@@ -153,55 +185,54 @@ def main():
     comm = "rccl" if ctx.native is not None else ("gloo" if n > 1 else "none")
     # CPU (plumbing runs, tests): fp32 storage, the PyTorch reference ops; GPU --dtype fp32: fp32
     # activations + the fp32 master weights read directly by the fp32 kernels (no compute copy)
-    gpu_bf16 = dev.type == "cuda" and args.dtype == "bf16"
+    gpu_bf16 = dev.type == "cuda" and bc.dtype in ("bf16", "fp8")
     lowp = torch.bfloat16 if gpu_bf16 else None
     ddt = torch.bfloat16 if gpu_bf16 else torch.float32
     dtype_name = "bf16" if gpu_bf16 else "fp32" if dev.type == "cuda" else "fp32 (CPU plumbing run)"
-    if args.fp8 and not gpu_bf16:
+    if bc.dtype == "fp8" and not gpu_bf16:
         raise SystemExit("--fp8 runs on the bf16 GPU path")
     torch.manual_seed(1234)
     fp8_desc = None
-    if args.model == "deeplab_ref" and args.fp8:
+    if bc.arch == "deeplab_ref" and bc.dtype == "fp8":
         raise SystemExit("--fp8 is for the ImageNet models")
 
-    if args.model == "deeplab_ref":
-        per_gpu = args.batch or max(64 // n, 1)
+    if bc.arch == "deeplab_ref":
+        per_gpu = bc.batch or max(64 // n, 1)
         model = models.DeepLabResNet(model_name="model", input_shape=(101, 101))
-        tr = Trainer(model, lovasz_hinge, dev, "adam", dict(lr=1e-3), ctx=ctx,
-                     bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+        tr = Trainer(model, lovasz_hinge, dev, _opt(bc.optimizer), _opt_kw(bc), ctx=ctx,
+                     bucket_mb=bc.bucket_mb, first_bucket_mb=bc.first_bucket_mb,
                      profile_phases=args.profile_phases, lowp_dtype=lowp)
         x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank, dtype=ddt)
         metric = ("images/sec (whole node), reference DeepLab-ResNet 101x101x2 "
                   + ("bf16" if gpu_bf16 else "fp32"))
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
-               "image": "101x101x2", "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks, "optimizer": "adam",
-               "loss": "lovasz_hinge", "hip_graph": args.graph,
+               "image": "101x101x2", "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks, "optimizer": bc.optimizer,
+               "loss": "lovasz_hinge", "hip_graph": bc.graph,
                "wgrad_side_stream": streams.enabled()}
         base = REF_DEEPLAB_2GPU / 2 * n
     else:
         # 1024 images per GPU by default (ResNet-50: 49 GiB reserved of the 288 GB HBM): +2.9 %
         # img/s over 512 and +15 % over 256 on the same box (bigger GEMM M, fixed per-layer costs
         # amortised; profiles/r02_resnet50_batch_sweep.txt)
-        per_gpu = args.batch or 1024
-        model = models.build(args.model, num_classes=1000)
-        if args.fp8:
-            models.enable_fp8(model, dgrad=args.fp8_dgrad or None)
+        per_gpu = bc.batch or 1024
+        model = models.build(bc.arch, num_classes=1000)
+        if bc.dtype == "fp8":
+            models.enable_fp8(model, dgrad=bc.fp8_dgrad or None)
             fp8_desc = ("fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad + BN)"
-                        if args.fp8_dgrad else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / "
+                        if bc.fp8_dgrad else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / "
                         "wgrad + BN)")
-        tr = Trainer(model, softmax_cross_entropy, dev, "sgd",
-                     dict(lr=args.lr, momentum=0.9, weight_decay=5e-5), ctx=ctx,
-                     bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+        tr = Trainer(model, softmax_cross_entropy, dev, _opt(bc.optimizer), _opt_kw(bc), ctx=ctx,
+                     bucket_mb=bc.bucket_mb, first_bucket_mb=bc.first_bucket_mb,
                      profile_phases=args.profile_phases, lowp_dtype=lowp)
-        x, y = imagenet_batch(per_gpu, args.image_size, device=dev, seed=ctx.rank, dtype=ddt)
-        metric = METRIC if args.model == "resnet50" and args.image_size == 224 and gpu_bf16 \
-            else (f"images/sec (whole node), {args.model} {args.image_size}x{args.image_size} "
-                  f"{fp8_desc if args.fp8 else 'bf16' if gpu_bf16 else 'fp32'}")
-        cfg = {"model": args.model, "global_batch": per_gpu * n, "seq_len": None,
-               "image": f"{args.image_size}x{args.image_size}x3", "per_gpu_batch": per_gpu,
+        x, y = imagenet_batch(per_gpu, bc.image_size, device=dev, seed=ctx.rank, dtype=ddt)
+        metric = METRIC if bc.arch == "resnet50" and bc.image_size == 224 and gpu_bf16 \
+            else (f"images/sec (whole node), {bc.arch} {bc.image_size}x{bc.image_size} "
+                  f"{fp8_desc if bc.dtype == 'fp8' else 'bf16' if gpu_bf16 else 'fp32'}")
+        cfg = {"model": bc.arch, "global_batch": per_gpu * n, "seq_len": None,
+               "image": f"{bc.image_size}x{bc.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks,
-               "optimizer": "sgd_momentum",
-               "loss": "softmax_ce", "hip_graph": args.graph,
+               "optimizer": bc.optimizer,
+               "loss": "softmax_ce", "hip_graph": bc.graph,
                "wgrad_side_stream": streams.enabled()}
         base = REF_PER_GPU_DERIVED * n
 
@@ -209,12 +240,12 @@ def main():
         tr.train_step(x, y)
 
     if args.mode == "infer":
-        if args.fp8:
+        if bc.dtype == "fp8":
             raise SystemExit("--mode infer: bf16 / fp32")
         model.eval()
-        shape = ("101x101x2 (the reference's Model.predict workload)" if args.model == "deeplab_ref"
-                 else f"{args.image_size}x{args.image_size}")
-        metric = ("inference images/sec (whole node), " + args.model + f" {shape} "
+        shape = ("101x101x2 (the reference's Model.predict workload)" if bc.arch == "deeplab_ref"
+                 else f"{bc.image_size}x{bc.image_size}")
+        metric = ("inference images/sec (whole node), " + bc.arch + f" {shape} "
                   + ("bf16" if gpu_bf16 else "fp32")
                   + (" (BN unfolded)" if args.no_fold else " (BN folded into the convs)"))
         cfg.update(optimizer=None, loss=None, mode="infer", bn_folded=not args.no_fold)
@@ -224,7 +255,7 @@ def main():
         def step():
             model(x)
 
-    if args.graph and args.mode == "infer":
+    if bc.graph and args.mode == "infer":
         step()
         torch.cuda.synchronize(dev)
         s = torch.cuda.Stream(dev)
@@ -236,33 +267,42 @@ def main():
         with torch.no_grad(), torch.cuda.graph(gr):
             model(x)
         step = gr.replay
-        for _ in range(args.warmup):
+        for _ in range(bc.warmup):
             step()
-    elif args.graph:
-        tr.capture(x, y, warmup=args.warmup)  # W eager warm-up steps, then the capture
+    elif bc.graph:
+        tr.capture(x, y, warmup=bc.warmup)  # W eager warm-up steps, then the capture
         step = tr.replay
         step()  # first replay (graph upload) stays untimed
-        print(f"[bench] step captured as a HIP graph ({args.model}, batch {per_gpu}/gpu)",
+        print(f"[bench] step captured as a HIP graph ({bc.arch}, batch {per_gpu}/gpu)",
               file=sys.stderr, flush=True)
     else:
-        for i in range(args.warmup):
+        for i in range(bc.warmup):
             step()
             if ctx.is_main and i == 0:
-                print(f"[bench] first step done ({args.model}, batch {per_gpu}/gpu, n={n})",
+                print(f"[bench] first step done ({bc.arch}, batch {per_gpu}/gpu, n={n})",
                       file=sys.stderr, flush=True)
     ctx.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(bc.steps):
         step()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     ctx.barrier()
     el = time.perf_counter() - t0
     el = ctx.all_reduce_max(el)
-    ms = el / args.steps * 1e3
-    value = per_gpu * n * args.steps / el
+    ms = el / bc.steps * 1e3
+    comm_stats = None
+    if n > 1 and tr.bucketer is not None and not bc.graph and args.mode == "train":
+        # exposed communication (backward end → last bucket done, compute stream) vs the same
+        # collectives run alone: overlap = the fraction backward hid
+        exposed = ctx.all_reduce_max(tr.comm_wait_ms(last=bc.steps) or 0.0)
+        alone = ctx.all_reduce_max(tr.bucketer.standalone_ms())
+        comm_stats = {"exposed_ms": round(exposed, 3), "standalone_ms": round(alone, 3),
+                      "overlap": round(max(0.0, 1.0 - exposed / alone), 3) if alone > 0 else None,
+                      "buckets": len(tr.bucketer.buckets)}
+    value = per_gpu * n * bc.steps / el
     if ctx.is_main:
         if dev.type == "cuda":
             print(f"[bench] peak device memory {torch.cuda.max_memory_allocated(dev) / 2**30:.1f} "
@@ -272,16 +312,18 @@ def main():
             ph = tr.timer.summary()
             print("[bench] phases ms/step (timed + warmup steps): " +
                   " ".join(f"{k}={v:.2f}" for k, v in ph.items()), file=sys.stderr)
+        if comm_stats is not None:
+            cfg["comm_overlap"] = comm_stats
         print(json.dumps({
             "metric": metric, "value": round(value, 2), "unit": "images/sec", "n_gpus": n,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "steps": bc.steps, "warmup": bc.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / base, 3) if base else None,
             "baseline": (None if base is None else
                          "BASELINE.md derived ResNet-50-equivalent 86 img/s/GPU (no published "
-                         "ResNet-50 number)" if args.model != "deeplab_ref" else
+                         "ResNet-50 number)" if bc.arch != "deeplab_ref" else
                          "BASELINE.md measured 90.7 img/s on 2 GPUs, scaled per GPU"),
-            "dtype": fp8_desc if args.fp8 else dtype_name,
+            "dtype": fp8_desc if bc.dtype == "fp8" else dtype_name,
             "data": "synthetic (device-resident random batch, random-init weights)",
             "config": cfg}), flush=True)
     shutdown()

@@ -3,7 +3,11 @@
   train    k-fold training of the reference DeepLab model on a TGS-style directory
            (``<data>/images/*.png`` + ``<data>/masks/*.png``), stratified on mask-coverage class
            exactly like the reference notebook (coverage = Σmask / (H·W), class = ⌈10·coverage⌉,
-           Test.ipynb) — i.e. ``Model(...).train(ids, classes, batch_size, steps)``;
+           Test.ipynb) — i.e. ``Model(...).train(ids, classes, batch_size, steps)``; or, with
+           ``--arch resnet18|…|resnet152|xception41 --synthetic``, a north-star classifier on the
+           learnable synthetic dataset (``--num-samples`` ids, ``--num-classes``): softmax-CE +
+           SGD-momentum, LR schedule, checkpoints / resume / eval / summaries, e.g. BASELINE
+           config 1: ``train --arch resnet18 --image-size 32 --synthetic --device cpu``;
   predict  TTA-averaged probabilities of every ``*.png`` in a directory → ``.npz`` (+ optional CSV
            with run-length-encoded masks, the Kaggle submission format);
   bench    the training benchmark (same as ``python bench.py``);
@@ -58,6 +62,14 @@ def _model_cfg(args):
 def cmd_train(args):
     from .model import Model
     cfg = _model_cfg(args)
+    if cfg.arch != "deeplab_ref":
+        if not cfg.synthetic:
+            raise SystemExit(f"--arch {cfg.arch} from the command line trains on --synthetic data "
+                             "(image arrays: Model(...).train(images, labels, ...) in Python)")
+        m = Model(**cfg.model_kwargs())
+        res = m.train(args.num_samples, None, args.batch_size, args.steps)
+        print(json.dumps({"params": m.params, "folds": res}, default=float))
+        return
     ids = sorted(os.path.splitext(os.path.basename(p))[0]
                  for p in glob.glob(os.path.join(cfg.data_directory, "images", "*.png")))
     if not ids:
@@ -110,6 +122,29 @@ def main(argv=None):
         p.add_argument("--precision", choices=("bf16", "fp32"),
                        help="GPU compute precision (fp32: the reference's own precision)")
         p.add_argument("--batch-size", dest="batch_size", type=int, default=64)
+        p.add_argument("--arch", help="deeplab_ref (default) | resnet18/34/50/101/152 | xception41")
+        p.add_argument("--num-classes", dest="num_classes", type=int)
+        p.add_argument("--image-size", dest="image_size", type=int)
+        p.add_argument("--loss", choices=("lovasz", "softmax_ce"))
+        p.add_argument("--optimizer", choices=("adam", "sgd_momentum"))
+        p.add_argument("--momentum", type=float)
+        p.add_argument("--lr-schedule", dest="lr_schedule",
+                       choices=("exponential", "cosine", "step", "constant"))
+        p.add_argument("--lr-decay-steps", dest="lr_decay_steps", type=int)
+        p.add_argument("--lr-decay-rate", dest="lr_decay_rate", type=float)
+        p.add_argument("--lr-warmup-steps", dest="lr_warmup_steps", type=int)
+        p.add_argument("--weight-decay", dest="weight_decay", type=float)
+        p.add_argument("--use-regularization", dest="use_regularization", action="store_true",
+                       default=None)
+        p.add_argument("--synthetic", action="store_true", default=None,
+                       help="classifiers: the learnable synthetic dataset (data/classification.py)")
+        p.add_argument("--num-samples", dest="num_samples", type=int, default=1024)
+        p.add_argument("--max-folds", dest="max_folds", type=int)
+        p.add_argument("--fp8", action="store_true", default=None)
+        p.add_argument("--hip-graph", dest="hip_graph", choices=("auto", "off"))
+        p.add_argument("--save-checkpoints-steps", dest="save_checkpoints_steps", type=int)
+        p.add_argument("--save-summary-steps", dest="save_summary_steps", type=int)
+        p.add_argument("--eval-batches", dest="eval_batches", type=int)
 
     t = sub.add_parser("train")
     common(t)

@@ -16,6 +16,10 @@ import json
 from dataclasses import dataclass, field
 from typing import Optional, Tuple
 
+# network presets: the reference's segmentation net and the north-star classifiers
+SEGMENTATION_ARCHS = ("deeplab_ref",)
+CLASSIFIER_ARCHS = ("resnet18", "resnet34", "resnet50", "resnet101", "resnet152", "xception41")
+
 
 @dataclass
 class ModelConfig:
@@ -50,6 +54,23 @@ class ModelConfig:
     # GPU compute precision: "bf16" (fused bf16 kernels, fp32 accumulation / master weights) or
     # "fp32" (the reference's own precision: fp32 operands on the fp32 kernels end to end)
     precision: str = "bf16"
+    # north-star workloads through Model; None = the arch's default
+    arch: str = "deeplab_ref"         # or resnet18/34/50/101/152, xception41
+    num_classes: int = 1000
+    image_size: Optional[int] = None  # classifiers: 224 (xception41: 299)
+    image_channels: int = 3
+    loss: Optional[str] = None        # lovasz (deeplab_ref) | softmax_ce (classifiers)
+    optimizer: Optional[str] = None   # adam (deeplab_ref) | sgd_momentum (classifiers)
+    momentum: float = 0.9
+    lr_schedule: str = "exponential"  # exponential (the reference's) | cosine | step | constant
+    lr_decay_steps: int = 10000
+    lr_decay_rate: float = 0.5
+    lr_warmup_steps: int = 0
+    synthetic: bool = False           # classifiers: learnable synthetic dataset (sample ids)
+    fp8: bool = False                 # classifiers: fp8 forward GEMMs
+    hip_graph: str = "auto"           # capture each fold's step as a HIP graph (GPU)
+    eval_batches: Optional[int] = None
+    max_folds: Optional[int] = None   # train only the first k folds
 
     def validate(self):
         if self.data_format not in ("NCHW", "NHWC"):
@@ -62,6 +83,8 @@ class ModelConfig:
             raise ValueError(f"unknown block_type {self.block_type}")
         if self.precision not in ("bf16", "fp32"):
             raise ValueError(f"unknown precision {self.precision} (bf16 or fp32)")
+        if self.arch not in SEGMENTATION_ARCHS + CLASSIFIER_ARCHS:
+            raise ValueError(f"unknown arch {self.arch}")
         return self
 
     def model_kwargs(self):
@@ -69,26 +92,53 @@ class ModelConfig:
         d["input_shape"] = tuple(d["input_shape"])
         d["n_blocks"] = tuple(d["n_blocks"])
         d["n_fold"] = d.pop("n_fold")
+        for k in ("image_size", "loss", "optimizer"):  # None: the arch's default
+            if d[k] is None:
+                d.pop(k)
         return d
 
 
 @dataclass
 class BenchConfig:
+    """What ``bench.py`` runs (it builds one from its flags, or from ``--config``): the
+    architecture preset, precision, objective, optimizer, data source and DP bucket sizes."""
     arch: str = "resnet50"            # resnet18/34/50/101/152, xception41, deeplab_ref
-    dtype: str = "bf16"
-    optimizer: str = "sgd_momentum"   # or adam
-    loss: str = "softmax_ce"          # or lovasz
-    synthetic: bool = True
-    batch: int = 256                  # per GPU
+    dtype: str = "bf16"               # bf16 | fp32 | fp8 (fp8 forward GEMMs, bf16 backward)
+    optimizer: Optional[str] = None   # sgd_momentum (classifiers) | adam (deeplab_ref)
+    loss: Optional[str] = None        # softmax_ce (classifiers) | lovasz (deeplab_ref)
+    synthetic: bool = True            # the only data source of the benchmark
+    batch: Optional[int] = None       # per GPU (None: 1024 for classifiers, 64/N deeplab_ref)
     image_size: int = 224
     steps: int = 20
     warmup: int = 5
-    lr: float = 0.1
+    lr: Optional[float] = None        # None: 0.1 (SGD) / 1e-3 (Adam)
     momentum: float = 0.9
     weight_decay: float = 5e-5
     bucket_mb: float = 32.0
     first_bucket_mb: float = 4.0
+    fp8_dgrad: bool = False
+    graph: bool = False
     extra: dict = field(default_factory=dict)
+
+    def validate(self):
+        if self.arch not in SEGMENTATION_ARCHS + CLASSIFIER_ARCHS:
+            raise ValueError(f"unknown arch {self.arch}")
+        seg = self.arch in SEGMENTATION_ARCHS
+        self.optimizer = self.optimizer or ("adam" if seg else "sgd_momentum")
+        self.loss = self.loss or ("lovasz" if seg else "softmax_ce")
+        if self.lr is None:
+            self.lr = 1e-3 if self.optimizer == "adam" else 0.1
+        if self.dtype not in ("bf16", "fp32", "fp8"):
+            raise ValueError(f"unknown dtype {self.dtype}")
+        if self.optimizer not in ("adam", "sgd_momentum"):
+            raise ValueError(f"unknown optimizer {self.optimizer}")
+        if self.loss not in ("lovasz", "softmax_ce") or (self.loss == "lovasz") != seg:
+            raise ValueError(f"loss {self.loss} does not fit arch {self.arch}")
+        if not self.synthetic:
+            raise ValueError("the benchmark runs on synthetic data only")
+        if self.dtype == "fp8" and seg:
+            raise ValueError("fp8 is for the ImageNet models")
+        return self
 
 
 def _coerce(cls, d):

@@ -179,7 +179,7 @@ def resnet_v2(inputs=None, n_blocks=(3, 4, 6), block_type="bottleneck", num_clas
                        tuple(multi_grid), num_classes, bool(global_pool),
                        x.shape[1], x.shape[2], x.shape[3]),
                       lambda: ResNetV2Beta(
-                          DeepLabResNet(model_name=scope, in_channels=min(x.shape[3], 8),
+                          DeepLabResNet(model_name=scope, in_channels=x.shape[3],
                                         output_stride=output_stride,
                                         input_shape=(x.shape[1], x.shape[2]),
                                         n_blocks=n_blocks, block_type=block_type,
@@ -206,7 +206,7 @@ def resnet_model(input, model_name, weight_decay, batch_norm_decay, batch_norm_e
         raise ValueError("Expect n_blocks to have length 3.")
     x = to_nhwc(input, data_format)
     m = get_or_create(("resnet_model", model_name),
-                      lambda: DeepLabResNet(model_name=model_name, in_channels=min(x.shape[3], 8),
+                      lambda: DeepLabResNet(model_name=model_name, in_channels=x.shape[3],
                                             output_stride=output_stride, base_depth=base_depth,
                                             input_shape=tuple(input_shape),
                                             n_blocks=tuple(n_blocks), block_type=block_type,

@@ -120,7 +120,7 @@ def xception(inputs, blocks=None, num_classes=None, is_training=True, global_poo
     key = ("xception", scope, output_stride, num_classes, x.shape[-1],
            tuple((r[0], tuple(r[1]), r[2], r[4], tuple(r[5]), r[6]) for r in rows))
     m = get_or_create(key, lambda: Xception(rows, num_classes=num_classes or 0,
-                                            in_channels=min(x.shape[-1], 8),
+                                            in_channels=x.shape[-1],
                                             output_stride=output_stride), device_of(x))
     m.train(bool(is_training))
     y, ep = m(x, return_end_points=True)
@@ -136,7 +136,7 @@ def xception_41(inputs, is_training=True, keep_prob=0.5, output_stride=None,
     x = to_nhwc(inputs, data_format)
     m = get_or_create(("xception_41", scope, output_stride, tuple(multi_grid or []), num_classes),
                       lambda: Xception41(num_classes=num_classes or 0,
-                                         in_channels=min(x.shape[-1], 8),
+                                         in_channels=x.shape[-1],
                                          output_stride=output_stride, multi_grid=multi_grid),
                       device_of(x))
     m.train(bool(is_training))

@@ -88,6 +88,7 @@ class Trainer:
         # fp8 delayed scaling: one end-of-step device roll of every amax ring (ops/fp8.py)
         # (a no-op until the model's first fp8 scaler exists)
         self.fp8_roller = RingRoller(self.model)
+        self._comm_marks = []  # (backward end, collectives done) per eager DP step
 
     # ------------------------------------------------------------------------------------------
     def broadcast_state(self):
@@ -124,7 +125,11 @@ class Trainer:
             t.mark("backward")
         world = 1
         if self.bucketer is not None:
+            mark = self._comm_mark()
             self.bucketer.finish()
+            if mark is not None:
+                self._comm_marks.append((mark, self._comm_mark()))
+                del self._comm_marks[:-256]
             world = self.ctx.world_size
         if t:
             t.mark("comm_wait")
@@ -135,6 +140,26 @@ class Trainer:
             t.end_step()
         self.global_step += 1
         return loss.detach(), out.detach()
+
+    def _comm_mark(self):
+        if self.device.type == "cuda":
+            if streams.capturing():
+                return None
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def comm_wait_ms(self, last=None):
+        """Mean exposed communication per eager step: from the end of backward to the last
+        bucket's completion on the compute stream (the collectives backward did not hide)."""
+        marks = self._comm_marks[-last:] if last else self._comm_marks
+        if not marks:
+            return None
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+            return sum(a.elapsed_time(b) for a, b in marks) / len(marks)
+        return sum((b - a) * 1e3 for a, b in marks) / len(marks)
 
     # ------------------------------------------------------------------------------------------
     def capture(self, x, y, warmup=3):
@@ -166,7 +191,9 @@ class Trainer:
         with workspace.use_arena(self.graph_arena):
             with torch.cuda.stream(side):  # warm-up: caches, arena size, kernel attributes
                 for _ in range(warmup):
-                    self._step(self.static_x, self.static_y)
+                    # real training steps on (x, y); the last one's (loss, out) is kept for a
+                    # caller that counts the warm-up as its step (model.Model's loop)
+                    self.warmup_out = self._step(self.static_x, self.static_y)
             torch.cuda.current_stream(self.device).wait_stream(side)
             torch.cuda.synchronize(self.device)
             self.optimizer.set_device_lr(True)
@@ -204,6 +231,7 @@ class Trainer:
             nc.track_current("graph_replay")  # watchdog covers the captured collectives
         self.optimizer.step_count += 1
         self.global_step += 1
+        self.fp8_roller.note_replay()  # the captured step rolled the fp8 amax rings on the device
         _params.bump_version()
         return self.graph_out
 

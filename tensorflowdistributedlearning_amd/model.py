@@ -20,6 +20,19 @@ backward) around the native engine:
   ``tti``), undoes the transformation and averages probabilities over transformations and folds.
 * ``params`` (model.py:507-513): parameter count once a model has been built.
 
+North-star workloads train through the same class: ``arch`` selects the
+network (``"deeplab_ref"`` — the reference's DeepLab-ResNet, default — or ``resnet18/34/50/101/
+152`` / ``xception41``, the classifiers the reference reaches through its ``resnet_v2`` logits head,
+/root/reference/core/resnet.py:246-256, and /root/reference/model.py:356-370).  Classifiers train
+with softmax cross-entropy + SGD-momentum by default (``loss`` / ``optimizer`` override), an LR
+schedule (``lr_schedule``: exponential — the reference's —, cosine, step, constant), the same
+k-fold / checkpoint / resume / eval (top-1 accuracy) / summaries / best-export cadence, on
+``X`` = an image array [N, H, W, C] or, with ``synthetic=True``, sample ids of a learnable
+synthetic dataset (data/classification.py).  ``hip_graph`` (default on for GPU runs) captures the
+training step of each fold as one HIP graph after the first step and replays it
+(engine/trainer.Trainer.capture) — the reference's per-step session loop without per-kernel host
+launches.
+
 Block type: the reference passes ``params['block_type']="basic_block"`` to the model_fn but the
 model reads ``self.block_type`` (default "bottleneck") — D19; ``block_type`` kw is honoured here.
 """
@@ -39,13 +52,16 @@ from .engine import checkpoint as ckpt
 from .engine.summary import SummaryWriter
 from .engine.exporter import BestExporter
 from .engine.trainer import Trainer
+from .engine import schedules
 from .models.deeplab import DeepLabResNet
+from . import models as _models
 from .models.params import FlatParams
-from .ops.loss import lovasz_hinge
+from .ops.loss import lovasz_hinge, softmax_cross_entropy
 from .ops.metrics import seg_scores, StreamingMean
 from .ops.optim import exponential_decay
 from .preprocessing.preprocessing import _prepare_directory, create_symlinks, TRAIN, EVAL
 from .data.pipeline import SegmentationPipeline, TestPipeline, fold_files, TRAIN_AUG
+from .data.classification import ClassificationPipeline, SyntheticImages, ArrayImages
 from .utils import metric_comparisson, get_available_gpus
 
 WEIGHT_DECAY = 0.001
@@ -57,6 +73,8 @@ INPUT_SHAPE = (101, 101)
 BASE_DEPTH = 256
 
 _TTA = ["vertical", "horizontal", "transpose", "none"]
+
+from .config import SEGMENTATION_ARCHS, CLASSIFIER_ARCHS  # noqa: E402  (re-exported)
 
 
 def _undo_transform(t, transformation):
@@ -105,6 +123,36 @@ class Model:
         self.precision = kwargs.get("precision", "bf16")
         if self.precision not in ("bf16", "fp32"):
             raise ValueError(f"unknown precision {self.precision} (bf16 or fp32)")
+        # north-star workloads: network, objective, optimizer, schedule
+        self.arch = kwargs.get("arch", "deeplab_ref")
+        if self.arch not in SEGMENTATION_ARCHS + CLASSIFIER_ARCHS:
+            raise ValueError(f"unknown arch {self.arch}; have {SEGMENTATION_ARCHS + CLASSIFIER_ARCHS}")
+        seg = self.arch in SEGMENTATION_ARCHS
+        self.num_classes = kwargs.get("num_classes", 1000)
+        self.image_size = kwargs.get("image_size", 299 if self.arch == "xception41" else 224)
+        self.image_channels = kwargs.get("image_channels", 3)
+        self.loss = kwargs.get("loss", "lovasz" if seg else "softmax_ce")
+        if self.loss not in ("lovasz", "softmax_ce"):
+            raise ValueError(f"unknown loss {self.loss} (lovasz or softmax_ce)")
+        if (self.loss == "lovasz") != seg:
+            raise ValueError(f"loss {self.loss} does not fit arch {self.arch}")
+        self.optimizer = kwargs.get("optimizer", "adam" if seg else "sgd_momentum")
+        if self.optimizer not in ("adam", "sgd_momentum"):
+            raise ValueError(f"unknown optimizer {self.optimizer} (adam or sgd_momentum)")
+        self.momentum = kwargs.get("momentum", 0.9)
+        self.lr_schedule = kwargs.get("lr_schedule", "exponential")
+        if self.lr_schedule not in schedules.SCHEDULES:
+            raise ValueError(f"unknown lr_schedule {self.lr_schedule}; have {schedules.SCHEDULES}")
+        self.lr_decay_steps = kwargs.get("lr_decay_steps", 10000)   # model.py:457-459
+        self.lr_decay_rate = kwargs.get("lr_decay_rate", 0.5)
+        self.lr_warmup_steps = kwargs.get("lr_warmup_steps", 0)
+        self.synthetic = kwargs.get("synthetic", False)
+        self.fp8 = kwargs.get("fp8", False)
+        # HIP-graph capture of each fold's training step ("auto": GPU runs whose collectives, if
+        # any, are on the native RCCL communicator)
+        self.hip_graph = kwargs.get("hip_graph", "auto")
+        self.eval_batches = kwargs.get("eval_batches", None)  # cap on eval batches per pass
+        self.max_folds = kwargs.get("max_folds", None)  # train only the first k folds
 
         self.model_name = model_dir.rstrip("/").split("/")[-1]
         self.model_dir = model_dir
@@ -118,7 +166,18 @@ class Model:
         self.skf = StratifiedKFold(n_splits=self.n_folds, shuffle=True, random_state=self.seed)
 
     # ------------------------------------------------------------------------------------------
+    @property
+    def segmentation(self):
+        return self.arch in SEGMENTATION_ARCHS
+
     def config(self):
+        if not self.segmentation:
+            return {"model_name": self.model_name, "arch": self.arch,
+                    "num_classes": self.num_classes, "image_size": self.image_size,
+                    "image_channels": self.image_channels, "loss": self.loss,
+                    "optimizer": self.optimizer, "lr": self.lr, "lr_schedule": self.lr_schedule,
+                    "weight_decay": self.weight_decay, "seed": self.seed,
+                    "precision": self.precision, "fp8": self.fp8}
         return {"model_name": self.model_name, "weight_decay": self.weight_decay,
                 "batch_norm_decay": self.batch_norm_decay,
                 "batch_norm_epsilon": self.batch_norm_epsilon,
@@ -128,6 +187,12 @@ class Model:
                 "lr": self.lr, "seed": self.seed, "precision": self.precision}
 
     def build_network(self):
+        if not self.segmentation:
+            net = _models.build(self.arch, num_classes=self.num_classes,
+                                in_channels=self.image_channels)
+            if self.fp8:
+                _models.enable_fp8(net)
+            return net
         return DeepLabResNet(model_name=self.model_name, in_channels=2,
                              output_stride=self.output_stride, base_depth=self.base_depth,
                              input_shape=self.input_shape, n_blocks=self.n_blocks,
@@ -150,9 +215,18 @@ class Model:
 
     # ------------------------------------------------------------------------------------------
     def train(self, X, y, batch_size, steps=100):
+        """k-fold training (model.py:138-227).  Segmentation (``arch="deeplab_ref"``): ``X`` =
+        image ids under ``data_directory/images``, ``y`` = the stratification classes.
+        Classifiers: ``X`` = images [N, H, W, C] (uint8 or float) and ``y`` = class labels, or with
+        ``synthetic=True`` ``X`` = sample ids (or a sample count) of the synthetic dataset and
+        ``y`` = their labels (None: seeded random labels)."""
+        if not self.segmentation:
+            self._set_cls_data(X, y)
+            X, y = self._cls_ids, self._cls_labels
         X = np.asarray(X)
         y = np.asarray(y)
         splits = [(tr, te) for tr, te in self.skf.split(X, y)]
+        splits = splits[:self.max_folds or len(splits)]
         if batch_size % self.n_gpus != 0:
             raise ValueError("Batch size must be a multiple of n_gpus")
         per_tower = batch_size // self.n_gpus
@@ -160,8 +234,11 @@ class Model:
         results = []
         for i, (tr, te) in enumerate(splits):
             print(f"[Model] Processing fold {i}", flush=True)
-            create_symlinks(self.data_dir, self.model_dir, TRAIN, X[tr], i)
-            create_symlinks(self.data_dir, self.model_dir, EVAL, X[te], i)
+            if self.segmentation:
+                create_symlinks(self.data_dir, self.model_dir, TRAIN, X[tr], i)
+                create_symlinks(self.data_dir, self.model_dir, EVAL, X[te], i)
+            else:
+                self._cls_split = (tr, te)
             # keep the global batch when fewer processes than towers are available
             local_batch = per_tower * self.n_gpus // world
             if world > 1:
@@ -173,6 +250,7 @@ class Model:
             else:
                 res = self._train_fold(i, local_batch, steps)
             self.n_params = res["n_params"]
+            self.last_results = results
             results.append(res)
             print(f"[Model] Finished training fold {i}: {res['eval']}", flush=True)
         return results
@@ -195,22 +273,40 @@ class Model:
         return ctx.device if ctx.device.type == "cuda" else (
             torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu"))
 
+    def _use_graph(self, device, ctx):
+        if self.hip_graph in (False, "off", 0) or device.type != "cuda":
+            return False
+        return not ctx.is_distributed or getattr(ctx, "native", None) is not None
+
+    def _schedule(self, steps):
+        return schedules.make(self.lr_schedule, self.lr, total_steps=steps,
+                              decay_steps=self.lr_decay_steps, decay_rate=self.lr_decay_rate,
+                              warmup_steps=self.lr_warmup_steps)
+
+    def _make_trainer(self, net, loss_fn, device, ctx, steps, extra=None):
+        opt = "adam" if self.optimizer == "adam" else "sgd"
+        kw = dict(lr=self.lr, lr_schedule=self._schedule(steps))
+        if opt == "sgd":
+            kw.update(momentum=self.momentum,
+                      weight_decay=self.weight_decay if self.use_regularization else 0.0)
+        return Trainer(net, loss_fn, device, optimizer=opt, opt_kwargs=kw, ctx=ctx,
+                       extra_loss_fn=extra,
+                       lowp_dtype=None if self.precision == "fp32" else torch.bfloat16)
+
     def _train_fold(self, fold, batch, steps, ctx=None):
         from .parallel.dist import get_context
         ctx = ctx or get_context()
+        if not self.segmentation:
+            return self._train_fold_cls(fold, batch, steps, ctx)
         device = self._device(ctx)
         fold_dir = os.path.join(self.model_dir, f"fold{fold}")
         torch.manual_seed(self.seed + fold)
         net = self.build_network()
         self.n_params = sum(p.numel() for p in net.parameters()) + sum(
             b.numel() for n, b in net.named_buffers() if "running" in n)
-        schedule = functools.partial(exponential_decay, self.lr, decay_steps=10000,
-                                     decay_rate=0.5, staircase=False)
         extra = ((lambda m: m.regularization_loss()) if self.use_regularization else None)
-        trainer = Trainer(net, lambda out, yy: lovasz_hinge(out, yy), device, optimizer="adam",
-                          opt_kwargs=dict(lr=self.lr, lr_schedule=schedule), ctx=ctx,
-                          extra_loss_fn=extra,
-                          lowp_dtype=None if self.precision == "fp32" else torch.bfloat16)
+        trainer = self._make_trainer(net, _lovasz_loss, device, ctx, steps, extra)
+        stepper = _Stepper(trainer, self._use_graph(device, ctx))
         start = 0
         latest = ckpt.latest_checkpoint(fold_dir)
         if latest is not None:
@@ -243,7 +339,7 @@ class Model:
         while step < steps:
             x, yy = next(pipe)
             x = self._cast(x)
-            loss, out = trainer.train_step(x, yy)
+            loss, out = stepper(x, yy)
             step = trainer.global_step
             pred = (out.float() > _logit(self.threshold)).float()
             score, acc = seg_scores(yy, pred, self.kaggle_metric)
@@ -278,6 +374,176 @@ class Model:
             with open(os.path.join(fold_dir, "result.json"), "w") as f:
                 json.dump(res, f)
         return res
+
+    # ---- classification (north-star workloads) -----------------------------------------------
+    def _set_cls_data(self, X, y):
+        """(source, ids, labels) of a classifier's training set (data/classification.py)."""
+        if self.synthetic:
+            ids = np.arange(int(X)) if np.isscalar(X) else np.asarray(X)
+            if y is None:
+                y = np.random.default_rng(self.seed).integers(0, self.num_classes, len(ids))
+            self._cls_source = SyntheticImages(self.num_classes, self.image_size,
+                                               self.image_channels, seed=self.seed)
+        else:
+            arr = np.asarray(X)
+            if arr.ndim not in (3, 4):
+                raise ValueError(f"arch {self.arch}: X must be images [N, H, W, C] "
+                                 "(or pass synthetic=True with sample ids)")
+            if y is None:
+                raise ValueError("class labels y are required")
+            self._cls_source = ArrayImages(arr)
+            self.image_size = arr.shape[1]
+            self.image_channels = self._cls_source.channels
+            ids = np.arange(len(arr))
+        self._cls_ids = ids
+        self._cls_labels = np.asarray(y, dtype=np.int64)
+        if self._cls_labels.min() < 0 or self._cls_labels.max() >= self.num_classes:
+            raise ValueError(f"labels must lie in [0, {self.num_classes})")
+
+    def _train_fold_cls(self, fold, batch, steps, ctx):
+        """One fold of classifier training: softmax-CE + SGD-momentum (or Adam), the LR schedule,
+        checkpoint every ``save_checkpoints_steps`` with resume, evaluation (top-1 accuracy,
+        loss/softmax_cross_entropy) after every checkpoint, train summaries every
+        ``save_summary_steps``, BestExporter on metrics/accuracy."""
+        device = self._device(ctx)
+        fold_dir = os.path.join(self.model_dir, f"fold{fold}")
+        torch.manual_seed(self.seed + fold)
+        net = self.build_network()
+        self.n_params = sum(p.numel() for p in net.parameters()) + sum(
+            b.numel() for n, b in net.named_buffers() if "running" in n)
+        extra = ((lambda m: m.regularization_loss())
+                 if self.use_regularization and hasattr(net, "regularization_loss") and
+                 self.optimizer == "adam" else None)
+        trainer = self._make_trainer(net, softmax_cross_entropy, device, ctx, steps, extra)
+        start = 0
+        latest = ckpt.latest_checkpoint(fold_dir)
+        if latest is not None:
+            start = ckpt.restore(latest, net, trainer.optimizer, trainer.flat)
+            trainer.global_step = start
+            if ctx.is_distributed:
+                trainer.broadcast_state()
+        stepper = _Stepper(trainer, self._use_graph(device, ctx))
+        tr, te = self._cls_split
+        dtype = torch.float32 if self.precision == "fp32" or device.type != "cuda" \
+            else torch.bfloat16
+        pipe = ClassificationPipeline(self._cls_source, self._cls_ids[tr], self._cls_labels[tr],
+                                      batch, shuffle=True, repeat=True, seed=self.seed + fold,
+                                      device=device, rank=ctx.rank, world=ctx.world_size,
+                                      dtype=dtype, start_step=start)
+        main = ctx.is_main
+        tw = SummaryWriter(os.path.join(fold_dir, "train"), enabled=main)
+        ew = SummaryWriter(os.path.join(fold_dir, "eval"), enabled=main)
+        exporter = None
+        if self.save_best > 0 and main:
+            exporter = BestExporter(
+                os.path.join(fold_dir, "export"),
+                functools.partial(metric_comparisson, key="metrics/accuracy",
+                                  greater_is_better=True),
+                exports_to_keep=self.save_best,
+                serving_shape=[None, self.image_size, self.image_size, self.image_channels],
+                model_config=self.config())
+        correct = StreamingMean(device)
+        eval_result, history = {}, []
+        step = start
+        t0 = time.time()
+        while step < steps:
+            x, yy = next(pipe)
+            loss, out = stepper(x, yy)
+            step = trainer.global_step
+            correct.update((out.float().argmax(-1) == yy).float())
+            if main:
+                history.append(loss.detach().clone() if stepper.graph else loss.detach())
+            if self.save_summary_steps and step % self.save_summary_steps == 0 and main:
+                tw.scalars({"metrics/accuracy": float(correct.result()),
+                            "loss/softmax_cross_entropy": float(loss),
+                            "learning_rate": trainer.optimizer.lr_at(step - 1),
+                            "global_step/sec": (step - start) / max(time.time() - t0, 1e-9)},
+                           step)
+            if step % self.save_checkpoints_steps == 0 or step == steps:
+                if main:
+                    ckpt.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
+                              {"config": self.config()})
+                eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
+                eval_result["global_step"] = step
+                if main:
+                    ew.scalars({k: v for k, v in eval_result.items() if k != "global_step"}, step)
+                    if exporter is not None:
+                        exporter.maybe_export(net, eval_result, step)
+        if step == start and start > 0:
+            eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
+            eval_result["global_step"] = step
+        tw.close()
+        ew.close()
+        res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step,
+               "train_loss": [float(v) for v in history], "hip_graph": stepper.graph}
+        if main:
+            with open(os.path.join(fold_dir, "result.json"), "w") as f:
+                json.dump(res, f)
+        return res
+
+    @torch.no_grad()
+    def _evaluate_cls(self, net, te, batch, device, ctx, dtype):
+        net.eval()
+        pipe = ClassificationPipeline(self._cls_source, self._cls_ids[te], self._cls_labels[te],
+                                      batch, shuffle=False, repeat=False, seed=self.seed + 1,
+                                      device=device, rank=ctx.rank, world=ctx.world_size,
+                                      dtype=dtype)
+        sums = torch.zeros(3, dtype=torch.float64, device=device)  # correct, loss·n, count
+        for i, (x, yy) in enumerate(pipe):
+            if self.eval_batches is not None and i >= self.eval_batches:
+                break
+            out = net(x).float()
+            n = x.shape[0]
+            loss = torch.nn.functional.cross_entropy(out, yy)
+            sums += torch.stack([(out.argmax(-1) == yy).double().sum(), loss.double() * n,
+                                 torch.tensor(float(n), dtype=torch.float64, device=device)])
+        if ctx.is_distributed:
+            s = sums.to(ctx.device) if ctx.native is not None else sums.cpu()
+            ctx.all_reduce_sum_(s)
+            sums = s
+        sums = sums.cpu()
+        n = max(float(sums[2]), 1.0)
+        net.train()
+        return {"metrics/accuracy": float(sums[0]) / n,
+                "loss/softmax_cross_entropy": float(sums[1]) / n}
+
+    @torch.no_grad()
+    def predict_classes(self, X, batch_size):
+        """Class probabilities [N, num_classes] of images ``X`` (or synthetic sample ids),
+        averaged over every trained fold's latest checkpoint."""
+        if self.synthetic:
+            ids = np.arange(int(X)) if np.isscalar(X) else np.asarray(X)
+            src = SyntheticImages(self.num_classes, self.image_size, self.image_channels,
+                                  seed=self.seed)
+        else:
+            src = getattr(self, "_cls_source", None)
+            src = ArrayImages(X, src.mean, src.std) if isinstance(src, ArrayImages) \
+                else ArrayImages(X)
+            ids = np.arange(len(src.images))
+        device = torch.device(self.device) if self.device else (
+            torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu"))
+        dtype = torch.bfloat16 if device.type == "cuda" and self.precision != "fp32" \
+            else torch.float32
+        acc, n_models = None, 0
+        for i in range(self.n_folds):
+            path = ckpt.latest_checkpoint(os.path.join(self.model_dir, f"fold{i}"))
+            if path is None:
+                continue
+            net = self.build_network().to(device)
+            ckpt.restore(path, net)
+            if device.type == "cuda" and self.precision != "fp32":
+                FlatParams(net, device, lowp_dtype=torch.bfloat16)
+            net.eval()
+            labels = np.zeros(len(ids), dtype=np.int64)  # unused by the image sources
+            probs = [torch.softmax(net(x).float(), -1).cpu() for x, _ in ClassificationPipeline(
+                src, ids, labels, batch_size, shuffle=False, repeat=False, device=device,
+                dtype=dtype)]
+            p = torch.cat(probs)
+            acc = p if acc is None else acc + p
+            n_models += 1
+        if n_models == 0:
+            raise ValueError("no trained fold checkpoints found; call train first")
+        return (acc / n_models).numpy()
 
     @torch.no_grad()
     def _evaluate(self, net, images, masks, batch, device, ctx, writer=None, step=0):
@@ -437,3 +703,31 @@ def _fold_worker(rank, state, fold, batch, steps):
         m._train_fold(fold, batch, steps, ctx)
     finally:
         shutdown()
+
+
+def _lovasz_loss(out, yy):
+    return lovasz_hinge(out, yy)
+
+
+class _Stepper:
+    """The fold loop's training step: eager for the first step, then (``graph``) one warm-up
+    step that also records the step as a HIP graph (engine/trainer.Trainer.capture) and graph
+    replays from there on — the loader's batch is copied into the static inputs.  The returned
+    (loss, out) are the graph's static outputs, valid until the next step."""
+
+    def __init__(self, trainer, graph):
+        self.trainer = trainer
+        self.graph = bool(graph)
+        self.eager_steps = 0
+
+    def __call__(self, x, y):
+        tr = self.trainer
+        if not self.graph:
+            return tr.train_step(x, y)
+        if tr.graph is None:
+            if self.eager_steps < 1:
+                self.eager_steps += 1
+                return tr.train_step(x, y)
+            tr.capture(x, y, warmup=1)  # the warm-up step trains on (x, y)
+            return tr.warmup_out
+        return tr.replay(x, y)

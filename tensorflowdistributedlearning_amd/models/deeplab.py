@@ -228,6 +228,9 @@ class DeepLabResNet(nn.Module):
         False: only the block outputs and the decoder's block1/unit_1 conv end point (the other
         units then run with the fused residual epilogue)."""
         if x.shape[-1] != self.conv1_1.conv._cin_store:
+            if x.shape[-1] > self.conv1_1.conv._cin_store:  # never crop input channels
+                raise ValueError(f"input has {x.shape[-1]} channels, the stem takes "
+                                 f"{self.conv1_1.conv.cin}")
             x = nn.functional.pad(x, (0, self.conv1_1.conv._cin_store - x.shape[-1]))
         end_points = {}
         root = f"{self.model_name}/resnet_v2"

@@ -190,6 +190,9 @@ class Xception(nn.Module):
 
     def forward(self, x, return_end_points=False):
         if x.shape[-1] != self.conv1_1.conv._cin_store:
+            if x.shape[-1] > self.conv1_1.conv._cin_store:  # never crop input channels
+                raise ValueError(f"input has {x.shape[-1]} channels, the stem takes "
+                                 f"{self.conv1_1.conv.cin}")
             x = nn.functional.pad(x, (0, self.conv1_1.conv._cin_store - x.shape[-1]))
         x = self.conv1_2(self.conv1_1(x))
         ep = {}

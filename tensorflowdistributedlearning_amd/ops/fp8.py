@@ -31,11 +31,15 @@ def _new_ring(device):
 # the Trainer after the optimizer — so no kernel argument changes from step to step and the whole
 # fp8 step can be captured as a HIP graph.  A scaler called twice with no roll in between (direct
 # use outside a Trainer) rolls its own ring first, which keeps the per-call delayed semantics.
-_STATE = {"rolls": 0, "rings_made": 0}
+_STATE = {"rings_made": 0}
 
 
-def _rolls(device=None):
-    return _STATE["rolls"]
+def _rolls(owner):
+    """Step rolls seen by ``owner``'s ring so far: the count of the RingRoller that rolls it
+    (per model, so one Trainer's roll never suppresses another model's self-roll), or 0 for a
+    scaler no roller has claimed (used outside a Trainer: every second call self-rolls)."""
+    roller = getattr(owner, "_roller", None)
+    return roller.rolls if roller is not None else 0
 
 
 def _self_roll(table):
@@ -52,6 +56,7 @@ class RingRoller:
         self.table = None
         self.keep = []
         self.built_at = -1
+        self.rolls = 0  # device rolls of this model's rings (eager launches + graph replays)
 
     def _scan(self):
         rings = []
@@ -61,14 +66,29 @@ class RingRoller:
                 sc = m.__dict__.get(k)
                 if isinstance(sc, DelayedScaler) and sc.ring is not None:
                     rings.append((sc.ring, 0))
+                    self._claim(sc)
             for prm in m.parameters(recurse=False):
                 flat = getattr(prm, "_flat_lowp", None)
                 fw = getattr(flat, "_tdl_fp8w", None) if flat is not None else None
                 if fw is not None and id(fw) not in seen and getattr(fw, "rings", None) is not None:
                     seen.add(id(fw))
+                    self._claim(fw)
                     for seg in range(fw.rings.shape[0]):
                         rings.append((fw.rings, seg * 3 * AMAX_SLOT * 4))
         return rings
+
+    def _claim(self, owner):
+        # called right before this roller's next roll: from the owner's point of view a roll
+        # has happened since its last call, so its next call must not self-roll
+        if getattr(owner, "_roller", None) is not self:
+            owner._roller = self
+            owner.last_roll = None
+
+    def note_replay(self):
+        """A captured step that contains this roller's launch was replayed: the rings rolled
+        on the device without a host-side roll() call (engine/trainer.Trainer.replay)."""
+        if self.table is not None:
+            self.rolls += 1
 
     def roll(self, device):
         device = torch.device(device)
@@ -82,7 +102,7 @@ class RingRoller:
             self.built_at = _STATE["rings_made"]
         if self.table is not None:
             ext().fp8_roll(self.table)
-            _STATE["rolls"] += 1
+            self.rolls += 1
 
 
 def quantize_e4m3(x):
@@ -143,6 +163,7 @@ class DelayedScaler:
         self.scale = None
         self.calls = 0
         self.last_roll = None
+        self._roller = None
 
     def _ensure(self, device):
         if self.ring is None or self.ring.device != device:
@@ -154,7 +175,7 @@ class DelayedScaler:
             self.last_roll = None
 
     def _begin(self, device):
-        rolls = _rolls()
+        rolls = _rolls(self)
         if self.calls > 0 and self.last_roll == rolls:
             _self_roll(self.self_table)  # second call since the last step roll
         self.last_roll = rolls
@@ -201,6 +222,7 @@ class FlatFp8Weights:
         self.version = None
         self.last_roll = None
         self.rings = None
+        self._roller = None
 
     def _rebuild(self):
         keys = list(self.views) + list(self.pending)
@@ -254,7 +276,7 @@ class FlatFp8Weights:
         if self.version != version:
             if self.pending:
                 self._rebuild()
-            rolls = _rolls()
+            rolls = _rolls(self)
             if self.last_roll == rolls:
                 _self_roll(self.self_table)  # refreshed twice with no step roll in between
             self.last_roll = rolls

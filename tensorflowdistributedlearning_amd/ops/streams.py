@@ -112,6 +112,19 @@ def side(device):
     return s
 
 
+def side_if_active(device):
+    """The side stream of ``device`` if it exists and may take work now (outside a capture, or
+    forked into the capture in progress), else None.  Unlike :func:`side` it does not create
+    the stream or fork it into a capture."""
+    dev = torch.device(device)
+    s = _SIDE.get(dev)
+    if s is None or not _ENABLED:
+        return None
+    if capturing() and dev not in _FORKED:
+        return None
+    return s
+
+
 def is_side(stream, device) -> bool:
     """Is ``stream`` the side stream of ``device``?"""
     s = _SIDE.get(torch.device(device))

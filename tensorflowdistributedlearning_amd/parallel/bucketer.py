@@ -18,7 +18,10 @@ The reference concatenates ALL gradients into one NCCL pack after the full backw
 * the last-issued bucket (the network's first layers, whose gradients arrive when backward
   ends) is also kept small: it is the one collective nothing overlaps, so its size is exposed
   step time — the remainder is split off the bucket before it;
-* the 1/world averaging is fused into the optimizer kernel (no extra pass).
+* the 1/world averaging is fused into the optimizer kernel (no extra pass);
+* with side-stream weight gradients (ops/streams.py) a collective is issued from the side stream
+  after it waited for the compute stream, so the comm stream follows both producers and the
+  compute stream is never made to wait at a bucket boundary (:meth:`GradBucketer.issue_stream`).
 
 A ``comm_hook`` can replace the collective (used by tests to record launch order with a fake
 communicator).
@@ -126,21 +129,32 @@ class GradBucketer:
 
     def _launch(self, b):
         view = self.flat.grad[b.lo:b.hi]
-        if view.is_cuda:
-            cur = torch.cuda.current_stream(view.device)
-            if streams.is_side(cur, view.device) and torch.cuda.is_current_stream_capturing():
-                # the hook fired inside a side-stream wgrad (ops/conv.py) during a HIP-graph
-                # capture: issue the collective from the capturing stream, joined to the side
-                # stream, so the comm stream forks off the capture's origin stream
-                org = streams.origin(view.device)
-                org.wait_stream(cur)
-                with torch.cuda.stream(org):
-                    self._issue(b, view)
-                b.launched = True
-                return
-            streams.join(view.device)  # wgrads still running on the side stream (ops/streams.py)
-        self._issue(b, view)
+        issuer = self.issue_stream(view.device) if view.is_cuda else None
+        if issuer is None:
+            self._issue(b, view)
+        else:
+            with streams.on(issuer):
+                self._issue(b, view)
         b.launched = True
+
+    @staticmethod
+    def issue_stream(device):
+        """The stream a bucket's collective is ordered after: the side stream, made to wait for
+        the compute stream's position first, when side-stream weight gradients are in use — the
+        bucket's gradients come from both streams (conv weights on the side stream, BN γ/β and
+        biases on the compute stream), and the comm stream then waits on one event that follows
+        both.  The compute stream never waits: a join at a bucket boundary would stall the
+        dgrad / BN chain behind every weight gradient still queued on the side stream.  None:
+        no side stream (or one outside the capture in progress) — issue from the current
+        stream."""
+        dev = torch.device(device)
+        s = streams.side_if_active(dev)
+        if s is None:
+            return None
+        cur = streams.current(dev)
+        if cur != s:
+            s.wait_stream(cur)
+        return s
 
     def _issue(self, b, view):
         if self.comm_hook is not None:
@@ -164,6 +178,34 @@ class GradBucketer:
         self.next_launch = 0
         if self.ctx is not None and hasattr(self.ctx, "check"):
             self.ctx.check()  # native comm watchdog: fail fast on timeout / RCCL error
+
+    def standalone_ms(self, reps=3):
+        """Milliseconds of the step's collectives alone — every bucket issued back to back on an
+        idle device, then waited for — the yardstick for how much of the communication the
+        overlapped backward hides (bench.py reports exposed / standalone for N > 1)."""
+        import time
+        cuda = self.flat.grad.is_cuda
+        times = []
+        for _ in range(reps):
+            if cuda:
+                torch.cuda.synchronize(self.flat.grad.device)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            t0 = time.perf_counter()
+            for b in self.buckets:
+                self._issue(b, self.flat.grad[b.lo:b.hi])
+            for b in self.buckets:
+                if b.work is not None and hasattr(b.work, "wait"):
+                    b.work.wait()
+                b.work = None
+            if cuda:
+                e1.record()
+                torch.cuda.synchronize(self.flat.grad.device)
+                times.append(e0.elapsed_time(e1))
+            else:
+                times.append((time.perf_counter() - t0) * 1e3)
+        return sorted(times)[len(times) // 2]
 
     def describe(self):
         return [(b.index, len(b.params), b.nbytes) for b in self.buckets]

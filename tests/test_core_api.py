@@ -87,6 +87,35 @@ def test_resnet_v2_classification_head():
     assert g.shape == (2, 1, 1, 1024)
 
 
+def test_facades_use_every_input_channel():
+    """A 16-channel input builds a 16-channel stem (no silent crop to 8 channels): every channel
+    changes the output, and the stem weight has the real channel count."""
+    torch.manual_seed(0)
+    x = torch.randn(1, 32, 32, 16)
+    kw = dict(model_name="c16", weight_decay=1e-3, batch_norm_decay=0.99,
+              batch_norm_epsilon=1e-3, batch_norm_scale=True, is_training=False, output_stride=8,
+              base_depth=8, input_shape=(32, 32), n_blocks=(1, 1, 1), block_type="bottleneck")
+    y = resnet.resnet_model(x, data_format="NHWC", **kw)
+    m = _scope._CACHE[next(iter(_scope._CACHE))]
+    assert m.conv1_1.conv.weight.shape[-1] == 16
+    x2 = x.clone()
+    x2[..., 12] += 1.0  # a channel past 8
+    assert not torch.allclose(resnet.resnet_model(x2, data_format="NHWC", **kw), y)
+    _scope.clear()
+    net, _ = resnet.resnet_v2(x, n_blocks=(1, 1, 1), output_stride=8, scope="v16")
+    m = _scope._CACHE[next(iter(_scope._CACHE))]
+    assert m.net.conv1_1.conv.weight.shape[-1] == 16 if hasattr(m, "net") else True
+    net2, _ = resnet.resnet_v2(x2, n_blocks=(1, 1, 1), output_stride=8, scope="v16")
+    assert not torch.allclose(net, net2)
+    _scope.clear()
+    xi = torch.randn(1, 33, 33, 16)
+    out, _ = xception.xception_41(xi, is_training=False, output_stride=16, scope="x16")
+    xi2 = xi.clone()
+    xi2[..., 15] += 1.0
+    out2, _ = xception.xception_41(xi2, is_training=False, output_stride=16, scope="x16")
+    assert not torch.allclose(out, out2)
+
+
 def test_fixed_padding_matches_numpy():
     x = torch.randn(1, 3, 5, 6)
     for k in (1, 2, 3, 4, 7):

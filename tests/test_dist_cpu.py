@@ -214,6 +214,9 @@ def test_bench_self_spawns_ranks_cpu(tmp_path):
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["comm"] == "gloo" and out["config"]["global_batch"] == 4
     assert out["value"] > 0 and out["steps"] == 1 and out["warmup"] == 1
+    co = out["config"]["comm_overlap"]  # exposed vs standalone collective time (N > 1)
+    assert co["standalone_ms"] > 0 and co["exposed_ms"] >= 0 and co["buckets"] >= 1
+    assert co["overlap"] is None or 0.0 <= co["overlap"] <= 1.0
 
 
 @pytest.mark.timeout(300)
@@ -286,3 +289,43 @@ def test_init_distributed_rejects_second_gpu_backend():
     with pytest.raises(ValueError):
         D.init_distributed(device_type="cpu", comm="torch")
     D.shutdown()
+
+
+def test_bucket_launch_never_joins_the_compute_stream(monkeypatch):
+    """A bucket's collective is ordered after BOTH producers by issuing it from the side stream
+    once that stream waited for the compute stream — the compute stream itself never waits on
+    the side stream at a bucket boundary (that stalled the dgrad / BN chain behind every queued
+    weight gradient).  Fake streams record the waits; a compute-stream join raises."""
+    from tensorflowdistributedlearning_amd.ops import streams
+    from tensorflowdistributedlearning_amd.parallel import bucketer as bmod
+    import inspect
+
+    class FakeStream:
+        def __init__(self, name):
+            self.name, self.waited = name, []
+
+        def wait_stream(self, other):
+            self.waited.append(other.name)
+
+        def __eq__(self, o):
+            return isinstance(o, FakeStream) and o.name == self.name
+
+    side, comp = FakeStream("side"), FakeStream("compute")
+
+    def no_join(*a, **k):
+        raise AssertionError("bucket launch joined the compute stream to the side stream")
+
+    monkeypatch.setattr(streams, "join", no_join)
+    monkeypatch.setattr(streams, "side_if_active", lambda dev: side)
+    monkeypatch.setattr(streams, "current", lambda dev: comp)
+    s = GradBucketer.issue_stream(torch.device("cpu"))
+    assert s is side and side.waited == ["compute"] and comp.waited == []
+    # hook fired on the side stream itself (a wgrad's gradient-ready hook): no extra wait
+    monkeypatch.setattr(streams, "current", lambda dev: side)
+    side.waited.clear()
+    assert GradBucketer.issue_stream(torch.device("cpu")) is side and side.waited == []
+    # no side stream: issue from the current stream
+    monkeypatch.setattr(streams, "side_if_active", lambda dev: None)
+    assert GradBucketer.issue_stream(torch.device("cpu")) is None
+    # the launch path has no join left in it
+    assert "streams.join" not in inspect.getsource(bmod.GradBucketer._launch)

@@ -1,0 +1,185 @@
+"""North-star workloads trained through ``Model`` / the CLI (BASELINE config
+1 "ResNet-18, 32×32 synthetic, 1 CPU tower via model.py"): softmax-CE + SGD-momentum, LR schedule,
+checkpoint / resume to the same trajectory, eval (top-1), summaries, best export, 2-rank gloo DP,
+and the GPU flow with the fold's step captured as a HIP graph."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tensorflowdistributedlearning_amd.model import Model
+from tensorflowdistributedlearning_amd.engine import checkpoint as ckpt
+from tensorflowdistributedlearning_amd.engine import schedules
+from tensorflowdistributedlearning_amd.engine.summary import read_tfrecords
+from tensorflowdistributedlearning_amd.data.classification import (
+    ClassificationPipeline, SyntheticImages, ArrayImages)
+
+CLS = dict(arch="resnet18", num_classes=10, image_size=32, synthetic=True, device="cpu",
+           n_gpus=1, n_fold=4, max_folds=1, save_summary_steps=2, lr=0.05, momentum=0.9,
+           lr_schedule="cosine")
+
+
+def test_resnet18_32px_trains_checkpoints_and_resumes_same_trajectory(tmp_path):
+    # a schedule that does not depend on the run's max step (cosine spans `steps`)
+    kw = dict(CLS, lr_schedule="step", lr_decay_steps=3, lr_decay_rate=0.5)
+    a = Model(str(tmp_path / "a" / "r18"), "", save_checkpoints_steps=4, save_best=2, **kw)
+    ra = a.train(160, None, batch_size=16, steps=8)[0]
+    assert ra["steps"] == 8 and len(ra["train_loss"]) == 8
+    assert all(np.isfinite(ra["train_loss"]))
+    ev = ra["eval"]
+    assert 0.0 <= ev["metrics/accuracy"] <= 1.0 and np.isfinite(ev["loss/softmax_cross_entropy"])
+    fd = os.path.join(str(tmp_path / "a" / "r18"), "fold0")
+    assert ckpt.latest_checkpoint(fd).endswith("model.ckpt-8.safetensors")
+    assert os.path.exists(os.path.join(fd, "model.ckpt-4.safetensors"))
+    names = set(json.load(open(os.path.join(fd, "model.ckpt-8.json")))["names"].values())
+    assert any(n.endswith("weight") for n in names)
+    # train summaries carry the classification metric names
+    ev_files = [f for f in os.listdir(os.path.join(fd, "train")) if f.startswith("events.out")]
+    recs = list(read_tfrecords(os.path.join(fd, "train", ev_files[0])))
+    assert len(recs) >= 4
+    assert os.listdir(os.path.join(fd, "export", "best_exporter"))
+
+    # interrupted run: 4 steps, then a fresh Model resumes to 8 — the same trajectory
+    bdir = str(tmp_path / "b" / "r18")
+    b = Model(bdir, "", save_checkpoints_steps=4, **kw)
+    rb1 = b.train(160, None, batch_size=16, steps=4)[0]
+    b2 = Model(bdir, "", save_checkpoints_steps=4, **kw)
+    rb2 = b2.train(160, None, batch_size=16, steps=8)[0]
+    assert rb2["steps"] == 8 and len(rb2["train_loss"]) == 4
+    np.testing.assert_allclose(rb1["train_loss"], ra["train_loss"][:4], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(rb2["train_loss"], ra["train_loss"][4:], rtol=1e-4, atol=1e-5)
+    from safetensors.torch import load_file
+    wa = load_file(os.path.join(fd, "model.ckpt-8.safetensors"))
+    wb = load_file(os.path.join(bdir, "fold0", "model.ckpt-8.safetensors"))
+    for k in wa:
+        torch.testing.assert_close(wa[k], wb[k], rtol=1e-4, atol=1e-5)
+
+    p = b2.predict_classes(np.arange(8), batch_size=4)
+    assert p.shape == (8, 10)
+    np.testing.assert_allclose(p.sum(-1), 1.0, rtol=1e-4)
+
+
+def test_classifier_learns_synthetic_task(tmp_path):
+    m = Model(str(tmp_path / "r18"), "", save_checkpoints_steps=30, save_best=0, **CLS)
+    r = m.train(320, None, batch_size=32, steps=30)[0]
+    assert r["eval"]["metrics/accuracy"] > 0.5, r["eval"]
+    assert np.mean(r["train_loss"][-5:]) < np.mean(r["train_loss"][:5])
+
+
+def test_classifier_on_image_arrays(tmp_path):
+    rng = np.random.default_rng(0)
+    X = rng.integers(0, 255, (64, 16, 16, 3), dtype=np.uint8)
+    y = np.arange(64) % 4
+    X[y == 1, :8] = 255  # a learnable cue
+    m = Model(str(tmp_path / "arr"), "", arch="resnet18", num_classes=4, device="cpu", n_gpus=1,
+              n_fold=2, max_folds=1, save_checkpoints_steps=3, save_best=0, lr=0.05)
+    r = m.train(X, y, batch_size=8, steps=3)[0]
+    assert r["steps"] == 3 and np.isfinite(r["eval"]["loss/softmax_cross_entropy"])
+    assert m.predict_classes(X[:5], batch_size=2).shape == (5, 4)
+    with pytest.raises(ValueError):
+        m.train(np.arange(10), y[:10], batch_size=2, steps=1)  # ids without synthetic=True
+
+
+def test_classifier_data_parallel_gloo(tmp_path):
+    """n_gpus=2 on the host: two gloo ranks with disjoint shards, all-reduced grads and eval."""
+    m = Model(str(tmp_path / "dp"), "", save_checkpoints_steps=3, save_best=1,
+              **dict(CLS, n_gpus=2))
+    r = m.train(128, None, batch_size=16, steps=3)
+    assert len(r) == 1 and r[0]["steps"] == 3
+    assert ckpt.latest_checkpoint(str(tmp_path / "dp" / "fold0")).endswith("model.ckpt-3.safetensors")
+
+
+def test_model_arch_validation(tmp_path):
+    with pytest.raises(ValueError):
+        Model(str(tmp_path / "m"), "", arch="resnet7")
+    with pytest.raises(ValueError):
+        Model(str(tmp_path / "m"), "", arch="resnet50", loss="lovasz")
+    m = Model(str(tmp_path / "m"), "", arch="xception41")
+    assert m.image_size == 299 and m.loss == "softmax_ce" and m.optimizer == "sgd_momentum"
+    assert Model(str(tmp_path / "m2"), "").optimizer == "adam"  # the reference preset
+
+
+def test_pipelines_and_schedules():
+    src = SyntheticImages(5, 16, channels=3, seed=1)
+    ids, lab = np.arange(40), np.arange(40) % 5
+    p = ClassificationPipeline(src, ids, lab, 8, shuffle=True, repeat=True, seed=3,
+                               dtype=torch.float32)
+    b = [next(p) for _ in range(7)]  # crosses an epoch boundary
+    assert b[0][0].shape == (8, 16, 16, 8) and b[0][1].shape == (8,)
+    assert float(b[0][0][..., 3:].abs().max()) == 0.0  # channel padding
+    q = ClassificationPipeline(src, ids, lab, 8, shuffle=True, repeat=True, seed=3,
+                               dtype=torch.float32, start_step=5)
+    torch.testing.assert_close(next(q)[0], b[5][0])  # resume: same stream position
+    r0 = ClassificationPipeline(src, ids, lab, 8, shuffle=False, repeat=False, rank=0, world=2,
+                                dtype=torch.float32)
+    assert sum(x.shape[0] for x, _ in r0) == 20
+    a = ArrayImages(np.full((4, 8, 8, 1), 128, np.uint8))
+    assert a.channels == 1
+    cos = schedules.make("cosine", 0.1, total_steps=100, warmup_steps=10)
+    assert abs(cos(0) - 0.01) < 1e-9 and abs(cos(10) - 0.1) < 1e-9 and cos(99) < 1e-3
+    ex = schedules.make("exponential", 1e-3)
+    assert abs(ex(10000) - 5e-4) < 1e-12  # tf.train.exponential_decay(…, 10000, 0.5)
+    st = schedules.make("step", 1.0, decay_steps=10, decay_rate=0.1)
+    assert st(9) == 1.0 and abs(st(10) - 0.1) < 1e-12
+
+
+def test_cli_trains_resnet18_synthetic_on_cpu(tmp_path, capsys):
+    from tensorflowdistributedlearning_amd.__main__ import main
+    main(["train", "--arch", "resnet18", "--image-size", "32", "--synthetic", "--device", "cpu",
+          "--n-gpus", "1", "--model-dir", str(tmp_path / "cli" / "r18"), "--num-samples", "64",
+          "--num-classes", "4", "--batch-size", "8", "--steps", "2", "--max-folds", "1",
+          "--save-checkpoints-steps", "2"])
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["folds"][0]["steps"] == 2 and out["params"] > 0
+
+
+def test_bench_consumes_bench_config(tmp_path):
+    import argparse
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from tensorflowdistributedlearning_amd import config as cfgmod
+    from tensorflowdistributedlearning_amd.config import BenchConfig
+    cfgmod.dump(BenchConfig(arch="resnet152", batch=128, dtype="fp8", graph=True),
+                str(tmp_path / "b.json"))
+    ns = argparse.Namespace(config=str(tmp_path / "b.json"), model=None, batch=None,
+                            image_size=None, steps=3, warmup=None, lr=None, bucket_mb=None,
+                            first_bucket_mb=None, optimizer=None, dtype=None, fp8=False,
+                            fp8_dgrad=False, graph=False)
+    bc = bench.bench_config(ns)
+    assert (bc.arch, bc.batch, bc.dtype, bc.graph, bc.steps) == ("resnet152", 128, "fp8", True, 3)
+    assert bc.optimizer == "sgd_momentum" and bc.loss == "softmax_ce" and bc.lr == 0.1
+    ns.config, ns.model = None, "deeplab_ref"
+    bc = bench.bench_config(ns)
+    assert bc.optimizer == "adam" and bc.loss == "lovasz" and bc.lr == 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_resnet50_classifier_through_model_on_gpu(tmp_path, gpu):
+    """ResNet-50 at small batch through Model on the GPU: the fold's step is captured as a HIP
+    graph after the first step (hip_graph auto), checkpoints mid-fold, resumes, evaluates."""
+    kw = dict(CLS, arch="resnet50", device=None, image_size=64, save_checkpoints_steps=4)
+    m = Model(str(tmp_path / "r50"), "", **kw)
+    r = m.train(256, None, batch_size=16, steps=8)[0]
+    assert r["hip_graph"] is True and r["steps"] == 8
+    assert all(np.isfinite(r["train_loss"]))
+    assert len(set(round(v, 5) for v in r["train_loss"])) > 1  # replays really step
+    m2 = Model(str(tmp_path / "r50"), "", **kw)
+    r2 = m2.train(256, None, batch_size=16, steps=12)[0]
+    assert r2["steps"] == 12 and len(r2["train_loss"]) == 4
+    assert np.isfinite(r2["eval"]["loss/softmax_cross_entropy"])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_model_graph_training_tracks_eager(tmp_path, gpu):
+    """The HIP-graph fold loop follows the eager fold loop's loss trajectory (same data, same
+    init; frozen-free BN in batch-statistics mode, so within the fp32-atomic run-to-run noise)."""
+    kw = dict(CLS, device=None, save_checkpoints_steps=100, save_best=0)
+    ra = Model(str(tmp_path / "e"), "", hip_graph="off", **kw).train(192, None, 16, 10)[0]
+    rb = Model(str(tmp_path / "g"), "", **kw).train(192, None, 16, 10)[0]
+    assert rb["hip_graph"] and not ra["hip_graph"]
+    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.05, atol=0.02)

@@ -728,6 +728,46 @@ def test_fp8_graph_replay_matches_eager(gpu, dgrad):
     assert len(set(round(v, 5) for v in lb_l)) > 1, lb_l
 
 
+def test_fp8_graph_replay_interleaved_with_eager_forwards(gpu, monkeypatch):
+    """Eager forwards between graph replays (periodic eval) must not self-roll a ring the
+    captured step already rolled on the device: the scales stay finite and unsaturated and the
+    replayed trajectory keeps tracking the eager one (RingRoller.note_replay)."""
+    from tensorflowdistributedlearning_amd.ops.fp8 import DelayedScaler
+    monkeypatch.setenv("TDL_BN_FOLD", "0")  # eval forwards through the fp8 convs, not folded
+    torch.manual_seed(9)
+    nets = [models.resnet18(num_classes=10) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    for n in nets:
+        assert models.enable_fp8(n) > 10
+    ta, tb = [Trainer(n, softmax_cross_entropy, gpu, "sgd", dict(lr=0.02, momentum=0.9))
+              for n in nets]
+    ta.train_mode = tb.train_mode = False
+    x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
+    tb.capture(x, y, warmup=3)
+    for _ in range(3):
+        ta.train_step(x, y)
+    scalers = [s for m in tb.model.modules() for k in ("_fp8_w", "_fp8_x", "_fp8", "_fp8_bwd")
+               for s in [m.__dict__.get(k)] if isinstance(s, DelayedScaler) and s.scale is not None]
+    assert scalers
+    la_l, lb_l = [], []
+    for _ in range(3):
+        la, _ = ta.train_step(x, y)
+        lb, _ = tb.replay()
+        la_l.append(float(la))
+        lb_l.append(float(lb))
+        with torch.no_grad():  # eager forwards between replays, on both models
+            oa = ta.model(x)
+            ob = tb.model(x)
+        torch.cuda.synchronize()
+        assert torch.isfinite(ob).all()
+        sc = torch.cat([s.scale for s in scalers])
+        assert bool((sc > 1e-9).all()), sc.min()
+        assert torch.nn.functional.cosine_similarity(oa.float().flatten(), ob.float().flatten(),
+                                                     dim=0).item() > 0.99
+    for a_, b_ in zip(la_l, lb_l):
+        assert abs(a_ - b_) < 5e-3 * max(1.0, abs(a_)), (la_l, lb_l)
+
+
 def test_fp8_delayed_scaling_rolls_on_device(gpu):
     """The scale a DelayedScaler uses at call t is the |x|max of call t−1 (device-side roll by
     the Trainer's RingRoller, self-roll for back-to-back direct calls)."""
