@@ -208,10 +208,23 @@ bool conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::opt
     TORCH_CHECK(res->sizes() == y.sizes(), "conv_fwd res: shaped like y");
     a.res = BF(*res);
     if (a.M == 0) return true;
-    return conv_fwd_res_launch(a, stream());
+    float* det_stats = nullptr;
+    if (a.stats && deterministic()) {
+      det_stats = a.stats;
+      a.stats = nullptr;
+    }
+    const bool ran = conv_fwd_res_launch(a, stream());  // false: nothing launched
+    if (ran && det_stats) bn_stats_launch(BF(y), det_stats, a.M, a.K, stream());
+    return ran;
   }
   if (a.M == 0) return true;
+  float* det_stats = nullptr;
+  if (a.stats && deterministic()) {  // fixed-order statistics pass instead of epilogue atomics
+    det_stats = a.stats;
+    a.stats = nullptr;
+  }
   conv_fwd_launch(a, stream());
+  if (det_stats) bn_stats_launch(BF(y), det_stats, a.M, a.K, stream());
   return true;
 }
 
@@ -236,7 +249,13 @@ void conv_fwd_fp8(Tensor x8, Tensor w8, Tensor y, c10::optional<Tensor> stats, T
   a.scale_x = sx.data_ptr<float>(); a.scale_w = sw_.data_ptr<float>();
   a.M = a.N * a.Ho * a.Wo; a.Ng = a.K; a.Kg = a.R * a.S * a.C; a.ldc = a.K; a.relu = relu;
   if (a.M == 0) return;
+  float* det_stats = nullptr;
+  if (a.stats && deterministic()) {
+    det_stats = a.stats;
+    a.stats = nullptr;
+  }
   conv_fwd_fp8_launch(a, stream());
+  if (det_stats) bn_stats_launch(BF(y), det_stats, a.M, a.K, stream());
 }
 
 // amax rings are fp32 [3, AMAX_SLOT] (kernels.h); slot indices 0..2
@@ -339,8 +358,11 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
     CHECK_T(*bn_red, torch::kFloat32);
     TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_red->numel() == 2 * dx.size(3) &&
                 bn_red->is_contiguous(), "conv_dgrad bn_x: shape of dx, bn_red fp32 [2, C]");
-    a.bn_x = BF(*bn_x);
-    a.stats = bn_red->data_ptr<float>();
+    // deterministic mode: no fused BN-backward sums (epilogue atomics); the BN reduces itself
+    if (!deterministic()) {
+      a.bn_x = BF(*bn_x);
+      a.stats = bn_red->data_ptr<float>();
+    }
   }
   if (a.M == 0) return false;
   return conv_dgrad_launch(a, stream());
@@ -712,6 +734,7 @@ void maxpool_bwd(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t
 bool maxpool_bwd_stats(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t pt,
                        int64_t pl, Tensor bn_x, Tensor mask, Tensor bn_red) {
   if (is_f32(dy)) return false;  // fp32: no fused ReLU mask / BN statistics
+  if (deterministic()) return false;  // epilogue atomics: the BN reduces itself (det.hip)
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
   CHECK_T(bn_x, torch::kBFloat16);
@@ -1084,7 +1107,7 @@ struct PyLoader {
   bool pin;
   PyLoader(std::vector<std::string> images, std::vector<std::string> masks, int batch, bool augment,
            bool shuffle, bool repeat, int64_t seed, int threads, int prefetch, int channels,
-           int transformation, bool pin_memory, py::dict aug)
+           int transformation, bool pin_memory, py::dict aug, bool fp32)
       : has_masks(!masks.empty()), pin(pin_memory) {
     tdl_rt::AugConfig cfg;
     for (auto item : aug) {
@@ -1102,7 +1125,7 @@ struct PyLoader {
     }
     impl.reset(new tdl_rt::BatchLoader(images, masks, batch, augment, shuffle, repeat,
                                        (uint64_t)seed, threads, prefetch, channels,
-                                       transformation, cfg));
+                                       transformation, cfg, fp32));
   }
   py::object next() {
     tdl_rt::Batch b;
@@ -1114,8 +1137,14 @@ struct PyLoader {
     if (!ok) return py::none();
     const int B = impl->batch(), H = impl->height(), W = impl->width(), C = impl->channels();
     auto opt = torch::TensorOptions().pinned_memory(pin);
-    Tensor x = torch::empty({B, H, W, C}, opt.dtype(torch::kBFloat16));
-    memcpy(x.data_ptr(), b.x.data(), b.x.size() * 2);
+    Tensor x;
+    if (impl->fp32()) {
+      x = torch::empty({B, H, W, C}, opt.dtype(torch::kFloat32));
+      memcpy(x.data_ptr(), b.xf.data(), b.xf.size() * 4);
+    } else {
+      x = torch::empty({B, H, W, C}, opt.dtype(torch::kBFloat16));
+      memcpy(x.data_ptr(), b.x.data(), b.x.size() * 2);
+    }
     Tensor ids = torch::from_blob(b.ids.data(), {(int64_t)b.ids.size()}, torch::kInt64).clone();
     if (has_masks) {
       Tensor y = torch::empty({B, H, W, 1}, opt.dtype(torch::kFloat32));
@@ -1266,6 +1295,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "conv kernel selection: 0 register-staged only, 1 LDS-DMA for large problems (default), "
         "2 LDS-DMA whenever aligned, -1 environment (TDL_CONV_GLDS)");
   m.def("conv_glds_mode", &conv_glds_mode);
+  m.def("deterministic", &deterministic,
+        "deterministic mode on (fixed-order slab reductions instead of fp32 atomics)");
+  m.def("det_set", &det_set, "deterministic mode: 1 on, 0 off, -1 environment (TDL_DETERMINISTIC)");
+  m.def("conv_set_halo_mode", &conv_set_halo_mode,
+        "halo-tiled stride-1 conv: -1 environment (TDL_HALO, default 1), 0 off, 1 default "
+        "selection, 2 every eligible problem regardless of size (tests)");
   m.def("conv_set_m32", &conv_set_m32, "32x32x16-MFMA K loop for KC-operand LDS-DMA convs (-1: env)");
   m.def("conv_m32", &conv_m32);
   m.def("conv_f32_set_tile", &conv_f32_set_tile, "fp32 conv FWD/DGRAD tile override (0, 0: auto)");
@@ -1296,11 +1331,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("world", [](PyComm& p) { return p.c->world(); });
   py::class_<PyLoader>(m, "BatchLoader")
       .def(py::init<std::vector<std::string>, std::vector<std::string>, int, bool, bool, bool,
-                    int64_t, int, int, int, int, bool, py::dict>(),
+                    int64_t, int, int, int, int, bool, py::dict, bool>(),
            py::arg("images"), py::arg("masks"), py::arg("batch"), py::arg("augment"),
            py::arg("shuffle"), py::arg("repeat"), py::arg("seed"), py::arg("threads"),
            py::arg("prefetch"), py::arg("channels"), py::arg("transformation"),
-           py::arg("pin_memory") = false, py::arg("aug") = py::dict())
+           py::arg("pin_memory") = false, py::arg("aug") = py::dict(),
+           py::arg("fp32") = false)
       .def("next", &PyLoader::next)
       .def_property_readonly("num_batches", [](PyLoader& l) { return l.impl->num_batches(); })
       .def_property_readonly("height", [](PyLoader& l) { return l.impl->height(); })

@@ -31,7 +31,7 @@ template <int KIND>  // 0: stats(x) ; 1: bwd reduce(dy,y,x)
 __global__ void reduce_scalar_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ y,
                                      const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                      float* __restrict__ out, long M, int C, long rows_per_block,
-                                     int relu) {
+                                     int relu, float* __restrict__ slab) {
   __shared__ float red[2][4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + lane;
@@ -60,8 +60,15 @@ __global__ void reduce_scalar_kernel(const bf16_t* __restrict__ a, const bf16_t*
   red[1][w][lane] = s1;
   __syncthreads();
   if (w == 0 && c < C) {
-    atomicAdd(out + c, red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane]);
-    atomicAdd(out + C + c, red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane]);
+    const float a0 = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+    const float a1 = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+    if (slab) {  // deterministic mode: this block's row of the slab (det.hip)
+      slab[blockIdx.x * 2L * C + c] = a0;
+      slab[blockIdx.x * 2L * C + C + c] = a1;
+    } else {
+      atomicAdd(out + c, a0);
+      atomicAdd(out + C + c, a1);
+    }
   }
 }
 
@@ -97,7 +104,8 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ x,
                                                         const float* __restrict__ coef,
                                                         float* __restrict__ out, long M, int C,
-                                                        long rows_per_block, int relu, long lda) {
+                                                        long rows_per_block, int relu, long lda,
+                                                        float* __restrict__ slab) {
   // lda: row stride (elements) of `a` (C, or wider for a channel slice of a concat gradient)
   __shared__ float red[2][NT][9];  // +1 pad against bank conflicts
   const int cvecs = C >> 3;
@@ -182,7 +190,10 @@ __global__ void __launch_bounds__(NT) reduce_vec_kernel(const bf16_t* __restrict
     const int v = c >> 3, j = c & 7;
     float s = 0.f;
     for (int r = 0; r < rpp; ++r) s += red[which][r * cvecs + v][j];
-    atomicAdd(out + which * C + c, s);
+    if (slab)
+      slab[blockIdx.x * 2L * C + which * C + c] = s;
+    else
+      atomicAdd(out + which * C + c, s);
   }
 }
 
@@ -197,7 +208,8 @@ __global__ void __launch_bounds__(NT) reduce2_vec_kernel(const bf16_t* __restric
                                                          const float* __restrict__ coef,
                                                          float* __restrict__ out,
                                                          float* __restrict__ out2, long M, int C,
-                                                         long rows_per_block) {
+                                                         long rows_per_block,
+                                                         float* __restrict__ slab) {
   __shared__ float red[3][NT][9];
   const int cvecs = C >> 3;
   const int rpp = NT / cvecs;
@@ -252,7 +264,17 @@ __global__ void __launch_bounds__(NT) reduce2_vec_kernel(const bf16_t* __restric
     const int v = c >> 3, j = c & 7;
     float sum = 0.f;
     for (int r = 0; r < rpp; ++r) sum += red[which][r * cvecs + v][j];
-    if (which == 0) {
+    if (slab) {  // row layout [Σg | Σg·x̂ | Σg | Σg·x2]: out = cols [0, 2C), out2 = [2C, 4C)
+      float* row = slab + blockIdx.x * 4L * C;
+      if (which == 0) {
+        row[c] = sum;
+        row[2 * C + c] = sum;
+      } else if (which == 1) {
+        row[C + c] = sum;
+      } else {
+        row[3 * C + c] = sum;
+      }
+    } else if (which == 0) {
       atomicAdd(out + c, sum);
       atomicAdd(out2 + c, sum);
     } else if (which == 1) {
@@ -284,33 +306,37 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     long blocks = std::min<long>(std::min<long>(cap, cap_atom), std::max<long>(1, M / (rpp * minr)));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
+    float* slab = deterministic() ? det_slab((size_t)blocks * 2 * C, st) : nullptr;
     if (u == 8)
       if (ntm)
         hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8, true>), dim3(blocks), dim3(NT), 0, st, a, y, x,
-                           coef, out, M, C, rpb, relu, lda);
+                           coef, out, M, C, rpb, relu, lda, slab);
       else
         hipLaunchKernelGGL((reduce_vec_kernel<KIND, 8>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                           out, M, C, rpb, relu, lda);
+                           out, M, C, rpb, relu, lda, slab);
     else if (u == 2)
       if (ntm)
         hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2, true>), dim3(blocks), dim3(NT), 0, st, a, y, x,
-                           coef, out, M, C, rpb, relu, lda);
+                           coef, out, M, C, rpb, relu, lda, slab);
       else
         hipLaunchKernelGGL((reduce_vec_kernel<KIND, 2>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                           out, M, C, rpb, relu, lda);
+                           out, M, C, rpb, relu, lda, slab);
     else
       if (ntm)
         hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4, true>), dim3(blocks), dim3(NT), 0, st, a, y, x,
-                           coef, out, M, C, rpb, relu, lda);
+                           coef, out, M, C, rpb, relu, lda, slab);
       else
         hipLaunchKernelGGL((reduce_vec_kernel<KIND, 4>), dim3(blocks), dim3(NT), 0, st, a, y, x, coef,
-                           out, M, C, rpb, relu, lda);
+                           out, M, C, rpb, relu, lda, slab);
+    if (slab) slab_sum_launch(slab, out, (int)blocks, 2L * C, 2L * C, st);
   } else {
     long blocks = std::min<long>(512, std::max<long>(1, M / 64));
     long rpb = (M + blocks - 1) / blocks;
     blocks = (M + rpb - 1) / rpb;
+    float* slab = deterministic() ? det_slab((size_t)blocks * 2 * C, st) : nullptr;
     hipLaunchKernelGGL(reduce_scalar_kernel<KIND>, dim3(blocks, (C + 63) / 64), dim3(NT), 0, st, a, y,
-                       x, coef, out, M, C, rpb, relu);
+                       x, coef, out, M, C, rpb, relu, slab);
+    if (slab) slab_sum_launch(slab, out, (int)blocks, 2L * C, 2L * C, st);
   }
 }
 
@@ -706,12 +732,17 @@ bool bn_bwd_reduce2_launch(const bf16_t* dy, const bf16_t* x, const bf16_t* x2, 
   const long rpb = (M + blocks - 1) / blocks;
   blocks = (M + rpb - 1) / rpb;
   static const bool ntm = env_int("TDL_BN_NT", 1) != 0;  // non-temporal streaming
+  float* slab = deterministic() ? det_slab((size_t)blocks * 4 * C, st) : nullptr;
   if (ntm)
     hipLaunchKernelGGL((reduce2_vec_kernel<4, true>), dim3(blocks), dim3(NT), 0, st, dy, x, x2, coef, red,
-                       red2, M, C, rpb);
+                       red2, M, C, rpb, slab);
   else
     hipLaunchKernelGGL((reduce2_vec_kernel<4>), dim3(blocks), dim3(NT), 0, st, dy, x, x2, coef, red, red2,
-                       M, C, rpb);
+                       M, C, rpb, slab);
+  if (slab) {
+    slab_sum_launch(slab, red, (int)blocks, 2L * C, 4L * C, st);
+    slab_sum_launch(slab + 2 * C, red2, (int)blocks, 2L * C, 4L * C, st);
+  }
   return true;
 }
 

@@ -241,20 +241,28 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 // FRES (FWD): add the residual a.res (laid out like the output) before the ReLU — the
 // DeepLab unit's relu(conv3 + bias + shortcut) in one pass (the statistics then are those of
 // the next unit's pre-activation BN input)
+// ROWS: the caller supplies each fragment's output-row byte offset in rows_in[] (ROW_OOB for
+// lanes without an output pixel — conv_halo.hip's padded / tail lanes, whose accumulators hold
+// values that must not reach memory or the statistics, so STATS then masks by row validity)
 template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false,
-          bool NJ = false, bool FRES = false>
+          bool NJ = false, bool FRES = false, bool ROWS = false>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
-                                                float (&s_sum)[RN][4], float (&s_sq)[RN][4]) {
+                                                float (&s_sum)[RN][4], float (&s_sq)[RN][4],
+                                                const uint32_t* rows_in = nullptr) {
   // Row byte offsets are 32-bit with invalid rows pushed past the buffer (ROW_OOB): a
   // fragment's store offset is then row base + a compile-time constant.  Rows past the GEMM's
   // M hold zeros (their A rows were fetched out of range), so the statistics need no mask.
   uint32_t rbase[RM];
 #pragma unroll
   for (int rm = 0; rm < RM; ++rm) {
-    const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
-    rbase[rm] = m < T.Mc ? out_row_fast<MODE, DGM>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
+    if constexpr (ROWS) {
+      rbase[rm] = rows_in[rm];
+    } else {
+      const int m = T.bm0 + wm * TM + rm * 16 + (lane & 15);
+      rbase[rm] = m < T.Mc ? out_row_fast<MODE, DGM>(a, T, m) * (uint32_t)a.ldc * 2u : ROW_OOB;
+    }
   }
   const int c0 = T.bn0 + wn * TN + (lane >> 4) * 4;  // this lane's column in fragment rn = 0
   const bool cols_ok = T.bn0 + wn * TN + TN <= a.Ng;   // wave-uniform: no ragged columns
@@ -379,8 +387,9 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
         __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
       if constexpr (STATS && MODE == DGRAD) {
         // (Σg, Σg·x) of the stored bf16 g; rows past M store zeros (x reads there return 0)
-        const float v0 = __uint_as_float(pk[rn][0] << 16), v1 = __uint_as_float(pk[rn][0] & 0xffff0000u);
-        const float v2 = __uint_as_float(pk[rn][1] << 16), v3 = __uint_as_float(pk[rn][1] & 0xffff0000u);
+        const float rg = (!ROWS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
+        const float v0 = __uint_as_float(pk[rn][0] << 16) * rg, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rg;
+        const float v2 = __uint_as_float(pk[rn][1] << 16) * rg, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rg;
         s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
         s_sq[rn][0] = fmaf(v0, __uint_as_float(xv[rm][rn][0] << 16), s_sq[rn][0]);
         s_sq[rn][1] = fmaf(v1, __uint_as_float(xv[rm][rn][0] & 0xffff0000u), s_sq[rn][1]);
@@ -388,7 +397,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
         s_sq[rn][3] = fmaf(v3, __uint_as_float(xv[rm][rn][1] & 0xffff0000u), s_sq[rn][3]);
       } else if constexpr (STATS) {
         // statistics of the stored bf16 values; rows past M are zero unless a bias was added
-        const float rv = (!BIAS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
+        const float rv = (!(BIAS || ROWS) || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
         const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;
         const float v2 = __uint_as_float(pk[rn][1] << 16) * rv, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rv;
         s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;

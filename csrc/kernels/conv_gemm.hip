@@ -741,6 +741,7 @@ static int pick_tpb(long tiles, int nkt) {
 }
 
 void conv_fwd_launch(const ConvArgs& a0, hipStream_t st) {
+  if (conv_fwd_halo(a0, st)) return;
   if (conv_fwd_glds(a0, st)) return;
   ConvArgs a = a0;
   convk::set_fastdivs(a);
@@ -798,6 +799,10 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   const bool masked = (a.sh > 1 && a.dh > 1) || (a.sw > 1 && a.dw > 1) ||
                       a.sh * a.sw > MAX_DG_CLASSES;
   a.dg_masked = masked ? 1 : 0;
+  if (!masked && a.sh == 1 && a.sw == 1) {  // stride 1: the halo-tiled direct conv
+    bool fused = false;
+    if (conv_dgrad_halo(a, st, &fused)) return fused;
+  }
   // build parity classes
   int ncls = 0;
   long Mmax = 0;

@@ -1,0 +1,626 @@
+// Halo-tiled direct convolution for stride-1 R×S filters (the 3×3 bodies of ResNet-18/50/152 and
+// of the reference DeepLab net, /root/reference/core/resnet.py:137-138) on gfx950 — forward and
+// input gradient.
+//
+// Why: the implicit-GEMM LDS-DMA kernel (conv_glds.hip) re-gathers the activation operand from
+// L2 for every filter tap — a 3×3 conv DMAs its A tile nine times per 64-channel chunk (32 KiB per
+// K-step of a 256×128 tile, 48 KiB with the weights), with per-lane bounds checks on every piece.
+// That footprint caps the ring at 3 stages and the DMA issue + tap arithmetic made the K-loop
+// vector-issue bound (≈30–40 % MFMA-busy on the ResNet-50 3×3 convs).  Here:
+//
+//  * a tile is TR complete output rows (of one or several images) × BN output channels; its
+//    input rows plus the filter halo — every input pixel the tile's taps touch, zero-padded — go
+//    to LDS ONCE per 64-channel chunk (`buffer_load … lds`, range-checked: padding taps read
+//    zeros, no per-tap checks), double-buffered so the next chunk / tile streams in under the
+//    current chunk's R·S K-steps;
+//  * a K-step is one tap × 64 channels: only the weight tile (BN × 64) is DMA'd per step, so the
+//    weight ring is 16 KiB per stage; the A fragment of a tap is the same halo image read at a
+//    wave-uniform slot offset (per-lane slot + tap delta, one swizzle per fragment);
+//  * persistent workgroups walk their tiles as one flat (tile, chunk, tap) sequence; the counted
+//    `s_waitcnt vmcnt` covers weight pieces, halo fills and epilogue stores in issue order;
+//  * epilogue shared with the implicit-GEMM kernels (conv_common.h store_tile_bf16, rows given):
+//    bias / ReLU / BN Σ, Σ² (forward), residual join / ReLU bit mask / BN-backward Σg, Σg·x (input
+//    gradient).
+//
+// The input gradient of a stride-1 conv is the same direct conv on dy with the taps mirrored and
+// the weights read as W[k][r][s][c] with k the reduction (a transposed, "MC" LDS image read with
+// ds_read_b64_tr_b16).
+#include "conv_common.h"
+
+namespace tdl {
+
+namespace {
+using namespace convk;
+
+constexpr int HALO_MAXTAP = 16;
+
+// geometry of one halo conv (host-prepared)
+struct HaloGeom {
+  int N, Hi, Wi, Ci;     // direct-conv input: FWD x [N,H,W,C]; DGRAD dy [N,Ho,Wo,K]
+  int Ho, Wo, Co;        // output: FWD y; DGRAD dx
+  int ntap, nchunk;      // R·S taps; Ci / 64 channel chunks
+  int tap_d[HALO_MAXTAP];  // per tap: halo slot delta (oy_t − oy_min)·HP + (ox_t − ox_min)
+  int tap_b[HALO_MAXTAP];  // per tap: weight element offset
+  int oy_min, ox_min, ext_h, ext_w;
+  int ldb;               // FWD: weight row (output channel) stride; DGRAD: k-row stride
+  int TR, HP;            // output rows per tile; halo pitch (slots per halo row)
+  int nrb, ncb, tpb;     // row blocks, column blocks, tiles per workgroup
+  FastDiv fd_HP, fd_Wo, fd_Ho, fd_seg;  // fd_seg: halo rows of a full image segment (Ho + ext_h)
+};
+
+template <int N>
+__device__ __forceinline__ void hwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void hbarrier() { asm volatile("s_barrier" ::: "memory"); }
+constexpr int vmc(int v) { return v < 63 ? v : 63; }
+
+// s_waitcnt vmcnt(IB·ahead + HL·nh + E·ne): the younger VMEM ops of the step being waited for
+// (weight pieces of `ahead` later steps, `nh` halo fills among them, `ne` epilogues' stores).
+// Counting fewer than are outstanding only waits longer, so nh / ne are clamped to 1.
+template <int IB, int HL, int E, int ST, int A = 0>
+__device__ __forceinline__ void wait_halo(int ahead, int nh, int ne) {
+  if constexpr (A <= ST - 2) {
+    if (ahead == A) {
+      if (nh == 0) {
+        if (ne == 0) hwait<vmc(IB * A)>(); else hwait<vmc(IB * A + E)>();
+      } else {
+        if (ne == 0) hwait<vmc(IB * A + HL)>(); else hwait<vmc(IB * A + HL + E)>();
+      }
+      return;
+    }
+    wait_halo<IB, HL, E, ST, A + 1>(ahead, nh, ne);
+  } else {
+    hwait<0>();
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) char lds_char_t;
+
+__device__ __forceinline__ void hdma16(rsrc_t r, char* lds_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_base, 16, voff, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 hread(uint32_t addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+template <int N, int I = 0>
+__device__ __forceinline__ void hread_rows(bf16x8 (&f)[N], uint32_t base) {
+  if constexpr (I < N) {
+    uint4 v;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(I * 2048) : "memory");
+    f[I] = __builtin_bit_cast(bf16x8, v);
+    hread_rows<N, I + 1>(f, base);
+  }
+}
+template <int COLS, int KK>
+__device__ __forceinline__ bf16x8 hread_mc(uint32_t addr) {
+  v2u32 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(addr), "n"(KK * 64 * COLS) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(addr), "n"(KK * 64 * COLS + 8 * COLS) : "memory");
+  uint4 v = make_uint4(lo[0], lo[1], hi[0], hi[1]);
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ void hlgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// an invalid DMA source: past any operand buffer even after a chunk / tap offset is added
+// (hosts keep operand buffers below 1.75 GiB)
+constexpr uint32_t HOOB = 0x80000000u;
+
+// Tile placement: workgroup b owns column block cb and row blocks [grp·tpb, +tpb) (its tiles
+// share the weight column block, so BN statistics flush once); the ncb workgroups of a row
+// group run together and read the same halo rows from L2.
+struct HTile {
+  int rho0, rows;   // first global output row (n·Ho + h), rows in the tile
+  int n_first, h_first;
+};
+
+__device__ __forceinline__ HTile htile(const HaloGeom& g, int rb) {
+  HTile t;
+  t.rho0 = rb * g.TR;
+  t.rows = min(g.TR, g.N * g.Ho - t.rho0);
+  t.n_first = (int)fdiv((uint32_t)t.rho0, g.fd_Ho);
+  t.h_first = t.rho0 - t.n_first * g.Ho;
+  return t;
+}
+
+template <int MODE, int BN, int WM, int WN, int RM, int ST, int HL, bool BIAS, bool STATS, bool NJ>
+__global__ void __launch_bounds__(512, 1) conv_halo_kernel(ConvArgs a, HaloGeom g) {
+  constexpr int NW = 8;
+  static_assert(WM * WN == NW, "8 waves");
+  constexpr int TN = BN / WN, RN = TN / 16, TM = RM * 16;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int IB = B_BYTES / (1024 * NW);  // weight DMA instructions per wave per step
+  static_assert(IB >= 1 && IB * 1024 * NW == B_BYTES, "weight tile / wave mismatch");
+  constexpr int HB = HL * NW * 1024;          // halo buffer bytes
+  constexpr int HSLOTS = HB / 128;
+  constexpr bool B_MC = (MODE == DGRAD);
+  constexpr int E = RM * RN / 2;              // epilogue 16-B stores per lane
+  static_assert(RN % 2 == 0, "paired 16-B stores");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = blk / g.ncb, cb = blk - grp * g.ncb;
+  const int rb0 = grp * g.tpb;
+  const int ntile = min(g.tpb, g.nrb - rb0);
+  if (ntile <= 0) return;
+  const int n0 = cb * BN;
+  const int spt = g.nchunk * g.ntap;  // K-steps per tile
+  const int T = ntile * spt;
+
+  const rsrc_t rin = make_rsrc(MODE == FWD ? (const void*)a.x : (const void*)a.dy,
+                               MODE == FWD ? a.x_bytes : a.dy_bytes);
+  const rsrc_t rw = make_rsrc(a.w, a.w_bytes);
+  const rsrc_t rout = make_rsrc(a.out, a.out_bytes);
+  const uint32_t smem_lds = (uint32_t)(size_t)(lds_char_t*)smem;
+
+  // ---------------- load side: halo fill + weight DMA offsets of the load tile ----------------
+  uint32_t foff[HL];   // per fill instruction: byte offset of this lane's 16-B piece (chunk 0)
+  auto prep_fill = [&](const HTile& t) {
+    const int seg = g.Ho + g.ext_h;
+    const int rows0 = min(t.rows, g.Ho - t.h_first);
+    const int cnt0 = rows0 + g.ext_h;
+    const int rest = t.rows - rows0;
+    const int hr_total = cnt0 + rest + ((rest + g.Ho - 1) / g.Ho) * g.ext_h;
+#pragma unroll
+    for (int j = 0; j < HL; ++j) {
+      const int s = (j * NW + wid) * 8 + (lane >> 3);
+      const int hr = (int)fdiv((uint32_t)s, g.fd_HP);
+      const int hc = s - hr * g.HP;
+      int k, hi;
+      if (hr < cnt0) {
+        k = 0;
+        hi = t.h_first + g.oy_min + hr;
+      } else {
+        const int u = hr - cnt0;
+        const int kk = (int)fdiv((uint32_t)u, g.fd_seg);
+        k = 1 + kk;
+        hi = u - kk * seg + g.oy_min;
+      }
+      const int wi = g.ox_min + hc;
+      const bool v = hr < hr_total && hc < g.Wo + g.ext_w && (unsigned)hi < (unsigned)g.Hi &&
+                     (unsigned)wi < (unsigned)g.Wi;
+      const int lc = (lane & 7) ^ ((s >> 1) & 7);
+      const int n = t.n_first + k;
+      foff[j] = v ? (uint32_t)((((n * g.Hi + hi) * g.Wi + wi) * g.Ci + lc * 8) * 2) : HOOB;
+    }
+  };
+  uint32_t bsrc[IB];   // per weight DMA instruction: byte offset at tap 0, chunk 0
+  {
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      if constexpr (!B_MC) {
+        const int row = (j * NW + wid) * 8 + (lane >> 3);
+        const int co = n0 + row;
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        bsrc[j] = co < g.Co ? (uint32_t)((co * g.ldb + lc * 8) * 2) : HOOB;
+      } else {
+        // MC image [64 k-rows][BN cols]: k-row krow, 8-column piece col (swizzled as conv_glds)
+        const int krow = (j * NW + wid) * (512 / BN) + lane / (BN / 8);
+        const int q = lane % (BN / 8);
+        const int swz = mc_swz<BN>(krow);
+        const int col = (((q >> 1) ^ swz) << 4) + ((q & 1) << 3);
+        const int c = n0 + col;
+        bsrc[j] = c < g.Co ? (uint32_t)((krow * g.ldb + c) * 2) : HOOB;
+      }
+    }
+  }
+
+  // ---------------- cursors ----------------
+  // load cursor: next step to issue (tile li, chunk lch, tap ltp); halo parity counter
+  int sl = 0, li = 0, lch = 0, ltp = 0, lhalo = 0;
+  uint32_t hhist = 0;  // bit i: the i-th most recent issued step had a halo fill
+  HTile LT = htile(g, rb0);
+  prep_fill(LT);
+  auto issue = [&]() {
+    char* ring = smem + 2 * HB + (sl % ST) * B_BYTES;
+    bool fill = ltp == 0;
+    if (fill) {
+      char* hbuf = smem + (lhalo & 1) * HB;
+      const uint32_t cadd = (uint32_t)(lch * 64 * 2);
+#pragma unroll
+      for (int j = 0; j < HL; ++j) hdma16(rin, hbuf + (j * NW + wid) * 1024, foff[j] + cadd);
+      ++lhalo;
+    }
+    const uint32_t badd = B_MC ? (uint32_t)((lch * 64 * g.ldb + g.tap_b[ltp]) * 2)
+                               : (uint32_t)((g.tap_b[ltp] + lch * 64) * 2);
+#pragma unroll
+    for (int j = 0; j < IB; ++j) hdma16(rw, ring + (j * NW + wid) * 1024, bsrc[j] + badd);
+    hhist = (hhist << 1) | (fill ? 1u : 0u);
+    ++sl;
+    if (++ltp == g.ntap) {
+      ltp = 0;
+      if (++lch == g.nchunk) {
+        lch = 0;
+        if (++li < ntile) {
+          LT = htile(g, rb0 + li);
+          prep_fill(LT);
+        }
+      }
+    }
+  };
+
+  // read cursor (fragment reads run half a step ahead of the MFMAs): tile ri, chunk rch, tap rtp
+  int ri = 0, rch = 0, rtp = 0, rhalo = 0;
+  uint32_t slot0[RM];  // per fragment: this lane's halo slot at tap delta 0 (0 for no pixel)
+  auto prep_read = [&](int i) {
+    const HTile t = htile(g, rb0 + i);
+    const int rows0 = min(t.rows, g.Ho - t.h_first);
+    const int cnt0 = rows0 + g.ext_h;
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const int q = (wm * RM + rm) * 16 + (lane & 15);
+      const int r = (int)fdiv((uint32_t)q, g.fd_Wo);
+      const int w = q - r * g.Wo;
+      int hrow;
+      if (r < rows0) {
+        hrow = r;
+      } else {
+        const int u = r - rows0;
+        const int kk = (int)fdiv((uint32_t)u, g.fd_Ho);
+        hrow = cnt0 + kk * (g.Ho + g.ext_h) + (u - kk * g.Ho);
+      }
+      slot0[rm] = r < t.rows ? (uint32_t)(hrow * g.HP + w) : 0u;
+    }
+  };
+  prep_read(0);
+  const int lane_ch = lane >> 4;
+  auto load_frags = [&](int kk, bf16x8 (&af)[RM], bf16x8 (&bfg)[RN], int step_slot) {
+    const uint32_t hbase = smem_lds + (uint32_t)((rhalo & 1) * HB);
+    const uint32_t d = (uint32_t)g.tap_d[rtp];
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const uint32_t s = slot0[rm] + d;
+      const uint32_t x = ((s >> 1) & 7u) ^ (uint32_t)(kk * 4 + lane_ch);
+      af[rm] = hread(hbase + (s << 7) + (x << 4));
+    }
+    const uint32_t Bs = smem_lds + (uint32_t)(2 * HB + step_slot * B_BYTES);
+    if constexpr (!B_MC) {
+      hread_rows<RN>(bfg, Bs + (uint32_t)kc_off(wn * TN + (lane & 15), kk * 4 + lane_ch));
+    } else {
+      const int mck = 8 * (lane >> 4) + ((lane >> 2) & 3);
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) {
+        const uint32_t ad = Bs + (uint32_t)mc_off<BN>(mck, wn * TN + rn * 16 + 4 * (lane & 3));
+        bfg[rn] = kk == 0 ? hread_mc<BN, 0>(ad) : hread_mc<BN, 1>(ad);
+      }
+    }
+  };
+  auto advance_read = [&]() {
+    if (++rtp == g.ntap) {
+      rtp = 0;
+      ++rhalo;
+      if (++rch == g.nchunk) {
+        rch = 0;
+        if (++ri < ntile) prep_read(ri);
+      }
+    }
+  };
+
+  f32x4 acc[RM][RN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto mfmas = [&](const bf16x8 (&af)[RM], const bf16x8 (&bfg)[RN]) {
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+        acc[rm][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[rn], af[rm], acc[rm][rn], 0, 0, 0);
+  };
+
+  float s_sum[RN][4], s_sq[RN][4];
+#pragma unroll
+  for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
+
+  Tile Tep;  // the shared epilogue reads bn0 (mask slab column) only; rows come from rows_in
+  Tep.bm0 = 0;
+  Tep.bn0 = n0;
+  Tep.cls = 0;
+  Tep.Mc = 0;
+  Tep.Kgc = 0;
+  Tep.kt0 = Tep.kt1 = 0;
+  Tep.split = 0;
+  auto epilogue = [&](int i) {
+    const HTile t = htile(g, rb0 + i);
+    uint32_t rows_in[RM];
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const int q = (wm * RM + rm) * 16 + (lane & 15);
+      const int r = (int)fdiv((uint32_t)q, g.fd_Wo);
+      const int w = q - r * g.Wo;
+      rows_in[rm] = r < t.rows ? (uint32_t)(((t.rho0 + r) * g.Wo + w) * a.ldc) * 2u : ROW_OOB;
+    }
+    store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, false, false, NJ, false, true>(
+        a, Tep, acc, wm, wn, lane, rout, 1.f, false, s_sum, s_sq, rows_in);
+  };
+
+  // ---------------- pipeline ----------------
+  int sc = 0;          // step being computed
+  int ct = 0, ck = 0;  // its tile, step within the tile
+  uint32_t ehist = 0;  // bit i: the epilogue of the i-th previous step issued its stores
+  for (int s = 0; s < ST - 1 && sl < T; ++s) issue();
+  zero_acc();
+  bf16x8 f0a[RM], f0b[RN], f1a[RM], f1b[RN];
+  {
+    const int ahead = sl - 1;
+    wait_halo<IB, HL, E, ST>(ahead, min(1, __builtin_popcount(hhist & ((1u << ahead) - 1u))), 0);
+    hbarrier();
+  }
+  if (sl < T) issue();
+  load_frags(0, f0a, f0b, 0);
+  hlgkm0();
+  while (sc < T) {
+    load_frags(1, f1a, f1b, sc % ST);
+    mfmas(f0a, f0b);
+    hlgkm0();
+    advance_read();
+    const bool has_next = sc + 1 < T;
+    if (has_next) {
+      const int ahead = sl - 1 - (sc + 1);
+      const int nh = min(1, __builtin_popcount(hhist & ((1u << ahead) - 1u)));
+      const int ne = min(1, __builtin_popcount(ehist & ((1u << (ST - 1)) - 1u)));
+      wait_halo<IB, HL, E, ST>(ahead, nh, ne);
+      hbarrier();
+      if (sl < T) issue();
+      load_frags(0, f0a, f0b, (sc + 1) % ST);
+    }
+    mfmas(f1a, f1b);
+    ehist <<= 1;
+    if (++ck == spt) {
+      epilogue(ct);
+      ehist |= 1u;
+      zero_acc();
+      ck = 0;
+      ++ct;
+    }
+    if (has_next) hlgkm0();
+    ++sc;
+  }
+
+  // ---------------- BN statistics flush (one per workgroup: its tiles share the columns) -----
+  if constexpr (STATS) {
+#pragma unroll
+    for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s_sum[rn][i] += __shfl_xor(s_sum[rn][i], o, 64);
+          s_sq[rn][i] += __shfl_xor(s_sq[rn][i], o, 64);
+        }
+      }
+    float* red = (float*)(smem + 2 * HB + ST * B_BYTES);
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int nl = wn * TN + rn * 16 + (lane >> 4) * 4 + i;
+          red[(wm * 2 + 0) * BN + nl] = s_sum[rn][i];
+          red[(wm * 2 + 1) * BN + nl] = s_sq[rn][i];
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < 2 * BN; t += 64 * NW) {
+      const int which = t / BN, nl = t - which * BN;
+      const int n = n0 + nl;
+      if (n < g.Co) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) v += red[(w * 2 + which) * BN + nl];
+        atomicAdd(a.stats + which * g.Co + n, v);
+      }
+    }
+  }
+  (void)HSLOTS;
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+struct HCfg {
+  int bn, st, hl;
+};
+
+constexpr int halo_lds(int bn, int st, int hl) {
+  return 2 * hl * 8 * 1024 + st * bn * 128 + 2 * 4 * bn * 4;
+}
+
+int henv(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+template <int MODE, int BN, int ST, int HL, bool BIAS, bool STATS, bool NJ>
+void launch_h(const ConvArgs& a, const HaloGeom& g, int blocks, hipStream_t st) {
+  auto k = conv_halo_kernel<MODE, BN, 4, 2, 4, ST, HL, BIAS, STATS, NJ>;
+  constexpr int lds = halo_lds(BN, ST, HL);
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, st, a, g);
+}
+
+// worst-case halo rows of a tile of TR output rows (images of Ho rows, ext_h halo rows each)
+int halo_rows(int TR, int Ho, int ext_h) {
+  int segs;
+  if (Ho % TR == 0) segs = 1;
+  else if (TR % Ho == 0) segs = TR / Ho;
+  else segs = (TR - 1 + Ho - 1) / Ho + 1;
+  return TR + segs * ext_h;
+}
+
+// Fill the geometry for a direct conv with output Ho×Wo, taps (oy_t, ox_t) and weight offsets;
+// pick TR / BN / HL.  Returns false when no configuration fits.
+bool plan_halo(HaloGeom& g, int bn, HCfg& cfg) {
+  const int hl_max = bn == 128 ? 6 : 8;
+  const int st = bn == 128 ? 3 : (hl_max == 8 ? 3 : 4);
+  int best_tr = 0, best_hl = 0;
+  for (int TR = std::max(1, 256 / g.Wo); TR >= 1; --TR) {
+    if (TR * g.Wo > 256) continue;
+    const int hr = halo_rows(TR, g.Ho, g.ext_h);
+    const int slots = hr * g.HP;
+    const int hl = (slots + 63) / 64;
+    if (hl > hl_max) continue;
+    best_tr = TR;
+    best_hl = hl <= 6 ? 6 : 8;
+    break;
+  }
+  if (!best_tr) return false;
+  g.TR = best_tr;
+  cfg.bn = bn;
+  cfg.hl = best_hl;
+  cfg.st = bn == 128 ? 3 : (best_hl == 8 ? 3 : 4);
+  (void)st;
+  return true;
+}
+
+template <int MODE, bool BIAS, bool STATS, bool NJ>
+void launch_hcfg(const ConvArgs& a, const HaloGeom& g, const HCfg& c, int blocks, hipStream_t st) {
+  if (c.bn == 128) {
+    launch_h<MODE, 128, 3, 6, BIAS, STATS, NJ>(a, g, blocks, st);
+  } else if (c.hl == 8) {
+    launch_h<MODE, 64, 3, 8, BIAS, STATS, NJ>(a, g, blocks, st);
+  } else {
+    launch_h<MODE, 64, 4, 6, BIAS, STATS, NJ>(a, g, blocks, st);
+  }
+}
+
+bool halo_common(const ConvArgs& a, HaloGeom& g, int R, int S, const int* oy, const int* ox,
+                 int bn, HCfg& cfg, int& blocks) {
+  g.ntap = R * S;
+  g.nchunk = g.Ci / 64;
+  int oy_min = 1 << 30, oy_max = -(1 << 30), ox_min = 1 << 30, ox_max = -(1 << 30);
+  for (int t = 0; t < g.ntap; ++t) {
+    oy_min = std::min(oy_min, oy[t]);
+    oy_max = std::max(oy_max, oy[t]);
+    ox_min = std::min(ox_min, ox[t]);
+    ox_max = std::max(ox_max, ox[t]);
+  }
+  g.oy_min = oy_min;
+  g.ox_min = ox_min;
+  g.ext_h = oy_max - oy_min;
+  g.ext_w = ox_max - ox_min;
+  g.HP = g.Wo + g.ext_w;
+  for (int t = 0; t < g.ntap; ++t) g.tap_d[t] = (oy[t] - oy_min) * g.HP + (ox[t] - ox_min);
+  if (!plan_halo(g, bn, cfg)) return false;
+  g.nrb = cdiv((long)g.N * g.Ho, g.TR);
+  g.ncb = cdiv(g.Co, cfg.bn);
+  const int cus = henv("TDL_HALO_SLOTS", 256);
+  const long tiles = (long)g.nrb * g.ncb;
+  g.tpb = (int)std::max<long>(1, (tiles + cus - 1) / cus);
+  blocks = cdiv(g.nrb, g.tpb) * g.ncb;
+  g.fd_HP = make_fastdiv((uint32_t)g.HP);
+  g.fd_Wo = make_fastdiv((uint32_t)g.Wo);
+  g.fd_Ho = make_fastdiv((uint32_t)g.Ho);
+  g.fd_seg = make_fastdiv((uint32_t)(g.Ho + g.ext_h));
+  return true;
+}
+
+}  // namespace
+
+static int g_halo_override = -1;
+int conv_halo_mode() {
+  static int m = henv("TDL_HALO", 0);  // default off until validated on the GPU
+  return g_halo_override >= 0 ? g_halo_override : m;
+}
+void conv_set_halo_mode(int mode) { g_halo_override = mode; }
+
+// FWD, stride 1: true when the halo kernel ran
+bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
+  if (!conv_halo_mode()) return false;
+  if (a.sh != 1 || a.sw != 1 || a.res || a.fp8) return false;
+  const int ntap = a.R * a.S;
+  if (ntap < 3 || ntap > HALO_MAXTAP || a.C % 64 || a.K % 8 || a.ldc % 8) return false;
+  if (a.x_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
+  if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;  // small: GEMMs
+  HaloGeom g{};
+  g.N = a.N; g.Hi = a.H; g.Wi = a.W; g.Ci = a.C;
+  g.Ho = a.Ho; g.Wo = a.Wo; g.Co = a.K;
+  g.ldb = ntap * a.C;
+  int oy[HALO_MAXTAP], ox[HALO_MAXTAP];
+  for (int r = 0; r < a.R; ++r)
+    for (int s = 0; s < a.S; ++s) {
+      const int t = r * a.S + s;
+      oy[t] = r * a.dh - a.ph;
+      ox[t] = s * a.dw - a.pw;
+      g.tap_b[t] = t * a.C;
+    }
+  HCfg c;
+  int blocks;
+  const int bn = henv("TDL_HALO_BN", a.K >= 128 ? 128 : 64);
+  if (!halo_common(a, g, a.R, a.S, oy, ox, bn, c, blocks)) return false;
+  const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
+  if (bias) {
+    if (stats) launch_hcfg<FWD, true, true, true>(a, g, c, blocks, st);
+    else launch_hcfg<FWD, true, false, true>(a, g, c, blocks, st);
+  } else {
+    if (stats) launch_hcfg<FWD, false, true, true>(a, g, c, blocks, st);
+    else launch_hcfg<FWD, false, false, true>(a, g, c, blocks, st);
+  }
+  return true;
+}
+
+// DGRAD, stride 1 (one parity class): true when the halo kernel ran; *fused: a.stats filled
+bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused) {
+  if (fused) *fused = false;
+  if (!conv_halo_mode()) return false;
+  if (a.sh != 1 || a.sw != 1 || a.fp8 || a.dg_masked) return false;
+  const int ntap = a.R * a.S;
+  if (ntap < 3 || ntap > HALO_MAXTAP || a.K % 64 || a.C % 8 || a.ldc % 8) return false;
+  if (a.dy_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
+  if (conv_halo_mode() != 2 && (long)a.N * a.H * a.W < 4096) return false;
+  const bool stats = a.stats && a.bn_x;
+  if (a.mask && a.ldc % 64) return false;  // mask slabs: 64-column rows
+  HaloGeom g{};
+  g.N = a.N; g.Hi = a.Ho; g.Wi = a.Wo; g.Ci = a.K;
+  g.Ho = a.H; g.Wo = a.W; g.Co = a.C;
+  g.ldb = ntap * a.C;
+  int oy[HALO_MAXTAP], ox[HALO_MAXTAP];
+  for (int r = 0; r < a.R; ++r)
+    for (int s = 0; s < a.S; ++s) {
+      const int t = r * a.S + s;
+      oy[t] = a.ph - r * a.dh;
+      ox[t] = a.pw - s * a.dw;
+      g.tap_b[t] = t * a.C;
+    }
+  HCfg c;
+  int blocks;
+  // 128-wide dx tiles with both the join's previous-dx and the BN-statistics x registers spill:
+  // 64-wide there
+  const int bn = henv("TDL_HALO_BN", a.C >= 128 && !(stats && a.beta) ? 128 : 64);
+  if (!halo_common(a, g, a.R, a.S, oy, ox, bn, c, blocks)) return false;
+  ConvArgs b = a;
+  b.Ng = a.C;  // the shared epilogue's column count
+  if (!stats) b.stats = nullptr;
+  const bool nj = !a.beta;
+  if (stats) {
+    if (nj) launch_hcfg<DGRAD, false, true, true>(b, g, c, blocks, st);
+    else launch_hcfg<DGRAD, false, true, false>(b, g, c, blocks, st);
+  } else {
+    if (nj) launch_hcfg<DGRAD, false, false, true>(b, g, c, blocks, st);
+    else launch_hcfg<DGRAD, false, false, false>(b, g, c, blocks, st);
+  }
+  if (fused) *fused = stats;
+  return true;
+}
+
+}  // namespace tdl

@@ -75,6 +75,13 @@ struct ConvArgs {
 };
 constexpr int MAX_DG_CLASSES = 16;
 
+// deterministic mode (det.hip): fixed-order slab reductions instead of fp32 atomics
+int deterministic();
+void det_set(int on);  // -1: environment (TDL_DETERMINISTIC)
+float* det_slab(size_t floats, hipStream_t st);  // per-stream scratch, grows on demand
+void slab_sum_launch(const float* slab, float* out, int rows, long n, long row_stride,
+                     hipStream_t st);  // out[i] += Σ_r slab[r·row_stride + i], rows in order
+
 void conv_fwd_launch(const ConvArgs& a, hipStream_t st);
 // FWD with a.res: false (nothing launched) when the LDS-DMA kernel does not take the problem
 bool conv_fwd_res_launch(const ConvArgs& a, hipStream_t st);
@@ -97,6 +104,12 @@ void conv_set_glds_mode(int mode);  // -1: environment / default
 int conv_m32();
 void conv_set_m32(int on);
 bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
+// halo-tiled direct conv (conv_halo.hip) for stride-1 R×S filters, Cin % 64 == 0: true when it
+// ran (TDL_HALO=0 disables); the dgrad sets *fused when a.stats was filled
+int conv_halo_mode();
+void conv_set_halo_mode(int mode);  // -1: environment; 2: every eligible problem (tests)
+bool conv_fwd_halo(const ConvArgs& a, hipStream_t st);
+bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused);
 // *fused: set to whether a.stats was filled (stride-1 FASTK problems only)
 bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st, bool* fused = nullptr);
 bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);

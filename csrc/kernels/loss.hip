@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const void* __restric
                                                            const int64_t* __restrict__ labels,
                                                            float* __restrict__ loss,
                                                            void* __restrict__ grad, int N, int K,
-                                                           float eps) {
+                                                           float eps, float* __restrict__ slab) {
   __shared__ float sh[4];
   const int row = blockIdx.x;
   const long base = (long)row * K;
@@ -93,7 +93,10 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const void* __restric
     else
       ((float*)grad)[base + i] = g;
   }
-  if (threadIdx.x == 0) atomicAdd(loss, l * invN);
+  if (threadIdx.x == 0) {
+    if (slab) slab[row] = l * invN;  // deterministic mode: summed in row order (det.hip)
+    else atomicAdd(loss, l * invN);
+  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -106,7 +109,7 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_kernel(const void* __restri
                                                             const void* __restrict__ labels,
                                                             int lkind, float* __restrict__ loss,
                                                             float* __restrict__ grad, int B,
-                                                            int P) {
+                                                            int P, float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char lsm[];
   float* key = (float*)lsm;                        // LV_MAXP floats (errors, later scan values)
   uint16_t* idx = (uint16_t*)(key + LV_MAXP);      // LV_MAXP indices
@@ -121,7 +124,10 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_kernel(const void* __restri
     if (i < P) {
       const float lab = ld_label(labels, lkind, base + i);
       const float sgn = 2.f * (lab > 0.5f ? 1.f : 0.f) - 1.f;
-      key[i] = 1.f - ld(logits, bf, base + i) * sgn;
+      const float e = 1.f - ld(logits, bf, base + i) * sgn;
+      // a NaN error (diverged logits) sorts first as +inf: a NaN compares false both ways and
+      // would let the −inf padding entries (index ≥ P) move into the first P positions
+      key[i] = e == e ? e : INFINITY;
     } else {
       key[i] = -INFINITY;
     }
@@ -192,7 +198,7 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_kernel(const void* __restri
     prev_j = 1.f - (gts - cg) / (gts + cng);
   }
   for (int i = s0; i < s1; ++i) {
-    const int pix = idx[i];
+    const int pix = min((int)idx[i], P - 1);  // (never a padding index: see the key init)
     const float g = ld_label(labels, lkind, base + pix) > 0.5f ? 1.f : 0.f;
     cum_gt += g;
     const float cng = (float)(i + 1) - cum_gt;
@@ -206,7 +212,10 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_kernel(const void* __restri
   }
   float* red = part + LV_THREADS + 4 + LV_THREADS / 64;
   const float tot = block_sum<LV_THREADS>(loss_local, red);
-  if (tid == 0) atomicAdd(loss, tot / (float)B);
+  if (tid == 0) {
+    if (slab) slab[img] = tot / (float)B;
+    else atomicAdd(loss, tot / (float)B);
+  }
 }
 
 // ---- multi-pass Lovász hinge for P > LV_MAXP ------------------------------------------------
@@ -228,6 +237,7 @@ __global__ void __launch_bounds__(256) lovasz_init_kernel(const void* __restrict
     const float lab = ld_label(labels, lkind, img * P + i);
     const float sgn = lab > 0.5f ? 1.f : -1.f;
     k = 1.f - ld(logits, bf, img * P + i) * sgn;
+    if (k != k) k = INFINITY;  // NaN sorts first (see lovasz_kernel)
   }
   key[img * Pp + i] = k;
   idx[img * Pp + i] = i;
@@ -302,7 +312,8 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_scan_kernel(const void* __r
                                                                  const int* __restrict__ idx,
                                                                  float* __restrict__ loss,
                                                                  float* __restrict__ grad, int B,
-                                                                 int P, int Pp) {
+                                                                 int P, int Pp,
+                                                                 float* __restrict__ slab) {
   __shared__ float wtot[LV_THREADS / 64];
   __shared__ float red[LV_THREADS / 64 + 4];
   const long img = blockIdx.x;
@@ -321,7 +332,7 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_scan_kernel(const void* __r
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int i = i0 + j;
-      pix[j] = i < P ? idx[kbase + i] : 0;
+      pix[j] = i < P ? min(idx[kbase + i], P - 1) : 0;  // never a padding index
       g[j] = i < P && ld_label(labels, lkind, lbase + pix[j]) > 0.5f ? 1.f : 0.f;
       mine += g[j];
     }
@@ -358,7 +369,10 @@ __global__ void __launch_bounds__(LV_THREADS) lovasz_scan_kernel(const void* __r
     carry += all;
   }
   const float tot = block_sum<LV_THREADS>(loss_local, red);
-  if (tid == 0) atomicAdd(loss, tot / (float)B);
+  if (tid == 0) {
+    if (slab) slab[img] = tot / (float)B;
+    else atomicAdd(loss, tot / (float)B);
+  }
 }
 
 __global__ void __launch_bounds__(256) seg_metrics_kernel(const void* __restrict__ labels, int lkind,
@@ -399,8 +413,10 @@ __global__ void __launch_bounds__(256) seg_metrics_kernel(const void* __restrict
 
 void softmax_xent_launch(const void* logits, bool bf16, const int64_t* labels, float* loss,
                          void* grad, int N, int K, float smoothing, hipStream_t st) {
+  float* slab = deterministic() ? det_slab((size_t)N, st) : nullptr;
   hipLaunchKernelGGL(softmax_xent_kernel, dim3(N), dim3(256), 0, st, logits, bf16 ? 1 : 0, labels,
-                     loss, grad, N, K, smoothing);
+                     loss, grad, N, K, smoothing, slab);
+  if (slab) slab_sum_launch(slab, loss, N, 1, 1, st);
 }
 
 void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* labels, int label_kind,
@@ -412,8 +428,10 @@ void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* label
                         (int)lds);
     attr_set = true;
   }
+  float* slab = deterministic() ? det_slab((size_t)B, st) : nullptr;
   hipLaunchKernelGGL(lovasz_kernel, dim3(B), dim3(LV_THREADS), lds, st, logits,
-                     logits_bf16 ? 1 : 0, labels, label_kind, loss, grad, B, P);
+                     logits_bf16 ? 1 : 0, labels, label_kind, loss, grad, B, P, slab);
+  if (slab) slab_sum_launch(slab, loss, B, 1, 1, st);
 }
 
 int lovasz_padded_len(int P) {
@@ -445,8 +463,10 @@ void lovasz_hinge_large_launch(const void* logits, bool logits_bf16, const void*
     hipLaunchKernelGGL(lovasz_bitonic_local_kernel, lgrid, dim3(LV_THREADS), lds, st, key, idx, Pp,
                        size, size);
   }
+  float* slab = deterministic() ? det_slab((size_t)B, st) : nullptr;
   hipLaunchKernelGGL(lovasz_scan_kernel, dim3(B), dim3(LV_THREADS), 0, st, labels, label_kind, key,
-                     idx, loss, grad, B, P, Pp);
+                     idx, loss, grad, B, P, Pp, slab);
+  if (slab) slab_sum_launch(slab, loss, B, 1, 1, st);
 }
 
 void seg_metrics_launch(const void* labels, int label_kind, const float* pred, float* score,

@@ -304,10 +304,10 @@ static inline uint16_t f2bf(float f) {
 BatchLoader::BatchLoader(const std::vector<std::string>& images,
                          const std::vector<std::string>& masks, int batch, bool augment,
                          bool shuffle, bool repeat, uint64_t seed, int threads, int prefetch,
-                         int channels, int transformation, const AugConfig& aug)
+                         int channels, int transformation, const AugConfig& aug, bool fp32)
     : images_(images), masks_(masks), batch_(batch), augment_(augment), shuffle_(shuffle),
       repeat_(repeat), seed_(seed), channels_(channels), transformation_(transformation),
-      aug_(aug) {
+      aug_(aug), fp32_(fp32) {
   if (aug_.crop_probability < 0 || aug_.crop_probability > 1 || aug_.brightness_range < 0 ||
       aug_.crop_min_percent <= 0 || aug_.crop_max_percent < aug_.crop_min_percent)
     throw std::runtime_error("invalid augmentation parameters");
@@ -396,7 +396,12 @@ void BatchLoader::build(long b, Batch& out) {
   const auto idx = indices_for(b);
   const int HW = H_ * W_;
   out.index = b;
-  out.x.assign((size_t)batch_ * HW * channels_, 0);
+  if (fp32_) {
+    out.xf.assign((size_t)batch_ * HW * channels_, 0.f);
+    out.x.clear();
+  } else {
+    out.x.assign((size_t)batch_ * HW * channels_, 0);
+  }
   out.y.assign(masks_.empty() ? 0 : (size_t)batch_ * HW, 0.f);
   out.ids.assign(idx.begin(), idx.end());
   out.count = 0;
@@ -423,10 +428,18 @@ void BatchLoader::build(long b, Batch& out) {
       }
     }
     laplace(img.data(), H_, W_, lap.data());
-    uint16_t* xo = &out.x[(size_t)i * HW * channels_];
-    for (int k = 0; k < HW; ++k) {
-      xo[(size_t)k * channels_] = f2bf(img[k]);
-      xo[(size_t)k * channels_ + 1] = f2bf(lap[k]);
+    if (fp32_) {
+      float* xo = &out.xf[(size_t)i * HW * channels_];
+      for (int k = 0; k < HW; ++k) {
+        xo[(size_t)k * channels_] = img[k];
+        xo[(size_t)k * channels_ + 1] = lap[k];
+      }
+    } else {
+      uint16_t* xo = &out.x[(size_t)i * HW * channels_];
+      for (int k = 0; k < HW; ++k) {
+        xo[(size_t)k * channels_] = f2bf(img[k]);
+        xo[(size_t)k * channels_ + 1] = f2bf(lap[k]);
+      }
     }
     if (gm) std::copy(msk.begin(), msk.end(), out.y.begin() + (size_t)i * HW);
   }

@@ -55,7 +55,8 @@ void single_transformation(const float* in, int H, int W, int kind, float* out);
 struct Batch {
   long index = -1;
   int count = 0;                 // valid samples (last batch of a non-repeating epoch may be short)
-  std::vector<uint16_t> x;       // bf16 [B,H,W,C]
+  std::vector<uint16_t> x;       // bf16 [B,H,W,C] (fp32 loaders: empty)
+  std::vector<float> xf;         // fp32 [B,H,W,C] (fp32 loaders only)
   std::vector<float> y;          // fp32 [B,H,W] (empty without masks)
   std::vector<int64_t> ids;      // dataset indices (-1 = padding)
 };
@@ -64,13 +65,15 @@ class BatchLoader {
  public:
   BatchLoader(const std::vector<std::string>& images, const std::vector<std::string>& masks,
               int batch, bool augment, bool shuffle, bool repeat, uint64_t seed, int threads,
-              int prefetch, int channels, int transformation, const AugConfig& aug = AugConfig());
+              int prefetch, int channels, int transformation, const AugConfig& aug = AugConfig(),
+              bool fp32 = false);
   ~BatchLoader();
   bool next(Batch& out);
   int height() const { return H_; }
   int width() const { return W_; }
   int channels() const { return channels_; }
   int batch() const { return batch_; }
+  bool fp32() const { return fp32_; }
   long num_batches() const { return n_batches_; }
 
  private:
@@ -86,6 +89,7 @@ class BatchLoader {
   uint64_t seed_;
   int channels_, transformation_;
   AugConfig aug_;
+  bool fp32_ = false;  // emit the image batch in fp32 (the reference's precision) instead of bf16
   int H_ = 0, W_ = 0, prefetch_ = 2;
   long n_batches_ = -1;
   std::vector<GrayImage> cache_img_, cache_mask_;

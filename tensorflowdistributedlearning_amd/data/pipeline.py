@@ -7,6 +7,9 @@ decode/augment/batch work runs in native worker threads writing pinned host buff
 H2D copy is asynchronous on the current stream.  In data-parallel runs each rank reads a disjoint
 shard (images[rank::world]) with its own seed — the per-tower batches of MirroredStrategy.
 ``TestPipeline`` is ``Model._make_test_input`` (model.py:257-283) with a TTA transformation.
+Images arrive in bf16 (the GPU compute dtype) or, with ``fp32=True``, in fp32 — normalisation,
+augmentation and the Laplacian run in fp32 either way (``Model(precision="fp32")`` uses it, so the
+reference-precision runs see unrounded inputs).
 """
 from __future__ import annotations
 
@@ -37,7 +40,8 @@ class SegmentationPipeline:
     height_shift_range, width_shift_range, brightness_range); default :data:`TRAIN_AUG`."""
 
     def __init__(self, images, masks, batch_size, augment, shuffle, repeat=True, seed=0,
-                 device="cpu", rank=0, world=1, threads=4, prefetch=4, channels=8, aug=None):
+                 device="cpu", rank=0, world=1, threads=4, prefetch=4, channels=8, aug=None,
+                 fp32=False):
         if world > 1:
             images = images[rank::world]
             masks = masks[rank::world] if masks else masks
@@ -50,7 +54,7 @@ class SegmentationPipeline:
         self._loader = _native.load().BatchLoader(
             list(images), list(masks or []), int(batch_size), bool(augment), bool(shuffle),
             bool(repeat), int(seed) * 1000 + rank, int(threads), int(prefetch), int(channels), 0,
-            self.device.type == "cuda", dict(TRAIN_AUG if aug is None else aug))
+            self.device.type == "cuda", dict(TRAIN_AUG if aug is None else aug), bool(fp32))
 
     def __iter__(self):
         return self
@@ -80,12 +84,12 @@ class TestPipeline:
     __test__ = False  # not a pytest class
 
     def __init__(self, images, batch_size, transformation="none", device="cpu", threads=4,
-                 prefetch=4, channels=8):
+                 prefetch=4, channels=8, fp32=False):
         self.device = torch.device(device)
         self.ids = [os.path.splitext(os.path.basename(p))[0] for p in images]
         self._loader = _native.load().BatchLoader(
             list(images), [], int(batch_size), False, False, False, 0, int(threads), int(prefetch),
-            int(channels), TRANSFORMS[transformation], self.device.type == "cuda")
+            int(channels), TRANSFORMS[transformation], self.device.type == "cuda", {}, bool(fp32))
 
     def __iter__(self):
         return self

@@ -10,7 +10,9 @@ Layout per fold directory (``model_dir/fold{i}``):
 Contents: every parameter and buffer (BN moving statistics), ``global_step``, optimizer slots
 (``<var>/Adam``, ``<var>/Adam_1`` or ``<var>/Momentum``), ``beta1_power`` / ``beta2_power`` for
 Adam — the TF1 variable set [TF-internal naming].  Saving copies the flat buffers to host once
-(device → host of one contiguous buffer per state tensor) and writes on rank 0 only.
+(device → host of one contiguous buffer per state tensor) and writes on rank 0 only;
+:class:`AsyncSaver` does the copies on a copy stream into pinned buffers and the file write on a
+worker thread, so the training loop never waits for the host.
 Resume: :func:`latest_checkpoint` + :func:`restore` reproduce TF's "continue from the latest
 checkpoint of the fold" behaviour; ``keep_max`` (default 5) old checkpoints are retained.
 """
@@ -34,29 +36,112 @@ def _names(model):
     return {k: m.get(k, k) for k in sd}
 
 
-def save(directory, step, model, optimizer=None, keep_max=5, extra_meta=None):
-    os.makedirs(directory, exist_ok=True)
+def _collect(model, optimizer, step, to_host):
+    """(tensors, slot plan, optimizer kind): every variable copied to the host by ``to_host``
+    (synchronous, or into pinned buffers on a copy stream); the optimizer slots as whole flat
+    buffers, split per variable by :func:`_finish` once the copies have landed."""
     names = _names(model)
     tensors = {}
     for k, v in model.state_dict().items():
-        tensors[names[k]] = v.detach().to("cpu", copy=True).contiguous()
+        tensors[names[k]] = to_host("v/" + k, v.detach())
     tensors["global_step"] = torch.tensor([step], dtype=torch.int64)
-    opt_kind = None
+    opt_kind, plan = None, None
     if optimizer is not None:
         opt_kind = type(optimizer).__name__
         flat = optimizer.flat
-        slots = optimizer.state_tensors()
-        host_slots = {s: t.detach().to("cpu") for s, t in slots.items()}
+        host_slots = {s: to_host("s/" + s, t.detach()) for s, t in optimizer.state_tensors().items()}
         pname = {id(p): n for n, p in model.named_parameters()}
-        for p in flat.params:
-            o, e = flat.slice_of(p)
-            base = names.get(pname[id(p)], pname[id(p)])
-            for sname, st in host_slots.items():
-                tensors[f"{base}/{sname}"] = st[o:e].reshape(p.shape).clone()
+        plan = (host_slots, [(names.get(pname[id(p)], pname[id(p)]), flat.slice_of(p), p.shape)
+                             for p in flat.params])
         if hasattr(optimizer, "beta1"):
             t = optimizer.step_count
             tensors["beta1_power"] = torch.tensor([optimizer.beta1 ** (t + 1)], dtype=torch.float32)
             tensors["beta2_power"] = torch.tensor([optimizer.beta2 ** (t + 1)], dtype=torch.float32)
+    return names, tensors, plan, opt_kind
+
+
+def _finish(tensors, plan):
+    if plan is not None:
+        host_slots, vars_ = plan
+        for base, (o, e), shape in vars_:
+            for sname, st in host_slots.items():
+                tensors[f"{base}/{sname}"] = st[o:e].reshape(shape).clone()
+    return {k: v.contiguous() for k, v in tensors.items()}
+
+
+def save(directory, step, model, optimizer=None, keep_max=5, extra_meta=None):
+    os.makedirs(directory, exist_ok=True)
+    names, tensors, plan, opt_kind = _collect(
+        model, optimizer, step, lambda key, t: t.to("cpu", copy=True))
+    return _write(directory, step, names, _finish(tensors, plan), opt_kind, keep_max, extra_meta)
+
+
+class AsyncSaver:
+    """Checkpoint writes off the training thread (SURVEY §5.4 "rank 0 writes after async D2H").
+
+    ``save`` copies every device tensor into pinned host buffers (reused across saves) on a
+    dedicated copy stream ordered after the work queued so far, makes the caller's stream wait
+    for those copies only (the next optimizer step cannot overwrite a variable before it is
+    copied; the host never blocks), and returns; a worker thread waits for the copies, then
+    writes the safetensors file and moves the ``checkpoint`` pointer.  At most one save is in
+    flight (a second waits for the first); :meth:`wait` joins — called before anything reads
+    the directory (fold end, restore)."""
+
+    def __init__(self):
+        self._thread = None
+        self._error = None
+        self._pinned = {}
+        self._stream = None
+
+    def _to_host(self, key, t):
+        if not t.is_cuda:
+            return t.to("cpu", copy=True)
+        buf = self._pinned.get(key)
+        if buf is None or buf.shape != t.shape or buf.dtype != t.dtype:
+            buf = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            self._pinned[key] = buf
+        with torch.cuda.stream(self._stream):
+            buf.copy_(t, non_blocking=True)
+        return buf
+
+    def save(self, directory, step, model, optimizer=None, keep_max=5, extra_meta=None):
+        self.wait()
+        os.makedirs(directory, exist_ok=True)
+        dev = next((p.device for p in model.parameters() if p.is_cuda), None)
+        if dev is None:  # host model: nothing to overlap
+            return save(directory, step, model, optimizer, keep_max, extra_meta)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev)
+        self._stream.wait_stream(cur)
+        names, tensors, plan, opt_kind = _collect(model, optimizer, step, self._to_host)
+        done = torch.cuda.Event()
+        done.record(self._stream)
+        cur.wait_event(done)  # the device waits for the copies, the host does not
+
+        def work():
+            try:
+                done.synchronize()
+                _write(directory, step, names, _finish(tensors, plan), opt_kind, keep_max,
+                       extra_meta)
+            except BaseException as e:  # surfaced by wait()
+                self._error = e
+
+        import threading
+        self._thread = threading.Thread(target=work, name="tdl-ckpt", daemon=True)
+        self._thread.start()
+        return os.path.join(directory, f"model.ckpt-{step}.safetensors")
+
+    def wait(self):
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise e
+
+
+def _write(directory, step, names, tensors, opt_kind, keep_max, extra_meta):
     prefix = f"model.ckpt-{step}"
     path = os.path.join(directory, prefix + ".safetensors")
     tmp = path + ".tmp"

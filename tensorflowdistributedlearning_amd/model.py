@@ -202,7 +202,8 @@ class Model:
                              weight_decay=self.weight_decay)
 
     def _cast(self, x):
-        """The network input in the compute precision (the loaders deliver bf16 images)."""
+        """The network input in the compute precision (the loaders deliver bf16 images, or fp32
+        ones for precision="fp32" — then this is a no-op)."""
         return x.float() if self.precision == "fp32" and x.dtype != torch.float32 else x
 
     def _world(self):
@@ -319,7 +320,8 @@ class Model:
         pipe = SegmentationPipeline(tr_imgs, tr_masks, batch, augment=True, shuffle=True,
                                     repeat=True, seed=self.seed + 7919 * fold + start,
                                     device=device, rank=ctx.rank, world=ctx.world_size,
-                                    threads=self.loader_threads, aug=self.augmentation)
+                                    threads=self.loader_threads, aug=self.augmentation,
+                                    fp32=self.precision == "fp32")
         main = ctx.is_main
         tw = SummaryWriter(os.path.join(fold_dir, "train"), enabled=main)
         ew = SummaryWriter(os.path.join(fold_dir, "eval"), enabled=main)
@@ -333,6 +335,7 @@ class Model:
                 serving_shape=[None, self.input_shape[0], self.input_shape[1], 2],
                 model_config=self.config())
         iou_m, acc_m = StreamingMean(device), StreamingMean(device)
+        saver = ckpt.AsyncSaver()  # D2H on a copy stream, file write on a worker thread
         eval_result = {}
         step = start
         t0 = time.time()
@@ -355,8 +358,8 @@ class Model:
                 _image_summaries(tw, "train", x, yy, out, self.threshold, step)
             if step % self.save_checkpoints_steps == 0 or step == steps:
                 if main:
-                    ckpt.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
-                              {"config": self.config()})
+                    saver.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
+                               {"config": self.config()})
                 eval_result = self._evaluate(net, ev_imgs, ev_masks, batch * 2, device, ctx,
                                              ew if main else None, step)
                 eval_result["global_step"] = step
@@ -367,6 +370,7 @@ class Model:
         if step == start and start > 0:  # already trained: evaluate the restored model
             eval_result = self._evaluate(net, ev_imgs, ev_masks, batch * 2, device, ctx)
             eval_result["global_step"] = step
+        saver.wait()
         tw.close()
         ew.close()
         res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step}
@@ -443,6 +447,7 @@ class Model:
                 serving_shape=[None, self.image_size, self.image_size, self.image_channels],
                 model_config=self.config())
         correct = StreamingMean(device)
+        saver = ckpt.AsyncSaver()  # D2H on a copy stream, file write on a worker thread
         eval_result, history = {}, []
         step = start
         t0 = time.time()
@@ -461,8 +466,8 @@ class Model:
                            step)
             if step % self.save_checkpoints_steps == 0 or step == steps:
                 if main:
-                    ckpt.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
-                              {"config": self.config()})
+                    saver.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
+                               {"config": self.config()})
                 eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
                 eval_result["global_step"] = step
                 if main:
@@ -472,6 +477,7 @@ class Model:
         if step == start and start > 0:
             eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
             eval_result["global_step"] = step
+        saver.wait()
         tw.close()
         ew.close()
         res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step,
@@ -532,7 +538,7 @@ class Model:
             net = self.build_network().to(device)
             ckpt.restore(path, net)
             if device.type == "cuda" and self.precision != "fp32":
-                FlatParams(net, device, lowp_dtype=torch.bfloat16)
+                net._tdl_flat = FlatParams(net, device, lowp_dtype=torch.bfloat16, with_grad=False)
             net.eval()
             labels = np.zeros(len(ids), dtype=np.int64)  # unused by the image sources
             probs = [torch.softmax(net(x).float(), -1).cpu() for x, _ in ClassificationPipeline(
@@ -551,7 +557,8 @@ class Model:
         net.eval()
         pipe = SegmentationPipeline(images, masks, batch, augment=False, shuffle=False,
                                     repeat=False, device=device, rank=ctx.rank,
-                                    world=ctx.world_size, threads=self.loader_threads)
+                                    world=ctx.world_size, threads=self.loader_threads,
+                                    fp32=self.precision == "fp32")
         sums = torch.zeros(4, dtype=torch.float64, device=device)  # iou, acc, loss, count
         first = True
         for x, yy in pipe:
@@ -596,14 +603,16 @@ class Model:
             net = self.build_network().to(device)
             ckpt.restore(path, net)
             if device.type == "cuda" and self.precision != "fp32":
-                # bf16 compute copies of the weights once per fold (not per batch); in eval mode
-                # under no_grad every conv+BN runs BN-folded (models/layers.ConvBN)
-                FlatParams(net, device, lowp_dtype=torch.bfloat16)
+                # bf16 compute copies of the weights once per fold (not per batch; no gradient
+                # buffer), kept with the network; in eval mode under no_grad every conv+BN runs
+                # BN-folded (models/layers.ConvBN)
+                net._tdl_flat = FlatParams(net, device, lowp_dtype=torch.bfloat16, with_grad=False)
             net.eval()
             for tf in transforms:
                 probs, fold_ids = [], []
                 for x, b_ids in TestPipeline(images, batch_size, tf, device=device,
-                                             threads=self.loader_threads):
+                                             threads=self.loader_threads,
+                                             fp32=self.precision == "fp32"):
                     p = torch.sigmoid(net(self._cast(x)).float())
                     probs.append(_undo_transform(p, tf)[..., 0].cpu())
                     fold_ids += b_ids
@@ -652,7 +661,8 @@ class Model:
             return SegmentationPipeline(imgs, masks, batch_size, augment=augment, shuffle=shuffle,
                                         repeat=(mode == TRAIN), seed=self.seed + fold,
                                         device=device, rank=rank, world=world,
-                                        threads=self.loader_threads, aug=self.augmentation)
+                                        threads=self.loader_threads, aug=self.augmentation,
+                                    fp32=self.precision == "fp32")
         return input_fn
 
     def _make_test_input(self, batch_size, test_directory, tti="none", device="cpu"):
@@ -665,7 +675,7 @@ class Model:
         def test_input_fn():
             images = sorted(glob.glob(os.path.join(test_directory, "*.png")))
             return TestPipeline(images, batch_size, transformation, device=device,
-                                threads=self.loader_threads)
+                                threads=self.loader_threads, fp32=self.precision == "fp32")
         return test_input_fn
 
     @property

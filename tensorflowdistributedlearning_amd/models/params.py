@@ -44,7 +44,9 @@ class FlatParams:
     """
 
     def __init__(self, module: torch.nn.Module, device, lowp_dtype=torch.bfloat16,
-                 no_decay=None):
+                 no_decay=None, with_grad=True):
+        """``with_grad=False`` (inference: ``Model.predict``): no gradient buffer — parameters get
+        their fp32 master views and bf16 compute views only."""
         self.device = torch.device(device)
         self.params = []
         self.names = []
@@ -62,7 +64,8 @@ class FlatParams:
             off += _align(p.numel())
         self.total = max(off, ALIGN)
         self.master = torch.zeros(self.total, dtype=torch.float32, device=self.device)
-        self.grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.grad = (torch.zeros(self.total, dtype=torch.float32, device=self.device)
+                     if with_grad else None)
         self.lowp = (torch.zeros(self.total, dtype=lowp_dtype, device=self.device)
                      if lowp_dtype is not None else None)
         flags = torch.ones(self.total // ALIGN, dtype=torch.uint8)
@@ -77,7 +80,7 @@ class FlatParams:
         for p, o in zip(self.params, self.offsets):
             n = p.numel()
             p.data = self.master[o:o + n].view(p.shape)
-            p.grad = self.grad[o:o + n].view(p.shape)
+            p.grad = self.grad[o:o + n].view(p.shape) if self.grad is not None else None
             p._lowp = self.lowp[o:o + n].view(p.shape) if self.lowp is not None else None
             p._flat_offset = o
             p._flat_lowp = self.lowp

@@ -55,16 +55,80 @@ CONV_SHAPES = [
     (2, 16, 16, 200, 328, 1, 1, 2, (0, 0, 0, 0), 1),    # 1x1 s2, ragged FASTK dgrad class
 ]
 
-CONV_IMPLS = ["reg", "glds"]
+CONV_IMPLS = ["reg", "glds", "halo"]
 
 
 @pytest.fixture(params=CONV_IMPLS)
 def conv_impl(request, gpu):
-    """Run a conv test with the register-staged kernels (0) or the LDS-DMA kernels forced for
-    every aligned problem (2)."""
-    ext().conv_set_glds_mode(0 if request.param == "reg" else 2)
+    """Run a conv test with the register-staged kernels (0), the LDS-DMA kernels forced for
+    every aligned problem (2), or the halo-tiled direct conv for every stride-1 problem it takes
+    (conv_halo.hip; the others fall back to the default selection)."""
+    ext().conv_set_glds_mode(0 if request.param == "reg" else 2 if request.param == "glds" else -1)
+    ext().conv_set_halo_mode(2 if request.param == "halo" else 0)
     yield request.param
     ext().conv_set_glds_mode(-1)
+    ext().conv_set_halo_mode(-1)
+
+
+# (N, H, W, Cin, Cout, k, dil): halo tiles of one image, of several images (rows spanning image
+# boundaries), dilation, multi-chunk Cin, ragged output-channel tiles, 64- and 128-wide tiles
+HALO_SHAPES = [
+    (4, 56, 56, 64, 64, 3, 1),      # ResNet layer1: 4-row tiles inside one image
+    (6, 28, 28, 128, 128, 3, 1),    # 8-row tiles straddling images
+    (8, 14, 14, 256, 256, 3, 1),    # 18-row tiles over up to 3 images
+    (8, 7, 7, 512, 512, 3, 1),      # 28-row tiles = 4 images
+    (4, 13, 13, 512, 256, 3, 2),    # DeepLab block3 dilation 2
+    (3, 13, 13, 64, 32, 3, 4),      # dilation 4, Cout 32 (ragged 64-wide tile)
+    (5, 17, 23, 192, 200, 3, 1),    # odd sizes, ragged Cout
+    (2, 51, 51, 64, 128, 3, 1),     # DeepLab stem width 51
+    (2, 20, 20, 128, 64, 5, 1),     # 5x5 filter
+]
+
+
+@pytest.mark.parametrize("shape", HALO_SHAPES)
+def test_conv_halo_fwd_dgrad(gpu, shape):
+    """Halo-tiled direct conv vs the fp32 oracle: forward with fused BN statistics, input
+    gradient plain / accumulated (residual join) / ReLU-masked with BN-backward statistics."""
+    from tensorflowdistributedlearning_amd.ops import bn as BN
+    N, H, W, Cin, K, k, dil = shape
+    p = dil * (k - 1) // 2
+    g = C.ConvGeom((1, 1), (p, p, p, p), (dil, dil))
+    torch.manual_seed(31)
+    x = (torch.randn(N, H, W, Cin) * 1.3 + 0.2).bfloat16()
+    w = (torch.randn(K, k, k, Cin) / math.sqrt(k * k * Cin)).bfloat16()
+    ext().conv_set_halo_mode(2)
+    try:
+        ref = C.ref_conv_fwd(x.float(), w.float(), g)
+        stats = torch.zeros(2, K, device=gpu)
+        y = C.conv_fwd(x.to(gpu), w.to(gpu), g, stats=stats)
+        assert rel_err(y, ref) < 2e-2
+        yb = y.float().cpu().reshape(-1, K)
+        assert rel_err(stats[0], yb.sum(0)) < 1e-3
+        assert rel_err(stats[1], (yb * yb).sum(0)) < 1e-3
+        dy = torch.randn(ref.shape).bfloat16()
+        dx_ref = C.ref_conv_dgrad(dy.float(), w.float(), x.shape, g)
+        dx = C.conv_dgrad(dy.to(gpu), w.to(gpu), x.shape, g)
+        assert rel_err(dx, dx_ref) < 2e-2
+        prev = torch.randn(N, H, W, Cin).bfloat16()
+        out = prev.to(gpu)
+        C.conv_dgrad(dy.to(gpu), w.to(gpu), x.shape, g, out=out, accumulate=True)
+        assert rel_err(out, dx_ref + prev.float()) < 2e-2
+        # masked dgrad with BN-backward statistics (the 3x3 conv2 of a bottleneck)
+        xg = x.to(gpu)
+        gam, bet = torch.rand(Cin, device=gpu) + 0.5, torch.randn(Cin, device=gpu) * 0.3
+        coef = BN.bn_finalize(BN.bn_stats(xg), N * H * W, gam, bet, torch.zeros(Cin, device=gpu),
+                              torch.ones(Cin, device=gpu), 0.9, 1e-3, True)
+        mask = torch.empty(xg.numel() // 8, device=gpu, dtype=torch.uint8)
+        BN.bn_apply(xg, coef, None, True, mask=mask)
+        keep = BN.unpack_relu_mask(mask.cpu(), Cin).reshape(x.shape)
+        dxm, red = C.conv_dgrad_bnstat(dy.to(gpu), w.to(gpu), x.shape, g, xg, mask=mask)
+        assert rel_err(dxm, dx_ref * keep) < 2e-2
+        assert (dxm.float().cpu()[~keep] == 0).all()
+        assert red is not None
+        gf, xf = dxm.float().reshape(-1, Cin), xg.float().reshape(-1, Cin)
+        assert rel_err(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-4
+    finally:
+        ext().conv_set_halo_mode(-1)
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)
@@ -239,6 +303,24 @@ def test_lovasz(gpu, P_):
     assert abs(loss.item() - l_ref.item()) < 1e-4 * max(1.0, abs(l_ref.item()))
     loss.backward()
     assert rel_err(lg.grad, g_ref) < 1e-3
+
+
+@pytest.mark.parametrize("P_", [101 * 101, 200 * 200])
+def test_lovasz_nan_logit_stays_in_bounds(gpu, P_):
+    """A NaN logit (diverged training) must give a non-finite loss, not an out-of-bounds
+    gradient store: NaN errors sort first, padding entries never reach the first P positions.
+    The other images' gradients are unaffected."""
+    torch.manual_seed(10)
+    logits = torch.randn(3, P_)
+    labels = (torch.rand(3, P_) > 0.5).float()
+    logits[2, 17] = float("nan")  # the last image: a stray padding index would write past grad
+    lg = logits.to(gpu).requires_grad_(True)
+    loss = L.lovasz_hinge(lg, labels.to(gpu))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert not math.isfinite(loss.item())
+    _, g_ref = L.ref_lovasz_hinge(logits[:2], labels[:2])
+    assert rel_err(lg.grad[:2] * 3 / 2, g_ref) < 1e-3  # (per-image mean over 3 vs 2 images)
 
 
 @pytest.mark.parametrize("P_", [5000, 200 * 200])

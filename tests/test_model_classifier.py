@@ -183,3 +183,25 @@ def test_model_graph_training_tracks_eager(tmp_path, gpu):
     rb = Model(str(tmp_path / "g"), "", **kw).train(192, None, 16, 10)[0]
     assert rb["hip_graph"] and not ra["hip_graph"]
     np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.05, atol=0.02)
+
+
+@pytest.mark.gpu
+def test_async_saver_snapshots_before_later_updates(tmp_path, gpu):
+    """AsyncSaver: the file holds the values at save time although the caller's stream updates
+    the variables right after save() returns (the stream waits for the pinned copies, the host
+    does not); the pointer file names the new checkpoint once wait() returns."""
+    from safetensors.torch import load_file
+    torch.manual_seed(3)
+    m = torch.nn.Linear(2048, 2048).to(gpu)
+    before = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    saver = ckpt.AsyncSaver()
+    path = saver.save(str(tmp_path), 7, m)
+    with torch.no_grad():
+        for _ in range(20):  # queued behind the copies on the same stream
+            m.weight.add_(1.0)
+    saver.wait()
+    got = load_file(path)
+    for k, v in before.items():
+        assert torch.equal(got[k], v)
+    assert ckpt.latest_checkpoint(str(tmp_path)) == path
+    assert float(m.weight[0, 0].cpu()) == float(before["weight"][0, 0]) + 20.0

@@ -966,3 +966,40 @@ def test_xception_depthwise_join_matches_autograd_sum(gpu):
             XceptionModule.grad_join = True
     cos = torch.nn.functional.cosine_similarity(grads[0], grads[1], dim=0).item()
     assert cos > 0.9999, cos
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "deeplab"])
+def test_deterministic_mode_bitwise_repeatable(gpu, arch):
+    """TDL_DETERMINISTIC (csrc/kernels/det.hip): two runs of the same training steps
+    from the same initial state are bit-identical — losses and every master weight — with batch
+    statistics, the side-stream weight gradients and every fused path that has a deterministic
+    form (BN statistics and backward sums reduced in slab order, per-row loss terms summed in
+    order)."""
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    torch.manual_seed(11)
+    if arch == "resnet18":
+        make = lambda: models.resnet18(num_classes=10)  # noqa: E731
+        lossf, opt, okw = softmax_cross_entropy, "sgd", dict(lr=0.05, momentum=0.9)
+        x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
+    else:
+        make = lambda: models.DeepLabResNet(model_name="m", input_shape=(101, 101))  # noqa: E731
+        lossf, opt, okw = lovasz_hinge, "adam", dict(lr=1e-3)
+        x, y = segmentation_batch(4, device=gpu)
+    init = make().state_dict()
+    ext().det_set(1)
+    try:
+        runs = []
+        for _ in range(2):
+            m = make()
+            m.load_state_dict(init)
+            tr = Trainer(m, lossf, gpu, opt, okw)
+            losses = [tr.train_step(x, y)[0].clone() for _ in range(4)]
+            torch.cuda.synchronize()
+            runs.append((torch.stack(losses).cpu(), tr.flat.master.clone().cpu(),
+                         torch.cat([b.float().flatten().cpu() for b in m.buffers()])))
+    finally:
+        ext().det_set(-1)
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2])
+    assert torch.isfinite(runs[0][1]).all() and len(set(runs[0][0].tolist())) > 1
