@@ -79,6 +79,11 @@ def main():
             def dgrad():
                 C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask)
 
+            dwb = torch.empty(K, 3, 3, Cin, device=dev)
+
+            def wgrad():
+                C.conv_wgrad(dy, x, tuple(w.shape), g, out=dwb)
+
             res = {}
             outs = {}
             for mode in (0, 2):  # correctness cross-check of the two paths first
@@ -86,22 +91,25 @@ def main():
                 stats.zero_()
                 y = C.conv_fwd(x, w, g, stats=stats)
                 dx, _ = C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask)
-                outs[mode] = (y.float(), dx.float())
+                dwv = C.conv_wgrad(dy, x, tuple(w.shape), g)
+                outs[mode] = (y.float(), dx.float(), dwv.float())
             ey = ((outs[0][0] - outs[2][0]).abs().max() / outs[0][0].abs().max()).item()
             ed = ((outs[0][1] - outs[2][1]).abs().max() / outs[0][1].abs().max()).item()
+            ew = ((outs[0][2] - outs[2][2]).abs().max() / outs[0][2].abs().max()).item()
             for r in range(args.rounds):
                 for mode in (0, 2):
                     ext().conv_set_halo_mode(mode)
-                    fwd(); dgrad()
+                    fwd(); dgrad(); wgrad()
                     torch.cuda.synchronize()
                     res.setdefault((mode, "fwd"), []).append(timeit(fwd, args.iters))
                     res.setdefault((mode, "dgrad"), []).append(timeit(dgrad, args.iters))
+                    res.setdefault((mode, "wgrad"), []).append(timeit(wgrad, args.iters))
             ext().conv_set_halo_mode(-1)
             fl = 2.0 * N * H * W * K * Cin * 9
             row = {"net": net, "shape": name, "batch": N, "count": cnt, "rel_diff_fwd": ey,
-                   "rel_diff_dgrad": ed}
+                   "rel_diff_dgrad": ed, "rel_diff_wgrad": ew}
             for mode, tag in ((0, "gemm"), (2, "halo")):
-                for p in ("fwd", "dgrad"):
+                for p in ("fwd", "dgrad", "wgrad"):
                     t = sorted(res[(mode, p)])[len(res[(mode, p)]) // 2]
                     row[f"{tag}_{p}_us"] = round(t, 1)
                     row[f"{tag}_{p}_tf"] = round(fl / t / 1e6, 1)
@@ -109,13 +117,16 @@ def main():
             print(f"{net:9s} {name:24s} N={N:5d}  fwd {row['gemm_fwd_us']:8.1f} -> "
                   f"{row['halo_fwd_us']:8.1f} us ({row['halo_fwd_tf']:6.1f} TF)   dgrad "
                   f"{row['gemm_dgrad_us']:8.1f} -> {row['halo_dgrad_us']:8.1f} us "
-                  f"({row['halo_dgrad_tf']:6.1f} TF)  x{cnt}  diff {ey:.1e}/{ed:.1e}", flush=True)
-            del x, w, dy, mask
+                  f"({row['halo_dgrad_tf']:6.1f} TF)   wgrad {row['gemm_wgrad_us']:8.1f} -> "
+                  f"{row['halo_wgrad_us']:8.1f} us ({row['halo_wgrad_tf']:6.1f} TF)  x{cnt}  "
+                  f"diff {ey:.1e}/{ed:.1e}/{ew:.1e}", flush=True)
+            del x, w, dy, mask, dwb
             torch.cuda.empty_cache()
     for net in SHAPES:
-        a = sum((r["gemm_fwd_us"] + r["gemm_dgrad_us"]) * r["count"] for r in rows if r["net"] == net)
-        b = sum((r["halo_fwd_us"] + r["halo_dgrad_us"]) * r["count"] for r in rows if r["net"] == net)
-        print(f"{net}: stride-1 3x3 fwd+dgrad per step {a / 1e3:.2f} ms -> {b / 1e3:.2f} ms")
+        for p in ("fwd", "dgrad", "wgrad"):
+            a = sum(r[f"gemm_{p}_us"] * r["count"] for r in rows if r["net"] == net)
+            b = sum(r[f"halo_{p}_us"] * r["count"] for r in rows if r["net"] == net)
+            print(f"{net}: stride-1 3x3 {p} per step {a / 1e3:.2f} ms -> {b / 1e3:.2f} ms")
     if args.out:
         with open(args.out, "w") as f:
             json.dump(rows, f, indent=1)

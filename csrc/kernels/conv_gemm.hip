@@ -886,6 +886,7 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
 }
 
 void conv_wgrad_plan(const ConvArgs& a, WgradPlan* p) {
+  if (conv_wgrad_halo_plan(a, p)) return;
   if (conv_wgrad_glds_plan(a, p)) return;
   p->impl = 0;
   p->cfg = 0;
@@ -906,7 +907,9 @@ void conv_wgrad_launch(const ConvArgs& a0, const WgradPlan& p, float* out, bool 
                        hipStream_t st) {
   ConvArgs a = a0;
   const int splits = p.splits;
-  if (p.impl == 1) {
+  if (p.impl == 2) {
+    conv_wgrad_halo_launch(a, p, st);
+  } else if (p.impl == 1) {
     conv_wgrad_glds_kernel_launch(a, p, st);
   } else {
     const long tiles = (long)cdiv(a.M, p.bm) * cdiv(a.Ng, p.bn) * splits;

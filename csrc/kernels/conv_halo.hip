@@ -431,6 +431,207 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(ConvArgs a, HaloGeom 
 }
 
 // ------------------------------------------------------------------------------------------
+// weight gradient: dW[co][t][ci] = Σ_p dy[p][co] · x[p + off_t][ci]  (stride 1, 3×3 taps)
+// ------------------------------------------------------------------------------------------
+// A workgroup owns (co block of BM, ci chunk of 64, all 9 taps) and a split of the pixel tiles;
+// per pixel tile (TRW complete output rows, ≤ 128 pixels) it stages the dy tile (an MC image:
+// pixel k-rows × BM co columns) and the x halo of the ci chunk once, double-buffered, and runs
+// 4 k-blocks × 9 taps of MFMAs from them — the 9 taps re-read the same halo at slot offsets, so
+// x is fetched once per tile instead of once per tap (the implicit-GEMM wgrad gathers it 9×).
+// Both operands are pixel-major in memory: the fragments are transposed reads
+// (ds_read_b64_tr_b16) — dy from its MC image, x from the halo's slot rows.  Waves: 2 along co
+// (RM = BM/32 fragments each) × 4 along ci (16 channels each); accumulators RM × 9 taps.
+// Output: this split's fp32 slab rows [co][t·C + ci] (splitk_reduce sums the splits in order).
+template <int KK>
+__device__ __forceinline__ bf16x8 hread_tr_pair(uint32_t a0, uint32_t a1) {
+  v2u32 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+  (void)KK;
+  uint4 v = make_uint4(lo[0], lo[1], hi[0], hi[1]);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct HaloWg {
+  int nsplit, ncb, nch;  // splits, co blocks, ci chunks
+  int rb_per_split;      // pixel tiles (row blocks) per split
+};
+
+template <int BM, int HL>
+__global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, HaloGeom g, HaloWg q) {
+  constexpr int NW = 8, NTAP = 9, RM = BM / 32;
+  constexpr int PX = 128;                      // pixels per tile (k-rows of the dy image)
+  constexpr int A_BYTES = PX * BM * 2;         // dy MC image
+  constexpr int IA = A_BYTES / (1024 * NW);    // dy DMA instructions per wave
+  constexpr int HB = HL * NW * 1024;           // halo buffer
+  constexpr int STAGE = A_BYTES + HB;
+  static_assert(IA * 1024 * NW == A_BYTES, "dy image / wave mismatch");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wco = wid >> 2, wci = wid & 3;  // 2 waves along co, 4 along ci
+  if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch = blk % q.nch;
+  const int cb = (blk / q.nch) % q.ncb;
+  const int split = blk / (q.nch * q.ncb);
+  const int rb0 = split * q.rb_per_split;
+  const int ntile = min(q.rb_per_split, g.nrb - rb0);
+  const int m0 = cb * BM, c0 = ch * 64;
+  const rsrc_t rx = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t rdy = make_rsrc(a.dy, a.dy_bytes);
+  const rsrc_t rout = make_rsrc(a.out, a.out_bytes);
+  const uint32_t smem_lds = (uint32_t)(size_t)(lds_char_t*)smem;
+
+  f32x4 acc[RM][NTAP];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (ntile > 0) {
+    // ---- per-tile DMA (dy MC image + x halo of chunk c0) into stage `b` ----
+    auto issue = [&](int i, int b) {
+      const HTile t = htile(g, rb0 + i);
+      char* As = smem + b * STAGE;
+      char* Hs = As + A_BYTES;
+      const int npx = t.rows * g.Wo;
+      const uint32_t p0 = (uint32_t)(t.rho0 * g.Wo);
+#pragma unroll
+      for (int j = 0; j < IA; ++j) {
+        const int krow = (j * NW + wid) * (512 / BM) + lane / (BM / 8);
+        const int qq = lane % (BM / 8);
+        const int col = (((qq >> 1) ^ mc_swz<BM>(krow)) << 4) + ((qq & 1) << 3);
+        const int co = m0 + col;
+        const bool v = krow < npx && co < g.Co;
+        hdma16(rdy, As + (j * NW + wid) * 1024,
+               v ? ((p0 + (uint32_t)krow) * (uint32_t)g.Co + (uint32_t)co) * 2u : HOOB);
+      }
+      const int seg = g.Ho + g.ext_h;
+      const int rows0 = min(t.rows, g.Ho - t.h_first);
+      const int cnt0 = rows0 + g.ext_h;
+      const int rest = t.rows - rows0;
+      const int hr_total = cnt0 + rest + ((rest + g.Ho - 1) / g.Ho) * g.ext_h;
+#pragma unroll
+      for (int j = 0; j < HL; ++j) {
+        const int s = (j * NW + wid) * 8 + (lane >> 3);
+        const int hr = (int)fdiv((uint32_t)s, g.fd_HP);
+        const int hc = s - hr * g.HP;
+        int k, hi;
+        if (hr < cnt0) {
+          k = 0;
+          hi = t.h_first + g.oy_min + hr;
+        } else {
+          const int u = hr - cnt0;
+          const int kk = (int)fdiv((uint32_t)u, g.fd_seg);
+          k = 1 + kk;
+          hi = u - kk * seg + g.oy_min;
+        }
+        const int wi = g.ox_min + hc;
+        const bool v = hr < hr_total && hc < g.Wo + g.ext_w && (unsigned)hi < (unsigned)g.Hi &&
+                       (unsigned)wi < (unsigned)g.Wi;
+        const int lc = (lane & 7) ^ ((s >> 1) & 7);
+        const int n = t.n_first + k;
+        hdma16(rx, Hs + (j * NW + wid) * 1024,
+               v ? (uint32_t)((((n * g.Hi + hi) * g.Wi + wi) * g.Ci + c0 + lc * 8) * 2) : HOOB);
+      }
+    };
+    // per-lane halo slots of this lane's two transposed-read pixel rows in each k-block
+    const int krow_l = 8 * (lane >> 4) + ((lane >> 2) & 3);
+    uint32_t sl[4][2];
+    auto prep = [&](int i) {
+      const HTile t = htile(g, rb0 + i);
+      const int npx = t.rows * g.Wo;
+      const int rows0 = min(t.rows, g.Ho - t.h_first);
+      const int cnt0 = rows0 + g.ext_h;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int qp = kb * 32 + krow_l + 4 * h;
+          const int r = (int)fdiv((uint32_t)qp, g.fd_Wo);
+          const int w = qp - r * g.Wo;
+          int hrow;
+          if (r < rows0) {
+            hrow = r;
+          } else {
+            const int u = r - rows0;
+            const int kk = (int)fdiv((uint32_t)u, g.fd_Ho);
+            hrow = cnt0 + kk * (g.Ho + g.ext_h) + (u - kk * g.Ho);
+          }
+          sl[kb][h] = qp < npx ? (uint32_t)(hrow * g.HP + w) : 0u;  // dy rows there are 0
+        }
+    };
+    // dy fragments: MC image column base per co fragment (k-row krow_l; +4 rows: +8·BM bytes)
+    uint32_t aoff[RM];
+#pragma unroll
+    for (int f = 0; f < RM; ++f)
+      aoff[f] = (uint32_t)mc_off<BM>(krow_l, wco * (BM / 2) + f * 16 + 4 * (lane & 3));
+    const uint32_t cq = (uint32_t)((wci * 16 + 4 * (lane & 3)) >> 3);  // x chunk of this lane
+    const uint32_t cbyte = (uint32_t)((lane & 1) * 8);
+
+    issue(0, 0);
+    for (int i = 0; i < ntile; ++i) {
+      const int b = i & 1;
+      if (i + 1 < ntile) {
+        issue(i + 1, b ^ 1);  // its stage was last read in step i−1 (barrier below)
+        hwait<vmc(IA + HL)>();
+      } else {
+        hwait<0>();
+      }
+      hbarrier();
+      prep(i);
+      const uint32_t As = smem_lds + (uint32_t)(b * STAGE);
+      const uint32_t Hs = As + (uint32_t)A_BYTES;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        bf16x8 af[RM];
+#pragma unroll
+        for (int f = 0; f < RM; ++f) {
+          const uint32_t ad = As + aoff[f] + (uint32_t)(kb * 32 * BM * 2);
+          af[f] = hread_tr_pair<0>(ad, ad + 8 * BM);
+        }
+        auto xaddr = [&](uint32_t s0) {
+          return Hs + (s0 << 7) + ((cq ^ ((s0 >> 1) & 7u)) << 4) + cbyte;
+        };
+        bf16x8 xf = hread_tr_pair<0>(xaddr(sl[kb][0] + (uint32_t)g.tap_d[0]),
+                                     xaddr(sl[kb][1] + (uint32_t)g.tap_d[0]));
+        hlgkm0();
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) {
+          bf16x8 xn;
+          if (t + 1 < NTAP)
+            xn = hread_tr_pair<0>(xaddr(sl[kb][0] + (uint32_t)g.tap_d[t + 1]),
+                                  xaddr(sl[kb][1] + (uint32_t)g.tap_d[t + 1]));
+#pragma unroll
+          for (int f = 0; f < RM; ++f)
+            acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, af[f], acc[f][t], 0, 0, 0);
+          hlgkm0();
+          if (t + 1 < NTAP) xf = xn;
+        }
+      }
+      hbarrier();  // every wave is done with stage b before step i+1 refills it
+    }
+  }
+  // ---- this split's slab rows: lane holds dW[co = m0 + wco·BM/2 + f·16 + (lane&15)]
+  //      [tap t][ci = c0 + wci·16 + (lane>>4)·4 + 0..3] (an empty split writes zeros) ----
+  const uint32_t RSC = (uint32_t)(NTAP * g.Ci);
+  const uint32_t slab0 = (uint32_t)split * (uint32_t)g.Co * RSC;
+#pragma unroll
+  for (int f = 0; f < RM; ++f) {
+    const int co = m0 + wco * (BM / 2) + f * 16 + (lane & 15);
+    const uint32_t ci = (uint32_t)(c0 + wci * 16 + (lane >> 4) * 4);
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) {
+      const uint32_t off = (slab0 + (uint32_t)co * RSC + (uint32_t)t * (uint32_t)g.Ci + ci) * 4u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, acc[f][t]), rout,
+                                             co < g.Co ? off : OOB, 0, 0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 struct HCfg {
@@ -535,11 +736,108 @@ bool halo_common(const ConvArgs& a, HaloGeom& g, int R, int S, const int* oy, co
   return true;
 }
 
+template <int BM>
+void launch_hw(const ConvArgs& a, const HaloGeom& g, const HaloWg& q, hipStream_t st) {
+  auto k = conv_halo_wgrad_kernel<BM, 4>;
+  constexpr int lds = 2 * (128 * BM * 2 + 4 * 8 * 1024);
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  const int blocks = q.nsplit * q.ncb * q.nch;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), lds, st, a, g, q);
+}
+
+// geometry of a stride-1 3×3 weight gradient on the halo kernel (pixel tiles of ≤ 128 pixels, a
+// 4-instruction-per-wave halo); false when not eligible
+bool plan_halo_wgrad(const ConvArgs& a, HaloGeom& g, HaloWg& q, int& bm) {
+  if (a.sh != 1 || a.sw != 1 || a.R != 3 || a.S != 3 || a.C % 64 || a.K % 8) return false;
+  if (a.x_bytes >= 0x70000000u || a.dy_bytes >= 0x70000000u) return false;
+  g = HaloGeom{};
+  g.N = a.N; g.Hi = a.H; g.Wi = a.W; g.Ci = a.C;
+  g.Ho = a.Ho; g.Wo = a.Wo; g.Co = a.K;
+  g.ntap = 9;
+  g.nchunk = a.C / 64;
+  int oy[9], ox[9];
+  for (int r = 0; r < 3; ++r)
+    for (int s = 0; s < 3; ++s) {
+      oy[r * 3 + s] = r * a.dh - a.ph;
+      ox[r * 3 + s] = s * a.dw - a.pw;
+    }
+  int oy_min = 1 << 30, oy_max = -(1 << 30), ox_min = 1 << 30, ox_max = -(1 << 30);
+  for (int t = 0; t < 9; ++t) {
+    oy_min = std::min(oy_min, oy[t]);
+    oy_max = std::max(oy_max, oy[t]);
+    ox_min = std::min(ox_min, ox[t]);
+    ox_max = std::max(ox_max, ox[t]);
+  }
+  g.oy_min = oy_min; g.ox_min = ox_min;
+  g.ext_h = oy_max - oy_min; g.ext_w = ox_max - ox_min;
+  g.HP = g.Wo + g.ext_w;
+  for (int t = 0; t < 9; ++t) g.tap_d[t] = (oy[t] - oy_min) * g.HP + (ox[t] - ox_min);
+  int TR = 0;
+  for (int tr = std::max(1, 128 / g.Wo); tr >= 1; --tr) {
+    if (tr * g.Wo > 128) continue;
+    if (halo_rows(tr, g.Ho, g.ext_h) * g.HP <= 4 * 64) {
+      TR = tr;
+      break;
+    }
+  }
+  if (!TR) return false;
+  g.TR = TR;
+  g.nrb = cdiv((long)g.N * g.Ho, TR);
+  bm = henv("TDL_HALO_WG_BM", a.K >= 128 ? 128 : 64);
+  q.ncb = cdiv(a.K, bm);
+  q.nch = a.C / 64;
+  // ≈ 2 workgroups per CU slot in all, ≥ 8 pixel tiles per split
+  const int target = henv("TDL_HALO_WG_TARGET", 512);
+  int ns = std::max(1, target / (q.ncb * q.nch));
+  ns = std::min(ns, std::max(1, g.nrb / 8));
+  q.rb_per_split = cdiv(g.nrb, ns);
+  q.nsplit = cdiv(g.nrb, q.rb_per_split);
+  g.fd_HP = make_fastdiv((uint32_t)g.HP);
+  g.fd_Wo = make_fastdiv((uint32_t)g.Wo);
+  g.fd_Ho = make_fastdiv((uint32_t)g.Ho);
+  g.fd_seg = make_fastdiv((uint32_t)(g.Ho + g.ext_h));
+  return true;
+}
+
 }  // namespace
+
+bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p) {
+  if (!conv_halo_mode()) return false;
+  if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
+  // default: ≥ 128 input channels and enough pixel tiles to split over the chip (ResNet-50 b1024
+  // layers 2–4: 362 → 328 / 295 / 290 µs; the small-batch DeepLab shapes stay on the GEMMs)
+  if (conv_halo_mode() == 1 && (a.C < 128 || (long)a.N * a.Ho * a.Wo < 65536)) return false;
+  HaloGeom g;
+  HaloWg q;
+  int bm;
+  if (!plan_halo_wgrad(a, g, q, bm)) return false;
+  p->impl = 2;
+  p->cfg = bm;
+  p->bm = bm;
+  p->bn = 64;
+  p->splits = q.nsplit;
+  p->kps = q.rb_per_split;
+  return true;
+}
+
+void conv_wgrad_halo_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st) {
+  HaloGeom g;
+  HaloWg q;
+  int bm;
+  if (!plan_halo_wgrad(a, g, q, bm) || q.nsplit != p.splits)
+    throw std::runtime_error("conv_wgrad_halo_launch: plan mismatch");
+  if (bm == 128) launch_hw<128>(a, g, q, st);
+  else launch_hw<64>(a, g, q, st);
+}
 
 static int g_halo_override = -1;
 int conv_halo_mode() {
-  static int m = henv("TDL_HALO", 0);  // default off until validated on the GPU
+  static int m = henv("TDL_HALO", 1);
   return g_halo_override >= 0 ? g_halo_override : m;
 }
 void conv_set_halo_mode(int mode) { g_halo_override = mode; }
@@ -552,6 +850,10 @@ bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
   if (ntap < 3 || ntap > HALO_MAXTAP || a.C % 64 || a.K % 8 || a.ldc % 8) return false;
   if (a.x_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
   if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;  // small: GEMMs
+  // default selection (same-box A/B, bench/halo_ab.py, profiles/r04_halo_ab.txt): the halo
+  // forward wins where the GEMM kernels run 64-wide output tiles (ResNet layer1 3×3, 683 → 520 µs
+  // at b1024; DeepLab conv1_2) and loses ~10 % to the LDS-DMA implicit GEMM on wider outputs
+  if (conv_halo_mode() == 1 && a.K > 64) return false;
   HaloGeom g{};
   g.N = a.N; g.Hi = a.H; g.Wi = a.W; g.Ci = a.C;
   g.Ho = a.Ho; g.Wo = a.Wo; g.Co = a.K;
@@ -588,6 +890,9 @@ bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused) {
   if (ntap < 3 || ntap > HALO_MAXTAP || a.K % 64 || a.C % 8 || a.ldc % 8) return false;
   if (a.dy_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
   if (conv_halo_mode() != 2 && (long)a.N * a.H * a.W < 4096) return false;
+  // the implicit-GEMM input gradients win on every measured shape (bench/halo_ab.py): the halo
+  // dgrad runs only when forced (mode 2)
+  if (conv_halo_mode() == 1) return false;
   const bool stats = a.stats && a.bn_x;
   if (a.mask && a.ldc % 64) return false;  // mask slabs: 64-column rows
   HaloGeom g{};

@@ -110,6 +110,9 @@ int conv_halo_mode();
 void conv_set_halo_mode(int mode);  // -1: environment; 2: every eligible problem (tests)
 bool conv_fwd_halo(const ConvArgs& a, hipStream_t st);
 bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused);
+// stride-1 3×3 weight gradient on the halo kernel: plan impl 2 (fp32 split slabs as usual)
+bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p);
+void conv_wgrad_halo_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 // *fused: set to whether a.stats was filled (stride-1 FASTK problems only)
 bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st, bool* fused = nullptr);
 bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);

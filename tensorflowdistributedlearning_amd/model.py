@@ -339,11 +339,13 @@ class Model:
         eval_result = {}
         step = start
         t0 = time.time()
+        clock = _StepClock(device, start)
         while step < steps:
             x, yy = next(pipe)
             x = self._cast(x)
             loss, out = stepper(x, yy)
             step = trainer.global_step
+            clock.tick(step)
             pred = (out.float() > _logit(self.threshold)).float()
             score, acc = seg_scores(yy, pred, self.kaggle_metric)
             iou_m.update(score)
@@ -373,7 +375,8 @@ class Model:
         saver.wait()
         tw.close()
         ew.close()
-        res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step}
+        res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step,
+               "hip_graph": stepper.graph, "steady_ms_per_step": clock.result(step)}
         if main:
             with open(os.path.join(fold_dir, "result.json"), "w") as f:
                 json.dump(res, f)
@@ -451,10 +454,12 @@ class Model:
         eval_result, history = {}, []
         step = start
         t0 = time.time()
+        clock = _StepClock(device, start)
         while step < steps:
             x, yy = next(pipe)
             loss, out = stepper(x, yy)
             step = trainer.global_step
+            clock.tick(step)
             correct.update((out.float().argmax(-1) == yy).float())
             if main:
                 history.append(loss.detach().clone() if stepper.graph else loss.detach())
@@ -481,7 +486,8 @@ class Model:
         tw.close()
         ew.close()
         res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step,
-               "train_loss": [float(v) for v in history], "hip_graph": stepper.graph}
+               "train_loss": [float(v) for v in history], "hip_graph": stepper.graph,
+               "steady_ms_per_step": clock.result(step)}
         if main:
             with open(os.path.join(fold_dir, "result.json"), "w") as f:
                 json.dump(res, f)
@@ -741,3 +747,31 @@ class _Stepper:
             tr.capture(x, y, warmup=1)  # the warm-up step trains on (x, y)
             return tr.warmup_out
         return tr.replay(x, y)
+
+
+class _StepClock:
+    """Steady-state step time of a fold loop: wall clock between the end of step start+10 (after
+    the graph capture and the caches warmed up) and the last step, with one device sync at
+    each end — everything the loop does per step (loader, step, metrics, summaries) included."""
+
+    WARM = 10
+
+    def __init__(self, device, start):
+        self.device = device
+        self.mark = start + self.WARM
+        self.t0 = None
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def tick(self, step):
+        if step == self.mark:
+            self._sync()
+            self.t0 = time.perf_counter()
+
+    def result(self, step):
+        if self.t0 is None or step <= self.mark:
+            return None
+        self._sync()
+        return (time.perf_counter() - self.t0) * 1e3 / (step - self.mark)

@@ -176,13 +176,20 @@ def test_resnet50_classifier_through_model_on_gpu(tmp_path, gpu):
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_model_graph_training_tracks_eager(tmp_path, gpu):
-    """The HIP-graph fold loop follows the eager fold loop's loss trajectory (same data, same
-    init; frozen-free BN in batch-statistics mode, so within the fp32-atomic run-to-run noise)."""
-    kw = dict(CLS, device=None, save_checkpoints_steps=100, save_best=0)
-    ra = Model(str(tmp_path / "e"), "", hip_graph="off", **kw).train(192, None, 16, 10)[0]
-    rb = Model(str(tmp_path / "g"), "", **kw).train(192, None, 16, 10)[0]
+    """The HIP-graph fold loop replays the eager fold loop: at lr = 0 (no chaotic amplification
+    of the fp32-atomic run-to-run noise of batch-statistics BN) every step's loss — on a new
+    batch each step, copied into the graph's static inputs — matches the eager loop's; with a
+    small learning rate the first steps still track."""
+    kw = dict(CLS, device=None, save_checkpoints_steps=100, save_best=0, lr=0.0)
+    ra = Model(str(tmp_path / "e"), "", hip_graph="off", **kw).train(192, None, 16, 8)[0]
+    rb = Model(str(tmp_path / "g"), "", **kw).train(192, None, 16, 8)[0]
     assert rb["hip_graph"] and not ra["hip_graph"]
-    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.05, atol=0.02)
+    assert len(set(round(v, 4) for v in ra["train_loss"])) > 3  # the batches differ
+    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=2e-3, atol=2e-3)
+    kw.update(lr=0.002, momentum=0.0)
+    ra = Model(str(tmp_path / "e2"), "", hip_graph="off", **kw).train(192, None, 16, 4)[0]
+    rb = Model(str(tmp_path / "g2"), "", **kw).train(192, None, 16, 4)[0]
+    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.02, atol=0.01)
 
 
 @pytest.mark.gpu
@@ -204,4 +211,7 @@ def test_async_saver_snapshots_before_later_updates(tmp_path, gpu):
     for k, v in before.items():
         assert torch.equal(got[k], v)
     assert ckpt.latest_checkpoint(str(tmp_path)) == path
-    assert float(m.weight[0, 0].cpu()) == float(before["weight"][0, 0]) + 20.0
+    want = before["weight"][0, 0].clone()
+    for _ in range(20):
+        want += 1.0  # fp32 rounding as on the device
+    assert float(m.weight[0, 0].cpu()) == float(want)
