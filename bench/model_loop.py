@@ -43,15 +43,23 @@ def main():
     ap.add_argument("--steps", type=int, default=120)
     ap.add_argument("--images", type=int, default=640)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--modes", default="off,auto",
+                    help="comma list of hip_graph modes; 'auto:T:S' = auto with T loader threads "
+                         "and summaries every S steps (0: none)")
     args = ap.parse_args()
     from tensorflowdistributedlearning_amd.model import Model
     res = {}
     with tempfile.TemporaryDirectory() as td:
         X, y = write_dataset(os.path.join(td, "data"), args.images)
-        for mode in ("off", "auto"):
-            m = Model(os.path.join(td, f"run_{mode}", "tgs"), os.path.join(td, "data"), n_gpus=1,
-                      n_fold=5, max_folds=1, save_best=0, save_checkpoints_steps=10 ** 9,
-                      save_summary_steps=20, hip_graph=mode)
+        for spec in args.modes.split(","):
+            mode, *rest = spec.split(":")
+            threads = int(rest[0]) if rest else 4
+            summ = int(rest[1]) if len(rest) > 1 else 20
+            m = Model(os.path.join(td, f"run_{spec.replace(':', '_')}", "tgs"),
+                      os.path.join(td, "data"), n_gpus=1, n_fold=5, max_folds=1, save_best=0,
+                      save_checkpoints_steps=10 ** 9, save_summary_steps=summ, hip_graph=mode,
+                      loader_threads=threads)
+            mode = spec
             r = m.train(X, y, args.batch, args.steps)[0]
             res[mode] = {"steady_ms_per_step": r["steady_ms_per_step"], "hip_graph": r["hip_graph"],
                          "img_per_s": args.batch * 1e3 / r["steady_ms_per_step"]}

@@ -1301,6 +1301,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_halo_mode", &conv_set_halo_mode,
         "halo-tiled stride-1 conv: -1 environment (TDL_HALO, default 1), 0 off, 1 default "
         "selection, 2 every eligible problem regardless of size (tests)");
+  m.def("conv_set_pc", &conv_set_pc, "wave-specialised producer/consumer forward (-1: env)");
   m.def("conv_set_m32", &conv_set_m32, "32x32x16-MFMA K loop for KC-operand LDS-DMA convs (-1: env)");
   m.def("conv_m32", &conv_m32);
   m.def("conv_f32_set_tile", &conv_f32_set_tile, "fp32 conv FWD/DGRAD tile override (0, 0: auto)");

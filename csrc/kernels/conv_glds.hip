@@ -1009,6 +1009,15 @@ int conv_m32() {
   return g_m32_override >= 0 ? g_m32_override : m;
 }
 void conv_set_m32(int on) { g_m32_override = on; }
+// producer/consumer forward (conv_pc.hip): TDL_CONV_PC unset = auto (4 producer waves for the
+// 3×3 convs with ≥ 256 input channels, where it measured faster: profiles/r04_conv_pc_ab.txt),
+// 0 = off, 1 / 2 = 2 / 4 producer waves on every FASTK 256×128 forward; conv_set_pc(-1) = env
+static int g_pc_override = -1;
+int conv_pc() {
+  static int m = env_int("TDL_CONV_PC", -1);
+  return g_pc_override >= 0 ? g_pc_override : m;
+}
+void conv_set_pc(int on) { g_pc_override = on; }
 
 bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int mode = conv_glds_mode();
@@ -1083,6 +1092,12 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
       else launch_g<FWD, 256, 128, 4, 2, 3, false, false, 1, false, false, false, true>(a, blocks, st);
     }
     return true;
+  }
+  // TDL_CONV_PC=1: the wave-specialised producer/consumer forward (conv_pc.hip)
+  {
+    int pc = conv_pc();
+    if (pc < 0) pc = (a.R * a.S > 1 && a.C >= 256) ? 2 : 0;
+    if (pc > 0 && fk != 0 && cfg == 0 && conv_fwd_pc_launch(a, blocks, fk, pc, st)) return true;
   }
   if (fk == 1) TDL_G(1);
   else if (fk == 2) TDL_G(2);

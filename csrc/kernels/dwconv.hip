@@ -3,11 +3,14 @@
 // (dgrad) pixel; wgrad keeps R·S·8 fp32 partial sums per lane over a pixel range, reduces them
 // through LDS and issues one contiguous atomic row per workgroup.  Scalar variants handle
 // C % 8 != 0 (e.g. the single-channel Laplacian of the preprocessing).
-#include "common.h"
-#include "kernels.h"
+#include "conv_common.h"
 
 namespace tdl {
 namespace {
+using convk::OOB;
+using convk::make_rsrc;
+using convk::rsrc_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int NT = 256;
 inline int blocks_for(long n) { return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT)); }
@@ -568,46 +571,49 @@ __global__ void __launch_bounds__(NT) dw_slide4_kernel(const bf16_t* __restrict_
 }
 
 // LDS-tiled depthwise 3×3 stride 1: a workgroup stages its (TR+2)×(TW+2) input pixels × 64
-// channels once (coalesced 16-B loads, ≈1.3× the tile's own bytes incl. halo), then every lane
+// channels once (LDS-DMA, ≈1.3× the tile's own bytes incl. halo), then every lane
 // (8 channels × one output column) slides down the TR rows reading its 3×3 window from LDS.
 // The register-window kernels above re-fetch each input row for 3 output-row workgroups from the
 // fabric (PMC: 3.2× the input bytes); here the re-reads are LDS reads.
 constexpr int DT_TR = 8, DT_TW = 32, DT_CH = 64;
-constexpr int DT_CHUNKS = (DT_TR + 2) * (DT_TW + 2) * (DT_CH / 8);
 
-__device__ __forceinline__ void unpack8x2(const uint4& v, f32x2* f) {
+__device__ __forceinline__ void unpack4x2(const uint2& v, f32x2* f) {
   f[0] = lo_hi(v.x);
   f[1] = lo_hi(v.y);
-  f[2] = lo_hi(v.z);
-  f[3] = lo_hi(v.w);
 }
+__device__ __forceinline__ uint2 relu4(uint2 v) { return make_uint2(relu2(v.x), relu2(v.y)); }
+
+constexpr int DT_NT = 512;  // tile-kernel workgroup cap (16 channel lanes × ≤ 32 columns)
 
 template <bool FLIP>
-__global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ in,
-                                                     const bf16_t* __restrict__ wt,
-                                                     const float* __restrict__ bias,
-                                                     bf16_t* __restrict__ out, int Hi, int Wi,
-                                                     int Ho, int Wo, int C, int Ph, int Pw,
-                                                     int relu, int tr, int tw, int rg, int tiles_h,
-                                                     int tiles_w, int relu_in,
-                                                     const bf16_t* __restrict__ mask_x,
-                                                     float* __restrict__ stats,
-                                                     const bf16_t* __restrict__ bn_x, int ntiles,
-                                                     const bf16_t* __restrict__ dadd) {
+__global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restrict__ in,
+                                                        const bf16_t* __restrict__ wt,
+                                                        const float* __restrict__ bias,
+                                                        bf16_t* __restrict__ out, int Hi, int Wi,
+                                                        int Ho, int Wo, int C, int Ph, int Pw,
+                                                        int relu, int tr, int tw, int rg,
+                                                        int tiles_h, int tiles_w, int relu_in,
+                                                        const bf16_t* __restrict__ mask_x,
+                                                        float* __restrict__ stats,
+                                                        const bf16_t* __restrict__ bn_x, int ntiles,
+                                                        const bf16_t* __restrict__ dadd) {
   // stats (optional, fp32 [2][C], accumulated): BN sums of the stored bf16 outputs — (Σy, Σy²)
   // for the BN that normalises this forward's output, or (Σg, Σg·bn_x) with bn_x the input of
   // the BN whose output gradient this dgrad produces (bn.hip red_raw) — so that BN skips its
   // separate reduce pass
   // tile: tr × tw output pixels (runtime, ≤ DT_TR × DT_TW, balanced splits of Ho / Wo); lanes:
-  // 8 channel lanes × tw column lanes × rg row groups (each slides over ⌈tr / rg⌉ rows)
+  // 16 channel lanes (4 channels each) × tw column lanes × rg row groups (each slides over
+  // ⌈tr / rg⌉ rows).  Four channels per lane keep the sliding window + taps at 72 fp32 registers
+  // (8 per lane needed ≈170 VGPRs: 2 waves per SIMD, too few to hide the halo DMA latency).
   // A workgroup walks tiles blockIdx.x, +gridDim.x, … < ntiles (one tile per workgroup unless
   // the launcher caps the grid — with statistics, so each workgroup flushes its sums once).
-  __shared__ uint4 tile[DT_CHUNKS];
+  extern __shared__ uint4 tile[];  // dw_tile_smem(): the launch's halo tile (whole DMA pieces)
+  const uint2* tile2 = (const uint2*)tile;
   const int t = threadIdx.x;
-  const int cl = t & 7, rest = t >> 3, cg0 = blockIdx.y * DT_CH;
-  float ss[8], sq[8];
+  const int cl = t & 15, rest = t >> 4, cg0 = blockIdx.y * DT_CH;
+  float ss[4], sq[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ss[j] = sq[j] = 0.f;
+  for (int j = 0; j < 4; ++j) ss[j] = sq[j] = 0.f;
   for (int tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
   if (tb != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
   int b = tb;
@@ -618,82 +624,102 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
   const int h0 = ty * tr, w0 = tx * tw;
   const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
   const bf16_t* src = in + (long)n * Hi * Wi * C;
-  for (int i = t; i < chunks; i += blockDim.x) {
-    const int k = i & 7, pix = i >> 3;
-    const int r = pix / pitch, cc = pix - r * pitch;
-    const int hi = h0 - Ph + r, wi = w0 - Pw + cc, ch = cg0 + k * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if ((unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi && ch < C) {
-      v = *(const uint4*)(src + ((long)hi * Wi + wi) * C + ch);
-      if (relu_in) v = relu8(v);
+  // staging: LDS-DMA, one 1-KiB piece (64 lanes × 16 B, lane-linear in LDS) per wave instruction;
+  // padding / ragged chunks read past the range-checked descriptor (zeros).  No per-chunk branch
+  // around a load, so the pieces stream back-to-back instead of one latency each.
+  {
+    const rsrc_t rs = make_rsrc(src, (uint32_t)((long)Hi * Wi * C * 2));
+    const int nwv = blockDim.x >> 6, ln = t & 63;
+    for (int j = t >> 6; j * 64 < chunks; j += nwv) {
+      const int i = j * 64 + ln, k = i & 7, pix = i >> 3;
+      const int r = pix / pitch, cc = pix - r * pitch;
+      const int hi = h0 - Ph + r, wi = w0 - Pw + cc, ch = cg0 + k * 8;
+      const bool ok = i < chunks && (unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi &&
+                      ch < C;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)((char*)tile + j * 1024), 16,
+                                               ok ? (uint32_t)(((hi * Wi + wi) * C + ch) * 2) : OOB,
+                                               0, 0, 0);
     }
-    tile[i] = v;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   const int pw = rest % tw, g = rest / tw;
-  const int w = w0 + pw, c = cg0 + cl * 8;
+  const int w = w0 + pw, c = cg0 + cl * 4;
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
   const int r1 = min(min(tr, r0 + rpg), Ho - h0);
   const bool active = !(g >= rg || w >= Wo || c >= C || r0 >= r1);
+  // the fused input ReLU is applied on the LDS read (the DMA stages raw values); a pixel's 64
+  // channels are 16 uint2 slots, this lane's 4 channels slot cl
+  auto ldt = [&](int pix) { const uint2 v = tile2[pix * 16 + cl]; return relu_in ? relu4(v) : v; };
   if (active) {
-  f32x2 wv[9][4], bb[4];
+  f32x2 wv[9][2], bb[2];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) unpack8x2(*(const uint4*)(wt + (long)(FLIP ? 8 - k : k) * C + c), wv[k]);
+  for (int k = 0; k < 9; ++k) unpack4x2(*(const uint2*)(wt + (long)(FLIP ? 8 - k : k) * C + c), wv[k]);
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 2; ++q)
     bb[q] = bias ? f32x2{bias[c + 2 * q], bias[c + 2 * q + 1]} : f32x2{0.f, 0.f};
-  f32x2 win[3][3][4];
+  f32x2 win[3][3][2];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int s2 = 0; s2 < 3; ++s2) unpack8x2(tile[((r0 + r) * pitch + pw + s2) * 8 + cl], win[r + 1][s2]);
+    for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt((r0 + r) * pitch + pw + s2), win[r + 1][s2]);
   for (int h = r0; h < r1; ++h) {
 #pragma unroll
     for (int s2 = 0; s2 < 3; ++s2) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 2; ++q) {
         win[0][s2][q] = win[1][s2][q];
         win[1][s2][q] = win[2][s2][q];
       }
-      unpack8x2(tile[((h + 2) * pitch + pw + s2) * 8 + cl], win[2][s2]);
+      unpack4x2(ldt((h + 2) * pitch + pw + s2), win[2][s2]);
     }
-    f32x2 acc[4] = {bb[0], bb[1], bb[2], bb[3]};
+    f32x2 acc[2] = {bb[0], bb[1]};
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
       for (int s2 = 0; s2 < 3; ++s2)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 2; ++q)
           acc[q] = __builtin_elementwise_fma(win[r][s2][q], wv[r * 3 + s2][q], acc[q]);
-    float o[8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      o[2 * q] = acc[q].x;
-      o[2 * q + 1] = acc[q].y;
-    }
+    float o[4] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y};
     if (relu) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+      for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
     }
     const long op = (((long)n * Ho + h0 + h) * Wo + w) * C + c;
-    if (mask_x) mask_pos(o, mask_x + op);
-    if (dadd) add8(o, dadd + op);
-    const uint4 packed = pack8(o);
-    *(uint4*)(out + op) = packed;
+    if (mask_x) {  // dx · [x > 0] for the fused input ReLU's backward
+      const uint2 xm = *(const uint2*)(mask_x + op);
+      const f32x2 x0 = lo_hi(xm.x), x1 = lo_hi(xm.y);
+      o[0] = x0.x > 0.f ? o[0] : 0.f;
+      o[1] = x0.y > 0.f ? o[1] : 0.f;
+      o[2] = x1.x > 0.f ? o[2] : 0.f;
+      o[3] = x1.y > 0.f ? o[3] : 0.f;
+    }
+    if (dadd) {  // residual-gradient join
+      const uint2 d = *(const uint2*)(dadd + op);
+      const f32x2 d0 = lo_hi(d.x), d1 = lo_hi(d.y);
+      o[0] += d0.x;
+      o[1] += d0.y;
+      o[2] += d1.x;
+      o[3] += d1.y;
+    }
+    const uint2 packed = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+    *(uint2*)(out + op) = packed;
     if (stats) {
-      float q[8];
-      unpack8(packed, q);  // the stored bf16 values
+      const f32x2 q0 = lo_hi(packed.x), q1 = lo_hi(packed.y);  // the stored bf16 values
+      const float q[4] = {q0.x, q0.y, q1.x, q1.y};
       if (bn_x) {
-        float xv[8];
-        unpack8(*(const uint4*)(bn_x + op), xv);
+        const uint2 xb = *(const uint2*)(bn_x + op);
+        const f32x2 x0 = lo_hi(xb.x), x1 = lo_hi(xb.y);
+        const float xv[4] = {x0.x, x0.y, x1.x, x1.y};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
           ss[j] += q[j];
           sq[j] = fmaf(q[j], xv[j], sq[j]);
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4; ++j) {
           ss[j] += q[j];
           sq[j] = fmaf(q[j], q[j], sq[j]);
         }
@@ -707,11 +733,11 @@ __global__ void __launch_bounds__(NT) dw_tile_kernel(const bf16_t* __restrict__ 
     // then one atomic pair per channel
     __syncthreads();
     float* red = (float*)tile;
-    const int L = blockDim.x >> 3;  // lanes per channel lane (≤ 32)
+    const int L = blockDim.x >> 4;  // lanes per channel lane (≤ 32)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[(cl * 8 + j) * L + rest] = ss[j];
-      red[(64 + cl * 8 + j) * L + rest] = sq[j];
+    for (int j = 0; j < 4; ++j) {
+      red[(cl * 4 + j) * L + rest] = ss[j];
+      red[(64 + cl * 4 + j) * L + rest] = sq[j];
     }
     __syncthreads();
     for (int o = t; o < 128; o += blockDim.x) {  // (64-thread workgroups for tiny images)
@@ -737,6 +763,7 @@ int dw_tile_grid(int ntiles, int C, bool stats) {
 }
 
 // balanced tiling of an Ho × Wo output: tw ≤ 32 columns, tr ≤ 8 rows, rg = 32 / tw row groups
+// (≤ 16 · 32 = 512 threads)
 struct DwTileGeom {
   int tr, tw, rg, th, twn, nt;
 };
@@ -747,8 +774,17 @@ DwTileGeom dw_tile_geom(int Ho, int Wo) {
   g.th = cdiv(Ho, DT_TR);
   g.tr = cdiv(Ho, g.th);
   g.rg = std::max(1, std::min(DT_TW / g.tw, g.tr));
-  g.nt = cdiv(8 * g.tw * g.rg, 64) * 64;
+  g.nt = cdiv(16 * g.tw * g.rg, 64) * 64;
   return g;
+}
+
+// dynamic LDS of a tile launch: the (tr+2)×(tw+2)×64-channel halo in whole 1-KiB DMA pieces (or
+// the statistics reduction's 128 × lanes floats) — sized to the launch, not the largest tile, so
+// small-image layers fit more workgroups per CU (24 KiB at 19×19 vs 43 KiB)
+size_t dw_tile_smem(const DwTileGeom& g, bool stats) {
+  const size_t halo = (size_t)cdiv((g.tr + 2) * (g.tw + 2) * 8, 64) * 64 * 16;
+  const size_t red = stats ? (size_t)128 * (g.nt / 16) * 4 : 0;
+  return std::max(halo, red);
 }
 
 // wgrad with the same sliding window over x: a lane walks a contiguous run of output columns of
@@ -866,6 +902,8 @@ bool dw_tile() {
   }();
   return v != 0;
 }
+// the tile kernel's DMA offsets are 32-bit bytes within one image
+bool dw_tile_fits(long h, long w, long c) { return h * w * c * 2 < (1L << 31) - 64; }
 
 // 4-channel sliding kernel (default; TDL_DW_VEC=8 selects the 8-channel one)
 bool slide4() {
@@ -933,11 +971,12 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
-  if (slide_ok(a) && dw_tile()) {
+  if (slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C)) {
     const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
     const int ntiles = a.N * g.th * g.twn;
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
-    hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), 0, st, a.x, a.w, a.bias, a.out,
+    hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
+                       st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
                        g.twn, a.relu_in, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
                        ntiles, (const bf16_t*)nullptr);
@@ -968,11 +1007,12 @@ bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
 
 bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
   const long ins = (long)a.N * a.H * a.W * a.C;
-  if (slide_ok(a) && dw_tile()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
+  if (slide_ok(a) && dw_tile() && dw_tile_fits(a.Ho, a.Wo, a.C)) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const DwTileGeom g = dw_tile_geom(a.H, a.W);
     const int ntiles = a.N * g.th * g.twn;
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
-    hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), 0, st, a.dy, a.w, nullptr, a.out,
+    hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
+                       st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
                        g.twn, 0, a.mask_x, a.stats, a.bn_x, ntiles, a.dadd);
     return a.stats != nullptr;

@@ -103,6 +103,9 @@ void conv_set_glds_mode(int mode);  // -1: environment / default
 // override (-1: environment)
 int conv_m32();
 void conv_set_m32(int on);
+int conv_pc();
+bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st);
+void conv_set_pc(int on);
 bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
 // halo-tiled direct conv (conv_halo.hip) for stride-1 R×S filters, Cin % 64 == 0: true when it
 // ran (TDL_HALO=0 disables); the dgrad sets *fused when a.stats was filled

@@ -10,6 +10,9 @@
            config 1: ``train --arch resnet18 --image-size 32 --synthetic --device cpu``;
   predict  TTA-averaged probabilities of every ``*.png`` in a directory → ``.npz`` (+ optional CSV
            with run-length-encoded masks, the Kaggle submission format);
+  export   the servable program of a trained fold (its latest checkpoint) → ``.pt2``
+           (engine/serving.py: ``--kind native`` tdl:: operators on the gfx950 kernels, or
+           ``portable`` stock ATen that any PyTorch loads);
   bench    the training benchmark (same as ``python bench.py``);
   config   print the default configuration (JSON) to start a config file from.
 
@@ -94,6 +97,14 @@ def cmd_predict(args):
     print(f"wrote {args.out}" + (f" and {args.csv}" if args.csv else ""))
 
 
+def cmd_export(args):
+    from .model import Model
+    cfg = _model_cfg(args)
+    m = Model(**cfg.model_kwargs())
+    path = m.export(args.out, args.fold, args.kind, args.checkpoint, batch=2)
+    print(f"wrote {path}")
+
+
 def cmd_bench(rest):
     sys.argv = ["bench.py"] + rest
     here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -145,6 +156,8 @@ def main(argv=None):
         p.add_argument("--save-checkpoints-steps", dest="save_checkpoints_steps", type=int)
         p.add_argument("--save-summary-steps", dest="save_summary_steps", type=int)
         p.add_argument("--eval-batches", dest="eval_batches", type=int)
+        p.add_argument("--export-format", dest="export_format",
+                       choices=("native", "portable", "both", "none"))
 
     t = sub.add_parser("train")
     common(t)
@@ -155,12 +168,20 @@ def main(argv=None):
     p.add_argument("--tta", action="store_true")
     p.add_argument("--out", default="predictions.npz")
     p.add_argument("--csv")
+    e = sub.add_parser("export")
+    common(e)
+    e.add_argument("--fold", type=int, default=0)
+    e.add_argument("--kind", choices=("native", "portable"), default="native")
+    e.add_argument("--checkpoint")
+    e.add_argument("--out", default="model.pt2")
     sub.add_parser("config")
     args = ap.parse_args(argv)
     if args.cmd == "train":
         cmd_train(args)
     elif args.cmd == "predict":
         cmd_predict(args)
+    elif args.cmd == "export":
+        cmd_export(args)
     elif args.cmd == "config":
         print(json.dumps(dataclasses.asdict(ModelConfig()), indent=1))
 

@@ -71,6 +71,7 @@ class ModelConfig:
     hip_graph: str = "auto"           # capture each fold's step as a HIP graph (GPU)
     eval_batches: Optional[int] = None
     max_folds: Optional[int] = None   # train only the first k folds
+    export_format: str = "native"     # servable program per best export: native|portable|both|none
 
     def validate(self):
         if self.data_format not in ("NCHW", "NHWC"):
@@ -85,6 +86,8 @@ class ModelConfig:
             raise ValueError(f"unknown precision {self.precision} (bf16 or fp32)")
         if self.arch not in SEGMENTATION_ARCHS + CLASSIFIER_ARCHS:
             raise ValueError(f"unknown arch {self.arch}")
+        if self.export_format not in ("native", "portable", "both", "none"):
+            raise ValueError(f"unknown export_format {self.export_format}")
         return self
 
     def model_kwargs(self):
@@ -108,7 +111,7 @@ class BenchConfig:
     loss: Optional[str] = None        # softmax_ce (classifiers) | lovasz (deeplab_ref)
     synthetic: bool = True            # the only data source of the benchmark
     batch: Optional[int] = None       # per GPU (None: 1024 for classifiers, 64/N deeplab_ref)
-    image_size: int = 224
+    image_size: Optional[int] = None  # None: 299 for xception41 (BASELINE config 4), else 224
     steps: int = 20
     warmup: int = 5
     lr: Optional[float] = None        # None: 0.1 (SGD) / 1e-3 (Adam)
@@ -128,6 +131,8 @@ class BenchConfig:
         self.loss = self.loss or ("lovasz" if seg else "softmax_ce")
         if self.lr is None:
             self.lr = 1e-3 if self.optimizer == "adam" else 0.1
+        if self.image_size is None:
+            self.image_size = 299 if self.arch == "xception41" else 224
         if self.dtype not in ("bf16", "fp32", "fp8"):
             raise ValueError(f"unknown dtype {self.dtype}")
         if self.optimizer not in ("adam", "sgd_momentum"):

@@ -5,8 +5,10 @@ model.py:189-204).
 Each export is an inference bundle under ``fold{i}/export/best_exporter/<timestamp>/``:
 ``variables.safetensors`` (weights + BN moving statistics, reference TF names when available),
 ``config.json`` (model config + serving signature: input key ``images`` [None, H, W, C] — the
-reference's serving key mismatch D3 is fixed) and ``eval_result.json``.  At most
-``exports_to_keep`` bundles are kept (oldest removed first, like TF's exporter GC).
+reference's serving key mismatch D3 is fixed), ``eval_result.json`` and — the SavedModel part —
+the servable program ``model.pt2`` (+ ``model.json``; ``model_portable.pt2`` for the stock-ATen
+lowering), see engine/serving.py.  At most ``exports_to_keep`` bundles are kept (oldest removed
+first, like TF's exporter GC).
 """
 from __future__ import annotations
 
@@ -14,6 +16,7 @@ import json
 import os
 import shutil
 import time
+import warnings
 
 import torch
 from safetensors.torch import save_file
@@ -21,7 +24,15 @@ from safetensors.torch import save_file
 
 class BestExporter:
     def __init__(self, export_dir, compare_fn, exports_to_keep=5, name="best_exporter",
-                 serving_shape=None, model_config=None):
+                 serving_shape=None, model_config=None, serving="native", task="segmentation",
+                 compute_dtype=None):
+        """``serving``: servable program(s) written with each bundle — "native" (tdl:: ops,
+        gfx950 kernels), "portable" (stock ATen), "both" or None (weights only)."""
+        if serving not in (None, "none", "native", "portable", "both"):
+            raise ValueError(f"unknown serving export {serving!r}")
+        self.serving = None if serving == "none" else serving
+        self.task = task
+        self.compute_dtype = compute_dtype
         self.dir = os.path.join(export_dir, name)
         self.compare_fn = compare_fn
         self.keep = exports_to_keep
@@ -52,14 +63,36 @@ class BestExporter:
         tensors = {names.get(k, k): v.detach().to("cpu").contiguous()
                    for k, v in model.state_dict().items()}
         save_file(tensors, os.path.join(out, "variables.safetensors"))
+        served = self._serving(model, out) if self.serving and self.serving_shape else {}
+        outputs = (["probabilities", "mask"] if self.task == "segmentation"
+                   else ["logits", "probabilities", "classes"])
         with open(os.path.join(out, "config.json"), "w") as f:
             json.dump({"model": self.model_config, "global_step": int(step),
                        "signature": {"inputs": {"images": self.serving_shape},
-                                     "outputs": ["probabilities", "mask"]}}, f)
+                                     "outputs": outputs}, "serving": served}, f)
         with open(os.path.join(out, "eval_result.json"), "w") as f:
             json.dump({k: float(v) for k, v in eval_result.items()}, f)
         self._gc()
         return out
+
+    def _serving(self, model, out):
+        """Write the servable program(s); a tracing failure is reported in config.json (and
+        warned) instead of ending the training run that produced the weights."""
+        from . import serving as sv
+        p = next(iter(model.parameters()))
+        example = torch.zeros([2] + list(self.serving_shape[1:]), device=p.device)
+        kinds = ("native", "portable") if self.serving == "both" else (self.serving,)
+        res = {}
+        for kind in kinds:
+            name = "model.pt2" if kind == "native" else "model_portable.pt2"
+            try:
+                sv.export_serving(model, example, os.path.join(out, name), self.task, kind,
+                                  self.compute_dtype)
+                res[kind] = name
+            except Exception as e:  # noqa: BLE001 — keep the weights bundle
+                warnings.warn(f"serving export ({kind}) failed: {e!r}")
+                res[kind] = f"error: {e!r}"
+        return res
 
     def _gc(self):
         exports = sorted(d for d in os.listdir(self.dir) if d.isdigit())

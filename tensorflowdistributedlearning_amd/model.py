@@ -88,6 +88,21 @@ def _undo_transform(t, transformation):
     return t
 
 
+def network_from_config(cfg):
+    """Rebuild the network a :meth:`Model.config` dict describes (export bundles' config.json)."""
+    arch = cfg.get("arch", "deeplab_ref")
+    if arch in CLASSIFIER_ARCHS:
+        return _models.build(arch, num_classes=cfg["num_classes"],
+                             in_channels=cfg.get("image_channels", 3))
+    return DeepLabResNet(model_name=cfg["model_name"], in_channels=2,
+                         output_stride=cfg["output_stride"], base_depth=cfg["base_depth"],
+                         input_shape=tuple(cfg["input_shape"]), n_blocks=tuple(cfg["n_blocks"]),
+                         block_type=cfg["block_type"], batch_norm_decay=cfg["batch_norm_decay"],
+                         batch_norm_epsilon=cfg["batch_norm_epsilon"],
+                         batch_norm_scale=cfg["batch_norm_scale"],
+                         weight_decay=cfg["weight_decay"])
+
+
 class Model:
     def __init__(self, model_dir, data_directory, data_format="NHWC", lr=0.001, n_gpus=2,
                  n_fold=5, seed=42, save_best=5, **kwargs):
@@ -153,6 +168,11 @@ class Model:
         self.hip_graph = kwargs.get("hip_graph", "auto")
         self.eval_batches = kwargs.get("eval_batches", None)  # cap on eval batches per pass
         self.max_folds = kwargs.get("max_folds", None)  # train only the first k folds
+        # servable program written with every best export (engine/serving.py; the reference's
+        # SavedModel): native (tdl:: ops) | portable (stock ATen) | both | none
+        self.export_format = kwargs.get("export_format", "native")
+        if self.export_format not in ("native", "portable", "both", "none"):
+            raise ValueError(f"unknown export_format {self.export_format}")
 
         self.model_name = model_dir.rstrip("/").split("/")[-1]
         self.model_dir = model_dir
@@ -187,19 +207,39 @@ class Model:
                 "lr": self.lr, "seed": self.seed, "precision": self.precision}
 
     def build_network(self):
-        if not self.segmentation:
-            net = _models.build(self.arch, num_classes=self.num_classes,
-                                in_channels=self.image_channels)
-            if self.fp8:
-                _models.enable_fp8(net)
-            return net
-        return DeepLabResNet(model_name=self.model_name, in_channels=2,
-                             output_stride=self.output_stride, base_depth=self.base_depth,
-                             input_shape=self.input_shape, n_blocks=self.n_blocks,
-                             block_type=self.block_type, batch_norm_decay=self.batch_norm_decay,
-                             batch_norm_epsilon=self.batch_norm_epsilon,
-                             batch_norm_scale=self.batch_norm_scale,
-                             weight_decay=self.weight_decay)
+        net = network_from_config(self.config())
+        if not self.segmentation and self.fp8:
+            _models.enable_fp8(net)
+        return net
+
+    def export(self, path, fold=0, kind="native", checkpoint=None, device=None, batch=2):
+        """Write the servable program of fold ``fold`` (its latest checkpoint, or ``checkpoint``)
+        to ``path`` — engine/serving.py; ``kind`` native | portable.  Returns the path."""
+        from .engine import serving
+        dev = torch.device(device or self.device or ("cuda" if torch.cuda.is_available()
+                                                      else "cpu"))
+        net = self.build_network().to(dev)
+        ck = checkpoint or ckpt.latest_checkpoint(os.path.join(self.model_dir, f"fold{fold}"))
+        if ck is None:
+            raise FileNotFoundError(f"no checkpoint for fold {fold} under {self.model_dir}")
+        ckpt.restore(ck, net)
+        if dev.type == "cuda" and self.precision == "bf16":
+            net._tdl_flat = FlatParams(net, dev, lowp_dtype=torch.bfloat16, with_grad=False)
+        shape = self._serving_shape()
+        example = torch.zeros([batch] + shape[1:], device=dev)
+        serving.export_serving(net, example, path, "segmentation" if self.segmentation
+                               else "classification", kind, self._serving_dtype(dev))
+        return path
+
+    def _serving_shape(self):
+        if self.segmentation:
+            return [None, self.input_shape[0], self.input_shape[1], 2]
+        return [None, self.image_size, self.image_size, self.image_channels]
+
+    def _serving_dtype(self, device):
+        if torch.device(device).type != "cuda" or self.precision == "fp32":
+            return torch.float32
+        return torch.bfloat16
 
     def _cast(self, x):
         """The network input in the compute precision (the loaders deliver bf16 images, or fp32
@@ -331,9 +371,9 @@ class Model:
                 os.path.join(fold_dir, "export"),
                 functools.partial(metric_comparisson, key="metrics/mean_iou",
                                   greater_is_better=True),
-                exports_to_keep=self.save_best,
-                serving_shape=[None, self.input_shape[0], self.input_shape[1], 2],
-                model_config=self.config())
+                exports_to_keep=self.save_best, serving_shape=self._serving_shape(),
+                model_config=self.config(), serving=self.export_format, task="segmentation",
+                compute_dtype=self._serving_dtype(device))
         iou_m, acc_m = StreamingMean(device), StreamingMean(device)
         saver = ckpt.AsyncSaver()  # D2H on a copy stream, file write on a worker thread
         eval_result = {}
@@ -446,9 +486,9 @@ class Model:
                 os.path.join(fold_dir, "export"),
                 functools.partial(metric_comparisson, key="metrics/accuracy",
                                   greater_is_better=True),
-                exports_to_keep=self.save_best,
-                serving_shape=[None, self.image_size, self.image_size, self.image_channels],
-                model_config=self.config())
+                exports_to_keep=self.save_best, serving_shape=self._serving_shape(),
+                model_config=self.config(), serving=self.export_format, task="classification",
+                compute_dtype=self._serving_dtype(device))
         correct = StreamingMean(device)
         saver = ckpt.AsyncSaver()  # D2H on a copy stream, file write on a worker thread
         eval_result, history = {}, []

@@ -32,6 +32,7 @@ from ..ops.upsample import upsample, upsample_into
 from ..ops.elementwise import add_relu
 from ..ops import gradjoin
 from ..ops.bn import ResidualLink
+from ..ops.common import export_impl
 
 
 class _Subsample(nn.Module):
@@ -261,7 +262,9 @@ class DeepLabResNet(nn.Module):
         atrous = end_points[f"{root}/block4"].contiguous()  # a copy only for unaligned widths
         last = 3 if self.block_type == "bottleneck" else 2
         b1 = end_points[f"{root}/block1/unit_1/bottleneck_v2/conv{last}"].contiguous()
-        if self.concat_free and self._concat_free_ok(atrous):
+        # (a serving trace takes the torch.cat head: the in-place concat writers are training
+        # fusions with no functional form)
+        if self.concat_free and export_impl() is None and self._concat_free_ok(atrous):
             out = self._head_concat_free(atrous, b1)
             return (out, end_points) if return_end_points else out
         size = (atrous.shape[1], atrous.shape[2])

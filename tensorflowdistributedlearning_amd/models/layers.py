@@ -528,8 +528,8 @@ class DepthwiseConv2d(nn.Module):
         residual-gradient join for x (ops/gradjoin.py; see ops.dwconv.joinable)."""
         pad = resolve_padding(self.padding, x.shape[1], x.shape[2], self.k, self.k, self.stride,
                               self.dilation)
-        return depthwise_conv2d(x, self.weight, self.bias, ConvGeom(self.stride, pad,
-                                                                    self.dilation), self.relu,
+        w, b = self.__dict__.get("_serve") or (self.weight, self.bias)  # frozen: serving.py
+        return depthwise_conv2d(x, w, b, ConvGeom(self.stride, pad, self.dilation), self.relu,
                                 relu_in, want_stats, join)
 
     def forward_folded(self, x, w, bias, relu, relu_in=False):

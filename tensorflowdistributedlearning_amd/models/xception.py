@@ -20,7 +20,7 @@ import torch.nn as nn
 from . import params as _params
 from .layers import (ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear, bn_fold_enabled,
                      fold_bn_affine)
-from ..ops import gradjoin
+from ..ops import bnfold, gradjoin
 from ..ops.dwconv import joinable
 
 
@@ -75,6 +75,14 @@ class SeparableConvBN(nn.Module):
             return self.pointwise(y, residual=residual)
         # training: the depthwise kernel accumulates the BN statistics of its output in its
         # epilogue (no separate reduce pass over y)
+        if self.training and not self.act_inside and bnfold.ENABLED:
+            # no activation between the depthwise BN and the pointwise conv: the BN is folded
+            # into the conv (scaled weights + bias, ops/bnfold.py) — its output never exists
+            z, stats = self.depthwise(x, relu_in=relu_in, want_stats=True, join=join)
+            pw = self.pointwise
+            y, st2 = bnfold.bn_conv1x1(z, stats, self.dw_bn, pw.conv, want_stats=True,
+                                       dy_sums_zero=pw.bn.training)
+            return pw.bn(y, stats=st2, residual=residual, relu=pw.relu, res_join=res_join)
         if self.training:
             y, stats = self.depthwise(x, relu_in=relu_in, want_stats=True, join=join)
         else:

@@ -20,8 +20,9 @@ from __future__ import annotations
 import os
 
 import torch
+import torch.nn.functional as F
 
-from .common import on_gpu, fused_gpu, ext, deliver_grad, grad_target, flat_view
+from .common import on_gpu, fused_gpu, ext, deliver_grad, grad_target, flat_view, export_impl
 from . import workspace
 from . import gradjoin
 
@@ -393,12 +394,32 @@ def _join_res(ctx, dres):
     return join.take()
 
 
+def eval_coef(bn, device):
+    """fp32 [4, C_phys] (scale, shift, mean, invstd) of an eval-mode BN — bn_finalize's layout
+    in plain tensor ops (traceable): y = x·scale + shift, zero on padding channels."""
+    gamma, beta = bn.phys_params()
+    C, c = beta.shape[0], bn.c
+    mean = bn.running_mean.float().to(device)
+    inv = torch.rsqrt(bn.running_var.float().to(device) + bn.eps)
+    scale = inv * gamma[:c].float().to(device) if gamma is not None else inv
+    shift = beta[:c].float().to(device) - mean * scale
+    pad = (0, C - c)
+    return torch.stack([F.pad(scale, pad), F.pad(shift, pad), F.pad(mean, pad), F.pad(inv, pad)])
+
+
 def batch_norm_act(x, bn, stats=None, residual=None, relu=True, training=True, res_join=None,
                    link=None):
     """act(BN(x) [+ residual]).  ``bn`` is a :class:`models.layers.BatchNorm` (holds γ, β and the
     moving statistics).  ``stats`` may carry Σx, Σx² already accumulated by the producer conv.
     ``res_join`` shares the residual's gradient buffer with its other consumers; ``link``
     (:class:`ResidualLink`) adds x's residual-path gradient to dx in the backward pass."""
+    ex = export_impl()
+    if ex is not None:  # serving trace: eval-mode BN as one affine (+residual, ReLU) pass
+        if training:
+            raise RuntimeError("batch_norm_act: export needs the network in eval mode")
+        coef = bn.__dict__.get("_serve")  # frozen by engine/serving.py
+        return ex.bn_act(x, coef if coef is not None else eval_coef(bn, x.device), residual,
+                         relu)
     # (grad mode is off inside Function.forward: decide here whether a backward will follow)
     need_grad = torch.is_grad_enabled() and (
         x.requires_grad or (residual is not None and residual.requires_grad))

@@ -31,6 +31,16 @@ def ext():
     return _native.ext()
 
 
+# the serving-export lowering while a model is traced (engine/serving.py export_mode), else None
+_EXPORT = [None]
+
+
+def export_impl():
+    """The active export lowering: the ops layer hands each primitive to it instead of launching
+    a kernel (the tracer's tensors are fakes)."""
+    return _EXPORT[0]
+
+
 def compute_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     """The tensor the kernels read for parameter ``p`` (bf16 shadow on GPU, else fp32 master)."""
     lp = getattr(p, "_lowp", None)

@@ -21,7 +21,8 @@ from dataclasses import dataclass
 import torch
 import torch.nn.functional as F
 
-from .common import on_gpu, fused_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view
+from .common import (on_gpu, fused_gpu, ext, compute_weight, grad_target, deliver_grad, flat_view,
+                     export_impl)
 from . import workspace
 from . import streams
 from . import gradjoin
@@ -99,6 +100,9 @@ def conv_fwd(x, w, geom: ConvGeom, bias=None, relu=False, stats=None, out_dtype=
     statistics epilogue).  ``residual`` (shaped like y) is added in the LDS-DMA kernel's epilogue
     before the ReLU (with a bias); problems that kernel does not take add it in one elementwise
     pass afterwards."""
+    ex = export_impl()
+    if ex is not None and stats is None and out_dtype is None:
+        return ex.conv2d(x, w, geom, bias, relu, residual)
     N, H, W, C = x.shape
     K, R, S, Cw = w.shape
     assert C == Cw, f"channel mismatch {C} vs {Cw}"
@@ -304,6 +308,9 @@ class _RowPackFn(torch.autograd.Function):
 
 def row_pack(x, creal, S, sw, pl, Wo, Cp):
     """See :func:`_row_pack`; differentiable when ``x`` requires a gradient."""
+    ex = export_impl()
+    if ex is not None:
+        return ex.row_pack(x, creal, S, sw, pl, Wo, Cp)
     if x.requires_grad and torch.is_grad_enabled():
         return _RowPackFn.apply(x, creal, S, sw, pl, Wo, Cp)
     return _row_pack(x, creal, S, sw, pl, Wo, Cp)
@@ -503,5 +510,15 @@ def conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=False, want_s
     """Differentiable NHWC conv. Returns (y, stats) where stats is fp32 [2, K] (sum, sumsq of y)
     when ``want_stats`` else an empty tensor.  ``join`` (ops.gradjoin.GradJoin) makes dx share one
     buffer with the other consumers of ``x``.  ``residual``: y = act(conv + bias + residual)."""
+    if export_impl() is not None:  # serving trace: inference forward, no statistics
+        sv = layer.__dict__.get("_serve") if layer is not None else None  # frozen (serving.py)
+        if sv is not None:
+            w, b = sv
+        else:
+            w = (layer.compute_weight(x.dtype) if layer is not None
+                 else compute_weight(weight, x.dtype))
+            b = None if bias is None else (layer.compute_bias() if layer is not None
+                                           else bias.detach())
+        return conv_fwd(x, w, geom, bias=b, relu=relu, residual=residual), None
     return _Conv2dFn.apply(x, weight, bias, geom, relu, want_stats, layer, join, residual,
                            res_link)

@@ -15,7 +15,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
+from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad, export_impl
 from .bn import bn_stats
 from . import gradjoin
 from . import workspace
@@ -32,12 +32,12 @@ def ref_dw_fwd(x, w, geom: ConvGeom, bias=None):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
-# TDL_DW_STATS=1: the depthwise tile kernels fuse the neighbouring BNs' statistics (forward
-# Σy, Σy²; dgrad Σg, Σg·x_bn with the ReLU mask applied as x > 0).  Off by default: on
-# Xception-41 b128 (same box, two alternating rounds, scripts/r3_dwab.sh) 2578 / 2577 img/s on vs
-# 2595 / 2604 off — the epilogue's extra x read, LDS reduction and atomics cost what the BNs'
-# reduce passes did (the per-kernel checks stay in tests/test_kernels_gpu.py)
-DW_STATS = os.environ.get("TDL_DW_STATS", "0") == "1"
+# TDL_DW_STATS (default 1): the depthwise tile kernels fuse the neighbouring BNs' statistics
+# (forward Σy, Σy²; dgrad Σg, Σg·x_bn with the ReLU mask applied as x > 0) instead of the BNs'
+# reduce passes.  Round 3 (8-channel lanes) it lost: 2578 / 2577 img/s on vs 2595 / 2604 off;
+# round 4 (LDS-DMA staging, 4-channel lanes) it wins narrowly: Xception-41 299² b128 2763 / 2765
+# on vs 2761 / 2755 off (same box, alternating runs)
+DW_STATS = os.environ.get("TDL_DW_STATS", "1") == "1"
 
 
 def _fusable_relu_in(x, R, S):
@@ -185,6 +185,11 @@ def depthwise_conv2d(x, weight, bias=None, geom: ConvGeom = ConvGeom(), relu=Fal
     in front of each separable conv, core/xception.py:90-110); the backward masks dx by x > 0.
     ``want_stats``: also return fp32 [2, C] = (Σy, Σy²) of the stored output for the BN that
     normalises it (fused into the stride-1 tile kernel's epilogue) — returns ``(y, stats)``."""
+    ex = export_impl()
+    if ex is not None and not want_stats:
+        w = compute_weight(weight, x.dtype)
+        return ex.dwconv2d(x, w, None if bias is None else bias.detach().float(), geom, relu,
+                           relu_in)
     if relu_in and on_gpu(x) and not _fusable_relu_in(x, weight.shape[0], weight.shape[1]):
         if join is not None:
             raise ValueError("depthwise_conv2d: a join on x needs the fused input ReLU "

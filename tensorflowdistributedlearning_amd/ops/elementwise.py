@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import torch
 
-from .common import on_gpu, ext
+from .common import on_gpu, ext, export_impl
 
 
 class _AddReluFn(torch.autograd.Function):
@@ -43,20 +43,30 @@ class _AddReluFn(torch.autograd.Function):
         return g, (g if ctx.has_b else None), None
 
 
+def _add_act(a, b, act):
+    ex = export_impl()
+    if ex is not None:
+        return ex.add_act(a, b, act)
+    return _AddReluFn.apply(a, b, act)
+
+
 def add_relu(a, b):
-    return _AddReluFn.apply(a, b, True)
+    return _add_act(a, b, True)
 
 
 def relu(a):
-    return _AddReluFn.apply(a, None, True)
+    return _add_act(a, None, True)
 
 
 def add(a, b):
-    return _AddReluFn.apply(a, b, False)
+    return _add_act(a, b, False)
 
 
 def sigmoid_threshold(logits, threshold=0.5):
     """(probabilities fp32, prediction {0,1} fp32)."""
+    ex = export_impl()
+    if ex is not None:
+        return ex.sigmoid_threshold(logits, threshold)
     if on_gpu(logits):
         prob = torch.empty(logits.shape, device=logits.device, dtype=torch.float32)
         pred = torch.empty_like(prob)

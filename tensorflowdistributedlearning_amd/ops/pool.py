@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from .common import on_gpu, ext
+from .common import on_gpu, ext, export_impl
 from . import gradjoin
 from . import workspace
 
@@ -80,6 +80,9 @@ class _MaxPoolFn(torch.autograd.Function):
 
 
 def max_pool2d(x, k, s, pad):
+    ex = export_impl()
+    if ex is not None:
+        return ex.max_pool2d(x, k, s, tuple(pad))
     return _MaxPoolFn.apply(x, k, s, tuple(pad))
 
 
@@ -125,4 +128,7 @@ class _GAPFn(torch.autograd.Function):
 def global_avg_pool(x, keepdims=False, join=None):
     """Mean over H, W.  ``join``: gradient join of x (ops/gradjoin.py; the backward adds the
     join buffer's earlier contributions, C % 8 == 0 on the GPU)."""
+    ex = export_impl()
+    if ex is not None:
+        return ex.avg_pool(x, keepdims)
     return _GAPFn.apply(x, keepdims, join)

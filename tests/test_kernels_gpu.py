@@ -853,6 +853,43 @@ def test_conv_m32_kloop(gpu, shape):
     assert rel_err(s1, s0) < 1e-5
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8, 28, 128, 512, 1, 1, (0, 0, 0, 0)),
+                                   (8, 14, 256, 256, 3, 1, (1, 1, 1, 1)),
+                                   (8, 28, 256, 256, 3, 2, (0, 1, 0, 1)),
+                                   (8, 19, 728, 728, 1, 1, (0, 0, 0, 0)),
+                                   (3, 9, 64, 200, 3, 1, (1, 1, 1, 1))])
+@pytest.mark.parametrize("bias", [False, True])
+def test_conv_producer_consumer_fwd(gpu, shape, bias):
+    """Wave-specialised producer/consumer forward (conv_pc.hip, TDL_CONV_PC) vs the default
+    LDS-DMA forward: same LDS images, fragment order and epilogue — outputs bit-identical,
+    fused BN statistics equal up to the atomic order; ragged 728-channel 1×1, strided 3×3,
+    partial tiles and column-ragged output channels included."""
+    N, H, Cin, K, k, s, pad = shape
+    g = C.ConvGeom((s, s), pad, (1, 1))
+    torch.manual_seed(9)
+    x = torch.randn(N, H, H, Cin).bfloat16().to(gpu)
+    w = (torch.randn(K, k, k, Cin) * 0.05).bfloat16().to(gpu)
+    b = torch.randn(K, device=gpu) if bias else None
+    outs = []
+    ext().conv_set_glds_mode(2)
+    try:
+        for pc in (0, 1, 2):  # conv_glds, 2 producer waves, 4 producer waves
+            ext().conv_set_pc(pc)
+            st = torch.zeros(2, K, device=gpu)
+            y = C.conv_fwd(x, w, g, bias=b, relu=bias, stats=st)
+            outs.append((y, st))
+    finally:
+        ext().conv_set_pc(-1)
+        ext().conv_set_glds_mode(-1)
+    y0, s0 = outs[0]
+    ref = C.ref_conv_fwd(x.cpu(), w.cpu(), g, None if b is None else b.cpu())
+    for y1, s1 in outs[1:]:
+        assert rel_err(y1, torch.relu(ref) if bias else ref) < 1e-2
+        assert torch.equal(y0, y1)
+        assert rel_err(s1, s0) < 1e-5
+
+
 def test_row_packed_stem_gpu(gpu):
     """The row-pack HIP kernel = its CPU oracle (bitwise), and the packed 7×7/s2 stem
     (RowPackedConv2d) = the plain conv on the 8-channel padded input: forward and dW on the GPU."""

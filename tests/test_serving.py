@@ -1,0 +1,192 @@
+"""Servable export (engine/serving.py): the eval network behind the serving signature as a
+``torch.export`` program — the reference's BestExporter SavedModel (/root/reference/model.py:
+189-204).  CPU: the tdl:: operators run their fp32 references; GPU: the gfx950 kernels."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from tensorflowdistributedlearning_amd import models
+from tensorflowdistributedlearning_amd.engine import serving
+from tensorflowdistributedlearning_amd.models.deeplab import DeepLabResNet
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _train_a_little(net, x, steps=2):
+    """A few train-mode forwards so the BN moving statistics are not the identity — with decay 0
+    they become the last batch's statistics, so the eval network stays normalised (random-init
+    eval activations otherwise grow layer by layer and any rounding difference is amplified)."""
+    from tensorflowdistributedlearning_amd.models.layers import BatchNorm
+    for m in net.modules():
+        if isinstance(m, BatchNorm):
+            m.decay = 0.0
+    net.train()
+    with torch.no_grad():
+        for _ in range(steps):
+            net(x)
+    net.eval()
+
+
+def _eager(net, x, task, dtype=torch.float32):
+    with torch.no_grad():
+        return serving.ServingModule(net, task, dtype)(x)
+
+
+def _ops(ep):
+    return {str(n.target) for n in ep.graph.nodes if n.op == "call_function"}
+
+
+@pytest.mark.parametrize("kind", ["native", "portable"])
+def test_classifier_export_matches_eager_with_dynamic_batch(tmp_path, kind):
+    torch.manual_seed(0)
+    net = models.build("resnet18", num_classes=10, in_channels=3)
+    _train_a_little(net, torch.randn(4, 32, 32, 3))
+    path = str(tmp_path / "m.pt2")
+    ep = serving.export_serving(net, torch.randn(2, 32, 32, 3), path, "classification", kind)
+    assert net.training is False  # mode restored (it was eval)
+    assert len(ep.state_dict) == 0  # folded weights are constants; raw parameters not kept
+    m = serving.load_serving(path)
+    x = torch.randn(5, 32, 32, 3)  # another batch size than the trace's
+    got, want = m(x), _eager(net, x, "classification")
+    assert set(got) == {"logits", "probabilities", "classes"}
+    torch.testing.assert_close(got["logits"], want["logits"], rtol=1e-4, atol=1e-4)
+    assert torch.equal(got["classes"], want["classes"])
+    meta = json.load(open(str(tmp_path / "m.json")))
+    assert meta["inputs"]["images"] == [None, 32, 32, 3] and meta["kind"] == kind
+
+
+def test_native_program_is_tdl_operators_portable_is_aten(tmp_path):
+    torch.manual_seed(0)
+    net = models.build("resnet18", num_classes=10, in_channels=3).eval()
+    x = torch.randn(2, 32, 32, 3)
+    nat = serving.export_serving(net, x, str(tmp_path / "n.pt2"), "classification", "native")
+    por = serving.export_serving(net, x, str(tmp_path / "p.pt2"), "classification", "portable")
+    n_ops, p_ops = _ops(nat), _ops(por)
+    assert {"tdl.conv2d.default", "tdl.max_pool2d.default", "tdl.avg_pool.default"} <= n_ops
+    # ResNet-18: stem + 16 body convs + 3 projection shortcuts + fc, every BN folded
+    assert sum(str(n.target) == "tdl.conv2d.default" for n in nat.graph.nodes) == 21
+    assert not any(o.startswith("tdl.") for o in p_ops)
+    assert "aten.conv2d.default" in p_ops or "aten.convolution.default" in p_ops
+
+
+def test_deeplab_export_matches_eager(tmp_path):
+    torch.manual_seed(1)
+    net = DeepLabResNet(in_channels=2, base_depth=32, input_shape=(64, 64), n_blocks=(1, 1, 1),
+                        block_widths=(16, 24, 32))
+    _train_a_little(net, torch.randn(2, 64, 64, 2))
+    x = torch.randn(3, 64, 64, 2)
+    for kind in ("native", "portable"):
+        path = str(tmp_path / f"dl_{kind}.pt2")
+        serving.export_serving(net, x[:2], path, "segmentation", kind)
+        got, want = serving.load_serving(path)(x), _eager(net, x, "segmentation")
+        assert set(got) == {"probabilities", "mask"}
+        assert got["probabilities"].shape == (3, 64, 64, 1)
+        torch.testing.assert_close(got["probabilities"], want["probabilities"], rtol=1e-3,
+                                   atol=1e-4)
+
+
+def test_xception_export_matches_eager(tmp_path):
+    torch.manual_seed(2)
+    net = models.build("xception41", num_classes=7, in_channels=3)
+    _train_a_little(net, torch.randn(2, 64, 64, 3), steps=1)
+    x = torch.randn(2, 64, 64, 3)
+    path = str(tmp_path / "xc.pt2")
+    ep = serving.export_serving(net, x, path, "classification", "native")
+    assert "tdl.dwconv2d.default" in _ops(ep)
+    got, want = serving.load_serving(path)(x), _eager(net, x, "classification")
+    torch.testing.assert_close(got["logits"], want["logits"], rtol=1e-3, atol=1e-3)
+
+
+def test_portable_program_loads_without_the_package(tmp_path):
+    torch.manual_seed(3)
+    net = models.build("resnet18", num_classes=4, in_channels=3).eval()
+    x = torch.randn(2, 32, 32, 3)
+    path = str(tmp_path / "p.pt2")
+    serving.export_serving(net, x, path, "classification", "portable")
+    want = _eager(net, x, "classification")["logits"]
+    torch.save(x, str(tmp_path / "x.pt"))
+    code = ("import sys, torch; m = torch.export.load(sys.argv[1]).module(); "
+            "x = torch.load(sys.argv[2], weights_only=True); y = m(x)['logits']; "
+            "assert not any(k.startswith('tensorflowdistributedlearning_amd') for k in sys.modules); "
+            "torch.save(y, sys.argv[3])")
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    subprocess.run([sys.executable, "-c", code, path, str(tmp_path / "x.pt"),
+                    str(tmp_path / "y.pt")], check=True, cwd=str(tmp_path), env=env,
+                   timeout=300)
+    got = torch.load(str(tmp_path / "y.pt"), weights_only=True)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4)
+
+
+def test_export_refuses_training_bn_and_bad_kind(tmp_path):
+    net = models.build("resnet18", num_classes=4, in_channels=3)
+    with pytest.raises(ValueError):
+        serving.export_serving(net, torch.randn(2, 32, 32, 3), str(tmp_path / "a.pt2"),
+                               "classification", "onnx")
+    with pytest.raises(ValueError):
+        serving.ServingModule(net, "detection")
+
+
+def test_model_best_export_writes_servable_bundle_and_cli_export(tmp_path, capsys):
+    from tensorflowdistributedlearning_amd.model import Model
+    from tensorflowdistributedlearning_amd.__main__ import main
+    kw = dict(arch="resnet18", num_classes=4, image_size=32, synthetic=True, device="cpu",
+              n_gpus=1, n_fold=2, max_folds=1, lr=0.05, export_format="both")
+    m = Model(str(tmp_path / "r18"), "", save_checkpoints_steps=3, save_best=1, **kw)
+    m.train(64, None, 16, 3)
+    root = tmp_path / "r18" / "fold0" / "export" / "best_exporter"
+    (bundle,) = [root / d for d in os.listdir(root)]
+    cfg = json.load(open(bundle / "config.json"))
+    assert cfg["serving"] == {"native": "model.pt2", "portable": "model_portable.pt2"}
+    assert cfg["signature"]["outputs"] == ["logits", "probabilities", "classes"]
+    x = torch.randn(3, 32, 32, 3)
+    a = serving.load_serving(str(bundle / "model.pt2"))(x)["logits"]
+    b = serving.load_serving(str(bundle / "model_portable.pt2"))(x)["logits"]
+    torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
+    out = str(tmp_path / "cli.pt2")
+    main(["export", "--model-dir", str(tmp_path / "r18"), "--arch", "resnet18",
+          "--num-classes", "4", "--image-size", "32", "--device", "cpu", "--n-fold", "2",
+          "--kind", "portable", "--out", out])
+    assert "wrote" in capsys.readouterr().out
+    c = serving.load_serving(out)(x)["logits"]
+    assert c.shape == (3, 4) and torch.isfinite(c).all()
+
+
+# ----------------------------------------------------------------------------------------------
+# GPU: the exported program runs the gfx950 kernels
+# ----------------------------------------------------------------------------------------------
+
+@pytest.mark.gpu
+def test_native_export_on_gpu_matches_eager_kernels(tmp_path, gpu, monkeypatch):
+    from tensorflowdistributedlearning_amd.models.params import FlatParams
+    # the eager reference takes the same (torch.cat) ASPP head as the trace: the concat-free head
+    # runs its branches' BN unfolded, a different bf16 rounding that random-init eval BN amplifies
+    monkeypatch.setattr(DeepLabResNet, "concat_free", False)
+    torch.manual_seed(4)
+    dev = torch.device("cuda", 0)
+    for arch, shape, task in (("resnet50", (4, 64, 64, 3), "classification"),
+                              ("deeplab", (4, 101, 101, 2), "segmentation")):
+        net = (models.build(arch, num_classes=10, in_channels=3) if arch != "deeplab"
+               else DeepLabResNet(in_channels=2)).to(dev)
+        net._tdl_flat = FlatParams(net, dev, lowp_dtype=torch.bfloat16, with_grad=False)
+        x = torch.randn(*shape, device=dev)
+        _train_a_little(net, x.bfloat16())
+        path = str(tmp_path / f"{arch}.pt2")
+        ep = serving.export_serving(net, x[:2], path, task, "native")
+        assert "tdl.conv2d.default" in _ops(ep)
+        m = serving.load_serving(path)
+        got = m(x)
+        want = _eager(net, x, task, torch.bfloat16)
+        k = "logits" if task == "classification" else "probabilities"
+        # same kernels, same folded weights (the eval BN coefficients of the unfolded
+        # pre-activation BNs come from tensor ops here, from the finalize kernel eagerly)
+        d = (got[k].float() - want[k].float()).abs()
+        assert d.max().item() < 0.05 and d.mean().item() < 2e-3, (d.max().item(), d.mean().item())
+        # the portable (ATen) lowering of the same network agrees to bf16 rounding
+        serving.export_serving(net, x[:2], str(tmp_path / "p.pt2"), task, "portable")
+        por = serving.load_serving(str(tmp_path / "p.pt2"))(x)
+        dp = (por[k].float() - got[k].float()).abs()
+        assert dp.mean().item() < 0.02, (dp.max().item(), dp.mean().item())

@@ -925,7 +925,8 @@ def _moving_stats_within_noise(a, b, c, make_trainer, x, y):
     """One training-mode step of models a, b and c (b and c identical): the moving statistics of
     a vs b differ by no more than b vs c do.  Batch statistics are summed with float atomics
     (non-deterministic order), and on a 4-image batch the last BNs of this 60-BN network move by
-    ~5 % run to run from that alone (tools/dbg_det.py), so a fixed tolerance is no test."""
+    ~5 % run to run from that alone (measured with two identical models; deterministic mode,
+    test_deterministic_mode_bitwise_repeatable, removes it), so a fixed tolerance is no test."""
     trs = [make_trainer(m) for m in (a, b, c)]
     for t in trs:
         t.train_mode = True
