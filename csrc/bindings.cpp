@@ -1,6 +1,8 @@
 // Python bindings of the gfx950 kernels (torch tensors in, launches on the current HIP stream).
 // Kernels themselves live in csrc/kernels/*.hip and see only raw pointers (no torch headers there).
 #include <torch/extension.h>
+
+#include <cstring>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPCachingAllocator.h>
 
@@ -474,6 +476,42 @@ void bn_finalize(c10::optional<Tensor> stats, Tensor coef, c10::optional<Tensor>
 // fp8 side output (delayed scaling): amax_ring is fp32[3, AMAX_SLOT]; slot `phase` holds the previous
 // step's |y|max (scale source), slot phase+1 accumulates this step's, slot phase+2 is cleared
 // for the next step — no separate memset launch.
+// training BN folded into its 1×1 consumer conv (ops/bnfold.py): W' = W·diag(coef[0]) and
+// bias = W·coef[1] (+ bias_in) in one launch
+void bn_fold_weight(Tensor w, Tensor coef, Tensor wout, c10::optional<Tensor> bias_in,
+                    Tensor bias_out) {
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && wout.is_contiguous() &&
+                  w.scalar_type() == wout.scalar_type() && w.numel() == wout.numel(),
+              "bn_fold_weight: w / wout");
+  const bool bf16 = w.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf16 || w.scalar_type() == torch::kFloat32, "bn_fold_weight: bf16 or fp32 weight");
+  CHECK_T(coef, torch::kFloat32);
+  CHECK_T(bias_out, torch::kFloat32);
+  const int64_t K = w.size(0), C = w.size(-1);
+  TORCH_CHECK(w.numel() == K * C, "bn_fold_weight: a 1x1 weight [K, 1, 1, C]");
+  TORCH_CHECK(coef.dim() == 2 && coef.size(0) >= 2 && coef.size(1) >= C, "bn_fold_weight: coef");
+  TORCH_CHECK(bias_out.numel() == K, "bn_fold_weight: bias_out [K]");
+  const float* bi = nullptr;
+  if (bias_in.has_value() && bias_in->defined()) {
+    CHECK_T(*bias_in, torch::kFloat32);
+    TORCH_CHECK(bias_in->numel() == K, "bn_fold_weight: bias_in [K]");
+    bi = bias_in->data_ptr<float>();
+  }
+  bn_fold_weight_launch(w.data_ptr(), bf16, coef.data_ptr<float>(), (int)K, (int)C,
+                        (int)coef.size(1), wout.data_ptr(), bi, bias_out.data_ptr<float>(),
+                        stream());
+}
+
+// dw[k][c] *= a[c] (fp32, in place)
+void scale_cols(Tensor dw, Tensor a) {
+  CHECK_T(dw, torch::kFloat32);
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == torch::kFloat32 && a.stride(-1) == 1,
+              "scale_cols: a fp32 HIP vector");
+  const int64_t C = dw.size(-1);
+  TORCH_CHECK(a.numel() >= C, "scale_cols: a shorter than the columns");
+  scale_cols_launch(dw.data_ptr<float>(), a.data_ptr<float>(), dw.numel(), (int)C, stream());
+}
+
 void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu,
               c10::optional<Tensor> y8, c10::optional<Tensor> amax_ring, int64_t phase,
               c10::optional<Tensor> scale_out, c10::optional<Tensor> mask) {
@@ -1155,6 +1193,40 @@ struct PyLoader {
   }
 };
 
+// CRC32C (Castagnoli) of a byte string — the TFRecord framing of the summary event files
+// (engine/summary.py); table-driven, slicing by 8 (the pure-Python loop cost ≈1 ms per 10 KB
+// image summary, several ms per summary step on the training thread)
+static uint32_t g_crc_tab[8][256];
+static void crc32c_init() {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? 0x82F63B78u : 0u);
+    g_crc_tab[0][i] = c;
+  }
+  for (uint32_t i = 0; i < 256; ++i)
+    for (int t = 1; t < 8; ++t)
+      g_crc_tab[t][i] = (g_crc_tab[t - 1][i] >> 8) ^ g_crc_tab[0][g_crc_tab[t - 1][i] & 0xFF];
+}
+uint32_t crc32c(const std::string& data) {
+  static const bool init = (crc32c_init(), true);
+  (void)init;
+  const uint8_t* p = reinterpret_cast<const uint8_t*>(data.data());
+  size_t n = data.size();
+  uint32_t crc = 0xFFFFFFFFu;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    v ^= crc;
+    crc = g_crc_tab[7][v & 0xFF] ^ g_crc_tab[6][(v >> 8) & 0xFF] ^ g_crc_tab[5][(v >> 16) & 0xFF] ^
+          g_crc_tab[4][(v >> 24) & 0xFF] ^ g_crc_tab[3][(v >> 32) & 0xFF] ^
+          g_crc_tab[2][(v >> 40) & 0xFF] ^ g_crc_tab[1][(v >> 48) & 0xFF] ^ g_crc_tab[0][v >> 56];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) crc = g_crc_tab[0][(crc ^ *p++) & 0xFF] ^ (crc >> 8);
+  return crc ^ 0xFFFFFFFFu;
+}
+
 Tensor png_decode_gray(const std::string& path) {
   tdl_rt::GrayImage g = tdl_rt::load_png_gray(path);
   Tensor t = torch::empty({g.h, g.w}, torch::kFloat32);
@@ -1301,6 +1373,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_halo_mode", &conv_set_halo_mode,
         "halo-tiled stride-1 conv: -1 environment (TDL_HALO, default 1), 0 off, 1 default "
         "selection, 2 every eligible problem regardless of size (tests)");
+  m.def("bn_fold_weight", &bn_fold_weight, py::arg("w"), py::arg("coef"), py::arg("wout"),
+        py::arg("bias_in"), py::arg("bias_out"));
+  m.def("scale_cols", &scale_cols, py::arg("dw"), py::arg("a"));
   m.def("conv_set_pc", &conv_set_pc, "wave-specialised producer/consumer forward (-1: env)");
   m.def("conv_set_m32", &conv_set_m32, "32x32x16-MFMA K loop for KC-operand LDS-DMA convs (-1: env)");
   m.def("conv_m32", &conv_m32);
@@ -1343,6 +1418,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("height", [](PyLoader& l) { return l.impl->height(); })
       .def_property_readonly("width", [](PyLoader& l) { return l.impl->width(); });
   m.def("png_decode_gray", &png_decode_gray);
+  m.def("crc32c", [](py::bytes b) { return crc32c(std::string(b)); });
   m.def("augment_one", &augment_one, py::arg("img"), py::arg("mask"), py::arg("transpose"),
         py::arg("hflip"), py::arg("vflip"), py::arg("angle"), py::arg("tx"), py::arg("ty"),
         py::arg("pad"), py::arg("brightness") = 0.0, py::arg("crop") = false,

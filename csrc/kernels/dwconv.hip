@@ -8,6 +8,7 @@
 namespace tdl {
 namespace {
 using convk::OOB;
+using convk::bload16;
 using convk::make_rsrc;
 using convk::rsrc_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -291,6 +292,68 @@ __global__ void __launch_bounds__(NT) dw_dgrad_rows(DwArgs a, int lanes_c, int r
     if (a.mask_x) mask_pos(acc, a.mask_x + ((long)row * a.W + w) * a.C + c);
     if (a.dadd) add8(acc, a.dadd + ((long)row * a.W + w) * a.C + c);
     *(uint4*)(xrow + (long)w * a.C) = pack8(acc);
+  }
+}
+
+// Stride-2 3×3 input gradient (Xception's strided separable convs, dilation 1): the forward reads
+// x[2t − p + r], so dx row h = 2m − p takes dy rows m (tap 0) and m−1 (tap 2) and row h+1 takes
+// dy row m (tap 1) — likewise for columns.  A lane owns one 2×2 dx block × 8 channels: it reads the
+// 2×2 dy window (rows m−1, m × columns n−1, n) once and does the 9 FMAs of the 4 outputs (4 + 2 +
+// 2 + 1 taps), no parity tests or divisions per pixel.  Loads are range-checked buffer loads
+// (outside the image → zeros) issued together; the row kernel's per-tap branches around loads
+// serialised them (4 dgrads, 1.78 ms of the Xception-41 b128 step,
+// profiles/r04_xception41_b128_fold_step_breakdown.txt).
+__global__ void __launch_bounds__(NT) dw_dgrad_s2_kernel(const bf16_t* __restrict__ dy,
+                                                         const bf16_t* __restrict__ wt,
+                                                         bf16_t* __restrict__ dx,
+                                                         const bf16_t* __restrict__ mask_x,
+                                                         const bf16_t* __restrict__ dadd, int N,
+                                                         int H, int W, int C, int Ho, int Wo,
+                                                         int ph, int pw, int MG, int NG) {
+  const int cv = C / 8;
+  const long total = (long)N * MG * NG * cv;
+  const rsrc_t rdy = make_rsrc(dy, (uint32_t)((long)N * Ho * Wo * C * 2));
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const int c = (int)(t % cv) * 8;
+    long q = t / cv;
+    const int ng = (int)(q % NG);
+    q /= NG;
+    const int mg = (int)(q % MG);
+    const int n = (int)(q / MG);
+    // dx rows h0 = 2·mg − ph (even u = h + ph), h0 + 1; columns w0 = 2·ng − pw, w0 + 1
+    const int h0 = 2 * mg - ph, w0 = 2 * ng - pw;
+    auto off = [&](int tm, int tn) -> uint32_t {
+      return ((unsigned)tm < (unsigned)Ho && (unsigned)tn < (unsigned)Wo)
+                 ? (uint32_t)((((long)n * Ho + tm) * Wo + tn) * C + c) * 2u
+                 : OOB;
+    };
+    const uint4 g11 = bload16(rdy, off(mg, ng)), g10 = bload16(rdy, off(mg, ng - 1));
+    const uint4 g01 = bload16(rdy, off(mg - 1, ng)), g00 = bload16(rdy, off(mg - 1, ng - 1));
+    float w9[9][8];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) unpack8(*(const uint4*)(wt + (long)k * C + c), w9[k]);
+    float a11[8], a10[8], a01[8], a00[8];
+    unpack8(g11, a11);
+    unpack8(g10, a10);
+    unpack8(g01, a01);
+    unpack8(g00, a00);
+    float o[4][8];  // (h0,w0) (h0,w1) (h1,w0) (h1,w1)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[0][j] = a11[j] * w9[0][j] + a10[j] * w9[2][j] + a01[j] * w9[6][j] + a00[j] * w9[8][j];
+      o[1][j] = a11[j] * w9[1][j] + a01[j] * w9[7][j];
+      o[2][j] = a11[j] * w9[3][j] + a10[j] * w9[5][j];
+      o[3][j] = a11[j] * w9[4][j];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int h = h0 + (e >> 1), w = w0 + (e & 1);
+      if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+      const long p = (((long)n * H + h) * W + w) * C + c;
+      if (mask_x) mask_pos(o[e], mask_x + p);
+      if (dadd) add8(o[e], dadd + p);
+      *(uint4*)(dx + p) = pack8(o[e]);
+    }
   }
 }
 
@@ -1028,6 +1091,16 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(dw_slide_kernel<true>, grid, dim3(NT), 0, st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.lanes_c, g.rpp, g.seg, 0,
                        a.mask_x, a.dadd);
+  } else if (a.C % 8 == 0 && a.R == 3 && a.S == 3 && a.sh == 2 && a.sw == 2 && a.dh == 1 &&
+             a.dwl == 1 && a.ph >= 0 && a.pw >= 0 && a.ph <= 2 && a.pw <= 2 &&
+             (long)a.N * a.Ho * a.Wo * a.C * 2 < (1L << 31) - 64 &&
+             getenv("TDL_DW_S2_OFF") == nullptr) {
+    // stride-2 3×3: one lane per 2×2 dx block (groups cover rows −ph … H−1 and columns −pw … W−1)
+    const int MG = (a.H + a.ph + 1) / 2, NG = (a.W + a.pw + 1) / 2;
+    const long work = (long)a.N * MG * NG * (a.C / 8);
+    hipLaunchKernelGGL(dw_dgrad_s2_kernel, dim3((unsigned)std::min<long>(65536, cdiv(work, NT))),
+                       dim3(NT), 0, st, a.dy, a.w, a.out, a.mask_x, a.dadd, a.N, a.H, a.W, a.C,
+                       a.Ho, a.Wo, a.ph, a.pw, MG, NG);
   } else if (a.C % 8 == 0 && a.R * a.S == 9) {
     const RowGeom g = row_geom(a.C / 8);
     dim3 grid((unsigned)(a.N * a.H), (unsigned)cdiv(a.C / 8, g.lanes_c));

@@ -103,6 +103,10 @@ void conv_set_glds_mode(int mode);  // -1: environment / default
 // override (-1: environment)
 int conv_m32();
 void conv_set_m32(int on);
+// training BN folded into its 1×1 consumer (bnfold.hip)
+void bn_fold_weight_launch(const void* w, bool bf16, const float* coef, int K, int C, int ldcoef,
+                           void* wout, const float* bias_in, float* bias_out, hipStream_t st);
+void scale_cols_launch(float* dw, const float* a, long n, int C, hipStream_t st);
 int conv_pc();
 bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st);
 void conv_set_pc(int on);

@@ -32,7 +32,26 @@ for _i in range(256):
     _TABLE.append(_c)
 
 
+def _native_crc():
+    try:
+        from .. import _native
+        return _native.load().crc32c
+    except Exception:  # noqa: BLE001 — no extension: the Python table loop below
+        return None
+
+
+_NATIVE_CRC = [None, False]
+
+
 def crc32c(data: bytes) -> int:
+    if not _NATIVE_CRC[1]:
+        _NATIVE_CRC[0], _NATIVE_CRC[1] = _native_crc(), True
+    if _NATIVE_CRC[0] is not None:
+        return _NATIVE_CRC[0](bytes(data))
+    return crc32c_py(data)
+
+
+def crc32c_py(data: bytes) -> int:
     crc = 0xFFFFFFFF
     for b in data:
         crc = _TABLE[(crc ^ b) & 0xFF] ^ (crc >> 8)

@@ -38,6 +38,7 @@ model reads ``self.block_type`` (default "bottleneck") — D19; ``block_type`` k
 """
 from __future__ import annotations
 
+import contextlib
 import functools
 import json
 import math
@@ -399,16 +400,18 @@ class Model:
                            step)
                 _image_summaries(tw, "train", x, yy, out, self.threshold, step)
             if step % self.save_checkpoints_steps == 0 or step == steps:
-                if main:
-                    saver.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
-                               {"config": self.config()})
-                eval_result = self._evaluate(net, ev_imgs, ev_masks, batch * 2, device, ctx,
-                                             ew if main else None, step)
+                with clock.paused():
+                    if main:
+                        saver.save(fold_dir, step, net, trainer.optimizer,
+                                   self.keep_checkpoint_max, {"config": self.config()})
+                    eval_result = self._evaluate(net, ev_imgs, ev_masks, batch * 2, device, ctx,
+                                                 ew if main else None, step)
                 eval_result["global_step"] = step
                 if main:
                     ew.scalars({k: v for k, v in eval_result.items() if k != "global_step"}, step)
                     if exporter is not None:
-                        exporter.maybe_export(net, eval_result, step)
+                        with clock.paused():
+                            exporter.maybe_export(net, eval_result, step)
         if step == start and start > 0:  # already trained: evaluate the restored model
             eval_result = self._evaluate(net, ev_imgs, ev_masks, batch * 2, device, ctx)
             eval_result["global_step"] = step
@@ -510,15 +513,17 @@ class Model:
                             "global_step/sec": (step - start) / max(time.time() - t0, 1e-9)},
                            step)
             if step % self.save_checkpoints_steps == 0 or step == steps:
-                if main:
-                    saver.save(fold_dir, step, net, trainer.optimizer, self.keep_checkpoint_max,
-                               {"config": self.config()})
-                eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
+                with clock.paused():
+                    if main:
+                        saver.save(fold_dir, step, net, trainer.optimizer,
+                                   self.keep_checkpoint_max, {"config": self.config()})
+                    eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
                 eval_result["global_step"] = step
                 if main:
                     ew.scalars({k: v for k, v in eval_result.items() if k != "global_step"}, step)
                     if exporter is not None:
-                        exporter.maybe_export(net, eval_result, step)
+                        with clock.paused():
+                            exporter.maybe_export(net, eval_result, step)
         if step == start and start > 0:
             eval_result = self._evaluate_cls(net, te, batch * 2, device, ctx, dtype)
             eval_result["global_step"] = step
@@ -792,7 +797,8 @@ class _Stepper:
 class _StepClock:
     """Steady-state step time of a fold loop: wall clock between the end of step start+10 (after
     the graph capture and the caches warmed up) and the last step, with one device sync at
-    each end — everything the loop does per step (loader, step, metrics, summaries) included."""
+    each end — everything the loop does per step (loader, step, metrics, summaries) included,
+    the checkpoint + evaluation passes (:meth:`paused`; reported by their own metrics) not."""
 
     WARM = 10
 
@@ -800,6 +806,20 @@ class _StepClock:
         self.device = device
         self.mark = start + self.WARM
         self.t0 = None
+        self.off = 0.0
+
+    @contextlib.contextmanager
+    def paused(self):
+        if self.t0 is None:
+            yield
+            return
+        self._sync()
+        t = time.perf_counter()
+        try:
+            yield
+        finally:
+            self._sync()
+            self.off += time.perf_counter() - t
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -814,4 +834,4 @@ class _StepClock:
         if self.t0 is None or step <= self.mark:
             return None
         self._sync()
-        return (time.perf_counter() - self.t0) * 1e3 / (step - self.mark)
+        return (time.perf_counter() - self.t0 - self.off) * 1e3 / (step - self.mark)

@@ -26,7 +26,7 @@ import os
 
 import torch
 
-from .common import on_gpu, fused_gpu, grad_target, deliver_grad, flat_view
+from .common import on_gpu, fused_gpu, grad_target, deliver_grad, ext
 from . import streams
 from . import workspace
 from .bn import (bn_stats, bn_finalize, bn_bwd_reduce, bn_bwd_apply, bn_red_xhat, _phys_params,
@@ -37,9 +37,16 @@ ENABLED = os.environ.get("TDL_BN_CONV_FOLD", "1") == "1"
 
 
 def _scaled_weight(layer, dtype, coef):
-    """(W·diag a in the compute dtype, fp32 W·b [+ the conv's own bias]) for this step."""
+    """(W·diag a in the compute dtype, fp32 W·b [+ the conv's own bias]) for this step — one
+    HIP launch on the GPU (csrc/kernels/bnfold.hip)."""
     w = layer.compute_weight(dtype)
     K, C = w.shape[0], w.shape[-1]
+    if on_gpu(w):
+        wf = torch.empty_like(w)
+        bias = torch.empty(K, device=w.device, dtype=torch.float32)
+        bi = layer.compute_bias().float().contiguous() if layer.bias is not None else None
+        ext().bn_fold_weight(w, coef, wf, bi, bias)
+        return wf, bias
     w2 = w.float().reshape(K, C)
     wf = (w2 * coef[0][:C].view(1, C)).to(dtype).reshape(w.shape)
     bias = torch.mv(w2, coef[1][:C].contiguous())
@@ -138,7 +145,10 @@ def _fold_wgrad(layer, weight, dy, z, geom, coef, dy_sums_zero):
     dw = conv_wgrad(dy, z, pshape, geom, out=target if direct else None, bias_grad=s)
     Cp = pshape[-1]
     d2 = dw.view(pshape[0], Cp)
-    d2.mul_(coef[0][:Cp].view(1, Cp))
+    if on_gpu(d2):
+        ext().scale_cols(d2, coef[0])
+    else:
+        d2.mul_(coef[0][:Cp].view(1, Cp))
     if s is not None:
         d2.addr_(s, coef[1][:Cp])
     if direct:

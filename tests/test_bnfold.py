@@ -87,3 +87,26 @@ def test_fold_matches_unfolded_gpu(monkeypatch, gpu):
         # the pointwise BN's moving mean sees W·u with u rounded to bf16 (unfolded) vs W'·z + W·b
         rel = float((ba - bb).abs().max() / bb.abs().max().clamp_min(1e-6))
         assert rel < 1e-2, (n, rel)
+
+
+@pytest.mark.gpu
+def test_fold_weight_kernels_match_torch(gpu):
+    """csrc/kernels/bnfold.hip: W·diag(a) (bf16 and fp32), bias W·b (+ bias_in), and the in-place
+    column scale of the fp32 weight gradient, against PyTorch."""
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    torch.manual_seed(3)
+    K, C, Cp = 300, 728, 736
+    coef = torch.randn(4, Cp, device=gpu)
+    bi = torch.randn(K, device=gpu)
+    for dt in (torch.bfloat16, torch.float32):
+        w = torch.randn(K, 1, 1, C, device=gpu).to(dt)
+        wf, b = torch.empty_like(w), torch.empty(K, device=gpu)
+        ext().bn_fold_weight(w, coef, wf, bi, b)
+        w2 = w.float().view(K, C)
+        torch.testing.assert_close(wf.float().view(K, C), (w2 * coef[0, :C]).to(dt).float(),
+                                   rtol=0, atol=0)
+        torch.testing.assert_close(b, w2 @ coef[1, :C] + bi, rtol=1e-5, atol=1e-4)
+    dw = torch.randn(K, 1, 1, C, device=gpu)
+    ref = dw.view(K, C) * coef[0, :C]
+    ext().scale_cols(dw, coef[0])
+    torch.testing.assert_close(dw.view(K, C), ref, rtol=0, atol=0)

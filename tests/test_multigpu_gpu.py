@@ -143,6 +143,44 @@ def test_dp_ranks_equal_large_batch(tmp_path, gpu):
     assert ((ua - ub).norm() / ub.norm()).item() < 0.03
 
 
+def _dp_graph_worker(rank, outdir, per, steps):
+    """One rank of the DP step captured as a HIP graph with its bucketed RCCL all-reduces."""
+    import torch
+    from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown
+    ctx = init_distributed()
+    tr = _frozen_resnet_trainer(ctx.device, ctx)
+    x, y = _global_batch(ctx.world_size, per)
+    xs = x[rank * per:(rank + 1) * per].to(ctx.device)
+    ys = y[rank * per:(rank + 1) * per].to(ctx.device)
+    tr.capture(xs, ys, warmup=1)  # the warm-up step trains too
+    for _ in range(steps - 1):
+        tr.replay()
+    torch.cuda.synchronize()
+    assert ctx.native.ok
+    torch.save(tr.flat.master.cpu(), os.path.join(outdir, f"g{rank}.pt"))
+    shutdown()
+
+
+@need2
+@pytest.mark.timeout(300)
+def test_dp_graph_capture_n_ranks_matches_eager(tmp_path, gpu):
+    """The data-parallel step captured as one HIP graph per rank — the bucket all-reduces forked
+    into the capture on the comm stream (engine/trainer.py, parallel/bucketer.py) — replayed on
+    2 real ranks: the replicas stay bit-identical and follow the eager DP trajectory (which
+    test_dp_ranks_equal_large_batch ties to the single-GPU large batch)."""
+    n, per, steps = 2, 8, 3
+    launcher.spawn(_dp_graph_worker, n, args=(str(tmp_path), per, steps))
+    launcher.spawn(_dp_worker, n, args=(str(tmp_path), per, steps))
+    g = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(n)]
+    e = torch.load(tmp_path / "m0.pt", weights_only=True)
+    assert torch.equal(g[0], g[1])
+    m0 = _frozen_resnet_trainer(gpu).flat.master.detach().cpu()
+    ug, ue = g[0] - m0, e - m0
+    cos = torch.nn.functional.cosine_similarity(ug, ue, dim=0).item()
+    assert cos > 0.9999, cos
+    assert ((ug - ue).norm() / ue.norm()).item() < 0.01
+
+
 @need2
 @pytest.mark.timeout(300)
 def test_bench_self_spawn_gpus(tmp_path):

@@ -32,3 +32,25 @@ for (hw, c) in [(19, 728), (150, 128), (75, 256), (38, 728)]:
     print(f"{hw}x{hw}x{c}: fwd {tf:7.1f} us ({2 * mb / tf:4.2f} TB/s)  dgrad {td:7.1f} us "
           f"({2 * mb / td:4.2f} TB/s)", flush=True)
     del x, y
+
+# stride-2 input gradients (Xception's strided separable convs, fixed padding 1): the 2x2-block
+# kernel vs the row kernel (TDL_DW_S2_OFF=1), same process
+import os  # noqa: E402
+for (hw, c) in [(150, 128), (75, 256), (38, 728), (19, 1024)]:
+    ho = (hw + 2 - 3) // 2 + 1
+    dy = torch.randn(128, ho, ho, c, device="cuda").bfloat16()
+    w = (torch.randn(3, 3, c, device="cuda") * 0.3).bfloat16()
+    dx = torch.empty(128, hw, hw, c, device="cuda").bfloat16()
+    d = lambda: ext().dwconv_dgrad(dy, w, dx, 2, 2, 1, 1, 1, 1, None)
+    res = {}
+    for off in (1, 0, 1, 0):
+        if off:
+            os.environ["TDL_DW_S2_OFF"] = "1"
+        else:
+            os.environ.pop("TDL_DW_S2_OFF", None)
+        res.setdefault(off, []).append(t(d))
+    mb = (dx.numel() + dy.numel()) * 2 / 1e6
+    a, b = min(res[1]), min(res[0])
+    print(f"s2 dgrad {hw}x{hw}x{c}: rows {a:7.1f} us ({mb / a:4.2f} TB/s) -> 2x2 blocks {b:7.1f} us "
+          f"({mb / b:4.2f} TB/s)", flush=True)
+    del dy, dx
