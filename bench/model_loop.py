@@ -44,8 +44,8 @@ def main():
     ap.add_argument("--images", type=int, default=640)
     ap.add_argument("--out", default=None)
     ap.add_argument("--modes", default="off,auto",
-                    help="comma list of hip_graph modes; 'auto:T:S' = auto with T loader threads "
-                         "and summaries every S steps (0: none)")
+                    help="comma list of hip_graph modes; 'auto:T:S:P' = auto with T loader "
+                         "threads, summaries every S steps (0: none), device prefetch P (1/0)")
     args = ap.parse_args()
     from tensorflowdistributedlearning_amd.model import Model
     res = {}
@@ -55,10 +55,11 @@ def main():
             mode, *rest = spec.split(":")
             threads = int(rest[0]) if rest else 4
             summ = int(rest[1]) if len(rest) > 1 else 20
+            pf = bool(int(rest[2])) if len(rest) > 2 else True
             m = Model(os.path.join(td, f"run_{spec.replace(':', '_')}", "tgs"),
                       os.path.join(td, "data"), n_gpus=1, n_fold=5, max_folds=1, save_best=0,
                       save_checkpoints_steps=10 ** 9, save_summary_steps=summ, hip_graph=mode,
-                      loader_threads=threads)
+                      loader_threads=threads, device_prefetch=pf)
             mode = spec
             r = m.train(X, y, args.batch, args.steps)[0]
             res[mode] = {"steady_ms_per_step": r["steady_ms_per_step"], "hip_graph": r["hip_graph"],

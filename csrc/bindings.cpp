@@ -1165,17 +1165,10 @@ struct PyLoader {
                                        (uint64_t)seed, threads, prefetch, channels,
                                        transformation, cfg, fp32));
   }
-  py::object next() {
-    tdl_rt::Batch b;
-    bool ok;
-    {
-      py::gil_scoped_release nogil;
-      ok = impl->next(b);
-    }
-    if (!ok) return py::none();
+  // pinned host tensors of one batch (no Python objects: runs without the GIL)
+  void to_tensors(const tdl_rt::Batch& b, Tensor& x, Tensor& y, Tensor& ids) {
     const int B = impl->batch(), H = impl->height(), W = impl->width(), C = impl->channels();
     auto opt = torch::TensorOptions().pinned_memory(pin);
-    Tensor x;
     if (impl->fp32()) {
       x = torch::empty({B, H, W, C}, opt.dtype(torch::kFloat32));
       memcpy(x.data_ptr(), b.xf.data(), b.xf.size() * 4);
@@ -1183,12 +1176,25 @@ struct PyLoader {
       x = torch::empty({B, H, W, C}, opt.dtype(torch::kBFloat16));
       memcpy(x.data_ptr(), b.x.data(), b.x.size() * 2);
     }
-    Tensor ids = torch::from_blob(b.ids.data(), {(int64_t)b.ids.size()}, torch::kInt64).clone();
+    ids = torch::from_blob((void*)b.ids.data(), {(int64_t)b.ids.size()}, torch::kInt64).clone();
     if (has_masks) {
-      Tensor y = torch::empty({B, H, W, 1}, opt.dtype(torch::kFloat32));
+      y = torch::empty({B, H, W, 1}, opt.dtype(torch::kFloat32));
       memcpy(y.data_ptr(), b.y.data(), b.y.size() * 4);
-      return py::make_tuple(x, y, ids, b.count);
     }
+  }
+  py::object next() {
+    tdl_rt::Batch b;
+    Tensor x, y, ids;
+    bool ok;
+    {
+      // the pinned copies (≈6 MB per DeepLab batch) run without the GIL too, so a prefetch
+      // thread (data/prefetch.py) overlaps them with the training thread
+      py::gil_scoped_release nogil;
+      ok = impl->next(b);
+      if (ok) to_tensors(b, x, y, ids);
+    }
+    if (!ok) return py::none();
+    if (has_masks) return py::make_tuple(x, y, ids, b.count);
     return py::make_tuple(x, py::none(), ids, b.count);
   }
 };

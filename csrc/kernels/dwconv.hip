@@ -648,14 +648,14 @@ __device__ __forceinline__ uint2 relu4(uint2 v) { return make_uint2(relu2(v.x), 
 
 constexpr int DT_NT = 512;  // tile-kernel workgroup cap (16 channel lanes × ≤ 32 columns)
 
-template <bool FLIP>
+template <bool FLIP, bool RIN>
 __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restrict__ in,
                                                         const bf16_t* __restrict__ wt,
                                                         const float* __restrict__ bias,
                                                         bf16_t* __restrict__ out, int Hi, int Wi,
                                                         int Ho, int Wo, int C, int Ph, int Pw,
                                                         int relu, int tr, int tw, int rg,
-                                                        int tiles_h, int tiles_w, int relu_in,
+                                                        int tiles_h, int tiles_w,
                                                         const bf16_t* __restrict__ mask_x,
                                                         float* __restrict__ stats,
                                                         const bf16_t* __restrict__ bn_x, int ntiles,
@@ -711,9 +711,9 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
   const int r1 = min(min(tr, r0 + rpg), Ho - h0);
   const bool active = !(g >= rg || w >= Wo || c >= C || r0 >= r1);
-  // the fused input ReLU is applied on the LDS read (the DMA stages raw values); a pixel's 64
-  // channels are 16 uint2 slots, this lane's 4 channels slot cl
-  auto ldt = [&](int pix) { const uint2 v = tile2[pix * 16 + cl]; return relu_in ? relu4(v) : v; };
+  // the fused input ReLU (RIN) is applied on the LDS read (the DMA stages raw values); a pixel's
+  // 64 channels are 16 uint2 slots, this lane's 4 channels slot cl
+  auto ldt = [&](int pix) { const uint2 v = tile2[pix * 16 + cl]; return RIN ? relu4(v) : v; };
   if (active) {
   f32x2 wv[9][2], bb[2];
 #pragma unroll
@@ -1038,10 +1038,11 @@ bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
     const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
     const int ntiles = a.N * g.th * g.twn;
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
-    hipLaunchKernelGGL(dw_tile_kernel<false>, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
+    auto kern = a.relu_in ? dw_tile_kernel<false, true> : dw_tile_kernel<false, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
                        st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
-                       g.twn, a.relu_in, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
+                       g.twn, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
                        ntiles, (const bf16_t*)nullptr);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {
@@ -1074,10 +1075,10 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
     const DwTileGeom g = dw_tile_geom(a.H, a.W);
     const int ntiles = a.N * g.th * g.twn;
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
-    hipLaunchKernelGGL(dw_tile_kernel<true>, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
-                       st, a.dy, a.w, nullptr, a.out,
+    hipLaunchKernelGGL((dw_tile_kernel<true, false>), grid, dim3(g.nt),
+                       dw_tile_smem(g, a.stats != nullptr), st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
-                       g.twn, 0, a.mask_x, a.stats, a.bn_x, ntiles, a.dadd);
+                       g.twn, a.mask_x, a.stats, a.bn_x, ntiles, a.dadd);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const Slide4Geom g = slide4_geom(a.C / 4, a.W);

@@ -59,18 +59,23 @@ class SegmentationPipeline:
     def __iter__(self):
         return self
 
-    def __next__(self):
+    def next_host(self):
+        """The next batch as host tensors (pinned for a GPU pipeline) — data/prefetch.py copies
+        them to the device on its own stream."""
         out = self._loader.next()
         if out is None:
             raise StopIteration
         x, y, ids, count = out
-        if self.device.type == "cuda":
-            x = x.to(self.device, non_blocking=True)
-            y = y.to(self.device, non_blocking=True) if y is not None else None
         if count < x.shape[0]:
             x = x[:count]
             y = y[:count] if y is not None else None
-            ids = ids[:count]
+        return x, y
+
+    def __next__(self):
+        x, y = self.next_host()
+        if self.device.type == "cuda":
+            x = x.to(self.device, non_blocking=True)
+            y = y.to(self.device, non_blocking=True) if y is not None else None
         return x, y
 
     @property

@@ -1,0 +1,98 @@
+"""Device prefetch: the next batches' host→device copies overlap the current training step.
+
+The reference's input_fn ends in ``prefetch(2·n_gpus)`` and MirroredStrategy's
+``experimental_distribute_dataset`` puts the batches on the devices ahead of the step
+(/root/reference/model.py:285-324).  Here a worker thread pulls host batches from a pipeline
+(pinned tensors from the native loader — its copies run without the GIL), issues the H2D copies
+(and an optional on-device cast) on a copy stream of its own, and hands the training thread
+``(x, y)`` plus an event; the training thread's stream waits on that event instead of running the
+copies in line with its kernels.  The training thread's per-step host work becomes the step
+launch plus the metrics (Model loop profile: loader 0.49 ms of 8.9 ms per DeepLab b32 step).
+
+During a HIP graph capture the worker must not touch the device (a capture in global mode
+rejects allocations and event creation from other threads): :meth:`quiesced` holds the lock the
+worker takes around its device section.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import contextlib
+
+import torch
+
+
+class DevicePrefetcher:
+    """Iterator of device batches ``(x, y)`` from ``source`` — a callable returning the next host
+    batch ``(x, y)`` (``y`` may be None) or raising StopIteration.  ``cast``: applied to ``x`` on
+    the copy stream (e.g. the compute-dtype conversion).  ``depth``: batches in flight."""
+
+    def __init__(self, source, device, depth=2, cast=None):
+        self.source = source
+        self.device = torch.device(device)
+        self.cast = cast
+        self.q = queue.Queue(maxsize=max(1, int(depth)))
+        self.lock = threading.Lock()
+        self.stop = threading.Event()
+        self.stream = torch.cuda.Stream(self.device)
+        self.thread = threading.Thread(target=self._run, name="tdl-device-prefetch", daemon=True)
+        self.thread.start()
+
+    def _put(self, item):
+        while not self.stop.is_set():
+            try:
+                self.q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _run(self):
+        try:
+            while not self.stop.is_set():
+                x, y = self.source()
+                with self.lock, torch.cuda.device(self.device), torch.cuda.stream(self.stream):
+                    xd = x.to(self.device, non_blocking=True)
+                    if self.cast is not None:
+                        xd = self.cast(xd)
+                    yd = y.to(self.device, non_blocking=True) if y is not None else None
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                if not self._put((xd, yd, ev)):
+                    return
+        except StopIteration:
+            self._put(StopIteration())
+        except BaseException as e:  # surfaced on the training thread
+            self._put(e)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        item = self.q.get()
+        if isinstance(item, BaseException):
+            self.stop.set()
+            if isinstance(item, StopIteration):
+                raise StopIteration
+            raise item
+        xd, yd, ev = item
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(ev)
+        # memory allocated on the copy stream, used (and freed) on the training stream
+        xd.record_stream(cur)
+        if yd is not None:
+            yd.record_stream(cur)
+        return xd, yd
+
+    @contextlib.contextmanager
+    def quiesced(self):
+        """No device work from the worker inside this block (HIP graph capture)."""
+        with self.lock:
+            yield
+
+    def close(self):
+        self.stop.set()
+        with contextlib.suppress(queue.Empty):
+            while True:
+                self.q.get_nowait()
+        self.thread.join(timeout=5.0)

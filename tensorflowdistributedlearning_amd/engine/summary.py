@@ -17,6 +17,7 @@ import json
 import os
 import socket
 import struct
+import threading
 import time
 import zlib
 
@@ -155,6 +156,8 @@ class SummaryWriter:
         self.logdir = logdir
         self._ev = None
         self._js = None
+        self._lock = threading.Lock()  # event-file writes from the caller and the image worker
+        self._pool = None
         if enabled:
             os.makedirs(logdir, exist_ok=True)
             now = time.time()
@@ -167,9 +170,11 @@ class SummaryWriter:
         if not self.enabled:
             return
         now = time.time()
-        self._ev.write(tfrecord(encode_scalar_event(tag, float(value), int(step), now)))
-        self._js.write(json.dumps({"step": int(step), "tag": tag, "value": float(value),
-                                   "wall_time": now}) + "\n")
+        rec = tfrecord(encode_scalar_event(tag, float(value), int(step), now))
+        with self._lock:
+            self._ev.write(rec)
+            self._js.write(json.dumps({"step": int(step), "tag": tag, "value": float(value),
+                                       "wall_time": now}) + "\n")
 
     def image(self, tag, img, step):
         """Grayscale image summary; ``img`` [H, W(, 1)] with values in [0, 1]."""
@@ -178,8 +183,24 @@ class SummaryWriter:
         import numpy as np
         a = np.asarray(img, dtype=np.float32)
         h, w = a.shape[:2]
-        self._ev.write(tfrecord(encode_image_event(tag, encode_png_gray(a), h, w, int(step),
-                                                   time.time())))
+        rec = tfrecord(encode_image_event(tag, encode_png_gray(a), h, w, int(step), time.time()))
+        with self._lock:
+            self._ev.write(rec)
+
+    def images_async(self, items, step):
+        """``[(tag, img), …]`` PNG-encoded and written on a background thread (the training
+        thread only hands over host arrays; :meth:`flush` / :meth:`close` wait for it)."""
+        if not self.enabled:
+            return
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(1, thread_name_prefix="tdl-summary")
+        self._pool.submit(lambda: [self.image(t, im, step) for t, im in items])
+
+    def _drain(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
 
     def scalars(self, d, step):
         for k, v in d.items():
@@ -187,11 +208,13 @@ class SummaryWriter:
 
     def flush(self):
         if self.enabled:
+            self._drain()
             self._ev.flush()
             self._js.flush()
 
     def close(self):
         if self.enabled:
+            self._drain()
             self._ev.close()
             self._js.close()
             self.enabled = False

@@ -62,6 +62,7 @@ from .ops.metrics import seg_scores, StreamingMean
 from .ops.optim import exponential_decay
 from .preprocessing.preprocessing import _prepare_directory, create_symlinks, TRAIN, EVAL
 from .data.pipeline import SegmentationPipeline, TestPipeline, fold_files, TRAIN_AUG
+from .data.prefetch import DevicePrefetcher
 from .data.classification import ClassificationPipeline, SyntheticImages, ArrayImages
 from .utils import metric_comparisson, get_available_gpus
 
@@ -128,6 +129,9 @@ class Model:
         self.use_regularization = kwargs.get("use_regularization", False)  # D5: opt-in
         self.kaggle_metric = kwargs.get("kaggle_metric", False)  # D16: reference formula default
         self.loader_threads = kwargs.get("loader_threads", 4)
+        # H2D copies of the next batches on a copy stream, fed by a worker thread
+        # (data/prefetch.py); False: the loader's batch is copied in line on the step's stream
+        self.device_prefetch = bool(kwargs.get("device_prefetch", True))
         # read_and_preprocess knobs of the training input (model.py:315-317: crop_probability=0,
         # the function's other defaults); e.g. augmentation={"brightness_range": 0.1}
         self.augmentation = dict(TRAIN_AUG, **kwargs.get("augmentation", {}))
@@ -348,7 +352,6 @@ class Model:
             b.numel() for n, b in net.named_buffers() if "running" in n)
         extra = ((lambda m: m.regularization_loss()) if self.use_regularization else None)
         trainer = self._make_trainer(net, _lovasz_loss, device, ctx, steps, extra)
-        stepper = _Stepper(trainer, self._use_graph(device, ctx))
         start = 0
         latest = ckpt.latest_checkpoint(fold_dir)
         if latest is not None:
@@ -363,6 +366,11 @@ class Model:
                                     device=device, rank=ctx.rank, world=ctx.world_size,
                                     threads=self.loader_threads, aug=self.augmentation,
                                     fp32=self.precision == "fp32")
+        batches, quiet = pipe, None
+        if device.type == "cuda" and self.device_prefetch:
+            batches = DevicePrefetcher(pipe.next_host, device, depth=2, cast=self._cast)
+            quiet = batches.quiesced
+        stepper = _Stepper(trainer, self._use_graph(device, ctx), quiet)
         main = ctx.is_main
         tw = SummaryWriter(os.path.join(fold_dir, "train"), enabled=main)
         ew = SummaryWriter(os.path.join(fold_dir, "eval"), enabled=main)
@@ -381,24 +389,33 @@ class Model:
         step = start
         t0 = time.time()
         clock = _StepClock(device, start)
+        lt = _LoopTimer()
         while step < steps:
-            x, yy = next(pipe)
-            x = self._cast(x)
+            lt.mark()
+            x, yy = next(batches)
+            if batches is pipe:
+                x = self._cast(x)
+            lt.mark("loader")
             loss, out = stepper(x, yy)
             step = trainer.global_step
             clock.tick(step)
+            lt.mark("step")
             pred = (out.float() > _logit(self.threshold)).float()
             score, acc = seg_scores(yy, pred, self.kaggle_metric)
             iou_m.update(score)
             acc_m.update(acc)
+            lt.mark("metrics")
             if self.save_summary_steps and step % self.save_summary_steps == 0 and main:
-                tw.scalars({"metrics/mean_acc": float(acc_m.result()),
-                            "metrics/mean_iou": float(iou_m.result()),
-                            "loss/lovasz_loss": float(loss),
+                # one device→host transfer for the scalars and the four images; PNG encoding
+                # and the event write happen on the writer's thread
+                vals, imgs = _summary_fetch([acc_m.result(), iou_m.result(), loss], x, yy, out,
+                                            self.threshold)
+                tw.scalars({"metrics/mean_acc": vals[0], "metrics/mean_iou": vals[1],
+                            "loss/lovasz_loss": vals[2],
                             "learning_rate": trainer.optimizer.lr_at(step - 1),
                             "global_step/sec": (step - start) / max(time.time() - t0, 1e-9)},
                            step)
-                _image_summaries(tw, "train", x, yy, out, self.threshold, step)
+                tw.images_async([(f"train/train_{k}", im) for k, im in imgs.items()], step)
             if step % self.save_checkpoints_steps == 0 or step == steps:
                 with clock.paused():
                     if main:
@@ -416,10 +433,13 @@ class Model:
             eval_result = self._evaluate(net, ev_imgs, ev_masks, batch * 2, device, ctx)
             eval_result["global_step"] = step
         saver.wait()
+        if batches is not pipe:
+            batches.close()
         tw.close()
         ew.close()
         res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step,
                "hip_graph": stepper.graph, "steady_ms_per_step": clock.result(step)}
+        lt.report()
         if main:
             with open(os.path.join(fold_dir, "result.json"), "w") as f:
                 json.dump(res, f)
@@ -737,6 +757,22 @@ class Model:
             raise ValueError("No model has been defined at this point! Call train method first.")
 
 
+def _summary_fetch(scalars, x, y, logits, threshold):
+    """The train-summary values in ONE device→host copy: ([float scalars], {name: [H, W] array})
+    — input (min-max scaled like TF's float image summary), label, probability, prediction of
+    the first sample (model.py:405-440)."""
+    img = x[0, :, :, 0].float()
+    img = (img - img.min()) / (img.max() - img.min()).clamp_min(1e-12)
+    prob = torch.sigmoid(logits[0, :, :, 0].float())
+    ims = torch.stack([img, y[0, :, :, 0].float(), prob, (prob > threshold).float()])
+    sc = torch.stack([torch.as_tensor(s, device=ims.device).float().reshape(()) for s in scalars])
+    host = torch.cat([sc, ims.reshape(-1)]).cpu().numpy()
+    n = len(scalars)
+    ims_h = host[n:].reshape(ims.shape)
+    return ([float(v) for v in host[:n]],
+            {"image": ims_h[0], "label": ims_h[1], "prob": ims_h[2], "prediction": ims_h[3]})
+
+
 def _image_summaries(writer, mode, x, y, logits, threshold, step):
     """``tf.summary.image`` of the first sample's input / label / probability / prediction
     (model.py:405-440); the input is min-max scaled like TF's float image summary."""
@@ -774,12 +810,14 @@ class _Stepper:
     """The fold loop's training step: eager for the first step, then (``graph``) one warm-up
     step that also records the step as a HIP graph (engine/trainer.Trainer.capture) and graph
     replays from there on — the loader's batch is copied into the static inputs.  The returned
-    (loss, out) are the graph's static outputs, valid until the next step."""
+    (loss, out) are the graph's static outputs, valid until the next step.  ``quiet``: a context
+    that keeps other threads off the device during the capture (the device prefetcher)."""
 
-    def __init__(self, trainer, graph):
+    def __init__(self, trainer, graph, quiet=None):
         self.trainer = trainer
         self.graph = bool(graph)
         self.eager_steps = 0
+        self.quiet = quiet if quiet is not None else contextlib.nullcontext
 
     def __call__(self, x, y):
         tr = self.trainer
@@ -789,9 +827,36 @@ class _Stepper:
             if self.eager_steps < 1:
                 self.eager_steps += 1
                 return tr.train_step(x, y)
-            tr.capture(x, y, warmup=1)  # the warm-up step trains on (x, y)
+            with self.quiet():
+                tr.capture(x, y, warmup=1)  # the warm-up step trains on (x, y)
             return tr.warmup_out
         return tr.replay(x, y)
+
+
+class _LoopTimer:
+    """TDL_LOOP_PROFILE=1: host time of each phase of the fold loop (where the training thread
+    waits), printed per fold — a host-bound loop shows up as one phase holding the step time."""
+
+    def __init__(self):
+        self.on = os.environ.get("TDL_LOOP_PROFILE", "0") == "1"
+        self.acc = {}
+        self.t = None
+        self.n = 0
+
+    def mark(self, phase=None):
+        if not self.on:
+            return
+        now = time.perf_counter()
+        if phase is None:
+            self.n += 1
+        elif self.t is not None:
+            self.acc[phase] = self.acc.get(phase, 0.0) + now - self.t
+        self.t = now
+
+    def report(self):
+        if self.on and self.n:
+            print("[Model] loop host ms/step: " + ", ".join(
+                f"{k} {v * 1e3 / self.n:.3f}" for k, v in self.acc.items()), flush=True)
 
 
 class _StepClock:
