@@ -44,6 +44,21 @@ def resnet50_shapes():
     return [(v[0], v[1], *k) for k, v in out.items()]
 
 
+def xception41_shapes():
+    """Xception-41 at 299² (models/xception.py): every dense conv — the pointwise 1×1 convs of the
+    separable blocks (26 of them at 19×19×728), the strided shortcuts and the stem."""
+    return [("stem1", 1, 299, 8, 32, 3, 2, 1), ("stem2", 1, 150, 32, 64, 3, 1, 1),
+            ("b1.pw1", 1, 150, 64, 128, 1, 1, 0), ("b1.pw2", 1, 150, 128, 128, 1, 1, 0),
+            ("b1.pw3", 1, 75, 128, 128, 1, 1, 0), ("b1.sc", 1, 150, 64, 128, 1, 2, 0),
+            ("b2.pw1", 1, 75, 128, 256, 1, 1, 0), ("b2.pw2", 1, 75, 256, 256, 1, 1, 0),
+            ("b2.pw3", 1, 38, 256, 256, 1, 1, 0), ("b2.sc", 1, 75, 128, 256, 1, 2, 0),
+            ("b3.pw1", 1, 38, 256, 728, 1, 1, 0), ("b3.pw2", 1, 38, 728, 728, 1, 1, 0),
+            ("mid.pw", 26, 19, 728, 728, 1, 1, 0), ("b3.sc", 1, 38, 256, 728, 1, 2, 0),
+            ("x1.pw2", 1, 19, 728, 1024, 1, 1, 0), ("x1.pw3", 1, 10, 1024, 1024, 1, 1, 0),
+            ("x1.sc", 1, 19, 728, 1024, 1, 2, 0), ("x2.pw1", 1, 10, 1024, 1536, 1, 1, 0),
+            ("x2.pw2", 1, 10, 1536, 1536, 1, 1, 0), ("x2.pw3", 1, 10, 1536, 2048, 1, 1, 0)]
+
+
 def timeit(fn, iters=5):
     s, e = torch.cuda.Event(True), torch.cuda.Event(True)
     fn()
@@ -61,6 +76,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--net", default="resnet50", choices=["resnet50", "xception41"])
+    ap.add_argument("--gemm", action="store_true",
+                    help="time the 1×1 convs' GEMMs with torch.mm (hipBLASLt) as a yardstick")
     ap.add_argument("--modes", default="1", help="comma list of conv kernel modes to time "
                     "(0 register-staged, 1 default selection, 2 LDS-DMA whenever aligned)")
     a = ap.parse_args()
@@ -69,7 +87,9 @@ def main():
     rows = []
     tot = {"miopen": 0.0}
     modes = [int(m) for m in a.modes.split(",")]
-    for name, mult, H, Cin, Cout, k, s, p in resnet50_shapes():
+    shapes = resnet50_shapes() if a.net == "resnet50" else xception41_shapes()
+    tot["gemm"] = 0.0
+    for name, mult, H, Cin, Cout, k, s, p in shapes:
         g = C.ConvGeom((s, s), (p, p, p, p), (1, 1))
         x = torch.randn(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
         w = torch.randn(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16) * 0.05
@@ -90,6 +110,16 @@ def main():
             msg += (f" m{mode}: fwd {t_f:6.1f} ({flop / t_f / 1e6:4.0f}TF) dgrad {t_d:6.1f} "
                     f"wgrad {t_w:6.1f} ({flop / t_w / 1e6:4.0f}TF) |")
         ext().conv_set_glds_mode(-1)
+        if a.gemm and k == 1 and s == 1:
+            A = x.view(-1, Cin)
+            W2 = w.view(Cout, Cin)
+            D = dy.view(-1, Cout)
+            g_f = timeit(lambda: torch.mm(A, W2.t()))
+            g_d = timeit(lambda: torch.mm(D, W2))
+            g_w = timeit(lambda: torch.mm(D.t(), A))
+            r.update(gemm_fwd_us=g_f, gemm_dgrad_us=g_d, gemm_wgrad_us=g_w)
+            tot["gemm"] += mult * (g_f + g_d + g_w)
+            msg += f" mm fwd {g_f:6.1f} dgrad {g_d:6.1f} wgrad {g_w:6.1f}"
         if not a.no_miopen:
             xm = x.permute(0, 3, 1, 2)  # channels_last view
             wm = w.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)

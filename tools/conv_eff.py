@@ -57,10 +57,16 @@ def main():
     seg = rows[idx[-2] + 1: idx[-1] + 1]
     by = {0: [], 1: [], 2: []}
     for r in seg:
-        mm = re.search(r"conv_(glds|gemm)_kernel<(\d)", r["Kernel_Name"])
-        if mm:
+        name = r["Kernel_Name"]
+        mm = re.search(r"conv_(glds|gemm|halo)_kernel<(\d)", name)
+        impl, mode = (mm.group(1), int(mm.group(2))) if mm else (None, None)
+        if "conv_pc_kernel<" in name:  # producer/consumer forward (conv_pc.hip)
+            impl, mode = "pc", 0
+        elif "conv_halo_wgrad_kernel<" in name:
+            impl, mode = "halo", 2
+        if impl is not None:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-            by[int(mm.group(2))].append((d, mm.group(1)))
+            by[mode].append((d, impl))
     print(f"{len(convs)} convs; kernels fwd {len(by[0])} dgrad {len(by[1])} wgrad {len(by[2])}")
     fw = by[0]
     tot = {}
