@@ -27,7 +27,8 @@ def conv_list(model, batch, image):
         dl = mod.dilation[0]
         # minimum HBM bytes (bf16): input + output activations + weights, each touched once
         by = 2.0 * (batch * (H * W * C + Ho * Wo * K) + K * C * mod.k[0] * mod.k[1])
-        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{st}" + (f" d{dl}" if dl > 1 else ""), fl, by))
+        out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{st}" + (f" d{dl}" if dl > 1 else ""), fl, by,
+                    2.0 * batch * H * W * C))
     for mod in m.modules():
         if isinstance(mod, Conv2d):
             mod.register_forward_hook(hook)
@@ -47,6 +48,9 @@ def main():
     ap.add_argument("--marker", default="sgd_kernel", help="optimizer kernel delimiting steps")
     ap.add_argument("--hbm", type=float, default=5.6, help="achievable HBM TB/s")
     ap.add_argument("--mfma", type=float, default=2.3, help="achievable dense bf16 PFLOP/s")
+    ap.add_argument("--fused-bytes", action="store_true",
+                    help="count a fused dgrad's extra operands (BN-statistics input, residual-join "
+                         "previous dx) in its minimum bytes")
     a = ap.parse_args()
 
     def bound_us(fl, by):
@@ -66,7 +70,15 @@ def main():
             impl, mode = "halo", 2
         if impl is not None:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-            by[mode].append((d, impl))
+            # fused dgrad operands (conv_glds_kernel<1, …, STATS, …, NJ, …>): the BN-backward
+            # statistics read a.bn_x and a residual join reads the previous dx — each one more
+            # dx-sized tensor through HBM
+            extra = 0
+            tp = re.search(r"conv_glds_kernel<([^>]*)>", name)
+            if mode == 1 and tp:
+                f = [t.strip() for t in tp.group(1).split(",")]
+                extra = (f[6] == "true") + (len(f) > 10 and f[10] == "false")
+            by[mode].append((d, impl, extra))
     print(f"{len(convs)} convs; kernels fwd {len(by[0])} dgrad {len(by[1])} wgrad {len(by[2])}")
     fw = by[0]
     tot = {}
@@ -77,7 +89,7 @@ def main():
         ks, cl = by[mode], lists[mode]
         if len(ks) != len(cl):
             agg = {}
-            for d, impl in ks:
+            for d, impl, _ in ks:
                 e = agg.setdefault(impl, [0, 0.0])
                 e[0] += 1
                 e[1] += d
@@ -86,7 +98,9 @@ def main():
             continue
         print(f"{nm}:  (bound = max(FLOP / {a.mfma} PF, min bytes / {a.hbm} TB/s))")
         agg = {}
-        for (d, impl), (name, fl, bts) in zip(ks, cl):
+        for (d, impl, extra), (name, fl, bts, dxb) in zip(ks, cl):
+            if a.fused_bytes:
+                bts = bts + extra * dxb
             e = agg.setdefault((name, impl), [0, 0.0, fl, bts])
             e[0] += 1
             e[1] += d
