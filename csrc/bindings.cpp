@@ -913,11 +913,35 @@ static DwF32Args dw_f32_args(const Tensor& x_like, const Tensor& w, int64_t Ho, 
   return a;
 }
 
+// aff (optional fp32 [≥2, ld ≥ C]: rows a, b of a BN's coefficients): the conv's input is
+// relu(a·x + b) — the BN + ReLU folded in (ops/dwfold.py); only where dwconv_aff_ok
+static void set_dw_aff(DwArgs& a, const c10::optional<Tensor>& aff, const char* who) {
+  if (!aff.has_value() || !aff->defined()) return;
+  CHECK_T(*aff, torch::kFloat32);
+  TORCH_CHECK(aff->dim() == 2 && aff->size(0) >= 2 && aff->size(1) >= a.C && aff->is_contiguous() &&
+                  aff->size(1) % 4 == 0,
+              who, " aff: contiguous fp32 [>=2, ld >= C], ld % 4 == 0");
+  TORCH_CHECK(dwconv_aff_ok(a), who, " aff: not supported for this geometry");
+  a.aff = aff->data_ptr<float>();
+  a.aff_ld = (int)aff->size(1);
+}
+
+static bool dwconv_aff_ok_py(Tensor x, Tensor w, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+                             int64_t dh, int64_t dw) {
+  if (x.dim() != 4 || w.dim() != 3 || w.size(2) != x.size(3)) return false;
+  const int64_t R = w.size(0), S = w.size(1);
+  const int64_t Ho = (x.size(1) + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+  const int64_t Wo = (x.size(2) + 2 * pw - dw * (S - 1) - 1) / sw + 1;
+  if (Ho <= 0 || Wo <= 0) return false;
+  DwArgs a = dw_args(x, w, Ho, Wo, sh, sw, ph, pw, dh, dw);
+  return dwconv_aff_ok(a);
+}
+
 // stats (optional fp32 [2, C], zeroed by the caller): BN sums of y fused into the kernel;
 // returns whether they were written (stride-1 3×3 tile kernel only)
 bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t sh, int64_t sw,
                 int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu, bool relu_in,
-                c10::optional<Tensor> stats) {
+                c10::optional<Tensor> stats, c10::optional<Tensor> aff) {
   if (is_f32(x)) {
     CHECK_T(x, torch::kFloat32);
     CHECK_T(w, torch::kFloat32);
@@ -940,6 +964,7 @@ bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_
     TORCH_CHECK(stats->numel() == 2 * a.C, "dwconv_fwd stats: fp32 [2, C]");
     a.stats = optfw(stats);
   }
+  set_dw_aff(a, aff, "dwconv_fwd");
   return dwconv_fwd_launch(a, stream());
 }
 
@@ -950,7 +975,7 @@ bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_
 bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                   int64_t dh, int64_t dw, c10::optional<Tensor> mask_x,
                   c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_red,
-                  c10::optional<Tensor> dadd) {
+                  c10::optional<Tensor> dadd, c10::optional<Tensor> aff) {
   if (is_f32(dy)) {
     CHECK_T(dy, torch::kFloat32);
     CHECK_T(w, torch::kFloat32);
@@ -985,11 +1010,14 @@ bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
     a.bn_x = BF(*bn_x);
     a.stats = optfw(bn_red);
   }
+  set_dw_aff(a, aff, "dwconv_dgrad");
+  TORCH_CHECK(!a.aff || (a.bn_x && !a.mask_x), "dwconv_dgrad aff: the mask comes from bn_x");
   return dwconv_dgrad_launch(a, stream());
 }
 
 void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int64_t sh, int64_t sw,
-                  int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu_in, bool accumulate) {
+                  int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu_in, bool accumulate,
+                  c10::optional<Tensor> aff) {
   if (is_f32(dy)) {
     CHECK_T(dy, torch::kFloat32);
     CHECK_T(x, torch::kFloat32);
@@ -1014,6 +1042,7 @@ void dwconv_wgrad(Tensor dy, Tensor x, Tensor dwt, c10::optional<Tensor> db, int
   a.accum = accumulate;
   TORCH_CHECK(!relu_in || (a.C % 8 == 0 && a.R * a.S == 9), "fused input ReLU: 3x3, C % 8 == 0");
   a.relu_in = relu_in;
+  set_dw_aff(a, aff, "dwconv_wgrad");
   const int slabs = dwconv_wgrad_slabs(a);
   Tensor ws;
   if (slabs > 0) ws = torch::empty({(int64_t)slabs * (a.R * a.S + 1) * a.C}, dwt.options());
@@ -1359,14 +1388,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("wd"), py::arg("gs"), py::arg("lr_scale") = py::none());
   m.def("dwconv_fwd", &dwconv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
-        py::arg("relu"), py::arg("relu_in"), py::arg("stats") = py::none());
+        py::arg("relu"), py::arg("relu_in"), py::arg("stats") = py::none(),
+        py::arg("aff") = py::none());
   m.def("dwconv_dgrad", &dwconv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
         py::arg("mask_x") = py::none(), py::arg("bn_x") = py::none(),
-        py::arg("bn_red") = py::none(), py::arg("dadd") = py::none());
+        py::arg("bn_red") = py::none(), py::arg("dadd") = py::none(), py::arg("aff") = py::none());
   m.def("dwconv_wgrad", &dwconv_wgrad, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("db"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dwl"),
-        py::arg("relu_in"), py::arg("accumulate") = true);
+        py::arg("relu_in"), py::arg("accumulate") = true, py::arg("aff") = py::none());
+  m.def("dwconv_aff_ok", &dwconv_aff_ok_py, py::arg("x"), py::arg("w"), py::arg("sh"),
+        py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
+        "whether the depthwise kernels for this geometry take a folded input BN + ReLU (aff)");
   m.def("upsample_fwd", &upsample_fwd);
   m.def("upsample_bwd", &upsample_bwd);
   m.def("conv_set_glds_mode", &conv_set_glds_mode,

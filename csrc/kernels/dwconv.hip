@@ -648,7 +648,7 @@ __device__ __forceinline__ uint2 relu4(uint2 v) { return make_uint2(relu2(v.x), 
 
 constexpr int DT_NT = 512;  // tile-kernel workgroup cap (16 channel lanes × ≤ 32 columns)
 
-template <bool FLIP, bool RIN>
+template <bool FLIP, bool RIN, bool AFF = false>
 __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restrict__ in,
                                                         const bf16_t* __restrict__ wt,
                                                         const float* __restrict__ bias,
@@ -659,7 +659,8 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
                                                         const bf16_t* __restrict__ mask_x,
                                                         float* __restrict__ stats,
                                                         const bf16_t* __restrict__ bn_x, int ntiles,
-                                                        const bf16_t* __restrict__ dadd) {
+                                                        const bf16_t* __restrict__ dadd,
+                                                        const float* __restrict__ aff, int aff_ld) {
   // stats (optional, fp32 [2][C], accumulated): BN sums of the stored bf16 outputs — (Σy, Σy²)
   // for the BN that normalises this forward's output, or (Σg, Σg·bn_x) with bn_x the input of
   // the BN whose output gradient this dgrad produces (bn.hip red_raw) — so that BN skips its
@@ -706,6 +707,30 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  if constexpr (!FLIP && AFF) {
+    // the input BN + ReLU folded in: u = relu(a·z + b), rounded to bf16 as the BN's apply pass
+    // would store it, in place on the staged tile; out-of-image pixels keep the DMA's zeros (the
+    // padding is zero in u, not relu(b))
+    const int ch = cg0 + (t & 7) * 8;  // blockDim.x % 64 == 0: a thread's chunks share one group
+    if (ch < C) {
+      // (coefficients re-read per chunk through a volatile pointer, L1 hits: hoisted out of the
+      // loop they held 16 VGPRs across it and the kernel spilled at its 128-register budget)
+      const volatile float* av = aff + ch;
+      const volatile float* bv = aff + aff_ld + ch;
+      for (int i = t; i < chunks; i += blockDim.x) {
+        const int pix = i >> 3, r = pix / pitch, cc = pix - r * pitch;
+        const int hi = h0 - Ph + r, wi = w0 - Pw + cc;
+        if ((unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi) {
+          float v[8];
+          unpack8(tile[i], v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(fmaf(v[j], av[j], bv[j]), 0.f);
+          tile[i] = pack8(v);
+        }
+      }
+    }
+    __syncthreads();
+  }
   const int pw = rest % tw, g = rest / tw;
   const int w = w0 + pw, c = cg0 + cl * 4;
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
@@ -750,7 +775,18 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
       for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
     }
     const long op = (((long)n * Ho + h0 + h) * Wo + w) * C + c;
-    if (mask_x) {  // dx · [x > 0] for the fused input ReLU's backward
+    uint2 xb = make_uint2(0, 0);
+    if constexpr (FLIP && AFF) {
+      // folded input BN + ReLU: dx · [a·bn_x + b > 0] (bn_x = the BN input the forward staged)
+      xb = *(const uint2*)(bn_x + op);
+      const volatile float* ma = aff + c;  // (per row, not hoisted: see the forward's transform)
+      const volatile float* mb = aff + aff_ld + c;
+      const f32x2 x0 = lo_hi(xb.x), x1 = lo_hi(xb.y);
+      o[0] = fmaf(x0.x, ma[0], mb[0]) > 0.f ? o[0] : 0.f;
+      o[1] = fmaf(x0.y, ma[1], mb[1]) > 0.f ? o[1] : 0.f;
+      o[2] = fmaf(x1.x, ma[2], mb[2]) > 0.f ? o[2] : 0.f;
+      o[3] = fmaf(x1.y, ma[3], mb[3]) > 0.f ? o[3] : 0.f;
+    } else if (mask_x) {  // dx · [x > 0] for the fused input ReLU's backward
       const uint2 xm = *(const uint2*)(mask_x + op);
       const f32x2 x0 = lo_hi(xm.x), x1 = lo_hi(xm.y);
       o[0] = x0.x > 0.f ? o[0] : 0.f;
@@ -772,7 +808,7 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
       const f32x2 q0 = lo_hi(packed.x), q1 = lo_hi(packed.y);  // the stored bf16 values
       const float q[4] = {q0.x, q0.y, q1.x, q1.y};
       if (bn_x) {
-        const uint2 xb = *(const uint2*)(bn_x + op);
+        if constexpr (!(FLIP && AFF)) xb = *(const uint2*)(bn_x + op);
         const f32x2 x0 = lo_hi(xb.x), x1 = lo_hi(xb.y);
         const float xv[4] = {x0.x, x0.y, x1.x, x1.y};
 #pragma unroll
@@ -869,6 +905,16 @@ __global__ void __launch_bounds__(NT) dw_wgrad_slide(DwArgs a, int lanes_c, int 
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) db[j] = 0.f;
+  float av[8], bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) av[j] = bv[j] = 0.f;
+  if (active && a.aff) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av[j] = a.aff[c + j];
+      bv[j] = a.aff[a.aff_ld + c + j];
+    }
+  }
   if (active && w0 < w1) {
     for (int row = r0; row < r1; ++row) {
       const int n = row / a.Ho, ho = row - n * a.Ho;
@@ -884,6 +930,13 @@ __global__ void __launch_bounds__(NT) dw_wgrad_slide(DwArgs a, int lanes_c, int 
       auto col = [&](int r, int wi) -> uint4 {
         if (!hv[r] || (unsigned)wi >= (unsigned)a.W) return make_uint4(0, 0, 0, 0);
         const uint4 v = *(const uint4*)(xn + ((long)hi[r] * a.W + wi) * a.C);
+        if (a.aff) {  // folded input BN + ReLU (bf16-rounded as the forward's staged u)
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], av[j], bv[j]), 0.f);
+          return pack8(f);
+        }
         return a.relu_in ? relu8(v) : v;
       };
       uint4 win[3][3], nxt[3];
@@ -1032,18 +1085,26 @@ void wgrad_dispatch(const DwArgs& a, hipStream_t st) {
 
 }  // namespace
 
+// the kernels that implement DwArgs::aff: stride-1 3×3 on the LDS tile kernels (fwd / dgrad) and
+// the sliding weight-gradient kernel
+bool dwconv_aff_ok(const DwArgs& a) {
+  return slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C) &&
+         dw_tile_fits(a.Ho, a.Wo, a.C) && dwconv_wgrad_slabs(a) > 0;
+}
+
 bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
   const long outs = (long)a.N * a.Ho * a.Wo * a.C;
   if (slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C)) {
     const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
     const int ntiles = a.N * g.th * g.twn;
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
-    auto kern = a.relu_in ? dw_tile_kernel<false, true> : dw_tile_kernel<false, false>;
+    auto kern = a.aff ? dw_tile_kernel<false, false, true>
+                : a.relu_in ? dw_tile_kernel<false, true> : dw_tile_kernel<false, false>;
     hipLaunchKernelGGL(kern, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
                        st, a.x, a.w, a.bias, a.out,
                        a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
                        g.twn, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
-                       ntiles, (const bf16_t*)nullptr);
+                       ntiles, (const bf16_t*)nullptr, a.aff, a.aff_ld);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {
     const Slide4Geom g = slide4_geom(a.C / 4, a.Wo);
@@ -1075,10 +1136,11 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
     const DwTileGeom g = dw_tile_geom(a.H, a.W);
     const int ntiles = a.N * g.th * g.twn;
     dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
-    hipLaunchKernelGGL((dw_tile_kernel<true, false>), grid, dim3(g.nt),
+    auto kern = a.aff ? dw_tile_kernel<true, false, true> : dw_tile_kernel<true, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(g.nt),
                        dw_tile_smem(g, a.stats != nullptr), st, a.dy, a.w, nullptr, a.out,
                        a.Ho, a.Wo, a.H, a.W, a.C, 2 - a.ph, 2 - a.pw, 0, g.tr, g.tw, g.rg, g.th,
-                       g.twn, a.mask_x, a.stats, a.bn_x, ntiles, a.dadd);
+                       g.twn, a.mask_x, a.stats, a.bn_x, ntiles, a.dadd, a.aff, a.aff_ld);
     return a.stats != nullptr;
   } else if (slide_ok(a) && slide4()) {  // stride-1 dgrad = fwd of dy, rotated filter, padding 2 − p
     const Slide4Geom g = slide4_geom(a.C / 4, a.W);

@@ -257,7 +257,14 @@ struct DwArgs {
   // dgrad: dx = (masked) dgrad + dadd (shaped like dx; may alias a.out) — the residual-gradient
   // join of a tensor whose other consumer's gradient is already in the buffer (ops/gradjoin.py)
   const bf16_t* dadd = nullptr;
+  // input BN + ReLU folded in (ops/dwfold.py): the conv's input is u = relu(a·x + b) with
+  // a = aff[c], b = aff[aff_ld + c] (fp32 BN coefficients) — fwd: applied to the staged tile;
+  // dgrad: the ReLU mask is a·bn_x + b > 0 (bn_x = x); wgrad: applied to the x loads.
+  // Stride-1 3×3 tile / sliding kernels only (dwconv_aff_ok)
+  const float* aff = nullptr;
+  int aff_ld = 0;
 };
+bool dwconv_aff_ok(const DwArgs& a);
 bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st);  // true: a.stats written
 bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st);  // true: a.stats written
 int dwconv_wgrad_slabs(const DwArgs& a);  // row-slab count of the fast wgrad (0: generic)

@@ -20,7 +20,7 @@ import torch.nn as nn
 from . import params as _params
 from .layers import (ConvBN, DepthwiseConv2d, BatchNorm, GlobalAvgPool, Linear, bn_fold_enabled,
                      fold_bn_affine)
-from ..ops import bnfold, gradjoin
+from ..ops import bnfold, dwfold, gradjoin
 from ..ops.dwconv import joinable
 
 
@@ -65,9 +65,19 @@ class SeparableConvBN(nn.Module):
                 c = self.__dict__["_fold"] = (key, w.to(dtype).contiguous(), sh.contiguous())
         return c[1], c[2]
 
-    def forward(self, x, relu_in=False, residual=None, join=None, res_join=None):
+    def forward(self, x, relu_in=False, residual=None, join=None, res_join=None, defer=False):
         """``join``: gradient join of x (its depthwise dgrad accumulates onto the other
-        consumer's contribution); ``res_join``: gradient join of the residual."""
+        consumer's contribution); ``res_join``: gradient join of the residual.  ``x`` may be a
+        deferred BN + ReLU (ops/dwfold.DeferredBNAct) that the depthwise conv applies on its
+        loads; ``defer``: return this conv's own BN + ReLU deferred the same way (training,
+        no residual) for the next separable conv."""
+        if isinstance(x, dwfold.DeferredBNAct):
+            fold_in = (self.training and not self.act_inside and bnfold.ENABLED and not relu_in
+                       and join is None)
+            if not fold_in:
+                x = x.materialize()
+        else:
+            fold_in = False
         if not self.training and not torch.is_grad_enabled() and bn_fold_enabled():
             # inference: the depthwise BN (+ReLU) folded into the depthwise conv's bias epilogue
             w, b = self._dw_folded(x.dtype, x.device)
@@ -78,10 +88,15 @@ class SeparableConvBN(nn.Module):
         if self.training and not self.act_inside and bnfold.ENABLED:
             # no activation between the depthwise BN and the pointwise conv: the BN is folded
             # into the conv (scaled weights + bias, ops/bnfold.py) — its output never exists
-            z, stats = self.depthwise(x, relu_in=relu_in, want_stats=True, join=join)
+            if fold_in:  # the previous pointwise BN + ReLU applied by the depthwise kernels
+                z, stats = dwfold.bn_act_dw(x, self.depthwise, want_stats=True)
+            else:
+                z, stats = self.depthwise(x, relu_in=relu_in, want_stats=True, join=join)
             pw = self.pointwise
             y, st2 = bnfold.bn_conv1x1(z, stats, self.dw_bn, pw.conv, want_stats=True,
                                        dy_sums_zero=pw.bn.training)
+            if defer and pw.relu and residual is None and res_join is None and dwfold.ENABLED:
+                return dwfold.DeferredBNAct(y, st2, pw.bn)
             return pw.bn(y, stats=st2, residual=residual, relu=pw.relu, res_join=res_join)
         if self.training:
             y, stats = self.depthwise(x, relu_in=relu_in, want_stats=True, join=join)
@@ -124,8 +139,11 @@ class XceptionModule(nn.Module):
         if (self.grad_join and self.skip in ("sum", "conv") and torch.is_grad_enabled()
                 and x.requires_grad and joinable(x, relu_in)):
             join = gradjoin.GradJoin(2)
-        r = self.convs[0](x, relu_in=relu_in, join=join)
-        r = self.convs[1](r)
+        # units 2 and 3 read only the previous pointwise BN + ReLU: it is deferred into their
+        # depthwise kernels (ops/dwfold.py; a geometry they cannot take applies it as usual)
+        defer = self.training and torch.is_grad_enabled()
+        r = self.convs[0](x, relu_in=relu_in, join=join, defer=defer)
+        r = self.convs[1](r, defer=defer)
         if self.skip == "sum":
             # identity skip: the add is folded into the last pointwise BN's apply (one pass,
             # one bf16 rounding of BN(y) + x instead of two)
