@@ -867,11 +867,22 @@ struct DwTileGeom {
   int tr, tw, rg, th, twn, nt;
 };
 DwTileGeom dw_tile_geom(int Ho, int Wo) {
+  // TDL_DW_TR: rows per tile at most (default DT_TR; A/B of the halo overhead vs workgroups per
+  // CU — a taller tile re-reads fewer halo rows but holds more LDS)
+  static const int tr_max = [] {
+    const char* e = getenv("TDL_DW_TR");
+    return e ? std::max(1, std::min(32, atoi(e))) : DT_TR;
+  }();
   DwTileGeom g;
   g.twn = cdiv(Wo, DT_TW);
   g.tw = cdiv(Wo, g.twn);
-  g.th = cdiv(Ho, DT_TR);
+  g.th = cdiv(Ho, tr_max);
   g.tr = cdiv(Ho, g.th);
+  // the halo tile within the 64 KiB of dynamic LDS a launch gets without an attribute
+  while (g.tr > 1 && (long)cdiv((g.tr + 2) * (g.tw + 2) * 8, 64) * 1024 > 65536) {
+    ++g.th;
+    g.tr = cdiv(Ho, g.th);
+  }
   g.rg = std::max(1, std::min(DT_TW / g.tw, g.tr));
   g.nt = cdiv(16 * g.tw * g.rg, 64) * 64;
   return g;

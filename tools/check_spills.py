@@ -25,10 +25,11 @@ def main():
     ap.add_argument("--all", action="store_true", help="list every kernel with a spill")
     a = ap.parse_args()
     bad = False
-    for src in ("conv_glds.hip", "conv_gemm.hip"):
+    for src in ("conv_glds.hip", "conv_gemm.hip", "conv_pc.hip", "conv_halo.hip", "dwconv.hip"):
         with tempfile.TemporaryDirectory() as td:
             r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                                "-I" + os.path.join(ROOT, "csrc"), "-c", os.path.join(ROOT, "csrc", "kernels", src),
+                                "-I" + os.path.join(ROOT, "csrc"), "-I" + os.path.join(ROOT, "csrc", "kernels"),
+                                "-c", os.path.join(ROOT, "csrc", "kernels", src),
                                 "-o", os.path.join(td, "k.o"), "-Rpass-analysis=kernel-resource-usage",
                                 "--save-temps"], capture_output=True, text=True, cwd=td)
             asm = ""
