@@ -634,11 +634,12 @@ __global__ void __launch_bounds__(NT) dw_slide4_kernel(const bf16_t* __restrict_
 }
 
 // LDS-tiled depthwise 3×3 stride 1: a workgroup stages its (TR+2)×(TW+2) input pixels × 64
-// channels once (LDS-DMA, ≈1.3× the tile's own bytes incl. halo), then every lane
-// (8 channels × one output column) slides down the TR rows reading its 3×3 window from LDS.
+// channels once (LDS-DMA; with tiles up to the 64 KiB LDS bound ≈1.1–1.2× the tile's own bytes
+// incl. halo), then every lane (4 channels × one output column) slides down the TR rows reading
+// its 3×3 window from LDS.
 // The register-window kernels above re-fetch each input row for 3 output-row workgroups from the
 // fabric (PMC: 3.2× the input bytes); here the re-reads are LDS reads.
-constexpr int DT_TR = 8, DT_TW = 32, DT_CH = 64;
+constexpr int DT_TW = 32, DT_CH = 64;
 
 __device__ __forceinline__ void unpack4x2(const uint2& v, f32x2* f) {
   f[0] = lo_hi(v.x);
@@ -665,7 +666,7 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
   // for the BN that normalises this forward's output, or (Σg, Σg·bn_x) with bn_x the input of
   // the BN whose output gradient this dgrad produces (bn.hip red_raw) — so that BN skips its
   // separate reduce pass
-  // tile: tr × tw output pixels (runtime, ≤ DT_TR × DT_TW, balanced splits of Ho / Wo); lanes:
+  // tile: tr × tw output pixels (runtime: tw ≤ DT_TW, tr bounded by LDS, balanced splits); lanes:
   // 16 channel lanes (4 channels each) × tw column lanes × rg row groups (each slides over
   // ⌈tr / rg⌉ rows).  Four channels per lane keep the sliding window + taps at 72 fp32 registers
   // (8 per lane needed ≈170 VGPRs: 2 waves per SIMD, too few to hide the halo DMA latency).
@@ -713,10 +714,15 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
     // padding is zero in u, not relu(b))
     const int ch = cg0 + (t & 7) * 8;  // blockDim.x % 64 == 0: a thread's chunks share one group
     if (ch < C) {
-      // (coefficients re-read per chunk through a volatile pointer, L1 hits: hoisted out of the
-      // loop they held 16 VGPRs across it and the kernel spilled at its 128-register budget)
-      const volatile float* av = aff + ch;
-      const volatile float* bv = aff + aff_ld + ch;
+      // (the coefficients are loaded per tile through a pointer the compiler cannot prove
+      // invariant: hoisted out of the tile loop they held 16 VGPRs across the whole computation
+      // and the kernel spilled at its 128-register budget)
+      const float* ap = aff + ch;
+      asm volatile("" : "+v"(ap));
+      const float4 a0 = *(const float4*)ap, a1 = *(const float4*)(ap + 4);
+      const float4 b0 = *(const float4*)(ap + aff_ld), b1 = *(const float4*)(ap + aff_ld + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       for (int i = t; i < chunks; i += blockDim.x) {
         const int pix = i >> 3, r = pix / pitch, cc = pix - r * pitch;
         const int hi = h0 - Ph + r, wi = w0 - Pw + cc;
@@ -779,13 +785,14 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
     if constexpr (FLIP && AFF) {
       // folded input BN + ReLU: dx · [a·bn_x + b > 0] (bn_x = the BN input the forward staged)
       xb = *(const uint2*)(bn_x + op);
-      const volatile float* ma = aff + c;  // (per row, not hoisted: see the forward's transform)
-      const volatile float* mb = aff + aff_ld + c;
+      const float* ap = aff + c;  // (re-read per row, not hoisted: see the forward's transform)
+      asm volatile("" : "+v"(ap));
+      const float4 ma = *(const float4*)ap, mb = *(const float4*)(ap + aff_ld);
       const f32x2 x0 = lo_hi(xb.x), x1 = lo_hi(xb.y);
-      o[0] = fmaf(x0.x, ma[0], mb[0]) > 0.f ? o[0] : 0.f;
-      o[1] = fmaf(x0.y, ma[1], mb[1]) > 0.f ? o[1] : 0.f;
-      o[2] = fmaf(x1.x, ma[2], mb[2]) > 0.f ? o[2] : 0.f;
-      o[3] = fmaf(x1.y, ma[3], mb[3]) > 0.f ? o[3] : 0.f;
+      o[0] = fmaf(x0.x, ma.x, mb.x) > 0.f ? o[0] : 0.f;
+      o[1] = fmaf(x0.y, ma.y, mb.y) > 0.f ? o[1] : 0.f;
+      o[2] = fmaf(x1.x, ma.z, mb.z) > 0.f ? o[2] : 0.f;
+      o[3] = fmaf(x1.y, ma.w, mb.w) > 0.f ? o[3] : 0.f;
     } else if (mask_x) {  // dx · [x > 0] for the fused input ReLU's backward
       const uint2 xm = *(const uint2*)(mask_x + op);
       const f32x2 x0 = lo_hi(xm.x), x1 = lo_hi(xm.y);
@@ -867,11 +874,12 @@ struct DwTileGeom {
   int tr, tw, rg, th, twn, nt;
 };
 DwTileGeom dw_tile_geom(int Ho, int Wo) {
-  // TDL_DW_TR: rows per tile at most (default DT_TR; A/B of the halo overhead vs workgroups per
-  // CU — a taller tile re-reads fewer halo rows but holds more LDS)
+  // rows per tile: as many as the 64 KiB LDS bound below allows (TDL_DW_TR caps it; 8 was the
+  // round-4 default — Xception b128 shapes 10–14 % faster with taller tiles: fewer halo re-reads
+  // per output, and the workgroups per CU are LDS-bound either way, tools/dw_micro.py)
   static const int tr_max = [] {
     const char* e = getenv("TDL_DW_TR");
-    return e ? std::max(1, std::min(32, atoi(e))) : DT_TR;
+    return e ? std::max(1, std::min(32, atoi(e))) : 32;
   }();
   DwTileGeom g;
   g.twn = cdiv(Wo, DT_TW);
@@ -890,7 +898,7 @@ DwTileGeom dw_tile_geom(int Ho, int Wo) {
 
 // dynamic LDS of a tile launch: the (tr+2)×(tw+2)×64-channel halo in whole 1-KiB DMA pieces (or
 // the statistics reduction's 128 × lanes floats) — sized to the launch, not the largest tile, so
-// small-image layers fit more workgroups per CU (24 KiB at 19×19 vs 43 KiB)
+// small-image layers fit more workgroups per CU (56 KiB for a whole 19×19 image)
 size_t dw_tile_smem(const DwTileGeom& g, bool stats) {
   const size_t halo = (size_t)cdiv((g.tr + 2) * (g.tw + 2) * 8, 64) * 64 * 16;
   const size_t red = stats ? (size_t)128 * (g.nt / 16) * 4 : 0;

