@@ -183,9 +183,6 @@ def main():
             and rccl_ranks != args.gpus:
         raise SystemExit(f"RCCL reports {rccl_ranks} ranks, --gpus {args.gpus}")
     comm = "rccl" if ctx.native is not None else ("gloo" if n > 1 else "none")
-    if dev.type == "cuda" and os.environ.get("TDL_STEP_PRIO", "0") == "1":
-        # A/B: the step's compute stream at high priority, the side-stream wgrads at normal
-        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=-1))
     # CPU (plumbing runs, tests): fp32 storage, the PyTorch reference ops; GPU --dtype fp32: fp32
     # activations + the fp32 master weights read directly by the fp32 kernels (no compute copy)
     gpu_bf16 = dev.type == "cuda" and bc.dtype in ("bf16", "fp8")
