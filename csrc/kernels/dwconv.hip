@@ -649,6 +649,64 @@ __device__ __forceinline__ uint2 relu4(uint2 v) { return make_uint2(relu2(v.x), 
 
 constexpr int DT_NT = 512;  // tile-kernel workgroup cap (16 channel lanes × ≤ 32 columns)
 
+// Stage one output tile's (tr+2)×(tw+2)-pixel × 64-channel input halo in LDS and (AFF) apply the
+// folded input BN + ReLU to it in place — shared by the forward / input-gradient tile kernel and
+// the weight-gradient tile kernel.
+template <bool AFF>
+__device__ __forceinline__ void dw_stage_tile(uint4* tile, const bf16_t* __restrict__ src, int Hi,
+                                              int Wi, int C, int h0, int w0, int Ph, int Pw,
+                                              int pitch, int chunks, int cg0, int t,
+                                              const float* __restrict__ aff, int aff_ld) {
+  // staging: LDS-DMA, one 1-KiB piece (64 lanes × 16 B, lane-linear in LDS) per wave instruction;
+  // padding / ragged chunks read past the range-checked descriptor (zeros).  No per-chunk branch
+  // around a load, so the pieces stream back-to-back instead of one latency each.
+  {
+    const rsrc_t rs = make_rsrc(src, (uint32_t)((long)Hi * Wi * C * 2));
+    const int nwv = blockDim.x >> 6, ln = t & 63;
+    for (int j = t >> 6; j * 64 < chunks; j += nwv) {
+      const int i = j * 64 + ln, k = i & 7, pix = i >> 3;
+      const int r = pix / pitch, cc = pix - r * pitch;
+      const int hi = h0 - Ph + r, wi = w0 - Pw + cc, ch = cg0 + k * 8;
+      const bool ok = i < chunks && (unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi &&
+                      ch < C;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)((char*)tile + j * 1024), 16,
+                                               ok ? (uint32_t)(((hi * Wi + wi) * C + ch) * 2) : OOB,
+                                               0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if constexpr (AFF) {
+    // the input BN + ReLU folded in: u = relu(a·z + b), rounded to bf16 as the BN's apply pass
+    // would store it, in place on the staged tile; out-of-image pixels keep the DMA's zeros (the
+    // padding is zero in u, not relu(b))
+    const int ch = cg0 + (t & 7) * 8;  // blockDim.x % 64 == 0: a thread's chunks share one group
+    if (ch < C) {
+      // (the coefficients are loaded per tile through a pointer the compiler cannot prove
+      // invariant: hoisted out of the tile loop they held 16 VGPRs across the whole computation
+      // and the kernel spilled at its 128-register budget)
+      const float* ap = aff + ch;
+      asm volatile("" : "+v"(ap));
+      const float4 a0 = *(const float4*)ap, a1 = *(const float4*)(ap + 4);
+      const float4 b0 = *(const float4*)(ap + aff_ld), b1 = *(const float4*)(ap + aff_ld + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      for (int i = t; i < chunks; i += blockDim.x) {
+        const int pix = i >> 3, r = pix / pitch, cc = pix - r * pitch;
+        const int hi = h0 - Ph + r, wi = w0 - Pw + cc;
+        if ((unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi) {
+          float v[8];
+          unpack8(tile[i], v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(fmaf(v[j], av[j], bv[j]), 0.f);
+          tile[i] = pack8(v);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <bool FLIP, bool RIN, bool AFF = false>
 __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restrict__ in,
                                                         const bf16_t* __restrict__ wt,
@@ -689,54 +747,8 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
   const int h0 = ty * tr, w0 = tx * tw;
   const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
   const bf16_t* src = in + (long)n * Hi * Wi * C;
-  // staging: LDS-DMA, one 1-KiB piece (64 lanes × 16 B, lane-linear in LDS) per wave instruction;
-  // padding / ragged chunks read past the range-checked descriptor (zeros).  No per-chunk branch
-  // around a load, so the pieces stream back-to-back instead of one latency each.
-  {
-    const rsrc_t rs = make_rsrc(src, (uint32_t)((long)Hi * Wi * C * 2));
-    const int nwv = blockDim.x >> 6, ln = t & 63;
-    for (int j = t >> 6; j * 64 < chunks; j += nwv) {
-      const int i = j * 64 + ln, k = i & 7, pix = i >> 3;
-      const int r = pix / pitch, cc = pix - r * pitch;
-      const int hi = h0 - Ph + r, wi = w0 - Pw + cc, ch = cg0 + k * 8;
-      const bool ok = i < chunks && (unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi &&
-                      ch < C;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)((char*)tile + j * 1024), 16,
-                                               ok ? (uint32_t)(((hi * Wi + wi) * C + ch) * 2) : OOB,
-                                               0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if constexpr (!FLIP && AFF) {
-    // the input BN + ReLU folded in: u = relu(a·z + b), rounded to bf16 as the BN's apply pass
-    // would store it, in place on the staged tile; out-of-image pixels keep the DMA's zeros (the
-    // padding is zero in u, not relu(b))
-    const int ch = cg0 + (t & 7) * 8;  // blockDim.x % 64 == 0: a thread's chunks share one group
-    if (ch < C) {
-      // (the coefficients are loaded per tile through a pointer the compiler cannot prove
-      // invariant: hoisted out of the tile loop they held 16 VGPRs across the whole computation
-      // and the kernel spilled at its 128-register budget)
-      const float* ap = aff + ch;
-      asm volatile("" : "+v"(ap));
-      const float4 a0 = *(const float4*)ap, a1 = *(const float4*)(ap + 4);
-      const float4 b0 = *(const float4*)(ap + aff_ld), b1 = *(const float4*)(ap + aff_ld + 4);
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      for (int i = t; i < chunks; i += blockDim.x) {
-        const int pix = i >> 3, r = pix / pitch, cc = pix - r * pitch;
-        const int hi = h0 - Ph + r, wi = w0 - Pw + cc;
-        if ((unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi) {
-          float v[8];
-          unpack8(tile[i], v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(fmaf(v[j], av[j], bv[j]), 0.f);
-          tile[i] = pack8(v);
-        }
-      }
-    }
-    __syncthreads();
-  }
+  dw_stage_tile<!FLIP && AFF>(tile, src, Hi, Wi, C, h0, w0, Ph, Pw, pitch, chunks, cg0, t, aff,
+                              aff_ld);
   const int pw = rest % tw, g = rest / tw;
   const int w = w0 + pw, c = cg0 + cl * 4;
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
@@ -858,6 +870,116 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
 // tile-kernel grid (x): every tile its own workgroup, except with fused statistics — then
 // ≈ TDL_DW_STAT_WG workgroups in all, each walking several tiles and flushing its sums once
 // (one atomic pair per channel per workgroup instead of per tile)
+// Weight gradient on the tile machinery: a workgroup walks output tiles (blockIdx.x, +gridDim.x,
+// …), stages each tile's input halo in LDS exactly as the forward does (RIN: input ReLU on the LDS
+// read; AFF: the folded BN + ReLU applied to the staged tile), and every lane (4 channels × one
+// output column) slides down its rows with the 3×3 window in fp32 registers, accumulating
+// dW[tap] += window[tap] · dy (18 packed FMAs per output row; dy read once, straight from global).
+// Per workgroup one partial per (tap, channel): shuffles over the 4 column lanes of a wave that
+// share a channel lane, then the waves through LDS, written to slab blockIdx.x (the caller's
+// split-K reduce sums the slabs).  The sliding-window kernel below unpacks its packed window
+// 9× per output (144 VALU per 8 channels per output vs ≈30 per 4 here).
+template <bool RIN, bool AFF>
+__global__ void __launch_bounds__(DT_NT, 4) dw_wgrad_tile_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, int Hi, int Wi, int Ho, int Wo,
+    int C, int Ph, int Pw, int tr, int tw, int rg, int tiles_h, int tiles_w, int ntiles,
+    const float* __restrict__ aff, int aff_ld, float* __restrict__ ws_w, float* __restrict__ ws_b) {
+  extern __shared__ uint4 tile[];
+  const uint2* tile2 = (const uint2*)tile;
+  const int t = threadIdx.x;
+  const int cl = t & 15, rest = t >> 4, cg0 = blockIdx.y * DT_CH;
+  f32x2 acc[9][2], dsum[2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k][0] = acc[k][1] = f32x2{0.f, 0.f};
+  dsum[0] = dsum[1] = f32x2{0.f, 0.f};
+  for (int tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+    if (tb != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+    int b = tb;
+    const int tx = b % tiles_w;
+    b /= tiles_w;
+    const int ty = b % tiles_h;
+    const int n = b / tiles_h;
+    const int h0 = ty * tr, w0 = tx * tw;
+    const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
+    dw_stage_tile<AFF>(tile, x + (long)n * Hi * Wi * C, Hi, Wi, C, h0, w0, Ph, Pw, pitch, chunks,
+                       cg0, t, aff, aff_ld);
+    const int pw = rest % tw, g = rest / tw;
+    const int w = w0 + pw, c = cg0 + cl * 4;
+    const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
+    const int r1 = min(min(tr, r0 + rpg), Ho - h0);
+    if (g >= rg || w >= Wo || c >= C || r0 >= r1) continue;
+    auto ldt = [&](int pix) { const uint2 v = tile2[pix * 16 + cl]; return RIN ? relu4(v) : v; };
+    f32x2 win[3][3][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt((r0 + r) * pitch + pw + s2), win[r + 1][s2]);
+    const bf16_t* gp = dy + (((long)n * Ho + h0) * Wo + w) * C + c;
+    for (int h = r0; h < r1; ++h) {
+      const uint2 gv = *(const uint2*)(gp + (long)h * Wo * C);
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          win[0][s2][q] = win[1][s2][q];
+          win[1][s2][q] = win[2][s2][q];
+        }
+        unpack4x2(ldt((h + 2) * pitch + pw + s2), win[2][s2]);
+      }
+      f32x2 gf[2];
+      unpack4x2(gv, gf);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            acc[r * 3 + s2][q] = __builtin_elementwise_fma(win[r][s2][q], gf[q], acc[r * 3 + s2][q]);
+      dsum[0] = dsum[0] + gf[0];
+      dsum[1] = dsum[1] + gf[1];
+    }
+  }
+  // reduce over the lanes that share a channel lane: within a wave the 4 column lanes t, t^16,
+  // t^32, t^48, then the waves through LDS (the staged tile is dead: reuse its space)
+  __syncthreads();
+  float* red = (float*)tile;  // [waves][16 channel lanes][40]
+  const int wv = t >> 6, lane = t & 63, nwv = blockDim.x >> 6;
+  float v[40];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    v[k * 4 + 0] = acc[k][0].x;
+    v[k * 4 + 1] = acc[k][0].y;
+    v[k * 4 + 2] = acc[k][1].x;
+    v[k * 4 + 3] = acc[k][1].y;
+  }
+  v[36] = dsum[0].x;
+  v[37] = dsum[0].y;
+  v[38] = dsum[1].x;
+  v[39] = dsum[1].y;
+#pragma unroll
+  for (int j = 0; j < 40; ++j) {
+    v[j] += __shfl_xor(v[j], 16, 64);
+    v[j] += __shfl_xor(v[j], 32, 64);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 40; ++j) red[(wv * 16 + lane) * 40 + j] = v[j];
+  }
+  __syncthreads();
+  const long slab = blockIdx.x;
+  for (int i = t; i < 16 * 40; i += blockDim.x) {
+    const int l = i / 40, j = i - l * 40;
+    float sum = 0.f;
+    for (int q = 0; q < nwv; ++q) sum += red[(q * 16 + l) * 40 + j];
+    const int c = cg0 + l * 4 + (j & 3);
+    if (c >= C) continue;
+    if (j < 36)
+      ws_w[(slab * 9 + (j >> 2)) * C + c] = sum;
+    else if (ws_b)
+      ws_b[slab * C + c] = sum;
+  }
+}
+
 int dw_tile_grid(int ntiles, int C, bool stats) {
   if (!stats) return ntiles;
   static const int target = [] {
@@ -868,8 +990,8 @@ int dw_tile_grid(int ntiles, int C, bool stats) {
   return std::max(1, std::min(ntiles, cdiv(target, cg)));
 }
 
-// balanced tiling of an Ho × Wo output: tw ≤ 32 columns, tr ≤ 8 rows, rg = 32 / tw row groups
-// (≤ 16 · 32 = 512 threads)
+// balanced tiling of an Ho × Wo output: tw ≤ 32 columns, tr as tall as the LDS bound allows,
+// rg = 32 / tw row groups (≤ 16 · 32 = 512 threads)
 struct DwTileGeom {
   int tr, tw, rg, th, twn, nt;
 };
@@ -1196,8 +1318,25 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
 }
 
 // slab rows for the row-oriented wgrad (0: generic atomic kernel)
+// the tile weight gradient (stride-1 3×3, like the forward tile kernel; TDL_DW_WG_TILE=0: the
+// sliding-window kernel): one slab per workgroup, ≈2048 workgroups
+namespace {
+bool dw_wgrad_tile_ok(const DwArgs& a) {
+  const char* e = getenv("TDL_DW_WG_TILE");  // (read per call: tools/dw_micro.py A/Bs in-process)
+  const bool on = e == nullptr || atoi(e) != 0;
+  return on && slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C) &&
+         dw_tile_fits(a.Ho, a.Wo, a.C);
+}
+int dw_wgrad_tile_grid(const DwArgs& a) {
+  const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
+  const int ntiles = a.N * g.th * g.twn;
+  return std::max(1, std::min(ntiles, cdiv(2048, cdiv(a.C, DT_CH))));
+}
+}  // namespace
+
 int dwconv_wgrad_slabs(const DwArgs& a) {
   if (!(a.C % 8 == 0 && a.R * a.S == 9)) return 0;
+  if (dw_wgrad_tile_ok(a)) return dw_wgrad_tile_grid(a);
   const int rows = a.N * a.Ho;
   const RowGeom g = row_geom(a.C / 8);
   const int groups = cdiv(a.C / 8, g.lanes_c);
@@ -1216,7 +1355,16 @@ void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st) {
     dim3 grid((unsigned)slabs, (unsigned)cdiv(a.C / 8, g.lanes_c));
     float* ws_w = ws;
     float* ws_b = ws + (long)slabs * 9 * a.C;
-    if (slide_ok(a)) {
+    if (dw_wgrad_tile_ok(a)) {
+      const DwTileGeom tg = dw_tile_geom(a.Ho, a.Wo);
+      const int ntiles = a.N * tg.th * tg.twn;
+      const size_t smem = std::max(dw_tile_smem(tg, false), (size_t)(tg.nt / 64) * 16 * 40 * 4);
+      auto k = a.aff ? dw_wgrad_tile_kernel<false, true>
+               : a.relu_in ? dw_wgrad_tile_kernel<true, false> : dw_wgrad_tile_kernel<false, false>;
+      hipLaunchKernelGGL(k, dim3((unsigned)slabs, (unsigned)cdiv(a.C, DT_CH)), dim3(tg.nt), smem, st,
+                         a.x, a.dy, a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, tg.tr, tg.tw, tg.rg,
+                         tg.th, tg.twn, ntiles, a.aff, a.aff_ld, ws_w, a.db ? ws_b : nullptr);
+    } else if (slide_ok(a)) {
       const SlideGeom sg = slide_geom(a.C / 8, a.Wo);
       hipLaunchKernelGGL(dw_wgrad_slide, grid, dim3(NT), 0, st, a, sg.lanes_c, sg.rpp, sg.seg, rpb,
                          ws_w, ws_b);

@@ -887,7 +887,8 @@ def test_xception_fused_bn_statistics_match_reduce_passes(gpu, monkeypatch):
 
 
 def _unfused_sep_forward(mod):
-    def fwd(x, relu_in=False, residual=None, join=None, res_join=None):
+    def fwd(x, relu_in=False, residual=None, join=None, res_join=None, defer=False):
+        # (``defer`` ignored: this conv's output BN is applied here, nothing is deferred)
         yy = mod.depthwise(x, relu_in=relu_in, join=join)
         yy = mod.dw_bn(yy, relu=mod.act_inside)
         return mod.pointwise(yy, residual=residual, res_join=res_join)

@@ -1,4 +1,6 @@
-"""Depthwise 3×3 forward / dgrad at Xception-41 b128 shapes: µs and HBM-equivalent TB/s."""
+"""Depthwise 3×3 forward / dgrad / wgrad at Xception-41 b128 shapes: µs and HBM-equivalent TB/s
+(wgrad: the tile kernel vs the sliding-window kernel, TDL_DW_WG_TILE=0, same process)."""
+import os
 import sys
 
 import torch
@@ -29,13 +31,21 @@ for (hw, c) in [(19, 728), (150, 128), (75, 256), (38, 728)]:
     d = lambda: ext().dwconv_dgrad(x, w, y, 1, 1, 1, 1, 1, 1, None)
     mb = x.numel() * 2 / 1e6
     tf, td = t(f), t(d)
+    gw = torch.zeros(3, 3, c, device="cuda")
+    wg = lambda: ext().dwconv_wgrad(y, x, gw, None, 1, 1, 1, 1, 1, 1, False, False)
+    res = {}
+    for on in ("0", "1", "0", "1"):
+        os.environ["TDL_DW_WG_TILE"] = on
+        res.setdefault(on, []).append(t(wg))
+    os.environ.pop("TDL_DW_WG_TILE", None)
+    w0, w1 = min(res["0"]), min(res["1"])
     print(f"{hw}x{hw}x{c}: fwd {tf:7.1f} us ({2 * mb / tf:4.2f} TB/s)  dgrad {td:7.1f} us "
-          f"({2 * mb / td:4.2f} TB/s)", flush=True)
+          f"({2 * mb / td:4.2f} TB/s)  wgrad slide {w0:7.1f} -> tile {w1:7.1f} us "
+          f"({2 * mb / w1:4.2f} TB/s)", flush=True)
     del x, y
 
 # stride-2 input gradients (Xception's strided separable convs, fixed padding 1): the 2x2-block
 # kernel vs the row kernel (TDL_DW_S2_OFF=1), same process
-import os  # noqa: E402
 for (hw, c) in [(150, 128), (75, 256), (38, 728), (19, 1024)]:
     ho = (hw + 2 - 3) // 2 + 1
     dy = torch.randn(128, ho, ho, c, device="cuda").bfloat16()
