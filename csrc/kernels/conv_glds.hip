@@ -1230,7 +1230,10 @@ bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
   const GCfg& g = cfg_of(cfg);
   const long tiles = (long)cdiv(a.M, g.bm) * cdiv(a.Ng, g.bn);
   const int nkt = cdiv(a.Kg, BK);
-  const int target = env_int("TDL_GLDS_WGRAD_TARGET", 256);
+  // ≈ tile-splits per launch (TDL_GLDS_WGRAD_TARGET): 128 (half a wave of CUs; fewer fp32 slabs to
+  // write and reduce) vs 256 / 512: Xception-41 b128 3,260 / 3,223 / 3,193 img/s, ResNet-50 b1024
+  // 13,316 / 13,273 / 13,084 (same box)
+  const int target = env_int("TDL_GLDS_WGRAD_TARGET", 128);
   int s = (int)std::max<long>(1, std::min<long>(nkt, (target + tiles - 1) / tiles));
   int per = std::max(cdiv(nkt, s), env_int("TDL_GLDS_WGRAD_MINSTEPS", 16));
   s = cdiv(nkt, per);

@@ -77,9 +77,9 @@ def test_dwfold_module_matches_unfolded_gpu(monkeypatch, gpu):
         return float(p @ q / (p.norm() * q.norm() + 1e-30))
     # the kernels are exact (test below), but the BN statistics are fp32 atomic sums in run order
     # (two unfolded runs differ the same way), and bf16 rounding flips propagate from there
-    assert cos(ya, yb) > 0.9999
+    assert cos(ya, yb) > 0.999
     assert (ya.float() - yb.float()).abs().mean() < 1e-2 * yb.float().abs().mean()
-    assert cos(gxa, gxb) > 0.9999
+    assert cos(gxa, gxb) > 0.999
     pa_all = dict(a.named_parameters())
     for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
         if n.endswith("dw_bn.beta"):
