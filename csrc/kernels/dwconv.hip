@@ -654,9 +654,10 @@ constexpr int DT_NT = 512;  // tile-kernel workgroup cap (16 channel lanes Ã— â‰
 // the weight-gradient tile kernel.
 template <bool AFF>
 __device__ __forceinline__ void dw_stage_tile(uint4* tile, const bf16_t* __restrict__ src, int Hi,
-                                              int Wi, int C, int h0, int w0, int Ph, int Pw,
-                                              int pitch, int chunks, int cg0, int t,
+                                              int Wi, int C, int ih0, int iw0, int pitch,
+                                              int chunks, int cg0, int t,
                                               const float* __restrict__ aff, int aff_ld) {
+  // (ih0, iw0): the input pixel of the halo's top-left corner (may be negative: padding)
   // staging: LDS-DMA, one 1-KiB piece (64 lanes Ã— 16 B, lane-linear in LDS) per wave instruction;
   // padding / ragged chunks read past the range-checked descriptor (zeros).  No per-chunk branch
   // around a load, so the pieces stream back-to-back instead of one latency each.
@@ -666,7 +667,7 @@ __device__ __forceinline__ void dw_stage_tile(uint4* tile, const bf16_t* __restr
     for (int j = t >> 6; j * 64 < chunks; j += nwv) {
       const int i = j * 64 + ln, k = i & 7, pix = i >> 3;
       const int r = pix / pitch, cc = pix - r * pitch;
-      const int hi = h0 - Ph + r, wi = w0 - Pw + cc, ch = cg0 + k * 8;
+      const int hi = ih0 + r, wi = iw0 + cc, ch = cg0 + k * 8;
       const bool ok = i < chunks && (unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi &&
                       ch < C;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)((char*)tile + j * 1024), 16,
@@ -693,7 +694,7 @@ __device__ __forceinline__ void dw_stage_tile(uint4* tile, const bf16_t* __restr
       const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       for (int i = t; i < chunks; i += blockDim.x) {
         const int pix = i >> 3, r = pix / pitch, cc = pix - r * pitch;
-        const int hi = h0 - Ph + r, wi = w0 - Pw + cc;
+        const int hi = ih0 + r, wi = iw0 + cc;
         if ((unsigned)hi < (unsigned)Hi && (unsigned)wi < (unsigned)Wi) {
           float v[8];
           unpack8(tile[i], v);
@@ -707,7 +708,7 @@ __device__ __forceinline__ void dw_stage_tile(uint4* tile, const bf16_t* __restr
   }
 }
 
-template <bool FLIP, bool RIN, bool AFF = false>
+template <bool FLIP, bool RIN, bool AFF = false, int ST = 1>
 __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restrict__ in,
                                                         const bf16_t* __restrict__ wt,
                                                         const float* __restrict__ bias,
@@ -744,11 +745,13 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
   b /= tiles_w;
   const int ty = b % tiles_h;
   const int n = b / tiles_h;
+  static_assert(ST == 1 || (ST == 2 && !FLIP), "stride 2: forward only");
   const int h0 = ty * tr, w0 = tx * tw;
-  const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
+  // the halo: (trâˆ’1)Â·ST + 3 input rows Ã— (twâˆ’1)Â·ST + 3 columns
+  const int pitch = (tw - 1) * ST + 3, chunks = ((tr - 1) * ST + 3) * pitch * 8;
   const bf16_t* src = in + (long)n * Hi * Wi * C;
-  dw_stage_tile<!FLIP && AFF>(tile, src, Hi, Wi, C, h0, w0, Ph, Pw, pitch, chunks, cg0, t, aff,
-                              aff_ld);
+  dw_stage_tile<!FLIP && AFF>(tile, src, Hi, Wi, C, h0 * ST - Ph, w0 * ST - Pw, pitch, chunks, cg0,
+                              t, aff, aff_ld);
   const int pw = rest % tw, g = rest / tw;
   const int w = w0 + pw, c = cg0 + cl * 4;
   const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
@@ -765,19 +768,33 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
   for (int q = 0; q < 2; ++q)
     bb[q] = bias ? f32x2{bias[c + 2 * q], bias[c + 2 * q + 1]} : f32x2{0.f, 0.f};
   f32x2 win[3][3][2];
+  const int pc = pw * ST;  // this lane's window columns pc â€¦ pc+2 of the halo
+  if constexpr (ST == 1) {
 #pragma unroll
-  for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt((r0 + r) * pitch + pw + s2), win[r + 1][s2]);
+      for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt((r0 + r) * pitch + pc + s2), win[r + 1][s2]);
+  } else {
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt(r0 * ST * pitch + pc + s2), win[2][s2]);
+  }
   for (int h = r0; h < r1; ++h) {
+    // slide the window down to output row h (input rows hÂ·ST â€¦ hÂ·ST+2)
 #pragma unroll
     for (int s2 = 0; s2 < 3; ++s2) {
+      if constexpr (ST == 1) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        win[0][s2][q] = win[1][s2][q];
-        win[1][s2][q] = win[2][s2][q];
+        for (int q = 0; q < 2; ++q) {
+          win[0][s2][q] = win[1][s2][q];
+          win[1][s2][q] = win[2][s2][q];
+        }
+        unpack4x2(ldt((h + 2) * pitch + pc + s2), win[2][s2]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) win[0][s2][q] = win[2][s2][q];
+        unpack4x2(ldt((h * ST + 1) * pitch + pc + s2), win[1][s2]);
+        unpack4x2(ldt((h * ST + 2) * pitch + pc + s2), win[2][s2]);
       }
-      unpack4x2(ldt((h + 2) * pitch + pw + s2), win[2][s2]);
     }
     f32x2 acc[2] = {bb[0], bb[1]};
 #pragma unroll
@@ -879,7 +896,7 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
 // share a channel lane, then the waves through LDS, written to slab blockIdx.x (the caller's
 // split-K reduce sums the slabs).  The sliding-window kernel below unpacks its packed window
 // 9Ã— per output (144 VALU per 8 channels per output vs â‰ˆ30 per 4 here).
-template <bool RIN, bool AFF>
+template <bool RIN, bool AFF, int ST = 1>
 __global__ void __launch_bounds__(DT_NT, 4) dw_wgrad_tile_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, int Hi, int Wi, int Ho, int Wo,
     int C, int Ph, int Pw, int tr, int tw, int rg, int tiles_h, int tiles_w, int ntiles,
@@ -900,9 +917,9 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_wgrad_tile_kernel(
     const int ty = b % tiles_h;
     const int n = b / tiles_h;
     const int h0 = ty * tr, w0 = tx * tw;
-    const int pitch = tw + 2, chunks = (tr + 2) * pitch * 8;
-    dw_stage_tile<AFF>(tile, x + (long)n * Hi * Wi * C, Hi, Wi, C, h0, w0, Ph, Pw, pitch, chunks,
-                       cg0, t, aff, aff_ld);
+    const int pitch = (tw - 1) * ST + 3, chunks = ((tr - 1) * ST + 3) * pitch * 8;
+    dw_stage_tile<AFF>(tile, x + (long)n * Hi * Wi * C, Hi, Wi, C, h0 * ST - Ph, w0 * ST - Pw, pitch,
+                       chunks, cg0, t, aff, aff_ld);
     const int pw = rest % tw, g = rest / tw;
     const int w = w0 + pw, c = cg0 + cl * 4;
     const int rpg = (tr + rg - 1) / rg, r0 = g * rpg;
@@ -910,21 +927,34 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_wgrad_tile_kernel(
     if (g >= rg || w >= Wo || c >= C || r0 >= r1) continue;
     auto ldt = [&](int pix) { const uint2 v = tile2[pix * 16 + cl]; return RIN ? relu4(v) : v; };
     f32x2 win[3][3][2];
+    const int pc = pw * ST;
+    if constexpr (ST == 1) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+      for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt((r0 + r) * pitch + pw + s2), win[r + 1][s2]);
+        for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt((r0 + r) * pitch + pc + s2), win[r + 1][s2]);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) unpack4x2(ldt(r0 * ST * pitch + pc + s2), win[2][s2]);
+    }
     const bf16_t* gp = dy + (((long)n * Ho + h0) * Wo + w) * C + c;
     for (int h = r0; h < r1; ++h) {
       const uint2 gv = *(const uint2*)(gp + (long)h * Wo * C);
 #pragma unroll
       for (int s2 = 0; s2 < 3; ++s2) {
+        if constexpr (ST == 1) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          win[0][s2][q] = win[1][s2][q];
-          win[1][s2][q] = win[2][s2][q];
+          for (int q = 0; q < 2; ++q) {
+            win[0][s2][q] = win[1][s2][q];
+            win[1][s2][q] = win[2][s2][q];
+          }
+          unpack4x2(ldt((h + 2) * pitch + pc + s2), win[2][s2]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) win[0][s2][q] = win[2][s2][q];
+          unpack4x2(ldt((h * ST + 1) * pitch + pc + s2), win[1][s2]);
+          unpack4x2(ldt((h * ST + 2) * pitch + pc + s2), win[2][s2]);
         }
-        unpack4x2(ldt((h + 2) * pitch + pw + s2), win[2][s2]);
       }
       f32x2 gf[2];
       unpack4x2(gv, gf);
@@ -993,9 +1023,11 @@ int dw_tile_grid(int ntiles, int C, bool stats) {
 // balanced tiling of an Ho Ã— Wo output: tw â‰¤ 32 columns, tr as tall as the LDS bound allows,
 // rg = 32 / tw row groups (â‰¤ 16 Â· 32 = 512 threads)
 struct DwTileGeom {
-  int tr, tw, rg, th, twn, nt;
+  int tr, tw, rg, th, twn, nt, st;
+  // 1-KiB DMA pieces of the (trâˆ’1)Â·st+3 Ã— (twâˆ’1)Â·st+3-pixel Ã— 64-channel input halo
+  long pieces() const { return cdiv(((tr - 1) * st + 3) * ((tw - 1) * st + 3) * 8, 64); }
 };
-DwTileGeom dw_tile_geom(int Ho, int Wo) {
+DwTileGeom dw_tile_geom(int Ho, int Wo, int st = 1) {
   // rows per tile: as many as the 64 KiB LDS bound below allows (TDL_DW_TR caps it; 8 was the
   // round-4 default â€” Xception b128 shapes 10â€“14 % faster with taller tiles: fewer halo re-reads
   // per output, and the workgroups per CU are LDS-bound either way, tools/dw_micro.py)
@@ -1004,12 +1036,13 @@ DwTileGeom dw_tile_geom(int Ho, int Wo) {
     return e ? std::max(1, std::min(32, atoi(e))) : 32;
   }();
   DwTileGeom g;
-  g.twn = cdiv(Wo, DT_TW);
+  g.st = st;
+  g.twn = cdiv(Wo, DT_TW / st);  // stride 2: â‰¤ 16 output columns (33 input columns) per tile
   g.tw = cdiv(Wo, g.twn);
   g.th = cdiv(Ho, tr_max);
   g.tr = cdiv(Ho, g.th);
   // the halo tile within the 64 KiB of dynamic LDS a launch gets without an attribute
-  while (g.tr > 1 && (long)cdiv((g.tr + 2) * (g.tw + 2) * 8, 64) * 1024 > 65536) {
+  while (g.tr > 1 && g.pieces() * 1024 > 65536) {
     ++g.th;
     g.tr = cdiv(Ho, g.th);
   }
@@ -1022,7 +1055,7 @@ DwTileGeom dw_tile_geom(int Ho, int Wo) {
 // the statistics reduction's 128 Ã— lanes floats) â€” sized to the launch, not the largest tile, so
 // small-image layers fit more workgroups per CU (56 KiB for a whole 19Ã—19 image)
 size_t dw_tile_smem(const DwTileGeom& g, bool stats) {
-  const size_t halo = (size_t)cdiv((g.tr + 2) * (g.tw + 2) * 8, 64) * 64 * 16;
+  const size_t halo = (size_t)g.pieces() * 1024;
   const size_t red = stats ? (size_t)128 * (g.nt / 16) * 4 : 0;
   return std::max(halo, red);
 }
@@ -1161,6 +1194,14 @@ bool dw_tile() {
 }
 // the tile kernel's DMA offsets are 32-bit bytes within one image
 bool dw_tile_fits(long h, long w, long c) { return h * w * c * 2 < (1L << 31) - 64; }
+// stride-2 3Ã—3 on the tile kernels (forward, weight gradient); TDL_DW_S2_TILE=0: the row kernels
+// (read per call: tools/dw_micro.py A/Bs in-process)
+bool s2_tile_ok(const DwArgs& a) {
+  const char* e = getenv("TDL_DW_S2_TILE");
+  return (e == nullptr || atoi(e) != 0) && a.C % 8 == 0 && a.R == 3 && a.S == 3 && a.sh == 2 &&
+         a.sw == 2 && a.dh == 1 && a.dwl == 1 && a.ph >= 0 && a.ph <= 2 && a.pw >= 0 &&
+         a.pw <= 2 && dw_tile() && dw_tile_fits(a.H, a.W, a.C);
+}
 
 // 4-channel sliding kernel (default; TDL_DW_VEC=8 selects the 8-channel one)
 bool slide4() {
@@ -1259,6 +1300,17 @@ bool dwconv_fwd_launch(const DwArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(dw_slide_kernel<false>, grid, dim3(NT), 0, st, a.x, a.w, a.bias, a.out, a.H,
                        a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.lanes_c, g.rpp, g.seg, a.relu_in,
                        (const bf16_t*)nullptr, (const bf16_t*)nullptr);
+  } else if (s2_tile_ok(a) && !a.aff) {
+    const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo, 2);
+    const int ntiles = a.N * g.th * g.twn;
+    dim3 grid((unsigned)dw_tile_grid(ntiles, a.C, a.stats != nullptr), (unsigned)cdiv(a.C, DT_CH));
+    auto kern = a.relu_in ? dw_tile_kernel<false, true, false, 2> : dw_tile_kernel<false, false, false, 2>;
+    hipLaunchKernelGGL(kern, grid, dim3(g.nt), dw_tile_smem(g, a.stats != nullptr),
+                       st, a.x, a.w, a.bias, a.out,
+                       a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, a.relu, g.tr, g.tw, g.rg, g.th,
+                       g.twn, (const bf16_t*)nullptr, a.stats, (const bf16_t*)nullptr,
+                       ntiles, (const bf16_t*)nullptr, (const float*)nullptr, 0);
+    return a.stats != nullptr;
   } else if (a.C % 8 == 0 && a.R * a.S == 9) {
     const RowGeom g = row_geom(a.C / 8);
     dim3 grid((unsigned)(a.N * a.Ho), (unsigned)cdiv(a.C / 8, g.lanes_c));
@@ -1324,11 +1376,12 @@ namespace {
 bool dw_wgrad_tile_ok(const DwArgs& a) {
   const char* e = getenv("TDL_DW_WG_TILE");  // (read per call: tools/dw_micro.py A/Bs in-process)
   const bool on = e == nullptr || atoi(e) != 0;
-  return on && slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C) &&
-         dw_tile_fits(a.Ho, a.Wo, a.C);
+  return on && ((slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C) &&
+                 dw_tile_fits(a.Ho, a.Wo, a.C)) ||
+                (s2_tile_ok(a) && !a.aff));
 }
 int dw_wgrad_tile_grid(const DwArgs& a) {
-  const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo);
+  const DwTileGeom g = dw_tile_geom(a.Ho, a.Wo, a.sh);
   const int ntiles = a.N * g.th * g.twn;
   return std::max(1, std::min(ntiles, cdiv(2048, cdiv(a.C, DT_CH))));
 }
@@ -1356,10 +1409,12 @@ void dwconv_wgrad_launch(const DwArgs& a, float* ws, hipStream_t st) {
     float* ws_w = ws;
     float* ws_b = ws + (long)slabs * 9 * a.C;
     if (dw_wgrad_tile_ok(a)) {
-      const DwTileGeom tg = dw_tile_geom(a.Ho, a.Wo);
+      const DwTileGeom tg = dw_tile_geom(a.Ho, a.Wo, a.sh);
       const int ntiles = a.N * tg.th * tg.twn;
       const size_t smem = std::max(dw_tile_smem(tg, false), (size_t)(tg.nt / 64) * 16 * 40 * 4);
-      auto k = a.aff ? dw_wgrad_tile_kernel<false, true>
+      auto k = a.sh == 2 ? (a.relu_in ? dw_wgrad_tile_kernel<true, false, 2>
+                                      : dw_wgrad_tile_kernel<false, false, 2>)
+               : a.aff ? dw_wgrad_tile_kernel<false, true>
                : a.relu_in ? dw_wgrad_tile_kernel<true, false> : dw_wgrad_tile_kernel<false, false>;
       hipLaunchKernelGGL(k, dim3((unsigned)slabs, (unsigned)cdiv(a.C, DT_CH)), dim3(tg.nt), smem, st,
                          a.x, a.dy, a.H, a.W, a.Ho, a.Wo, a.C, a.ph, a.pw, tg.tr, tg.tw, tg.rg,

@@ -64,3 +64,23 @@ for (hw, c) in [(150, 128), (75, 256), (38, 728), (19, 1024)]:
     print(f"s2 dgrad {hw}x{hw}x{c}: rows {a:7.1f} us ({mb / a:4.2f} TB/s) -> 2x2 blocks {b:7.1f} us "
           f"({mb / b:4.2f} TB/s)", flush=True)
     del dy, dx
+
+# stride-2 forward / weight gradient: the tile kernels vs the row kernels (TDL_DW_S2_TILE=0)
+for (hw, c) in [(150, 128), (75, 256), (38, 728), (19, 1024)]:
+    ho = (hw + 2 - 3) // 2 + 1
+    x = torch.randn(128, hw, hw, c, device="cuda").bfloat16()
+    w = (torch.randn(3, 3, c, device="cuda") * 0.3).bfloat16()
+    y = torch.empty(128, ho, ho, c, device="cuda").bfloat16()
+    gw = torch.zeros(3, 3, c, device="cuda")
+    f = lambda: ext().dwconv_fwd(x, w, None, y, 2, 2, 1, 1, 1, 1, False, False)
+    g = lambda: ext().dwconv_wgrad(y, x, gw, None, 2, 2, 1, 1, 1, 1, False, False)
+    res = {}
+    for on in ("0", "1", "0", "1"):
+        os.environ["TDL_DW_S2_TILE"] = on
+        res.setdefault(on, []).append((t(f), t(g)))
+    os.environ.pop("TDL_DW_S2_TILE", None)
+    (f0, g0), (f1, g1) = (min(v) for v in (res["0"], res["1"]))
+    mb = (x.numel() + y.numel()) * 2 / 1e6
+    print(f"s2 {hw}x{hw}x{c}: fwd rows {f0:7.1f} -> tile {f1:7.1f} us ({mb / f1:4.2f} TB/s)  "
+          f"wgrad rows {g0:7.1f} -> tile {g1:7.1f} us", flush=True)
+    del x, y
