@@ -1224,7 +1224,8 @@ bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
   const bool stem = (stem_env ? atoi(stem_env) : 0) != 0 && a.M <= 64 && a.Ng > 128 &&
                     a.Ng <= 256 && (long)a.Kg >= 65536;
   // default: 1×1 filters with ≥ 256 output channels (3×3 gathers of x favour the other kernel)
-  if (mode == 1 && !stem && ((long)a.Kg < 4096 || a.M < 256 || a.R * a.S != 1)) return false;
+  static const int mmin = env_int("TDL_GLDS_WGRAD_MMIN", 256);
+  if (mode == 1 && !stem && ((long)a.Kg < 4096 || a.M < mmin || a.R * a.S != 1)) return false;
   int cfg = stem ? 7 : a.M <= 128 ? 2 : 0;
   cfg = env_int("TDL_GLDS_CFG_WGRAD", cfg);
   const GCfg& g = cfg_of(cfg);

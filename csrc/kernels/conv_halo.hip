@@ -811,7 +811,8 @@ bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p) {
   if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
   // default: ≥ 128 input channels and enough pixel tiles to split over the chip (ResNet-50 b1024
   // layers 2–4: 362 → 328 / 295 / 290 µs; the small-batch DeepLab shapes stay on the GEMMs)
-  if (conv_halo_mode() == 1 && (a.C < 128 || (long)a.N * a.Ho * a.Wo < 65536)) return false;
+  static const int cmin = henv("TDL_HALO_WG_CMIN", 128);
+  if (conv_halo_mode() == 1 && (a.C < cmin || (long)a.N * a.Ho * a.Wo < 65536)) return false;
   HaloGeom g;
   HaloWg q;
   int bm;
