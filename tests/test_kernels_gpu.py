@@ -1106,3 +1106,32 @@ def test_join_dadd_kernels(gpu, dtype):
     buf = prev.clone()
     ext().avgpool_bwd(g, buf, buf)
     assert rel_err(buf, plain.float() + prev.float()) <= (1e-6 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("hw,c,stride,relu_in", [(75, 256, 1, False), (150, 64, 1, True),
+                                                 (38, 728, 1, False), (75, 128, 2, False),
+                                                 (38, 256, 2, True), (19, 1024, 2, False)])
+def test_depthwise_tiles_at_xception_scale(gpu, hw, c, stride, relu_in):
+    """The LDS tile kernels on Xception-sized maps — several tile bands and column tiles per image
+    (tiles as tall as 64 KiB of LDS allows), ragged last tiles, 728 = 11·64 + 24 channels —
+    forward, input gradient and the tile weight gradient (stride 1 and 2) against fp32 PyTorch."""
+    from tensorflowdistributedlearning_amd.models.layers import resolve_padding
+    torch.manual_seed(hw + c + stride)
+    pad = resolve_padding("SAME" if stride == 1 else (1, 1, 1, 1), hw, hw, 3, 3,
+                          (stride, stride), (1, 1))
+    g = C.ConvGeom((stride, stride), pad, (1, 1))
+    x = torch.randn(2, hw, hw, c).bfloat16()
+    w = (torch.randn(3, 3, c) * 0.3).bfloat16()
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = D.ref_dw_fwd(torch.relu(xr) if relu_in else xr, wr, g)
+    wp = torch.nn.Parameter(w.float().to(gpu))
+    wp._lowp = w.to(gpu)
+    xg = x.to(gpu).requires_grad_(True)
+    y = D.depthwise_conv2d(xg, wp, None, g, False, relu_in)
+    assert rel_err(y, yr) < 2e-2
+    dy = torch.randn(yr.shape).bfloat16()
+    yr.backward(dy.float())
+    y.backward(dy.to(gpu))
+    assert rel_err(xg.grad, xr.grad) < 2e-2
+    assert rel_err(wp.grad, wr.grad) < 2e-2
