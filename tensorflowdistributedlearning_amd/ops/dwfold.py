@@ -50,6 +50,9 @@ class DeferredBNAct:
         return self.bn(self.z, stats=self.stats, relu=True)
 
 
+_FOLDABLE = {}  # (shape, padding) -> the kernels' answer (asked once per geometry)
+
+
 def foldable(z, layer):
     """Can ``layer`` (models.layers.DepthwiseConv2d) consume BN + ReLU of ``z`` folded?"""
     if not (ENABLED and on_gpu(z) and z.dtype == torch.bfloat16 and layer.k == 3
@@ -61,8 +64,12 @@ def foldable(z, layer):
                           layer.dilation)
     if pad[0] != pad[1] or pad[2] != pad[3]:
         return False
-    w = torch.empty((3, 3, z.shape[-1]), dtype=torch.bfloat16, device="meta")
-    return bool(ext().dwconv_aff_ok(z, w, 1, 1, pad[0], pad[2], 1, 1))
+    key = (tuple(z.shape), pad)
+    ok = _FOLDABLE.get(key)
+    if ok is None:
+        w = torch.empty((3, 3, z.shape[-1]), dtype=torch.bfloat16, device="meta")
+        ok = _FOLDABLE[key] = bool(ext().dwconv_aff_ok(z, w, 1, 1, pad[0], pad[2], 1, 1))
+    return ok
 
 
 class _BNActDwFn(torch.autograd.Function):
