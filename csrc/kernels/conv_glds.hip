@@ -918,6 +918,16 @@ void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), lds, st, a);
 }
 
+// the tile configs launch_gcfg instantiates for (mode, statistics): an environment override
+// (TDL_GLDS_CFG_*) outside them keeps the default — the tile count is computed from cfg_of(cfg),
+// so a config the launcher does not have would leave output tiles unwritten
+bool cfg_valid(int mode, bool stats, int cfg) {
+  if (cfg >= 0 && cfg <= 4) return true;
+  if (cfg == 6) return mode == DGRAD && stats;
+  if (cfg == 7) return mode == WGRAD;
+  return false;
+}
+
 template <int MODE, bool STATS, bool BIAS, int FK, bool NJ = false>
 void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
   if (cfg == 0)
@@ -1032,7 +1042,7 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
   int cfg = a.Ng <= 64 ? 4 : 0;
-  cfg = env_int("TDL_GLDS_CFG_FWD", cfg);
+  if (const int e = env_int("TDL_GLDS_CFG_FWD", cfg); cfg_valid(FWD, false, e)) cfg = e;
   const GCfg& g = cfg_of(cfg);
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
   // fewer than half a tile per CU: the register-staged kernel's smaller tiles and two workgroups
@@ -1132,7 +1142,8 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
   int cfg = a.Ng <= 64 ? (a.fp8 ? 1 : 4) : 0;
-  if (!a.fp8) cfg = env_int("TDL_GLDS_CFG_DGRAD", cfg);
+  if (const int e = env_int("TDL_GLDS_CFG_DGRAD", cfg); !a.fp8 && cfg_valid(DGRAD, false, e))
+    cfg = e;
   const GCfg& g = cfg_of(cfg);
   a.cls_tile0[0] = 0;
   for (int c = 0; c < a.ncls; ++c) {
@@ -1156,8 +1167,9 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
     // tile config (tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
     // tiles (NJ: no previous-dx registers); with the join's previous-dx loads as well they spill,
     // so 8 waves of 32×64 (cfg 6); 64-wide dx: the 8-wave 256×64 tiles
-    const int scfg = env_int(a.beta ? "TDL_GLDS_CFG_DGSTAT_J" : "TDL_GLDS_CFG_DGSTAT",
-                             a.Ng <= 64 ? 4 : (a.beta ? 6 : 0));
+    const int sdef = a.Ng <= 64 ? 4 : (a.beta ? 6 : 0);
+    const int senv = env_int(a.beta ? "TDL_GLDS_CFG_DGSTAT_J" : "TDL_GLDS_CFG_DGSTAT", sdef);
+    const int scfg = cfg_valid(DGRAD, true, senv) ? senv : sdef;
     const GCfg& g = cfg_of(scfg);
     const long ntn = cdiv(a.Ng, g.bn);
     long ntm_all = 0, ntm_max = 1;
@@ -1227,7 +1239,7 @@ bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
   static const int mmin = env_int("TDL_GLDS_WGRAD_MMIN", 256);
   if (mode == 1 && !stem && ((long)a.Kg < 4096 || a.M < mmin || a.R * a.S != 1)) return false;
   int cfg = stem ? 7 : a.M <= 128 ? 2 : 0;
-  cfg = env_int("TDL_GLDS_CFG_WGRAD", cfg);
+  if (const int e = env_int("TDL_GLDS_CFG_WGRAD", cfg); cfg_valid(WGRAD, false, e)) cfg = e;
   const GCfg& g = cfg_of(cfg);
   const long tiles = (long)cdiv(a.M, g.bm) * cdiv(a.Ng, g.bn);
   const int nkt = cdiv(a.Kg, BK);
