@@ -867,26 +867,22 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_tile_kernel(const bf16_t* __restr
     // workgroup reduction over the lanes of each of the 64 channels (the LDS tile is free now),
     // then one atomic pair per channel
     __syncthreads();
+    // layout [2][L lanes][64 channels]: a lane's 4 channels are one 16-B store and the summing
+    // threads read consecutive channels (no bank conflicts either way)
     float* red = (float*)tile;
     const int L = blockDim.x >> 4;  // lanes per channel lane (≤ 32)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      red[(cl * 4 + j) * L + rest] = ss[j];
-      red[(64 + cl * 4 + j) * L + rest] = sq[j];
-    }
+    *(float4*)(red + rest * 64 + cl * 4) = make_float4(ss[0], ss[1], ss[2], ss[3]);
+    *(float4*)(red + (L + rest) * 64 + cl * 4) = make_float4(sq[0], sq[1], sq[2], sq[3]);
     __syncthreads();
     for (int o = t; o < 128; o += blockDim.x) {  // (64-thread workgroups for tiny images)
       const int which = o >> 6, ch = o & 63;
       float v = 0.f;
-      for (int i = 0; i < L; ++i) v += red[(which * 64 + ch) * L + i];
+      for (int i = 0; i < L; ++i) v += red[(which * L + i) * 64 + ch];
       if (cg0 + ch < C) atomicAdd(stats + which * C + cg0 + ch, v);
     }
   }
 }
 
-// tile-kernel grid (x): every tile its own workgroup, except with fused statistics — then
-// ≈ TDL_DW_STAT_WG workgroups in all, each walking several tiles and flushing its sums once
-// (one atomic pair per channel per workgroup instead of per tile)
 // Weight gradient on the tile machinery: a workgroup walks output tiles (blockIdx.x, +gridDim.x,
 // …), stages each tile's input halo in LDS exactly as the forward does (RIN: input ReLU on the LDS
 // read; AFF: the folded BN + ReLU applied to the staged tile), and every lane (4 channels × one
@@ -1010,6 +1006,9 @@ __global__ void __launch_bounds__(DT_NT, 4) dw_wgrad_tile_kernel(
   }
 }
 
+// tile-kernel grid (x): every tile its own workgroup, except with fused statistics — then
+// ≈ TDL_DW_STAT_WG workgroups in all, each walking several tiles and flushing its sums once
+// (one atomic pair per channel per workgroup instead of per tile)
 int dw_tile_grid(int ntiles, int C, bool stats) {
   if (!stats) return ntiles;
   static const int target = [] {
