@@ -67,9 +67,21 @@ class ArrayImages:
         self.std = np.asarray(std if std is not None else af.std(0) + 1e-6, dtype=np.float32)
 
     def batch(self, ids, labels, device, dtype, gen_seed):
-        x = torch.from_numpy(self.images[np.asarray(ids)].astype(np.float32) / self.scale)
-        x = (x - torch.from_numpy(self.mean)) / torch.from_numpy(self.std)
-        return x.to(device)
+        """The raw samples cross to the device as stored (uint8: a quarter of the fp32 bytes, from
+        pinned memory, asynchronously) and are normalised there — host fp32 normalisation of a
+        299² batch cost tens of ms per step on the training thread."""
+        dev = torch.device(device)
+        raw = torch.from_numpy(np.ascontiguousarray(self.images[np.asarray(ids)]))
+        if dev.type == "cuda":
+            raw = raw.pin_memory().to(dev, non_blocking=True)
+        st = self.__dict__.setdefault("_stats", {})
+        if dev not in st:
+            st[dev] = (torch.from_numpy(self.mean).to(dev), torch.from_numpy(self.std).to(dev))
+        mean, std = st[dev]
+        x = raw.float()
+        if self.scale != 1.0:
+            x = x / self.scale
+        return (x - mean) / std
 
 
 class ClassificationPipeline:

@@ -215,3 +215,16 @@ def test_async_saver_snapshots_before_later_updates(tmp_path, gpu):
     for _ in range(20):
         want += 1.0  # fp32 rounding as on the device
     assert float(m.weight[0, 0].cpu()) == float(want)
+
+
+def test_array_images_normalisation_matches_numpy():
+    rng = np.random.default_rng(0)
+    imgs = rng.integers(0, 256, (6, 5, 5, 3), dtype=np.uint8)
+    a = ArrayImages(imgs)
+    x = a.batch([4, 1, 2], None, "cpu", torch.float32, 0)
+    ref = (imgs[[4, 1, 2]].astype(np.float32) / 255.0 - a.mean) / a.std
+    np.testing.assert_allclose(x.numpy(), ref, rtol=1e-6, atol=1e-6)
+    f = ArrayImages(imgs.astype(np.float32) / 255.0)  # float input: no rescale
+    np.testing.assert_allclose(f.batch([0], None, "cpu", torch.float32, 0).numpy(),
+                               (imgs[[0]].astype(np.float32) / 255.0 - f.mean) / f.std,
+                               rtol=1e-5, atol=1e-5)
