@@ -228,3 +228,16 @@ def test_array_images_normalisation_matches_numpy():
     np.testing.assert_allclose(f.batch([0], None, "cpu", torch.float32, 0).numpy(),
                                (imgs[[0]].astype(np.float32) / 255.0 - f.mean) / f.std,
                                rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_array_images_on_gpu_match_cpu(gpu):
+    """The device-side normalisation of ArrayImages (pinned async copy of the raw uint8 samples)
+    equals the CPU path."""
+    rng = np.random.default_rng(1)
+    a = ArrayImages(rng.integers(0, 256, (10, 17, 17, 3), dtype=np.uint8))
+    ids = [9, 0, 3, 3]
+    g = a.batch(ids, None, gpu, torch.bfloat16, 0)
+    assert g.is_cuda and g.dtype == torch.float32
+    torch.testing.assert_close(g.cpu(), a.batch(ids, None, "cpu", torch.float32, 0),
+                               rtol=1e-6, atol=1e-6)
