@@ -35,6 +35,7 @@ class DevicePrefetcher:
         self.lock = threading.Lock()
         self.stop = threading.Event()
         self.stream = torch.cuda.Stream(self.device)
+        self.done = None  # the exception that ended the stream (re-raised by later calls)
         self.thread = threading.Thread(target=self._run, name="tdl-device-prefetch", daemon=True)
         self.thread.start()
 
@@ -69,12 +70,13 @@ class DevicePrefetcher:
         return self
 
     def __next__(self):
+        if self.done is not None:
+            raise self.done
         item = self.q.get()
         if isinstance(item, BaseException):
             self.stop.set()
-            if isinstance(item, StopIteration):
-                raise StopIteration
-            raise item
+            self.done = StopIteration() if isinstance(item, StopIteration) else item
+            raise self.done
         xd, yd, ev = item
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(ev)

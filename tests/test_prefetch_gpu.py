@@ -37,6 +37,8 @@ def test_prefetched_batches_match_pipeline(tmp_path, gpu):
         got.append((x * 1.0, y * 1.0))  # consumed on the training stream (waits on the event)
     pf.close()
     assert len(got) == len(ref) == 3  # 7 images, batch 3: the short last batch too
+    with pytest.raises(StopIteration):  # (stays ended)
+        next(pf)
     for (a, b), (c, d) in zip(got, ref):
         torch.testing.assert_close(a.cpu(), c.float(), rtol=0, atol=0)
         torch.testing.assert_close(b.cpu(), d, rtol=0, atol=0)
@@ -55,6 +57,8 @@ def test_prefetch_error_reaches_training_thread(gpu):
     pf = DevicePrefetcher(source, gpu)
     assert next(pf)[0].sum().item() == 8
     assert next(pf)[1] is None
+    with pytest.raises(RuntimeError, match="loader failed"):
+        next(pf)
     with pytest.raises(RuntimeError, match="loader failed"):
         next(pf)
     pf.close()
