@@ -960,7 +960,9 @@ bool dwconv_fwd(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_
   a.x = BF(x); a.w = BF(w); a.bias = optf(bias); a.out = BFW(y); a.relu = relu;
   TORCH_CHECK(!relu_in || (a.C % 8 == 0 && a.R * a.S == 9), "fused input ReLU: 3x3, C % 8 == 0");
   a.relu_in = relu_in;
-  if (stats.has_value() && stats->defined()) {
+  // deterministic mode: no fused statistics (epilogue atomics) — the caller's bn_stats pass
+  // reduces in a fixed order (det.hip)
+  if (stats.has_value() && stats->defined() && !deterministic()) {
     TORCH_CHECK(stats->numel() == 2 * a.C, "dwconv_fwd stats: fp32 [2, C]");
     a.stats = optfw(stats);
   }
@@ -1007,8 +1009,8 @@ bool dwconv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_
     CHECK_T(*bn_x, torch::kBFloat16);
     TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_red->numel() == 2 * a.C,
                 "dwconv_dgrad bn_x: shape of dx, bn_red fp32 [2, C]");
-    a.bn_x = BF(*bn_x);
-    a.stats = optfw(bn_red);
+    a.bn_x = BF(*bn_x);  // (the folded BN's mask source even without the sums)
+    if (!deterministic()) a.stats = optfw(bn_red);  // else the BN backward reduces itself
   }
   set_dw_aff(a, aff, "dwconv_dgrad");
   TORCH_CHECK(!a.aff || (a.bn_x && !a.mask_x), "dwconv_dgrad aff: the mask comes from bn_x");

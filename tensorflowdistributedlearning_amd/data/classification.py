@@ -61,10 +61,32 @@ class ArrayImages:
         self.channels = a.shape[-1]
         self.image_size = a.shape[1]
         scale = 255.0 if a.dtype == np.uint8 else 1.0
-        af = a.reshape(-1, a.shape[-1]).astype(np.float64) / scale
         self.scale = scale
-        self.mean = np.asarray(mean if mean is not None else af.mean(0), dtype=np.float32)
-        self.std = np.asarray(std if std is not None else af.std(0) + 1e-6, dtype=np.float32)
+        if mean is None or std is None:
+            m, s = self._channel_stats(a, scale)
+            mean = m if mean is None else mean
+            std = s if std is None else std
+        self.mean = np.asarray(mean, dtype=np.float32)
+        self.std = np.asarray(std, dtype=np.float32)
+
+    @staticmethod
+    def _channel_stats(a, scale, chunk_bytes=64 << 20):
+        """Per-channel mean / std (+1e-6) accumulated over chunks of images (float64 sums of one
+        chunk at a time: a uint8 dataset is never copied whole at 8 bytes per element)."""
+        C = a.shape[-1]
+        per_img = max(1, int(np.prod(a.shape[1:])))
+        step = max(1, chunk_bytes // (8 * per_img))
+        s1 = np.zeros(C, np.float64)
+        s2 = np.zeros(C, np.float64)
+        n = 0
+        for i in range(0, a.shape[0], step):
+            c = a[i:i + step].reshape(-1, C).astype(np.float64) / scale
+            s1 += c.sum(0)
+            s2 += (c * c).sum(0)
+            n += c.shape[0]
+        mean = s1 / max(n, 1)
+        var = np.maximum(s2 / max(n, 1) - mean * mean, 0.0)
+        return mean, np.sqrt(var) + 1e-6
 
     def batch(self, ids, labels, device, dtype, gen_seed):
         """The raw samples cross to the device as stored (uint8: a quarter of the fp32 bytes, from

@@ -198,6 +198,7 @@ class Trainer:
             torch.cuda.synchronize(self.device)
             self.optimizer.set_device_lr(True)
             step_count, global_step = self.optimizer.step_count, self.global_step
+            rolls = self.fp8_roller.rolls  # the captured roll() counts one that never ran
             _params.bump_version()  # derived weight copies (channel padding) refresh in-graph
             g = torch.cuda.CUDAGraph()
             cap_stream = None
@@ -214,6 +215,7 @@ class Trainer:
                 streams.end_capture(cap_stream)
         # capture records without executing: the host-side counters did not really advance
         self.optimizer.step_count, self.global_step = step_count, global_step
+        self.fp8_roller.rolls = rolls
         self.graph = g
         return self
 

@@ -23,8 +23,18 @@ The reference concatenates ALL gradients into one NCCL pack after the full backw
   after it waited for the compute stream, so the comm stream follows both producers and the
   compute stream is never made to wait at a bucket boundary (:meth:`GradBucketer.issue_stream`).
 
+Delivery accounting: a bucket is launched when each of its parameters has delivered its *final*
+contribution of the step, not when the hook has fired ``len(params)`` times.  ``deliver_grad``
+fires the hook on every contribution; a parameter that legitimately receives several (a weight
+used twice in the forward) declares it with ``p._tdl_contribs = n``.  A delivery beyond that
+raises — a second delivery after the bucket was launched would mean the collective read a
+gradient that was still changing — and :meth:`finish` records parameters that delivered nothing
+(unused ones, zero-filled by ``FlatParams.finish_grads``) in ``last_missing`` (an error with
+``strict=True``).  ``early_launches`` counts the collectives issued from the hooks, i.e. while
+backward was still running (the overlap), as opposed to those forced by :meth:`finish`.
+
 A ``comm_hook`` can replace the collective (used by tests to record launch order with a fake
-communicator).
+communicator, or to snapshot each bucket in stream order: tests/test_bucket_order_gpu.py).
 """
 from __future__ import annotations
 
@@ -55,8 +65,13 @@ class Bucket:
 
 class GradBucketer:
     def __init__(self, flat, ctx=None, bucket_mb=32.0, first_bucket_mb=4.0, comm_hook=None,
-                 group=None):
+                 group=None, strict=False):
         self.flat = flat
+        self.strict = strict
+        self._seen = {}          # id(param) -> contributions delivered this step
+        self.early_launches = 0  # collectives issued from hooks in the last finished step
+        self._early = 0
+        self.last_missing = []   # parameters that delivered nothing in the last finished step
         self.ctx = ctx
         self.group = group
         self.comm_hook = comm_hook
@@ -116,8 +131,22 @@ class GradBucketer:
         b = self.bucket_of.get(id(p))
         if b is None:
             return
+        k = id(p)
+        n = self._seen.get(k, 0) + 1
+        self._seen[k] = n
+        need = getattr(p, "_tdl_contribs", 1)
+        if n > need:
+            raise RuntimeError(
+                f"GradBucketer: gradient of parameter {tuple(p.shape)} (bucket {b.index}) "
+                f"delivered {n} times in one step, expected {need}"
+                + (" — its bucket's collective was already issued" if b.launched else "")
+                + "; declare extra contributions with p._tdl_contribs")
+        if n < need:
+            return
         b.pending -= 1
+        before = self.next_launch
         self._launch_ready()
+        self._early += self.next_launch - before
 
     def _launch_ready(self, force=False):
         while self.next_launch < len(self.buckets):
@@ -154,6 +183,11 @@ class GradBucketer:
         cur = streams.current(dev)
         if cur != s:
             s.wait_stream(cur)
+        else:
+            # the hook fired inside a side-stream section (a weight gradient's delivery): the
+            # bucket may also hold gradients written on the compute stream before it (BN γ/β of
+            # the folded depthwise BN, ops/bnfold.py), which the side stream has not waited for
+            s.wait_stream(streams.origin(dev))
         return s
 
     def _issue(self, b, view):
@@ -168,7 +202,13 @@ class GradBucketer:
     def finish(self):
         """After backward: launch any bucket still pending (unused parameters — their grads were
         zeroed by ``FlatParams.finish_grads``), wait for all collectives, reset for next step."""
+        missing = [p for b in self.buckets for p in b.params
+                   if self._seen.get(id(p), 0) < getattr(p, "_tdl_contribs", 1)]
         self._launch_ready(force=True)
+        self.last_missing = missing
+        self.early_launches = self._early
+        self._early = 0
+        self._seen = {}
         for b in self.buckets:
             if b.work is not None and hasattr(b.work, "wait"):
                 b.work.wait()
@@ -178,6 +218,9 @@ class GradBucketer:
         self.next_launch = 0
         if self.ctx is not None and hasattr(self.ctx, "check"):
             self.ctx.check()  # native comm watchdog: fail fast on timeout / RCCL error
+        if missing and self.strict:
+            raise RuntimeError(f"GradBucketer: {len(missing)} parameter(s) delivered no final "
+                               f"gradient this step: {[tuple(p.shape) for p in missing[:8]]}")
 
     def standalone_ms(self, reps=3):
         """Milliseconds of the step's collectives alone — every bucket issued back to back on an

@@ -83,6 +83,43 @@ def test_bucketer_reset_between_steps():
     assert log == list(range(len(b.buckets))) * 2
 
 
+def test_bucketer_counts_final_deliveries_not_hook_calls():
+    """A parameter's extra contribution raises instead of silently completing another
+    parameter's bucket (the collective would read a gradient still being written)."""
+    from tensorflowdistributedlearning_amd.ops.common import deliver_grad
+    m = TinyNet()
+    f = FlatParams(m, "cpu", lowp_dtype=None)
+    log = []
+    b = GradBucketer(f, None, 0.004, 0.001, comm_hook=lambda bk, v: log.append(bk.index),
+                     strict=True)
+    f.begin_step()
+    m(torch.randn(2, 8, 8, 8)).sum().backward()
+    assert b.early_launches == 0 and b._early >= len(b.buckets) - 1  # launched during backward
+    with pytest.raises(RuntimeError, match="delivered 2 times"):
+        deliver_grad(m.fc.conv.weight, torch.zeros_like(m.fc.conv.weight))
+    f.finish_grads()
+    b.finish()
+    assert b.early_launches >= len(b.buckets) - 1 and b.last_missing == []
+    # declared double contribution: the bucket waits for the second one
+    w = m.c3.weight
+    w._tdl_contribs = 2
+    try:
+        log.clear()
+        f.begin_step()
+        bk = b.bucket_of[id(w)]
+        deliver_grad(w, torch.ones_like(w))
+        assert bk.index not in log
+        deliver_grad(w, torch.ones_like(w))
+        assert bk.pending == len(bk.params) - 1
+    finally:
+        del w._tdl_contribs
+    # a parameter that delivered nothing is reported (strict: raised after the reset)
+    with pytest.raises(RuntimeError, match="delivered no final gradient"):
+        f.finish_grads()
+        b.finish()
+    assert len(b.last_missing) == len(f.params) - 1 and b.next_launch == 0
+
+
 def _dp_worker(rank, tmpdir, world=2):
     import torch
     from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown

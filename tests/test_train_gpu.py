@@ -972,7 +972,7 @@ def test_xception_depthwise_join_matches_autograd_sum(gpu):
     assert cos > 0.9999, cos
 
 
-@pytest.mark.parametrize("arch", ["resnet18", "deeplab"])
+@pytest.mark.parametrize("arch", ["resnet18", "deeplab", "xception41"])
 def test_deterministic_mode_bitwise_repeatable(gpu, arch):
     """TDL_DETERMINISTIC (csrc/kernels/det.hip): two runs of the same training steps
     from the same initial state are bit-identical — losses and every master weight — with batch
@@ -985,6 +985,12 @@ def test_deterministic_mode_bitwise_repeatable(gpu, arch):
         make = lambda: models.resnet18(num_classes=10)  # noqa: E731
         lossf, opt, okw = softmax_cross_entropy, "sgd", dict(lr=0.05, momentum=0.9)
         x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
+    elif arch == "xception41":
+        # depthwise tile kernels with fused statistics, the depthwise-BN → pointwise fold and
+        # the pointwise-BN → depthwise fold (ops/bnfold.py, ops/dwfold.py)
+        make = lambda: models.xception_41(num_classes=10)  # noqa: E731
+        lossf, opt, okw = softmax_cross_entropy, "sgd", dict(lr=0.05, momentum=0.9)
+        x, y = imagenet_batch(4, 96, num_classes=10, device=gpu)
     else:
         make = lambda: models.DeepLabResNet(model_name="m", input_shape=(101, 101))  # noqa: E731
         lossf, opt, okw = lovasz_hinge, "adam", dict(lr=1e-3)
