@@ -75,6 +75,19 @@ ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_
   return a;
 }
 
+// folded BN + ReLU of a conv's input (ConvArgs::aff): bn_finalize's fp32 coefficient rows
+// [≥2, C] (row 0 the scale a, row 1 the shift b)
+static void set_conv_aff(ConvArgs& a, const c10::optional<Tensor>& aff, int64_t C, const char* who) {
+  a.aff = nullptr;
+  a.aff_ld = 0;
+  if (!aff.has_value() || !aff->defined()) return;
+  TORCH_CHECK(aff->is_cuda() && aff->scalar_type() == torch::kFloat32 && aff->is_contiguous() &&
+                  aff->dim() == 2 && aff->size(0) >= 2 && aff->size(1) == C && C % 8 == 0,
+              who, " aff: fp32 [>=2, C] BN coefficients, C % 8 == 0");
+  a.aff = aff->data_ptr<float>();
+  a.aff_ld = (int)C;
+}
+
 // ------------------------------------------------------------------------------- fp32 path (f32.hip)
 // Every entry point below dispatches on the activation dtype: fp32 tensors run the fp32 kernels
 // (the reference's precision), bf16 the fused bf16 kernels.  The fp32 path has no fused ReLU bit
@@ -187,10 +200,15 @@ void conv_wgrad_f32(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_
 // res (optional, shaped like y): y = act(conv + bias + res) in the LDS-DMA epilogue; returns
 // false — nothing launched — when that kernel does not take the problem (the caller then adds
 // the residual itself)
+// aff (optional): the input is relu(aff[0]·x + aff[1]) — a training BN + ReLU folded into this
+// conv (ops/bnconv.py); no bias / residual with it
 bool conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::optional<Tensor> stats,
               int64_t sh, int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool relu,
-              c10::optional<Tensor> res) {
-  if (is_f32(x)) return conv_fwd_f32(x, w, y, bias, stats, sh, sw, ph, pw, dh, dw, relu, res);
+              c10::optional<Tensor> res, c10::optional<Tensor> aff) {
+  if (is_f32(x)) {
+    TORCH_CHECK(!(aff.has_value() && aff->defined()), "fp32 conv: no folded BN");
+    return conv_fwd_f32(x, w, y, bias, stats, sh, sw, ph, pw, dh, dw, relu, res);
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
@@ -205,6 +223,9 @@ bool conv_fwd(Tensor x, Tensor w, Tensor y, c10::optional<Tensor> bias, c10::opt
   a.stats = optfw(stats);
   if (a.stats) TORCH_CHECK(stats->numel() == 2 * a.K, "stats must be [2, K]");
   a.M = a.N * a.Ho * a.Wo; a.Ng = a.K; a.Kg = a.R * a.S * a.C; a.ldc = a.K; a.relu = relu;
+  set_conv_aff(a, aff, a.C, "conv_fwd");
+  if (a.aff) TORCH_CHECK(!a.bias && !(res.has_value() && res->defined()) && a.K % 8 == 0,
+                         "conv_fwd aff: no bias / residual, K % 8 == 0");
   if (res.has_value() && res->defined()) {
     CHECK_T(*res, torch::kBFloat16);
     TORCH_CHECK(res->sizes() == y.sizes(), "conv_fwd res: shaped like y");
@@ -322,11 +343,17 @@ void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
 // stored dx into bn_red fp32 [2, C] (zeroed by the caller), x = bn_x the input of the BN whose
 // output this conv consumed.  Returns whether they were computed (stride-1 problems on the
 // LDS-DMA kernel); otherwise bn_red is untouched and the BN backward reduces itself.
+// aff (optional, with bn_x / bn_red): the ReLU mask of a folded BN — dx · [aff[0]·bn_x + aff[1]
+// > 0] — applied together with the fused statistics; the return value says whether both ran
+// (otherwise dx is unmasked and the BN backward masks: relu mode 2)
 bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                 int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask,
                 c10::optional<Tensor> w_t, c10::optional<Tensor> bn_x,
-                c10::optional<Tensor> bn_red) {
-  if (is_f32(dy)) return conv_dgrad_f32(dy, w, dx, sh, sw, ph, pw, dh, dw, accumulate, mask);
+                c10::optional<Tensor> bn_red, c10::optional<Tensor> aff) {
+  if (is_f32(dy)) {
+    TORCH_CHECK(!(aff.has_value() && aff->defined()), "fp32 conv_dgrad: no folded BN");
+    return conv_dgrad_f32(dy, w, dx, sh, sw, ph, pw, dh, dw, accumulate, mask);
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(w, torch::kBFloat16);
   CHECK_T(dx, torch::kBFloat16);
@@ -364,7 +391,11 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
     if (!deterministic()) {
       a.bn_x = BF(*bn_x);
       a.stats = bn_red->data_ptr<float>();
+      set_conv_aff(a, aff, a.C, "conv_dgrad");
+      TORCH_CHECK(!a.aff || (!a.mask && !accumulate), "conv_dgrad aff: no bit mask / join");
     }
+  } else {
+    TORCH_CHECK(!(aff.has_value() && aff->defined()), "conv_dgrad aff needs bn_x / bn_red");
   }
   if (a.M == 0) return false;
   return conv_dgrad_launch(a, stream());
@@ -409,9 +440,14 @@ void conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, i
   }
 }
 
+// aff (optional): x is the pre-BN tensor of a folded BN + ReLU (dW = dyᵀ · relu(aff[0]·x + aff[1]))
 void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad, int64_t sh,
-                int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate) {
-  if (is_f32(dy)) return conv_wgrad_f32(dy, x, out, bias_grad, sh, sw, ph, pw, dh, dw, accumulate);
+                int64_t sw, int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate,
+                c10::optional<Tensor> aff) {
+  if (is_f32(dy)) {
+    TORCH_CHECK(!(aff.has_value() && aff->defined()), "fp32 conv_wgrad: no folded BN");
+    return conv_wgrad_f32(dy, x, out, bias_grad, sh, sw, ph, pw, dh, dw, accumulate);
+  }
   CHECK_T(dy, torch::kBFloat16);
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(out, torch::kFloat32);
@@ -422,6 +458,8 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad
   a.dy = BF(dy); a.x = BF(x);
   a.dy_bytes = nbytes32(dy); a.x_bytes = nbytes32(x);
   a.M = a.K; a.Ng = a.R * a.S * a.C; a.Kg = a.N * a.Ho * a.Wo;
+  set_conv_aff(a, aff, a.C, "conv_wgrad");
+  if (a.aff) TORCH_CHECK(a.K % 8 == 0, "conv_wgrad aff: K % 8 == 0");
   WgradPlan plan;
   conv_wgrad_plan(a, &plan);
   a.kps = plan.kps;
@@ -1315,12 +1353,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "tensorflowdistributedlearning_amd native gfx950 kernels";
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"),
         py::arg("stats"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
-        py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("res") = py::none());
+        py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("res") = py::none(),
+        py::arg("aff") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
         py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none(),
-        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none());
-  m.def("conv_wgrad", &conv_wgrad);
+        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none(), py::arg("aff") = py::none());
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("out"),
+        py::arg("bias_grad"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dh"), py::arg("dw"), py::arg("accumulate"), py::arg("aff") = py::none());
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
   m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dy8"), py::arg("w8t"), py::arg("dx"),
         py::arg("scale_dy"), py::arg("scale_w"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),

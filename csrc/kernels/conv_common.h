@@ -66,6 +66,31 @@ __device__ __forceinline__ uint4 gather8(const bf16_t* v) {
                     (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
 }
 
+// u = relu(a·z + b) of 8 consecutive bf16 channels (a folded training BN + ReLU, ConvArgs::aff),
+// bit-identical to bn.hip apply_vec: one fma per element, ReLU, round-to-nearest-even
+__device__ __forceinline__ uint4 aff_relu8(uint4 z, const float (&ca)[8], const float (&cb)[8]) {
+  const uint32_t w[4] = {z.x, z.y, z.z, z.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float lo = fmaf(__uint_as_float(w[j] << 16), ca[2 * j], cb[2 * j]);
+    const float hi = fmaf(__uint_as_float(w[j] & 0xffff0000u), ca[2 * j + 1], cb[2 * j + 1]);
+    o[j] = relu_pk_bf16(cvt_pk_bf16(lo, hi));
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// the 8 (a, b) coefficient pairs of channels c … c+7 (ConvArgs::aff rows, ld = aff_ld)
+__device__ __forceinline__ void aff_load8(const float* aff, int ld, int c, float (&ca)[8],
+                                          float (&cb)[8]) {
+  const float4 a0 = *(const float4*)(aff + c), a1 = *(const float4*)(aff + c + 4);
+  const float4 b0 = *(const float4*)(aff + ld + c), b1 = *(const float4*)(aff + ld + c + 4);
+  ca[0] = a0.x; ca[1] = a0.y; ca[2] = a0.z; ca[3] = a0.w;
+  ca[4] = a1.x; ca[5] = a1.y; ca[6] = a1.z; ca[7] = a1.w;
+  cb[0] = b0.x; cb[1] = b0.y; cb[2] = b0.z; cb[3] = b0.w;
+  cb[4] = b1.x; cb[5] = b1.y; cb[6] = b1.z; cb[7] = b1.w;
+}
+
 // ---------------------------------------------------------------------------------------------
 // per-tile geometry
 // ---------------------------------------------------------------------------------------------
@@ -244,8 +269,10 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 // ROWS: the caller supplies each fragment's output-row byte offset in rows_in[] (ROW_OOB for
 // lanes without an output pixel — conv_halo.hip's padded / tail lanes, whose accumulators hold
 // values that must not reach memory or the statistics, so STATS then masks by row validity)
+// AFM (DGRAD with STATS): the ReLU mask of a folded BN (ConvArgs::aff) — a·x + b > 0 of the BN
+// input x the statistics load anyway
 template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false,
-          bool NJ = false, bool FRES = false, bool ROWS = false>
+          bool NJ = false, bool FRES = false, bool ROWS = false, bool AFM = false>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
@@ -308,6 +335,22 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
         xv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
             rbx, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
       }
+  }
+  // folded BN + ReLU of this dgrad's output (ConvArgs::aff): dx is masked by a·x + b > 0 of the
+  // BN input x the statistics read anyway — no bit mask exists (ops/bnconv.py)
+  constexpr bool aff_mask = AFM && MODE == DGRAD && STATS;
+  v4u32 aff_a[aff_mask ? RN : 1], aff_b[aff_mask ? RN : 1];
+  if constexpr (aff_mask) {
+    {
+      const rsrc_t raff = make_rsrc(a.aff, (uint32_t)a.aff_ld * 8u);
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) {
+        const int n0 = c0 + rn * 16;
+        aff_a[rn] = __builtin_amdgcn_raw_buffer_load_b128(raff, n0 < a.Ng ? n0 * 4u : OOB, 0, 0);
+        aff_b[rn] = __builtin_amdgcn_raw_buffer_load_b128(
+            raff, n0 < a.Ng ? (uint32_t)(a.aff_ld + n0) * 4u : OOB, 0, 0);
+      }
+    }
   }
   if constexpr (MODE == DGRAD) {
     if (join_mask) {
@@ -372,6 +415,18 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
           for (int i = 0; i < 4; ++i)
             t[i] = __uint_as_float(__float_as_uint(t[i]) &
                                    (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + i, 1));
+        }
+      }
+      if constexpr (aff_mask) {
+        {
+          const float z[4] = {__uint_as_float(xv[rm][rn][0] << 16),
+                              __uint_as_float(xv[rm][rn][0] & 0xffff0000u),
+                              __uint_as_float(xv[rm][rn][1] << 16),
+                              __uint_as_float(xv[rm][rn][1] & 0xffff0000u)};
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            t[i] = fmaf(z[i], __uint_as_float(aff_a[rn][i]), __uint_as_float(aff_b[rn][i])) > 0.f
+                       ? t[i] : 0.f;
         }
       }
       pk[rn][0] = cvt_pk_bf16(t[0], t[1]);

@@ -43,8 +43,12 @@ using namespace convk;
 // ---------------------------------------------------------------------------------------------
 // the kernel
 // ---------------------------------------------------------------------------------------------
-template <int MODE, int BM, int BN, bool ALIGNED, bool STATS, bool BIAS>
+// AFF (aligned FWD / WGRAD): the input x is u = relu(a·x + b) of a folded training BN
+// (ConvArgs::aff) — applied to the staged registers before the LDS store; loads that fell in the
+// padding / past M or K (validity bit 0) stay 0
+template <int MODE, int BM, int BN, bool ALIGNED, bool STATS, bool BIAS, bool AFF = false>
 __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
+  static_assert(!AFF || (ALIGNED && MODE != DGRAD), "folded BN: aligned FWD / WGRAD only");
   constexpr int WM = 2, WN = 2;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
   constexpr bool A_MC = (MODE == WGRAD), B_MC = (MODE != FWD);
@@ -72,6 +76,8 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
   int b_base[PB];
   int b_ok[PB];
   int a_fix = 0, b_fix = 0, b_fix2 = 0, b_fix3 = 0;
+  float aff_a[8], aff_b[8];  // AFF: coefficients of this lane's 8 channels
+  uint32_t aff_v = 0;        // AFF: validity bit per staged load of the folded operand
 
   auto prep_tile = [&](const Tile& T) {
     if constexpr (!ALIGNED) return;
@@ -127,6 +133,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
         b_fix = ci;
         b_fix2 = r * a.dh - a.ph;
         b_fix3 = s * a.dw - a.pw;
+        if constexpr (AFF) aff_load8(a.aff, a.aff_ld, ci, aff_a, aff_b);
       } else {
         b_fix = -1;
         b_fix2 = -(1 << 28);
@@ -145,12 +152,17 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
         const int rs = (int)fdiv((uint32_t)k, a.fd_C), c = k - rs * a.C;
         const int r = (int)fdiv((uint32_t)rs, a.fd_S), s = rs - r * a.S;
         const int ro = r * a.dh, so = s * a.dw;
+        if constexpr (AFF) {
+          aff_load8(a.aff, a.aff_ld, kv ? c : 0, aff_a, aff_b);
+          aff_v = 0;
+        }
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
           const int hi = a_p0[i] + ro, wi = a_p1[i] + so;
           const bool v = kv && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
           const uint32_t off = (uint32_t)(a_base[i] + (hi * a.W + wi) * a.C + c) * 2u;
           ra[i] = bload16(rx, v ? off : OOB);
+          if constexpr (AFF) aff_v |= (v ? 1u : 0u) << i;
         }
 #pragma unroll
         for (int i = 0; i < PB; ++i) {
@@ -183,6 +195,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
           rb[i] = bload16(rw, v ? off : OOB);
         }
       } else {  // WGRAD
+        if constexpr (AFF) aff_v = 0;
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
           const int p = kt * BK + tid / A_CPR + i * (NT / A_CPR);
@@ -201,6 +214,7 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
                          (unsigned)wi < (unsigned)a.W;
           const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_fix) * 2u;
           rb[i] = bload16(rx, v ? off : OOB);
+          if constexpr (AFF) aff_v |= (v ? 1u : 0u) << i;
         }
       }
     } else {
@@ -243,6 +257,16 @@ __global__ void __launch_bounds__(NT, 2) conv_gemm_kernel(ConvArgs a) {
   auto store_step = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + A_BYTES;
+    if constexpr (AFF) {  // the folded BN + ReLU, on the data that has arrived by now
+      const uint4 zero = make_uint4(0, 0, 0, 0);
+      if constexpr (MODE == FWD) {
+#pragma unroll
+        for (int i = 0; i < PA; ++i) ra[i] = (aff_v >> i) & 1u ? aff_relu8(ra[i], aff_a, aff_b) : zero;
+      } else {
+#pragma unroll
+        for (int i = 0; i < PB; ++i) rb[i] = (aff_v >> i) & 1u ? aff_relu8(rb[i], aff_a, aff_b) : zero;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       if constexpr (!A_MC) {
@@ -697,21 +721,21 @@ __global__ void __launch_bounds__(256) colsum_reduce_kernel(const float* __restr
   }
 }
 
-template <int MODE, int BM, int BN, bool AL, bool ST, bool BI>
+template <int MODE, int BM, int BN, bool AL, bool ST, bool BI, bool AF = false>
 void launch_t(const ConvArgs& a, int blocks, hipStream_t st) {
-  hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, AL, ST, BI>), dim3(blocks), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<MODE, BM, BN, AL, ST, BI, AF>), dim3(blocks), dim3(NT), 0, st, a);
 }
 
-template <int MODE, bool AL, bool ST, bool BI = false>
+template <int MODE, bool AL, bool ST, bool BI = false, bool AF = false>
 void launch_cfg(const ConvArgs& a, int bm, int bn, int blocks, hipStream_t st) {
   if (bm == 128 && bn == 128)
-    launch_t<MODE, 128, 128, AL, ST, BI>(a, blocks, st);
+    launch_t<MODE, 128, 128, AL, ST, BI, AF>(a, blocks, st);
   else if (bm == 128 && bn == 64)
-    launch_t<MODE, 128, 64, AL, ST, BI>(a, blocks, st);
+    launch_t<MODE, 128, 64, AL, ST, BI, AF>(a, blocks, st);
   else if (bm == 64 && bn == 128)
-    launch_t<MODE, 64, 128, AL, ST, BI>(a, blocks, st);
+    launch_t<MODE, 64, 128, AL, ST, BI, AF>(a, blocks, st);
   else
-    launch_t<MODE, 64, 64, AL, ST, BI>(a, blocks, st);
+    launch_t<MODE, 64, 64, AL, ST, BI, AF>(a, blocks, st);
 }
 
 }  // namespace
@@ -741,7 +765,12 @@ static int pick_tpb(long tiles, int nkt) {
 }
 
 void conv_fwd_launch(const ConvArgs& a0, hipStream_t st) {
-  if (conv_fwd_halo(a0, st)) return;
+  const bool aff = a0.aff != nullptr;
+  if (aff && (a0.C % 8 || a0.K % 8 || a0.bias || a0.res))
+    throw std::runtime_error("folded-BN conv: C % 8 == 0, K % 8 == 0, no bias / residual");
+  // the halo kernel has no folded-BN staging; the LDS-DMA launcher takes a folded BN only onto
+  // the producer/consumer kernel (its producers stage the transformed operand)
+  if (!aff && conv_fwd_halo(a0, st)) return;
   if (conv_fwd_glds(a0, st)) return;
   ConvArgs a = a0;
   convk::set_fastdivs(a);
@@ -760,7 +789,10 @@ void conv_fwd_launch(const ConvArgs& a0, hipStream_t st) {
   const bool al = (a.C % 8 == 0) && (a.K % 8 == 0);
   const bool stats = a.stats != nullptr;
   const bool bias = a.bias != nullptr;
-  if (al) {
+  if (aff) {
+    if (stats) launch_cfg<FWD, true, true, false, true>(a, bm, bn, blocks, st);
+    else launch_cfg<FWD, true, false, false, true>(a, bm, bn, blocks, st);
+  } else if (al) {
     if (bias) {
       if (stats) launch_cfg<FWD, true, true, true>(a, bm, bn, blocks, st);
       else launch_cfg<FWD, true, false, true>(a, bm, bn, blocks, st);
@@ -886,8 +918,9 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
 }
 
 void conv_wgrad_plan(const ConvArgs& a, WgradPlan* p) {
-  if (conv_wgrad_halo_plan(a, p)) return;
-  if (conv_wgrad_glds_plan(a, p)) return;
+  // a folded BN on x (ConvArgs::aff): the register-staged kernel (it transforms the staged B rows)
+  if (!a.aff && conv_wgrad_halo_plan(a, p)) return;
+  if (!a.aff && conv_wgrad_glds_plan(a, p)) return;
   p->impl = 0;
   p->cfg = 0;
   p->bm = a.M <= 64 ? 64 : 128;
@@ -921,7 +954,10 @@ void conv_wgrad_launch(const ConvArgs& a0, const WgradPlan& p, float* out, bool 
     a.kps = p.kps;
     convk::set_fastdivs(a);
     const bool al = (a.C % 8 == 0) && (a.K % 8 == 0);
-    if (al) launch_cfg<WGRAD, true, false>(a, p.bm, p.bn, (int)tiles, st);
+    if (a.aff) {
+      if (!al) throw std::runtime_error("folded-BN weight gradient: C % 8 == 0, K % 8 == 0");
+      launch_cfg<WGRAD, true, false, false, true>(a, p.bm, p.bn, (int)tiles, st);
+    } else if (al) launch_cfg<WGRAD, true, false>(a, p.bm, p.bn, (int)tiles, st);
     else launch_cfg<WGRAD, false, false>(a, p.bm, p.bn, (int)tiles, st);
   }
   splitk_reduce_launch((const float*)a.out, out, (long)a.M * a.Ng, splits, accumulate, st);

@@ -154,8 +154,9 @@ __device__ __forceinline__ void acc32_to_16(const f32x16 (&c)[QM][QN], f32x4 (&a
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, int FK,
-          bool FP8 = false, bool NJ = false, bool FRES = false, bool M32 = false>
+          bool FP8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  // AFM: DGRAD statistics epilogue masking by a folded BN's a·x + b > 0 (conv_common.h)
   // M32: the K loop runs v_mfma_f32_32x32x16_bf16 on 32×32 blocks (half the MFMA instructions
   // and half the vector-issue hold per FLOP of the 16×16×32 form); accumulators are re-laid to
   // the 16×16 fragment layout (acc32_to_16) before the shared epilogue.  Both operands must be
@@ -619,7 +620,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }
     } else {
       if constexpr (M32) acc32_to_16<QM, QN>(acc32, acc);
-      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES>(
+      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES, false, AFM>(
           a, T, acc, wm, wn, lane, rout, out_scale, no_epi_mem, s_sum, s_sq);
     }
   };
@@ -906,9 +907,9 @@ constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, int FK,
-          bool F8 = false, bool NJ = false, bool FRES = false, bool M32 = false>
+          bool F8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES, M32>;
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES, M32, AFM>;
   constexpr int lds = lds_bytes(BM, BN, WM, ST);
   static bool attr = false;
   if (!attr) {
@@ -1033,6 +1034,7 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const int mode = conv_glds_mode();
   if (mode == 0 || a0.C % 8 || a0.K % 8) return false;
   if (a0.res && !a0.bias) return false;  // residual epilogue instantiated with bias only
+  if (a0.aff && (a0.res || a0.C % 64)) return false;
   // default selection (ResNet-50 b256, tools/n64_configs.py): ≥ 128 output channels, and 1×1
   // filters with 64 (the 8-wave 256×64 tiles: 35 vs 53 µs on 56×56 64→64); 3×3 filters with 64
   // output channels stay on the register-staged kernel
@@ -1073,6 +1075,12 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
       else launch_gcfg<FWD, false, false, FK>(a, cfg, blocks, st);           \
     }                                                                        \
   } while (0)
+  if (a.aff) {
+    // folded BN + ReLU on x: only the producer/consumer kernel stages a transformed operand
+    // (FASTK 256×128 tiles); anything else runs on the register-staged kernel
+    if (fk != 1 || cfg != 0 || bias) return false;
+    return conv_fwd_pc_launch(a, blocks, fk, 2, st);
+  }
   if (a.res) {
     // residual epilogue (DeepLab units): the default FWD tile configs, bias, ± statistics
 #define TDL_R(FK)                                                                            \
@@ -1161,15 +1169,18 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   // joins need stride 1 — an accumulate leaves the pixels of such a class unmasked)
   // K % 64 != 0 (Xception's 728-channel pointwise convs): the ragged FASTK form for 1×1 filters
   const bool rag_stats = a.K % 64 != 0 && a.R * a.S == 1 && a.ncls == 1 && a.K % 8 == 0;
+  // a folded BN's mask (a.aff) rides on the single-consumer statistics epilogue: K % 64 == 0,
+  // no join, the default tile configs
+  const bool aff_ok = !a.aff || (a.K % 64 == 0 && !a.beta);
   const bool bn_stats = a.stats && a.bn_x && !a.fp8 && (a.K % 64 == 0 || rag_stats) &&
-                        (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1));
+                        (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1)) && aff_ok;
   if (bn_stats) {
     // tile config (tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
     // tiles (NJ: no previous-dx registers); with the join's previous-dx loads as well they spill,
     // so 8 waves of 32×64 (cfg 6); 64-wide dx: the 8-wave 256×64 tiles
     const int sdef = a.Ng <= 64 ? 4 : (a.beta ? 6 : 0);
     const int senv = env_int(a.beta ? "TDL_GLDS_CFG_DGSTAT_J" : "TDL_GLDS_CFG_DGSTAT", sdef);
-    const int scfg = cfg_valid(DGRAD, true, senv) ? senv : sdef;
+    const int scfg = a.aff ? (a.Ng <= 64 ? 4 : 6) : (cfg_valid(DGRAD, true, senv) ? senv : sdef);
     const GCfg& g = cfg_of(scfg);
     const long ntn = cdiv(a.Ng, g.bn);
     long ntm_all = 0, ntm_max = 1;
@@ -1186,7 +1197,12 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
     }
     const int blocks = a.cls_tile0[a.ncls] / a.tpb;
     a.splits = 1;
-    if (rag_stats) {
+    if (a.aff) {  // (K % 64 == 0, no join: aff_ok)
+      if (scfg == 4)
+        launch_g<DGRAD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, true>(a, blocks, st);
+      else  // (8 waves of 32×64: the 256×128 tiles spill with the coefficient registers)
+        launch_g<DGRAD, 128, 128, 4, 2, 4, true, false, 1, false, true, false, false, true>(a, blocks, st);
+    } else if (rag_stats) {
       if (a.beta)
         launch_gcfg<DGRAD, true, false, 2>(a, scfg, blocks, st);
       else

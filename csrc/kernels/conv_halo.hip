@@ -807,6 +807,7 @@ bool plan_halo_wgrad(const ConvArgs& a, HaloGeom& g, HaloWg& q, int& bm) {
 }  // namespace
 
 bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p) {
+  if (a.aff) return false;
   if (!conv_halo_mode()) return false;
   if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
   // default: ≥ 128 input channels and enough pixel tiles to split over the chip (ResNet-50 b1024
@@ -845,6 +846,7 @@ void conv_set_halo_mode(int mode) { g_halo_override = mode; }
 
 // FWD, stride 1: true when the halo kernel ran
 bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
+  if (a.aff) return false;  // no folded-BN staging
   if (!conv_halo_mode()) return false;
   if (a.sh != 1 || a.sw != 1 || a.res || a.fp8) return false;
   const int ntap = a.R * a.S;
@@ -885,6 +887,7 @@ bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
 // DGRAD, stride 1 (one parity class): true when the halo kernel ran; *fused: a.stats filled
 bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused) {
   if (fused) *fused = false;
+  if (a.aff) return false;  // the folded-BN mask: LDS-DMA statistics epilogue only
   if (!conv_halo_mode()) return false;
   if (a.sh != 1 || a.sw != 1 || a.fp8 || a.dg_masked) return false;
   const int ntap = a.R * a.S;

@@ -50,9 +50,16 @@ __device__ __forceinline__ void pc_rows(bf16x8 (&f)[N], uint32_t base) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ST, int NP, bool STATS, bool BIAS, int FK>
+// AFF: a training BN + ReLU folded into this conv (ConvArgs::aff, ops/bnconv.py) — the producers
+// stage the A tile through registers instead of LDS-DMA: buffer_load → u = relu(a·z + b) (bf16,
+// exactly as the BN apply pass rounds it; padding taps / rows past M stay 0) → ds_write_b128 to
+// the same swizzled LDS image.  Step j's loads are issued one step ahead (two register sets), so
+// they land under the consumers' MFMAs of step j−1; the consumers are unchanged.
+template <int BM, int BN, int WM, int WN, int ST, int NP, bool STATS, bool BIAS, int FK,
+          bool AFF = false>
 __global__ void __launch_bounds__(64 * (WM * WN + NP), 1) conv_pc_kernel(ConvArgs a) {
   static_assert(FK == 1 || FK == 2, "FASTK forward only");
+  static_assert(!AFF || (FK == 1 && NP % 2 == 0), "folded BN: FASTK, even producer count");
   constexpr bool RAG = FK == 2;
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN, RM = TM / 16, RN = TN / 16;
@@ -96,6 +103,146 @@ __global__ void __launch_bounds__(64 * (WM * WN + NP), 1) conv_pc_kernel(ConvArg
       b_ch[q] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
       const int n = T0.bn0 + r;
       b_row[q] = n < a.Ng ? n * a.Kg + b_ch[q] : -1;
+    }
+    if constexpr (AFF) {
+      // ---- register-staged producers with the folded BN + ReLU ----
+      // this lane's channel chunk is the same in every piece: row r = (q·NP + pid)·8 + lane/8,
+      // (r/2) mod 8 = (pid & 1)·4 + lane/16 for even NP
+      const int ach = a_ch[0];
+      float* tbl = (float*)(smem + ST * STAGE + 2 * BN * 4);  // a[C] then b[C]
+      // every producer wave writes the whole coefficient table itself (identical values, its 64
+      // lanes cover all 8 chunks of every 64 channels): no cross-wave ordering before its reads
+      for (int c0 = 0; c0 < a.C; c0 += BK) {
+        float ta[8], tb[8];
+        aff_load8(a.aff, a.aff_ld, c0 + ach, ta, tb);
+        *(float4*)(tbl + c0 + ach) = make_float4(ta[0], ta[1], ta[2], ta[3]);
+        *(float4*)(tbl + c0 + ach + 4) = make_float4(ta[4], ta[5], ta[6], ta[7]);
+        *(float4*)(tbl + a.C + c0 + ach) = make_float4(tb[0], tb[1], tb[2], tb[3]);
+        *(float4*)(tbl + a.C + c0 + ach + 4) = make_float4(tb[4], tb[5], tb[6], tb[7]);
+      }
+      uint4 ra0[QA], ra1[QA];
+      uint32_t av0 = 0, av1 = 0;
+      int fc0 = 0, fc1 = 0;  // channel offset (pc0) of the step held in ra0 / ra1
+      int islot = 0, fslot = 0, par = 0;
+      bool have = false;
+      const uint4 zero = make_uint4(0, 0, 0, 0);
+      const uint32_t lds0 = (uint32_t)(size_t)(pc_lds_char_t*)smem;
+      const uint32_t tbl_lds = lds0 + (uint32_t)(ST * STAGE + 2 * BN * 4);
+      // issue step (tile state, pr/ps/pc0, k) into RA: A loads to registers, B LDS-DMA into its slot
+#define TDL_PC_ISSUE(RA, AV, FC)                                                                \
+  do {                                                                                        \
+    const int rdh_ = pr * a.dh, sdw_ = ps * a.dw;                                             \
+    const int tuni_ = (rdh_ * a.W + sdw_) * a.C + pc0;                                        \
+    uint32_t vb_ = 0;                                                                         \
+    _Pragma("unroll") for (int q = 0; q < QA; ++q) {                                          \
+      /* branch-free validity (a short-circuit && compiles to exec-mask branches per piece) */ \
+      const bool in_ = ((unsigned)(a_p0[q] + rdh_) < (unsigned)a.H) &                         \
+                       ((unsigned)(a_p1[q] + sdw_) < (unsigned)a.W);                           \
+      const bool v_ = pointwise ? a_p0[q] >= 0 : in_;                                         \
+      RA[q] = bload16(rx, v_ ? (uint32_t)(a_row[q] + tuni_) * 2u : OOB);                      \
+      vb_ |= (uint32_t)v_ << q;                                                               \
+    }                                                                                         \
+    AV = vb_;                                                                                 \
+    FC = pc0;                                                                                 \
+    char* Bs_ = smem + islot * STAGE + A_BYTES;                                               \
+    const int kb_ = k * BK;                                                                   \
+    _Pragma("unroll") for (int q = 0; q < QB; ++q)                                            \
+      pc_dma16(rw, Bs_ + (q * NP + pid) * 1024, b_row[q] >= 0 ? (uint32_t)(b_row[q] + kb_) * 2u : OOB); \
+    islot = islot + 1 == ST ? 0 : islot + 1;                                                  \
+  } while (0)
+      // transform + write the A tile of the step held in RA into its slot, publish the step.
+      // Every LDS access here is inline asm: a compiler-visible ds_read / ds_write after an
+      // LDS-DMA issue makes hipcc wait vmcnt(0) first (a possible alias of the DMA's LDS
+      // writes), which would drain the next step's loads just issued.
+#define TDL_PC_FINISH(RA, AV, FC)                                                               \
+  do {                                                                                        \
+    uint4 ca0_, ca1_, cb0_, cb1_;                                                             \
+    const uint32_t ta_ = tbl_lds + (uint32_t)((FC) + ach) * 4u;                               \
+    const uint32_t tb_ = ta_ + (uint32_t)a.C * 4u;                                            \
+    asm volatile("ds_read_b128 %0, %1" : "=v"(ca0_) : "v"(ta_) : "memory");                   \
+    asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(ca1_) : "v"(ta_) : "memory");         \
+    asm volatile("ds_read_b128 %0, %1" : "=v"(cb0_) : "v"(tb_) : "memory");                   \
+    asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(cb1_) : "v"(tb_) : "memory");         \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    const float ca_[8] = {__uint_as_float(ca0_.x), __uint_as_float(ca0_.y),                   \
+                          __uint_as_float(ca0_.z), __uint_as_float(ca0_.w),                   \
+                          __uint_as_float(ca1_.x), __uint_as_float(ca1_.y),                   \
+                          __uint_as_float(ca1_.z), __uint_as_float(ca1_.w)};                  \
+    const float cb_[8] = {__uint_as_float(cb0_.x), __uint_as_float(cb0_.y),                   \
+                          __uint_as_float(cb0_.z), __uint_as_float(cb0_.w),                   \
+                          __uint_as_float(cb1_.x), __uint_as_float(cb1_.y),                   \
+                          __uint_as_float(cb1_.z), __uint_as_float(cb1_.w)};                  \
+    const uint32_t as_ = lds0 + (uint32_t)(fslot * STAGE + pid * 1024 + lane * 16);           \
+    _Pragma("unroll") for (int q = 0; q < QA; ++q) {                                          \
+      uint4 u_ = aff_relu8(RA[q], ca_, cb_);                                                  \
+      const uint32_t m_ = 0u - (((AV) >> q) & 1u); /* padding / rows past M stay 0 */         \
+      u_.x &= m_; u_.y &= m_; u_.z &= m_; u_.w &= m_;                                         \
+      const v4u32 w_ = {u_.x, u_.y, u_.z, u_.w};                                             \
+      asm volatile("ds_write_b128 %0, %1" ::"v"(as_ + (uint32_t)(q * NP * 1024)), "v"(w_)      \
+                   : "memory");                                                               \
+    }                                                                                         \
+    fslot = fslot + 1 == ST ? 0 : fslot + 1;                                                  \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                        \
+    pc_barrier();                                                                             \
+  } while (0)
+      (void)lds0;
+      for (int ti = 0; ti < ntiles; ++ti) {
+        const int bm0 = T0.bm0 + ti * BM;
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+          const int m = bm0 + (q * NP + pid) * 8 + (lane >> 3);
+          if (m < T0.Mc) {
+            const int n = fdiv(m, a.fd_HoWo), rem = m - n * HoWo;
+            const int ho = fdiv(rem, a.fd_Wo), wo = rem - ho * a.Wo;
+            a_p0[q] = ho * a.sh - a.ph;
+            a_p1[q] = wo * a.sw - a.pw;
+            a_row[q] = n * a.H * a.W * a.C + (a_p0[q] * a.W + a_p1[q]) * a.C + ach;
+          } else {
+            a_p0[q] = -(1 << 28);
+            a_p1[q] = 0;
+            a_row[q] = 0;
+          }
+        }
+        int pr = 0, ps = 0, pc0 = 0;
+        for (int k = 0; k < nk; ++k) {
+          // step j's loads go into one register set while step j−1 (the other set) is
+          // transformed and published once its loads have retired (QA + QB younger ops)
+          if (par == 0) {
+            TDL_PC_ISSUE(ra0, av0, fc0);
+            if (have) {
+              pc_vmwait<QA + QB>();
+              TDL_PC_FINISH(ra1, av1, fc1);
+            }
+          } else {
+            TDL_PC_ISSUE(ra1, av1, fc1);
+            if (have) {
+              pc_vmwait<QA + QB>();
+              TDL_PC_FINISH(ra0, av0, fc0);
+            }
+          }
+          par ^= 1;
+          have = true;
+          pc0 += BK;
+          if (pc0 >= a.C) {
+            pc0 = 0;
+            if (++ps == a.S) {
+              ps = 0;
+              ++pr;
+            }
+          }
+        }
+      }
+      pc_vmwait<0>();
+      if (par == 1) TDL_PC_FINISH(ra0, av0, fc0);  // the last issued step
+      else TDL_PC_FINISH(ra1, av1, fc1);
+#undef TDL_PC_ISSUE
+#undef TDL_PC_FINISH
+      if constexpr (STATS) {
+        __syncthreads();
+        __syncthreads();
+      }
+      return;
     }
     int issued = 0, bar = 0, slot = 0;
     for (int ti = 0; ti < ntiles; ++ti) {
@@ -277,14 +424,20 @@ __global__ void __launch_bounds__(64 * (WM * WN + NP), 1) conv_pc_kernel(ConvArg
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ST, int NP, bool STATS, bool BIAS, int FK>
+// largest folded-BN channel count whose coefficient table fits beside the ring (256×128 tiles)
+constexpr int PC_LDS_MAX = 160 * 1024;
+constexpr int pc_lds(int bm, int bn, int st) { return st * (bm + bn) * BK * 2 + 2 * bn * 4; }
+
+template <int BM, int BN, int WM, int WN, int ST, int NP, bool STATS, bool BIAS, int FK,
+          bool AFF = false>
 void launch_pc(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_pc_kernel<BM, BN, WM, WN, ST, NP, STATS, BIAS, FK>;
-  constexpr int lds = ST * (BM + BN) * BK * 2 + 2 * BN * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
+  auto k = conv_pc_kernel<BM, BN, WM, WN, ST, NP, STATS, BIAS, FK, AFF>;
+  const int lds = pc_lds(BM, BN, ST) + (AFF ? 2 * a.C * 4 : 0);
+  static int attr = 0;  // the largest size set so far
+  if (lds > attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              AFF ? PC_LDS_MAX : lds);
+    attr = AFF ? PC_LDS_MAX : lds;
   }
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * (WM * WN + NP)), lds, st, a);
 }
@@ -297,6 +450,13 @@ void launch_pc(const ConvArgs& a, int blocks, hipStream_t st) {
 bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st) {
   if (a.res || a.dbg) return false;
   const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
+  if (a.aff) {
+    // folded BN + ReLU: 4 register-staging producers, FASTK, no bias, coefficient table in LDS
+    if (fk != 1 || bias || pc_lds(256, 128, 3) + 2 * a.C * 4 > PC_LDS_MAX) return false;
+    if (stats) launch_pc<256, 128, 4, 2, 3, 4, true, false, 1, true>(a, blocks, st);
+    else launch_pc<256, 128, 4, 2, 3, 4, false, false, 1, true>(a, blocks, st);
+    return true;
+  }
   const bool np4 = mode == 2;
 #define TDL_PC(NP, FK)                                                              \
   do {                                                                              \

@@ -72,6 +72,16 @@ struct ConvArgs {
   int cls_tile0[17]; // prefix sum of tiles per class
   int cls_a[16], cls_b[16], cls_Hc[16], cls_Wc[16];
   int cls_r0[16], cls_Th[16], cls_s0[16], cls_Tw[16];
+  // Training BN + ReLU of the conv's input folded into this conv (ops/bnconv.py): the input is
+  // u = relu(a·x + b), a = aff[c], b = aff[aff_ld + c] (bn_finalize's fp32 coefficient rows),
+  // rounded to bf16 exactly as the BN apply pass stores it; padding taps stay 0.
+  //   FWD    the A operand (conv_pc producers, conv_gemm staging)
+  //   WGRAD  the B operand (conv_gemm staging)
+  //   DGRAD  the ReLU mask of dx is a·bn_x + b > 0 (only together with the fused BN-backward
+  //          statistics, a.stats / a.bn_x — the launcher's return value says whether it ran)
+  // Launchers that cannot apply it must not run the problem (conv_aff_fwd_ok / the routing).
+  const float* aff;
+  int aff_ld;
 };
 constexpr int MAX_DG_CLASSES = 16;
 

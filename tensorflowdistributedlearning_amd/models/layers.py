@@ -18,6 +18,8 @@ from ..ops.conv import ConvGeom, conv2d, conv_fwd, same_padding, symmetric_paddi
 from ..ops.bn import batch_norm_act, batch_norm_act_into
 from ..ops.pool import max_pool2d, global_avg_pool
 from ..ops.dwconv import depthwise_conv2d
+from ..ops import bnconv
+from ..ops.bnconv import DeferredBNAct, bn_act_conv
 from ..ops.common import compute_weight, flat_view
 from ..ops.fp8 import DelayedScaler, flat_weights_for, transpose_weight
 from . import params as _params
@@ -433,10 +435,19 @@ class ConvBN(nn.Module):
         self.__dict__["_fold"] = (key, wf, sh.contiguous())
         return wf, self.__dict__["_fold"][2]
 
-    def forward(self, x, residual=None, join=None, res_join=None, into=None):
+    def forward(self, x, residual=None, join=None, res_join=None, into=None, defer=False):
         """``join``: gradient join for x (ops/gradjoin.py); ``res_join``: for the residual.
         ``into`` = (buf, c0): write act(BN(conv(x))) into ``buf[..., c0:c0+C]`` (a concat
-        buffer, ops/bn.batch_norm_act_into) and return ``buf``."""
+        buffer, ops/bn.batch_norm_act_into) and return ``buf``.
+        ``x`` may be an ops.bnconv.DeferredBNAct (the previous layer's BN + ReLU, folded into
+        this conv where the kernels take it); ``defer``: in training, return this layer's own
+        BN + ReLU deferred the same way for a single consumer conv (ops/bnconv.py)."""
+        if isinstance(x, DeferredBNAct):
+            if join is not None or not self.training:
+                x = x.materialize()
+            else:
+                y, stats = bn_act_conv(x, self.conv, want_stats=True)
+                return self._bn_out(y, stats, residual, res_join, into, defer)
         if (not self.training and into is None and not torch.is_grad_enabled()
                 and bn_fold_enabled()):
             wf, bf = self.folded_params(x.dtype, x.device)
@@ -445,6 +456,12 @@ class ConvBN(nn.Module):
             y, stats = self.conv(x, want_stats=True, join=join)
         else:
             y, stats = self.conv(x, join=join), None
+        return self._bn_out(y, stats, residual, res_join, into, defer)
+
+    def _bn_out(self, y, stats, residual, res_join, into, defer):
+        if (defer and self.relu and self.training and residual is None and into is None
+                and bnconv.ENABLED and torch.is_grad_enabled()):
+            return DeferredBNAct(y, stats, self.bn)
         if into is not None:
             if residual is not None:
                 raise ValueError("ConvBN: no residual with into=")

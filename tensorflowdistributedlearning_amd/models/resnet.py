@@ -4,7 +4,8 @@ beta-variant DeepLab encoder (core/resnet.py:284-354, see :mod:`models.deeplab`)
 optional classification head (core/resnet.py:246-256) is what ``num_classes`` reproduces.
 
 Every conv is followed by BN whose batch statistics are accumulated in the conv's epilogue; the
-bottleneck's last BN, the residual add and the ReLU are a single fused kernel pass.
+bottleneck's last BN, the residual add and the ReLU are a single fused kernel pass; the first two
+BN + ReLU of a block are folded into the next conv's operand staging (ops/bnconv.py).
 """
 from __future__ import annotations
 
@@ -45,7 +46,8 @@ class BasicBlock(nn.Module):
             sc, res_join = x, join
         else:
             sc, res_join = self.downsample(x, join=join), None
-        out = self.conv1(x, join=join)
+        # conv1's BN + ReLU is folded into conv2 (ops/bnconv.py; applied where it cannot be)
+        out = self.conv1(x, join=join, defer=True)
         return self.conv2(out, residual=sc, res_join=res_join)
 
 
@@ -71,8 +73,10 @@ class Bottleneck(nn.Module):
             sc, res_join = x, join
         else:
             sc, res_join = self.downsample(x, join=join), None
-        y = self.conv1(x, join=join)
-        y = self.conv2(y)
+        # bn1 + ReLU folded into conv2, bn2 + ReLU into conv3 (ops/bnconv.py): their outputs are
+        # never written (/root/reference/core/resnet.py:134-144 conv+BN+ReLU, single consumers)
+        y = self.conv1(x, join=join, defer=True)
+        y = self.conv2(y, defer=True)
         return self.conv3(y, residual=sc, res_join=res_join)
 
 

@@ -28,26 +28,9 @@ from .common import on_gpu, ext, compute_weight, grad_target, deliver_grad
 from . import workspace
 from .bn import (bn_stats, bn_finalize, bn_bwd_reduce, bn_bwd_apply, bn_red_xhat, _phys_params,
                  _grad_target_phys)
+from .bnconv import DeferredBNAct  # noqa: F401  (shared with the dense-conv fold)
 
 ENABLED = os.environ.get("TDL_BN_DW_FOLD", "1") == "1"
-
-
-class DeferredBNAct:
-    """A training BN + ReLU whose apply is deferred to its single consumer (a depthwise conv):
-    ``z`` the BN input, ``stats`` its (Σz, Σz²) if the producer accumulated them, ``bn`` the
-    models.layers.BatchNorm.  :meth:`materialize` applies it the ordinary way."""
-
-    __slots__ = ("z", "stats", "bn")
-
-    def __init__(self, z, stats, bn):
-        self.z, self.stats, self.bn = z, stats, bn
-
-    @property
-    def shape(self):
-        return self.z.shape
-
-    def materialize(self):
-        return self.bn(self.z, stats=self.stats, relu=True)
 
 
 _FOLDABLE = {}  # (shape, padding) -> the kernels' answer (asked once per geometry)

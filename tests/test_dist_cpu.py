@@ -357,10 +357,14 @@ def test_bucket_launch_never_joins_the_compute_stream(monkeypatch):
     monkeypatch.setattr(streams, "current", lambda dev: comp)
     s = GradBucketer.issue_stream(torch.device("cpu"))
     assert s is side and side.waited == ["compute"] and comp.waited == []
-    # hook fired on the side stream itself (a wgrad's gradient-ready hook): no extra wait
+    # hook fired on the side stream itself (a wgrad's gradient-ready hook): the side stream still
+    # waits for the compute (origin) stream — the bucket can hold γ/β gradients written there
+    # before the side-stream section (the folded depthwise BN's γ/β)
     monkeypatch.setattr(streams, "current", lambda dev: side)
+    monkeypatch.setattr(streams, "origin", lambda dev: comp)
     side.waited.clear()
-    assert GradBucketer.issue_stream(torch.device("cpu")) is side and side.waited == []
+    assert GradBucketer.issue_stream(torch.device("cpu")) is side and side.waited == ["compute"]
+    assert comp.waited == []
     # no side stream: issue from the current stream
     monkeypatch.setattr(streams, "side_if_active", lambda dev: None)
     assert GradBucketer.issue_stream(torch.device("cpu")) is None

@@ -61,7 +61,7 @@ def main():
                 elif m.group(1) == "VGPRs Spill" and default:
                     bad = True
                 if a.all or default:
-                    print(f"{'DEFAULT ' if default else ''}{cur[:90]}: {m.group(1)} {m.group(2)}{note}")
+                    print(f"{'DEFAULT ' if default else ''}{cur[:150]}: {m.group(1)} {m.group(2)}{note}")
     print("scratch in a default conv kernel" if bad else "default conv kernels: no scratch")
     sys.exit(1 if bad else 0)
 
