@@ -867,6 +867,26 @@ void softmax_xent(Tensor logits, Tensor labels, Tensor loss, Tensor grad, double
                       grad.data_ptr(), logits.size(0), logits.size(1), (float)smoothing, stream());
 }
 
+// logits [N, K] bf16 / fp32; labels (optional int64 [N]) with loss_sum / correct (fp32 [1],
+// accumulated); probs (optional fp32 [N, K])
+void softmax_eval(Tensor logits, c10::optional<Tensor> labels, c10::optional<Tensor> loss_sum,
+                  c10::optional<Tensor> correct, c10::optional<Tensor> probs) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "softmax_eval logits");
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "softmax_eval: bf16 / fp32 logits");
+  const int64_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    TORCH_CHECK(labels->scalar_type() == torch::kInt64 && labels->is_contiguous() &&
+                labels->numel() == logits.size(0), "softmax_eval labels: int64 [N]");
+    lab = labels->data_ptr<int64_t>();
+  }
+  float* p = optfw(probs);
+  if (p) TORCH_CHECK(probs->numel() == logits.numel() && probs->is_contiguous(), "probs: fp32 [N, K]");
+  if (logits.size(0) == 0) return;
+  softmax_eval_launch(logits.data_ptr(), bf, lab, optfw(loss_sum), optfw(correct), p,
+                      logits.size(0), logits.size(1), stream());
+}
+
 int label_kind(const Tensor& t) {
   switch (t.scalar_type()) {
     case torch::kFloat32: return 0;
@@ -1421,6 +1441,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd, py::arg("dy"), py::arg("dx"), py::arg("dadd") = py::none());
   m.def("softmax_xent", &softmax_xent);
+  m.def("softmax_eval", &softmax_eval, py::arg("logits"), py::arg("labels") = py::none(),
+        py::arg("loss_sum") = py::none(), py::arg("correct") = py::none(),
+        py::arg("probs") = py::none());
   m.def("lovasz_hinge", &lovasz_hinge);
   m.def("seg_metrics", &seg_metrics);
   m.def("sgd_momentum", &sgd_momentum, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("lowp"),

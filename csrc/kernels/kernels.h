@@ -225,6 +225,10 @@ void avgpool_bwd_launch(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipS
 // losses -------------------------------------------------------------------------------------
 void softmax_xent_launch(const void* logits, bool bf16, const int64_t* labels, float* loss,
                          void* grad, int N, int K, float smoothing, hipStream_t st);
+// evaluation head: probs (optional) = softmax rows (fp32); with labels, loss_sum += Σ row CE and
+// correct += Σ [argmax == label] (either may be null)
+void softmax_eval_launch(const void* logits, bool bf16, const int64_t* labels, float* loss_sum,
+                         float* correct, float* probs, int N, int K, hipStream_t st);
 void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* labels, int label_kind,
                          float* loss, float* grad, int B, int P, hipStream_t st);
 // P > 16384 pixels per image: multi-pass global bitonic sort; key / idx hold B × padded_len(P)

@@ -99,6 +99,55 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const void* __restric
   }
 }
 
+// Forward-only classification head for evaluation / prediction (no gradient): per row the
+// softmax probabilities (optional, fp32), and with labels the summed cross-entropy and the count
+// of rows whose argmax (first maximal index, like torch.argmax) is the label.  One workgroup per
+// row; deterministic mode sums the per-row terms in row order.
+__global__ void __launch_bounds__(256) softmax_eval_kernel(const void* __restrict__ logits, int bf,
+                                                           const int64_t* __restrict__ labels,
+                                                           float* __restrict__ loss_sum,
+                                                           float* __restrict__ correct,
+                                                           float* __restrict__ probs, int N, int K,
+                                                           float* __restrict__ slab) {
+  __shared__ float sh[4];
+  __shared__ int shi[4];
+  const int row = blockIdx.x;
+  const long base = (long)row * K;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < K; i += 256) mx = fmaxf(mx, ld(logits, bf, base + i));
+  mx = block_max<256>(mx, sh);
+  float se = 0.f;
+  int first = K;
+  for (int i = threadIdx.x; i < K; i += 256) {
+    const float v = ld(logits, bf, base + i);
+    se += __expf(v - mx);
+    if (v == mx && i < first) first = i;
+  }
+  se = block_sum<256>(se, sh);
+  // block minimum of the first maximal index
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
+  if ((threadIdx.x & 63) == 0) shi[threadIdx.x >> 6] = first;
+  __syncthreads();
+  first = min(min(shi[0], shi[1]), min(shi[2], shi[3]));
+  const float lse = mx + __logf(se);
+  if (probs) {
+    for (int i = threadIdx.x; i < K; i += 256) probs[base + i] = __expf(ld(logits, bf, base + i) - lse);
+  }
+  if (labels && threadIdx.x == 0) {
+    const int lab = (int)labels[row];
+    const float l = lse - ld(logits, bf, base + lab);
+    const float c = first == lab ? 1.f : 0.f;
+    if (slab) {
+      slab[row] = l;
+      slab[N + row] = c;
+    } else {
+      if (loss_sum) atomicAdd(loss_sum, l);
+      if (correct) atomicAdd(correct, c);
+    }
+  }
+}
+
 // --------------------------------------------------------------------------------------------
 // Lovász hinge
 // --------------------------------------------------------------------------------------------
@@ -417,6 +466,17 @@ void softmax_xent_launch(const void* logits, bool bf16, const int64_t* labels, f
   hipLaunchKernelGGL(softmax_xent_kernel, dim3(N), dim3(256), 0, st, logits, bf16 ? 1 : 0, labels,
                      loss, grad, N, K, smoothing, slab);
   if (slab) slab_sum_launch(slab, loss, N, 1, 1, st);
+}
+
+void softmax_eval_launch(const void* logits, bool bf16, const int64_t* labels, float* loss_sum,
+                         float* correct, float* probs, int N, int K, hipStream_t st) {
+  float* slab = (labels && deterministic()) ? det_slab((size_t)2 * N, st) : nullptr;
+  hipLaunchKernelGGL(softmax_eval_kernel, dim3(N), dim3(256), 0, st, logits, bf16 ? 1 : 0, labels,
+                     loss_sum, correct, probs, N, K, slab);
+  if (slab) {
+    if (loss_sum) slab_sum_launch(slab, loss_sum, N, 1, 1, st);
+    if (correct) slab_sum_launch(slab + N, correct, N, 1, 1, st);
+  }
 }
 
 void lovasz_hinge_launch(const void* logits, bool logits_bf16, const void* labels, int label_kind,

@@ -22,6 +22,7 @@ import torch.nn as nn
 from ..models.deeplab import DeepLabResNet, BetaUnit
 from ..models.layers import ConvBN, Conv2d
 from ..ops.pool import global_avg_pool
+from ..ops.loss import softmax_eval
 from ._scope import get_or_create, to_nhwc, from_nhwc, device_of
 
 _DEFAULT_MULTI_GRID = [2, 2, 2]
@@ -148,7 +149,9 @@ class ResNetV2Beta(nn.Module):
             if net.shape[-1] != self.num_classes:
                 net = net[..., :self.num_classes].contiguous()
             ep[f"{scope}/logits"] = net
-            ep["predictions"] = torch.softmax(net.float(), dim=-1)
+            # the HIP softmax head (ops/loss.softmax_eval; fp32 rows on the CPU)
+            ep["predictions"] = softmax_eval(net.reshape(-1, net.shape[-1]), probs=True)[2] \
+                .reshape(net.shape)
         return net, ep
 
 

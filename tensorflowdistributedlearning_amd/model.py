@@ -57,7 +57,7 @@ from .engine import schedules
 from .models.deeplab import DeepLabResNet
 from . import models as _models
 from .models.params import FlatParams
-from .ops.loss import lovasz_hinge, softmax_cross_entropy
+from .ops.loss import lovasz_hinge, softmax_cross_entropy, softmax_eval
 from .ops.metrics import seg_scores, StreamingMean
 from .ops.optim import exponential_decay
 from .preprocessing.preprocessing import _prepare_directory, create_symlinks, TRAIN, EVAL
@@ -514,7 +514,12 @@ class Model:
                 compute_dtype=self._serving_dtype(device))
         correct = StreamingMean(device)
         saver = ckpt.AsyncSaver()  # D2H on a copy stream, file write on a worker thread
-        eval_result, history = {}, []
+        eval_result = {}
+        # per-step losses land in one preallocated device buffer (no per-step allocation or host
+        # sync; read once when the fold ends)
+        history = torch.zeros(max(steps - start, 0), dtype=torch.float32, device=device) \
+            if main else None
+        n_hist = 0
         step = start
         t0 = time.time()
         clock = _StepClock(device, start)
@@ -523,9 +528,11 @@ class Model:
             loss, out = stepper(x, yy)
             step = trainer.global_step
             clock.tick(step)
-            correct.update((out.float().argmax(-1) == yy).float())
-            if main:
-                history.append(loss.detach().clone() if stepper.graph else loss.detach())
+            _, top1, _ = softmax_eval(out, yy)  # top-1 count in one HIP launch
+            correct.update_sum(top1, yy.shape[0])
+            if main and n_hist < history.numel():
+                history[n_hist].copy_(loss.detach().reshape(()))
+                n_hist += 1
             if self.save_summary_steps and step % self.save_summary_steps == 0 and main:
                 tw.scalars({"metrics/accuracy": float(correct.result()),
                             "loss/softmax_cross_entropy": float(loss),
@@ -551,7 +558,8 @@ class Model:
         tw.close()
         ew.close()
         res = {"fold": fold, "n_params": self.n_params, "eval": eval_result, "steps": step,
-               "train_loss": [float(v) for v in history], "hip_graph": stepper.graph,
+               "train_loss": history[:n_hist].cpu().tolist() if history is not None else [],
+               "hip_graph": stepper.graph,
                "steady_ms_per_step": clock.result(step)}
         if main:
             with open(os.path.join(fold_dir, "result.json"), "w") as f:
@@ -569,10 +577,10 @@ class Model:
         for i, (x, yy) in enumerate(pipe):
             if self.eval_batches is not None and i >= self.eval_batches:
                 break
-            out = net(x).float()
             n = x.shape[0]
-            loss = torch.nn.functional.cross_entropy(out, yy)
-            sums += torch.stack([(out.argmax(-1) == yy).double().sum(), loss.double() * n,
+            # loss sum and top-1 count in one HIP launch (ops/loss.softmax_eval)
+            loss_sum, correct, _ = softmax_eval(net(x), yy)
+            sums += torch.stack([correct.double(), loss_sum.double(),
                                  torch.tensor(float(n), dtype=torch.float64, device=device)])
         if ctx.is_distributed:
             s = sums.to(ctx.device) if ctx.native is not None else sums.cpu()
@@ -612,7 +620,7 @@ class Model:
                 net._tdl_flat = FlatParams(net, device, lowp_dtype=torch.bfloat16, with_grad=False)
             net.eval()
             labels = np.zeros(len(ids), dtype=np.int64)  # unused by the image sources
-            probs = [torch.softmax(net(x).float(), -1).cpu() for x, _ in ClassificationPipeline(
+            probs = [softmax_eval(net(x), probs=True)[2].cpu() for x, _ in ClassificationPipeline(
                 src, ids, labels, batch_size, shuffle=False, repeat=False, device=device,
                 dtype=dtype)]
             p = torch.cat(probs)

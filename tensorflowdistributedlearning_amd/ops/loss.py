@@ -61,6 +61,33 @@ def softmax_cross_entropy(logits, labels, label_smoothing=0.0):
     return _SoftmaxXentFn.apply(logits, labels, label_smoothing)
 
 
+def softmax_eval(logits, labels=None, probs=False):
+    """Forward-only classification head (evaluation / prediction, no gradient): returns
+    ``(loss_sum, correct, p)`` — the summed softmax cross-entropy and the number of rows whose
+    argmax is the label (fp32 device scalars, None without ``labels``) and the fp32 softmax
+    probabilities [N, K] when ``probs``.  GPU: one HIP launch (``loss.hip`` softmax_eval_kernel);
+    CPU: the fp32 reference ops."""
+    logits = logits.contiguous()
+    if logits.dim() != 2:
+        raise ValueError(f"softmax_eval: logits [N, K], got {tuple(logits.shape)}")
+    if on_gpu(logits) and logits.dtype in (torch.bfloat16, torch.float32):
+        dev = logits.device
+        ls = torch.zeros(1, device=dev) if labels is not None else None
+        cr = torch.zeros(1, device=dev) if labels is not None else None
+        p = torch.empty(logits.shape, device=dev, dtype=torch.float32) if probs else None
+        lab = labels.to(device=dev, dtype=torch.int64).contiguous() if labels is not None else None
+        ext().softmax_eval(logits, lab, ls, cr, p)
+        return (ls[0] if ls is not None else None), (cr[0] if cr is not None else None), p
+    lf = logits.float()
+    p = torch.softmax(lf, -1) if probs else None
+    if labels is None:
+        return None, None, p
+    lab = labels.long().view(-1)
+    ls = (torch.logsumexp(lf, -1) - lf.gather(1, lab.view(-1, 1)).view(-1)).sum()
+    cr = (lf.argmax(-1) == lab).float().sum()
+    return ls, cr, p
+
+
 # ----------------------------------------------------------------------------------------------
 # Lovász hinge (binary, per image)
 # ----------------------------------------------------------------------------------------------

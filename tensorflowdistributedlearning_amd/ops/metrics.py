@@ -58,6 +58,12 @@ class StreamingMean:
         self.count += v.numel()
         return self.result()
 
+    def update_sum(self, total, count):
+        """Fold in a pre-reduced batch: ``total`` (device scalar) over ``count`` values."""
+        self.total += total.detach().double()
+        self.count += float(count)
+        return self.result()
+
     def result(self):
         return self.total / self.count.clamp_min(1)
 
