@@ -109,7 +109,7 @@ def bench_config(args):
     over = {"arch": args.model, "batch": args.batch, "image_size": args.image_size,
             "steps": args.steps, "warmup": args.warmup, "lr": args.lr,
             "bucket_mb": args.bucket_mb, "first_bucket_mb": args.first_bucket_mb,
-            "optimizer": args.optimizer, "dtype": args.dtype}
+            "optimizer": args.optimizer, "dtype": args.dtype, "grad_dtype": args.grad_dtype}
     for k, v in over.items():
         if v is not None:
             setattr(cfg, k, v)
@@ -132,6 +132,9 @@ def main():
     ap.add_argument("--image-size", type=int, default=None)
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--first-bucket-mb", type=float, default=None)
+    ap.add_argument("--grad-dtype", choices=("fp32", "bf16"), default=None,
+                    help="dtype of the bucketed gradient all-reduces (bf16: half the xGMI bytes, "
+                         "fp32 accumulation in the optimizer; default fp32)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--optimizer", choices=("sgd_momentum", "adam"), default=None)
     ap.add_argument("--fp8", action="store_true",
@@ -201,13 +204,14 @@ def main():
         model = models.DeepLabResNet(model_name="model", input_shape=(101, 101))
         tr = Trainer(model, lovasz_hinge, dev, _opt(bc.optimizer), _opt_kw(bc), ctx=ctx,
                      bucket_mb=bc.bucket_mb, first_bucket_mb=bc.first_bucket_mb,
-                     profile_phases=args.profile_phases, lowp_dtype=lowp)
+                     profile_phases=args.profile_phases, lowp_dtype=lowp,
+                     grad_comm_dtype=torch.bfloat16 if bc.grad_dtype == "bf16" else torch.float32)
         x, y = segmentation_batch(per_gpu, device=dev, seed=ctx.rank, dtype=ddt)
         metric = ("images/sec (whole node), reference DeepLab-ResNet 101x101x2 "
                   + ("bf16" if gpu_bf16 else "fp32"))
         cfg = {"model": "deeplab_resnet_v2_beta(3,4,6) os8", "global_batch": per_gpu * n,
                "image": "101x101x2", "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks, "optimizer": bc.optimizer,
-               "loss": "lovasz_hinge", "hip_graph": bc.graph,
+               "loss": "lovasz_hinge", "hip_graph": bc.graph, "grad_comm_dtype": bc.grad_dtype,
                "wgrad_side_stream": streams.enabled()}
         base = REF_DEEPLAB_2GPU / 2 * n
     else:
@@ -223,7 +227,8 @@ def main():
                         "wgrad + BN)")
         tr = Trainer(model, softmax_cross_entropy, dev, _opt(bc.optimizer), _opt_kw(bc), ctx=ctx,
                      bucket_mb=bc.bucket_mb, first_bucket_mb=bc.first_bucket_mb,
-                     profile_phases=args.profile_phases, lowp_dtype=lowp)
+                     profile_phases=args.profile_phases, lowp_dtype=lowp,
+                     grad_comm_dtype=torch.bfloat16 if bc.grad_dtype == "bf16" else torch.float32)
         x, y = imagenet_batch(per_gpu, bc.image_size, device=dev, seed=ctx.rank, dtype=ddt)
         metric = METRIC if bc.arch == "resnet50" and bc.image_size == 224 and gpu_bf16 \
             else (f"images/sec (whole node), {bc.arch} {bc.image_size}x{bc.image_size} "
@@ -232,7 +237,7 @@ def main():
                "image": f"{bc.image_size}x{bc.image_size}x3", "per_gpu_batch": per_gpu,
                "parallelism": f"dp{n}", "comm": comm, "rccl_ranks": rccl_ranks,
                "optimizer": bc.optimizer,
-               "loss": "softmax_ce", "hip_graph": bc.graph,
+               "loss": "softmax_ce", "hip_graph": bc.graph, "grad_comm_dtype": bc.grad_dtype,
                "wgrad_side_stream": streams.enabled()}
         base = REF_PER_GPU_DERIVED * n
 
@@ -301,7 +306,8 @@ def main():
         alone = ctx.all_reduce_max(tr.bucketer.standalone_ms())
         comm_stats = {"exposed_ms": round(exposed, 3), "standalone_ms": round(alone, 3),
                       "overlap": round(max(0.0, 1.0 - exposed / alone), 3) if alone > 0 else None,
-                      "buckets": len(tr.bucketer.buckets)}
+                      "buckets": len(tr.bucketer.buckets),
+                      "comm_mb_per_step": round(tr.bucketer.comm_bytes / 2 ** 20, 1)}
     value = per_gpu * n * bc.steps / el
     if ctx.is_main:
         if dev.type == "cuda":

@@ -765,6 +765,19 @@ void scale_by_scalar(Tensor x, Tensor s, Tensor y) {
   scale_by_scalar_launch(x.data_ptr(), s.data_ptr<float>(), y.data_ptr(), x.numel(), bf, stream());
 }
 
+// dtype conversion between a flat fp32 and a flat bf16 buffer (either direction)
+void convert(Tensor x, Tensor y) {
+  TORCH_CHECK(x.is_cuda() && y.is_cuda() && x.is_contiguous() && y.is_contiguous() &&
+              x.numel() == y.numel(), "convert: contiguous GPU tensors of equal numel");
+  const bool xb = x.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK((xb && y.scalar_type() == torch::kFloat32) ||
+              (x.scalar_type() == torch::kFloat32 && y.scalar_type() == torch::kBFloat16),
+              "convert: fp32 <-> bf16");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0) &&
+              (reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0), "convert: 16-B aligned");
+  convert_launch(x.data_ptr(), xb, y.data_ptr(), x.numel(), stream());
+}
+
 void sigmoid_threshold(Tensor x, Tensor prob, Tensor pred, double thr) {
   const bool bf = x.scalar_type() == torch::kBFloat16;
   sigmoid_threshold_launch(x.data_ptr(), bf, prob.data_ptr<float>(), pred.data_ptr<float>(),
@@ -1434,6 +1447,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("row_pack", &row_pack);
   m.def("add_act", &add_act);
   m.def("scale_by_scalar", &scale_by_scalar);
+  m.def("convert", &convert, "fp32 <-> bf16 flat conversion (RNE)");
   m.def("sigmoid_threshold", &sigmoid_threshold);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -179,6 +179,40 @@ void scale_by_scalar_launch(const void* x, const float* s, void* y, long n, bool
   hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(n)), dim3(NT), 0, st, x, s, y, n, bf16 ? 1 : 0);
 }
 
+// fp32 ↔ bf16 conversion (RNE) of flat buffers — the bf16 gradient buckets' pack / unpack
+// (parallel/bucketer.py); 8 elements per thread, grid-stride, scalar tail
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const float4 a = ((const float4*)x)[2 * i], b = ((const float4*)x)[2 * i + 1];
+    ((uint4*)y)[i] = make_uint4(cvt_pk_bf16(a.x, a.y), cvt_pk_bf16(a.z, a.w), cvt_pk_bf16(b.x, b.y),
+                                cvt_pk_bf16(b.z, b.w));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) y[n8 * 8 + threadIdx.x] = f2bf(x[n8 * 8 + threadIdx.x]);
+}
+
+__global__ void bf16_to_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long n) {
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float f[8];
+    unpack8(((const uint4*)x)[i], f);
+    ((float4*)y)[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    ((float4*)y)[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 7)) y[n8 * 8 + threadIdx.x] = bf2f(x[n8 * 8 + threadIdx.x]);
+}
+
+void convert_launch(const void* x, bool x_bf16, void* y, long n, hipStream_t st) {
+  if (n <= 0) return;
+  const int blocks = (int)std::min<long>(4096, std::max<long>(1, (n / 8 + NT - 1) / NT));
+  if (x_bf16)
+    hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(blocks), dim3(NT), 0, st, (const bf16_t*)x,
+                       (float*)y, n);
+  else
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(blocks), dim3(NT), 0, st, (const float*)x,
+                       (bf16_t*)y, n);
+}
+
 void sigmoid_threshold_launch(const void* x, bool x_bf16, float* prob, float* pred, long n,
                               float thr, hipStream_t st) {
   hipLaunchKernelGGL(sigmoid_threshold_kernel, dim3(blocks_for(n)), dim3(NT), 0, st, x,

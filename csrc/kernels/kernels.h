@@ -203,6 +203,8 @@ void add_act_launch(const bf16_t* a, const bf16_t* b, bf16_t* y, long n, bool re
                     hipStream_t st);
 void scale_by_scalar_launch(const void* x, const float* s, void* y, long n, bool bf16,
                             hipStream_t st);
+// fp32 → bf16 (RNE) or bf16 → fp32 of n contiguous elements (16-B aligned buffers)
+void convert_launch(const void* x, bool x_bf16, void* y, long n, hipStream_t st);
 void sigmoid_threshold_launch(const void* x, bool x_bf16, float* prob, float* pred, long n,
                               float thr, hipStream_t st);
 

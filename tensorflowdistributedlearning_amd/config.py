@@ -119,11 +119,14 @@ class BenchConfig:
     weight_decay: float = 5e-5
     bucket_mb: float = 32.0
     first_bucket_mb: float = 4.0
+    grad_dtype: str = "fp32"          # dtype of the bucketed gradient all-reduces (fp32 | bf16)
     fp8_dgrad: bool = False
     graph: bool = False
     extra: dict = field(default_factory=dict)
 
     def validate(self):
+        if self.grad_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"unknown gradient bucket dtype {self.grad_dtype}")
         if self.arch not in SEGMENTATION_ARCHS + CLASSIFIER_ARCHS:
             raise ValueError(f"unknown arch {self.arch}")
         seg = self.arch in SEGMENTATION_ARCHS

@@ -69,7 +69,8 @@ class PhaseTimer:
 class Trainer:
     def __init__(self, model, loss_fn, device, optimizer="sgd", opt_kwargs=None, ctx=None,
                  bucket_mb=32.0, first_bucket_mb=4.0, lowp_dtype=torch.bfloat16,
-                 broadcast_init=True, extra_loss_fn=None, profile_phases=False):
+                 broadcast_init=True, extra_loss_fn=None, profile_phases=False,
+                 grad_comm_dtype=torch.float32):
         self.device = torch.device(device)
         self.model = model.to(self.device)
         self.loss_fn = loss_fn
@@ -79,7 +80,10 @@ class Trainer:
         if self.ctx.is_distributed and broadcast_init:
             self.broadcast_state()
         self.optimizer = build_optimizer(optimizer, self.flat, **(opt_kwargs or {}))
-        self.bucketer = (GradBucketer(self.flat, self.ctx, bucket_mb, first_bucket_mb)
+        # grad_comm_dtype: the dtype the bucketed all-reduces move (bf16: half the bytes; the
+        # optimizer still accumulates into fp32, parallel/bucketer.py)
+        self.bucketer = (GradBucketer(self.flat, self.ctx, bucket_mb, first_bucket_mb,
+                                      comm_dtype=grad_comm_dtype)
                          if self.ctx.is_distributed else None)
         self.global_step = 0
         self.train_mode = True  # False: BN uses moving statistics while training (frozen BN)

@@ -33,6 +33,13 @@ gradient that was still changing — and :meth:`finish` records parameters that 
 ``strict=True``).  ``early_launches`` counts the collectives issued from the hooks, i.e. while
 backward was still running (the overlap), as opposed to those forced by :meth:`finish`.
 
+bf16 gradient buckets (``comm_dtype=torch.bfloat16``, SURVEY §5.8 "bf16/fp32 gradient buckets"):
+each bucket's fp32 gradients are packed into a bf16 mirror of the flat gradient buffer on the
+issuing stream (``ext().convert``, one pass over the slice), the collective runs on the bf16
+slice — half the bytes on xGMI — and :meth:`finish` unpacks the whole mirror back into the fp32
+buffer in one pass after the collectives, so the optimizer still accumulates in fp32.  The RCCL /
+gloo reduction itself sums in bf16 (an option for communication-bound runs, off by default).
+
 A ``comm_hook`` can replace the collective (used by tests to record launch order with a fake
 communicator, or to snapshot each bucket in stream order: tests/test_bucket_order_gpu.py).
 """
@@ -55,7 +62,7 @@ class Bucket:
 
     @property
     def nbytes(self):
-        return (self.hi - self.lo) * 4
+        return (self.hi - self.lo) * 4  # (fp32 slice; a bf16 bucket moves half)
 
     @staticmethod
     def hi_of(p, flat):
@@ -65,9 +72,16 @@ class Bucket:
 
 class GradBucketer:
     def __init__(self, flat, ctx=None, bucket_mb=32.0, first_bucket_mb=4.0, comm_hook=None,
-                 group=None, strict=False):
+                 group=None, strict=False, comm_dtype=torch.float32):
         self.flat = flat
         self.strict = strict
+        if comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"gradient bucket dtype: float32 or bfloat16, not {comm_dtype}")
+        self.comm_dtype = comm_dtype
+        # the bf16 mirror of the flat gradient buffer the collectives run on (bf16 buckets)
+        self.comm16 = (torch.zeros(flat.grad.numel(), dtype=torch.bfloat16,
+                                   device=flat.grad.device)
+                       if comm_dtype == torch.bfloat16 else None)
         self._seen = {}          # id(param) -> contributions delivered this step
         self.early_launches = 0  # collectives issued from hooks in the last finished step
         self._early = 0
@@ -160,11 +174,35 @@ class GradBucketer:
         view = self.flat.grad[b.lo:b.hi]
         issuer = self.issue_stream(view.device) if view.is_cuda else None
         if issuer is None:
-            self._issue(b, view)
+            self._issue(b, self._pack(b, view))
         else:
             with streams.on(issuer):
-                self._issue(b, view)
+                self._issue(b, self._pack(b, view))
         b.launched = True
+
+    def _pack(self, b, view):
+        """The tensor the collective runs on: the fp32 slice, or its bf16 copy (packed on the
+        current stream, i.e. after the bucket's producers)."""
+        if self.comm16 is None:
+            return view
+        v16 = self.comm16[b.lo:b.hi]
+        if view.is_cuda:
+            from ..ops.common import ext
+            ext().convert(view, v16)
+        else:
+            v16.copy_(view)
+        return v16
+
+    def _unpack(self):
+        """bf16 buckets: the reduced bf16 mirror back into the fp32 gradient buffer (one pass, on
+        the current stream, after every collective was waited for)."""
+        if self.comm16 is None:
+            return
+        if self.flat.grad.is_cuda:
+            from ..ops.common import ext
+            ext().convert(self.comm16, self.flat.grad)
+        else:
+            self.flat.grad.copy_(self.comm16)
 
     @staticmethod
     def issue_stream(device):
@@ -216,6 +254,7 @@ class GradBucketer:
             b.launched = False
             b.pending = len(b.params)
         self.next_launch = 0
+        self._unpack()
         if self.ctx is not None and hasattr(self.ctx, "check"):
             self.ctx.check()  # native comm watchdog: fail fast on timeout / RCCL error
         if missing and self.strict:
@@ -237,7 +276,7 @@ class GradBucketer:
                 e0.record()
             t0 = time.perf_counter()
             for b in self.buckets:
-                self._issue(b, self.flat.grad[b.lo:b.hi])
+                self._issue(b, self._pack(b, self.flat.grad[b.lo:b.hi]))
             for b in self.buckets:
                 if b.work is not None and hasattr(b.work, "wait"):
                     b.work.wait()
@@ -252,3 +291,9 @@ class GradBucketer:
 
     def describe(self):
         return [(b.index, len(b.params), b.nbytes) for b in self.buckets]
+
+    @property
+    def comm_bytes(self):
+        """Bytes one step's collectives move per rank (before the ring's 2·(n−1)/n factor)."""
+        per = 2 if self.comm16 is not None else 4
+        return sum((b.hi - b.lo) * per for b in self.buckets)

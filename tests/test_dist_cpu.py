@@ -120,7 +120,7 @@ def test_bucketer_counts_final_deliveries_not_hook_calls():
     assert len(b.last_missing) == len(f.params) - 1 and b.next_launch == 0
 
 
-def _dp_worker(rank, tmpdir, world=2):
+def _dp_worker(rank, tmpdir, world=2, grad_dtype="fp32"):
     import torch
     from tensorflowdistributedlearning_amd.parallel.dist import init_distributed, shutdown
     from tensorflowdistributedlearning_amd.engine.trainer import Trainer
@@ -132,7 +132,8 @@ def _dp_worker(rank, tmpdir, world=2):
     m = TinyNet()
     tr = Trainer(m, softmax_cross_entropy, "cpu", "sgd", dict(lr=0.1, momentum=0.9,
                                                               weight_decay=1e-4),
-                 ctx=ctx, bucket_mb=0.004, first_bucket_mb=0.001, lowp_dtype=None)
+                 ctx=ctx, bucket_mb=0.004, first_bucket_mb=0.001, lowp_dtype=None,
+                 grad_comm_dtype=torch.bfloat16 if grad_dtype == "bf16" else torch.float32)
     g = torch.Generator().manual_seed(7)
     x = torch.randn(8, 8, 8, 8, generator=g)
     y = torch.randint(0, 5, (8,), generator=g)
@@ -145,11 +146,12 @@ def _dp_worker(rank, tmpdir, world=2):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("world", [2, 4])
-def test_gloo_dp_equals_large_batch(tmp_path, world):
+@pytest.mark.parametrize("world,grad_dtype", [(2, "fp32"), (4, "fp32"), (2, "bf16")])
+def test_gloo_dp_equals_large_batch(tmp_path, world, grad_dtype):
     """W ranks × batch 8/W with mean-gradient all-reduce == 1 process × batch 8 (rank 0's
-    parameters broadcast at start: rank 1 starts from different weights)."""
-    launcher.spawn(_dp_worker, world, args=(str(tmp_path), world))
+    parameters broadcast at start: rank 1 starts from different weights).  bf16 gradient buckets
+    (parallel/bucketer.py): the replicas stay bit-identical and track fp32 to bf16 rounding."""
+    launcher.spawn(_dp_worker, world, args=(str(tmp_path), world, grad_dtype))
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     for r in range(1, world):  # replicas stay identical
         assert torch.equal(r0, torch.load(tmp_path / f"rank{r}.pt", weights_only=True))
@@ -164,7 +166,12 @@ def test_gloo_dp_equals_large_batch(tmp_path, world):
     y = torch.randint(0, 5, (8,), generator=g)
     for _ in range(3):
         tr.train_step(x, y)
-    assert torch.allclose(r0, tr.flat.master, atol=1e-5, rtol=1e-4)
+    if grad_dtype == "bf16":  # gradients rounded to 8 mantissa bits before the reduction
+        rel = ((r0 - tr.flat.master).norm() / tr.flat.master.norm()).item()
+        assert rel < 2e-3, rel
+        assert not torch.equal(r0, tr.flat.master)  # the bf16 path really ran
+    else:
+        assert torch.allclose(r0, tr.flat.master, atol=1e-5, rtol=1e-4)
 
 
 def test_phase_timer_cpu():
