@@ -183,7 +183,8 @@ class Trainer:
         step (ops/fp8.RingRoller), so no kernel argument changes between steps."""
         if self.device.type != "cuda":
             raise RuntimeError("graph capture needs a GPU")
-        if self.bucketer is not None and getattr(self.ctx, "native", None) is None:
+        if (self.bucketer is not None and self.bucketer.comm_hook is None
+                and getattr(self.ctx, "native", None) is None):
             raise RuntimeError("data-parallel graph capture needs the native RCCL communicator "
                                "(GPU ranks; not the TDL_SHARE_GPU gloo rehearsal)")
         self.timer = None

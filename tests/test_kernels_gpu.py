@@ -1135,3 +1135,23 @@ def test_depthwise_tiles_at_xception_scale(gpu, hw, c, stride, relu_in):
     y.backward(dy.to(gpu))
     assert rel_err(xg.grad, xr.grad) < 2e-2
     assert rel_err(wp.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_softmax_eval_head(gpu, dtype):
+    """The forward-only classification head (evaluation / prediction): CE sum, top-1 count (first
+    maximal index, ties included) and fp32 probabilities vs the fp32 reference."""
+    torch.manual_seed(4)
+    logits = (torch.randn(37, 1000) * 3).to(dtype)
+    logits[5, 10] = logits[5, 20] = logits[5].float().max() + 1  # a tie: argmax is the first
+    labels = torch.randint(0, 1000, (37,))
+    labels[5] = 10
+    labels[:8] = logits[:8].float().argmax(-1)
+    ls, cr, p = L.softmax_eval(logits.to(gpu), labels.to(gpu), probs=True)
+    lf = logits.float()
+    ref_ls = (torch.logsumexp(lf, -1) - lf.gather(1, labels.view(-1, 1)).view(-1)).sum()
+    assert abs(float(ls) - float(ref_ls)) < 1e-4 * float(ref_ls)
+    assert float(cr) == float((lf.argmax(-1) == labels).sum())
+    assert rel_err(p, torch.softmax(lf, -1)) < 1e-5
+    _, _, p2 = L.softmax_eval(logits.to(gpu), probs=True)
+    assert torch.equal(p2, p)
