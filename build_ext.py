@@ -62,7 +62,7 @@ def build(verbose=True, force=False):
     jobs = []
     common = ["-O3", "-std=c++17", "-fPIC", "-I" + CSRC, "-Wno-unused-result",
               "-Wno-deprecated-declarations"]
-    if os.environ.get("TDL_CONV_ABLATION") == "1":  # timing-only TDL_CONV_DBG flags (tools/*_ablate.py)
+    if os.environ.get("TDL_CONV_ABLATION") == "1":  # timing-only TDL_CONV_DBG flags (dev/tools/*_ablate.py)
         common.append("-DTDL_CONV_ABLATION=1")
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(OBJ, os.path.basename(src) + ".o")

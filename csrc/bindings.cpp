@@ -346,10 +346,13 @@ void fp8_dequantize(Tensor y8, Tensor scale, Tensor out) {
 // aff (optional, with bn_x / bn_red): the ReLU mask of a folded BN — dx · [aff[0]·bn_x + aff[1]
 // > 0] — applied together with the fused statistics; the return value says whether both ran
 // (otherwise dx is unmasked and the BN backward masks: relu mode 2)
+// w_flip (optional, stride 1): the flipped, transposed weights [C][R][S][K] (conv_flip_weight) —
+// the input gradient may then run as the forward conv of dy (conv_dgrad_as_fwd)
 bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
                 int64_t dh, int64_t dw, bool accumulate, c10::optional<Tensor> mask,
                 c10::optional<Tensor> w_t, c10::optional<Tensor> bn_x,
-                c10::optional<Tensor> bn_red, c10::optional<Tensor> aff) {
+                c10::optional<Tensor> bn_red, c10::optional<Tensor> aff,
+                c10::optional<Tensor> w_flip) {
   if (is_f32(dy)) {
     TORCH_CHECK(!(aff.has_value() && aff->defined()), "fp32 conv_dgrad: no folded BN");
     return conv_dgrad_f32(dy, w, dx, sh, sw, ph, pw, dh, dw, accumulate, mask);
@@ -378,6 +381,16 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
                 w_t->size(2) == a.C && w_t->size(3) == a.K && w_t->is_contiguous(),
                 "conv_dgrad w_t must be the [R,S,C,K] transpose of w");
     a.w_t = BF(*w_t);
+  }
+  a.w_flip = nullptr;
+  a.w_flip_bytes = 0;
+  if (w_flip.has_value() && w_flip->defined()) {
+    CHECK_T(*w_flip, torch::kBFloat16);
+    TORCH_CHECK(w_flip->dim() == 4 && w_flip->size(0) == a.C && w_flip->size(1) == a.R &&
+                w_flip->size(2) == a.S && w_flip->size(3) == a.K && w_flip->is_contiguous(),
+                "conv_dgrad w_flip must be the [C,R,S,K] flipped transpose of w");
+    a.w_flip = BF(*w_flip);
+    a.w_flip_bytes = nbytes32(*w_flip);
   }
   a.stats = nullptr;
   a.bn_x = nullptr;
@@ -1391,7 +1404,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("sh"),
         py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"),
         py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none(),
-        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none(), py::arg("aff") = py::none());
+        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none(), py::arg("aff") = py::none(),
+        py::arg("w_flip") = py::none());
+  m.def("conv_flip_weight", [](Tensor w, Tensor wf) {
+    CHECK_T(w, torch::kBFloat16);
+    CHECK_T(wf, torch::kBFloat16);
+    TORCH_CHECK(w.dim() == 4 && wf.dim() == 4 && w.is_contiguous() && wf.is_contiguous() &&
+                wf.size(0) == w.size(3) && wf.size(1) == w.size(1) && wf.size(2) == w.size(2) &&
+                wf.size(3) == w.size(0), "conv_flip_weight: w [K,R,S,C] -> wf [C,R,S,K]");
+    conv_flip_weight_launch(BF(w), BFW(wf), w.size(0), w.size(1), w.size(2), w.size(3), stream());
+  }, "w_flip[c][r][s][k] = w[k][R-1-r][S-1-s][c]");
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("out"),
         py::arg("bias_grad"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dh"), py::arg("dw"), py::arg("accumulate"), py::arg("aff") = py::none());

@@ -299,7 +299,7 @@ void reduce_launch(const bf16_t* a, const bf16_t* y, const bf16_t* x, const floa
     static const int minr = env_int("TDL_BN_RED_MINR", 8);
     static const bool ntm = env_int("TDL_BN_NT", 1) != 0;  // non-temporal streaming
     // optional cap on the atomics per launch (every workgroup adds 2C partial sums): measured
-    // (tools/bn_micro.py) 1 Mi: b256 reduce total 2.92 -> 2.85 ms but b1024 8.43 -> 8.86 ms —
+    // (dev/tools/bn_micro.py) 1 Mi: b256 reduce total 2.92 -> 2.85 ms but b1024 8.43 -> 8.86 ms —
     // fewer workgroups cost more bandwidth than the atomics save; off by default
     static const long atom = env_int("TDL_BN_RED_ATOM", 1 << 30);
     const long cap_atom = std::max<long>(128, atom / (2L * C));

@@ -298,7 +298,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
   // per-element epilogue (64-bit row math, integer divisions, per-fragment validity selects,
   // runtime mask / join / ReLU tests on every value) cost ≈1,200 VALU instructions per wave
   // per tile — at 4 cycles per wave64 VALU op that, not HBM, paced the 1–4-K-step tiles of
-  // 1×1 convs (tools/dgrad_ablate.py: 129 µs for a 1×1 dgrad with no memory traffic).
+  // 1×1 convs (dev/tools/dgrad_ablate.py: 129 µs for a 1×1 dgrad with no memory traffic).
   v4u32 bias_v[RN];
   if constexpr (BIAS) {
     const rsrc_t rbias = make_rsrc(a.bias, (uint32_t)a.Ng * 4u);

@@ -831,6 +831,10 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   const bool masked = (a.sh > 1 && a.dh > 1) || (a.sw > 1 && a.dw > 1) ||
                       a.sh * a.sw > MAX_DG_CLASSES;
   a.dg_masked = masked ? 1 : 0;
+  if (!masked && a.sh == 1 && a.sw == 1 && a.w_flip) {  // stride 1: as the forward conv of dy
+    bool fused = false;
+    if (conv_dgrad_as_fwd(a, a.w_flip, a.w_flip_bytes, st, &fused)) return fused;
+  }
   if (!masked && a.sh == 1 && a.sw == 1) {  // stride 1: the halo-tiled direct conv
     bool fused = false;
     if (conv_dgrad_halo(a, st, &fused)) return fused;

@@ -107,7 +107,7 @@ __device__ __forceinline__ bf16x8 lds_read_mc(uint32_t tile, int krow, int col) 
 }
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 // fp8 A/B fragment of v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds bytes k = 32·(l>>4) … +31 of
-// row l&15 (any k permutation applied to both operands is exact; tools/mfma_fp8_layout.hip)
+// row l&15 (any k permutation applied to both operands is exact; dev/tools/mfma_fp8_layout.hip)
 __device__ __forceinline__ i32x8 lds_read_kc_f8(uint32_t tile, int row, int g) {
   uint4 lo, hi;
   asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(tile + (uint32_t)kc_off(row, 2 * g)) : "memory");
@@ -153,9 +153,14 @@ __device__ __forceinline__ void acc32_to_16(const f32x16 (&c)[QM][QN], f32x4 (&a
         }
 }
 
+// DEPI (FWD K loop): the DGRAD epilogue — a stride-1 input gradient computed as the forward conv
+// of dy with the flipped, transposed filter (conv_dgrad_as_fwd below): mask, residual join and
+// BN-backward statistics exactly as the DGRAD kernels store them
 template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool BIAS, int FK,
-          bool FP8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false>
+          bool FP8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false,
+          bool DEPI = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
+  static_assert(!DEPI || (MODE == FWD && !FP8 && !FRES && !BIAS), "dgrad epilogue on the FWD loop");
   // AFM: DGRAD statistics epilogue masking by a folded BN's a·x + b > 0 (conv_common.h)
   // M32: the K loop runs v_mfma_f32_32x32x16_bf16 on 32×32 blocks (half the MFMA instructions
   // and half the vector-issue hold per FLOP of the 16×16×32 form); accumulators are re-laid to
@@ -209,7 +214,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   const int wm = wid / WN, wn = wid % WN;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   // static priority 1 for the second-dispatched half of the waves, the arbitration loser of every
-  // segment (MI355X_MICROARCH.md, two waves per SIMD, item 4): 0–5 % (tools/fwd_ablate.py, dbg
+  // segment (MI355X_MICROARCH.md, two waves per SIMD, item 4): 0–5 % (dev/tools/fwd_ablate.py, dbg
   // 512 turns it off)
   if (!(DBG & 512) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int tile_begin = blk * a.tpb;
@@ -620,7 +625,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }
     } else {
       if constexpr (M32) acc32_to_16<QM, QN>(acc32, acc);
-      store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES, false, AFM>(
+      store_tile_bf16<DEPI ? DGRAD : MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES,
+                      false, AFM>(
           a, T, acc, wm, wn, lane, rout, out_scale, no_epi_mem, s_sum, s_sq);
     }
   };
@@ -907,9 +913,10 @@ constexpr int lds_bytes(int bm, int bn, int wm, int stages) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, int ST, bool STATS, bool BIAS, int FK,
-          bool F8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false>
+          bool F8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false,
+          bool DEPI = false>
 void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES, M32, AFM>;
+  auto k = conv_glds_kernel<MODE, BM, BN, WM, WN, ST, STATS, BIAS, FK, F8, NJ, FRES, M32, AFM, DEPI>;
   constexpr int lds = lds_bytes(BM, BN, WM, ST);
   static bool attr = false;
   if (!attr) {
@@ -1035,7 +1042,7 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   if (mode == 0 || a0.C % 8 || a0.K % 8) return false;
   if (a0.res && !a0.bias) return false;  // residual epilogue instantiated with bias only
   if (a0.aff && (a0.res || a0.C % 64)) return false;
-  // default selection (ResNet-50 b256, tools/n64_configs.py): ≥ 128 output channels, and 1×1
+  // default selection (ResNet-50 b256, dev/tools/n64_configs.py): ≥ 128 output channels, and 1×1
   // filters with 64 (the 8-wave 256×64 tiles: 35 vs 53 µs on 56×56 64→64); 3×3 filters with 64
   // output channels stay on the register-staged kernel
   const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
@@ -1049,7 +1056,7 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
   // fewer than half a tile per CU: the register-staged kernel's smaller tiles and two workgroups
   // per CU win (reference DeepLab preset, 13×13×1024→256 at batch 64: 20.6 vs 25.0 µs;
-  // tools/cfg_ab.py)
+  // dev/tools/cfg_ab.py)
   if (mode == 1 && ntm * ntn < 128) return false;
   a.ncls = 1;
   a.splits = 1;
@@ -1100,7 +1107,7 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
 #undef TDL_R
     return true;
   }
-  // TDL_M32=1: the 256×128 FASTK forward on 32×32×16 MFMA blocks (A/B: tools/m32_ab.py)
+  // TDL_M32=1: the 256×128 FASTK forward on 32×32×16 MFMA blocks (A/B: dev/tools/m32_ab.py)
   if (conv_m32() && fk == 1 && cfg == 0) {
     if (bias) {
       if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, true, 1, false, false, false, true>(a, blocks, st);
@@ -1126,6 +1133,104 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
 
 bool conv_fwd_res_launch(const ConvArgs& a, hipStream_t st) { return conv_fwd_glds(a, st); }
 
+// Stride-1 input gradient as the FORWARD conv of dy with the flipped, transposed filter:
+// dx[n,h,w,c] = Σ_{r',s',k} dy[n, h − ph' + r'·dh, w − pw' + s'·dw, k] · w_flip[c][r'][s'][k],
+// ph' = dh·(R−1) − ph — the forward kernels' K loop (LDS-DMA / producer-consumer; both operands
+// K-contiguous, no transposed LDS reads, no parity-class bookkeeping) with the DGRAD epilogue
+// (DEPI: ReLU bit mask, residual join, BN-backward statistics).  bench/dgrad_paths.py, ResNet-50
+// b1024: 3×3 dgrads 22–31 % faster than the DGRAD kernel, 1×1 3–15 %.
+bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, hipStream_t st,
+                       bool* fused) {
+  if (fused) *fused = false;
+  const int mode = conv_glds_mode();
+  if (mode == 0 || wf == nullptr || a0.fp8 || a0.aff || a0.dg_masked) return false;
+  if (a0.sh != 1 || a0.sw != 1 || a0.K % 64 || a0.C % 8 || a0.ldc != a0.C) return false;
+  // the DGRAD epilogue indexes dx through dy's geometry: same spatial size ("same" padding)
+  if (a0.Ho != a0.H || a0.Wo != a0.W) return false;
+  const int ph = a0.dh * (a0.R - 1) - a0.ph, pw = a0.dw * (a0.S - 1) - a0.pw;
+  if (ph < 0 || pw < 0) return false;
+  static const int on = env_int("TDL_DGRAD_AS_FWD", 1);
+  if (!on) return false;
+  ConvArgs a = a0;
+  a.x = a0.dy;
+  a.x_bytes = a0.dy_bytes;
+  a.w = wf;
+  a.w_bytes = wf_bytes;
+  a.w_t = nullptr;
+  a.C = a0.K;  // input channels of the forward conv: dy's
+  a.K = a0.C;  // its output channels: dx's
+  a.ph = ph;
+  a.pw = pw;
+  a.M = a.N * a.Ho * a.Wo;
+  a.Ng = a.K;
+  a.Kg = a.R * a.S * a.C;
+  a.relu = 0;
+  // one identity parity class for the epilogue's row mapping (out_row_fast<DGRAD>)
+  a.ncls = 1;
+  a.cls_a[0] = a.cls_b[0] = 0;
+  a.cls_Hc[0] = a.H;
+  a.cls_Wc[0] = a.W;
+  a.cls_r0[0] = a.cls_s0[0] = 0;
+  a.cls_Th[0] = a.R;
+  a.cls_Tw[0] = a.S;
+  a.dbg = 0;
+  a.splits = 1;
+  set_fastdivs(a);
+  const bool stats = a.stats != nullptr && a.bn_x != nullptr;
+  if (!stats) a.stats = nullptr;
+  if (stats && a.beta) return false;  // statistics + join: the DGRAD kernel's 8-wave tiles
+  const int cfg = a.Ng <= 64 ? 4 : 0;
+  const GCfg& g = cfg_of(cfg);
+  const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
+  if (mode == 1 && ((long)a.M < 4096 || ntm * ntn < 128)) return false;
+  a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm * ntn)), ntm);
+  const long groups = (ntm + a.tpb - 1) / a.tpb;
+  const int blocks = (int)(groups * ntn);
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+  // the producer/consumer kernel where the forward routes its 3×3 convs
+  if (cfg == 0 && a.R * a.S > 1 && a.C >= 256 && conv_fwd_pc_launch(a, blocks, 1, 2, st, true)) {
+    if (fused) *fused = stats;
+    return true;
+  }
+  if (cfg == 4) {
+    if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
+    else launch_g<FWD, 256, 64, 8, 1, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
+  } else {
+    if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
+    else launch_g<FWD, 256, 128, 4, 2, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
+  }
+  if (fused) *fused = stats;
+  return true;
+}
+
+// w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c]: a 32×32-element tiled transpose per filter tap
+__global__ void __launch_bounds__(256) flip_weight_kernel(const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ wf, int K, int R,
+                                                          int S, int C) {
+  __shared__ bf16_t t[32][33];
+  const int tap = blockIdx.z;  // r·S + s of the output
+  const int r = tap / S, s = tap - r * S;
+  const int src_tap = (R - 1 - r) * S + (S - 1 - s);
+  const int k0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 × 8
+  for (int i = ty; i < 32; i += 8) {
+    const int k = k0 + i, c = c0 + tx;
+    t[i][tx] = (k < K && c < C) ? w[((long)k * R * S + src_tap) * C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, k = k0 + tx;
+    if (c < C && k < K) wf[((long)c * R * S + tap) * K + k] = t[tx][i];
+  }
+}
+
+void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, int C,
+                             hipStream_t st) {
+  dim3 grid((unsigned)cdiv(C, 32), (unsigned)cdiv(K, 32), (unsigned)(R * S));
+  hipLaunchKernelGGL(flip_weight_kernel, grid, dim3(256), 0, st, w, wf, K, R, S, C);
+}
+
 // DGRAD with prepared parity classes (conv_dgrad_launch builds them); returns false when the
 // register-staged kernel should run instead.
 bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* fused) {
@@ -1136,7 +1241,7 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   } else {
     if (mode == 0 || a0.C % 8 || a0.K % 8 || a0.dg_masked) return false;
     // 1×1 filters with 64 input channels (dx width): 8-wave 256×64 tiles (49 vs 88 µs on
-    // ResNet-50 56×56 64→64, tools/n64_configs.py)
+    // ResNet-50 56×56 64→64, dev/tools/n64_configs.py)
     const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
     // with fused BN statistics the 64-wide 3×3 dgrads too (ResNet-50 layer1 conv2: the LDS-DMA
     // 8-wave 256×64 dgrad is within 5 % of the register-staged one, and the fusion saves the BN's
@@ -1175,7 +1280,7 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   const bool bn_stats = a.stats && a.bn_x && !a.fp8 && (a.K % 64 == 0 || rag_stats) &&
                         (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1)) && aff_ok;
   if (bn_stats) {
-    // tile config (tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
+    // tile config (dev/tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
     // tiles (NJ: no previous-dx registers); with the join's previous-dx loads as well they spill,
     // so 8 waves of 32×64 (cfg 6); 64-wide dx: the 8-wave 256×64 tiles
     const int sdef = a.Ng <= 64 ? 4 : (a.beta ? 6 : 0);
@@ -1246,7 +1351,7 @@ bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
   if (mode == 0 || a.C % 8 || a.K % 8) return false;
   // the ResNet stem (64 output channels × 168 row-packed columns, K = every output pixel): one
   // 64×256 tile column reads dy once, where the register-staged kernel's 64×128 tiles read it twice
-  // — measured slower on the row-packed stem at b1024 (1120 vs 1040 us, tools/stem_ab.py: the x
+  // — measured slower on the row-packed stem at b1024 (1120 vs 1040 us, dev/tools/stem_ab.py: the x
   // gather, not the dy re-read, bounds it), so opt-in (TDL_GLDS_STEM_WGRAD=1)
   const char* stem_env = getenv("TDL_GLDS_STEM_WGRAD");
   const bool stem = (stem_env ? atoi(stem_env) : 0) != 0 && a.M <= 64 && a.Ng > 128 &&

@@ -55,9 +55,13 @@ __device__ __forceinline__ void pc_rows(bf16x8 (&f)[N], uint32_t base) {
 // exactly as the BN apply pass rounds it; padding taps / rows past M stay 0) → ds_write_b128 to
 // the same swizzled LDS image.  Step j's loads are issued one step ahead (two register sets), so
 // they land under the consumers' MFMAs of step j−1; the consumers are unchanged.
+// DEPI: the DGRAD epilogue (mask / join / BN-backward statistics) on this forward K loop — a
+// stride-1 input gradient as the forward conv of dy with the flipped filter (conv_glds.hip
+// conv_dgrad_as_fwd); NJ: no join (the statistics form)
 template <int BM, int BN, int WM, int WN, int ST, int NP, bool STATS, bool BIAS, int FK,
-          bool AFF = false>
+          bool AFF = false, bool DEPI = false, bool NJ = false>
 __global__ void __launch_bounds__(64 * (WM * WN + NP), 1) conv_pc_kernel(ConvArgs a) {
+  static_assert(!DEPI || (!AFF && !BIAS), "dgrad epilogue: plain operands");
   static_assert(FK == 1 || FK == 2, "FASTK forward only");
   static_assert(!AFF || (FK == 1 && NP % 2 == 0), "folded BN: FASTK, even producer count");
   constexpr bool RAG = FK == 2;
@@ -384,7 +388,7 @@ __global__ void __launch_bounds__(64 * (WM * WN + NP), 1) conv_pc_kernel(ConvArg
     for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
       for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
-    store_tile_bf16<FWD, RM, RN, TM, TN, BIAS, STATS, false, false, false, false>(
+    store_tile_bf16<DEPI ? DGRAD : FWD, RM, RN, TM, TN, BIAS, STATS, false, false, NJ, false>(
         a, CT, acc, wm, wn, lane, rout, 1.f, false, s_sum, s_sq);
     if constexpr (STATS) {
 #pragma unroll
@@ -429,9 +433,9 @@ constexpr int PC_LDS_MAX = 160 * 1024;
 constexpr int pc_lds(int bm, int bn, int st) { return st * (bm + bn) * BK * 2 + 2 * bn * 4; }
 
 template <int BM, int BN, int WM, int WN, int ST, int NP, bool STATS, bool BIAS, int FK,
-          bool AFF = false>
+          bool AFF = false, bool DEPI = false, bool NJ = false>
 void launch_pc(const ConvArgs& a, int blocks, hipStream_t st) {
-  auto k = conv_pc_kernel<BM, BN, WM, WN, ST, NP, STATS, BIAS, FK, AFF>;
+  auto k = conv_pc_kernel<BM, BN, WM, WN, ST, NP, STATS, BIAS, FK, AFF, DEPI, NJ>;
   const int lds = pc_lds(BM, BN, ST) + (AFF ? 2 * a.C * 4 : 0);
   static int attr = 0;  // the largest size set so far
   if (lds > attr) {
@@ -447,9 +451,16 @@ void launch_pc(const ConvArgs& a, int blocks, hipStream_t st) {
 // the 256×128 forward of conv_fwd_glds (arguments prepared there: fast divisors, tiles per
 // workgroup, FWD tile order); fk 1 = C % 64 == 0, 2 = ragged 1×1
 // (mode 1: 2 producer waves, 2: 4)
-bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st) {
+bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st, bool depi) {
   if (a.res || a.dbg) return false;
   const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
+  if (depi) {
+    // input gradient as a forward conv: DGRAD epilogue; statistics only without a join
+    if (fk != 1 || bias || a.aff || (stats && a.beta)) return false;
+    if (stats) launch_pc<256, 128, 4, 2, 3, 4, true, false, 1, false, true, true>(a, blocks, st);
+    else launch_pc<256, 128, 4, 2, 3, 4, false, false, 1, false, true, false>(a, blocks, st);
+    return true;
+  }
   if (a.aff) {
     // folded BN + ReLU: 4 register-staging producers, FASTK, no bias, coefficient table in LDS
     if (fk != 1 || bias || pc_lds(256, 128, 3) + 2 * a.C * 4 > PC_LDS_MAX) return false;

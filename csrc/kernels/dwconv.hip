@@ -1029,7 +1029,7 @@ struct DwTileGeom {
 DwTileGeom dw_tile_geom(int Ho, int Wo, int st = 1) {
   // rows per tile: as many as the 64 KiB LDS bound below allows (TDL_DW_TR caps it; 8 was the
   // round-4 default — Xception b128 shapes 10–14 % faster with taller tiles: fewer halo re-reads
-  // per output, and the workgroups per CU are LDS-bound either way, tools/dw_micro.py)
+  // per output, and the workgroups per CU are LDS-bound either way, dev/tools/dw_micro.py)
   static const int tr_max = [] {
     const char* e = getenv("TDL_DW_TR");
     return e ? std::max(1, std::min(32, atoi(e))) : 32;
@@ -1194,7 +1194,7 @@ bool dw_tile() {
 // the tile kernel's DMA offsets are 32-bit bytes within one image
 bool dw_tile_fits(long h, long w, long c) { return h * w * c * 2 < (1L << 31) - 64; }
 // stride-2 3×3 on the tile kernels (forward, weight gradient); TDL_DW_S2_TILE=0: the row kernels
-// (read per call: tools/dw_micro.py A/Bs in-process)
+// (read per call: dev/tools/dw_micro.py A/Bs in-process)
 bool s2_tile_ok(const DwArgs& a) {
   const char* e = getenv("TDL_DW_S2_TILE");
   return (e == nullptr || atoi(e) != 0) && a.C % 8 == 0 && a.R == 3 && a.S == 3 && a.sh == 2 &&
@@ -1373,7 +1373,7 @@ bool dwconv_dgrad_launch(const DwArgs& a, hipStream_t st) {
 // sliding-window kernel): one slab per workgroup, ≈2048 workgroups
 namespace {
 bool dw_wgrad_tile_ok(const DwArgs& a) {
-  const char* e = getenv("TDL_DW_WG_TILE");  // (read per call: tools/dw_micro.py A/Bs in-process)
+  const char* e = getenv("TDL_DW_WG_TILE");  // (read per call: dev/tools/dw_micro.py A/Bs in-process)
   const bool on = e == nullptr || atoi(e) != 0;
   return on && ((slide_ok(a) && dw_tile() && dw_tile_fits(a.H, a.W, a.C) &&
                  dw_tile_fits(a.Ho, a.Wo, a.C)) ||

@@ -82,6 +82,11 @@ struct ConvArgs {
   // Launchers that cannot apply it must not run the problem (conv_aff_fwd_ok / the routing).
   const float* aff;
   int aff_ld;
+  // DGRAD (bf16, stride 1): optional flipped, transposed weights w_flip[c][r][s][k] =
+  // w[k][R−1−r][S−1−s][c] — the input gradient then runs as the forward conv of dy (the forward
+  // kernels' K loop with the DGRAD epilogue, conv_dgrad_as_fwd)
+  const bf16_t* w_flip;
+  uint32_t w_flip_bytes;
 };
 constexpr int MAX_DG_CLASSES = 16;
 
@@ -118,7 +123,16 @@ void bn_fold_weight_launch(const void* w, bool bf16, const float* coef, int K, i
                            void* wout, const float* bias_in, float* bias_out, hipStream_t st);
 void scale_cols_launch(float* dw, const float* a, long n, int C, hipStream_t st);
 int conv_pc();
-bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st);
+bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStream_t st,
+                        bool depi = false);
+// stride-1 input gradient as the forward conv of dy with the flipped filter w_flip [C][R][S][K]
+// (conv_glds.hip): true when it ran (*fused: the BN-backward statistics were written); false =
+// not eligible, nothing launched
+bool conv_dgrad_as_fwd(const ConvArgs& a, const bf16_t* w_flip, uint32_t w_flip_bytes,
+                       hipStream_t st, bool* fused);
+// w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c] (bf16)
+void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, int C,
+                             hipStream_t st);
 void conv_set_pc(int on);
 bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
 // halo-tiled direct conv (conv_halo.hip) for stride-1 R×S filters, Cin % 64 == 0: true when it

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build the extension at git revision REV into ab/_C_REV.so (for same-box A/B timing with
 # TDL_EXT_SO=ab/_C_REV.so), leaving the working tree's own build untouched.
-#   bash scripts/ab_build.sh REV
+#   bash dev/scripts/ab_build.sh REV
 set -e
 rev=$1
 root=$(cd "$(dirname "$0")/.." && pwd)

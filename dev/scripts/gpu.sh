@@ -1,7 +1,7 @@
 #!/bin/bash
 # gpurun with a retry when the box could not be prepared (status=transient / exit 3: nothing ran,
 # nothing charged).  A command that ran and failed is never retried.
-#   bash scripts/gpu.sh TIMEOUT 'command'
+#   bash dev/scripts/gpu.sh TIMEOUT 'command'
 to=$1; shift
 for attempt in 1 2 3; do
   rm -f gpurun_out/summary.txt

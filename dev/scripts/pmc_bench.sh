@@ -1,6 +1,6 @@
 # rocprofv3 hardware counters over a few ResNet-50 b256 training steps (one pass per counter group,
 # each within the per-block slot limits; --kernel-trace only alongside --pmc).
-#   bash scripts/pmc_bench.sh [model] [batch] [image]
+#   bash dev/scripts/pmc_bench.sh [model] [batch] [image]
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 M=${1:-resnet50}; B=${2:-256}; I=${3:-224}

@@ -1,4 +1,4 @@
-# depthwise kernel counters (tools/dw_micro.py), one pass per counter group
+# depthwise kernel counters (dev/tools/dw_micro.py), one pass per counter group
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 timeout -k 10 120 python3 $R/tools/dw_micro.py > $R/gpurun_out/dw_micro.log 2>&1 || exit $?

@@ -1,7 +1,7 @@
 """Microbenchmark of the BN kernels at the ResNet-50 (default) or ResNet-152 layer shapes:
 µs and TB/s per kernel and shape, plus the per-step total weighted by how often each shape occurs.
 
-  python tools/bn_micro.py [--model resnet50|resnet152] [--batch 256] [--iters 30]
+  python dev/tools/bn_micro.py [--model resnet50|resnet152] [--batch 256] [--iters 30]
 
 Per-step classes (ResNet bottleneck, training): "apply" = BN+ReLU (bn1/bn2/stem), "apply_res" =
 BN + residual + ReLU with the 1-bit mask (bn3), "apply_ds" = BN without ReLU (downsample branch);

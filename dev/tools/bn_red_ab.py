@@ -1,6 +1,6 @@
 """BN backward reduction at ResNet-50 b256 shapes: µs and TB/s per shape (A/B of the reduce
 variants via TDL_BN_RED_* env knobs, which are read once per process).
-  TDL_BN_RED_PART=1 TDL_BN_RED_NT=512 python tools/bn_red_ab.py"""
+  TDL_BN_RED_PART=1 TDL_BN_RED_NT=512 python dev/tools/bn_red_ab.py"""
 import os
 import sys
 

@@ -5,7 +5,7 @@
 stages; "reg" = the register-staged kernel.  For the low-tile-count convs of the reference DeepLab
 preset (13x13 feature maps at batch 64: 43 row tiles of 256).
 
-  python tools/cfg_ab.py [--op fwd|dgrad] [--shapes N,H,Cin,Cout,k,s,p[,d];...] [--cfgs 0,2,3,5,reg]"""
+  python dev/tools/cfg_ab.py [--op fwd|dgrad] [--shapes N,H,Cin,Cout,k,s,p[,d];...] [--cfgs 0,2,3,5,reg]"""
 import argparse
 import os
 import sys

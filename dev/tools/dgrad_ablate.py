@@ -3,7 +3,7 @@
 residual-join accumulate (dx += …), + the ReLU bit mask, and TDL_CONV_DBG ablations
 (2 = skip MFMA, 128 = epilogue without global loads / stores).
 
-  python tools/dgrad_ablate.py [--rounds 5]
+  python dev/tools/dgrad_ablate.py [--rounds 5]
 
 Needs a TDL_CONV_ABLATION=1 build of the extension (TDL_CONV_ABLATION=1 python build_ext.py
 --force): production builds compile the TDL_CONV_DBG flags out."""

@@ -6,7 +6,7 @@ For each ResNet-50 shape (batch N) times
   B  conv_dgrad_bnstat (the dgrad epilogue accumulates Σg, Σg·x)
 and checks that B's sums match A's reduce (after the Σg·x → Σg·x̂ conversion) and dx is equal.
 
-  python tools/dgrad_bnstat_ab.py [--n 256] [--iters 20] [--json gpurun_out/dgrad_bnstat.jsonl]
+  python dev/tools/dgrad_bnstat_ab.py [--n 256] [--iters 20] [--json gpurun_out/dgrad_bnstat.jsonl]
 """
 import argparse
 import json

@@ -1,6 +1,6 @@
 """fp8 dgrad vs bf16 dgrad on identical weights (lr = 0, so both models stay equal): per-layer
 cosine of the parameter gradients after the e5m2 scalers warmed up.
-  python tools/fp8_dgrad_check.py [--depth 18] [--train-bn]"""
+  python dev/tools/fp8_dgrad_check.py [--depth 18] [--train-bn]"""
 import argparse
 import sys
 

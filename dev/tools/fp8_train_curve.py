@@ -1,5 +1,5 @@
 """Loss curves of the same ResNet on a fixed batch: bf16, fp8 forward, fp8 forward + fp8 dgrad.
-  python tools/fp8_train_curve.py [--depth 50] [--batch 64] [--size 128] [--steps 12] [--lr 0.01]"""
+  python dev/tools/fp8_train_curve.py [--depth 50] [--batch 64] [--size 128] [--steps 12] [--lr 0.01]"""
 import argparse
 import sys
 

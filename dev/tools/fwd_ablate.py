@@ -4,7 +4,7 @@ shape under TDL_CONV_DBG ablations: 1 = operand loads out of range (the DMA stil
 memory traffic), 2 = no MFMA, 16 = no LDS fragment reads, 32 = no barrier, 64 = no DMA at all,
 128 = epilogue without global memory.  Timing-only: the results are wrong.
 
-  python tools/fwd_ablate.py [--op fwd|dgrad] [--shapes N,H,Cin,Cout,k,s,p;...] [--dbg 0,1,2,...]
+  python dev/tools/fwd_ablate.py [--op fwd|dgrad] [--shapes N,H,Cin,Cout,k,s,p;...] [--dbg 0,1,2,...]
 
 Needs a TDL_CONV_ABLATION=1 build of the extension (TDL_CONV_ABLATION=1 python build_ext.py
 --force): production builds compile the TDL_CONV_DBG flags out."""

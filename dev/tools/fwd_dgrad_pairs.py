@@ -1,6 +1,6 @@
 """Per-layer forward vs dgrad conv kernel time from a rocprofv3 kernel trace of bench.py
 (ResNet bottleneck order: forward [downsample] conv1 conv2 conv3 …, backward in reverse).
-  python tools/fwd_dgrad_pairs.py gpurun_out/prof_X/run_kernel_trace.csv"""
+  python dev/tools/fwd_dgrad_pairs.py gpurun_out/prof_X/run_kernel_trace.csv"""
 import csv
 import re
 import sys

@@ -3,7 +3,7 @@
 fp32 oracle path for one training step.  Localises a wrong backward kernel: a bug shows up as one
 layer with low cosine, bf16 noise as a smooth degradation towards the input.
 
-  python tools/grad_compare.py --model resnet18 --size 64 --batch 16
+  python dev/tools/grad_compare.py --model resnet18 --size 64 --batch 16
 """
 import argparse
 import os

@@ -3,7 +3,7 @@
 ``Trainer.train_step`` (no device sync) vs the wall time per step, plus a cProfile of a few steps.
 If the issue time approaches the wall time the step is launch-bound (HIP graphs remove it).
 
-  python tools/host_overhead.py [--model deeplab_ref|resnet50|xception41] [--batch B] [--profile]"""
+  python dev/tools/host_overhead.py [--model deeplab_ref|resnet50|xception41] [--batch B] [--profile]"""
 import argparse
 import cProfile
 import io

@@ -5,7 +5,7 @@ input gradient with transposed weights (conv_dgrad(w_t=...)).  Same process, int
 graph-timed (min over rounds); outputs are compared (bf16 rounding of different fp32 summation
 orders only).
 
-  python tools/m32_ab.py [--batch 1024] [--rounds 3]"""
+  python dev/tools/m32_ab.py [--batch 1024] [--rounds 3]"""
 import argparse
 import os
 import sys

@@ -2,7 +2,7 @@
 // 512-thread workgroups (8 waves, 4×2), a 256×128×64 KC-swizzled bf16 tile pair in LDS, each wave
 // a 64×64 sub-tile (4×4 v_mfma_f32_16x16x32_bf16 per 32-deep slice).  Variants differ only in
 // the read / wait / MFMA schedule.  Build + run (on the GPU box):
-//   hipcc --offload-arch=gfx950 -O3 -o /tmp/mm tools/mfma_lds_micro.hip && /tmp/mm
+//   hipcc --offload-arch=gfx950 -O3 -o /tmp/mm dev/tools/mfma_lds_micro.hip && /tmp/mm
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -1,7 +1,7 @@
 """A/B of conv kernel configurations for the 64-output-channel ResNet-50 layer1 convs (fwd and
 dgrad): register-staged (reg) vs LDS-DMA configs (TDL_GLDS_CFG_*: 1 = 256x64/4 waves,
 4 = 256x64/8 waves, 5 = 128x64/4 waves/4 stages).  Interleaved rounds, min over rounds.
-  python tools/n64_configs.py [--batch 256]"""
+  python dev/tools/n64_configs.py [--batch 256]"""
 import argparse
 import os
 import sys

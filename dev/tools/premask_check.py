@@ -1,7 +1,7 @@
 """Pre-masked residual joins (ops/gradjoin.py) vs the BN applying its ReLU mask: gradient
 agreement per parameter, against the run-to-run noise floor of the baseline path itself.
 
-  python tools/premask_check.py [--depth 18] [--batch 8] [--size 64] [--eval-bn]"""
+  python dev/tools/premask_check.py [--depth 18] [--batch 8] [--size 64] [--eval-bn]"""
 import argparse
 import sys
 

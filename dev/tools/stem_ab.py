@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Row-packed 7x7 stem (7x1 conv over [N, 224, 112, 24], 24 -> 64, stride (2, 1)) under the conv
 kernel selections: register-staged (mode 0), default (1), LDS-DMA forced (2) with tile configs.
-python tools/stem_ab.py --batch 1024"""
+python dev/tools/stem_ab.py --batch 1024"""
 import argparse
 import os
 import sys

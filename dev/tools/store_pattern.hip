@@ -4,7 +4,7 @@
 // (a wave instruction covers 4 rows × 256 B), (c) fragment layout with 16 B per lane (8 columns:
 // 16 rows × 64 B per instruction).  Tiles of 256 × 128 (8 waves, 64 × 64 per wave), as the
 // LDS-DMA conv kernel.
-//   hipcc --offload-arch=gfx950 -O3 -o /tmp/store_pattern tools/store_pattern.hip && /tmp/store_pattern
+//   hipcc --offload-arch=gfx950 -O3 -o /tmp/store_pattern dev/tools/store_pattern.hip && /tmp/store_pattern
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-stream kernel time of the last N training steps of a rocprofv3 kernel trace: which kernels
 sit on the compute stream (the critical path) and which on the side (weight-gradient) stream.
-python tools/stream_split.py gpurun_out/prof_x/run_kernel_trace.csv --steps 5"""
+python dev/tools/stream_split.py gpurun_out/prof_x/run_kernel_trace.csv --steps 5"""
 import argparse
 import collections
 import csv

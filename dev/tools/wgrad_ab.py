@@ -3,7 +3,7 @@
 selection, the LDS-DMA kernel forced on (conv_set_glds_mode(2)) with its configurations, and the
 register-staged kernel (mode 0).  Reports µs per call and TFLOP/s.
 
-  python tools/wgrad_ab.py [--rounds 5] [--batch 256]"""
+  python dev/tools/wgrad_ab.py [--rounds 5] [--batch 256]"""
 import argparse
 import os
 import sys

@@ -2,7 +2,7 @@
 """Dgrad with the weights as [K,R,S,C] (transposed LDS reads of the B operand) vs a [R,S,C,K]
 copy (K-contiguous rows, ds_read_b128): graph-timed A/B in one process, bitwise result check.
 
-  python tools/wt_ab.py [--shapes N,H,Cin,Cout,k,s,p;...]"""
+  python dev/tools/wt_ab.py [--shapes N,H,Cin,Cout,k,s,p;...]"""
 import argparse
 import os
 import sys

@@ -154,6 +154,26 @@ class Conv2d(nn.Module):
             self._padded_version = v
         return self._padded
 
+    def flip_weight(self, w):
+        """[C, R, S, K] flipped transpose of the compute weight ``w`` (w_flip[c][r][s][k] =
+        w[k][R−1−r][S−1−s][c]): the stride-1 input gradient then runs as the forward conv of dy
+        (ops/conv.py, conv_glds.hip conv_dgrad_as_fwd).  One HIP launch per parameter version into
+        a persistent buffer (fixed address: HIP-graph replays refresh it in place)."""
+        v = _params.version()
+        c = self.__dict__.get("_flip")
+        shape = (w.shape[3], w.shape[1], w.shape[2], w.shape[0])
+        if c is not None and c[0] == v and c[1].device == w.device and tuple(c[1].shape) == shape:
+            return c[1]
+        if c is not None and c[1].device == w.device and tuple(c[1].shape) == shape \
+                and c[1].dtype == w.dtype:
+            wf = c[1]
+        else:
+            wf = torch.empty(shape, dtype=w.dtype, device=w.device)
+        from ..ops.common import ext
+        ext().conv_flip_weight(w.contiguous(), wf)
+        self.__dict__["_flip"] = (v, wf)
+        return wf
+
     def compute_bias(self):
         """fp32 bias as the kernels read it, ``_cout_store`` long with zero padding channels (the
         flat master buffer's slack when flat-backed, else a padded copy)."""

@@ -16,6 +16,7 @@ Padding is explicit (top, bottom, left, right) so TF ``SAME`` (asymmetric at str
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -160,18 +161,20 @@ def conv_fwd_fp8(x8, sx, w8, sw, geom: ConvGeom, relu=False, stats=None):
 
 
 def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumulate=False,
-               mask=None, w_t=None):
+               mask=None, w_t=None, w_flip=None):
     """dx.  With ``out`` the result is written there (``accumulate``: dx += …, fused in the GEMM
     epilogue — used by the residual-gradient join, ops/gradjoin.py).  ``mask`` (uint8, 1 bit per
     element of dx, GPU): dx = ([dx +] dgrad)·[bit] for the elements this dgrad writes.  ``w_t``
     (GPU, optional): the same weights transposed to [R,S,C,K]; the LDS-DMA kernel then reads both
-    operands as K-contiguous rows (same result)."""
+    operands as K-contiguous rows (same result).  ``w_flip`` (GPU, stride 1, optional): the
+    flipped transpose [C,R,S,K] (models.layers.Conv2d.flip_weight) — dx is then computed as the
+    forward conv of dy on the forward kernels (:func:`dgrad_as_fwd_ok`)."""
     if on_gpu(dy):
         dx = out if out is not None else torch.empty(x_shape, device=dy.device,
                                                      dtype=out_dtype or dy.dtype)
         ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
                          geom.padding[2], geom.dilation[0], geom.dilation[1],
-                         bool(accumulate and out is not None), mask, w_t)
+                         bool(accumulate and out is not None), mask, w_t, w_flip=w_flip)
         return dx
     r = ref_conv_dgrad(dy, w, x_shape, geom)
     if mask is not None:
@@ -190,7 +193,7 @@ def conv_dgrad(dy, w, x_shape, geom: ConvGeom, out_dtype=None, out=None, accumul
 
 
 def conv_dgrad_bnstat(dy, w, x_shape, geom: ConvGeom, bn_x, out=None, accumulate=False,
-                      mask=None):
+                      mask=None, w_flip=None):
     """:func:`conv_dgrad` that also returns the BN-backward sums of the stored dx: fp32 [2, C] =
     (Σg, Σg·x) with g = dx (as stored, after the join accumulate / ReLU mask) and x = ``bn_x``,
     the input of the BN whose output this conv consumed — the BN backward then skips its reduce
@@ -202,7 +205,8 @@ def conv_dgrad_bnstat(dy, w, x_shape, geom: ConvGeom, bn_x, out=None, accumulate
         red = workspace.zeros((2, x_shape[-1]), dy.device)
         fused = ext().conv_dgrad(dy, w, dx, geom.stride[0], geom.stride[1], geom.padding[0],
                                  geom.padding[2], geom.dilation[0], geom.dilation[1],
-                                 bool(accumulate and out is not None), mask, None, bn_x, red)
+                                 bool(accumulate and out is not None), mask, None, bn_x, red,
+                                 w_flip=w_flip)
         return dx, (red if fused else None)
     dx = conv_dgrad(dy, w, x_shape, geom, out=out, accumulate=accumulate, mask=mask)
     if accumulate and out is not None and geom.stride != (1, 1):
@@ -211,6 +215,17 @@ def conv_dgrad_bnstat(dy, w, x_shape, geom: ConvGeom, bn_x, out=None, accumulate
     g = dx.float().reshape(-1, C)
     red = torch.stack([g.sum(0), (g * bn_x.float().reshape(-1, C)).sum(0)])
     return dx, red
+
+
+DGRAD_AS_FWD = os.environ.get("TDL_DGRAD_AS_FWD", "1") == "1"
+
+
+def dgrad_as_fwd_ok(dy, x_shape, geom: ConvGeom) -> bool:
+    """Can this input gradient run as the forward conv of dy with the flipped filter?  bf16 on the
+    GPU, stride 1, dy channels % 64 (the forward kernels' FASTK), dx channels % 8, dx and dy of
+    the same spatial size (the kernel still declines problems its forward route would not take)."""
+    return (DGRAD_AS_FWD and fused_gpu(dy) and geom.stride == (1, 1) and dy.shape[-1] % 64 == 0
+            and x_shape[-1] % 8 == 0 and tuple(dy.shape[1:3]) == tuple(x_shape[1:3]))
 
 
 def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
@@ -409,6 +424,7 @@ class _Conv2dFn(torch.autograd.Function):
             w = ctx.layer.compute_weight(dy.dtype) if ctx.layer is not None else \
                 compute_weight(weight, dy.dtype)
             fp8_dg = fp8_dgrad_eligible(ctx.layer, dy, geom, tuple(w.shape))
+            wf = None
             if fp8_dg:
                 # fp8 dgrad: e5m2 dy (the BN backward's side output) × e4m3 W^T
                 dy8, sdy = dy._tdl_fp8
@@ -418,9 +434,13 @@ class _Conv2dFn(torch.autograd.Function):
                     return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
                                           accumulate=accumulate, mask=mask)
             else:
+                # stride 1: the flipped filter lets the forward kernels compute dx
+                wf = (ctx.layer.flip_weight(w) if ctx.layer is not None and
+                      dgrad_as_fwd_ok(dy, ctx.x_shape, geom) else None)
+
                 def dgrad(out=None, accumulate=False, mask=None):
                     return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,
-                                      mask=mask)
+                                      mask=mask, w_flip=wf)
             join = ctx.join
             masks_ok = fused_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
             stats_ok = masks_ok and not fp8_dg  # (the kernel decides; strided: parity classes)
@@ -435,7 +455,7 @@ class _Conv2dFn(torch.autograd.Function):
                     if (stats_ok or tok.mask is None) and not fp8_dg and tok.x is not None \
                             and gradjoin.STATS_SINGLE:
                         dx, red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, tok.x,
-                                                    mask=tok.mask)
+                                                    mask=tok.mask, w_flip=wf)
                     else:
                         dx, red = dgrad(mask=tok.mask), None
                     tok.mark(dx, red)
@@ -453,7 +473,8 @@ class _Conv2dFn(torch.autograd.Function):
                     # the final contribution writes every pixel through the mask: its epilogue
                     # sees the finished gradient and can fuse the BN statistics
                     _, join.red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, join.stats_x,
-                                                    out=join.buf, accumulate=True, mask=mask)
+                                                    out=join.buf, accumulate=True, mask=mask,
+                                                    w_flip=wf)
                     join.note(True)
                 else:
                     dgrad(out=join.buf, accumulate=True, mask=mask)

@@ -35,7 +35,7 @@ KEEP_ALIVE = os.environ.get("TDL_SIDE_KEEPALIVE", "1") == "1"
 def current(device):
     """``torch.cuda.current_stream(device)`` without its Python-level device normalisation (this
     runs several times per conv backward; the public helper cost ≈5 µs per call, ≈1.4 ms of host
-    time per step of the reference DeepLab preset — tools/host_overhead.py)."""
+    time per step of the reference DeepLab preset — dev/tools/host_overhead.py)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     sid, di, dt = torch._C._cuda_getCurrentStream(idx)
     return torch.cuda.Stream(stream_id=sid, device_index=di, device_type=dt)

@@ -1155,3 +1155,69 @@ def test_softmax_eval_head(gpu, dtype):
     assert rel_err(p, torch.softmax(lf, -1)) < 1e-5
     _, _, p2 = L.softmax_eval(logits.to(gpu), probs=True)
     assert torch.equal(p2, p)
+
+
+# (N, H, W, Cin, K, k, dilation): stride-1 dgrads the forward kernels take (K % 64 == 0)
+AS_FWD_SHAPES = [
+    (4, 14, 14, 64, 64, 3, 1),      # 256x64 8-wave tiles
+    (4, 14, 14, 128, 128, 3, 1),
+    (4, 14, 14, 256, 256, 3, 1),    # producer/consumer kernel (C_in of the forward = K >= 256)
+    (4, 14, 14, 256, 64, 1, 1),
+    (4, 14, 14, 64, 256, 1, 1),
+    (3, 9, 9, 128, 128, 3, 1),      # ragged last row tile
+    (2, 13, 13, 64, 128, 3, 2),     # dilated
+]
+
+
+@pytest.mark.parametrize("shape", AS_FWD_SHAPES)
+@pytest.mark.parametrize("epi", ["plain", "mask", "join", "bnstat"])
+def test_conv_dgrad_as_forward(gpu, shape, epi):
+    """A stride-1 input gradient computed as the forward conv of dy with the flipped filter
+    (conv_glds.hip conv_dgrad_as_fwd, models.layers.Conv2d.flip_weight) against the DGRAD kernel
+    and the fp32 oracle, for every DGRAD epilogue it carries: plain, ReLU bit mask, residual join
+    (dx += …, masked) and the fused BN-backward statistics (Σg, Σg·x)."""
+    N, H, W, Cin, K, k, d = shape
+    p = d * (k - 1) // 2
+    g = C.ConvGeom((1, 1), (p, p, p, p), (d, d))
+    torch.manual_seed(41)
+    w = (torch.randn(K, k, k, Cin) / math.sqrt(k * k * Cin)).bfloat16().to(gpu)
+    wf = torch.empty(Cin, k, k, K, device=gpu, dtype=torch.bfloat16)
+    ext().conv_flip_weight(w, wf)
+    assert torch.equal(wf, w.flip(1, 2).permute(3, 1, 2, 0))
+    dy = torch.randn(N, H, W, K).bfloat16().to(gpu)
+    x = (torch.randn(N, H, W, Cin) * 1.3 + 0.4).bfloat16().to(gpu)
+    mask = None
+    if epi != "plain":
+        gam, bet = torch.rand(Cin, device=gpu) + 0.5, torch.randn(Cin, device=gpu) * 0.3
+        coef = B.bn_finalize(B.bn_stats(x), N * H * W, gam, bet, torch.zeros(Cin, device=gpu),
+                             torch.ones(Cin, device=gpu), 0.9, 1e-3, True)
+        mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+        B.bn_apply(x, coef, None, True, mask=mask)
+    prev = torch.randn(N, H, W, Cin).bfloat16().to(gpu) if epi == "join" else None
+    ext().conv_set_glds_mode(2)
+    try:
+        if epi == "bnstat":
+            ref, red0 = C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask)
+            got, red1 = C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask, w_flip=wf)
+        else:
+            ref = C.conv_dgrad(dy, w, x.shape, g, mask=mask,
+                               out=prev.clone() if prev is not None else None,
+                               accumulate=prev is not None)
+            got = C.conv_dgrad(dy, w, x.shape, g, mask=mask, w_flip=wf,
+                               out=prev.clone() if prev is not None else None,
+                               accumulate=prev is not None)
+    finally:
+        ext().conv_set_glds_mode(-1)
+    torch.cuda.synchronize()
+    oracle = C.ref_conv_dgrad(dy.float().cpu(), w.float().cpu(), x.shape, g)
+    if prev is not None:
+        oracle = oracle + prev.float().cpu()
+    if mask is not None:
+        oracle = oracle * B.unpack_relu_mask(mask.cpu(), Cin).reshape(oracle.shape)
+    assert rel_err(got, oracle) < 1e-2
+    assert rel_err(got, ref) < 1e-2
+    if epi == "bnstat":
+        assert red0 is not None and red1 is not None
+        gf, xf = got.float().reshape(-1, Cin), x.float().reshape(-1, Cin)
+        want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
+        assert rel_err(red1, want) < 1e-4

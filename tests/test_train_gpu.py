@@ -55,7 +55,7 @@ def _paired(model_fn, gpu, x, y, lossf, train_mode):
 def test_gpu_step_matches_cpu_reference(gpu):
     """One step of ResNet-18: GPU (bf16 HIP kernels) vs CPU fp32 oracle.  BN uses moving stats
     so the backward has no batch-statistics cancellation (with tiny batches that cancellation
-    turns bf16 rounding into O(1) gradient noise on *both* paths — tools/grad_compare.py
+    turns bf16 rounding into O(1) gradient noise on *both* paths — dev/tools/grad_compare.py
     --cpu-bf16 shows the same cosine for a bf16 CPU run)."""
     torch.manual_seed(1)
     x, y = imagenet_batch(8, 32, num_classes=10, dtype=torch.float32)
@@ -276,7 +276,7 @@ def test_resnet_fp8_dgrad_trains(gpu, depth, monkeypatch):
     net = models.build(f"resnet{depth}", num_classes=10)
     models.enable_fp8(net, dgrad=True)
     # ResNet-50 from random init on one 64-px batch diverges in bf16 too at lr 0.01
-    # (tools/fp8_train_curve.py): a smaller step for it
+    # (dev/tools/fp8_train_curve.py): a smaller step for it
     tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01 if depth == 18 else 0.001,
                                                             momentum=0.9, weight_decay=0.0))
     x, y = imagenet_batch(32, 64, num_classes=10, device=gpu)
@@ -540,7 +540,7 @@ def test_side_stream_wgrad_matches_serial(gpu, model):
     atomics, ~1e-12 here).  No host synchronisation between the steps and the read-back, and the
     side stream is stalled before every step, so an optimizer that read a half-written (stale or
     zero) gradient would move the trajectory by orders of magnitude more
-    (tools/race_negative_control.py)."""
+    (dev/tools/race_negative_control.py)."""
     from tensorflowdistributedlearning_amd.ops import streams
     torch.manual_seed(9)
     nets = [models.build(model, num_classes=10) for _ in range(2)]
@@ -570,7 +570,7 @@ def test_side_stream_wgrad_matches_serial(gpu, model):
     assert not torch.equal(masters[0], start)  # the steps really updated the parameters
     # the two trajectories differ only by the BN backward's fp32 atomic summation order, which
     # this unnormalised frozen-BN net amplifies over the steps; a missing join reads stale or
-    # zero gradients and moves the update by O(1) (tools/race_negative_control.py)
+    # zero gradients and moves the update by O(1) (dev/tools/race_negative_control.py)
     u0, u1 = masters[0] - start, masters[1] - start
     assert ((u1 - u0).norm() / u0.norm()).item() < 1e-2
 
@@ -603,7 +603,7 @@ def test_plain_backward_joins_side_stream(gpu):
     finally:
         streams.set_enabled(old)
     # equal up to the BN backward's fp32 atomic summation order; a read before the stalled side
-    # stream finished would see stale gradients (tools/race_negative_control.py)
+    # stream finished would see stale gradients (dev/tools/race_negative_control.py)
     assert ((outs[1] - outs[0]).norm() / outs[0].norm()).item() < 1e-3
 
 

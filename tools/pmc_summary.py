@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel hardware-counter summary of one training step from rocprofv3 ``--pmc`` passes
-(scripts/pmc_bench.sh): MFMA utilisation, LDS bank-conflict share, HBM bytes and bandwidth.
+(dev/scripts/pmc_bench.sh): MFMA utilisation, LDS bank-conflict share, HBM bytes and bandwidth.
 
   python tools/pmc_summary.py gpurun_out/pmc_resnet50_{sq,fetch,write}
 
