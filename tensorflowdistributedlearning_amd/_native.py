@@ -37,7 +37,7 @@ def load():
     if _EXT_ERR is not None:
         raise _EXT_ERR
     # TDL_EXT_SO: load another build of the same extension (same-box A/B of kernel changes,
-    # tools/ab_build.sh); the module name stays tensorflowdistributedlearning_amd._C
+    # dev/scripts/ab_build.sh); the module name stays tensorflowdistributedlearning_amd._C
     so = os.environ.get("TDL_EXT_SO") or _find_so("_C")
     if so is None:
         _EXT_ERR = ImportError(
