@@ -1179,6 +1179,8 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
   if (!stats) a.stats = nullptr;
   if (stats && a.beta) return false;  // statistics + join: the DGRAD kernel's 8-wave tiles
+  // ≤ 64-wide dx, 3×3: the halo forward loader (as the forward routes those convs)
+  if (conv_fwd_halo_depi(a, st, fused)) return true;
   const int cfg = a.Ng <= 64 ? 4 : 0;
   const GCfg& g = cfg_of(cfg);
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);

@@ -129,8 +129,12 @@ __device__ __forceinline__ HTile htile(const HaloGeom& g, int rb) {
   return t;
 }
 
-template <int MODE, int BN, int WM, int WN, int RM, int ST, int HL, bool BIAS, bool STATS, bool NJ>
+// DEPI (FWD loader): the DGRAD epilogue — a stride-1 input gradient as the forward conv of dy
+// with the flipped filter (conv_glds.hip conv_dgrad_as_fwd)
+template <int MODE, int BN, int WM, int WN, int RM, int ST, int HL, bool BIAS, bool STATS, bool NJ,
+          bool DEPI = false>
 __global__ void __launch_bounds__(512, 1) conv_halo_kernel(ConvArgs a, HaloGeom g) {
+  static_assert(!DEPI || (MODE == FWD && !BIAS), "dgrad epilogue on the forward loader");
   constexpr int NW = 8;
   static_assert(WM * WN == NW, "8 waves");
   constexpr int TN = BN / WN, RN = TN / 16, TM = RM * 16;
@@ -345,7 +349,8 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(ConvArgs a, HaloGeom 
       const int w = q - r * g.Wo;
       rows_in[rm] = r < t.rows ? (uint32_t)(((t.rho0 + r) * g.Wo + w) * a.ldc) * 2u : ROW_OOB;
     }
-    store_tile_bf16<MODE, RM, RN, TM, TN, BIAS, STATS, false, false, NJ, false, true>(
+    store_tile_bf16<DEPI ? DGRAD : MODE, RM, RN, TM, TN, BIAS, STATS, false, false, NJ, false,
+                    true>(
         a, Tep, acc, wm, wn, lane, rout, 1.f, false, s_sum, s_sq, rows_in);
   };
 
@@ -647,9 +652,9 @@ int henv(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-template <int MODE, int BN, int ST, int HL, bool BIAS, bool STATS, bool NJ>
+template <int MODE, int BN, int ST, int HL, bool BIAS, bool STATS, bool NJ, bool DEPI = false>
 void launch_h(const ConvArgs& a, const HaloGeom& g, int blocks, hipStream_t st) {
-  auto k = conv_halo_kernel<MODE, BN, 4, 2, 4, ST, HL, BIAS, STATS, NJ>;
+  auto k = conv_halo_kernel<MODE, BN, 4, 2, 4, ST, HL, BIAS, STATS, NJ, DEPI>;
   constexpr int lds = halo_lds(BN, ST, HL);
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr = false;
@@ -694,14 +699,14 @@ bool plan_halo(HaloGeom& g, int bn, HCfg& cfg) {
   return true;
 }
 
-template <int MODE, bool BIAS, bool STATS, bool NJ>
+template <int MODE, bool BIAS, bool STATS, bool NJ, bool DEPI = false>
 void launch_hcfg(const ConvArgs& a, const HaloGeom& g, const HCfg& c, int blocks, hipStream_t st) {
   if (c.bn == 128) {
-    launch_h<MODE, 128, 3, 6, BIAS, STATS, NJ>(a, g, blocks, st);
+    launch_h<MODE, 128, 3, 6, BIAS, STATS, NJ, DEPI>(a, g, blocks, st);
   } else if (c.hl == 8) {
-    launch_h<MODE, 64, 3, 8, BIAS, STATS, NJ>(a, g, blocks, st);
+    launch_h<MODE, 64, 3, 8, BIAS, STATS, NJ, DEPI>(a, g, blocks, st);
   } else {
-    launch_h<MODE, 64, 4, 6, BIAS, STATS, NJ>(a, g, blocks, st);
+    launch_h<MODE, 64, 4, 6, BIAS, STATS, NJ, DEPI>(a, g, blocks, st);
   }
 }
 
@@ -881,6 +886,45 @@ bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
     if (stats) launch_hcfg<FWD, false, true, true>(a, g, c, blocks, st);
     else launch_hcfg<FWD, false, false, true>(a, g, c, blocks, st);
   }
+  return true;
+}
+
+// A stride-1 input gradient prepared as a forward conv (conv_dgrad_as_fwd: x = dy, w = the
+// flipped filter, C / K swapped) on the halo forward loader with the DGRAD epilogue — where the
+// halo forward wins (≤ 64 output channels, 3×3: ResNet layer1, 698 → 503 µs at b1024,
+// bench/dgrad_paths.py).  *fused: the BN-backward statistics were written.
+bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused) {
+  if (fused) *fused = false;
+  if (!conv_halo_mode() || a.aff || a.fp8 || a.sh != 1 || a.sw != 1) return false;
+  const int ntap = a.R * a.S;
+  if (ntap < 3 || ntap > HALO_MAXTAP || a.C % 64 || a.K % 8 || a.ldc % 8) return false;
+  if (a.mask && a.ldc % 64) return false;
+  if (a.x_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
+  if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
+  if (conv_halo_mode() == 1 && a.K > 64) return false;
+  const bool stats = a.stats != nullptr && a.bn_x != nullptr;
+  if (stats && a.beta) return false;
+  HaloGeom g{};
+  g.N = a.N; g.Hi = a.H; g.Wi = a.W; g.Ci = a.C;
+  g.Ho = a.Ho; g.Wo = a.Wo; g.Co = a.K;
+  g.ldb = ntap * a.C;
+  int oy[HALO_MAXTAP], ox[HALO_MAXTAP];
+  for (int r = 0; r < a.R; ++r)
+    for (int s = 0; s < a.S; ++s) {
+      const int t = r * a.S + s;
+      oy[t] = r * a.dh - a.ph;
+      ox[t] = s * a.dw - a.pw;
+      g.tap_b[t] = t * a.C;
+    }
+  HCfg c;
+  int blocks;
+  const int bn = henv("TDL_HALO_BN", a.K >= 128 ? 128 : 64);
+  if (!halo_common(a, g, a.R, a.S, oy, ox, bn, c, blocks)) return false;
+  ConvArgs b = a;
+  if (!stats) b.stats = nullptr;
+  if (stats) launch_hcfg<FWD, false, true, true, true>(b, g, c, blocks, st);
+  else launch_hcfg<FWD, false, false, false, true>(b, g, c, blocks, st);
+  if (fused) *fused = stats;
   return true;
 }
 
