@@ -1190,8 +1190,10 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   const int blocks = (int)(groups * ntn);
   a.cls_tile0[0] = 0;
   a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
-  // the producer/consumer kernel where the forward routes its 3×3 convs
-  if (cfg == 0 && a.R * a.S > 1 && a.C >= 256 && conv_fwd_pc_launch(a, blocks, 1, 2, st, true)) {
+  // the producer/consumer kernel where the forward routes its 3×3 convs (not with the
+  // statistics epilogue: its x registers spill at the 12-wave register budget)
+  if (cfg == 0 && !stats && a.R * a.S > 1 && a.C >= 256 &&
+      conv_fwd_pc_launch(a, blocks, 1, 2, st, true)) {
     if (fused) *fused = stats;
     return true;
   }

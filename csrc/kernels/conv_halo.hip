@@ -903,7 +903,9 @@ bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused) {
   if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
   if (conv_halo_mode() == 1 && a.K > 64) return false;
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
-  if (stats && a.beta) return false;
+  // the statistics form lost to the DGRAD kernel's 256×64 tiles (ResNet layer1 3×3, b1024: 700
+  // vs 607 µs — profiles/r05_dgrad_as_fwd.txt): plain / join only
+  if (stats) return false;
   HaloGeom g{};
   g.N = a.N; g.Hi = a.H; g.Wi = a.W; g.Ci = a.C;
   g.Ho = a.Ho; g.Wo = a.Wo; g.Co = a.K;
@@ -921,10 +923,8 @@ bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused) {
   const int bn = henv("TDL_HALO_BN", a.K >= 128 ? 128 : 64);
   if (!halo_common(a, g, a.R, a.S, oy, ox, bn, c, blocks)) return false;
   ConvArgs b = a;
-  if (!stats) b.stats = nullptr;
-  if (stats) launch_hcfg<FWD, false, true, true, true>(b, g, c, blocks, st);
-  else launch_hcfg<FWD, false, false, false, true>(b, g, c, blocks, st);
-  if (fused) *fused = stats;
+  b.stats = nullptr;
+  launch_hcfg<FWD, false, false, false, true>(b, g, c, blocks, st);
   return true;
 }
 

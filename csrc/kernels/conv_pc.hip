@@ -456,9 +456,10 @@ bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStre
   const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
   if (depi) {
     // input gradient as a forward conv: DGRAD epilogue; statistics only without a join
-    if (fk != 1 || bias || a.aff || (stats && a.beta)) return false;
-    if (stats) launch_pc<256, 128, 4, 2, 3, 4, true, false, 1, false, true, true>(a, blocks, st);
-    else launch_pc<256, 128, 4, 2, 3, 4, false, false, 1, false, true, false>(a, blocks, st);
+    // (no statistics form: its BN-input registers spill at the 12-wave register budget — the
+    // LDS-DMA kernel takes those)
+    if (fk != 1 || bias || a.aff || stats) return false;
+    launch_pc<256, 128, 4, 2, 3, 4, false, false, 1, false, true, false>(a, blocks, st);
     return true;
   }
   if (a.aff) {
