@@ -109,7 +109,7 @@ def bench_config(args):
     over = {"arch": args.model, "batch": args.batch, "image_size": args.image_size,
             "steps": args.steps, "warmup": args.warmup, "lr": args.lr,
             "bucket_mb": args.bucket_mb, "first_bucket_mb": args.first_bucket_mb,
-            "optimizer": args.optimizer, "dtype": args.dtype, "grad_dtype": args.grad_dtype}
+            "optimizer": args.optimizer, "dtype": args.dtype, "grad_dtype": getattr(args, "grad_dtype", None)}
     for k, v in over.items():
         if v is not None:
             setattr(cfg, k, v)

@@ -7,6 +7,7 @@
 #include <c10/hip/HIPCachingAllocator.h>
 
 #include "kernels/kernels.h"
+#include "kernels/conv_route.h"
 #include "runtime/loader.h"
 #include "runtime/comm.h"
 
@@ -1518,6 +1519,64 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias_in"), py::arg("bias_out"));
   m.def("scale_cols", &scale_cols, py::arg("dw"), py::arg("a"));
   m.def("conv_set_pc", &conv_set_pc, "wave-specialised producer/consumer forward (-1: env)");
+  // ---- the conv route table (kernels/conv_route.h)
+  m.def("conv_route_table", []() {
+    py::list out;
+    static const char* impls[] = {"gemm", "glds", "pc", "halo", "asfwd"};
+    static const char* ops[] = {"fwd", "dgrad", "wgrad"};
+    for (int i = 0; i < route_count(); ++i) {
+      const RouteRule& r = route_rule(i);
+      py::dict d;
+      d["name"] = r.name; d["op"] = ops[r.op]; d["impl"] = impls[r.impl];
+      d["taps"] = py::make_tuple(r.taps_min, r.taps_max); d["stride1"] = (bool)r.stride1;
+      d["cin"] = py::make_tuple(r.cin_min, r.cin_max); d["cout"] = py::make_tuple(r.cout_min, r.cout_max);
+      d["rows_min"] = r.rows_min; d["tile"] = py::make_tuple(r.tile_m, r.tile_n);
+      d["tiles_min"] = r.tiles_min; d["need"] = r.need; d["forbid"] = r.forbid;
+      d["cfg"] = route_cfg(i); d["default_cfg"] = r.cfg; d["on"] = route_on(i);
+      d["default_on"] = r.on; d["test"] = r.test; d["evidence"] = r.evidence;
+      d["instantiated"] = route_cfg_instantiated(r.impl, r.op, route_cfg(i), r.need);
+      d["mode"] = route_family_mode(r);
+      out.append(d);
+    }
+    return out;
+  }, "every conv routing row in order, with its current state");
+  m.def("conv_route_select", [](int op, int taps, int stride, int cin, int cout, int64_t rows,
+                                int flags, std::vector<int64_t> cls_rows) {
+    RouteProblem p;
+    p.op = op; p.taps = taps; p.stride = stride; p.cin = cin; p.cout = cout; p.rows = rows;
+    p.flags = flags;
+    TORCH_CHECK(cls_rows.size() <= (size_t)MAX_DG_CLASSES, "too many parity classes");
+    p.ncls = (int)cls_rows.size();
+    for (size_t c = 0; c < cls_rows.size(); ++c) p.cls_rows[c] = cls_rows[c];
+    py::list names;
+    for (int i = route_next(p, -1); i >= 0; i = route_next(p, i)) names.append(route_rule(i).name);
+    return names;
+  }, py::arg("op"), py::arg("taps"), py::arg("stride"), py::arg("cin"), py::arg("cout"),
+     py::arg("rows"), py::arg("flags") = 0, py::arg("cls_rows") = std::vector<int64_t>{},
+     "the rows a launcher would try for this problem, in order (each launcher then runs the first "
+     "whose kernel takes it)");
+  m.def("conv_route_force", [](int op, std::string name) { route_force(op, name.c_str()); },
+        py::arg("op"), py::arg("name") = "",
+        "tests: only this row for op (0 fwd, 1 dgrad, 2 wgrad); a launcher that cannot run it "
+        "raises; '' clears");
+  m.def("conv_route_set", [](std::string name, int on, int cfg) { route_set(name.c_str(), on, cfg); },
+        py::arg("name"), py::arg("on") = -1, py::arg("cfg") = -1,
+        "in-process A/B: turn a row on (1) / off (0) and / or set its tile config (validated)");
+  m.def("conv_route_reset", &route_reset, "route rows back to the table + environment");
+  m.def("conv_last_route", [](int op) -> py::object {
+    const int i = route_last(op);
+    if (i < 0) return py::none();
+    return py::str(route_rule(i).name);
+  }, py::arg("op"), "the row the last conv launch of op ran on this thread");
+  m.def("conv_route_counts", [](bool reset) {
+    py::dict d;
+    for (int i = 0; i < route_count(); ++i)
+      if (route_count_of(i)) d[py::str(route_rule(i).name)] = route_count_of(i);
+    if (reset) route_counts_reset();
+    return d;
+  }, py::arg("reset") = false, "launches per route row since the last reset (eager launches)");
+  m.def("conv_route_cfg_instantiated", &route_cfg_instantiated, py::arg("impl"), py::arg("op"),
+        py::arg("cfg"), py::arg("flags") = 0);
   m.def("conv_set_m32", &conv_set_m32, "32x32x16-MFMA K loop for KC-operand LDS-DMA convs (-1: env)");
   m.def("conv_m32", &conv_m32);
   m.def("conv_f32_set_tile", &conv_f32_set_tile, "fp32 conv FWD/DGRAD tile override (0, 0: auto)");

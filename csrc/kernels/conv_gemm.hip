@@ -31,7 +31,9 @@
 // 16-B fp32 vector stores.  Epilogue: bias, ReLU, and per-channel Σy / Σy² of the stored bf16
 // values (BatchNorm statistics) reduced lanes → waves (LDS) → one contiguous atomic row per tile.
 #include "conv_common.h"
+#include "conv_route.h"
 #include <stdexcept>
+#include <string>
 
 namespace tdl {
 
@@ -764,14 +766,53 @@ static int pick_tpb(long tiles, int nkt) {
   return (int)tpb;
 }
 
+[[noreturn]] static void route_fail(int op, const RouteProblem& p) {
+  const int f = route_forced(op);
+  std::string msg = std::string(op == 0 ? "conv_fwd" : op == 1 ? "conv_dgrad" : "conv_wgrad") +
+                    ": no conv route ran the problem (taps " + std::to_string(p.taps) +
+                    ", stride " + std::to_string(p.stride) + ", C " + std::to_string(p.cin) +
+                    ", K " + std::to_string(p.cout) + ", rows " + std::to_string(p.rows) +
+                    ", flags " + std::to_string(p.flags) + ")";
+  if (f >= 0) msg += std::string(" — forced route '") + route_rule(f).name + "' does not take it";
+  throw std::runtime_error(msg);
+}
+
+static void conv_fwd_gemm(const ConvArgs& a0, hipStream_t st);
+
+// the forward through the route table (conv_route.hip): false when no row took it (a residual
+// problem outside the LDS-DMA kernel: the caller adds the residual itself)
+static bool conv_fwd_route(const ConvArgs& a0, hipStream_t st) {
+  const int flags = (a0.stats ? RF_STATS : 0) | (a0.aff ? RF_AFF : 0) | (a0.res ? RF_RES : 0) |
+                    (a0.bias ? RF_BIAS : 0);
+  const RouteProblem p = route_problem(0, a0, flags);
+  for (int i = route_next(p, -1); i >= 0; i = route_next(p, i)) {
+    bool ran = false;
+    switch (route_rule(i).impl) {
+      case RT_HALO: ran = conv_fwd_halo(a0, st); break;
+      case RT_PC: ran = conv_fwd_pc_run(a0, st); break;
+      case RT_GLDS: ran = conv_fwd_glds(a0, route_cfg(i), st); break;
+      case RT_GEMM: conv_fwd_gemm(a0, st); ran = true; break;
+      default: break;
+    }
+    if (ran) {
+      route_record(0, i);
+      return true;
+    }
+  }
+  if (route_forced(0) >= 0) route_fail(0, p);
+  return false;
+}
+
 void conv_fwd_launch(const ConvArgs& a0, hipStream_t st) {
-  const bool aff = a0.aff != nullptr;
-  if (aff && (a0.C % 8 || a0.K % 8 || a0.bias || a0.res))
+  if (a0.aff && (a0.C % 8 || a0.K % 8 || a0.bias || a0.res))
     throw std::runtime_error("folded-BN conv: C % 8 == 0, K % 8 == 0, no bias / residual");
-  // the halo kernel has no folded-BN staging; the LDS-DMA launcher takes a folded BN only onto
-  // the producer/consumer kernel (its producers stage the transformed operand)
-  if (!aff && conv_fwd_halo(a0, st)) return;
-  if (conv_fwd_glds(a0, st)) return;
+  if (!conv_fwd_route(a0, st)) route_fail(0, route_problem(0, a0, 0));
+}
+
+bool conv_fwd_res_launch(const ConvArgs& a, hipStream_t st) { return conv_fwd_route(a, st); }
+
+static void conv_fwd_gemm(const ConvArgs& a0, hipStream_t st) {
+  const bool aff = a0.aff != nullptr;
   ConvArgs a = a0;
   convk::set_fastdivs(a);
   a.dbg = gemm_dbg();
@@ -826,19 +867,14 @@ static void zero_fill(void* p, uint32_t bytes, hipStream_t st) {
   hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)p, n4);
 }
 
+static void conv_dgrad_gemm(const ConvArgs& a0, bool masked, long Mmax, hipStream_t st);
+
 bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   const bool masked = (a.sh > 1 && a.dh > 1) || (a.sw > 1 && a.dw > 1) ||
                       a.sh * a.sw > MAX_DG_CLASSES;
   a.dg_masked = masked ? 1 : 0;
-  if (!masked && a.sh == 1 && a.sw == 1 && a.w_flip) {  // stride 1: as the forward conv of dy
-    bool fused = false;
-    if (conv_dgrad_as_fwd(a, a.w_flip, a.w_flip_bytes, st, &fused)) return fused;
-  }
-  if (!masked && a.sh == 1 && a.sw == 1) {  // stride 1: the halo-tiled direct conv
-    bool fused = false;
-    if (conv_dgrad_halo(a, st, &fused)) return fused;
-  }
+  const ConvArgs a_s1 = a;  // (stride-1 executors: their own geometry, no parity classes)
   // build parity classes
   int ncls = 0;
   long Mmax = 0;
@@ -890,15 +926,57 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   // instead of GEMM tiles (they are last after the LPT sort)
   int nz = ncls;
   while (nz > 0 && a.cls_Th[nz - 1] * a.cls_Tw[nz - 1] == 0) --nz;
-  // (when accumulating into an existing dx the zero classes simply keep their values)
-  if (nz < ncls && !a.beta) zero_fill(a.out, a.out_bytes, st);
-  ncls = nz;
-  if (ncls == 0) return false;
-  a.ncls = ncls;
-  bool fused = false;
-  if (!masked && conv_dgrad_glds(a, Mmax * ncls, st, &fused)) return fused;
+  a.ncls = nz;
+  // the route problem: dx rows per parity class with taps; fused statistics only where the
+  // LDS-DMA epilogue can take them (dgrad_stats_fusable)
+  const bool s1 = !masked && a.sh == 1 && a.sw == 1;
+  const bool stats = nz > 0 && dgrad_stats_fusable(a);
+  const int flags = (stats ? RF_STATS : 0) | (a.beta ? RF_JOIN : 0) |
+                    (stats && a.beta ? RF_STATS_JOIN : 0) | (a.aff ? RF_AFF : 0) |
+                    (a.fp8 ? RF_FP8 : 0) | (s1 && a.w_flip ? RF_WFLIP : 0);
+  RouteProblem p = route_problem(1, a, flags);
+  p.ncls = nz;
+  p.rows = 0;
+  for (int c = 0; c < nz; ++c) {
+    p.cls_rows[c] = (long)a.N * a.cls_Hc[c] * a.cls_Wc[c];
+    p.rows += p.cls_rows[c];
+  }
+  if (nz == 0) {  // no pixel of dx receives a tap
+    if (!a.beta) zero_fill(a.out, a.out_bytes, st);
+    return false;
+  }
+  bool zeroed = false;
+  for (int i = route_next(p, -1); i >= 0; i = route_next(p, i)) {
+    const RouteRule& r = route_rule(i);
+    bool fused = false, ran = false;
+    if (r.impl == RT_ASFWD) {
+      ran = s1 && conv_dgrad_as_fwd(a_s1, a.w_flip, a.w_flip_bytes, route_cfg(i), st, &fused);
+    } else if (r.impl == RT_HALO) {
+      ran = s1 && conv_dgrad_halo(a_s1, st, &fused);
+    } else {
+      // (when accumulating into an existing dx the zero classes simply keep their values)
+      if (!zeroed && nz < ncls && !a.beta) zero_fill(a.out, a.out_bytes, st);
+      zeroed = true;
+      if (r.impl == RT_GLDS) {
+        ran = conv_dgrad_glds(a, route_cfg(i), st, &fused);
+      } else if (r.impl == RT_GEMM) {
+        conv_dgrad_gemm(a, masked, Mmax, st);
+        ran = true;
+      }
+    }
+    if (ran) {
+      route_record(1, i);
+      return fused;
+    }
+  }
   if (a.fp8) throw std::runtime_error("fp8 dgrad: LDS-DMA kernel not eligible (K % 128, C % 8, "
                                       "stride with dilation)");
+  route_fail(1, p);
+}
+
+static void conv_dgrad_gemm(const ConvArgs& a0, bool masked, long Mmax, hipStream_t st) {
+  ConvArgs a = a0;
+  const int ncls = a.ncls;
   convk::set_fastdivs(a);
   a.dbg = gemm_dbg();
   int bm, bn;
@@ -911,20 +989,38 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
     maxkt = std::max(maxkt, cdiv((long)a.cls_Th[c] * a.cls_Tw[c] * a.K, BK));
   }
   const long tiles = a.cls_tile0[ncls];
-  if (tiles == 0) return false;
+  if (tiles == 0) return;
   a.tpb = pick_tpb(tiles, maxkt);
   a.splits = 1;
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
   const bool al = (a.C % 8 == 0) && (a.K % 8 == 0) && !masked;
   if (al) launch_cfg<DGRAD, true, false>(a, bm, bn, blocks, st);
   else launch_cfg<DGRAD, false, false>(a, bm, bn, blocks, st);
-  return false;  // the register-staged kernel does not fuse BN-backward statistics
+  // (the register-staged kernel does not fuse BN-backward statistics)
 }
 
+static void conv_wgrad_gemm_plan(const ConvArgs& a, WgradPlan* p);
+
+// a folded BN on x (ConvArgs::aff): the register-staged kernel (it transforms the staged B rows)
 void conv_wgrad_plan(const ConvArgs& a, WgradPlan* p) {
-  // a folded BN on x (ConvArgs::aff): the register-staged kernel (it transforms the staged B rows)
-  if (!a.aff && conv_wgrad_halo_plan(a, p)) return;
-  if (!a.aff && conv_wgrad_glds_plan(a, p)) return;
+  RouteProblem q = route_problem(2, a, a.aff ? RF_AFF : 0);
+  for (int i = route_next(q, -1); i >= 0; i = route_next(q, i)) {
+    bool ran = false;
+    switch (route_rule(i).impl) {
+      case RT_HALO: ran = conv_wgrad_halo_plan(a, p); break;
+      case RT_GLDS: ran = conv_wgrad_glds_plan(a, route_cfg(i), p); break;
+      case RT_GEMM: conv_wgrad_gemm_plan(a, p); ran = true; break;
+      default: break;
+    }
+    if (ran) {
+      route_record(2, i);
+      return;
+    }
+  }
+  route_fail(2, q);
+}
+
+static void conv_wgrad_gemm_plan(const ConvArgs& a, WgradPlan* p) {
   p->impl = 0;
   p->cfg = 0;
   p->bm = a.M <= 64 ? 64 : 128;

@@ -25,6 +25,7 @@
 // Epilogue (bias, ReLU, BN Σ/Σ² statistics of the stored bf16 values, DGRAD class scatter, WGRAD
 // fp32 split-K slabs) is the same as conv_gemm.hip's.
 #include "conv_common.h"
+#include "conv_route.h"
 
 namespace tdl {
 
@@ -926,16 +927,9 @@ void launch_g(const ConvArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * WM * WN), lds, st, a);
 }
 
-// the tile configs launch_gcfg instantiates for (mode, statistics): an environment override
-// (TDL_GLDS_CFG_*) outside them keeps the default — the tile count is computed from cfg_of(cfg),
-// so a config the launcher does not have would leave output tiles unwritten
-bool cfg_valid(int mode, bool stats, int cfg) {
-  if (cfg >= 0 && cfg <= 4) return true;
-  if (cfg == 6) return mode == DGRAD && stats;
-  if (cfg == 7) return mode == WGRAD;
-  return false;
-}
-
+// the tile configs launch_gcfg instantiates: 0–5 (5 = the 128×64 default), 6 for fused-statistics
+// dgrads, 7 for weight gradients — route_cfg_instantiated (conv_route.hip) is the table of record;
+// a config the launcher does not have would leave output tiles unwritten
 template <int MODE, bool STATS, bool BIAS, int FK, bool NJ = false>
 void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
   if (cfg == 0)
@@ -950,10 +944,13 @@ void launch_gcfg(const ConvArgs& a, int cfg, int blocks, hipStream_t st) {
     launch_g<MODE, 256, 64, 8, 1, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
   else if (cfg == 6 && MODE == DGRAD && STATS)  // fused-statistics dgrads only
     launch_g<MODE, 128, 128, 4, 2, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
-  else if (cfg == 7) {  // weight gradients of few-output-channel convs only (the ResNet stem)
+  else if (cfg == 7 && MODE == WGRAD) {  // few-output-channel weight gradients (the ResNet stem)
     if constexpr (MODE == WGRAD) launch_g<MODE, 64, 256, 1, 4, 3, STATS, BIAS, FK, false, NJ>(a, blocks, st);
-  } else
+  } else if (cfg == 5)
     launch_g<MODE, 128, 64, 4, 1, 4, STATS, BIAS, FK, false, NJ>(a, blocks, st);
+  else
+    throw std::runtime_error("LDS-DMA conv: tile config " + std::to_string(cfg) +
+                             " not instantiated for this problem");
 }
 
 const GCfg& cfg_of(int c) {
@@ -983,12 +980,20 @@ int persistent_tpb(long tiles) {
 
 }  // namespace
 
-// fp8 forward: LDS-DMA kernel only (C % 16 == 0: a 16-B chunk never crosses a filter tap)
+// fp8 forward: LDS-DMA kernel only (C % 16 == 0: a 16-B chunk never crosses a filter tap); the
+// tile config from the route table (fwd.glds.fp8 / fwd.glds.fp8.n64)
 void conv_fwd_fp8_launch(const ConvArgs& a0, hipStream_t st) {
+  const RouteProblem p = route_problem(FWD, a0, RF_FP8 | (a0.stats ? RF_STATS : 0));
+  const int ri = route_next(p, -1);
+  if (ri < 0) throw std::runtime_error("fp8 forward: no conv route takes this problem");
+  const int cfg = route_cfg(ri);
+  if (cfg != 0 && cfg != 1)
+    throw std::runtime_error(std::string("fp8 forward: route ") + route_rule(ri).name +
+                             " is not an fp8 tile config");
+  route_record(FWD, ri);
   ConvArgs a = a0;
   a.dbg = 0;
   set_fastdivs(a);
-  const int cfg = a.Ng >= 128 ? 0 : 1;
   const GCfg& g = cfg_of(cfg);
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
   a.ncls = 1;
@@ -1027,9 +1032,9 @@ int conv_m32() {
   return g_m32_override >= 0 ? g_m32_override : m;
 }
 void conv_set_m32(int on) { g_m32_override = on; }
-// producer/consumer forward (conv_pc.hip): TDL_CONV_PC unset = auto (4 producer waves for the
-// 3×3 convs with ≥ 256 input channels, where it measured faster: profiles/r04_conv_pc_ab.txt),
-// 0 = off, 1 / 2 = 2 / 4 producer waves on every FASTK 256×128 forward; conv_set_pc(-1) = env
+// producer/consumer forward (conv_pc.hip): TDL_CONV_PC unset = the route table's rows
+// (fwd.pc.*), 0 = those rows off, 1 / 2 = 2 / 4 producer waves on every FASTK 256×128 forward;
+// conv_set_pc(-1) = env
 static int g_pc_override = -1;
 int conv_pc() {
   static int m = env_int("TDL_CONV_PC", -1);
@@ -1037,36 +1042,43 @@ int conv_pc() {
 }
 void conv_set_pc(int on) { g_pc_override = on; }
 
-bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
-  const int mode = conv_glds_mode();
-  if (mode == 0 || a0.C % 8 || a0.K % 8) return false;
-  if (a0.res && !a0.bias) return false;  // residual epilogue instantiated with bias only
-  if (a0.aff && (a0.res || a0.C % 64)) return false;
-  // default selection (ResNet-50 b256, dev/tools/n64_configs.py): ≥ 128 output channels, and 1×1
-  // filters with 64 (the 8-wave 256×64 tiles: 35 vs 53 µs on 56×56 64→64); 3×3 filters with 64
-  // output channels stay on the register-staged kernel
-  const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
-  if (mode == 1 && ((long)a0.M < 4096 || (a0.Ng < 128 && !n64_1x1))) return false;
+// FWD tile order (tile_of): a workgroup owns one column tile and tpb consecutive row tiles
+static int fwd_tiling(ConvArgs& a, const GCfg& g) {
+  const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
+  a.ncls = 1;
+  a.splits = 1;
+  a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm * ntn)), ntm);
+  const long groups = (ntm + a.tpb - 1) / a.tpb;
+  a.cls_tile0[0] = 0;
+  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+  return (int)(groups * ntn);
+}
+
+// route rows fwd.pc.*: the wave-specialised producer/consumer forward on 256×128 FASTK tiles; a
+// folded BN (a.aff) only here — its producers stage the transformed operand
+bool conv_fwd_pc_run(const ConvArgs& a0, hipStream_t st) {
+  if (a0.C % 8 || a0.K % 8 || a0.res) return false;
+  if (a0.aff && (a0.C % 64 || a0.bias)) return false;
+  const int fk = a0.C % 64 == 0 ? 1 : (a0.R * a0.S == 1 ? 2 : 0);
+  if (fk == 0) return false;
   ConvArgs a = a0;
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
-  int cfg = a.Ng <= 64 ? 4 : 0;
-  if (const int e = env_int("TDL_GLDS_CFG_FWD", cfg); cfg_valid(FWD, false, e)) cfg = e;
-  const GCfg& g = cfg_of(cfg);
-  const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
-  // fewer than half a tile per CU: the register-staged kernel's smaller tiles and two workgroups
-  // per CU win (reference DeepLab preset, 13×13×1024→256 at batch 64: 20.6 vs 25.0 µs;
-  // dev/tools/cfg_ab.py)
-  if (mode == 1 && ntm * ntn < 128) return false;
-  a.ncls = 1;
-  a.splits = 1;
-  // FWD tile order (tile_of): a workgroup owns one column tile and tpb consecutive row tiles
-  a.tpb = std::max(1, persistent_tpb(ntm * ntn) );
-  a.tpb = std::min<long>(a.tpb, ntm);
-  const long groups = (ntm + a.tpb - 1) / a.tpb;
-  const int blocks = (int)(groups * ntn);
-  a.cls_tile0[0] = 0;
-  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
+  const int blocks = fwd_tiling(a, G256x128);
+  const int waves = a.aff ? 2 : (conv_pc() > 0 ? conv_pc() : 2);
+  return conv_fwd_pc_launch(a, blocks, fk, waves, st);
+}
+
+// route rows fwd.glds.*: the LDS-DMA forward with tile config `cfg` (false: not eligible /
+// not instantiated — nothing launched)
+bool conv_fwd_glds(const ConvArgs& a0, int cfg, hipStream_t st) {
+  if (a0.C % 8 || a0.K % 8 || a0.aff) return false;
+  if (a0.res && !a0.bias) return false;  // residual epilogue instantiated with bias only
+  if (!route_cfg_instantiated(RT_GLDS, FWD, cfg, a0.res ? RF_RES : 0)) return false;
+  ConvArgs a = a0;
+  a.dbg = env_int("TDL_CONV_DBG", 0);
+  set_fastdivs(a);
+  const int blocks = fwd_tiling(a, cfg_of(cfg));
   // FASTK (FK 1): a K-step is one filter tap × 64 channels; 1×1 filters with C % 64 != 0 take
   // it with the row's last channel chunk range-checked (FK 2: Xception's 728-channel pointwise
   // convs); otherwise the generic K decomposition (FK 0)
@@ -1082,12 +1094,6 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
       else launch_gcfg<FWD, false, false, FK>(a, cfg, blocks, st);           \
     }                                                                        \
   } while (0)
-  if (a.aff) {
-    // folded BN + ReLU on x: only the producer/consumer kernel stages a transformed operand
-    // (FASTK 256×128 tiles); anything else runs on the register-staged kernel
-    if (fk != 1 || cfg != 0 || bias) return false;
-    return conv_fwd_pc_launch(a, blocks, fk, 2, st);
-  }
   if (a.res) {
     // residual epilogue (DeepLab units): the default FWD tile configs, bias, ± statistics
 #define TDL_R(FK)                                                                            \
@@ -1118,12 +1124,9 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
     }
     return true;
   }
-  // TDL_CONV_PC=1: the wave-specialised producer/consumer forward (conv_pc.hip)
-  {
-    int pc = conv_pc();
-    if (pc < 0) pc = (a.R * a.S > 1 && a.C >= 256) ? 2 : 0;
-    if (pc > 0 && fk != 0 && cfg == 0 && conv_fwd_pc_launch(a, blocks, fk, pc, st)) return true;
-  }
+  // TDL_CONV_PC=1 / 2: the producer/consumer forward on every FASTK 256×128 problem (A/B)
+  if (conv_pc() > 0 && fk != 0 && cfg == 0 && conv_fwd_pc_launch(a, blocks, fk, conv_pc(), st))
+    return true;
   if (fk == 1) TDL_G(1);
   else if (fk == 2) TDL_G(2);
   else TDL_G(0);
@@ -1131,26 +1134,23 @@ bool conv_fwd_glds(const ConvArgs& a0, hipStream_t st) {
   return true;
 }
 
-bool conv_fwd_res_launch(const ConvArgs& a, hipStream_t st) { return conv_fwd_glds(a, st); }
-
 // Stride-1 input gradient as the FORWARD conv of dy with the flipped, transposed filter:
 // dx[n,h,w,c] = Σ_{r',s',k} dy[n, h − ph' + r'·dh, w − pw' + s'·dw, k] · w_flip[c][r'][s'][k],
 // ph' = dh·(R−1) − ph — the forward kernels' K loop (LDS-DMA / producer-consumer; both operands
 // K-contiguous, no transposed LDS reads, no parity-class bookkeeping) with the DGRAD epilogue
 // (DEPI: ReLU bit mask, residual join, BN-backward statistics).  bench/dgrad_paths.py, ResNet-50
 // b1024: 3×3 dgrads 22–31 % faster than the DGRAD kernel, 1×1 3–15 %.
-bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, hipStream_t st,
-                       bool* fused) {
+// cfg (the route row's): 0 / 4 the LDS-DMA K loop with 256×128 / 8-wave 256×64 tiles, 100 the
+// halo forward loader, 102 the producer/consumer kernel.
+bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, int cfg,
+                       hipStream_t st, bool* fused) {
   if (fused) *fused = false;
-  const int mode = conv_glds_mode();
-  if (mode == 0 || wf == nullptr || a0.fp8 || a0.aff || a0.dg_masked) return false;
+  if (wf == nullptr || a0.fp8 || a0.aff || a0.dg_masked) return false;
   if (a0.sh != 1 || a0.sw != 1 || a0.K % 64 || a0.C % 8 || a0.ldc != a0.C) return false;
   // the DGRAD epilogue indexes dx through dy's geometry: same spatial size ("same" padding)
   if (a0.Ho != a0.H || a0.Wo != a0.W) return false;
   const int ph = a0.dh * (a0.R - 1) - a0.ph, pw = a0.dw * (a0.S - 1) - a0.pw;
   if (ph < 0 || pw < 0) return false;
-  static const int on = env_int("TDL_DGRAD_AS_FWD", 1);
-  if (!on) return false;
   ConvArgs a = a0;
   a.x = a0.dy;
   a.x_bytes = a0.dy_bytes;
@@ -1179,24 +1179,15 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
   if (!stats) a.stats = nullptr;
   if (stats && a.beta) return false;  // statistics + join: the DGRAD kernel's 8-wave tiles
-  // ≤ 64-wide dx, 3×3: the halo forward loader (as the forward routes those convs)
-  if (conv_fwd_halo_depi(a, st, fused)) return true;
-  const int cfg = a.Ng <= 64 ? 4 : 0;
-  const GCfg& g = cfg_of(cfg);
-  const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
-  if (mode == 1 && ((long)a.M < 4096 || ntm * ntn < 128)) return false;
-  a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm * ntn)), ntm);
-  const long groups = (ntm + a.tpb - 1) / a.tpb;
-  const int blocks = (int)(groups * ntn);
-  a.cls_tile0[0] = 0;
-  a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
-  // the producer/consumer kernel where the forward routes its 3×3 convs (not with the
-  // statistics epilogue: its x registers spill at the 12-wave register budget)
-  if (cfg == 0 && !stats && a.R * a.S > 1 && a.C >= 256 &&
-      conv_fwd_pc_launch(a, blocks, 1, 2, st, true)) {
-    if (fused) *fused = stats;
-    return true;
+  if (cfg == 100) return conv_fwd_halo_depi(a, st, fused);
+  if (cfg == 102) {
+    // (not with the statistics epilogue: its x registers spill at the 12-wave register budget)
+    if (stats) return false;
+    const int blocks = fwd_tiling(a, G256x128);
+    return conv_fwd_pc_launch(a, blocks, 1, 2, st, true);
   }
+  if (cfg != 0 && cfg != 4) return false;
+  const int blocks = fwd_tiling(a, cfg_of(cfg));
   if (cfg == 4) {
     if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
     else launch_g<FWD, 256, 64, 8, 1, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
@@ -1235,32 +1226,31 @@ void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, i
   hipLaunchKernelGGL(flip_weight_kernel, grid, dim3(256), 0, st, w, wf, K, R, S, C);
 }
 
-// DGRAD with prepared parity classes (conv_dgrad_launch builds them); returns false when the
-// register-staged kernel should run instead.
-bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* fused) {
+// fused BN-backward statistics in the LDS-DMA DGRAD epilogue (a.stats, a.bn_x): FASTK (K % 64 == 0,
+// or the ragged form of a one-class 1×1); joins need stride 1 — an accumulate leaves the pixels of
+// a class without taps unmasked; a folded BN's mask (a.aff) rides on the single-consumer form
+bool dgrad_stats_fusable(const ConvArgs& a) {
+  if (!a.stats || !a.bn_x || a.fp8 || a.dg_masked) return false;
+  const bool rag = a.K % 64 != 0 && a.R * a.S == 1 && a.ncls == 1 && a.K % 8 == 0;
+  if (a.K % 64 != 0 && !rag) return false;
+  if (a.beta && !(a.ncls == 1 && a.sh == 1 && a.sw == 1)) return false;
+  return !a.aff || (a.K % 64 == 0 && !a.beta);
+}
+
+// DGRAD with prepared parity classes (conv_dgrad_launch builds them) on tile config `cfg` (the
+// route row's); false when the kernel does not take the problem or config — nothing launched
+bool conv_dgrad_glds(const ConvArgs& a0, int cfg, hipStream_t st, bool* fused) {
   if (fused) *fused = false;
-  const int mode = conv_glds_mode();
-  if (a0.fp8) {  // fp8 operands exist only for this kernel
-    if (a0.C % 8 || a0.K % 128 || a0.dg_masked) return false;
-  } else {
-    if (mode == 0 || a0.C % 8 || a0.K % 8 || a0.dg_masked) return false;
-    // 1×1 filters with 64 input channels (dx width): 8-wave 256×64 tiles (49 vs 88 µs on
-    // ResNet-50 56×56 64→64, dev/tools/n64_configs.py)
-    const bool n64_1x1 = a0.R * a0.S == 1 && a0.Ng > 48 && a0.Ng <= 64;
-    // with fused BN statistics the 64-wide 3×3 dgrads too (ResNet-50 layer1 conv2: the LDS-DMA
-    // 8-wave 256×64 dgrad is within 5 % of the register-staged one, and the fusion saves the BN's
-    // reduce pass; TDL_DGSTAT_N64=0 turns it off)
-    static const bool n64_stats_on = env_int("TDL_DGSTAT_N64", 1) != 0;
-    const bool n64_stats = n64_stats_on && a0.stats && a0.bn_x && a0.Ng > 48 && a0.Ng <= 64 &&
-                           a0.ncls == 1 && a0.sh == 1 && a0.sw == 1 && a0.K % 64 == 0;
-    if (mode == 1 && (Mmax_total < 4096 || (a0.Ng < 128 && !n64_1x1 && !n64_stats))) return false;
+  if (a0.dg_masked || a0.C % 8) return false;
+  if (a0.fp8 ? (a0.K % 128 || (cfg != 0 && cfg != 1)) : a0.K % 8) return false;
+  const bool bn_stats = dgrad_stats_fusable(a0);
+  if (!a0.fp8) {
+    const int flags = (bn_stats ? RF_STATS : 0) | (bn_stats && a0.aff ? RF_AFF : 0);
+    if (!route_cfg_instantiated(RT_GLDS, DGRAD, cfg, flags)) return false;
   }
   ConvArgs a = a0;
   a.dbg = env_int("TDL_CONV_DBG", 0);
   set_fastdivs(a);
-  int cfg = a.Ng <= 64 ? (a.fp8 ? 1 : 4) : 0;
-  if (const int e = env_int("TDL_GLDS_CFG_DGRAD", cfg); !a.fp8 && cfg_valid(DGRAD, false, e))
-    cfg = e;
   const GCfg& g = cfg_of(cfg);
   a.cls_tile0[0] = 0;
   for (int c = 0; c < a.ncls; ++c) {
@@ -1269,28 +1259,14 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   }
   const long tiles = a.cls_tile0[a.ncls];
   if (tiles == 0) return true;
-  if (mode == 1 && !a.fp8 && tiles < 128) return false;  // see conv_fwd_glds
-  // BN-backward statistics in the epilogue (a.stats, a.bn_x): stride 1 (one class covering
-  // every pixel), FASTK; tiles in the forward's column-grouped order (tile_of COLG) so each
-  // workgroup flushes its column sums once
-  // (strided dgrads: every parity class in the same order, each class's tiles padded to whole
-  // workgroups so none straddles two classes; a class without taps was zero-filled and adds 0;
-  // joins need stride 1 — an accumulate leaves the pixels of such a class unmasked)
-  // K % 64 != 0 (Xception's 728-channel pointwise convs): the ragged FASTK form for 1×1 filters
-  const bool rag_stats = a.K % 64 != 0 && a.R * a.S == 1 && a.ncls == 1 && a.K % 8 == 0;
-  // a folded BN's mask (a.aff) rides on the single-consumer statistics epilogue: K % 64 == 0,
-  // no join, the default tile configs
-  const bool aff_ok = !a.aff || (a.K % 64 == 0 && !a.beta);
-  const bool bn_stats = a.stats && a.bn_x && !a.fp8 && (a.K % 64 == 0 || rag_stats) &&
-                        (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1)) && aff_ok;
+  // BN-backward statistics: tiles in the forward's column-grouped order (tile_of COLG) so each
+  // workgroup flushes its column sums once (strided dgrads: every parity class in the same order,
+  // each class's tiles padded to whole workgroups so none straddles two classes; a class without
+  // taps was zero-filled and adds 0).  Tile configs (dev/tools/dgrad_bnstat_ab.py, ResNet-50
+  // b256): without a join 256×128 (NJ: no previous-dx registers); with the join's previous-dx
+  // loads as well those spill — 8 waves of 32×64 (cfg 6); a folded BN's coefficients likewise
+  const bool rag_stats = a.K % 64 != 0;
   if (bn_stats) {
-    // tile config (dev/tools/dgrad_bnstat_ab.py, ResNet-50 b256): without a join the usual 256×128
-    // tiles (NJ: no previous-dx registers); with the join's previous-dx loads as well they spill,
-    // so 8 waves of 32×64 (cfg 6); 64-wide dx: the 8-wave 256×64 tiles
-    const int sdef = a.Ng <= 64 ? 4 : (a.beta ? 6 : 0);
-    const int senv = env_int(a.beta ? "TDL_GLDS_CFG_DGSTAT_J" : "TDL_GLDS_CFG_DGSTAT", sdef);
-    const int scfg = a.aff ? (a.Ng <= 64 ? 4 : 6) : (cfg_valid(DGRAD, true, senv) ? senv : sdef);
-    const GCfg& g = cfg_of(scfg);
     const long ntn = cdiv(a.Ng, g.bn);
     long ntm_all = 0, ntm_max = 1;
     for (int c = 0; c < a.ncls; ++c) {
@@ -1306,20 +1282,20 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
     }
     const int blocks = a.cls_tile0[a.ncls] / a.tpb;
     a.splits = 1;
-    if (a.aff) {  // (K % 64 == 0, no join: aff_ok)
-      if (scfg == 4)
+    if (a.aff) {  // (K % 64 == 0, no join; cfg 4 or 6)
+      if (cfg == 4)
         launch_g<DGRAD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, true>(a, blocks, st);
       else  // (8 waves of 32×64: the 256×128 tiles spill with the coefficient registers)
         launch_g<DGRAD, 128, 128, 4, 2, 4, true, false, 1, false, true, false, false, true>(a, blocks, st);
     } else if (rag_stats) {
       if (a.beta)
-        launch_gcfg<DGRAD, true, false, 2>(a, scfg, blocks, st);
+        launch_gcfg<DGRAD, true, false, 2>(a, cfg, blocks, st);
       else
-        launch_gcfg<DGRAD, true, false, 2, true>(a, scfg, blocks, st);
+        launch_gcfg<DGRAD, true, false, 2, true>(a, cfg, blocks, st);
     } else if (a.beta) {
-      launch_gcfg<DGRAD, true, false, 1>(a, scfg, blocks, st);
+      launch_gcfg<DGRAD, true, false, 1>(a, cfg, blocks, st);
     } else {
-      launch_gcfg<DGRAD, true, false, 1, true>(a, scfg, blocks, st);
+      launch_gcfg<DGRAD, true, false, 1, true>(a, cfg, blocks, st);
     }
     if (fused) *fused = true;
     return true;
@@ -1349,22 +1325,12 @@ bool conv_dgrad_glds(const ConvArgs& a0, long Mmax_total, hipStream_t st, bool* 
   return true;
 }
 
-// WGRAD split-K plan for the LDS-DMA kernel: ≈ one tile-split per CU slot, ≥ 16 K-steps each
-bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p) {
-  const int mode = conv_glds_mode();
-  if (mode == 0 || a.C % 8 || a.K % 8) return false;
-  // the ResNet stem (64 output channels × 168 row-packed columns, K = every output pixel): one
-  // 64×256 tile column reads dy once, where the register-staged kernel's 64×128 tiles read it twice
-  // — measured slower on the row-packed stem at b1024 (1120 vs 1040 us, dev/tools/stem_ab.py: the x
-  // gather, not the dy re-read, bounds it), so opt-in (TDL_GLDS_STEM_WGRAD=1)
-  const char* stem_env = getenv("TDL_GLDS_STEM_WGRAD");
-  const bool stem = (stem_env ? atoi(stem_env) : 0) != 0 && a.M <= 64 && a.Ng > 128 &&
-                    a.Ng <= 256 && (long)a.Kg >= 65536;
-  // default: 1×1 filters with ≥ 256 output channels (3×3 gathers of x favour the other kernel)
-  static const int mmin = env_int("TDL_GLDS_WGRAD_MMIN", 256);
-  if (mode == 1 && !stem && ((long)a.Kg < 4096 || a.M < mmin || a.R * a.S != 1)) return false;
-  int cfg = stem ? 7 : a.M <= 128 ? 2 : 0;
-  if (const int e = env_int("TDL_GLDS_CFG_WGRAD", cfg); cfg_valid(WGRAD, false, e)) cfg = e;
+// WGRAD split-K plan for the LDS-DMA kernel on tile config `cfg` (the route row's: 0 / 2 the
+// usual tiles, 7 the 64×256 column of the row-packed stem): ≈ one tile-split per CU slot,
+// ≥ 16 K-steps each
+bool conv_wgrad_glds_plan(const ConvArgs& a, int cfg, WgradPlan* p) {
+  if (a.C % 8 || a.K % 8 || a.aff) return false;
+  if (!route_cfg_instantiated(RT_GLDS, WGRAD, cfg, 0)) return false;
   const GCfg& g = cfg_of(cfg);
   const long tiles = (long)cdiv(a.M, g.bm) * cdiv(a.Ng, g.bn);
   const int nkt = cdiv(a.Kg, BK);

@@ -811,14 +811,9 @@ bool plan_halo_wgrad(const ConvArgs& a, HaloGeom& g, HaloWg& q, int& bm) {
 
 }  // namespace
 
+// route rows wgrad.halo.*: false when the kernel does not take the problem
 bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p) {
   if (a.aff) return false;
-  if (!conv_halo_mode()) return false;
-  if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
-  // default: ≥ 128 input channels and enough pixel tiles to split over the chip (ResNet-50 b1024
-  // layers 2–4: 362 → 328 / 295 / 290 µs; the small-batch DeepLab shapes stay on the GEMMs)
-  static const int cmin = henv("TDL_HALO_WG_CMIN", 128);
-  if (conv_halo_mode() == 1 && (a.C < cmin || (long)a.N * a.Ho * a.Wo < 65536)) return false;
   HaloGeom g;
   HaloWg q;
   int bm;
@@ -852,16 +847,10 @@ void conv_set_halo_mode(int mode) { g_halo_override = mode; }
 // FWD, stride 1: true when the halo kernel ran
 bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
   if (a.aff) return false;  // no folded-BN staging
-  if (!conv_halo_mode()) return false;
   if (a.sh != 1 || a.sw != 1 || a.res || a.fp8) return false;
   const int ntap = a.R * a.S;
   if (ntap < 3 || ntap > HALO_MAXTAP || a.C % 64 || a.K % 8 || a.ldc % 8) return false;
   if (a.x_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
-  if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;  // small: GEMMs
-  // default selection (same-box A/B, bench/halo_ab.py, profiles/r04_halo_ab.txt): the halo
-  // forward wins where the GEMM kernels run 64-wide output tiles (ResNet layer1 3×3, 683 → 520 µs
-  // at b1024; DeepLab conv1_2) and loses ~10 % to the LDS-DMA implicit GEMM on wider outputs
-  if (conv_halo_mode() == 1 && a.K > 64) return false;
   HaloGeom g{};
   g.N = a.N; g.Hi = a.H; g.Wi = a.W; g.Ci = a.C;
   g.Ho = a.Ho; g.Wo = a.Wo; g.Co = a.K;
@@ -895,13 +884,11 @@ bool conv_fwd_halo(const ConvArgs& a, hipStream_t st) {
 // bench/dgrad_paths.py).  *fused: the BN-backward statistics were written.
 bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused) {
   if (fused) *fused = false;
-  if (!conv_halo_mode() || a.aff || a.fp8 || a.sh != 1 || a.sw != 1) return false;
+  if (a.aff || a.fp8 || a.sh != 1 || a.sw != 1) return false;
   const int ntap = a.R * a.S;
   if (ntap < 3 || ntap > HALO_MAXTAP || a.C % 64 || a.K % 8 || a.ldc % 8) return false;
   if (a.mask && a.ldc % 64) return false;
   if (a.x_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
-  if (conv_halo_mode() != 2 && (long)a.N * a.Ho * a.Wo < 4096) return false;
-  if (conv_halo_mode() == 1 && a.K > 64) return false;
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
   // the statistics form lost to the DGRAD kernel's 256×64 tiles (ResNet layer1 3×3, b1024: 700
   // vs 607 µs — profiles/r05_dgrad_as_fwd.txt): plain / join only
@@ -932,15 +919,10 @@ bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused) {
 bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused) {
   if (fused) *fused = false;
   if (a.aff) return false;  // the folded-BN mask: LDS-DMA statistics epilogue only
-  if (!conv_halo_mode()) return false;
   if (a.sh != 1 || a.sw != 1 || a.fp8 || a.dg_masked) return false;
   const int ntap = a.R * a.S;
   if (ntap < 3 || ntap > HALO_MAXTAP || a.K % 64 || a.C % 8 || a.ldc % 8) return false;
   if (a.dy_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
-  if (conv_halo_mode() != 2 && (long)a.N * a.H * a.W < 4096) return false;
-  // the implicit-GEMM input gradients win on every measured shape (bench/halo_ab.py): the halo
-  // dgrad runs only when forced (mode 2)
-  if (conv_halo_mode() == 1) return false;
   const bool stats = a.stats && a.bn_x;
   if (a.mask && a.ldc % 64) return false;  // mask slabs: 64-column rows
   HaloGeom g{};

@@ -128,15 +128,17 @@ bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStre
 // stride-1 input gradient as the forward conv of dy with the flipped filter w_flip [C][R][S][K]
 // (conv_glds.hip): true when it ran (*fused: the BN-backward statistics were written); false =
 // not eligible, nothing launched
-bool conv_dgrad_as_fwd(const ConvArgs& a, const bf16_t* w_flip, uint32_t w_flip_bytes,
+bool conv_dgrad_as_fwd(const ConvArgs& a, const bf16_t* w_flip, uint32_t w_flip_bytes, int cfg,
                        hipStream_t st, bool* fused);
 // w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c] (bf16)
 void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, int C,
                              hipStream_t st);
 void conv_set_pc(int on);
-bool conv_fwd_glds(const ConvArgs& a, hipStream_t st);
+// route executors (conv_route.h): true when they ran, false = not eligible, nothing launched
+bool conv_fwd_glds(const ConvArgs& a, int cfg, hipStream_t st);
+bool conv_fwd_pc_run(const ConvArgs& a, hipStream_t st);
 // halo-tiled direct conv (conv_halo.hip) for stride-1 R×S filters, Cin % 64 == 0: true when it
-// ran (TDL_HALO=0 disables); the dgrad sets *fused when a.stats was filled
+// ran (TDL_HALO=0 turns its route rows off); the dgrad sets *fused when a.stats was filled
 int conv_halo_mode();
 void conv_set_halo_mode(int mode);  // -1: environment; 2: every eligible problem (tests)
 bool conv_fwd_halo(const ConvArgs& a, hipStream_t st);
@@ -148,8 +150,10 @@ bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused);
 bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p);
 void conv_wgrad_halo_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 // *fused: set to whether a.stats was filled (stride-1 FASTK problems only)
-bool conv_dgrad_glds(const ConvArgs& a, long m_total, hipStream_t st, bool* fused = nullptr);
-bool conv_wgrad_glds_plan(const ConvArgs& a, WgradPlan* p);
+bool conv_dgrad_glds(const ConvArgs& a, int cfg, hipStream_t st, bool* fused = nullptr);
+// can the LDS-DMA DGRAD epilogue fuse this problem's BN-backward statistics (classes built)?
+bool dgrad_stats_fusable(const ConvArgs& a);
+bool conv_wgrad_glds_plan(const ConvArgs& a, int cfg, WgradPlan* p);
 void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 // fp8 (OCP e4m3) forward conv: a.x / a.w point at e4m3 bytes, a.scale_x / a.scale_w at their fp32 scales
 void conv_fwd_fp8_launch(const ConvArgs& a, hipStream_t st);

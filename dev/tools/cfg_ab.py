@@ -12,9 +12,10 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
+from route_ab import glds_cfg  # noqa: E402
 
 SHAPES = ["64,13,512,512,3,1,2,2", "64,13,1024,256,1,1,0", "64,13,512,2048,1,1,0",
           "64,13,2048,512,1,1,0", "64,13,264,264,3,1,1", "64,13,256,256,3,1,4,4",
@@ -46,7 +47,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     dev = torch.device("cuda")
-    env = "TDL_GLDS_CFG_FWD" if a.op == "fwd" else "TDL_GLDS_CFG_DGRAD"
     for shp in a.shapes.split(";"):
         v = [int(t) for t in shp.split(",")]
         N, H, Cin, Cout, k, s, p = v[:7]
@@ -62,16 +62,16 @@ def main():
         res = {c: [] for c in cfgs}
         for _ in range(a.rounds):
             for c in cfgs:
-                os.environ.pop(env, None)
+                glds_cfg(a.op, None)
                 os.environ["TDL_GLDS_SLOTS"] = "512" if c == "3" else "256"
                 if c == "reg":
                     ext().conv_set_glds_mode(0)
                 else:
                     ext().conv_set_glds_mode(2)
-                    os.environ[env] = c
+                    glds_cfg(a.op, c)
                 res[c].append(timed(fn))
         ext().conv_set_glds_mode(-1)
-        os.environ.pop(env, None)
+        glds_cfg(a.op, None)
         os.environ["TDL_GLDS_SLOTS"] = "256"
         best = min(res, key=lambda c: min(res[c]))
         print(f"{a.op} {shp:24s} " + " | ".join(f"cfg{c} {min(t):6.1f}us {flop / min(t) / 1e6:4.0f}TF"

@@ -6,7 +6,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import fp8 as F8  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402

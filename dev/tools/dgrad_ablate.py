@@ -13,9 +13,10 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
+from route_ab import glds_cfg  # noqa: E402
 
 # (N, H, Cin, Cout, k, stride, pad): the conv whose dgrad writes dx [N, H, H, Cin]
 SHAPES = ["256,56,256,64,1,1,0", "256,28,512,128,1,1,0", "256,14,1024,256,1,1,0",
@@ -65,10 +66,10 @@ def main():
         for _ in range(a.rounds):
             for name, dbg, fn in variants:
                 cfg = dbg if isinstance(dbg, str) else None
-                os.environ.pop("TDL_GLDS_CFG_DGRAD", None)
+                glds_cfg("dgrad", None)
                 os.environ["TDL_GLDS_SLOTS"] = "256"
                 if cfg:
-                    os.environ["TDL_GLDS_CFG_DGRAD"] = cfg[3:]
+                    glds_cfg("dgrad", cfg[3:])
                     os.environ["TDL_GLDS_SLOTS"] = "512"
                     dbg = 0
                 os.environ["TDL_CONV_DBG"] = str(dbg)

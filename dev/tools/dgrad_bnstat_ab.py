@@ -15,9 +15,10 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import bn as B  # noqa: E402
+from route_ab import glds_cfg, RF_STATS, RF_JOIN  # noqa: E402
 
 # (name, H, dx channels C, dy channels K, k, join): the BN whose output is the conv input has C
 # channels; join = the block-input gradient join (accumulate into the residual gradient + mask)
@@ -54,7 +55,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default="")
     ap.add_argument("--cfgs", default="", help="comma list of fused-dgrad tile configs to time "
-                    "(TDL_GLDS_CFG_DGSTAT[_J]); default: the built-in choice")
+                    "(route_ab.glds_cfg on the statistics rows); default: the table's choice")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -105,17 +106,13 @@ def main():
                        s1=float((s1 - reda[1]).abs().max() / (reda[1].abs().max() + 1e-6)))
         copy_us = timeit(lambda: buf.copy_(prev), a.iters) if join else 0.0
         cfgs = [c for c in a.cfgs.split(",") if c] or [None]
-        env = "TDL_GLDS_CFG_DGSTAT_J" if join else "TDL_GLDS_CFG_DGSTAT"
         ta, tb = 0.0, {c: 0.0 for c in cfgs}
         for _ in range(3):  # interleaved
             ta += timeit(run_a, a.iters)
             for c in cfgs:
-                if c is None:
-                    os.environ.pop(env, None)
-                else:
-                    os.environ[env] = c
+                glds_cfg("dgrad", c, RF_STATS | (RF_JOIN if join else 0))
                 tb[c] += timeit(run_b, a.iters)
-        os.environ.pop(env, None)
+        glds_cfg("dgrad", None, RF_STATS)
         ta = ta / 3 - copy_us
         tb = {c: v / 3 - copy_us for c, v in tb.items()}
         best = min(tb, key=tb.get)

@@ -5,7 +5,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
 

@@ -2,11 +2,12 @@
 cosine of the parameter gradients after the e5m2 scalers warmed up.
   python dev/tools/fp8_dgrad_check.py [--depth 18] [--train-bn]"""
 import argparse
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd import models  # noqa: E402
 from tensorflowdistributedlearning_amd.engine.trainer import Trainer  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy  # noqa: E402

@@ -1,11 +1,12 @@
 """Loss curves of the same ResNet on a fixed batch: bf16, fp8 forward, fp8 forward + fp8 dgrad.
   python dev/tools/fp8_train_curve.py [--depth 50] [--batch 64] [--size 128] [--steps 12] [--lr 0.01]"""
 import argparse
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd import models  # noqa: E402
 from tensorflowdistributedlearning_amd.engine.trainer import Trainer  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy  # noqa: E402

@@ -14,7 +14,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 
 SHAPES = ["256,14,256,256,3,1,1", "256,28,128,128,3,1,1", "256,56,64,256,1,1,0"]

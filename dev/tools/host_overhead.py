@@ -14,7 +14,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd import models  # noqa: E402
 from tensorflowdistributedlearning_amd.engine.trainer import Trainer  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import softmax_cross_entropy, lovasz_hinge  # noqa: E402

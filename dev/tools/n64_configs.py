@@ -1,5 +1,5 @@
 """A/B of conv kernel configurations for the 64-output-channel ResNet-50 layer1 convs (fwd and
-dgrad): register-staged (reg) vs LDS-DMA configs (TDL_GLDS_CFG_*: 1 = 256x64/4 waves,
+dgrad): register-staged (reg) vs LDS-DMA configs (route_ab.glds_cfg: 1 = 256x64/4 waves,
 4 = 256x64/8 waves, 5 = 128x64/4 waves/4 stages).  Interleaved rounds, min over rounds.
   python dev/tools/n64_configs.py [--batch 256]"""
 import argparse
@@ -8,9 +8,10 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
+from route_ab import glds_cfg  # noqa: E402
 
 SHAPES = [(56, 64, 64, 3, 1, 1), (56, 64, 64, 1, 1, 0), (56, 256, 64, 1, 1, 0),
           (28, 128, 128, 3, 1, 1)]
@@ -45,11 +46,7 @@ def main():
             for name, mode, cfg in (("reg", 0, None), ("g1", 2, 1), ("g4", 2, 4), ("g5", 2, 5)):
                 ext().conv_set_glds_mode(mode)
                 for op in ("fwd", "dgrad"):
-                    key = "TDL_GLDS_CFG_FWD" if op == "fwd" else "TDL_GLDS_CFG_DGRAD"
-                    if cfg is None:
-                        os.environ.pop(key, None)
-                    else:
-                        os.environ[key] = str(cfg)
+                    glds_cfg(op, cfg)
                     fn = (lambda: C.conv_fwd(x, w, g)) if op == "fwd" else \
                         (lambda: C.conv_dgrad(dy, w, x.shape, g))
                     res.setdefault((name, op), []).append(t(fn))

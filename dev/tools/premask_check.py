@@ -3,11 +3,12 @@ agreement per parameter, against the run-to-run noise floor of the baseline path
 
   python dev/tools/premask_check.py [--depth 18] [--batch 8] [--size 64] [--eval-bn]"""
 import argparse
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd import models  # noqa: E402
 from tensorflowdistributedlearning_amd.ops import gradjoin  # noqa: E402
 

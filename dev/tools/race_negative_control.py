@@ -2,7 +2,7 @@
 final-callback join disabled, reading p.grad right after backward must show a mismatch (proves
 the stalled-side-stream test can detect a missing join)."""
 import sys, os
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from tensorflowdistributedlearning_amd import models, _native
 from tensorflowdistributedlearning_amd.ops import streams

@@ -8,10 +8,11 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench"))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
+from route_ab import glds_cfg  # noqa: E402
 from conv_bench import timeit  # noqa: E402
 
 
@@ -36,7 +37,7 @@ def main():
         for cfg in cfgs:
             ext().conv_set_glds_mode(mode)
             if cfg:
-                os.environ["TDL_GLDS_CFG_FWD"] = cfg
+                glds_cfg("fwd", cfg)
             y = C.conv_fwd(t, w, g)
             if ref is None:
                 ref = y.float()
@@ -46,19 +47,19 @@ def main():
             print(f"mode {mode} cfg {cfg}: fwd {tf:7.1f} us ({flop / tf / 1e6:4.0f} TF, "
                   f"{(t.numel() + y.numel()) * 2 / tf / 1e6:.2f} TB/s min-bytes) wgrad {tw:7.1f} us "
                   f"({flop / tw / 1e6:4.0f} TF)  err {err:.2e}", flush=True)
-            os.environ.pop("TDL_GLDS_CFG_FWD", None)
+            glds_cfg("fwd", None)
     ext().conv_set_glds_mode(-1)
     # weight gradient: register-staged 64x128 tiles (dy read twice) vs the LDS-DMA 64x256 tile
     for v in ("0", "1", "0", "1"):
-        os.environ["TDL_GLDS_STEM_WGRAD"] = v
+        ext().conv_route_set("wgrad.glds.stem", on=int(v))
         dw = C.conv_wgrad(dy, t, tuple(w.shape), g)
         tw = timeit(lambda: C.conv_wgrad(dy, t, tuple(w.shape), g))
         if v == "0":
             dw0 = dw.float()
         err = ((dw.float() - dw0).abs().max() / dw0.abs().max()).item()
-        print(f"stem wgrad TDL_GLDS_STEM_WGRAD={v}: {tw:7.1f} us ({flop / tw / 1e6:4.0f} TF) "
+        print(f"stem wgrad wgrad.glds.stem on={v}: {tw:7.1f} us ({flop / tw / 1e6:4.0f} TF) "
               f"err vs register-staged {err:.2e}", flush=True)
-    os.environ.pop("TDL_GLDS_STEM_WGRAD", None)
+    ext().conv_route_reset()
 
 
 if __name__ == "__main__":

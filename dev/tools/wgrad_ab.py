@@ -10,9 +10,10 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from tensorflowdistributedlearning_amd.ops import conv as C  # noqa: E402
 from tensorflowdistributedlearning_amd.ops.common import ext  # noqa: E402
+from route_ab import glds_cfg  # noqa: E402
 
 # (H, Cin, Cout, k, stride, pad[, dilation]) of the conv whose weight gradient is taken (input H×H×Cin)
 SHAPES = ["56,64,64,3,1,1", "28,128,128,3,1,1", "56,128,128,3,2,1", "14,256,256,3,1,1",
@@ -31,15 +32,15 @@ def main():
     N = a.batch
     variants = {
         "default": (1, {}), "gemm": (0, {}),
-        "glds0": (2, {"TDL_GLDS_CFG_WGRAD": "0"}), "glds2": (2, {"TDL_GLDS_CFG_WGRAD": "2"}),
-        "glds3": (2, {"TDL_GLDS_CFG_WGRAD": "3", "TDL_GLDS_SLOTS": "512"}),
-        "glds1": (2, {"TDL_GLDS_CFG_WGRAD": "1"}), "glds5": (2, {"TDL_GLDS_CFG_WGRAD": "5"}),
-        "glds0m8": (2, {"TDL_GLDS_CFG_WGRAD": "0", "TDL_GLDS_WGRAD_MINSTEPS": "8"}),
-        "glds0m32": (2, {"TDL_GLDS_CFG_WGRAD": "0", "TDL_GLDS_WGRAD_MINSTEPS": "32"}),
-        "glds2m8": (2, {"TDL_GLDS_CFG_WGRAD": "2", "TDL_GLDS_WGRAD_MINSTEPS": "8"}),
+        "glds0": (2, {"cfg": "0"}), "glds2": (2, {"cfg": "2"}),
+        "glds3": (2, {"cfg": "3", "TDL_GLDS_SLOTS": "512"}),
+        "glds1": (2, {"cfg": "1"}), "glds5": (2, {"cfg": "5"}),
+        "glds0m8": (2, {"cfg": "0", "TDL_GLDS_WGRAD_MINSTEPS": "8"}),
+        "glds0m32": (2, {"cfg": "0", "TDL_GLDS_WGRAD_MINSTEPS": "32"}),
+        "glds2m8": (2, {"cfg": "2", "TDL_GLDS_WGRAD_MINSTEPS": "8"}),
     }
     names = a.variants.split(",")
-    keys = sorted({k for _, e in variants.values() for k in e})
+    keys = sorted({k for _, e in variants.values() for k in e if k != "cfg"})
     for shp in a.shapes.split(";"):
         v = [int(t) for t in shp.split(",")]
         H, Cin, Cout, k, s, p = v[:6]
@@ -57,7 +58,8 @@ def main():
                 mode, env = variants[n]
                 for kk in keys:
                     os.environ.pop(kk, None)
-                os.environ.update(env)
+                os.environ.update({kk: vv for kk, vv in env.items() if kk != "cfg"})
+                glds_cfg("wgrad", env.get("cfg"))
                 ext().conv_set_glds_mode(mode)
                 C.conv_wgrad(dy, x, out.shape, g, out=out)
                 torch.cuda.synchronize()
@@ -75,6 +77,7 @@ def main():
                 res[n].append(e0.elapsed_time(e1) / 10 * 1e3)
         for kk in keys:
             os.environ.pop(kk, None)
+        glds_cfg("wgrad", None)
         ext().conv_set_glds_mode(-1)
         best = min(res, key=lambda n: min(res[n]))
         print(f"{shp:18s} " + " | ".join(f"{n} {min(v):6.1f}us {flop / min(v) / 1e6:4.0f}TF"

@@ -147,7 +147,7 @@ def test_bench_consumes_bench_config(tmp_path):
     ns = argparse.Namespace(config=str(tmp_path / "b.json"), model=None, batch=None,
                             image_size=None, steps=3, warmup=None, lr=None, bucket_mb=None,
                             first_bucket_mb=None, optimizer=None, dtype=None, fp8=False,
-                            fp8_dgrad=False, graph=False)
+                            fp8_dgrad=False, graph=False, grad_dtype=None)
     bc = bench.bench_config(ns)
     assert (bc.arch, bc.batch, bc.dtype, bc.graph, bc.steps) == ("resnet152", 128, "fp8", True, 3)
     assert bc.optimizer == "sgd_momentum" and bc.loss == "softmax_ce" and bc.lr == 0.1
