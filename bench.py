@@ -142,7 +142,8 @@ def main():
                          "forward e4m3 activations x e4m3 weights; weight and input gradients "
                          "stay bf16")
     ap.add_argument("--fp8-dgrad", action="store_true",
-                    help="with --fp8: also the input gradients on fp8 (e5m2 x e4m3; experimental)")
+                    help="with --fp8: the input gradients on fp8 too (e5m2 x e4m3) — the default "
+                         "unless TDL_FP8_DGRAD=0")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step as a HIP graph and replay it (removes "
                          "host launch overhead in launch-bound configs; with N>1 the bucketed "
@@ -222,9 +223,11 @@ def main():
         model = models.build(bc.arch, num_classes=1000)
         if bc.dtype == "fp8":
             models.enable_fp8(model, dgrad=bc.fp8_dgrad or None)
-            fp8_desc = ("fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad + BN)"
-                        if bc.fp8_dgrad else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / "
-                        "wgrad + BN)")
+            dg = any(getattr(m, "emit_fp8_bwd", False) for m in model.modules())
+            st = int(os.environ.get("TDL_FP8_BF16_STAGES", "2"))
+            fp8_desc = (("fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad + BN"
+                         if dg else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / wgrad + BN")
+                        + (f"; stages 1-{st} bf16)" if st > 0 else ")"))
         tr = Trainer(model, softmax_cross_entropy, dev, _opt(bc.optimizer), _opt_kw(bc), ctx=ctx,
                      bucket_mb=bc.bucket_mb, first_bucket_mb=bc.first_bucket_mb,
                      profile_phases=args.profile_phases, lowp_dtype=lowp,

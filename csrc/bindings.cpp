@@ -1518,6 +1518,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fold_weight", &bn_fold_weight, py::arg("w"), py::arg("coef"), py::arg("wout"),
         py::arg("bias_in"), py::arg("bias_out"));
   m.def("scale_cols", &scale_cols, py::arg("dw"), py::arg("a"));
+  m.def("fp8_set_policy", &fp8_set_policy, py::arg("margin_e4m3") = -1.0, py::arg("margin_e5m2") = -1.0,
+        py::arg("decay") = -1.0,
+        "fp8 delayed scaling: scale = margin * amax / fp8_max, amax history slot <- max(step amax, "
+        "decay * previous) at each roll; < 0: environment (TDL_FP8_MARGIN, TDL_FP8_MARGIN_E5M2, "
+        "TDL_FP8_AMAX_DECAY)");
+  m.def("fp8_policy", []() { auto p = fp8_policy(); return py::make_tuple(p.margin_e4m3, p.margin_e5m2, p.decay); });
   m.def("conv_set_pc", &conv_set_pc, "wave-specialised producer/consumer forward (-1: env)");
   // ---- the conv route table (kernels/conv_route.h)
   m.def("conv_route_table", []() {

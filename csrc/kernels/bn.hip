@@ -392,7 +392,8 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
                                                        float* __restrict__ scale_out,
                                                        float* __restrict__ amax_out,
                                                        float* __restrict__ amax_zero,
-                                                       uint8_t* __restrict__ mask, int ldy_v) {
+                                                       uint8_t* __restrict__ mask, int ldy_v,
+                                                       float margin) {
   // ldy_v: y's row stride in 8-element vectors (C/8 contiguous; wider when y is a channel slice
   // of a concat buffer — the concat-free ASPP / decoder)
   float inv8 = 0.f, vmax = 0.f;
@@ -400,7 +401,7 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
   if (amax_out) {
     // a zero (or never-set) previous |y|max falls back to unit scale: the e4m3 copy is always
     // written when requested, so a consumer never reads uninitialised bytes
-    const float ap0 = amax_read(amax_prev);
+    const float ap0 = amax_read(amax_prev) * margin;  // (fp8_policy: headroom over the history)
     const float ap = ap0 > 0.f ? ap0 : 448.f;
     emit8 = y8 != nullptr;
     inv8 = 448.f / ap;
@@ -513,23 +514,23 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
     float* __restrict__ dbeta, long nvec, int C, float inv_count, int relu,
     uint8_t* __restrict__ dx8, const float* __restrict__ amax_prev, float* __restrict__ scale_out,
     float* __restrict__ amax_out, float* __restrict__ amax_zero, int red_raw, int ldd_v,
-    const bf16_t* __restrict__ dadd) {
+    const bf16_t* __restrict__ dadd, float margin) {
   // dadd (optional, shaped like dx): another consumer's gradient of x added to dx in this pass
   // (a DeepLab unit input feeds its pre-activation BN and, as the identity shortcut, the
   // residual of conv3's epilogue) instead of autograd summing the two
   // ldd_v: dy's row stride in 8-element vectors (a channel slice of a concat gradient when > C/8)
   // red_raw: red = (Σg, Σg·x) accumulated by the producing dgrad's epilogue (conv_common.h);
   // Σg·x̂ = invstd·(Σg·x − mean·Σg) here
-  // optional e5m2 side output of dx (fp8 dgrad of the producing conv; delayed scaling with 4×
-  // headroom over the previous call's |dx|max: gradients can grow step to step, e5m2 has 30
-  // binades to spare, a clipped gradient biases the update)
+  // optional e5m2 side output of dx (fp8 dgrad of the producing conv; delayed scaling with
+  // `margin` (fp8_policy, default 16×) headroom over the previous |dx|max: gradients can grow step
+  // to step, e5m2 has 30 binades to spare, a clipped gradient biases the update)
   float inv8 = 0.f, vmax = 0.f;
   bool emit8 = false;
   if (amax_out) {
     // a zero previous |dx|max (e.g. a step whose loss gradient was exactly zero) falls back to
     // unit scale: dx8 is always written when requested (values clamped to ±57344), never left
     // as uninitialised bytes behind a zero scale
-    const float ap0 = amax_read(amax_prev) * 4.f;
+    const float ap0 = amax_read(amax_prev) * margin;
     const float ap = ap0 > 0.f ? ap0 : 57344.f;
     emit8 = dx8 != nullptr;
     inv8 = 57344.f / ap;
@@ -711,7 +712,7 @@ void bn_apply_launch(const bf16_t* x, const float* coef, const bf16_t* res, bf16
                  : (u == 2 ? apply_vec_kernel<2> : u == 4 ? apply_vec_kernel<4> : apply_vec_kernel<1>);
     hipLaunchKernelGGL(k, dim3(ew_blocks(n / 8, C / 8, u)), dim3(NT), 0, st, x, coef, res, y, n / 8, C,
                        relu ? 1 : 0, y8, amax_prev, scale_out, amax_out, amax_zero, mask,
-                       (int)(ldy / 8));
+                       (int)(ldy / 8), fp8_policy().margin_e4m3);
   } else {
     hipLaunchKernelGGL(apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, x, coef, res, y, n,
                        C, relu ? 1 : 0);
@@ -765,7 +766,7 @@ void bn_bwd_apply_launch(const bf16_t* dy, const bf16_t* y, const bf16_t* x, con
                    : bwd_apply_vec_kernel<false, 1>;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(NT), 0, st, dy, y, x, coef, red, gamma, dx, dres, dgamma,
                        dbeta, n / 8, C, 1.f / count, relu, dx8, amax_prev, scale_out, amax_out,
-                       amax_zero, red_raw ? 1 : 0, (int)(ldd / 8), dadd);
+                       amax_zero, red_raw ? 1 : 0, (int)(ldd / 8), dadd, fp8_policy().margin_e5m2);
   } else {
     hipLaunchKernelGGL(bwd_apply_scalar_kernel, dim3(ew_blocks(n)), dim3(NT), 0, st, dy, y, x, coef,
                        red, gamma, dx, dres, dgamma, dbeta, n, C, 1.f / count, relu,

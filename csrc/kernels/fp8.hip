@@ -50,8 +50,8 @@ __global__ void __launch_bounds__(NT) quantize_e5m2_kernel(const bf16_t* __restr
                                                            float* __restrict__ meas,
                                                            float* __restrict__ clr,
                                                            float* __restrict__ scale_out,
-                                                           uint8_t* __restrict__ y) {
-  const float am = fmaxf(amax_read(prev), 1e-30f);
+                                                           uint8_t* __restrict__ y, float margin) {
+  const float am = fmaxf(amax_read(prev) * margin, 1e-30f);
   const float inv = E5M2_MAX / am;
   if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = am / E5M2_MAX;
   if (clr) amax_clear(clr);
@@ -114,8 +114,8 @@ __global__ void __launch_bounds__(NT) quantize_kernel(const bf16_t* __restrict__
                                                       const float* __restrict__ prev,
                                                       float* __restrict__ meas, float* __restrict__ clr,
                                                       float* __restrict__ scale_out,
-                                                      uint8_t* __restrict__ y) {
-  const float am = fmaxf(amax_read(prev), 1e-12f);
+                                                      uint8_t* __restrict__ y, float margin) {
+  const float am = fmaxf(amax_read(prev) * margin, 1e-12f);
   const float inv = E4M3_MAX / am;
   if (blockIdx.x == 0 && threadIdx.x == 0 && scale_out) *scale_out = am / E4M3_MAX;
   if (clr) amax_clear(clr);
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(NT) multi_quantize_kernel(const bf16_t* __rest
                                                             const long* __restrict__ chunks,
                                                             float* __restrict__ rings,
                                                             float* __restrict__ scales, int phase,
-                                                            int prime) {
+                                                            int prime, float margin) {
   const long* c = chunks + 4 * (long)blockIdx.x;
   const long seg = c[0], start = c[1], n16 = c[2] / 16;
   float* ring = rings + seg * 3 * AMAX_SLOT;
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(NT) multi_quantize_kernel(const bf16_t* __rest
     amax_publish(prev, m);
     return;
   }
-  const float am = fmaxf(amax_read(prev), 1e-12f);
+  const float am = fmaxf(amax_read(prev) * margin, 1e-12f);
   const float inv = E4M3_MAX / am;
   if (c[3] && threadIdx.x == 0) scales[seg] = am / E4M3_MAX;
   if (c[3] && threadIdx.x < AMAX_SPREAD)
@@ -202,12 +202,15 @@ __global__ void dequantize_kernel(const uint8_t* __restrict__ y, long n, const f
 }
 
 // End-of-step roll of every delayed-scaling amax ring (graph-capturable: the slot roles are fixed,
-// the data moves): slot 0 (read by the next call) ← slot 1 (accumulated by this step's call),
+// the data moves): slot 0 (read by the next call) ← max(slot 1 (accumulated by this step's call),
+// decay · slot 0) — an exponentially forgetting amax history: with decay > 0 a step whose |x|max
+// dips does not shrink the scale at once, so the next step's larger values are not clipped —
 // slot 1 ← 0.  rings: n ring base addresses (fp32 [3][AMAX_SLOT] each)
-__global__ void __launch_bounds__(NT) roll_kernel(const unsigned long long* __restrict__ rings) {
+__global__ void __launch_bounds__(NT) roll_kernel(const unsigned long long* __restrict__ rings,
+                                                  float decay) {
   float* r = (float*)rings[blockIdx.x];
   for (int t = threadIdx.x; t < AMAX_SLOT; t += NT) {
-    r[t] = r[AMAX_SLOT + t];
+    r[t] = fmaxf(r[AMAX_SLOT + t], decay * r[t]);
     r[AMAX_SLOT + t] = 0.f;
   }
 }
@@ -216,9 +219,33 @@ inline int grid_for(long n) { return (int)std::min<long>(4096, std::max<long>(1,
 
 }  // namespace
 
+// delayed-scaling policy (TDL_FP8_MARGIN / TDL_FP8_MARGIN_E5M2 / TDL_FP8_AMAX_DECAY, or
+// fp8_set_policy): scale = margin · amax_history / fp8_max.  Defaults from the memorisation sweep
+// (dev/tools/fp8_policy_sweep.py, profiles/r05_fp8_numerics.txt): e4m3 margin 1 (2 was worse:
+// a binade of precision lost at the bottom for no clipping saved), e5m2 margin 16 (loss tail
+// 0.023 vs 0.030 at 4: e5m2's 32 binades afford it, a clipped gradient biases the update), no
+// amax decay (0.9 did not help)
+static float g_policy[3] = {-1.f, -1.f, -1.f};
+static float env_f(const char* name, float dflt) {
+  const char* e = getenv(name);
+  return e ? (float)atof(e) : dflt;
+}
+Fp8Policy fp8_policy() {
+  static const Fp8Policy env{env_f("TDL_FP8_MARGIN", 1.f), env_f("TDL_FP8_MARGIN_E5M2", 16.f),
+                             env_f("TDL_FP8_AMAX_DECAY", 0.f)};
+  return Fp8Policy{g_policy[0] >= 0.f ? g_policy[0] : env.margin_e4m3,
+                   g_policy[1] >= 0.f ? g_policy[1] : env.margin_e5m2,
+                   g_policy[2] >= 0.f ? g_policy[2] : env.decay};
+}
+void fp8_set_policy(float margin_e4m3, float margin_e5m2, float decay) {
+  g_policy[0] = margin_e4m3;
+  g_policy[1] = margin_e5m2;
+  g_policy[2] = decay;
+}
+
 void fp8_roll_launch(const unsigned long long* rings, int n, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(roll_kernel, dim3(n), dim3(NT), 0, st, rings);
+  hipLaunchKernelGGL(roll_kernel, dim3(n), dim3(NT), 0, st, rings, fp8_policy().decay);
 }
 
 void fp8_amax_launch(const bf16_t* x, long n, float* slot, hipStream_t st) {
@@ -230,21 +257,21 @@ void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas
                          float* scale_out, uint8_t* y, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(quantize_kernel, dim3(grid_for(n / 16)), dim3(NT), 0, st, x, n / 16, prev, meas,
-                     clr, scale_out, y);
+                     clr, scale_out, y, meas ? fp8_policy().margin_e4m3 : 1.f);  // (JIT: exact)
 }
 
 void fp8_multi_quantize_launch(const bf16_t* src, uint8_t* dst, const long* chunks, int nchunks,
                                float* rings, float* scales, int phase, bool prime, hipStream_t st) {
   if (nchunks <= 0) return;
   hipLaunchKernelGGL(multi_quantize_kernel, dim3(nchunks), dim3(NT), 0, st, src, dst, chunks, rings,
-                     scales, phase, prime ? 1 : 0);
+                     scales, phase, prime ? 1 : 0, fp8_policy().margin_e4m3);
 }
 
 void fp8_quantize_e5m2_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,
                               float* scale_out, uint8_t* y, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(quantize_e5m2_kernel, dim3(grid_for(n / 16)), dim3(NT), 0, st, x, n / 16, prev,
-                     meas, clr, scale_out, y);
+                     meas, clr, scale_out, y, meas ? fp8_policy().margin_e5m2 : 1.f);
 }
 
 void fp8_dequantize_e5m2_launch(const uint8_t* y, long n, const float* scale, float* out,

@@ -160,6 +160,13 @@ void conv_fwd_fp8_launch(const ConvArgs& a, hipStream_t st);
 void fp8_amax_launch(const bf16_t* x, long n, float* slot, hipStream_t st);
 // end-of-step roll of n amax rings (device pointer table): slot0 ← slot1, slot1 ← 0
 void fp8_roll_launch(const unsigned long long* rings, int n, hipStream_t st);
+// delayed-scaling policy: scale = margin · amax / fp8_max (e4m3 activations and weights; e5m2
+// gradients), amax slot 0 ← max(this step's, decay · previous) at each roll
+struct Fp8Policy {
+  float margin_e4m3, margin_e5m2, decay;
+};
+Fp8Policy fp8_policy();
+void fp8_set_policy(float margin_e4m3, float margin_e5m2, float decay);  // < 0: environment
 // prev: amax slot giving the scale; meas (optional): slot accumulating |x|max; clr (optional):
 // slot cleared for the next call
 void fp8_quantize_launch(const bf16_t* x, long n, const float* prev, float* meas, float* clr,

@@ -16,22 +16,29 @@ _REGISTRY = {
 }
 
 
-def enable_fp8(model, fuse_bn=True, dgrad=None):
+def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None):
     """fp8 GEMMs for every bias-free conv whose input channels are a multiple of 16 (the
     3-channel stem and biased heads stay bf16): the forward on e4m3 activations × e4m3 weights
     and — with ``dgrad`` — the input gradient on e5m2 output gradients × e4m3 weights (convs with
     K % 128 == 0 output channels that feed a BN; the weight gradient stays bf16).  With
-    ``fuse_bn`` the BN layers write the e4m3 copy of their output in the same pass (scale from the
-    previous step's |y|max), so those conv inputs need no separate quantisation pass; the BN after
-    an fp8 conv likewise writes the e5m2 copy of its input gradient in the backward apply.
-    Returns the conv count.
+    ``fuse_bn`` the BN layers whose output feeds an fp8 conv write the e4m3 copy of it in the same
+    pass (scale from the previous step's |y|max), so those conv inputs need no separate
+    quantisation pass; the BN after an fp8 conv likewise writes the e5m2 copy of its input
+    gradient in the backward apply.  Returns the fp8 conv count.
 
-    The fp8 dgrad is opt-in (``dgrad=True`` or ``TDL_FP8_DGRAD=1``): the forward-only mode is the
-    one whose loss curve is pinned against bf16 (tests/test_train_gpu.py::test_fp8_loss_curve_*)."""
+    ``bf16_stages`` (ResNets; default ``TDL_FP8_BF16_STAGES`` or 2): the first residual stages
+    keep bf16 GEMMs.  On the memorisation curve (dev/tools/fp8_policy_sweep.py,
+    profiles/r05_fp8_numerics.txt) their quantisation noise dominates: last-10-step loss tail
+    bf16 0.0088, every stage fp8 0.057 (6.5×), stage 1 bf16 0.025 (2.8×), stages 1–2 bf16
+    0.015 (1.7×, fp8 dgrad included).  ResNet-152 keeps 39 of its 50 blocks on fp8.
+
+    The fp8 dgrad defaults on (``TDL_FP8_DGRAD=0`` or ``dgrad=False`` turns it off)."""
     import os
     from .layers import Conv2d, BatchNorm, ConvBN
     if dgrad is None:
-        dgrad = os.environ.get("TDL_FP8_DGRAD", "0") == "1"
+        dgrad = os.environ.get("TDL_FP8_DGRAD", "1") == "1"
+    if bf16_stages is None:
+        bf16_stages = int(os.environ.get("TDL_FP8_BF16_STAGES", "2"))
     n = 0
     for m in model.modules():
         if isinstance(m, Conv2d) and m.bias is None and m._cin_store % 16 == 0:
@@ -39,11 +46,44 @@ def enable_fp8(model, fuse_bn=True, dgrad=None):
             n += 1
         elif isinstance(m, BatchNorm) and fuse_bn:
             m.emit_fp8 = True  # conv inputs arrive pre-quantised (delayed scaling, ops/bn.py)
+    stages = [getattr(model, f"layer{i}", None) for i in (1, 2, 3, 4)]
+    if isinstance(model, ResNet) and all(s is not None for s in stages):
+        n = _resnet_fp8_plan(model, stages, bf16_stages, fuse_bn)
     if dgrad:
         for m in model.modules():
             if isinstance(m, ConvBN) and getattr(m.conv, "fp8", False):
                 m.bn.emit_fp8_bwd = True  # e5m2 dy for the conv's fp8 dgrad (ops/conv.py)
     return n
+
+
+def _resnet_fp8_plan(model, stages, bf16_stages, fuse_bn):
+    """fp8 convs from stage ``bf16_stages`` on; a BN emits its e4m3 copy only where an fp8 conv
+    reads it (inside a block: the next conv; a block's output BN: the next block's conv1 and
+    shortcut conv; never the shortcut BN, whose output is the residual of a bf16 add, nor the
+    stem's, which max-pool consumes)."""
+    blocks = [(si, b) for si, st in enumerate(stages) for b in st]
+    n = 0
+    for si, b in blocks:
+        on = si >= bf16_stages
+        for cb in _block_convbns(b) + ([b.downsample] if b.downsample is not None else []):
+            cb.conv.fp8 = on and getattr(cb.conv, "fp8", False)
+            n += int(cb.conv.fp8)
+    model.stem.bn.emit_fp8 = False
+    if not fuse_bn:
+        return n
+    for i, (si, b) in enumerate(blocks):
+        inner = _block_convbns(b)
+        for j in range(len(inner) - 1):
+            inner[j].bn.emit_fp8 = bool(getattr(inner[j + 1].conv, "fp8", False))
+        nxt = blocks[i + 1][1] if i + 1 < len(blocks) else None
+        inner[-1].bn.emit_fp8 = nxt is not None and bool(getattr(nxt.conv1.conv, "fp8", False))
+        if b.downsample is not None:
+            b.downsample.bn.emit_fp8 = False
+    return n
+
+
+def _block_convbns(b):
+    return [b.conv1, b.conv2] + ([b.conv3] if hasattr(b, "conv3") else [])
 
 
 def build(name, **kw):

@@ -170,7 +170,7 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
     On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch.
     ``red_raw``: ``red`` holds (Σg, Σg·x) from a fused dgrad epilogue (:func:`bn_red_xhat`).
     ``fp8`` = (amax_ring, phase, scale, emit): also write an e5m2 copy of dx with delayed scaling
-    (4× headroom over the previous call's |dx|max) — attached as ``dx._tdl_fp8`` = (dx8, scale)
+    (16× headroom over the previous call's |dx|max: fp8_policy) — attached as ``dx._tdl_fp8`` = (dx8, scale)
     for the fp8 dgrad of the producing conv.  ``dadd`` (shaped like x): another gradient of x
     added to dx in the same pass."""
     C = x.shape[-1]

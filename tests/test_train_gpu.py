@@ -248,7 +248,7 @@ def test_resnet_fp8_forward_trains(gpu, fuse_bn):
     (fuse_bn: conv inputs quantised by the producing BN with delayed scaling)."""
     torch.manual_seed(0)
     m = models.resnet18(num_classes=10)
-    n = models.enable_fp8(m, fuse_bn=fuse_bn)
+    n = models.enable_fp8(m, fuse_bn=fuse_bn, bf16_stages=0)
     assert n >= 15
     tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01, momentum=0.9,
                                                           weight_decay=0.0))
@@ -314,11 +314,11 @@ def test_fp8_dgrad_after_zero_gradient_step_is_finite(gpu):
     assert l == l and torch.isfinite(tr.flat.master).all() and torch.isfinite(tr.flat.grad).all()
 
 
-def _loss_curve(depth, fp8, steps, dgrad=False, batch=32, size=64, lr=0.002):
+def _loss_curve(depth, fp8, steps, dgrad=False, batch=32, size=64, lr=0.002, bf16_stages=None):
     torch.manual_seed(0)
     net = models.build(f"resnet{depth}", num_classes=10)
     if fp8:
-        models.enable_fp8(net, dgrad=dgrad)
+        models.enable_fp8(net, dgrad=dgrad, bf16_stages=bf16_stages)
     tr = Trainer(net, softmax_cross_entropy, torch.device("cuda", 0), "sgd",
                  dict(lr=lr, momentum=0.9, weight_decay=0.0))
     data = [imagenet_batch(batch, size, num_classes=10, device="cuda", seed=s) for s in range(4)]
@@ -327,28 +327,28 @@ def _loss_curve(depth, fp8, steps, dgrad=False, batch=32, size=64, lr=0.002):
 
 @pytest.mark.timeout(300)
 def test_fp8_loss_curve_tracks_bf16(gpu):
-    """ResNet-50, 60 steps over 4 fixed synthetic batches (memorisation task), identical init and
-    data: the fp8 forward (e4m3 × e4m3 GEMMs, delayed scaling) loss curve stays within a bounded
-    relative gap of the bf16 curve, and both learn.  fp8 + fp8 dgrad is reported and must stay
-    finite and learn (its default is off, models.enable_fp8)."""
+    """ResNet-50, 80 steps over 4 fixed synthetic batches (memorisation task), identical init and
+    data: the default fp8 recipe (e4m3 forward + e5m2 dgrad GEMMs, delayed scaling, stages 1-2
+    bf16: models.enable_fp8) tracks the bf16 curve — same function at step 0, the early
+    trajectory within 15 %, the last-10-step loss tail within 3× of bf16's (the sweep behind the
+    recipe, profiles/r05_fp8_numerics.txt: 1.7× on the mean of 3 runs; one run's tail is noisy —
+    bf16 alone spans 0.006-0.012 run to run from the fp32-atomic BN statistics order).  Every
+    stage on fp8 is reported and must learn."""
     n = 80
     ref = _loss_curve(50, False, n, lr=0.003)
-    f8 = _loss_curve(50, True, n, lr=0.003)
-    f8d = _loss_curve(50, True, n, dgrad=True, lr=0.003)
+    f8 = _loss_curve(50, True, n, dgrad=True, lr=0.003)
+    f8all = _loss_curve(50, True, n, dgrad=False, lr=0.003, bf16_stages=0)
     tail = lambda c: sum(c[-10:]) / 10
-    print("bf16", [round(v, 3) for v in ref[::6]], tail(ref))
-    print("fp8 ", [round(v, 3) for v in f8[::6]], tail(f8))
-    print("fp8d", [round(v, 3) for v in f8d[::6]], tail(f8d))
-    assert all(v == v for v in ref + f8 + f8d)
+    print("bf16 ", [round(v, 3) for v in ref[::6]], tail(ref))
+    print("fp8  ", [round(v, 3) for v in f8[::6]], tail(f8))
+    print("fp8all", [round(v, 3) for v in f8all[::6]], tail(f8all))
+    assert all(v == v for v in ref + f8 + f8all)
     assert tail(ref) < 0.7 * ref[0]                  # the task is learnable in bf16
-    assert tail(f8) < 0.8 * f8[0]
-    # same function at step 0 (e4m3 rounding through 50 layers: 2.53-2.69 vs bf16 2.545 over
-    # round-4 runs — the fp32-atomic BN statistics reorder run to run)
-    assert abs(f8[0] - ref[0]) < 0.08 * ref[0]
+    assert abs(f8[0] - ref[0]) < 0.08 * ref[0]       # same function at step 0
     gap = max(abs(a - b) for a, b in zip(ref[:20], f8[:20])) / ref[0]
-    assert gap < 0.15, gap                          # early trajectory tracks bf16
-    assert abs(tail(f8) - tail(ref)) < 0.2 * ref[0]  # bounded gap at the end of the run
-    assert tail(f8d) < 0.85 * f8d[0]
+    assert gap < 0.15, gap                           # early trajectory tracks bf16
+    assert tail(f8) < 3.0 * max(tail(ref), 0.006), (tail(f8), tail(ref))
+    assert tail(f8all) < 0.8 * f8all[0]
 
 
 @pytest.mark.timeout(300)
@@ -703,7 +703,7 @@ def test_fp8_graph_replay_matches_eager(gpu, dgrad):
     nets = [models.resnet18(num_classes=10) for _ in range(2)]
     nets[1].load_state_dict(nets[0].state_dict())
     for n in nets:
-        assert models.enable_fp8(n, dgrad=dgrad) > 10
+        assert models.enable_fp8(n, dgrad=dgrad, bf16_stages=0) > 10
     ta, tb = [Trainer(n, softmax_cross_entropy, gpu, "sgd", dict(lr=0.02, momentum=0.9))
               for n in nets]
     ta.train_mode = tb.train_mode = False
@@ -740,7 +740,7 @@ def test_fp8_graph_replay_interleaved_with_eager_forwards(gpu, monkeypatch):
     nets = [models.resnet18(num_classes=10) for _ in range(2)]
     nets[1].load_state_dict(nets[0].state_dict())
     for n in nets:
-        assert models.enable_fp8(n) > 10
+        assert models.enable_fp8(n, bf16_stages=0) > 10
     ta, tb = [Trainer(n, softmax_cross_entropy, gpu, "sgd", dict(lr=0.02, momentum=0.9))
               for n in nets]
     ta.train_mode = tb.train_mode = False
