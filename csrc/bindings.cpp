@@ -1407,6 +1407,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none(), py::arg("aff") = py::none(),
         py::arg("w_flip") = py::none());
+  m.def("conv_flip_weights_multi", [](Tensor src, Tensor dst, Tensor rows) {
+    CHECK_T(src, torch::kBFloat16);
+    CHECK_T(dst, torch::kBFloat16);
+    TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && dst.numel() == src.numel(),
+                "conv_flip_weights_multi: contiguous flat buffers of one size");
+    TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == torch::kInt64 && rows.dim() == 2 &&
+                rows.size(1) == 8 && rows.is_contiguous(), "rows: int64 [n, 8]");
+    conv_flip_weights_multi_launch(BF(src), BFW(dst), rows.data_ptr<int64_t>(), (int)rows.size(0),
+                                   stream());
+  }, "every registered filter flip of a flat weight buffer in one launch (rows: offset, K, R, S, "
+     "C, tap, k tile, c tile; validated on the host by ops/conv.FlatFlips)");
   m.def("conv_flip_weight", [](Tensor w, Tensor wf) {
     CHECK_T(w, torch::kBFloat16);
     CHECK_T(wf, torch::kBFloat16);

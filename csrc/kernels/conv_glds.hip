@@ -1226,6 +1226,40 @@ void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, i
   hipLaunchKernelGGL(flip_weight_kernel, grid, dim3(256), 0, st, w, wf, K, R, S, C);
 }
 
+// every flipped filter of a model in ONE launch (after each optimizer step): the bf16 weights live
+// in one flat buffer (models/params.py), their flips at the same offsets of a parallel buffer.
+// Work row (8 × int64): element offset, K, R, S, C, output tap, k tile, c tile — one 32×32 tile
+// per workgroup, the same transpose as flip_weight_kernel.
+__global__ void __launch_bounds__(256) multi_flip_kernel(const bf16_t* __restrict__ src,
+                                                         bf16_t* __restrict__ dst,
+                                                         const long* __restrict__ rows) {
+  __shared__ bf16_t t[32][33];
+  const long* q = rows + 8 * (long)blockIdx.x;
+  const long off = q[0];
+  const int K = (int)q[1], R = (int)q[2], S = (int)q[3], C = (int)q[4], tap = (int)q[5];
+  const int k0 = (int)q[6] * 32, c0 = (int)q[7] * 32;
+  const bf16_t* w = src + off;
+  bf16_t* wf = dst + off;
+  const int r = tap / S, s = tap - r * S;
+  const int src_tap = (R - 1 - r) * S + (S - 1 - s);
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int k = k0 + i, c = c0 + tx;
+    t[i][tx] = (k < K && c < C) ? w[((long)k * R * S + src_tap) * C + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, k = k0 + tx;
+    if (c < C && k < K) wf[((long)c * R * S + tap) * K + k] = t[tx][i];
+  }
+}
+
+void conv_flip_weights_multi_launch(const bf16_t* src, bf16_t* dst, const long* rows, int nrows,
+                                    hipStream_t st) {
+  if (nrows <= 0) return;
+  hipLaunchKernelGGL(multi_flip_kernel, dim3(nrows), dim3(256), 0, st, src, dst, rows);
+}
+
 // fused BN-backward statistics in the LDS-DMA DGRAD epilogue (a.stats, a.bn_x): FASTK (K % 64 == 0,
 // or the ragged form of a one-class 1×1); joins need stride 1 — an accumulate leaves the pixels of
 // a class without taps unmasked; a folded BN's mask (a.aff) rides on the single-consumer form

@@ -133,6 +133,10 @@ bool conv_dgrad_as_fwd(const ConvArgs& a, const bf16_t* w_flip, uint32_t w_flip_
 // w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c] (bf16)
 void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, int C,
                              hipStream_t st);
+// many flips in one launch: rows int64 [n][8] = (offset, K, R, S, C, tap, k tile, c tile), the
+// flip of the [K,R,S,C] filter at src + offset written at dst + offset
+void conv_flip_weights_multi_launch(const bf16_t* src, bf16_t* dst, const long* rows, int nrows,
+                                    hipStream_t st);
 void conv_set_pc(int on);
 // route executors (conv_route.h): true when they ran, false = not eligible, nothing launched
 bool conv_fwd_glds(const ConvArgs& a, int cfg, hipStream_t st);

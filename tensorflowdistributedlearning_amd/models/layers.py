@@ -84,6 +84,68 @@ def resolve_padding(mode, H, W, R, S, stride, dilation):
 # layers
 # ----------------------------------------------------------------------------------------------
 
+class FlatFlips:
+    """The flipped filters (Conv2d.flip_weight) of every flat-backed conv of one flat bf16 weight
+    buffer (models/params.FlatParams), refreshed by ONE launch per parameter version
+    (``conv_flip_weights_multi``) instead of one per layer (46 per ResNet-50 step).  The flips sit
+    at their weights' offsets in a parallel buffer, so a view never moves (HIP-graph replays
+    refresh it in place).  A layer joins at its first call (flipped on its own for that version)
+    and the work list is rebuilt at the next version."""
+
+    def __init__(self, flat):
+        self.flat = flat
+        self.buf = torch.empty_like(flat)
+        self.segs = {}      # id(param) -> (offset, (K, R, S, C))
+        self.pending = {}
+        self.rows = None
+        self.version = None
+
+    @staticmethod
+    def of(p, w):
+        """The FlatFlips of ``p``'s flat buffer when ``w`` (the compute weight handed to the
+        backward) is ``p``'s own slice of it, else None."""
+        flat = getattr(p, "_flat_lowp", None)
+        if flat is None or not flat.is_cuda or flat.dtype != torch.bfloat16 or w.dim() != 4:
+            return None
+        off = getattr(p, "_flat_offset", None)
+        if off is None or w.data_ptr() != flat.data_ptr() + off * flat.element_size() \
+                or not w.is_contiguous():
+            return None
+        fl = getattr(flat, "_tdl_flips", None)
+        if fl is None:
+            fl = flat._tdl_flips = FlatFlips(flat)
+        return fl
+
+    def get(self, p, version):
+        if self.version != version:  # first call of a parameter version: flip every member
+            if self.pending:
+                self._rebuild()
+            if self.segs:
+                from ..ops.common import ext
+                ext().conv_flip_weights_multi(self.flat, self.buf, self.rows)
+            self.version = version
+        k = id(p)
+        if k not in self.segs:
+            self.pending[k] = (p._flat_offset, tuple(p.shape))
+            return None
+        off, (K, R, S, C) = self.segs[k]
+        return self.buf[off:off + K * R * S * C].view(C, R, S, K)
+
+    def _rebuild(self):
+        self.segs.update(self.pending)
+        self.pending = {}
+        rows = []
+        n = self.flat.numel()
+        for off, (K, R, S, C) in self.segs.values():
+            if off < 0 or off + K * R * S * C > n:
+                raise ValueError(f"flip span ({off}, {K}x{R}x{S}x{C}) outside the flat buffer")
+            for tap in range(R * S):
+                for kb in range((K + 31) // 32):
+                    for cb in range((C + 31) // 32):
+                        rows.append((off, K, R, S, C, tap, kb, cb))
+        self.rows = torch.tensor(rows, dtype=torch.int64).to(self.flat.device)
+
+
 class Conv2d(nn.Module):
     """NHWC conv, KRSC weight, optional bias and fused ReLU.
 
@@ -158,8 +220,14 @@ class Conv2d(nn.Module):
         """[C, R, S, K] flipped transpose of the compute weight ``w`` (w_flip[c][r][s][k] =
         w[k][R−1−r][S−1−s][c]): the stride-1 input gradient then runs as the forward conv of dy
         (ops/conv.py, conv_glds.hip conv_dgrad_as_fwd).  One HIP launch per parameter version into
-        a persistent buffer (fixed address: HIP-graph replays refresh it in place)."""
+        a persistent buffer (fixed address: HIP-graph replays refresh it in place); flat-backed
+        weights join their buffer's :class:`FlatFlips` — every flip of the model in one launch."""
         v = _params.version()
+        fl = FlatFlips.of(self.weight, w)
+        if fl is not None:
+            wf = fl.get(self.weight, v)
+            if wf is not None:
+                return wf
         c = self.__dict__.get("_flip")
         shape = (w.shape[3], w.shape[1], w.shape[2], w.shape[0])
         if c is not None and c[0] == v and c[1].device == w.device and tuple(c[1].shape) == shape:

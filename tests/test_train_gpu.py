@@ -1013,3 +1013,34 @@ def test_deterministic_mode_bitwise_repeatable(gpu, arch):
     assert torch.equal(runs[0][1], runs[1][1])
     assert torch.equal(runs[0][2], runs[1][2])
     assert torch.isfinite(runs[0][1]).all() and len(set(runs[0][0].tolist())) > 1
+
+
+def test_flat_flips_match_per_layer_flips(gpu):
+    """The flipped filters of the stride-1 input gradients (dgrad as a forward conv) come from ONE
+    launch per parameter version over the flat weight buffer (models.layers.FlatFlips): after a
+    few steps every flat-backed conv's batched flip equals the per-layer flip of its current
+    weight, and the batch covers every such conv."""
+    from tensorflowdistributedlearning_amd.models.layers import Conv2d, FlatFlips
+    from tensorflowdistributedlearning_amd.models import params as P
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    torch.manual_seed(11)
+    m = models.resnet50(num_classes=10)
+    tr = Trainer(m, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01, momentum=0.9))
+    x, y = imagenet_batch(8, 64, num_classes=10, device=gpu)
+    for _ in range(3):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    n = 0
+    for mod in m.modules():
+        if not isinstance(mod, Conv2d):
+            continue
+        w = mod.compute_weight(torch.bfloat16)
+        fl = FlatFlips.of(mod.weight, w)
+        if fl is None or id(mod.weight) not in fl.segs:
+            continue
+        got = fl.get(mod.weight, P.version())
+        ref = torch.empty_like(got)
+        ext().conv_flip_weight(w.contiguous(), ref)
+        assert torch.equal(got, ref)
+        n += 1
+    assert n >= 40, n
