@@ -491,6 +491,44 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor out, c10::optional<Tensor> bias_grad
   }
 }
 
+// fp8 weight gradient: dy8 e5m2 [N,Ho,Wo,K], x8 e4m3 [N,H,W,C] (1-byte tensors), per-tensor
+// device scales sdy / sx; dW fp32 [K,R,S,C] (accumulate: +=).  C % 16, K % 16 (a 16-B chunk never
+// crosses a filter tap)
+void conv_wgrad_fp8(Tensor dy8, Tensor x8, Tensor out, Tensor sdy, Tensor sx, int64_t sh, int64_t sw,
+                    int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate) {
+  TORCH_CHECK(dy8.is_cuda() && x8.is_cuda() && dy8.element_size() == 1 && x8.element_size() == 1 &&
+              dy8.is_contiguous() && x8.is_contiguous(), "fp8 operands expected");
+  CHECK_T(out, torch::kFloat32);
+  CHECK_T(sdy, torch::kFloat32);
+  CHECK_T(sx, torch::kFloat32);
+  TORCH_CHECK(out.dim() == 4 && out.is_contiguous(), "dW must be contiguous KRSC");
+  ConvArgs a = conv_args(x8, out, x8.size(0), x8.size(1), x8.size(2), x8.size(3), out.size(0),
+                         out.size(1), out.size(2), sh, sw, ph, pw, dh, dw, dy8.size(1), dy8.size(2));
+  TORCH_CHECK(out.size(3) == a.C && dy8.size(3) == a.K && dy8.size(0) == a.N && a.C % 16 == 0 &&
+              a.K % 16 == 0, "fp8 weight gradient shapes: C % 16 == 0, K % 16 == 0");
+  TORCH_CHECK(x8.numel() < (1LL << 32) && dy8.numel() < (1LL << 32), "tensor too large");
+  a.dy = (const bf16_t*)dy8.data_ptr(); a.x = (const bf16_t*)x8.data_ptr();
+  a.dy_bytes = (uint32_t)dy8.numel(); a.x_bytes = (uint32_t)x8.numel();
+  a.M = a.K; a.Ng = a.R * a.S * a.C; a.Kg = a.N * a.Ho * a.Wo;
+  a.fp8 = 1;
+  a.scale_x = sdy.data_ptr<float>(); a.scale_w = sx.data_ptr<float>();
+  if (a.Kg == 0) {
+    if (!accumulate) out.zero_();
+    return;
+  }
+  WgradPlan plan;
+  try {
+    conv_wgrad_plan(a, &plan);
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, e.what());
+  }
+  a.kps = plan.kps;
+  auto ws = torch::empty({(int64_t)plan.splits * a.M * a.Ng}, out.options());
+  a.out = ws.data_ptr();
+  a.out_bytes = nbytes32(ws);
+  conv_wgrad_launch(a, plan, out.data_ptr<float>(), accumulate, stream());
+}
+
 // ------------------------------------------------------------------------------------------- bn
 void bn_stats(Tensor x, Tensor stats) {
   if (is_f32(x)) {
@@ -1407,6 +1445,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("accumulate") = false, py::arg("mask") = py::none(), py::arg("w_t") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none(), py::arg("aff") = py::none(),
         py::arg("w_flip") = py::none());
+  m.def("conv_wgrad_fp8", &conv_wgrad_fp8, py::arg("dy8"), py::arg("x8"), py::arg("out"),
+        py::arg("sdy"), py::arg("sx"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dh"), py::arg("dw"), py::arg("accumulate") = false,
+        "fp8 weight gradient: e5m2 dy x e4m3 x on the f8f6f4 MFMA, fp32 dW");
   m.def("conv_flip_weights_multi", [](Tensor src, Tensor dst, Tensor rows) {
     CHECK_T(src, torch::kBFloat16);
     CHECK_T(dst, torch::kBFloat16);

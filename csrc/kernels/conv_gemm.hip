@@ -1003,13 +1003,17 @@ static void conv_wgrad_gemm_plan(const ConvArgs& a, WgradPlan* p);
 
 // a folded BN on x (ConvArgs::aff): the register-staged kernel (it transforms the staged B rows)
 void conv_wgrad_plan(const ConvArgs& a, WgradPlan* p) {
-  RouteProblem q = route_problem(2, a, a.aff ? RF_AFF : 0);
+  RouteProblem q = route_problem(2, a, (a.aff ? RF_AFF : 0) | (a.fp8 ? RF_FP8 : 0));
   for (int i = route_next(q, -1); i >= 0; i = route_next(q, i)) {
     bool ran = false;
     switch (route_rule(i).impl) {
       case RT_HALO: ran = conv_wgrad_halo_plan(a, p); break;
       case RT_GLDS: ran = conv_wgrad_glds_plan(a, route_cfg(i), p); break;
-      case RT_GEMM: conv_wgrad_gemm_plan(a, p); ran = true; break;
+      case RT_GEMM:
+        if (a.fp8) break;  // (fp8 operands: the LDS-DMA kernel only)
+        conv_wgrad_gemm_plan(a, p);
+        ran = true;
+        break;
       default: break;
     }
     if (ran) {

@@ -119,6 +119,42 @@ __device__ __forceinline__ i32x8 lds_read_kc_f8(uint32_t tile, int row, int g) {
   return v;
 }
 
+// fp8 MC image (weight gradients: [128 k-rows = pixels][COLS bytes]): 16-B chunk c of k-row r
+// is stored at chunk c ^ mc8_swz(r), so the 16 k-rows a 32-lane half reads with one
+// ds_read_b64_tr_b8 (two 8-row blocks 32 rows apart, one chunk column) sit on distinct banks
+template <int COLS>
+__device__ __forceinline__ int mc8_swz(int r) {
+  static_assert(COLS == 256 || COLS == 128, "fp8 MC images: 128- or 256-byte rows");
+  if constexpr (COLS == 256)
+    return (r & 7) | (((r >> 5) & 1) << 3);
+  else
+    return ((r >> 1) & 3) | (((r >> 5) & 1) << 2);
+}
+template <int COLS>
+__device__ __forceinline__ int mc8_off(int r, int chunk) {
+  return r * COLS + ((chunk ^ mc8_swz<COLS>(r)) << 4);
+}
+// fp8 fragment of v_mfma_scale_f32_16x16x128_f8f6f4 from an MC image: four ds_read_b64_tr_b8
+// (per 16-lane group a block of 8 k-rows × 16 columns, delivered column-major: lane i of the group
+// gets column i of the 8 rows; lane 2q+p supplies row q, bytes 8p … 8p+7).  Lane l (group
+// g = l>>4) holds column col0 + (l&15) of k-rows 32g + 8j + 0..7, j = 0..3 — one k order shared
+// by both operands, which is all the product needs (lds_read_kc_f8).  The swizzle of the rows a
+// lane reads does not change with j, so one base address serves the four reads.
+template <int COLS>
+__device__ __forceinline__ i32x8 lds_read_mc_f8(uint32_t tile, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const uint32_t base = tile + (uint32_t)(mc8_off<COLS>(32 * g + (i >> 1), col0 >> 4) + 8 * (i & 1));
+  v2u32 x0, x1, x2, x3;
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(x0) : "v"(base) : "memory");
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(x1) : "v"(base), "n"(8 * COLS) : "memory");
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(x2) : "v"(base), "n"(16 * COLS) : "memory");
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(x3) : "v"(base), "n"(24 * COLS) : "memory");
+  i32x8 v;
+  v[0] = (int)x0[0]; v[1] = (int)x0[1]; v[2] = (int)x1[0]; v[3] = (int)x1[1];
+  v[4] = (int)x2[0]; v[5] = (int)x2[1]; v[6] = (int)x3[0]; v[7] = (int)x3[1];
+  return v;
+}
+
 __device__ __forceinline__ void lgkm_wait0() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
@@ -186,7 +222,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
   // DGRAD: dy e5m2 (gradients: wider range) × W^T e4m3 — the weight copy is stored transposed
   // ([R][S][C][K], ops/fp8.py) so both operands are K-contiguous rows (KC LDS images, no
   // transposed LDS reads); FASTK only (K % 128 == 0: a K-step is one tap, 128 output channels).
-  static_assert(!FP8 || MODE != WGRAD, "fp8 forward / dgrad only");
+  // WGRAD (fp8): dy e5m2 × x e4m3, both as MC images of 128 pixels per K-step (fp8 MC layout
+  // mc8_off, fragments by transposed 8-bit reads lds_read_mc_f8), fp32 split-K slabs × the scales
+  static_assert(!FP8 || MODE != WGRAD || ((BM == 256 || BM == 128) && BN == 128),
+                "fp8 weight gradients: 256x128 / 128x128 tiles");
   static_assert(!FP8 || MODE != DGRAD || FASTK, "fp8 dgrad needs K % 128 == 0");
   constexpr int ESZ = FP8 ? 1 : 2;         // bytes per element
   constexpr int EPC = 16 / ESZ;            // elements per 16-B chunk
@@ -244,6 +283,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     const int swz = cols >= 128 ? ((krow & 3) | (((krow >> 3) & 1) << 2))
                                 : (((krow >> 1) & 1) | (((krow >> 3) & 1) << 1));
     return lin_src ? (q << 3) : ((((q >> 1) ^ swz) << 4) + ((q & 1) << 3));
+  };
+
+  // fp8 MC image [128][COLS bytes]: instruction j fills k-rows (j·NW + wid)·(1024/COLS) … ; the
+  // lane fetches the logical 16-column chunk that belongs at its physical (swizzled) slot
+  auto mc8_row = [&](int j, int cols) { return (j * NW + wid) * (1024 / cols) + lane / (cols / 16); };
+  auto mc8_col = [&](int j, int cols) {
+    const int r = mc8_row(j, cols), q = lane % (cols / 16);
+    return 16 * (q ^ (cols == 256 ? mc8_swz<256>(r) : mc8_swz<128>(r)));
   };
 
   // ---- per-tile load state ----
@@ -317,12 +364,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     } else {  // WGRAD
 #pragma unroll
       for (int j = 0; j < IA; ++j) {
-        const int co = T.bm0 + mc_col(j, BM, mc_krow(j, BM));
+        const int co = T.bm0 + (FP8 ? mc8_col(j, BM) : mc_col(j, BM, mc_krow(j, BM)));
         a_base[j] = co < a.M ? co : -1;
       }
 #pragma unroll
       for (int j = 0; j < IB; ++j) {
-        const int nn = T.bn0 + mc_col(j, BN, mc_krow(j, BN));
+        const int nn = T.bn0 + (FP8 ? mc8_col(j, BN) : mc_col(j, BN, mc_krow(j, BN)));
         if (nn < a.Ng) {
           const int rs = fdiv(nn, a.fd_C), ci = nn - rs * a.C;
           const int r = fdiv(rs, a.fd_S), s = rs - r * a.S;
@@ -486,28 +533,28 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
     } else {  // WGRAD
 #pragma unroll
       for (int j = 0; j < IA; ++j) {
-        const int p = kb + mc_krow(j, BM);
+        const int p = kb + (FP8 ? mc8_row(j, BM) : mc_krow(j, BM));
         const bool v = p < a.Kg && a_base[j] >= 0;
-        dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.K + a_base[j]) * 2u : OOB);
+        dma16(ra_src, As + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.K + a_base[j]) * (uint32_t)ESZ : OOB);
       }
       if (pointwise && a.sh == 1 && a.sw == 1) {
         // 1×1, stride 1, no padding: x pixel = output pixel p (no per-DMA pixel divisions)
 #pragma unroll
         for (int j = 0; j < IB; ++j) {
-          const int p = kb + mc_krow(j, BN);
+          const int p = kb + (FP8 ? mc8_row(j, BN) : mc_krow(j, BN));
           const bool v = p < a.Kg && b_base[j] >= 0;
-          dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.C + b_base[j]) * 2u : OOB);
+          dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? (uint32_t)(p * a.C + b_base[j]) * (uint32_t)ESZ : OOB);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < IB; ++j) {
-          const int p = kb + mc_krow(j, BN);
+          const int p = kb + (FP8 ? mc8_row(j, BN) : mc_krow(j, BN));
           const int ni = fdiv(p, a.fd_HoWo), rem = p - ni * HoWo;
           const int ho = fdiv(rem, a.fd_Wo), wo = rem - ho * a.Wo;
           const int hi = ho * a.sh + b_f2[j], wi = wo * a.sw + b_f3[j];
           const bool v = p < a.Kg && b_base[j] >= 0 && (unsigned)hi < (unsigned)a.H &&
                          (unsigned)wi < (unsigned)a.W;
-          const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_base[j]) * 2u;
+          const uint32_t off = (uint32_t)(((ni * a.H + hi) * a.W + wi) * a.C + b_base[j]) * (uint32_t)ESZ;
           dma16(rb_src, Bs + (j * NW + wid) * 1024, v ? off : OOB);
         }
       }
@@ -620,8 +667,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
           const int n0 = T.bn0 + wn * TN + rn * 16 + (lane >> 4) * 4;
           const bool v = m < a.M && n0 < a.Ng;
           const uint32_t off = (slab0 + (uint32_t)(m * a.Ng + n0)) * 4u;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, acc[rm][rn]), rout,
-                                                 v ? off : OOB, 0, 0);
+          f32x4 o = acc[rm][rn];
+          if constexpr (FP8) o *= out_scale;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, o), rout, v ? off : OOB, 0, 0);
         }
       }
     } else {
@@ -783,19 +831,26 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }                                                                                        \
       const uint32_t As = smem_lds + (uint32_t)(slot_comp * STAGE), Bs = As + A_BYTES;         \
       i32x8 a8[RM], b8[RN];                                                                    \
+      if constexpr (MODE == WGRAD) {                                                           \
 _Pragma("unroll")                                                                             \
-      for (int rm = 0; rm < RM; ++rm) a8[rm] = lds_read_kc_f8(As, wm * TM + rm * 16 + (lane & 15), lane >> 4);\
+        for (int rm = 0; rm < RM; ++rm) a8[rm] = lds_read_mc_f8<BM>(As, wm * TM + rm * 16, lane);\
 _Pragma("unroll")                                                                             \
-      for (int rn = 0; rn < RN; ++rn) b8[rn] = lds_read_kc_f8(Bs, wn * TN + rn * 16 + (lane & 15), lane >> 4);\
+        for (int rn = 0; rn < RN; ++rn) b8[rn] = lds_read_mc_f8<BN>(Bs, wn * TN + rn * 16, lane);\
+      } else {                                                                                 \
+_Pragma("unroll")                                                                             \
+        for (int rm = 0; rm < RM; ++rm) a8[rm] = lds_read_kc_f8(As, wm * TM + rm * 16 + (lane & 15), lane >> 4);\
+_Pragma("unroll")                                                                             \
+        for (int rn = 0; rn < RN; ++rn) b8[rn] = lds_read_kc_f8(Bs, wn * TN + rn * 16 + (lane & 15), lane >> 4);\
+      }                                                                                        \
       lgkm_wait0();                                                                            \
 _Pragma("unroll")                                                                             \
       for (int rm = 0; rm < RM; ++rm)                                                          \
 _Pragma("unroll")                                                                             \
         for (int rn = 0; rn < RN; ++rn)                                                        \
-/* operand formats: first (B tile: weights) e4m3 = 0; second (A tile) e4m3 = 0 for */          \
-/* FWD activations, e5m2 (bf8) = 1 for DGRAD output gradients */                               \
+/* operand formats: first (B tile: weights / WGRAD activations) e4m3 = 0; second (A tile) */  \
+/* e4m3 = 0 for FWD activations, e5m2 (bf8) = 1 for DGRAD / WGRAD output gradients */          \
           acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(                      \
-              b8[rn], a8[rm], acc[rm][rn], 0, MODE == DGRAD ? 1 : 0, 0, 127, 0, 127);          \
+              b8[rn], a8[rm], acc[rm][rn], 0, MODE == FWD ? 0 : 1, 0, 127, 0, 127);            \
       slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;                                 \
       --inflight;                                                                              \
       if (ckt + 1 >= CT.kt1) {                                                                 \
@@ -1363,6 +1418,7 @@ bool conv_dgrad_glds(const ConvArgs& a0, int cfg, hipStream_t st, bool* fused) {
 // usual tiles, 7 the 64×256 column of the row-packed stem): ≈ one tile-split per CU slot,
 // ≥ 16 K-steps each
 bool conv_wgrad_glds_plan(const ConvArgs& a, int cfg, WgradPlan* p) {
+  if (a.fp8) return conv_wgrad_fp8_plan(a, cfg, p);
   if (a.C % 8 || a.K % 8 || a.aff) return false;
   if (!route_cfg_instantiated(RT_GLDS, WGRAD, cfg, 0)) return false;
   const GCfg& g = cfg_of(cfg);
@@ -1374,6 +1430,26 @@ bool conv_wgrad_glds_plan(const ConvArgs& a, int cfg, WgradPlan* p) {
   const int target = env_int("TDL_GLDS_WGRAD_TARGET", 128);
   int s = (int)std::max<long>(1, std::min<long>(nkt, (target + tiles - 1) / tiles));
   int per = std::max(cdiv(nkt, s), env_int("TDL_GLDS_WGRAD_MINSTEPS", 16));
+  s = cdiv(nkt, per);
+  p->impl = 1;
+  p->cfg = cfg;
+  p->bm = g.bm;
+  p->bn = g.bn;
+  p->splits = s;
+  p->kps = per;
+  return true;
+}
+
+// fp8 weight gradient (route rows wgrad.glds.fp8*: dy e5m2 × x e4m3, a.scale_x / a.scale_w the
+// per-tensor scales): cfg 0 = 256×128, 2 = 128×128 tiles; K-steps of 128 pixels
+bool conv_wgrad_fp8_plan(const ConvArgs& a, int cfg, WgradPlan* p) {
+  if (!a.fp8 || a.C % 16 || a.K % 16 || a.aff || (cfg != 0 && cfg != 2)) return false;
+  const GCfg& g = cfg_of(cfg);
+  const long tiles = (long)cdiv(a.M, g.bm) * cdiv(a.Ng, g.bn);
+  const int nkt = cdiv(a.Kg, 128);
+  const int target = env_int("TDL_GLDS_WGRAD_TARGET", 128);
+  int s = (int)std::max<long>(1, std::min<long>(nkt, (target + tiles - 1) / tiles));
+  int per = std::max(cdiv(nkt, s), std::max(1, env_int("TDL_GLDS_WGRAD_MINSTEPS", 16) / 2));
   s = cdiv(nkt, per);
   p->impl = 1;
   p->cfg = cfg;
@@ -1396,6 +1472,15 @@ void conv_wgrad_glds_kernel_launch(const ConvArgs& a0, const WgradPlan& p, hipSt
   a.cls_tile0[1] = (int)tiles;
   a.tpb = persistent_tpb(tiles);
   const int blocks = (int)((tiles + a.tpb - 1) / a.tpb);
+  if (a.fp8) {
+    if (p.cfg == 0)
+      launch_g<WGRAD, 256, 128, 4, 2, 3, false, false, 1, true>(a, blocks, st);
+    else if (p.cfg == 2)
+      launch_g<WGRAD, 128, 128, 2, 2, 4, false, false, 1, true>(a, blocks, st);
+    else
+      throw std::runtime_error("fp8 weight gradient: tile config not instantiated");
+    return;
+  }
   launch_gcfg<WGRAD, false, false, 1>(a, p.cfg, blocks, st);
 }
 

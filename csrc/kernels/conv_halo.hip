@@ -813,7 +813,7 @@ bool plan_halo_wgrad(const ConvArgs& a, HaloGeom& g, HaloWg& q, int& bm) {
 
 // route rows wgrad.halo.*: false when the kernel does not take the problem
 bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p) {
-  if (a.aff) return false;
+  if (a.aff || a.fp8) return false;
   HaloGeom g;
   HaloWg q;
   int bm;

@@ -93,19 +93,23 @@ const RouteRule kRoutes[] = {
   {"dgrad.gemm",                  DGRAD, RT_GEMM,  1, TAPS,  0, 1, INF,      1, INF,      0,     0, 0,     0,  0,                  RF_FP8,                               0,    true,  false,
    "register-staged implicit GEMM over the stride parity classes"},
   // -------------------------------------------------------------------------------- weight gradient
-  {"wgrad.halo.wide3x3",          WGRAD, RT_HALO,  9, 9,     1, 128, INF,    8, INF,      65536, 0, 0,     0,  0,                  RF_AFF,                               0,    true,  false,
+  {"wgrad.glds.fp8",              WGRAD, RT_GLDS,  1, TAPS,  0, 16, INF,    129, INF,    0,     0, 0,     0,  RF_FP8,             0,                                    0,    true,  false,
+   "fp8 weight gradient (e5m2 dy x e4m3 x, transposed 8-bit LDS reads): LDS-DMA kernel only"},
+  {"wgrad.glds.fp8.m128",         WGRAD, RT_GLDS,  1, TAPS,  0, 16, INF,    16, 128,     0,     0, 0,     0,  RF_FP8,             0,                                    2,    true,  false,
+   "fp8 weight gradient with <= 128 output channels: 128x128 tiles"},
+  {"wgrad.halo.wide3x3",          WGRAD, RT_HALO,  9, 9,     1, 128, INF,    8, INF,      65536, 0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  false,
    "3x3 with >= 128 inputs: halo weight gradient, ResNet-50 layers 2-4 362 -> 295 us at b1024 (profiles/r04_halo_ab.txt)"},
-  {"wgrad.halo.aligned",          WGRAD, RT_HALO,  9, 9,     1, 64, INF,     8, INF,      0,     0, 0,     0,  0,                  RF_AFF,                               0,    true,  true,
+  {"wgrad.halo.aligned",          WGRAD, RT_HALO,  9, 9,     1, 64, INF,     8, INF,      0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  true,
    "tests: every eligible problem on the halo kernel"},
-  {"wgrad.glds.stem",             WGRAD, RT_GLDS,  1, TAPS,  0, 1, 32,       1, 64,       65536, 0, 0,     0,  0,                  RF_AFF,                               7,    false, false,
+  {"wgrad.glds.stem",             WGRAD, RT_GLDS,  1, TAPS,  0, 1, 32,       1, 64,       65536, 0, 0,     0,  0,                  RF_AFF | RF_FP8,                               7,    false, false,
    "opt-in: one 64x256 tile column for the row-packed stem, 1120 vs 1040 us (profiles/r03_stem_wgrad_ab.txt)"},
-  {"wgrad.glds.1x1",              WGRAD, RT_GLDS,  1, 1,     0, 8, INF,      256, INF,    4096,  0, 0,     0,  0,                  RF_AFF,                               0,    true,  false,
+  {"wgrad.glds.1x1",              WGRAD, RT_GLDS,  1, 1,     0, 8, INF,      256, INF,    4096,  0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  false,
    "1x1 with >= 256 outputs on the LDS-DMA kernel (3x3 gathers of x favour the others; README round-4 A/B)"},
-  {"wgrad.glds.aligned.m128",     WGRAD, RT_GLDS,  1, TAPS,  0, 8, INF,      1, 128,      0,     0, 0,     0,  0,                  RF_AFF,                               2,    true,  true,
+  {"wgrad.glds.aligned.m128",     WGRAD, RT_GLDS,  1, TAPS,  0, 8, INF,      1, 128,      0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                               2,    true,  true,
    "tests: every aligned problem on the LDS-DMA family"},
-  {"wgrad.glds.aligned",          WGRAD, RT_GLDS,  1, TAPS,  0, 8, INF,      129, INF,    0,     0, 0,     0,  0,                  RF_AFF,                               0,    true,  true,
+  {"wgrad.glds.aligned",          WGRAD, RT_GLDS,  1, TAPS,  0, 8, INF,      129, INF,    0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  true,
    "tests: every aligned problem on the LDS-DMA family"},
-  {"wgrad.gemm",                  WGRAD, RT_GEMM,  1, TAPS,  0, 1, INF,      1, INF,      0,     0, 0,     0,  0,                  0,                                    0,    true,  false,
+  {"wgrad.gemm",                  WGRAD, RT_GEMM,  1, TAPS,  0, 1, INF,      1, INF,      0,     0, 0,     0,  0,                  RF_FP8,                               0,    true,  false,
    "register-staged split-K weight gradient"},
 };
 // clang-format on
@@ -240,7 +244,7 @@ bool route_cfg_instantiated(int impl, int op, int cfg, int flags) {
     case RT_ASFWD:
       return op == DGRAD && (cfg == 0 || cfg == 4 || cfg == ASF_HALO || cfg == ASF_PC);
     case RT_GLDS:
-      if (flags & RF_FP8) return cfg == 0 || cfg == 1;
+      if (flags & RF_FP8) return op == WGRAD ? (cfg == 0 || cfg == 2) : (cfg == 0 || cfg == 1);
       if (op == FWD) return (flags & RF_RES) ? (cfg == 0 || cfg == 4) : (cfg >= 0 && cfg <= 5);
       if (op == DGRAD) {
         if (flags & RF_AFF) return cfg == 4 || cfg == 6;

@@ -157,7 +157,8 @@ void conv_wgrad_halo_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t s
 bool conv_dgrad_glds(const ConvArgs& a, int cfg, hipStream_t st, bool* fused = nullptr);
 // can the LDS-DMA DGRAD epilogue fuse this problem's BN-backward statistics (classes built)?
 bool dgrad_stats_fusable(const ConvArgs& a);
-bool conv_wgrad_glds_plan(const ConvArgs& a, int cfg, WgradPlan* p);
+bool conv_wgrad_glds_plan(const ConvArgs& a, int cfg, WgradPlan* p);  // (a.fp8: the fp8 plan)
+bool conv_wgrad_fp8_plan(const ConvArgs& a, int cfg, WgradPlan* p);
 void conv_wgrad_glds_kernel_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);
 // fp8 (OCP e4m3) forward conv: a.x / a.w point at e4m3 bytes, a.scale_x / a.scale_w at their fp32 scales
 void conv_fwd_fp8_launch(const ConvArgs& a, hipStream_t st);

@@ -16,7 +16,7 @@ _REGISTRY = {
 }
 
 
-def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None):
+def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None, wgrad=None):
     """fp8 GEMMs for every bias-free conv whose input channels are a multiple of 16 (the
     3-channel stem and biased heads stay bf16): the forward on e4m3 activations × e4m3 weights
     and — with ``dgrad`` — the input gradient on e5m2 output gradients × e4m3 weights (convs with
@@ -32,11 +32,15 @@ def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None):
     bf16 0.0088, every stage fp8 0.057 (6.5×), stage 1 bf16 0.025 (2.8×), stages 1–2 bf16
     0.015 (1.7×, fp8 dgrad included).  ResNet-152 keeps 39 of its 50 blocks on fp8.
 
-    The fp8 dgrad defaults on (``TDL_FP8_DGRAD=0`` or ``dgrad=False`` turns it off)."""
+    The fp8 dgrad defaults on (``TDL_FP8_DGRAD=0`` or ``dgrad=False`` turns it off), and so does
+    the fp8 weight gradient (``TDL_FP8_WGRAD=0`` / ``wgrad=False``): e5m2 output gradients × the
+    forward's e4m3 input, which the conv then keeps for its backward instead of the bf16 one."""
     import os
     from .layers import Conv2d, BatchNorm, ConvBN
     if dgrad is None:
         dgrad = os.environ.get("TDL_FP8_DGRAD", "1") == "1"
+    if wgrad is None:
+        wgrad = os.environ.get("TDL_FP8_WGRAD", "1") == "1"
     if bf16_stages is None:
         bf16_stages = int(os.environ.get("TDL_FP8_BF16_STAGES", "2"))
     n = 0
@@ -49,10 +53,13 @@ def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None):
     stages = [getattr(model, f"layer{i}", None) for i in (1, 2, 3, 4)]
     if isinstance(model, ResNet) and all(s is not None for s in stages):
         n = _resnet_fp8_plan(model, stages, bf16_stages, fuse_bn)
-    if dgrad:
+    for m in model.modules():
+        if isinstance(m, Conv2d) and getattr(m, "fp8", False):
+            m.fp8_dgrad, m.fp8_wgrad = bool(dgrad), bool(wgrad)
+    if dgrad or wgrad:
         for m in model.modules():
             if isinstance(m, ConvBN) and getattr(m.conv, "fp8", False):
-                m.bn.emit_fp8_bwd = True  # e5m2 dy for the conv's fp8 dgrad (ops/conv.py)
+                m.bn.emit_fp8_bwd = True  # e5m2 dy for the conv's fp8 dgrad / wgrad (ops/conv.py)
     return n
 
 

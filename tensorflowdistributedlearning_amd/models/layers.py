@@ -261,6 +261,8 @@ class Conv2d(nn.Module):
         return g
 
     fp8 = False  # set by models.enable_fp8: e4m3 forward GEMM (ops/fp8.py)
+    fp8_dgrad = False  # … and the e5m2 × e4m3 input gradient
+    fp8_wgrad = False  # … and the e5m2 × e4m3 weight gradient (the forward's e4m3 input saved)
 
     def fp8_weight(self, w_lowp):
         """e4m3 copy of the weight + its scale, re-quantised once per optimizer step (delayed

@@ -261,12 +261,24 @@ def fp8_dgrad_eligible(layer, dy, geom: ConvGeom, w_shape):
     """Can this conv's dgrad run on fp8 operands?  An fp8 layer whose output gradient arrived
     with an e5m2 copy (the BN backward's side output), K % 128 == 0 (one tap per 128-deep K-step)
     and no stride-with-dilation (masked-class dgrad)."""
-    if layer is None or not getattr(layer, "fp8", False) or getattr(dy, "_tdl_fp8", None) is None:
+    if layer is None or not getattr(layer, "fp8_dgrad", False) or \
+            getattr(dy, "_tdl_fp8", None) is None:
         return False
     K, R, S, C = w_shape
     (sh, sw), (dh, dw) = geom.stride, geom.dilation
     masked = (sh > 1 and dh > 1) or (sw > 1 and dw > 1)
     return K % 128 == 0 and C % 8 == 0 and not masked and not layer.grad_needs_unpad()
+
+
+FP8_WGRAD = os.environ.get("TDL_FP8_WGRAD", "1") == "1"
+
+
+def fp8_wgrad_eligible(layer, x, w) -> bool:
+    """Does this fp8 conv's weight gradient run on fp8 operands (csrc conv_wgrad_fp8)?  A layer
+    enabled for it (models.enable_fp8), unpadded weights, C % 16 and K % 16 (a 16-byte chunk never
+    crosses a filter tap), no bias."""
+    return (FP8_WGRAD and getattr(layer, "fp8_wgrad", False) and not layer.grad_needs_unpad()
+            and layer.bias is None and x.shape[-1] % 16 == 0 and w.shape[0] % 16 == 0)
 
 
 def dgrad_covers_input(geom: ConvGeom, R, S):
@@ -378,6 +390,10 @@ class _Conv2dFn(torch.autograd.Function):
             x8, sx = pre if pre is not None else layer.fp8_input(x)
             w8, sw = layer.fp8_weight(w)
             y = conv_fwd_fp8(x8, sx, w8, sw, geom, relu=relu, stats=stats)
+            if fp8_wgrad_eligible(layer, x, w):
+                # the weight gradient runs on this e4m3 copy (ops/conv._conv_param_grads): the
+                # bf16 input is not kept for the backward
+                ctx.x8 = (x8, sx)
         else:
             y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats, residual=residual)
         ctx.has_res = residual is not None
@@ -390,7 +406,8 @@ class _Conv2dFn(torch.autograd.Function):
         # the ReLU-mask token of the BN that produced x (ops/gradjoin.py): a single-consumer conv
         # applies the mask in its dgrad and may fuse that BN's backward statistics
         ctx.bn_tok = getattr(x, "_tdl_mask_token", None) if join is None else None
-        ctx.save_for_backward(x, weight, bias, y if relu else None)
+        ctx.save_for_backward(None if getattr(ctx, "x8", None) is not None else x, weight, bias,
+                              y if relu else None)
         if stats is None:
             stats = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(stats)
@@ -487,7 +504,9 @@ class _Conv2dFn(torch.autograd.Function):
                 side.wait_stream(streams.current(dy.device))
             with streams.on(side):
                 _conv_param_grads(ctx, dy, x, weight, bias)
-            streams.keep_alive(dy.device, dy, x)  # until the next join (no record_stream)
+            # until the next join (no record_stream)
+            streams.keep_alive(dy.device, *[t for t in (dy, x) if t is not None],
+                               *getattr(ctx, "fp8_keep", ()))
             streams.join_at_backward_end(dy.device)  # backward() returns joined
         return dx, None, None, None, None, None, None, None, dres, None
 
@@ -505,6 +524,26 @@ def _conv_param_grads(ctx, dy, x, weight, bias):
         bias_direct = bt is not None and bfresh
         bias_buf = bt if bias_direct else torch.empty(nb, device=dy.device,
                                                       dtype=torch.float32)
+    x8 = getattr(ctx, "x8", None)
+    if x8 is not None and weight.requires_grad:
+        # fp8 weight gradient: e5m2 dy (the BN backward's side output, else quantised here) ×
+        # the forward's e4m3 input
+        from .fp8 import quantize_e5m2
+        ctx.x8 = None
+        d8 = getattr(dy, "_tdl_fp8", None)
+        dy8, sdy = d8 if d8 is not None else quantize_e5m2(dy)
+        target, fresh = grad_target(weight)
+        out = target if target is not None else torch.empty(tuple(weight.shape), device=dy.device,
+                                                            dtype=torch.float32)
+        (sh, sw), (dh, dw) = geom.stride, geom.dilation
+        ext().conv_wgrad_fp8(dy8, x8[0], out, sdy, x8[1], sh, sw, geom.padding[0],
+                             geom.padding[2], dh, dw, target is not None and not fresh)
+        ctx.fp8_keep = (dy8, x8[0])
+        if target is not None:
+            deliver_grad(weight, written=True)
+        else:
+            deliver_grad(weight, out)
+        return
     if weight.requires_grad:
         target, fresh = grad_target(weight)
         if ctx.layer is not None and ctx.layer.grad_needs_unpad():

@@ -140,6 +140,15 @@ def _run_wgrad(r, gpu, N, H, k, cin, cout, g):
     x = torch.randn(N, H, H, cin).bfloat16().to(gpu)
     dy = torch.randn(N, H, H, cout).bfloat16().to(gpu)
     out = torch.empty(cout, k, k, cin, device=gpu)
+    if r["need"] & RF_FP8:
+        from tensorflowdistributedlearning_amd.ops import fp8 as F8
+        x8, sx = F8.quantize_e4m3(x)
+        dy8, sdy = F8.quantize_e5m2(dy)
+        e.conv_wgrad_fp8(dy8, x8, out, sdy, sx, *_args(g), False)
+        torch.cuda.synchronize()
+        ref = C.ref_conv_wgrad(F8.dequantize_e5m2(dy8, sdy).cpu(), F8.dequantize(x8, sx).cpu(),
+                               (cout, k, k, cin), g)
+        return out, ref, 1e-3
     e.conv_wgrad(dy, x, out, None, *_args(g), False, None)
     torch.cuda.synchronize()
     ref = C.ref_conv_wgrad(dy.float().cpu(), x.float().cpu(), (cout, k, k, cin), g)

@@ -1221,3 +1221,38 @@ def test_conv_dgrad_as_forward(gpu, shape, epi):
         gf, xf = got.float().reshape(-1, Cin), x.float().reshape(-1, Cin)
         want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
         assert rel_err(red1, want) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [(4, 14, 14, 128, 256, 1, 1, 1, 0),    # 1x1, 256x128 tiles
+                                   (4, 14, 14, 64, 128, 3, 3, 1, 1),     # 3x3, <= 128 outputs: 128x128
+                                   (3, 15, 15, 256, 512, 3, 3, 2, 1),    # 3x3 / s2, ragged pixels
+                                   (2, 9, 11, 48, 144, 1, 1, 2, 0),      # C, K % 16 only
+                                   (8, 28, 28, 256, 64, 1, 1, 1, 0)])    # many pixels, split-K
+def test_conv_wgrad_fp8(gpu, shape):
+    """fp8 weight gradient (e5m2 dy x e4m3 x through transposed 8-bit LDS reads into the f8f6f4
+    MFMA, fp32 split-K slabs x the per-tensor scales) vs the fp32 wgrad of the same dequantised
+    operands; accumulate adds onto dW."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    N, H, W, Cin, K, R, S, st, p = shape
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
+    torch.manual_seed(23)
+    Ho, Wo = g.out_hw(H, W, R, S)
+    x = torch.randn(N, H, W, Cin).bfloat16()
+    dy = torch.randn(N, Ho, Wo, K).bfloat16()
+    x8, sx = F8.quantize_e4m3(x.to(gpu))
+    dy8, sdy = F8.quantize_e5m2(dy.to(gpu))
+    ref = C.ref_conv_wgrad(F8.dequantize_e5m2(dy8, sdy).cpu(), F8.dequantize(x8, sx).cpu(),
+                           (K, R, S, Cin), g)
+    out = torch.full((K, R, S, Cin), 3.0, device=gpu)
+    ext().conv_wgrad_fp8(dy8.view(torch.uint8), x8.view(torch.uint8), out, sdy, sx,
+                         *(st, st, p, p, 1, 1), False)
+    torch.cuda.synchronize()
+    assert ext().conv_last_route(2).startswith("wgrad.glds.fp8")
+    assert rel_err(out, ref) < 1e-3
+    acc = torch.ones((K, R, S, Cin), device=gpu)
+    ext().conv_wgrad_fp8(dy8.view(torch.uint8), x8.view(torch.uint8), acc, sdy, sx,
+                         *(st, st, p, p, 1, 1), True)
+    torch.cuda.synchronize()
+    assert rel_err(acc, ref + 1.0) < 1e-3
+    # quantisation error only vs the bf16 wgrad of the unquantised data
+    assert rel_err(out, C.ref_conv_wgrad(dy.float(), x.float(), (K, R, S, Cin), g)) < 0.1
