@@ -72,6 +72,7 @@ ConvArgs conv_args(const Tensor& x_like, const Tensor& w_like, int64_t N, int64_
   a.N = N; a.H = H; a.W = W; a.C = C; a.K = K; a.R = R; a.S = S;
   a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
   a.Ho = Ho; a.Wo = Wo;
+  a.eH = H; a.eW = W; a.esh = sh; a.esw = sw;
   (void)x_like; (void)w_like;
   return a;
 }
@@ -387,9 +388,14 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
   a.w_flip_bytes = 0;
   if (w_flip.has_value() && w_flip->defined()) {
     CHECK_T(*w_flip, torch::kBFloat16);
-    TORCH_CHECK(w_flip->dim() == 4 && w_flip->size(0) == a.C && w_flip->size(1) == a.R &&
-                w_flip->size(2) == a.S && w_flip->size(3) == a.K && w_flip->is_contiguous(),
-                "conv_dgrad w_flip must be the [C,R,S,K] flipped transpose of w");
+    if (sh == 1 && sw == 1) {
+      TORCH_CHECK(w_flip->dim() == 4 && w_flip->size(0) == a.C && w_flip->size(1) == a.R &&
+                  w_flip->size(2) == a.S && w_flip->size(3) == a.K && w_flip->is_contiguous(),
+                  "conv_dgrad w_flip must be the [C,R,S,K] flipped transpose of w");
+    } else {  // strided: the per-parity-class flipped sub-filters, concatenated (ops/conv.py)
+      TORCH_CHECK(w_flip->is_contiguous() && w_flip->numel() == a.C * a.R * a.S * a.K,
+                  "conv_dgrad w_flip (strided): the class sub-filters, C*R*S*K elements");
+    }
     a.w_flip = BF(*w_flip);
     a.w_flip_bytes = nbytes32(*w_flip);
   }

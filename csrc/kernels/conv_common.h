@@ -210,9 +210,9 @@ __device__ __forceinline__ long out_row(const ConvArgs& a, const Tile& T, int m)
     const int c = T.cls;
     const int Hc = a.cls_Hc[c], Wc = a.cls_Wc[c];
     const int n = m / (Hc * Wc), rem = m - n * Hc * Wc, i = rem / Wc, j = rem - i * Wc;
-    const int psh = a.dg_masked ? 1 : a.sh, psw = a.dg_masked ? 1 : a.sw;
+    const int psh = a.dg_masked ? 1 : a.esh, psw = a.dg_masked ? 1 : a.esw;
     const int h = a.cls_a[c] + psh * i, w = a.cls_b[c] + psw * j;
-    return ((long)n * a.H + h) * a.W + w;
+    return ((long)n * a.eH + h) * a.eW + w;
   } else {
     return m;
   }
@@ -244,11 +244,11 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
     const uint32_t rem = (uint32_t)m - n * Hc * Wc;
     const uint32_t i = fdiv(rem, a.cls_fdW[c]);
     const uint32_t j = rem - i * Wc;
-    const uint32_t psh = DGM && a.dg_masked ? 1u : (uint32_t)a.sh;
-    const uint32_t psw = DGM && a.dg_masked ? 1u : (uint32_t)a.sw;
+    const uint32_t psh = DGM && a.dg_masked ? 1u : (uint32_t)a.esh;
+    const uint32_t psw = DGM && a.dg_masked ? 1u : (uint32_t)a.esw;
     const uint32_t h = (uint32_t)a.cls_a[c] + psh * i;
     const uint32_t w = (uint32_t)a.cls_b[c] + psw * j;
-    return (n * (uint32_t)a.H + h) * (uint32_t)a.W + w;
+    return (n * (uint32_t)a.eH + h) * (uint32_t)a.eW + w;
   } else {
     return (uint32_t)m;
   }

@@ -861,7 +861,9 @@ __global__ void zero_fill_kernel(uint32_t* __restrict__ p, long n4) {
   if (blockIdx.x == 0 && threadIdx.x < (n4 & 3)) p[n16 * 4 + threadIdx.x] = 0u;
 }
 
-static void zero_fill(void* p, uint32_t bytes, hipStream_t st) {
+void conv_zero_fill(void* p, uint32_t bytes, hipStream_t st);
+static void zero_fill(void* p, uint32_t bytes, hipStream_t st) { conv_zero_fill(p, bytes, st); }
+void conv_zero_fill(void* p, uint32_t bytes, hipStream_t st) {
   const long n4 = bytes / 4;
   const int blocks = (int)std::min<long>(2048, std::max<long>(1, (n4 / 4 + 255) / 256));
   hipLaunchKernelGGL(zero_fill_kernel, dim3(blocks), dim3(256), 0, st, (uint32_t*)p, n4);
@@ -933,7 +935,8 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   const bool stats = nz > 0 && dgrad_stats_fusable(a);
   const int flags = (stats ? RF_STATS : 0) | (a.beta ? RF_JOIN : 0) |
                     (stats && a.beta ? RF_STATS_JOIN : 0) | (a.aff ? RF_AFF : 0) |
-                    (a.fp8 ? RF_FP8 : 0) | (s1 && a.w_flip ? RF_WFLIP : 0);
+                    (a.fp8 ? RF_FP8 : 0) | (!masked && a.w_flip ? RF_WFLIP : 0) |
+                    (!s1 && !masked ? RF_STRIDED : 0);
   RouteProblem p = route_problem(1, a, flags);
   p.ncls = nz;
   p.rows = 0;
@@ -949,8 +952,8 @@ bool conv_dgrad_launch(const ConvArgs& a0, hipStream_t st) {
   for (int i = route_next(p, -1); i >= 0; i = route_next(p, i)) {
     const RouteRule& r = route_rule(i);
     bool fused = false, ran = false;
-    if (r.impl == RT_ASFWD) {
-      ran = s1 && conv_dgrad_as_fwd(a_s1, a.w_flip, a.w_flip_bytes, route_cfg(i), st, &fused);
+    if (r.impl == RT_ASFWD) {  // (strided: per-class forward convs, conv_glds.hip)
+      ran = !masked && conv_dgrad_as_fwd(a_s1, a.w_flip, a.w_flip_bytes, route_cfg(i), st, &fused);
     } else if (r.impl == RT_HALO) {
       ran = s1 && conv_dgrad_halo(a_s1, st, &fused);
     } else {

@@ -1195,11 +1195,112 @@ bool conv_fwd_glds(const ConvArgs& a0, int cfg, hipStream_t st) {
 // K-contiguous, no transposed LDS reads, no parity-class bookkeeping) with the DGRAD epilogue
 // (DEPI: ReLU bit mask, residual join, BN-backward statistics).  bench/dgrad_paths.py, ResNet-50
 // b1024: 3×3 dgrads 22–31 % faster than the DGRAD kernel, 1×1 3–15 %.
+// Strided (sh, sw > 1, no dilation): one forward conv of dy per parity class (a, b) of dx.  Class
+// (a, b) — pixels h = a + sh·i, w = b + sw·j — receives only the taps r ≡ a + ph (mod sh),
+// s ≡ b + pw (mod sw): Th × Tw of them, so it is a stride-1 Th × Tw forward conv over dy with
+// padding Th − 1 − (a + ph − r0)/sh, whose filter is that class's flipped sub-filter
+// (w_flip: the classes' [C][Th][Tw][K] sub-filters concatenated a-major, empty classes skipped —
+// ops/conv.py flip_classes), and whose DGRAD epilogue scatters class row (n, i, j) to dx pixel
+// (n, a + sh·i, b + sw·j) (ConvArgs::esh / esw / eH / eW).  Classes without taps are zero-filled
+// first unless the dgrad accumulates.  bench/dgrad_strided.py, ResNet-50 b1024: 3×3 / s2 dgrads
+// 1.2–1.8×, 1×1 / s2 1.9–2.2× (before the zero fill).
+static bool dgrad_as_fwd_strided(const ConvArgs& a0, const bf16_t* wf, int cfg, hipStream_t st,
+                                 bool* fused) {
+  if (a0.dh != 1 || a0.dw != 1 || (cfg != 0 && cfg != 4)) return false;
+  const int sh = a0.sh, sw = a0.sw;
+  if (sh > 16 || sw > 16) return false;
+  struct Cls { int a, r0, T, p, Hc; };
+  Cls rows[16], cols[16];
+  auto classes = [](int s, int R, int pad, int H, Cls* out) {
+    for (int a = 0; a < s; ++a) {
+      const int r0 = ((a + pad) % s + s) % s;
+      const int T = r0 < R ? (R - r0 + s - 1) / s : 0;
+      const int e = (a + pad - r0) / s;  // exact: r0 ≡ a + pad (mod s)
+      out[a] = Cls{a, r0, T, T - 1 - e, a < H ? (H - a + s - 1) / s : 0};
+    }
+  };
+  classes(sh, a0.R, a0.ph, a0.H, rows);
+  classes(sw, a0.S, a0.pw, a0.W, cols);
+  // (a class's padding Th − 1 − e may be negative — stride > kernel reach, e.g. 3×3 / s3: the
+  // forward K loop's gather is plain arithmetic on ho − ph, range-checked against dy)
+  bool any_empty = false;
+  for (int i = 0; i < sh; ++i)
+    for (int j = 0; j < sw; ++j) {
+      const Cls &r = rows[i], &c = cols[j];
+      if (r.T == 0 || c.T == 0 || r.Hc == 0 || c.Hc == 0) any_empty = true;
+    }
+  const bool stats = a0.stats != nullptr && a0.bn_x != nullptr;
+  if (stats && a0.beta) return false;
+  if (any_empty && !a0.beta) conv_zero_fill(a0.out, a0.out_bytes, st);
+  long off = 0;
+  for (int i = 0; i < sh; ++i)
+    for (int j = 0; j < sw; ++j) {
+      const Cls &r = rows[i], &c = cols[j];
+      if (r.T == 0 || c.T == 0) continue;
+      const long nsub = (long)a0.C * r.T * c.T * a0.K;
+      if (r.Hc == 0 || c.Hc == 0) {
+        off += nsub;
+        continue;
+      }
+      ConvArgs a = a0;
+      a.x = a0.dy;
+      a.x_bytes = a0.dy_bytes;
+      a.w = wf + off;
+      a.w_bytes = (uint32_t)(nsub * 2);
+      a.w_t = nullptr;
+      a.C = a0.K;  // input channels of the forward conv: dy's
+      a.K = a0.C;  // its output channels: dx's
+      a.R = r.T;
+      a.S = c.T;
+      a.sh = a.sw = 1;
+      a.ph = r.p;
+      a.pw = c.p;
+      a.H = a0.Ho;  // the forward's input: dy
+      a.W = a0.Wo;
+      a.Ho = r.Hc;  // its output: the class grid
+      a.Wo = c.Hc;
+      a.M = a.N * a.Ho * a.Wo;
+      a.Ng = a.K;
+      a.Kg = a.R * a.S * a.C;
+      a.relu = 0;
+      a.ncls = 1;
+      a.cls_a[0] = r.a;
+      a.cls_b[0] = c.a;
+      a.cls_Hc[0] = r.Hc;
+      a.cls_Wc[0] = c.Hc;
+      a.cls_r0[0] = a.cls_s0[0] = 0;
+      a.cls_Th[0] = a.R;
+      a.cls_Tw[0] = a.S;
+      a.eH = a0.H;  // the epilogue's scatter into dx
+      a.eW = a0.W;
+      a.esh = sh;
+      a.esw = sw;
+      a.dbg = 0;
+      a.splits = 1;
+      a.stats = stats ? a0.stats : nullptr;
+      set_fastdivs(a);
+      const int blocks = fwd_tiling(a, cfg_of(cfg));
+      if (cfg == 4) {
+        if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
+        else launch_g<FWD, 256, 64, 8, 1, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
+      } else {
+        if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
+        else launch_g<FWD, 256, 128, 4, 2, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
+      }
+      off += nsub;
+    }
+  if (fused) *fused = stats;
+  return true;
+}
+
 // cfg (the route row's): 0 / 4 the LDS-DMA K loop with 256×128 / 8-wave 256×64 tiles, 100 the
 // halo forward loader, 102 the producer/consumer kernel.
 bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, int cfg,
                        hipStream_t st, bool* fused) {
   if (fused) *fused = false;
+  if (wf != nullptr && (a0.sh > 1 || a0.sw > 1) && !a0.fp8 && !a0.aff && !a0.dg_masked &&
+      a0.K % 64 == 0 && a0.C % 8 == 0 && a0.ldc == a0.C)
+    return dgrad_as_fwd_strided(a0, wf, cfg, st, fused);
   if (wf == nullptr || a0.fp8 || a0.aff || a0.dg_masked) return false;
   if (a0.sh != 1 || a0.sw != 1 || a0.K % 64 || a0.C % 8 || a0.ldc != a0.C) return false;
   // the DGRAD epilogue indexes dx through dy's geometry: same spatial size ("same" padding)

@@ -30,6 +30,7 @@ enum RouteFlag {
   RF_BIAS = 32,   // FWD bias
   RF_WFLIP = 64,  // DGRAD: the flipped filter is available (dgrad as a forward conv)
   RF_STATS_JOIN = 128,  // DGRAD: statistics together with a join (only the 8-wave stats tiles)
+  RF_STRIDED = 256,     // DGRAD: stride > 1 without dilation (parity classes)
 };
 
 struct RouteRule {

@@ -66,6 +66,10 @@ const RouteRule kRoutes[] = {
    "stride-1 dgrad as the forward conv: LDS-DMA K loop, DGRAD epilogue (profiles/r05_dgrad_as_fwd.txt)"},
   {"dgrad.asfwd.glds",            DGRAD, RT_ASFWD, 1, TAPS,  1, 65, INF,     64, INF,     4096,  256, 128, 128, RF_WFLIP,         RF_STATS_JOIN | RF_AFF | RF_FP8,      0,    true,  false,
    "stride-1 dgrad as the forward conv: LDS-DMA K loop, DGRAD epilogue (profiles/r05_dgrad_as_fwd.txt)"},
+  {"dgrad.asfwd.strided.n64",     DGRAD, RT_ASFWD, 1, TAPS,  0, 8, 64,       64, INF,     4096,  256, 64,  128, RF_WFLIP | RF_STRIDED, RF_STATS_JOIN | RF_AFF | RF_FP8, 4, true, false,
+   "strided dgrad as one forward conv of dy per parity class (bench/dgrad_strided.py)"},
+  {"dgrad.asfwd.strided",         DGRAD, RT_ASFWD, 1, TAPS,  0, 65, INF,     64, INF,     4096,  256, 128, 128, RF_WFLIP | RF_STRIDED, RF_STATS_JOIN | RF_AFF | RF_FP8, 0, true, false,
+   "strided dgrad as one forward conv of dy per parity class: 3x3/s2 1.2-1.8x, 1x1/s2 1.9-2.2x (bench/dgrad_strided.py)"},
   {"dgrad.halo",                  DGRAD, RT_HALO,  3, HT,    1, 8, INF,      64, INF,     0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                      0,    true,  true,
    "tests only: the halo dgrad lost to the implicit GEMMs on every measured shape (profiles/r04_halo_ab.txt)"},
   {"dgrad.glds.stats.aff.n64",    DGRAD, RT_GLDS,  1, TAPS,  1, 49, 64,      8, INF,      4096,  256, 64,  128, RF_STATS | RF_AFF, RF_FP8,                              4,    true,  false,

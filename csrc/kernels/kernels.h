@@ -69,6 +69,11 @@ struct ConvArgs {
   // DGRAD parity classes (stride s: s_h·s_w classes of input pixels, each with its exact taps)
   int ncls;
   int dg_masked;     // 1: stride>1 with dilation>1 — single class, divisibility-masked taps
+  // DGRAD epilogue scatter geometry (out_row_fast<DGRAD>): dx pixel of class row (n, i, j) =
+  // (n, cls_a + esh·i, cls_b + esw·j) in an eH × eW image — the conv's own H, W, sh, sw
+  // (conv_args), except for a strided input gradient run as per-class forward convs of dy
+  // (conv_dgrad_as_fwd), whose K loop sees stride 1 over dy's Ho × Wo
+  int eH, eW, esh, esw;
   int cls_tile0[17]; // prefix sum of tiles per class
   int cls_a[16], cls_b[16], cls_Hc[16], cls_Wc[16];
   int cls_r0[16], cls_Th[16], cls_s0[16], cls_Tw[16];
@@ -130,6 +135,8 @@ bool conv_fwd_pc_launch(const ConvArgs& a, int blocks, int fk, int mode, hipStre
 // not eligible, nothing launched
 bool conv_dgrad_as_fwd(const ConvArgs& a, const bf16_t* w_flip, uint32_t w_flip_bytes, int cfg,
                        hipStream_t st, bool* fused);
+// zero a byte range (multiple of 4) with a kernel (graph-capturable, stream-ordered)
+void conv_zero_fill(void* p, uint32_t bytes, hipStream_t st);
 // w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c] (bf16)
 void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, int C,
                              hipStream_t st);

@@ -242,6 +242,22 @@ class Conv2d(nn.Module):
         self.__dict__["_flip"] = (v, wf)
         return wf
 
+    def flip_weight_classes(self, w, geom):
+        """The per-parity-class flipped sub-filters of this strided conv (ops/conv.flip_classes),
+        rebuilt once per parameter version into a persistent buffer (HIP-graph replays refresh
+        it in place)."""
+        from ..ops.conv import flip_classes
+        v = _params.version()
+        c = self.__dict__.get("_flipc")
+        if c is not None and c[0] == v and c[1].device == w.device:
+            return c[1]
+        f = flip_classes(w, geom)
+        if c is not None and c[1].device == w.device and c[1].shape == f.shape:
+            c[1].copy_(f)
+            f = c[1]
+        self.__dict__["_flipc"] = (v, f)
+        return f
+
     def compute_bias(self):
         """fp32 bias as the kernels read it, ``_cout_store`` long with zero padding channels (the
         flat master buffer's slack when flat-backed, else a padded copy)."""

@@ -222,10 +222,41 @@ DGRAD_AS_FWD = os.environ.get("TDL_DGRAD_AS_FWD", "1") == "1"
 
 def dgrad_as_fwd_ok(dy, x_shape, geom: ConvGeom) -> bool:
     """Can this input gradient run as the forward conv of dy with the flipped filter?  bf16 on the
-    GPU, stride 1, dy channels % 64 (the forward kernels' FASTK), dx channels % 8, dx and dy of
-    the same spatial size (the kernel still declines problems its forward route would not take)."""
-    return (DGRAD_AS_FWD and fused_gpu(dy) and geom.stride == (1, 1) and dy.shape[-1] % 64 == 0
-            and x_shape[-1] % 8 == 0 and tuple(dy.shape[1:3]) == tuple(x_shape[1:3]))
+    GPU, dy channels % 64 (the forward kernels' FASTK), dx channels % 8; stride 1: dx and dy of
+    the same spatial size; strided: no dilation (one forward conv per parity class,
+    :func:`flip_classes`).  The kernel still declines problems its forward route would not take."""
+    if not (DGRAD_AS_FWD and fused_gpu(dy) and dy.shape[-1] % 64 == 0 and x_shape[-1] % 8 == 0):
+        return False
+    if geom.stride == (1, 1):
+        return tuple(dy.shape[1:3]) == tuple(x_shape[1:3])
+    return geom.dilation == (1, 1) and geom.stride[0] <= 16 and geom.stride[1] <= 16
+
+
+def _classes(s, R, pad):
+    """per parity class a of one dimension: the taps it receives, flipped (the forward conv's order)"""
+    out = []
+    for a in range(s):
+        r0 = (a + pad) % s
+        T = (R - r0 + s - 1) // s if r0 < R else 0
+        out.append([r0 + s * (T - 1 - t) for t in range(T)])
+    return out
+
+
+def flip_classes(w, geom: ConvGeom):
+    """The per-parity-class flipped sub-filters of a strided conv's weight w [K, R, S, C], each
+    [C, Th, Tw, K], concatenated a-major over the classes with taps (csrc/kernels/conv_glds.hip
+    dgrad_as_fwd_strided reads them in the same order): class (a, b) of dx is the stride-1
+    forward conv of dy with its sub-filter."""
+    (sh, sw), ph, pw = geom.stride, geom.padding[0], geom.padding[2]
+    R, S = w.shape[1], w.shape[2]
+    parts = []
+    # (strided slices + flips only: no index tensors, so the rebuild is HIP-graph capturable)
+    for rr in _classes(sh, R, ph):
+        for ss in _classes(sw, S, pw):
+            if rr and ss:
+                sub = w[:, rr[-1]:rr[0] + 1:sh, ss[-1]:ss[0] + 1:sw].flip(1, 2)  # [K, Th, Tw, C]
+                parts.append(sub.permute(3, 1, 2, 0).reshape(-1))  # [C, Th, Tw, K]
+    return torch.cat(parts)
 
 
 def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
@@ -451,9 +482,12 @@ class _Conv2dFn(torch.autograd.Function):
                     return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
                                           accumulate=accumulate, mask=mask)
             else:
-                # stride 1: the flipped filter lets the forward kernels compute dx
-                wf = (ctx.layer.flip_weight(w) if ctx.layer is not None and
-                      dgrad_as_fwd_ok(dy, ctx.x_shape, geom) else None)
+                # the flipped filter (strided: per-class sub-filters) lets the forward kernels
+                # compute dx
+                wf = None
+                if ctx.layer is not None and dgrad_as_fwd_ok(dy, ctx.x_shape, geom):
+                    wf = (ctx.layer.flip_weight(w) if geom.stride == (1, 1)
+                          else ctx.layer.flip_weight_classes(w, geom))
 
                 def dgrad(out=None, accumulate=False, mask=None):
                     return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,

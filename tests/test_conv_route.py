@@ -82,6 +82,16 @@ def test_dgrad_variants(e):
     assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f)[0] == "dgrad.glds.stats.join"
     # no flipped filter: the DGRAD kernel
     assert e.conv_route_select(DGRAD, 9, 1, 128, 128, 256 * 28 * 28, S)[0] == "dgrad.glds.stats"
+    # strided with the per-class flipped sub-filters: one forward conv per parity class
+    st = S | W | 256
+    cls = [256 * 28 * 28] * 4
+    assert e.conv_route_select(DGRAD, 9, 2, 128, 128, 256 * 56 * 56, st, cls)[0] == \
+        "dgrad.asfwd.strided"
+    assert e.conv_route_select(DGRAD, 9, 2, 64, 64, 256 * 56 * 56, st, cls)[0] == \
+        "dgrad.asfwd.strided.n64"
+    # ... not with statistics + join
+    assert e.conv_route_select(DGRAD, 1, 2, 256, 512, 256 * 56 * 56, st | J | 128, cls[:1])[0] \
+        == "dgrad.glds.stats.join"
     # fp8 rows ignore the LDS-DMA mode switch (no other kernel has fp8 operands)
     e.conv_set_glds_mode(0)
     assert e.conv_route_select(DGRAD, 9, 1, 64, 128, 4096, F8)[0] == "dgrad.glds.fp8.n64"

@@ -18,7 +18,7 @@ from tensorflowdistributedlearning_amd.ops import bn as B
 
 pytestmark = pytest.mark.gpu
 
-RF_STATS, RF_JOIN, RF_AFF, RF_FP8, RF_WFLIP = 1, 2, 4, 8, 64
+RF_STATS, RF_JOIN, RF_AFF, RF_FP8, RF_WFLIP, RF_STRIDED = 1, 2, 4, 8, 64, 256
 OPS = {"fwd": 0, "dgrad": 1, "wgrad": 2}
 
 
@@ -98,7 +98,8 @@ def _run_dgrad(r, gpu, N, H, k, cin, cout, g):
     e = _ext()
     need = r["need"]
     w = (torch.randn(cout, k, k, cin) / math.sqrt(k * k * cout)).bfloat16().to(gpu)
-    dy = torch.randn(N, H, H, cout).bfloat16().to(gpu)
+    Ho, _ = g.out_hw(H, H, k, k)
+    dy = torch.randn(N, Ho, Ho, cout).bfloat16().to(gpu)
     if need & RF_FP8:
         from tensorflowdistributedlearning_amd.ops import fp8 as F8
         dy8, sdy = F8.quantize_e5m2(dy)
@@ -123,7 +124,9 @@ def _run_dgrad(r, gpu, N, H, k, cin, cout, g):
         B.bn_apply(x, aff, None, True, mask=mask)
         ref = ref * B.unpack_relu_mask(mask.cpu(), cin).reshape(ref.shape)
     wf = None
-    if need & RF_WFLIP:
+    if need & RF_STRIDED:
+        wf = C.flip_classes(w, g)
+    elif need & RF_WFLIP:
         wf = torch.empty(cin, k, k, cout, device=gpu, dtype=torch.bfloat16)
         e.conv_flip_weight(w, wf)
     fused = e.conv_dgrad(dy, w, dx, *_args(g), join, None, None, bn_x, red, aff, wf)
@@ -161,7 +164,8 @@ def test_every_route_row_runs_and_matches_oracle(gpu, name):
     op = OPS[r["op"]]
     k, cin, cout = _problem(r)
     p = (k - 1) // 2
-    g = C.ConvGeom((1, 1), (p, p, p, p), (1, 1))
+    st = 2 if r["need"] & RF_STRIDED else 1
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
     N, H = 4, 14
     torch.manual_seed(zlib.crc32(name.encode()) % 1000)
     e = _ext()

@@ -1256,3 +1256,74 @@ def test_conv_wgrad_fp8(gpu, shape):
     assert rel_err(acc, ref + 1.0) < 1e-3
     # quantisation error only vs the bf16 wgrad of the unquantised data
     assert rel_err(out, C.ref_conv_wgrad(dy.float(), x.float(), (K, R, S, Cin), g)) < 0.1
+
+
+# (N, H, W, Cin, K, k, stride, pad (t, b, l, r)): strided dgrads as one forward conv per parity class
+AS_FWD_STRIDED = [
+    (4, 28, 28, 128, 128, 3, 2, (1, 1, 1, 1)),   # ResNet 3x3 / s2
+    (4, 14, 14, 64, 256, 1, 2, (0, 0, 0, 0)),    # 1x1 / s2: three empty classes (zero fill)
+    (3, 15, 17, 128, 64, 3, 2, (1, 1, 1, 1)),    # odd sizes, 64-wide dx
+    (2, 16, 16, 64, 128, 3, 2, (0, 1, 0, 1)),    # TF SAME asymmetric padding
+    (2, 12, 12, 64, 64, 3, 3, (1, 1, 1, 1)),     # stride 3
+]
+
+
+@pytest.mark.parametrize("shape", AS_FWD_STRIDED)
+@pytest.mark.parametrize("epi", ["plain", "mask", "join", "bnstat"])
+def test_conv_dgrad_as_forward_strided(gpu, shape, epi):
+    """A strided input gradient as one stride-1 forward conv of dy per parity class with that
+    class's flipped sub-filter (ops/conv.flip_classes, conv_glds.hip dgrad_as_fwd_strided) vs the
+    DGRAD kernel and the fp32 oracle, for every DGRAD epilogue: plain, ReLU bit mask, residual
+    join, fused BN-backward statistics."""
+    N, H, W, Cin, K, k, s, pad = shape
+    g = C.ConvGeom((s, s), pad, (1, 1))
+    Ho, Wo = g.out_hw(H, W, k, k)
+    torch.manual_seed(43)
+    w = (torch.randn(K, k, k, Cin) / math.sqrt(k * k * Cin)).bfloat16().to(gpu)
+    wf = C.flip_classes(w, g)
+    assert wf.numel() == w.numel()
+    dy = torch.randn(N, Ho, Wo, K).bfloat16().to(gpu)
+    x = (torch.randn(N, H, W, Cin) * 1.3 + 0.4).bfloat16().to(gpu)
+    mask = None
+    if epi != "plain":
+        gam, bet = torch.rand(Cin, device=gpu) + 0.5, torch.randn(Cin, device=gpu) * 0.3
+        coef = B.bn_finalize(B.bn_stats(x), N * H * W, gam, bet, torch.zeros(Cin, device=gpu),
+                             torch.ones(Cin, device=gpu), 0.9, 1e-3, True)
+        mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+        B.bn_apply(x, coef, None, True, mask=mask)
+    prev = torch.randn(N, H, W, Cin).bfloat16().to(gpu) if epi == "join" else None
+    ext().conv_set_glds_mode(2)
+    try:
+        if epi == "bnstat":
+            ref, red0 = C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask)
+            got, red1 = C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask, w_flip=wf)
+        else:
+            ref = C.conv_dgrad(dy, w, x.shape, g, mask=mask,
+                               out=prev.clone() if prev is not None else None,
+                               accumulate=prev is not None)
+            got = C.conv_dgrad(dy, w, x.shape, g, mask=mask, w_flip=wf,
+                               out=prev.clone() if prev is not None else None,
+                               accumulate=prev is not None)
+        route = ext().conv_last_route(1)
+    finally:
+        ext().conv_set_glds_mode(-1)
+    torch.cuda.synchronize()
+    assert route.startswith("dgrad.asfwd.strided"), route
+    oracle = C.ref_conv_dgrad(dy.float().cpu(), w.float().cpu(), x.shape, g)
+    if prev is not None:
+        oracle = oracle + prev.float().cpu()
+    if mask is not None:
+        # the kernels mask every pixel of a parity class that has taps (whether or not a tap
+        # lands in range); pixels of classes without taps keep the joined value unmasked
+        rows = torch.tensor([len(t) > 0 for t in C._classes(s, k, pad[0])])[torch.arange(H) % s]
+        cols = torch.tensor([len(t) > 0 for t in C._classes(s, k, pad[2])])[torch.arange(W) % s]
+        touched = (rows[:, None] & cols[None, :]).reshape(1, H, W, 1)
+        keep = B.unpack_relu_mask(mask.cpu(), Cin).reshape(oracle.shape)
+        oracle = oracle * (keep | ~touched) if prev is not None else oracle * keep
+    assert rel_err(got, oracle) < 1e-2
+    assert rel_err(got, ref) < 1e-2
+    if epi == "bnstat":
+        assert red1 is not None
+        gf, xf = got.float().reshape(-1, Cin), x.float().reshape(-1, Cin)
+        want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
+        assert rel_err(red1, want) < 1e-4
