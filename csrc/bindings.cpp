@@ -610,7 +610,7 @@ void scale_cols(Tensor dw, Tensor a) {
 
 void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool relu,
               c10::optional<Tensor> y8, c10::optional<Tensor> amax_ring, int64_t phase,
-              c10::optional<Tensor> scale_out, c10::optional<Tensor> mask) {
+              c10::optional<Tensor> scale_out, c10::optional<Tensor> mask, bool store_y) {
   if (is_f32(x)) {
     CHECK_T(x, torch::kFloat32);
     CHECK_T(coef, torch::kFloat32);
@@ -654,8 +654,12 @@ void bn_apply(Tensor x, Tensor coef, c10::optional<Tensor> res, Tensor y, bool r
                 "relu bit mask: uint8 [numel/8], C % 8 == 0");
     maskp = (uint8_t*)mask->data_ptr();
   }
-  bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), BFW(y), x.numel() / C, C, relu,
-                  stream(), y8p, prev, optfw(scale_out), out, zero, maskp, ldy);
+  // store_y = false: only the e4m3 copy (and mask / amax) — an fp8-only BN output whose every
+  // consumer reads the e4m3 tensor (ops/bn.py, models.enable_fp8)
+  TORCH_CHECK(store_y || (y8p != nullptr && C % 8 == 0), "bn_apply store_y=False needs the e4m3 copy");
+  bn_apply_launch(BF(x), coef.data_ptr<float>(), optb(res), store_y ? BFW(y) : nullptr,
+                  x.numel() / C, C, relu, stream(), y8p, prev, optfw(scale_out), out, zero, maskp,
+                  ldy);
 }
 
 // relu mode 3: `y` is the uint8 bit mask bn_apply wrote (vector kernels only: C % 8 == 0 and
@@ -1491,7 +1495,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply, py::arg("x"), py::arg("coef"), py::arg("res"), py::arg("y"),
         py::arg("relu"), py::arg("y8") = py::none(), py::arg("amax_ring") = py::none(),
-        py::arg("phase") = 0, py::arg("scale_out") = py::none(), py::arg("mask") = py::none());
+        py::arg("phase") = 0, py::arg("scale_out") = py::none(), py::arg("mask") = py::none(),
+        py::arg("store_y") = true);
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_reduce2", &bn_bwd_reduce2);
   m.def("bn_bwd_apply", &bn_bwd_apply, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("coef"),

@@ -450,7 +450,8 @@ __global__ void __launch_bounds__(NT) apply_vec_kernel(const bf16_t* __restrict_
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
     }
     const uint4 packed = pack8(v);
-    st16<NTM>(y, ldy_v == cvecs ? k : (k / cvecs) * ldy_v + k % cvecs, packed);
+    // (y == nullptr: e4m3 copy only — an fp8-only BN output, ops/bn.py)
+    if (y) st16<NTM>(y, ldy_v == cvecs ? k : (k / cvecs) * ldy_v + k % cvecs, packed);
     if (mask) {  // ReLU mask of the stored bf16 values, one bit per element (backward relu mode 3)
       float q[8];
       unpack8(packed, q);

@@ -41,6 +41,8 @@ const RouteRule kRoutes[] = {
    "LDS-DMA 256x128 tiles for >= 128 outputs; < 128 tiles stay on the GEMM (DeepLab 13x13x1024->256 b64: 20.6 vs 25.0 us)"},
   {"fwd.glds.1x1n64",             FWD,   RT_GLDS,  1, 1,     0, 8, INF,      49, 64,      4096,  256, 64,  128, 0,                RF_AFF | RF_FP8,                      4,    true,  false,
    "1x1 with 64 outputs: 8-wave 256x64 tiles, 35 vs 53 us on 56x56 64->64 (profiles/r02_conv_n64_configs.txt)"},
+  {"fwd.glds.stem",               FWD,   RT_GLDS,  2, TAPS,  0, 8, 32,       49, 64,      65536, 256, 64,  128, 0,                RF_AFF | RF_FP8,                      4,    false, false,
+   "opt-in: row-packed ResNet stem (7 taps x 24 channels -> 64) on 8-wave 256x64 tiles, 914 vs 1017 us alone at b1024 but no step gain (13,386 / 13,398 vs 13,396 / 13,435 img/s; profiles/r05_stem_ab.txt)"},
   {"fwd.pc.aligned.aff",          FWD,   RT_PC,    1, TAPS,  0, 64, INF,     65, INF,     0,     0, 0,     0,  RF_AFF,             RF_BIAS | RF_RES | RF_FP8,            0,    true,  true,
    "tests: folded-BN forwards of any size"},
   {"fwd.pc.aligned",              FWD,   RT_PC,    2, TAPS,  0, 256, INF,    65, INF,     0,     0, 0,     0,  0,                  RF_AFF | RF_RES | RF_FP8,             0,    true,  true,
@@ -106,7 +108,7 @@ const RouteRule kRoutes[] = {
   {"wgrad.halo.aligned",          WGRAD, RT_HALO,  9, 9,     1, 64, INF,     8, INF,      0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  true,
    "tests: every eligible problem on the halo kernel"},
   {"wgrad.glds.stem",             WGRAD, RT_GLDS,  1, TAPS,  0, 1, 32,       1, 64,       65536, 0, 0,     0,  0,                  RF_AFF | RF_FP8,                               7,    false, false,
-   "opt-in: one 64x256 tile column for the row-packed stem, 1120 vs 1040 us (profiles/r03_stem_wgrad_ab.txt)"},
+   "opt-in: one 64x256 tile column for the row-packed stem — slower (r03: 1120 vs 1040 us; r05: 11.6 vs 0.97 ms, profiles/r05_stem_ab.txt)"},
   {"wgrad.glds.1x1",              WGRAD, RT_GLDS,  1, 1,     0, 8, INF,      256, INF,    4096,  0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  false,
    "1x1 with >= 256 outputs on the LDS-DMA kernel (3x3 gathers of x favour the others; README round-4 A/B)"},
   {"wgrad.glds.aligned.m128",     WGRAD, RT_GLDS,  1, TAPS,  0, 8, INF,      1, 128,      0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                               2,    true,  true,

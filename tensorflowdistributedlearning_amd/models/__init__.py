@@ -56,6 +56,16 @@ def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None, wgrad=None):
     for m in model.modules():
         if isinstance(m, Conv2d) and getattr(m, "fp8", False):
             m.fp8_dgrad, m.fp8_wgrad = bool(dgrad), bool(wgrad)
+    if wgrad and fuse_bn and isinstance(model, ResNet) and all(s is not None for s in stages):
+        # a block's inner BNs (bn1 → conv2, bn2 → conv3) have one consumer each; when it is an
+        # fp8 conv with an fp8 weight gradient, nothing reads their bf16 output: write e4m3 only
+        for _, b in [(si, b) for si, st in enumerate(stages) for b in st]:
+            inner = _block_convbns(b)
+            for j in range(len(inner) - 1):
+                nxt = inner[j + 1].conv
+                inner[j].bn.fp8_only = bool(
+                    inner[j].bn.emit_fp8 and getattr(nxt, "fp8_wgrad", False) and nxt.bias is None
+                    and not nxt.grad_needs_unpad() and nxt.cin % 16 == 0 and nxt.cout % 16 == 0)
     if dgrad or wgrad:
         for m in model.modules():
             if isinstance(m, ConvBN) and getattr(m.conv, "fp8", False):

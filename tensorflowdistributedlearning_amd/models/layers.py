@@ -446,6 +446,7 @@ class BatchNorm(nn.Module):
         return (None if g is None else pad(self.gamma, g)), pad(self.beta, b)
 
     emit_fp8 = False  # set by models.enable_fp8: also emit an e4m3 copy for the fp8 consumer conv
+    fp8_only = False  # … and write only that copy (every consumer is an fp8 conv with fp8 wgrad)
 
     def fp8_state(self, x):
         """(amax ring, phase, scale, emit) for the delayed-scaling e4m3 side output of bn_apply

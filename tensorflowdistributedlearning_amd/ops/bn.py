@@ -72,13 +72,16 @@ def bn_finalize(stats, count, gamma, beta, running_mean, running_var, decay, eps
     return torch.stack([scale, shift, mean, invstd])
 
 
-def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None, out=None):
+def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None, out=None, store_y=True):
     """``out``: write y there instead (e.g. a channel slice ``buf[..., c0:c0+C]`` of a wider
     NHWC concat buffer — the kernel takes its pixel stride; no fp8 side output then).
     ``fp8`` = (amax_ring fp32[3], phase, scale fp32[1], emit): also write an e4m3 copy of y
     scaled by the previous call's |y|max (delayed scaling) — returned as ``y._tdl_fp8`` =
     (y8, scale) for an fp8 consumer conv (ops/conv.py) when ``emit``.  ``mask`` (uint8
-    [numel/8], GPU): also write the ReLU mask y > 0 as one bit per element (relu mode 3)."""
+    [numel/8], GPU): also write the ReLU mask y > 0 as one bit per element (relu mode 3).
+    ``store_y=False`` (with an emitted e4m3 copy): y is NOT written — an fp8-only output whose
+    every consumer reads ``y._tdl_fp8`` (models.enable_fp8 marks such BNs ``fp8_only``); the
+    returned y is then an unwritten buffer carrying the shape and the attributes."""
     if out is not None and fp8 is not None:
         raise ValueError("bn_apply: no fp8 side output into a strided destination")
     if on_gpu(x):
@@ -89,7 +92,7 @@ def bn_apply(x, coef, residual=None, relu=True, fp8=None, mask=None, out=None):
         ring, phase, scale, emit = fp8
         y8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e4m3fn) if emit else None
         ext().bn_apply(x, coef, residual, y, bool(relu), y8.view(torch.uint8) if emit else None,
-                       ring, int(phase), scale, mask)
+                       ring, int(phase), scale, mask, store_y=bool(store_y or not emit))
         if emit:
             y._tdl_fp8 = (y8, scale)
         return y
@@ -258,7 +261,13 @@ class _BatchNormActFn(torch.autograd.Function):
             # without a residual only for the fused-statistics path: the consuming conv's dgrad
             # applies the mask and accumulates this BN's backward sums (ops/gradjoin.py)
             mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8)
-        y = bn_apply(x, coef, residual, relu, fp8, mask)
+        # fp8-only output (models.enable_fp8): every consumer is an fp8 conv that reads the e4m3
+        # copy and keeps it for its weight gradient — the bf16 y is not written
+        # (no residual: the backward never saves y — relu mode 3 reads the bit mask, mode 2
+        # recomputes from x; a ReLU without the mask would leave y > 0 to a depthwise consumer)
+        fp8_only = (fp8 is not None and getattr(bn, "fp8_only", False) and residual is None
+                    and (mask is not None or not relu))
+        y = bn_apply(x, coef, residual, relu, fp8, mask, store_y=not fp8_only)
         ctx.mask_token = None
         if mask is not None:  # the consumers' dgrads may apply it for us (ops/gradjoin.py)
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask, x)

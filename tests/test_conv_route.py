@@ -100,6 +100,13 @@ def test_dgrad_variants(e):
     assert e.conv_route_select(DGRAD, 9, 1, 128, 64, rows, F8) == []
 
 
+def test_stem_forward_row(e):
+    # the row-packed stem: 7 taps x 24 channels -> 64 at 112x112 (b256)
+    assert e.conv_route_select(FWD, 7, 2, 24, 64, 256 * 112 * 112, S)[0] == "fwd.gemm"  # opt-in
+    e.conv_route_set("fwd.glds.stem", on=1)
+    assert e.conv_route_select(FWD, 7, 2, 24, 64, 256 * 112 * 112, S)[0] == "fwd.glds.stem"
+
+
 def test_small_problems_stay_on_the_gemm(e):
     # < 128 tiles of 256x128: the register-staged kernel (DeepLab 13x13x1024->256 at b64)
     assert e.conv_route_select(FWD, 1, 1, 1024, 256, 64 * 13 * 13, 0)[0] == "fwd.gemm"
