@@ -27,8 +27,15 @@ def conv_list(model, batch, image):
         dl = mod.dilation[0]
         # minimum HBM bytes (bf16): input + output activations + weights, each touched once
         by = 2.0 * (batch * (H * W * C + Ho * Wo * K) + K * C * mod.k[0] * mod.k[1])
+        # launches of its input gradient as forward convs of dy: one per parity class with taps
+        g = mod._geom_cache.get((H, W))
+        ncls = 1
+        if g is not None and st > 1:
+            from tensorflowdistributedlearning_amd.ops.conv import _classes
+            ncls = sum(1 for r in _classes(st, mod.k[0], g.padding[0]) if r) * \
+                sum(1 for c in _classes(st, mod.k[1], g.padding[2]) if c)
         out.append((f"{H}x{W}x{C}->{Ho}x{Wo}x{K} k{mod.k[0]} s{st}" + (f" d{dl}" if dl > 1 else ""), fl, by,
-                    2.0 * batch * H * W * C))
+                    2.0 * batch * H * W * C, ncls))
     for mod in m.modules():
         if isinstance(mod, Conv2d):
             mod.register_forward_hook(hook)
@@ -68,6 +75,13 @@ def main():
             impl, mode = "pc", 0
         elif "conv_halo_wgrad_kernel<" in name:
             impl, mode = "halo", 2
+        # dgrad as the forward conv of dy (DEPI: the dgrad epilogue on a forward kernel)
+        tp = re.search(r"conv_(glds|halo|pc)_kernel<([^>]*)>", name)
+        if tp and mode == 0:
+            f = [t.strip() for t in tp.group(2).split(",")]
+            at = {"glds": 14, "halo": 10, "pc": 10}[tp.group(1)]
+            if len(f) > at and f[at] == "true":
+                mode = 1
         if impl is not None:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             # fused dgrad operands (conv_glds_kernel<1, …, STATS, …, NJ, …>): the BN-backward
@@ -85,6 +99,16 @@ def main():
     # forward in forward order; dgrad (no stem: its input is the image) and wgrad in reverse
     lists = {0: convs, 1: [c for c in convs[1:]][::-1], 2: convs[::-1]}
     grand = [0.0, 0.0]
+    # a dgrad that ran as forward convs is one launch per parity class: merge them
+    ks1, i = [], 0
+    for c in lists[1]:
+        if i < len(by[1]):
+            n = 1 if by[1][i][1] == "gemm" or c[4] == 1 else c[4]
+            grp = by[1][i:i + n]
+            ks1.append((sum(g[0] for g in grp), grp[0][1] + (f"/{n}" if n > 1 else ""), grp[0][2]))
+            i += n
+    if i == len(by[1]):
+        by[1] = ks1
     for mode, nm in ((0, "forward"), (1, "dgrad"), (2, "wgrad")):
         ks, cl = by[mode], lists[mode]
         if len(ks) != len(cl):
@@ -98,7 +122,7 @@ def main():
             continue
         print(f"{nm}:  (bound = max(FLOP / {a.mfma} PF, min bytes / {a.hbm} TB/s))")
         agg = {}
-        for (d, impl, extra), (name, fl, bts, dxb) in zip(ks, cl):
+        for (d, impl, extra), (name, fl, bts, dxb, _) in zip(ks, cl):
             if a.fused_bytes:
                 bts = bts + extra * dxb
             e = agg.setdefault((name, impl), [0, 0.0, fl, bts])
@@ -109,7 +133,7 @@ def main():
             b = bound_us(fl, bts)
             tot[0] += d
             tot[1] += b * n
-            print(f"  {name:32s} {impl:5s} x{n:2d} {d / n:7.1f} us  {fl / (d / n) / 1e6:7.1f} TF/s "
+            print(f"  {name:32s} {impl:7s} x{n:2d} {d / n:7.1f} us  {fl / (d / n) / 1e6:7.1f} TF/s "
                   f"{bts / (d / n) / 1e6:5.2f} TB/s  bound {b:6.1f} us ({b / (d / n) * 100:3.0f} %)  total {d:7.1f} us")
         print(f"  sum {tot[0] / 1e3:.2f} ms, bound {tot[1] / 1e3:.2f} ms ({tot[1] / tot[0] * 100:.0f} %)")
         grand[0] += tot[0]
