@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(ConvArgs a, HaloGeom 
       const int wi = g.ox_min + hc;
       const bool v = hr < hr_total && hc < g.Wo + g.ext_w && (unsigned)hi < (unsigned)g.Hi &&
                      (unsigned)wi < (unsigned)g.Wi;
-      const int lc = (lane & 7) ^ ((s >> 1) & 7);
+      const int lc = (lane & 7) ^ (s & 7);  // slot swizzle: see load_frags
       const int n = t.n_first + k;
       foff[j] = v ? (uint32_t)((((n * g.Hi + hi) * g.Wi + wi) * g.Ci + lc * 8) * 2) : HOOB;
     }
@@ -283,8 +283,12 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(ConvArgs a, HaloGeom 
     const uint32_t d = (uint32_t)g.tap_d[rtp];
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm) {
+      // 16-B chunk c of slot s sits at position c ^ (s & 7): a ds_read_b128 lane group reads 16
+      // consecutive slots (two chunks), conflict-free while a halo row's pitch HP ≡ Wo (mod 8)
+      // keeps the slots consecutive mod 8 across the row wraps (halo_common pads HP to that;
+      // the former (s >> 1) swizzle left 70 % of these reads 2-way conflicted)
       const uint32_t s = slot0[rm] + d;
-      const uint32_t x = ((s >> 1) & 7u) ^ (uint32_t)(kk * 4 + lane_ch);
+      const uint32_t x = (s & 7u) ^ (uint32_t)(kk * 4 + lane_ch);
       af[rm] = hread(hbase + (s << 7) + (x << 4));
     }
     const uint32_t Bs = smem_lds + (uint32_t)(2 * HB + step_slot * B_BYTES);
@@ -725,9 +729,20 @@ bool halo_common(const ConvArgs& a, HaloGeom& g, int R, int S, const int* oy, co
   g.ox_min = ox_min;
   g.ext_h = oy_max - oy_min;
   g.ext_w = ox_max - ox_min;
+  // halo pitch: padded to HP ≡ Wo (mod 8) for conflict-free fragment reads (load_frags), unless
+  // the padding costs output rows per tile
+  g.HP = g.Wo + ((g.ext_w + 7) & ~7);
+  HCfg cp;
+  const bool padded = plan_halo(g, bn, cp);
+  const int tr_padded = padded ? g.TR : 0;
   g.HP = g.Wo + g.ext_w;
-  for (int t = 0; t < g.ntap; ++t) g.tap_d[t] = (oy[t] - oy_min) * g.HP + (ox[t] - ox_min);
   if (!plan_halo(g, bn, cfg)) return false;
+  if (padded && tr_padded >= g.TR) {
+    g.HP = g.Wo + ((g.ext_w + 7) & ~7);
+    g.TR = tr_padded;
+    cfg = cp;
+  }
+  for (int t = 0; t < g.ntap; ++t) g.tap_d[t] = (oy[t] - oy_min) * g.HP + (ox[t] - ox_min);
   g.nrb = cdiv((long)g.N * g.Ho, g.TR);
   g.ncb = cdiv(g.Co, cfg.bn);
   const int cus = henv("TDL_HALO_SLOTS", 256);
