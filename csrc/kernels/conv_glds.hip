@@ -1334,7 +1334,8 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   set_fastdivs(a);
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
   if (!stats) a.stats = nullptr;
-  if (stats && a.beta) return false;  // statistics + join: the DGRAD kernel's 8-wave tiles
+  // statistics + join: only the 8-wave 256×64 tiles (cfg 4; the 256×128 ones spill)
+  if (stats && a.beta && cfg != 4) return false;
   if (cfg == 100) return conv_fwd_halo_depi(a, st, fused);
   if (cfg == 102) {
     // (not with the statistics epilogue: its x registers spill at the 12-wave register budget)
@@ -1345,7 +1346,9 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   if (cfg != 0 && cfg != 4) return false;
   const int blocks = fwd_tiling(a, cfg_of(cfg));
   if (cfg == 4) {
-    if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
+    if (stats && a.beta)  // statistics + join: the 8-wave tiles hold both the x and previous-dx loads
+      launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, false, false, false, false, true>(a, blocks, st);
+    else if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
     else launch_g<FWD, 256, 64, 8, 1, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
   } else {
     if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);

@@ -77,9 +77,12 @@ def test_dgrad_variants(e):
     # no statistics: the producer/consumer dgrad-as-forward for wide 3x3s, the halo one for narrow
     assert e.conv_route_select(DGRAD, 9, 1, 256, 256, 256 * 14 * 14, W)[0] == "dgrad.asfwd.pc"
     assert e.conv_route_select(DGRAD, 9, 1, 64, 64, rows, W)[0] == "dgrad.asfwd.halo"
-    # statistics + join: only the DGRAD kernel's 8-wave tiles
+    # statistics + join: 8-wave tiles only — the forward K loop's with a flipped filter, else the
+    # DGRAD kernel's
     f = S | J | 128 | W
-    assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f)[0] == "dgrad.glds.stats.join"
+    assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f)[0] == "dgrad.asfwd.glds.join"
+    assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f & ~W)[0] == \
+        "dgrad.glds.stats.join"
     # no flipped filter: the DGRAD kernel
     assert e.conv_route_select(DGRAD, 9, 1, 128, 128, 256 * 28 * 28, S)[0] == "dgrad.glds.stats"
     # strided with the per-class flipped sub-filters: one forward conv per parity class
