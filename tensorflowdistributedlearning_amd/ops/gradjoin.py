@@ -42,7 +42,9 @@ MASK_ENABLED = os.environ.get("TDL_PREMASK", "1") == "1"  # 0: the BN applies it
 # single-consumer convs; 3 — only for residual joins.  ResNet-50 b1024 same-box A/B
 # (profiles/r02_bnstat_fuse_ab.txt): 0 11993 / 11999, 1 11994 / 11984, 2 12029 / 12012,
 # 3 11882 / 11840 img/s — the join variant's smaller tiles (the 256×128 ones spill with both the
-# previous-dx and the x loads) lose next to the side-stream weight gradients
+# previous-dx and the x loads) lose next to the side-stream weight gradients.  Round 5, with the
+# joins' statistics on the dgrad-as-forward 8-wave tiles (route row dgrad.asfwd.glds.join): 1
+# 12,990 / 12,992 vs 2 13,179 / 13,170 img/s (dev/scripts/gpu_r05_statsjoin.sh) — still slower
 _FUSE = os.environ.get("TDL_BNSTAT_FUSE", "2")
 STATS_ENABLED = _FUSE != "0"
 STATS_SINGLE = _FUSE in ("1", "2")
