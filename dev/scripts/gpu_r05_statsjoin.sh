@@ -1,4 +1,5 @@
 # dgrad-as-forward statistics + join (8-wave tiles): forced-row oracle test, then same-box A/Bs:
+# (TDL_COMPUTE_PRIORITY was a temporary bench.py knob, removed after this A/B: no gain)
 # TDL_BNSTAT_FUSE=1 (statistics fused into the join's last dgrad) vs the default 2, and the compute
 # stream at a higher HIP priority than the weight-gradient side stream
 set -e
