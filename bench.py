@@ -224,9 +224,11 @@ def main():
         if bc.dtype == "fp8":
             models.enable_fp8(model, dgrad=bc.fp8_dgrad or None)
             dg = any(getattr(m, "emit_fp8_bwd", False) for m in model.modules())
+            wg = any(getattr(m, "fp8_wgrad", False) for m in model.modules())
             st = int(os.environ.get("TDL_FP8_BF16_STAGES", "2"))
-            fp8_desc = (("fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad + BN"
-                         if dg else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / wgrad + BN")
+            fp8_desc = (("fp8 (e4m3 fwd, e5m2 x e4m3 dgrad + wgrad GEMMs, bf16 BN" if dg and wg
+                         else "fp8 (e4m3 fwd, e5m2 x e4m3 dgrad GEMMs, bf16 wgrad + BN" if dg
+                         else "fp8 (e4m3 x e4m3 forward GEMMs, bf16 dgrad / wgrad + BN")
                         + (f"; stages 1-{st} bf16)" if st > 0 else ")"))
         tr = Trainer(model, softmax_cross_entropy, dev, _opt(bc.optimizer), _opt_kw(bc), ctx=ctx,
                      bucket_mb=bc.bucket_mb, first_bucket_mb=bc.first_bucket_mb,

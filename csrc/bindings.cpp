@@ -717,8 +717,9 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
                   c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, double count,
                   int64_t relu, c10::optional<Tensor> dx8, c10::optional<Tensor> amax_ring,
                   int64_t phase, c10::optional<Tensor> scale_out, bool red_raw,
-                  c10::optional<Tensor> dadd) {
+                  c10::optional<Tensor> dadd, bool store_dx) {
   if (is_f32(x)) {
+    TORCH_CHECK(store_dx, "fp32 bn_bwd_apply: dx is always stored");
     CHECK_T(x, torch::kFloat32);
     CHECK_T(dx, torch::kFloat32);
     CHECK_T(coef, torch::kFloat32);
@@ -766,8 +767,13 @@ void bn_bwd_apply(Tensor dy, c10::optional<Tensor> y, Tensor x, Tensor coef, Ten
       d8 = (uint8_t*)dx8->data_ptr();
     }
   }
+  // store_dx == false: only the e5m2 copy is written (every reader of this gradient is an fp8
+  // dgrad / weight gradient, models.enable_fp8 fp8_bwd_only); dx stays an unwritten placeholder
+  TORCH_CHECK(store_dx || (d8 != nullptr && C % 8 == 0),
+              "bn_bwd_apply: store_dx=False needs the e5m2 side output (C % 8 == 0)");
   bn_bwd_apply_launch(BF(dy), mask_or_y(y, x, relu), BF(x), coef.data_ptr<float>(), red.data_ptr<float>(),
-                      optf(gamma), BFW(dx), optbw(dres), optfw(dgamma), optfw(dbeta), x.numel() / C,
+                      optf(gamma), store_dx ? BFW(dx) : nullptr, optbw(dres), optfw(dgamma),
+                      optfw(dbeta), x.numel() / C,
                       C, (float)count, (int)relu, stream(), d8, prev, optfw(scale_out), out, zero,
                       red_raw, ldd, addp);
 }
@@ -1503,7 +1509,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("red"), py::arg("gamma"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("count"), py::arg("relu"), py::arg("dx8") = py::none(),
         py::arg("amax_ring") = py::none(), py::arg("phase") = 0, py::arg("scale_out") = py::none(),
-        py::arg("red_raw") = false, py::arg("dadd") = py::none());
+        py::arg("red_raw") = false, py::arg("dadd") = py::none(), py::arg("store_dx") = true);
   m.def("fp8_quantize_e5m2", [](Tensor x, Tensor ring, int64_t phase, bool measure, Tensor scale,
                                 Tensor y8) {
     CHECK_T(x, torch::kBFloat16);

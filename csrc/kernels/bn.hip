@@ -621,7 +621,7 @@ __global__ void __launch_bounds__(NT) bwd_apply_vec_kernel(
         for (int j = 0; j < 8; ++j) o[j] += va[j];
       }
       const uint4 packed = pack8(o);
-      st16<NTM>(dx, k, packed);
+      if (dx) st16<NTM>(dx, k, packed);  // (null: the e5m2 copy only, bindings bn_bwd_apply)
       if (amax_out) {
         float q[8];
         unpack8(packed, q);  // quantise the stored bf16 values

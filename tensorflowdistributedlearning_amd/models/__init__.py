@@ -67,9 +67,19 @@ def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None, wgrad=None):
                     inner[j].bn.emit_fp8 and getattr(nxt, "fp8_wgrad", False) and nxt.bias is None
                     and not nxt.grad_needs_unpad() and nxt.cin % 16 == 0 and nxt.cout % 16 == 0)
     if dgrad or wgrad:
+        from ..ops.conv import FP8_WGRAD
+        bwd_only = os.environ.get("TDL_FP8_BWD_ONLY", "1") == "1"
         for m in model.modules():
             if isinstance(m, ConvBN) and getattr(m.conv, "fp8", False):
                 m.bn.emit_fp8_bwd = True  # e5m2 dy for the conv's fp8 dgrad / wgrad (ops/conv.py)
+                # … and only that copy when both of the conv's backward GEMMs read it
+                # (ops/conv.fp8_dgrad_eligible / fp8_wgrad_eligible on the conv's static shape)
+                c = m.conv
+                (sh, sw), (dh, dw) = c.stride, c.dilation
+                m.bn.fp8_bwd_only = bool(
+                    dgrad and wgrad and FP8_WGRAD and bwd_only and c.bias is None and not c.relu
+                    and not c.grad_needs_unpad() and c.cout % 128 == 0 and c._cin_store % 16 == 0
+                    and not ((sh > 1 and dh > 1) or (sw > 1 and dw > 1)))
     return n
 
 

@@ -459,6 +459,7 @@ class BatchNorm(nn.Module):
         return sc.bn_args(x)
 
     emit_fp8_bwd = False  # set by models.enable_fp8: e5m2 copy of dx for the fp8 dgrad
+    fp8_bwd_only = False  # … and write only that copy (the conv's dgrad and wgrad are both fp8)
 
     def fp8_bwd_state(self, x):
         """(amax ring, phase, scale, emit) for the e5m2 side output of the backward apply (the

@@ -168,14 +168,16 @@ def bn_red_xhat(red, coef):
 
 
 def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None, dbeta=None,
-                 fp8=None, red_raw=False, dadd=None):
+                 fp8=None, red_raw=False, dadd=None, fp8_only=False):
     """dx (same dtype as x) and optionally the masked gradient g for the residual branch.
     On the GPU, ``dgamma``/``dbeta`` (fp32 [C]) receive Σg·x̂ / Σg from the same launch.
     ``red_raw``: ``red`` holds (Σg, Σg·x) from a fused dgrad epilogue (:func:`bn_red_xhat`).
     ``fp8`` = (amax_ring, phase, scale, emit): also write an e5m2 copy of dx with delayed scaling
     (16× headroom over the previous call's |dx|max: fp8_policy) — attached as ``dx._tdl_fp8`` = (dx8, scale)
     for the fp8 dgrad of the producing conv.  ``dadd`` (shaped like x): another gradient of x
-    added to dx in the same pass."""
+    added to dx in the same pass.  ``fp8_only`` (with an emitting ``fp8``): write only the e5m2
+    copy — the returned bf16 dx is an unwritten placeholder carrying it (every reader of this
+    gradient is the producing conv's fp8 dgrad / weight gradient)."""
     C = x.shape[-1]
     if on_gpu(dy):
         dx = torch.empty_like(x)
@@ -188,7 +190,8 @@ def bn_bwd_apply(dy, y, x, coef, red, gamma, count, relu, want_dres, dgamma=None
         dx8 = torch.empty(x.shape, device=x.device, dtype=torch.float8_e5m2) if emit else None
         ext().bn_bwd_apply(dy, y, x, coef, red, gamma, dx, dres, dgamma, dbeta, float(count),
                            int(relu), dx8.view(torch.uint8) if emit else None, ring, int(phase),
-                           scale, red_raw=bool(red_raw), dadd=dadd)
+                           scale, red_raw=bool(red_raw), dadd=dadd,
+                           store_dx=not (fp8_only and emit and C % 8 == 0))
         if emit:
             dx._tdl_fp8 = (dx8, scale)
         return dx, dres
@@ -357,7 +360,8 @@ class _BatchNormActFn(torch.autograd.Function):
         dx, dres = bn_bwd_apply(dy, y, x, coef, red, gp, count, relu,
                                 ctx.has_res and not premasked and relu != 0,
                                 gt if direct_g else None, bt if direct_b else None, fp8=fp8,
-                                red_raw=red_raw, dadd=extra.contiguous() if fuse_add else None)
+                                red_raw=red_raw, dadd=extra.contiguous() if fuse_add else None,
+                                fp8_only=getattr(ctx.bn, "fp8_bwd_only", False) and extra is None)
         if extra is not None and not fuse_add:
             dx = dx + extra
         if ctx.has_res and (premasked or relu == 0):

@@ -292,6 +292,52 @@ def test_resnet_fp8_dgrad_trains(gpu, depth, monkeypatch):
     assert all(l == l for l in losses) and min(losses[-3:]) < losses[0], losses
 
 
+def test_fp8_bwd_only_bn_gradients_match_stored(gpu, monkeypatch):
+    """BNs whose input gradient is read only by the producing conv's fp8 dgrad and fp8 weight
+    gradient write just its e5m2 copy (models.enable_fp8 ``fp8_bwd_only``; the bf16 dx is an
+    unwritten placeholder): training is bit-identical to writing both (deterministic mode), and
+    the e5m2-only store is taken for every such BN once the scalers have measured."""
+    from tensorflowdistributedlearning_amd.ops import bn as Bmod
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    real = ext()
+    skipped = []
+
+    class Spy:
+        def __getattr__(self, k):
+            return getattr(real, k)
+
+        def bn_bwd_apply(self, *a, **k):
+            if k.get("store_dx", True) is False:
+                skipped.append(1)
+            return real.bn_bwd_apply(*a, **k)
+    monkeypatch.setattr(Bmod, "ext", lambda: Spy())
+    torch.manual_seed(5)
+    init = models.resnet50(num_classes=10).state_dict()
+    x, y = imagenet_batch(16, 64, num_classes=10, device=gpu)
+    real.det_set(1)
+    try:
+        runs = []
+        for only in (True, False):
+            net = models.resnet50(num_classes=10)
+            net.load_state_dict(init)
+            models.enable_fp8(net)
+            flagged = [m for m in net.modules() if getattr(m, "fp8_bwd_only", False)]
+            assert len(flagged) > 10
+            if not only:
+                for m in flagged:
+                    m.fp8_bwd_only = False
+            tr = Trainer(net, softmax_cross_entropy, gpu, "sgd", dict(lr=0.01, momentum=0.9))
+            skipped.clear()
+            losses = [tr.train_step(x, y)[0].clone() for _ in range(4)]
+            torch.cuda.synchronize()
+            runs.append((torch.stack(losses).cpu(), tr.flat.master.clone().cpu(), len(skipped)))
+    finally:
+        real.det_set(-1)
+    assert runs[0][2] >= 3 * len(flagged) and runs[1][2] == 0, (runs[0][2], runs[1][2])
+    assert torch.equal(runs[0][0], runs[1][0]), (runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+
+
 def test_fp8_dgrad_after_zero_gradient_step_is_finite(gpu):
     """A step whose loss gradient is exactly zero leaves |dx|max = 0 for the e5m2 delayed scaling;
     the next step's fp8 dgrad must still read a fully written dx8 (unit fallback scale), not
