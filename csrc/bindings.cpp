@@ -423,9 +423,12 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
 
 // fp8 dgrad: dy8 e5m2 [N,Ho,Wo,K], w8t e4m3 transposed weights [R,S,C,K] (ops/fp8.py), dx bf16
 // [N,H,W,C]; per-tensor scales sdy, sw (device scalars); join accumulate / ReLU mask as conv_dgrad
-void conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, int64_t sh, int64_t sw,
+// bn_x / bn_red (optional): the BN-backward statistics (Σg, Σg·x) of the stored dx in the epilogue,
+// as conv_dgrad (no join); returns whether they were fused
+bool conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, int64_t sh, int64_t sw,
                     int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate,
-                    c10::optional<Tensor> mask) {
+                    c10::optional<Tensor> mask, c10::optional<Tensor> bn_x,
+                    c10::optional<Tensor> bn_red) {
   TORCH_CHECK(dy8.is_cuda() && w8t.is_cuda() && dy8.element_size() == 1 && w8t.element_size() == 1,
               "fp8 operands expected");
   TORCH_CHECK(dy8.is_contiguous() && w8t.is_contiguous(), "contiguous operands expected");
@@ -452,12 +455,27 @@ void conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, i
                 "conv_dgrad mask: uint8 [numel(dx)/8], C % 64 == 0");
     a.mask = (const uint8_t*)mask->data_ptr();
   }
-  if (a.M == 0) return;
+  a.stats = nullptr;
+  a.bn_x = nullptr;
+  if (bn_x.has_value() && bn_x->defined()) {
+    TORCH_CHECK(bn_red.has_value() && bn_red->defined() && !accumulate,
+                "conv_dgrad_fp8: bn_x needs bn_red, no join");
+    CHECK_T(*bn_x, torch::kBFloat16);
+    CHECK_T(*bn_red, torch::kFloat32);
+    TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_red->numel() == 2 * dx.size(3) &&
+                bn_red->is_contiguous(), "conv_dgrad_fp8 bn_x: shape of dx, bn_red fp32 [2, C]");
+    if (!deterministic()) {  // (deterministic mode: the BN reduces itself, no epilogue atomics)
+      a.bn_x = BF(*bn_x);
+      a.stats = bn_red->data_ptr<float>();
+    }
+  }
+  if (a.M == 0) return false;
   try {
-    conv_dgrad_launch(a, stream());
+    return conv_dgrad_launch(a, stream());
   } catch (const std::exception& e) {
     TORCH_CHECK(false, e.what());
   }
+  return false;
 }
 
 // aff (optional): x is the pre-BN tensor of a folded BN + ReLU (dW = dyᵀ · relu(aff[0]·x + aff[1]))
@@ -1490,7 +1508,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_fp8", &conv_fwd_fp8);
   m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dy8"), py::arg("w8t"), py::arg("dx"),
         py::arg("scale_dy"), py::arg("scale_w"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
-        py::arg("dh"), py::arg("dw"), py::arg("accumulate") = false, py::arg("mask") = py::none());
+        py::arg("dh"), py::arg("dw"), py::arg("accumulate") = false, py::arg("mask") = py::none(),
+        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none());
   m.attr("AMAX_SLOT") = AMAX_SLOT;
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_roll", &fp8_roll);

@@ -270,22 +270,25 @@ def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
 
 
 def conv_dgrad_fp8(dy8, sdy, w8t, sw, x_shape, geom: ConvGeom, out=None, accumulate=False,
-                   mask=None):
+                   mask=None, bn_x=None):
     """dx from fp8 operands: ``dy8`` e5m2 [N,Ho,Wo,K] with scale ``sdy``, ``w8t`` the e4m3 weight
     transposed to [R,S,C,K] with scale ``sw`` (ops/fp8.py).  GPU: the LDS-DMA dgrad on
     v_mfma_scale_f32_16x16x128_f8f6f4 (K % 128 == 0); join accumulate / ReLU mask as
-    :func:`conv_dgrad`.  CPU: fp32 on the dequantised operands."""
+    :func:`conv_dgrad`.  CPU: fp32 on the dequantised operands.  With ``bn_x`` (no join) returns
+    ``(dx, red)`` as :func:`conv_dgrad_bnstat`: the BN-backward sums fused into the epilogue."""
     if on_gpu(dy8):
         dx = out if out is not None else torch.empty(x_shape, device=dy8.device,
                                                      dtype=torch.bfloat16)
-        ext().conv_dgrad_fp8(dy8.view(torch.uint8), w8t.view(torch.uint8), dx, sdy, sw,
-                             geom.stride[0], geom.stride[1], geom.padding[0], geom.padding[2],
-                             geom.dilation[0], geom.dilation[1],
-                             bool(accumulate and out is not None), mask)
-        return dx
+        red = workspace.zeros((2, x_shape[-1]), dy8.device) if bn_x is not None else None
+        fused = ext().conv_dgrad_fp8(dy8.view(torch.uint8), w8t.view(torch.uint8), dx, sdy, sw,
+                                     geom.stride[0], geom.stride[1], geom.padding[0],
+                                     geom.padding[2], geom.dilation[0], geom.dilation[1],
+                                     bool(accumulate and out is not None), mask, bn_x, red)
+        return dx if bn_x is None else (dx, red if fused else None)
     w = (w8t.float() * sw).permute(3, 0, 1, 2).contiguous()
-    return conv_dgrad(dy8.float() * sdy, w, x_shape, geom, out=out, accumulate=accumulate,
-                      mask=mask, out_dtype=torch.bfloat16)
+    dx = conv_dgrad(dy8.float() * sdy, w, x_shape, geom, out=out, accumulate=accumulate,
+                    mask=mask, out_dtype=torch.bfloat16)
+    return dx if bn_x is None else (dx, None)
 
 
 def fp8_dgrad_eligible(layer, dy, geom: ConvGeom, w_shape):
@@ -302,6 +305,8 @@ def fp8_dgrad_eligible(layer, dy, geom: ConvGeom, w_shape):
 
 
 FP8_WGRAD = os.environ.get("TDL_FP8_WGRAD", "1") == "1"
+# the BN-backward sums in the fp8 dgrad's epilogue (0: the BN reduces itself, for A/B)
+FP8_DGRAD_STATS = os.environ.get("TDL_FP8_DGRAD_STATS", "1") == "1"
 
 
 def fp8_wgrad_eligible(layer, x, w) -> bool:
@@ -481,6 +486,10 @@ class _Conv2dFn(torch.autograd.Function):
                 def dgrad(out=None, accumulate=False, mask=None):
                     return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
                                           accumulate=accumulate, mask=mask)
+
+                def dgrad_bnstat(bn_x, mask=None):
+                    return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, mask=mask,
+                                          bn_x=bn_x)
             else:
                 # the flipped filter (strided: per-class sub-filters) lets the forward kernels
                 # compute dx
@@ -492,9 +501,13 @@ class _Conv2dFn(torch.autograd.Function):
                 def dgrad(out=None, accumulate=False, mask=None):
                     return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,
                                       mask=mask, w_flip=wf)
+
+                def dgrad_bnstat(bn_x, mask=None):
+                    return conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, bn_x, mask=mask, w_flip=wf)
             join = ctx.join
             masks_ok = fused_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
-            stats_ok = masks_ok and not fp8_dg  # (the kernel decides; strided: parity classes)
+            # (the kernel decides; strided: parity classes; fp8: no join)
+            stats_ok = masks_ok and (not fp8_dg or FP8_DGRAD_STATS)
             if join is None:
                 tok = ctx.bn_tok
                 # a statistics-only token (BN without ReLU) needs no 64-channel mask slabs
@@ -503,10 +516,9 @@ class _Conv2dFn(torch.autograd.Function):
                 if tok is not None and (masks_ok or (fused_gpu(dy) and tok.mask is None)):
                     # sole consumer of a masked BN output: apply the mask here, and fuse the BN's
                     # backward statistics when the kernel can (ops/gradjoin.py)
-                    if (stats_ok or tok.mask is None) and not fp8_dg and tok.x is not None \
+                    if (stats_ok or tok.mask is None) and tok.x is not None \
                             and gradjoin.STATS_SINGLE:
-                        dx, red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, tok.x,
-                                                    mask=tok.mask, w_flip=wf)
+                        dx, red = dgrad_bnstat(tok.x, mask=tok.mask)
                     else:
                         dx, red = dgrad(mask=tok.mask), None
                     tok.mark(dx, red)
@@ -519,8 +531,8 @@ class _Conv2dFn(torch.autograd.Function):
                 if join.buf is None:
                     join.buf = dgrad(mask=mask)
                     join.note(mask is not None)
-                elif (join.last and mask is not None and stats_ok and geom.stride == (1, 1)
-                      and join.stats_x is not None):
+                elif (join.last and mask is not None and stats_ok and not fp8_dg
+                      and geom.stride == (1, 1) and join.stats_x is not None):
                     # the final contribution writes every pixel through the mask: its epilogue
                     # sees the finished gradient and can fuse the BN statistics
                     _, join.red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, join.stats_x,

@@ -697,6 +697,38 @@ def test_conv_dgrad_fp8(gpu, shape, accumulate):
         assert rel_err(dx, C.ref_conv_dgrad(dy.float(), w.float(), (N, H, W, Cin), g)) < 0.15
 
 
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 3, 1, 1), (4, 14, 14, 256, 256, 1, 1, 2, 0),
+                                   (2, 9, 9, 128, 128, 3, 3, 2, 1)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_conv_dgrad_fp8_bnstat(gpu, shape, masked):
+    """fp8 dgrad with the BN-backward statistics in its epilogue (no join): dx as the plain fp8
+    dgrad, and (Σg, Σg·x) of the stored (masked) dx against the same sums computed from it."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    if ext().deterministic():
+        pytest.skip("deterministic mode: no fused epilogue sums")
+    N, H, W, Cin, K, R, S, st, p = shape
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
+    torch.manual_seed(23)
+    Ho, Wo = g.out_hw(H, W, R, S)
+    dy8, sdy = F8.quantize_e5m2(torch.randn(N, Ho, Wo, K).bfloat16().to(gpu))
+    w8, sw = F8.quantize_e4m3((torch.randn(K, R, S, Cin) / math.sqrt(R * S * K)).bfloat16().to(gpu))
+    w8t = F8.transpose_weight(w8)
+    bn_x = (torch.randn(N, H, W, Cin) * 1.5 + 0.3).bfloat16().to(gpu)
+    mask = None
+    if masked:
+        keep = torch.rand(N, H, W, Cin) > 0.4
+        bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)
+        mask = bits.sum(1).to(torch.uint8).to(gpu)
+    plain = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, mask=mask)
+    dx, red = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, mask=mask, bn_x=bn_x)
+    assert red is not None, "fp8 dgrad did not fuse the statistics"
+    assert torch.equal(dx, plain)
+    gf, xf = dx.float().cpu().reshape(-1, Cin), bn_x.float().cpu().reshape(-1, Cin)
+    want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
+    assert rel_err(red.cpu(), want) < 1e-3
+
+
 def test_fp8_e5m2_quantize_and_transpose(gpu):
     from tensorflowdistributedlearning_amd.ops import fp8 as F8
     torch.manual_seed(19)
