@@ -424,7 +424,7 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
 // fp8 dgrad: dy8 e5m2 [N,Ho,Wo,K], w8t e4m3 transposed weights [R,S,C,K] (ops/fp8.py), dx bf16
 // [N,H,W,C]; per-tensor scales sdy, sw (device scalars); join accumulate / ReLU mask as conv_dgrad
 // bn_x / bn_red (optional): the BN-backward statistics (Σg, Σg·x) of the stored dx in the epilogue,
-// as conv_dgrad (no join); returns whether they were fused
+// as conv_dgrad (a join: stride 1 only); returns whether they were fused
 bool conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, int64_t sh, int64_t sw,
                     int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate,
                     c10::optional<Tensor> mask, c10::optional<Tensor> bn_x,
@@ -458,8 +458,7 @@ bool conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, i
   a.stats = nullptr;
   a.bn_x = nullptr;
   if (bn_x.has_value() && bn_x->defined()) {
-    TORCH_CHECK(bn_red.has_value() && bn_red->defined() && !accumulate,
-                "conv_dgrad_fp8: bn_x needs bn_red, no join");
+    TORCH_CHECK(bn_red.has_value() && bn_red->defined(), "conv_dgrad_fp8: bn_x needs bn_red");
     CHECK_T(*bn_x, torch::kBFloat16);
     CHECK_T(*bn_red, torch::kFloat32);
     TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_red->numel() == 2 * dx.size(3) &&

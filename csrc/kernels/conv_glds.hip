@@ -1424,8 +1424,10 @@ void conv_flip_weights_multi_launch(const bf16_t* src, bf16_t* dst, const long* 
 // a class without taps unmasked; a folded BN's mask (a.aff) rides on the single-consumer form
 bool dgrad_stats_fusable(const ConvArgs& a) {
   if (!a.stats || !a.bn_x || a.dg_masked) return false;
-  // fp8 (e5m2 dy × e4m3 Wᵀ, K % 128 == 0): the statistics epilogue without a join or folded BN
-  if (a.fp8) return a.K % 128 == 0 && !a.beta && !a.aff;
+  // fp8 (e5m2 dy × e4m3 Wᵀ, K % 128 == 0): the statistics epilogue, no folded BN; a join only at
+  // stride 1 (as below)
+  if (a.fp8)
+    return a.K % 128 == 0 && !a.aff && (!a.beta || (a.ncls == 1 && a.sh == 1 && a.sw == 1));
   const bool rag = a.K % 64 != 0 && a.R * a.S == 1 && a.ncls == 1 && a.K % 8 == 0;
   if (a.K % 64 != 0 && !rag) return false;
   if (a.beta && !(a.ncls == 1 && a.sh == 1 && a.sw == 1)) return false;
@@ -1477,11 +1479,17 @@ bool conv_dgrad_glds(const ConvArgs& a0, int cfg, hipStream_t st, bool* fused) {
     }
     const int blocks = a.cls_tile0[a.ncls] / a.tpb;
     a.splits = 1;
-    if (a.fp8) {  // (no join: NJ)
-      if (cfg == 1)
+    if (a.fp8) {
+      if (a.beta) {  // + the join's previous-dx loads
+        if (cfg == 1)
+          launch_g<DGRAD, 256, 64, 4, 1, 3, true, false, 1, true, false>(a, blocks, st);
+        else
+          launch_g<DGRAD, 256, 128, 4, 2, 3, true, false, 1, true, false>(a, blocks, st);
+      } else if (cfg == 1) {
         launch_g<DGRAD, 256, 64, 4, 1, 3, true, false, 1, true, true>(a, blocks, st);
-      else
+      } else {
         launch_g<DGRAD, 256, 128, 4, 2, 3, true, false, 1, true, true>(a, blocks, st);
+      }
     } else if (a.aff) {  // (K % 64 == 0, no join; cfg 4 or 6)
       if (cfg == 4)
         launch_g<DGRAD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, true>(a, blocks, st);

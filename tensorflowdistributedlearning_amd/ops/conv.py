@@ -487,9 +487,9 @@ class _Conv2dFn(torch.autograd.Function):
                     return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
                                           accumulate=accumulate, mask=mask)
 
-                def dgrad_bnstat(bn_x, mask=None):
-                    return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, mask=mask,
-                                          bn_x=bn_x)
+                def dgrad_bnstat(bn_x, mask=None, out=None):
+                    return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
+                                          accumulate=out is not None, mask=mask, bn_x=bn_x)
             else:
                 # the flipped filter (strided: per-class sub-filters) lets the forward kernels
                 # compute dx
@@ -502,8 +502,9 @@ class _Conv2dFn(torch.autograd.Function):
                     return conv_dgrad(dy, w, ctx.x_shape, geom, out=out, accumulate=accumulate,
                                       mask=mask, w_flip=wf)
 
-                def dgrad_bnstat(bn_x, mask=None):
-                    return conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, bn_x, mask=mask, w_flip=wf)
+                def dgrad_bnstat(bn_x, mask=None, out=None):
+                    return conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, bn_x, out=out,
+                                             accumulate=out is not None, mask=mask, w_flip=wf)
             join = ctx.join
             masks_ok = fused_gpu(dy) and ctx.x_shape[-1] % 64 == 0  # 64-channel mask slabs
             # (the kernel decides; strided: parity classes; fp8: no join)
@@ -531,13 +532,12 @@ class _Conv2dFn(torch.autograd.Function):
                 if join.buf is None:
                     join.buf = dgrad(mask=mask)
                     join.note(mask is not None)
-                elif (join.last and mask is not None and stats_ok and not fp8_dg
-                      and geom.stride == (1, 1) and join.stats_x is not None):
+                elif (join.last and mask is not None and stats_ok and geom.stride == (1, 1)
+                      and join.stats_x_for(fp8_dg and FP8_DGRAD_STATS) is not None):
                     # the final contribution writes every pixel through the mask: its epilogue
                     # sees the finished gradient and can fuse the BN statistics
-                    _, join.red = conv_dgrad_bnstat(dy, w, ctx.x_shape, geom, join.stats_x,
-                                                    out=join.buf, accumulate=True, mask=mask,
-                                                    w_flip=wf)
+                    _, join.red = dgrad_bnstat(join.stats_x_for(fp8_dg and FP8_DGRAD_STATS),
+                                               mask=mask, out=join.buf)
                     join.note(True)
                 else:
                     dgrad(out=join.buf, accumulate=True, mask=mask)

@@ -49,6 +49,8 @@ _FUSE = os.environ.get("TDL_BNSTAT_FUSE", "2")
 STATS_ENABLED = _FUSE != "0"
 STATS_SINGLE = _FUSE in ("1", "2")
 STATS_JOIN = _FUSE in ("1", "3")
+# the fp8 dgrads (e5m2 × e4m3) fuse the join's statistics unless TDL_FP8_JOIN_STATS=0 (A/B)
+FP8_JOIN_STATS = STATS_ENABLED and os.environ.get("TDL_FP8_JOIN_STATS", "1") == "1"
 
 
 class MaskToken:
@@ -110,8 +112,13 @@ class GradJoin:
     @property
     def stats_x(self):
         """The BN input to fuse statistics against (None: not applicable)."""
+        return self.stats_x_for(False)
+
+    def stats_x_for(self, fp8):
+        """:attr:`stats_x` for a last contribution that is an fp8 dgrad (``fp8``): fused there by
+        default (FP8_JOIN_STATS), the bf16 joins per STATS_JOIN."""
         t = self.mask_token
-        return t.x if t is not None and STATS_JOIN else None
+        return t.x if t is not None and (STATS_JOIN or (fp8 and FP8_JOIN_STATS)) else None
 
     @property
     def mask(self):

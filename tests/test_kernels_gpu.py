@@ -699,10 +699,11 @@ def test_conv_dgrad_fp8(gpu, shape, accumulate):
 
 @pytest.mark.parametrize("shape", [(4, 14, 14, 64, 128, 3, 3, 1, 1), (4, 14, 14, 256, 256, 1, 1, 2, 0),
                                    (2, 9, 9, 128, 128, 3, 3, 2, 1)])
-@pytest.mark.parametrize("masked", [False, True])
-def test_conv_dgrad_fp8_bnstat(gpu, shape, masked):
-    """fp8 dgrad with the BN-backward statistics in its epilogue (no join): dx as the plain fp8
-    dgrad, and (Σg, Σg·x) of the stored (masked) dx against the same sums computed from it."""
+@pytest.mark.parametrize("masked,join", [(False, False), (True, False), (True, True)])
+def test_conv_dgrad_fp8_bnstat(gpu, shape, masked, join):
+    """fp8 dgrad with the BN-backward statistics in its epilogue: dx as the plain fp8 dgrad, and
+    (Σg, Σg·x) of the stored (masked) dx against the same sums computed from it; ``join``: the
+    residual join's dx += … (stride 1; the strided shapes then take the BN's own reduce)."""
     from tensorflowdistributedlearning_amd.ops import fp8 as F8
     from tensorflowdistributedlearning_amd.ops.common import ext
     if ext().deterministic():
@@ -720,8 +721,14 @@ def test_conv_dgrad_fp8_bnstat(gpu, shape, masked):
         keep = torch.rand(N, H, W, Cin) > 0.4
         bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)
         mask = bits.sum(1).to(torch.uint8).to(gpu)
-    plain = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, mask=mask)
-    dx, red = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, mask=mask, bn_x=bn_x)
+    prev = torch.randn(N, H, W, Cin).bfloat16().to(gpu) if join else None
+    plain = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, mask=mask,
+                             out=None if prev is None else prev.clone(), accumulate=join)
+    dx, red = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, mask=mask, bn_x=bn_x,
+                               out=None if prev is None else prev.clone(), accumulate=join)
+    if join and st > 1:
+        assert red is None  # strided joins: not fused (pixels of tap-less classes stay unmasked)
+        return
     assert red is not None, "fp8 dgrad did not fuse the statistics"
     assert torch.equal(dx, plain)
     gf, xf = dx.float().cpu().reshape(-1, Cin), bn_x.float().cpu().reshape(-1, Cin)
