@@ -428,7 +428,7 @@ bool conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t sh, int64_t sw, int64_t 
 bool conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, int64_t sh, int64_t sw,
                     int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool accumulate,
                     c10::optional<Tensor> mask, c10::optional<Tensor> bn_x,
-                    c10::optional<Tensor> bn_red) {
+                    c10::optional<Tensor> bn_red, c10::optional<Tensor> w_flip) {
   TORCH_CHECK(dy8.is_cuda() && w8t.is_cuda() && dy8.element_size() == 1 && w8t.element_size() == 1,
               "fp8 operands expected");
   TORCH_CHECK(dy8.is_contiguous() && w8t.is_contiguous(), "contiguous operands expected");
@@ -454,6 +454,17 @@ bool conv_dgrad_fp8(Tensor dy8, Tensor w8t, Tensor dx, Tensor sdy, Tensor sw_, i
                 mask->numel() * 8 == dx.numel() && dx.size(3) % 64 == 0,
                 "conv_dgrad mask: uint8 [numel(dx)/8], C % 64 == 0");
     a.mask = (const uint8_t*)mask->data_ptr();
+  }
+  // w_flip (optional, stride 1): the e4m3 flipped filter [C, R, S, K] — the route row
+  // dgrad.asfwd.fp8 runs the dgrad as the forward conv of dy with it (for a 1x1 conv it is w8t)
+  a.w_flip = nullptr;
+  a.w_flip_bytes = 0;
+  if (w_flip.has_value() && w_flip->defined()) {
+    TORCH_CHECK(w_flip->is_cuda() && w_flip->element_size() == 1 && w_flip->is_contiguous() &&
+                    w_flip->numel() == w8t.numel() && sh == 1 && sw == 1,
+                "conv_dgrad_fp8 w_flip: the e4m3 [C,R,S,K] flipped filter, stride 1");
+    a.w_flip = (const bf16_t*)w_flip->data_ptr();
+    a.w_flip_bytes = (uint32_t)w_flip->numel();
   }
   a.stats = nullptr;
   a.bn_x = nullptr;
@@ -1508,7 +1519,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dy8"), py::arg("w8t"), py::arg("dx"),
         py::arg("scale_dy"), py::arg("scale_w"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dh"), py::arg("dw"), py::arg("accumulate") = false, py::arg("mask") = py::none(),
-        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none());
+        py::arg("bn_x") = py::none(), py::arg("bn_red") = py::none(), py::arg("w_flip") = py::none());
   m.attr("AMAX_SLOT") = AMAX_SLOT;
   m.def("fp8_amax", &fp8_amax);
   m.def("fp8_roll", &fp8_roll);

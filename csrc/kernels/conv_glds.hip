@@ -197,7 +197,7 @@ template <int MODE, int BM, int BN, int WM, int WN, int STAGES, bool STATS, bool
           bool FP8 = false, bool NJ = false, bool FRES = false, bool M32 = false, bool AFM = false,
           bool DEPI = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) {
-  static_assert(!DEPI || (MODE == FWD && !FP8 && !FRES && !BIAS), "dgrad epilogue on the FWD loop");
+  static_assert(!DEPI || (MODE == FWD && !FRES && !BIAS), "dgrad epilogue on the FWD loop");
   // AFM: DGRAD statistics epilogue masking by a folded BN's a·x + b > 0 (conv_common.h)
   // M32: the K loop runs v_mfma_f32_32x32x16_bf16 on 32×32 blocks (half the MFMA instructions
   // and half the vector-issue hold per FLOP of the 16×16×32 form); accumulators are re-laid to
@@ -848,9 +848,10 @@ _Pragma("unroll")                                                               
 _Pragma("unroll")                                                                             \
         for (int rn = 0; rn < RN; ++rn)                                                        \
 /* operand formats: first (B tile: weights / WGRAD activations) e4m3 = 0; second (A tile) */  \
-/* e4m3 = 0 for FWD activations, e5m2 (bf8) = 1 for DGRAD / WGRAD output gradients */          \
+/* e4m3 = 0 for FWD activations, e5m2 (bf8) = 1 for DGRAD / WGRAD output gradients and for */  \
+/* the dy of a dgrad run as the forward conv (DEPI) */                                          \
           acc[rm][rn] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(                      \
-              b8[rn], a8[rm], acc[rm][rn], 0, MODE == FWD ? 0 : 1, 0, 127, 0, 127);            \
+              b8[rn], a8[rm], acc[rm][rn], 0, (MODE == FWD && !DEPI) ? 0 : 1, 0, 127, 0, 127); \
       slot_comp = slot_comp + 1 == STAGES ? 0 : slot_comp + 1;                                 \
       --inflight;                                                                              \
       if (ckt + 1 >= CT.kt1) {                                                                 \
@@ -1295,9 +1296,56 @@ static bool dgrad_as_fwd_strided(const ConvArgs& a0, const bf16_t* wf, int cfg, 
 
 // cfg (the route row's): 0 / 4 the LDS-DMA K loop with 256×128 / 8-wave 256×64 tiles, 100 the
 // halo forward loader, 102 the producer/consumer kernel.
+// fp8 (stride 1): e5m2 dy × the e4m3 flipped filter [C][R][S][K] on the forward fp8 K loop
+// (A-operand format e5m2) with the scaled DGRAD epilogue; K % 128 == 0, cfg 0 (256×128)
+static bool dgrad_as_fwd_fp8(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, int cfg,
+                             hipStream_t st, bool* fused) {
+  if (cfg != 0 || a0.sh != 1 || a0.sw != 1 || a0.K % 128 || a0.C % 8 || a0.ldc != a0.C ||
+      a0.aff || a0.dg_masked || a0.Ho != a0.H || a0.Wo != a0.W)
+    return false;
+  const int ph = a0.dh * (a0.R - 1) - a0.ph, pw = a0.dw * (a0.S - 1) - a0.pw;
+  if (ph < 0 || pw < 0) return false;
+  ConvArgs a = a0;
+  a.x = a0.dy;
+  a.x_bytes = a0.dy_bytes;
+  a.w = wf;
+  a.w_bytes = wf_bytes;
+  a.w_t = nullptr;
+  a.C = a0.K;
+  a.K = a0.C;
+  a.ph = ph;
+  a.pw = pw;
+  a.M = a.N * a.Ho * a.Wo;
+  a.Ng = a.K;
+  a.Kg = a.R * a.S * a.C;
+  a.relu = 0;
+  a.ncls = 1;
+  a.cls_a[0] = a.cls_b[0] = 0;
+  a.cls_Hc[0] = a.H;
+  a.cls_Wc[0] = a.W;
+  a.cls_r0[0] = a.cls_s0[0] = 0;
+  a.cls_Th[0] = a.R;
+  a.cls_Tw[0] = a.S;
+  a.dbg = 0;
+  a.splits = 1;
+  set_fastdivs(a);
+  const bool stats = a.stats != nullptr && a.bn_x != nullptr;
+  if (!stats) a.stats = nullptr;
+  const int blocks = fwd_tiling(a, cfg_of(0));
+  if (stats && a.beta)
+    launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, true, false, false, false, false, true>(a, blocks, st);
+  else if (stats)
+    launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, true, true, false, false, false, true>(a, blocks, st);
+  else
+    launch_g<FWD, 256, 128, 4, 2, 3, false, false, 1, true, false, false, false, false, true>(a, blocks, st);
+  if (fused) *fused = stats;
+  return true;
+}
+
 bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, int cfg,
                        hipStream_t st, bool* fused) {
   if (fused) *fused = false;
+  if (a0.fp8) return wf != nullptr && dgrad_as_fwd_fp8(a0, wf, wf_bytes, cfg, st, fused);
   if (wf != nullptr && (a0.sh > 1 || a0.sw > 1) && !a0.fp8 && !a0.aff && !a0.dg_masked &&
       a0.K % 64 == 0 && a0.C % 8 == 0 && a0.ldc == a0.C)
     return dgrad_as_fwd_strided(a0, wf, cfg, st, fused);

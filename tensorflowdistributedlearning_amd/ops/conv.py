@@ -270,12 +270,14 @@ def _dgrad_touched(w_shape, x_shape, geom: ConvGeom):
 
 
 def conv_dgrad_fp8(dy8, sdy, w8t, sw, x_shape, geom: ConvGeom, out=None, accumulate=False,
-                   mask=None, bn_x=None):
+                   mask=None, bn_x=None, w_flip=None):
     """dx from fp8 operands: ``dy8`` e5m2 [N,Ho,Wo,K] with scale ``sdy``, ``w8t`` the e4m3 weight
     transposed to [R,S,C,K] with scale ``sw`` (ops/fp8.py).  GPU: the LDS-DMA dgrad on
     v_mfma_scale_f32_16x16x128_f8f6f4 (K % 128 == 0); join accumulate / ReLU mask as
     :func:`conv_dgrad`.  CPU: fp32 on the dequantised operands.  With ``bn_x`` (no join) returns
-    ``(dx, red)`` as :func:`conv_dgrad_bnstat`: the BN-backward sums fused into the epilogue."""
+    ``(dx, red)`` as :func:`conv_dgrad_bnstat`: the BN-backward sums fused into the epilogue.
+    ``w_flip`` (stride 1): the e4m3 flipped filter [C, R, S, K] (:func:`fp8_flip_weight`) — the
+    dgrad then runs as the forward fp8 conv of dy (route row dgrad.asfwd.fp8)."""
     if on_gpu(dy8):
         dx = out if out is not None else torch.empty(x_shape, device=dy8.device,
                                                      dtype=torch.bfloat16)
@@ -283,12 +285,29 @@ def conv_dgrad_fp8(dy8, sdy, w8t, sw, x_shape, geom: ConvGeom, out=None, accumul
         fused = ext().conv_dgrad_fp8(dy8.view(torch.uint8), w8t.view(torch.uint8), dx, sdy, sw,
                                      geom.stride[0], geom.stride[1], geom.padding[0],
                                      geom.padding[2], geom.dilation[0], geom.dilation[1],
-                                     bool(accumulate and out is not None), mask, bn_x, red)
+                                     bool(accumulate and out is not None), mask, bn_x, red,
+                                     None if w_flip is None else w_flip.view(torch.uint8))
         return dx if bn_x is None else (dx, red if fused else None)
     w = (w8t.float() * sw).permute(3, 0, 1, 2).contiguous()
     dx = conv_dgrad(dy8.float() * sdy, w, x_shape, geom, out=out, accumulate=accumulate,
                     mask=mask, out_dtype=torch.bfloat16)
     return dx if bn_x is None else (dx, None)
+
+
+def fp8_flip_weight(w8t):
+    """The e4m3 flipped filter [C, R, S, K] (w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c]) from the
+    transposed fp8 weight [R, S, C, K]; for a 1×1 conv the same bytes (a view, no copy)."""
+    R, S, C, K = w8t.shape
+    if R == 1 and S == 1:
+        return w8t.reshape(C, 1, 1, K)
+    return w8t.view(torch.uint8).flip(0, 1).permute(2, 0, 1, 3).contiguous().view(w8t.dtype)
+
+
+# the fp8 dgrad as the forward conv of dy: 1 — 1×1 stride-1 convs (the flipped filter is the
+# transposed weight itself), 2 (default) — every stride-1 conv (a flip pass per 3×3 weight and
+# step), 0 off.  ResNet-152 b256 fp8 graph, same box: 6,167 / 6,171 (2) vs 6,160 / 6,164 (1) vs
+# 6,151 / 6,151 img/s (0) — profiles/r05_fp8_dgrad_as_fwd_ab.txt
+FP8_DGRAD_AS_FWD = int(os.environ.get("TDL_FP8_DGRAD_AS_FWD", "2"))
 
 
 def fp8_dgrad_eligible(layer, dy, geom: ConvGeom, w_shape):
@@ -482,14 +501,20 @@ class _Conv2dFn(torch.autograd.Function):
                 # fp8 dgrad: e5m2 dy (the BN backward's side output) × e4m3 W^T
                 dy8, sdy = dy._tdl_fp8
                 w8t, sw8 = ctx.layer.fp8_weight_t(w)
+                # 1×1 stride 1: the transposed weight is the flipped filter — the dgrad runs as
+                # the forward fp8 conv of dy (no extra weight pass)
+                one = w8t.shape[0] == 1 and w8t.shape[1] == 1
+                wf8 = (fp8_flip_weight(w8t) if geom.stride == (1, 1) and
+                       (FP8_DGRAD_AS_FWD >= 2 or (FP8_DGRAD_AS_FWD == 1 and one)) else None)
 
                 def dgrad(out=None, accumulate=False, mask=None):
                     return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
-                                          accumulate=accumulate, mask=mask)
+                                          accumulate=accumulate, mask=mask, w_flip=wf8)
 
                 def dgrad_bnstat(bn_x, mask=None, out=None):
                     return conv_dgrad_fp8(dy8, sdy, w8t, sw8, ctx.x_shape, geom, out=out,
-                                          accumulate=out is not None, mask=mask, bn_x=bn_x)
+                                          accumulate=out is not None, mask=mask, bn_x=bn_x,
+                                          w_flip=wf8)
             else:
                 # the flipped filter (strided: per-class sub-filters) lets the forward kernels
                 # compute dx

@@ -104,7 +104,9 @@ def _run_dgrad(r, gpu, N, H, k, cin, cout, g):
         from tensorflowdistributedlearning_amd.ops import fp8 as F8
         dy8, sdy = F8.quantize_e5m2(dy)
         w8, sw = F8.quantize_e4m3(w)
-        dx = C.conv_dgrad_fp8(dy8, sdy, F8.transpose_weight(w8), sw, (N, H, H, cin), g)
+        w8t = F8.transpose_weight(w8)
+        wf8 = C.fp8_flip_weight(w8t) if need & RF_WFLIP else None
+        dx = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, H, cin), g, w_flip=wf8)
         ref = C.ref_conv_dgrad(F8.dequantize_e5m2(dy8, sdy).cpu(), F8.dequantize(w8, sw).cpu(),
                                (N, H, H, cin), g)
         return dx, ref, 2e-2

@@ -736,6 +736,43 @@ def test_conv_dgrad_fp8_bnstat(gpu, shape, masked, join):
     assert rel_err(red.cpu(), want) < 1e-3
 
 
+@pytest.mark.parametrize("shape", [(4, 14, 14, 256, 128, 1, 1, 1, 0), (2, 14, 14, 64, 256, 3, 3, 1, 1)])
+@pytest.mark.parametrize("mode", ["plain", "stats", "join"])
+def test_conv_dgrad_fp8_as_forward(gpu, shape, mode):
+    """The fp8 dgrad as the forward fp8 conv of e5m2 dy with the e4m3 flipped filter (route row
+    dgrad.asfwd.fp8) against the fp8 DGRAD kernel on the same operands: dx (with the ReLU mask,
+    and the join's accumulate), and the fused BN-backward sums."""
+    from tensorflowdistributedlearning_amd.ops import fp8 as F8
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    N, H, W, Cin, K, R, S, st, p = shape
+    g = C.ConvGeom((st, st), (p, p, p, p), (1, 1))
+    torch.manual_seed(31)
+    dy8, sdy = F8.quantize_e5m2(torch.randn(N, H, W, K).bfloat16().to(gpu))
+    w8, sw = F8.quantize_e4m3((torch.randn(K, R, S, Cin) / math.sqrt(R * S * K)).bfloat16().to(gpu))
+    w8t = F8.transpose_weight(w8)
+    wf8 = C.fp8_flip_weight(w8t)
+    keep = torch.rand(N, H, W, Cin) > 0.4
+    bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)
+    mask = bits.sum(1).to(torch.uint8).to(gpu)
+    bn_x = (torch.randn(N, H, W, Cin) + 0.3).bfloat16().to(gpu) if mode != "plain" else None
+    prev = torch.randn(N, H, W, Cin).bfloat16().to(gpu) if mode == "join" else None
+    kw = dict(mask=mask, out=None if prev is None else prev.clone(), accumulate=mode == "join")
+    ref = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, **kw)
+    kw = dict(mask=mask, out=None if prev is None else prev.clone(), accumulate=mode == "join")
+    ext().conv_route_force(1, "dgrad.asfwd.fp8")
+    try:
+        got = C.conv_dgrad_fp8(dy8, sdy, w8t, sw, (N, H, W, Cin), g, bn_x=bn_x, w_flip=wf8, **kw)
+        assert ext().conv_last_route(1) == "dgrad.asfwd.fp8"
+    finally:
+        ext().conv_route_force(1, "")
+    dx, red = got if bn_x is not None else (got, None)
+    assert rel_err(dx, ref) < 1e-2
+    if bn_x is not None and not ext().deterministic():
+        assert red is not None
+        gf, xf = dx.float().cpu().reshape(-1, Cin), bn_x.float().cpu().reshape(-1, Cin)
+        assert rel_err(red.cpu(), torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-3
+
+
 def test_fp8_e5m2_quantize_and_transpose(gpu):
     from tensorflowdistributedlearning_amd.ops import fp8 as F8
     torch.manual_seed(19)
