@@ -11,19 +11,21 @@ inline int blocks_for(long n) {
   return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT));
 }
 
-template <int V, typename T>  // V = 8 (vector) or 1 (scalar); T = bf16_t or float storage
+// V = 8 (vector) or 1 (scalar); T = bf16_t or float storage; KK / SS / I as maxpool_bwd_stats
+template <int V, typename T, int KK = 0, int SS = 0, typename I = long>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                    uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho,
-                                   int Wo, int k, int s, int pt, int pl) {
+                                   int Wo, int k_, int s_, int pt, int pl) {
+  const int k = KK ? KK : k_, s = SS ? SS : s_;
   const int cv = C / V;
-  const long total = (long)N * Ho * Wo * cv;
-  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
-    const int c = (int)(t % cv) * V;
-    long p = t / cv;
-    const int wo = (int)(p % Wo);
-    p /= Wo;
-    const int ho = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+  const I total = (I)N * Ho * Wo * cv;
+  for (I t = blockIdx.x * (I)NT + threadIdx.x; t < total; t += (I)gridDim.x * NT) {
+    const int c = (int)(t % (I)cv) * V;
+    I p = t / (I)cv;
+    const int wo = (int)(p % (I)Wo);
+    p /= (I)Wo;
+    const int ho = (int)(p % (I)Ho);
+    const int n = (int)(p / (I)Ho);
     float best[V];
     int arg[V];
 #pragma unroll
@@ -37,7 +39,7 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
       for (int q = 0; q < k; ++q) {
         const int wi = wo * s - pl + q;
         if ((unsigned)wi >= (unsigned)W) continue;
-        const long off = (((long)n * H + hi) * W + wi) * C + c;
+        const I off = (((I)n * H + hi) * W + wi) * C + c;
         float v[V];
         if constexpr (V == 8) {
           load8(x + off, v);
@@ -52,7 +54,7 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
           }
       }
     }
-    const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+    const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
     if constexpr (V == 8) {
       store8(y + o, best);
       uint2 packed;
@@ -121,23 +123,28 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
 // (ops/gradjoin.py fused statistics): dx = gathered dy · [ReLU bit], and (Σg, Σg·x) of the stored
 // dx with x = that BN's input — the BN backward then skips its reduce pass.  8-channel vectors;
 // NT % (C/8) == 0 so each thread's channel vector is fixed over the grid-stride loop.
+// KK / SS: compile-time window and stride (the ResNet stem's 3×3 / 2: constant divisions, unrolled
+// window loops), 0 = runtime k / s; I: uint32_t index math when every element offset fits (64-bit
+// divisions cost ≈4× the 32-bit ones per thread)
+template <int KK, int SS, typename I>
 __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
     const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
     const bf16_t* __restrict__ bx, const uint8_t* __restrict__ mask, float* __restrict__ red, int N,
-    int H, int W, int C, int Ho, int Wo, int k, int s, int pt, int pl) {
+    int H, int W, int C, int Ho, int Wo, int k_, int s_, int pt, int pl) {
   __shared__ float lds[2][NT][9];  // +1 pad against bank conflicts
+  const int k = KK ? KK : k_, s = SS ? SS : s_;
   const int cv = C / 8;
-  const long total = (long)N * H * W * cv;
+  const I total = (I)N * H * W * cv;
   float s0[8], s1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
-  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
-    const int c = (int)(t % cv) * 8;
-    long p = t / cv;
-    const int w = (int)(p % W);
-    p /= W;
-    const int h = (int)(p % H);
-    const int n = (int)(p / H);
+  for (I t = blockIdx.x * (I)NT + threadIdx.x; t < total; t += (I)gridDim.x * NT) {
+    const int c = (int)(t % (I)cv) * 8;
+    I p = t / (I)cv;
+    const int w = (int)(p % (I)W);
+    p /= (I)W;
+    const int h = (int)(p % (I)H);
+    const int n = (int)(p / (I)H);
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -150,7 +157,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
       const int r = hh - ho * s;
       for (int wo = wo_lo; wo <= wo_hi; ++wo) {
         const int want = r * k + (ww - wo * s);
-        const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+        const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
         float g[8];
         unpack8(*(const uint4*)(dy + o), g);
         const uint2 packed = *(const uint2*)(idx + o);
@@ -161,7 +168,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
         }
       }
     }
-    const long off = (((long)n * H + h) * W + w) * C + c;
+    const I off = (((I)n * H + h) * W + w) * C + c;
     const uint32_t mb = mask[off >> 3];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = (mb >> j) & 1u ? acc[j] : 0.f;
@@ -267,7 +274,11 @@ __global__ void avgpool_scalar_bwd(const T* __restrict__ dy, T* __restrict__ dx,
 template <typename T>
 static void maxpool_fwd_impl(const T* x, T* y, uint8_t* idx, int N, int H, int W, int C,
                         int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
-  if (C % 8 == 0)
+  static const bool spec = getenv("TDL_POOL_SPEC") == nullptr || atoi(getenv("TDL_POOL_SPEC")) != 0;
+  if (C % 8 == 0 && spec && k == 3 && s == 2 && (long)N * H * W * C < (1L << 31))
+    hipLaunchKernelGGL((maxpool_fwd_kernel<8, T, 3, 2, uint32_t>), dim3(blocks_for((long)N * Ho * Wo * C / 8)),
+                       dim3(NT), 0, st, x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  else if (C % 8 == 0)
     hipLaunchKernelGGL((maxpool_fwd_kernel<8, T>), dim3(blocks_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0,
                        st, x, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
   else
@@ -290,8 +301,14 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
                               const uint8_t* mask, float* red, int N, int H, int W, int C, int Ho,
                               int Wo, int k, int s, int pt, int pl, hipStream_t st) {
   if (C % 8 || NT % (C / 8)) return false;
-  hipLaunchKernelGGL(maxpool_bwd_stats_kernel, dim3(blocks_for((long)N * H * W * C / 8)), dim3(NT), 0,
-                     st, dy, idx, dx, bx, mask, red, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  const long n = (long)N * H * W * C;
+  static const bool spec = getenv("TDL_POOL_SPEC") == nullptr || atoi(getenv("TDL_POOL_SPEC")) != 0;
+  const bool small = spec && n < (1L << 31) && (long)N * Ho * Wo * C < (1L << 31);
+  auto kern = maxpool_bwd_stats_kernel<0, 0, long>;
+  if (small) kern = k == 3 && s == 2 ? maxpool_bwd_stats_kernel<3, 2, uint32_t>
+                                     : maxpool_bwd_stats_kernel<0, 0, uint32_t>;
+  hipLaunchKernelGGL(kern, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, idx, dx, bx, mask, red, N,
+                     H, W, C, Ho, Wo, k, s, pt, pl);
   return true;
 }
 
