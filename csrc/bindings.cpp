@@ -1504,6 +1504,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                    stream());
   }, "every registered filter flip of a flat weight buffer in one launch (rows: offset, K, R, S, "
      "C, tap, k tile, c tile; validated on the host by ops/conv.FlatFlips)");
+  m.def("conv_flip_classes", [](Tensor w, Tensor out, int64_t sh, int64_t sw, int64_t ph,
+                                int64_t pw) {
+    CHECK_T(w, torch::kBFloat16);
+    CHECK_T(out, torch::kBFloat16);
+    TORCH_CHECK(w.dim() == 4 && w.is_contiguous() && out.is_contiguous() &&
+                    out.numel() <= w.numel(), "conv_flip_classes: w [K,R,S,C], out contiguous");
+    conv_flip_classes_launch(BF(w), BFW(out), (int)w.size(0), (int)w.size(1), (int)w.size(2),
+                             (int)w.size(3), (int)sh, (int)sw, (int)ph, (int)pw, stream());
+  });
   m.def("conv_flip_weight", [](Tensor w, Tensor wf) {
     CHECK_T(w, torch::kBFloat16);
     CHECK_T(wf, torch::kBFloat16);

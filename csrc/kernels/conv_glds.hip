@@ -1406,6 +1406,34 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   return true;
 }
 
+// the per-parity-class flipped sub-filters of a strided conv in one launch (was a flip, a
+// permute copy and a concatenation per class in ATen): element e of class i (offset off[i],
+// [C][Th][Tw][K]) = w[k][r0 + sh·(Th−1−t)][s0 + sw·(Tw−1−u)][c]
+struct FlipCls {
+  int n;
+  int r0[16], th[16], s0[16], tw[16];
+  long off[17];
+};
+__global__ void __launch_bounds__(256) flip_classes_kernel(const bf16_t* __restrict__ w,
+                                                           bf16_t* __restrict__ out, int K, int R,
+                                                           int S, int C, int sh, int sw,
+                                                           FlipCls fc) {
+  const long total = fc.off[fc.n];
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    int i = 0;
+    while (i + 1 < fc.n && e >= fc.off[i + 1]) ++i;
+    long q = e - fc.off[i];
+    const int k = (int)(q % K);
+    q /= K;
+    const int u = (int)(q % fc.tw[i]);
+    q /= fc.tw[i];
+    const int t = (int)(q % fc.th[i]);
+    const int c = (int)(q / fc.th[i]);
+    const int r = fc.r0[i] + sh * (fc.th[i] - 1 - t), s2 = fc.s0[i] + sw * (fc.tw[i] - 1 - u);
+    out[e] = w[(((long)k * R + r) * S + s2) * C + c];
+  }
+}
+
 // w_flip[c][r][s][k] = w[k][R−1−r][S−1−s][c]: a 32×32-element tiled transpose per filter tap
 __global__ void __launch_bounds__(256) flip_weight_kernel(const bf16_t* __restrict__ w,
                                                           bf16_t* __restrict__ wf, int K, int R,
@@ -1459,6 +1487,32 @@ __global__ void __launch_bounds__(256) multi_flip_kernel(const bf16_t* __restric
     const int c = c0 + i, k = k0 + tx;
     if (c < C && k < K) wf[((long)c * R * S + tap) * K + k] = t[tx][i];
   }
+}
+
+void conv_flip_classes_launch(const bf16_t* w, bf16_t* out, int K, int R, int S, int C, int sh,
+                              int sw, int ph, int pw, hipStream_t st) {
+  if (sh > 4 || sw > 4) throw std::runtime_error("conv_flip_classes: stride <= 4");
+  FlipCls fc{};
+  long off = 0;
+  for (int a = 0; a < sh; ++a) {
+    const int r0 = ((a + ph) % sh + sh) % sh, th = r0 < R ? (R - r0 + sh - 1) / sh : 0;
+    for (int b = 0; b < sw; ++b) {
+      const int s0 = ((b + pw) % sw + sw) % sw, tw = s0 < S ? (S - s0 + sw - 1) / sw : 0;
+      if (!th || !tw) continue;
+      fc.r0[fc.n] = r0;
+      fc.th[fc.n] = th;
+      fc.s0[fc.n] = s0;
+      fc.tw[fc.n] = tw;
+      fc.off[fc.n] = off;
+      off += (long)C * th * tw * K;
+      ++fc.n;
+    }
+  }
+  fc.off[fc.n] = off;
+  if (off == 0) return;
+  const int blocks = (int)std::min<long>(4096, (off + 255) / 256);
+  hipLaunchKernelGGL(flip_classes_kernel, dim3(blocks), dim3(256), 0, st, w, out, K, R, S, C, sh, sw,
+                     fc);
 }
 
 void conv_flip_weights_multi_launch(const bf16_t* src, bf16_t* dst, const long* rows, int nrows,

@@ -142,6 +142,10 @@ void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, i
                              hipStream_t st);
 // many flips in one launch: rows int64 [n][8] = (offset, K, R, S, C, tap, k tile, c tile), the
 // flip of the [K,R,S,C] filter at src + offset written at dst + offset
+// strided dgrad-as-forward sub-filters (ops/conv.flip_classes): for every stride parity class
+// with taps (a-major, then b), [C][Th][Tw][K] with tap t ↦ r0 + sh·(Th−1−t), concatenated
+void conv_flip_classes_launch(const bf16_t* w, bf16_t* out, int K, int R, int S, int C, int sh,
+                              int sw, int ph, int pw, hipStream_t st);
 void conv_flip_weights_multi_launch(const bf16_t* src, bf16_t* dst, const long* rows, int nrows,
                                     hipStream_t st);
 void conv_set_pc(int on);

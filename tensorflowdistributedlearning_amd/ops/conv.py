@@ -249,6 +249,11 @@ def flip_classes(w, geom: ConvGeom):
     forward conv of dy with its sub-filter."""
     (sh, sw), ph, pw = geom.stride, geom.padding[0], geom.padding[2]
     R, S = w.shape[1], w.shape[2]
+    if on_gpu(w) and w.dtype == torch.bfloat16 and sh <= 4 and sw <= 4:
+        n = sum(len(rr) for rr in _classes(sh, R, ph)) * sum(len(ss) for ss in _classes(sw, S, pw))
+        out = torch.empty(n * w.shape[0] * w.shape[3], device=w.device, dtype=w.dtype)
+        ext().conv_flip_classes(w.contiguous(), out, sh, sw, ph, pw)  # one launch
+        return out
     parts = []
     # (strided slices + flips only: no index tensors, so the rebuild is HIP-graph capturable)
     for rr in _classes(sh, R, ph):

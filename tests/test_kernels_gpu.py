@@ -773,6 +773,18 @@ def test_conv_dgrad_fp8_as_forward(gpu, shape, mode):
         assert rel_err(red.cpu(), torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-3
 
 
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (1, 2, 0), (3, 3, 1), (5, 2, 2), (2, 2, 0)])
+def test_flip_classes_native_matches_reference(gpu, k, s, p):
+    """ops/conv.flip_classes on the GPU (one conv_flip_classes launch) equals the ATen slice /
+    flip / permute / cat form bit for bit, classes a-major, empty classes skipped."""
+    torch.manual_seed(37)
+    w = torch.randn(48, k, k, 24).bfloat16()
+    g = C.ConvGeom((s, s), (p, p, p, p), (1, 1))
+    ref = C.flip_classes(w, g)  # CPU: the reference form
+    got = C.flip_classes(w.to(gpu), g)
+    assert got.shape == ref.shape and torch.equal(got.cpu(), ref)
+
+
 def test_fp8_e5m2_quantize_and_transpose(gpu):
     from tensorflowdistributedlearning_amd.ops import fp8 as F8
     torch.manual_seed(19)
