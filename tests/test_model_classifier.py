@@ -190,7 +190,10 @@ def test_model_graph_training_tracks_eager(tmp_path, gpu):
     kw.update(lr=0.002, momentum=0.0)
     ra = Model(str(tmp_path / "e2"), "", hip_graph="off", **kw).train(192, None, 16, 4)[0]
     rb = Model(str(tmp_path / "g2"), "", **kw).train(192, None, 16, 4)[0]
-    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.02, atol=0.01)
+    # once the weights move, two EAGER runs differ by up to 2.4 % at step 4 themselves (fp32-atomic
+    # BN statistics, amplified by the updates; dev/tools/graph_eager_gap.py,
+    # profiles/r05_graph_eager_gap.txt) — the graph must stay within that noise band
+    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.05, atol=0.01)
 
 
 @pytest.mark.gpu
