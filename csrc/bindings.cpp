@@ -1508,8 +1508,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                 int64_t pw) {
     CHECK_T(w, torch::kBFloat16);
     CHECK_T(out, torch::kBFloat16);
-    TORCH_CHECK(w.dim() == 4 && w.is_contiguous() && out.is_contiguous() &&
-                    out.numel() <= w.numel(), "conv_flip_classes: w [K,R,S,C], out contiguous");
+    TORCH_CHECK(w.dim() == 4 && w.is_contiguous() && out.is_contiguous() && sh >= 1 && sw >= 1,
+                "conv_flip_classes: w [K,R,S,C], out contiguous, stride >= 1");
+    const long need = conv_flip_classes_numel((int)w.size(0), (int)w.size(1), (int)w.size(2),
+                                              (int)w.size(3), (int)sh, (int)sw, (int)ph, (int)pw);
+    TORCH_CHECK(out.numel() == need, "conv_flip_classes: out has ", out.numel(),
+                " elements, the parity-class sub-filters need ", need);
     conv_flip_classes_launch(BF(w), BFW(out), (int)w.size(0), (int)w.size(1), (int)w.size(2),
                              (int)w.size(3), (int)sh, (int)sw, (int)ph, (int)pw, stream());
   });

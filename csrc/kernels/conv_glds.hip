@@ -1489,9 +1489,24 @@ __global__ void __launch_bounds__(256) multi_flip_kernel(const bf16_t* __restric
   }
 }
 
+long conv_flip_classes_numel(int K, int R, int S, int C, int sh, int sw, int ph, int pw) {
+  if (sh < 1 || sw < 1 || sh > 4 || sw > 4)
+    throw std::runtime_error("conv_flip_classes: 1 <= stride <= 4");
+  long total = 0;
+  for (int a = 0; a < sh; ++a) {
+    const int r0 = ((a + ph) % sh + sh) % sh, th = r0 < R ? (R - r0 + sh - 1) / sh : 0;
+    for (int b = 0; b < sw; ++b) {
+      const int s0 = ((b + pw) % sw + sw) % sw, tw = s0 < S ? (S - s0 + sw - 1) / sw : 0;
+      total += (long)C * th * tw * K;
+    }
+  }
+  return total;
+}
+
 void conv_flip_classes_launch(const bf16_t* w, bf16_t* out, int K, int R, int S, int C, int sh,
                               int sw, int ph, int pw, hipStream_t st) {
-  if (sh > 4 || sw > 4) throw std::runtime_error("conv_flip_classes: stride <= 4");
+  if (sh < 1 || sw < 1 || sh > 4 || sw > 4)
+    throw std::runtime_error("conv_flip_classes: 1 <= stride <= 4");
   FlipCls fc{};
   long off = 0;
   for (int a = 0; a < sh; ++a) {

@@ -12,14 +12,17 @@
 // column sums, depthwise weight gradients) already reduces fixed slabs in order.
 //
 // Scope: the bf16 GPU path.  Slabs are per stream (the side-stream weight gradients run
-// concurrently with the compute stream) and grow on demand, so deterministic mode is an eager-mode
-// (debug / reproducibility) feature: growth is not allowed inside a HIP-graph capture.
+// concurrently with the compute stream) and grow on demand.  Growth is not allowed inside a
+// HIP-graph capture (no allocation on the capturing thread): Trainer.capture runs its warm-up
+// steps on the capture stream itself, so the slabs exist at their final size.  A slab a capture
+// has baked into a graph is never freed — a later growth of that stream's slab retires it.
 #include "common.h"
 #include "kernels.h"
 
 #include <map>
 #include <mutex>
 #include <stdexcept>
+#include <vector>
 
 namespace tdl {
 
@@ -40,9 +43,11 @@ namespace {
 struct Slab {
   float* p = nullptr;
   size_t cap = 0;
+  bool captured = false;  // referenced by a captured graph: retire instead of free
 };
 std::mutex g_slab_mu;
 std::map<hipStream_t, Slab> g_slabs;
+std::vector<float*> g_retired;  // slabs of captured graphs (live as long as the process)
 
 __global__ void slab_sum_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                 int rows, long n, long row_stride) {
@@ -58,20 +63,26 @@ __global__ void slab_sum_kernel(const float* __restrict__ slab, float* __restric
 float* det_slab(size_t floats, hipStream_t st) {
   std::lock_guard<std::mutex> g(g_slab_mu);
   Slab& s = g_slabs[st];
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(st, &cap);
   if (floats > s.cap) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cap);
     if (cap != hipStreamCaptureStatusNone)
       throw std::runtime_error("deterministic mode: slab growth inside a HIP-graph capture "
-                               "(run a warm-up step first, or capture without TDL_DETERMINISTIC)");
+                               "(run the warm-up steps on the capture stream, as "
+                               "Trainer.capture does, or capture without TDL_DETERMINISTIC)");
     if (s.p) {
       (void)hipStreamSynchronize(st);
-      (void)hipFree(s.p);
+      if (s.captured)
+        g_retired.push_back(s.p);
+      else
+        (void)hipFree(s.p);
+      s.captured = false;
     }
     s.cap = std::max<size_t>(floats, (size_t)1 << 20);
     if (hipMalloc((void**)&s.p, s.cap * sizeof(float)) != hipSuccess)
       throw std::runtime_error("deterministic mode: slab allocation failed");
   }
+  if (cap != hipStreamCaptureStatusNone) s.captured = true;
   return s.p;
 }
 

@@ -144,6 +144,8 @@ void conv_flip_weight_launch(const bf16_t* w, bf16_t* wf, int K, int R, int S, i
 // flip of the [K,R,S,C] filter at src + offset written at dst + offset
 // strided dgrad-as-forward sub-filters (ops/conv.flip_classes): for every stride parity class
 // with taps (a-major, then b), [C][Th][Tw][K] with tap t ↦ r0 + sh·(Th−1−t), concatenated
+// elements conv_flip_classes_launch writes (every parity class's sub-filter, back to back)
+long conv_flip_classes_numel(int K, int R, int S, int C, int sh, int sw, int ph, int pw);
 void conv_flip_classes_launch(const bf16_t* w, bf16_t* out, int K, int R, int S, int C, int sh,
                               int sw, int ph, int pw, hipStream_t st);
 void conv_flip_weights_multi_launch(const bf16_t* src, bf16_t* dst, const long* rows, int nrows,

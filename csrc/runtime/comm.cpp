@@ -137,6 +137,7 @@ uint64_t Communicator::enqueue(const char* name, hipStream_t producer, hipStream
   }
   if (cap != hipStreamCaptureStatusNone)
     throw std::runtime_error("RCCL collective on a stream whose capture was invalidated");
+  recycle_graph_events();
   if (producer != comm) {
     check_hip(hipEventRecord(ready_, producer), "hipEventRecord");
     check_hip(hipStreamWaitEvent(comm, ready_, 0), "hipStreamWaitEvent");
@@ -177,9 +178,23 @@ uint64_t Communicator::all_gather(const void* send, void* recv, size_t count, DT
   });
 }
 
+// A finished capture's events: stream capture turned their record / wait pairs into graph edges,
+// so no graph node references them — the next eager collective (or tracked replay) returns them
+// to the free list instead of keeping two per captured collective for the communicator's life.
+// Tickets of a finished capture are only waited on inside that capture, so its list is dropped.
+void Communicator::recycle_graph_events() {
+  if (graph_events_.empty() && graph_works_.empty()) return;
+  free_events_.insert(free_events_.end(), graph_events_.begin(), graph_events_.end());
+  graph_events_.clear();
+  graph_works_.clear();
+}
+
 uint64_t Communicator::track(const char* name, hipStream_t comm) {
   std::lock_guard<std::mutex> g(mu_);
   if (failed_ || !comm_) throw std::runtime_error("RCCL communicator failed: " + error_);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(comm, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone)
+    recycle_graph_events();
   hipEvent_t done = take_event();
   check_hip(hipEventRecord(done, comm), "hipEventRecord");
   const uint64_t t = next_ticket_++;

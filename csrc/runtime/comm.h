@@ -97,7 +97,9 @@ class Communicator {
   std::vector<hipEvent_t> parked_events_;
   // collectives issued while the producer stream is being captured into a HIP graph: they run
   // at every replay, so they are not watched as outstanding work (ncclCommGetAsyncError still
-  // is); their ordering events belong to the graph and live as long as the communicator
+  // is); their ordering events become graph edges at capture, so they return to the free list at
+  // the next eager collective or tracked replay (recycle_graph_events)
+  void recycle_graph_events();  // caller holds mu_, no capture in progress
   std::vector<std::pair<uint64_t, hipEvent_t>> graph_works_;
   std::vector<hipEvent_t> graph_events_;
   int sync_pins_ = 0;

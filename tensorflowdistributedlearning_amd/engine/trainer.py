@@ -191,6 +191,9 @@ class Trainer:
         self.static_x = x.detach().clone()
         self.static_y = y.detach().clone()
         self.graph_arena = workspace.ZeroArena()  # private: its addresses are baked in
+        # the warm-up runs on the stream the capture then records on: per-stream state sized by
+        # the warm-up (deterministic mode's reduction slabs, csrc/kernels/det.hip) exists at
+        # capture time, where it must not be allocated
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with workspace.use_arena(self.graph_arena):
@@ -211,7 +214,7 @@ class Trainer:
                 # thread_local: the native communicator's watchdog thread keeps polling its
                 # eager collectives' events during the capture (a global-mode capture would be
                 # invalidated by that)
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     # wgrads fork onto the side stream inside the capture and are joined back
                     # after backward (ops/streams.py), as in eager steps
                     cap_stream = torch.cuda.current_stream(self.device)

@@ -56,7 +56,9 @@ def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None, wgrad=None):
     for m in model.modules():
         if isinstance(m, Conv2d) and getattr(m, "fp8", False):
             m.fp8_dgrad, m.fp8_wgrad = bool(dgrad), bool(wgrad)
-    if wgrad and fuse_bn and isinstance(model, ResNet) and all(s is not None for s in stages):
+    from ..ops.conv import FP8_WGRAD
+    if wgrad and FP8_WGRAD and fuse_bn and isinstance(model, ResNet) \
+            and all(s is not None for s in stages):
         # a block's inner BNs (bn1 → conv2, bn2 → conv3) have one consumer each; when it is an
         # fp8 conv with an fp8 weight gradient, nothing reads their bf16 output: write e4m3 only
         for _, b in [(si, b) for si, st in enumerate(stages) for b in st]:
@@ -67,7 +69,6 @@ def enable_fp8(model, fuse_bn=True, dgrad=None, bf16_stages=None, wgrad=None):
                     inner[j].bn.emit_fp8 and getattr(nxt, "fp8_wgrad", False) and nxt.bias is None
                     and not nxt.grad_needs_unpad() and nxt.cin % 16 == 0 and nxt.cout % 16 == 0)
     if dgrad or wgrad:
-        from ..ops.conv import FP8_WGRAD
         bwd_only = os.environ.get("TDL_FP8_BWD_ONLY", "1") == "1"
         for m in model.modules():
             if isinstance(m, ConvBN) and getattr(m.conv, "fp8", False):

@@ -90,7 +90,12 @@ class FlatFlips:
     (``conv_flip_weights_multi``) instead of one per layer (46 per ResNet-50 step).  The flips sit
     at their weights' offsets in a parallel buffer, so a view never moves (HIP-graph replays
     refresh it in place).  A layer joins at its first call (flipped on its own for that version)
-    and the work list is rebuilt at the next version."""
+    and the work list is rebuilt at the next version.
+
+    The work list is never rebuilt while a HIP graph is being captured: its host-to-device copy
+    would read a pageable temporary freed after capture.  Layers still pending then flip on their
+    own inside the graph (``get`` returns None), and every work-list tensor a launch ever read is
+    kept alive, so a graph captured against an older list replays valid offsets."""
 
     def __init__(self, flat):
         self.flat = flat
@@ -98,6 +103,7 @@ class FlatFlips:
         self.segs = {}      # id(param) -> (offset, (K, R, S, C))
         self.pending = {}
         self.rows = None
+        self.retired = []   # earlier work lists (a captured graph may still read one)
         self.version = None
 
     @staticmethod
@@ -117,8 +123,9 @@ class FlatFlips:
         return fl
 
     def get(self, p, version):
+        capturing = torch.cuda.is_current_stream_capturing()
         if self.version != version:  # first call of a parameter version: flip every member
-            if self.pending:
+            if self.pending and not capturing:
                 self._rebuild()
             if self.segs:
                 from ..ops.common import ext
@@ -127,7 +134,7 @@ class FlatFlips:
         k = id(p)
         if k not in self.segs:
             self.pending[k] = (p._flat_offset, tuple(p.shape))
-            return None
+            return None  # flipped on its own (Conv2d.flip_weight) until the next rebuild
         off, (K, R, S, C) = self.segs[k]
         return self.buf[off:off + K * R * S * C].view(C, R, S, K)
 
@@ -143,6 +150,8 @@ class FlatFlips:
                 for kb in range((K + 31) // 32):
                     for cb in range((C + 31) // 32):
                         rows.append((off, K, R, S, C, tap, kb, cb))
+        if self.rows is not None:
+            self.retired.append(self.rows)
         self.rows = torch.tensor(rows, dtype=torch.int64).to(self.flat.device)
 
 

@@ -271,6 +271,8 @@ class _BatchNormActFn(torch.autograd.Function):
         fp8_only = (fp8 is not None and getattr(bn, "fp8_only", False) and residual is None
                     and (mask is not None or not relu))
         y = bn_apply(x, coef, residual, relu, fp8, mask, store_y=not fp8_only)
+        if fp8_only:  # the bf16 bytes of y are unwritten: consumers must read y._tdl_fp8
+            y._tdl_fp8_only = True
         ctx.mask_token = None
         if mask is not None:  # the consumers' dgrads may apply it for us (ops/gradjoin.py)
             ctx.mask_token = y._tdl_mask_token = gradjoin.MaskToken(mask, x)

@@ -437,6 +437,7 @@ class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, geom, relu, want_stats, layer, join, residual=None,
                 res_link=None):
+        x_in = x
         w = layer.compute_weight(x.dtype) if layer is not None else compute_weight(weight, x.dtype)
         stats = None
         if want_stats:
@@ -454,7 +455,15 @@ class _Conv2dFn(torch.autograd.Function):
                 # the weight gradient runs on this e4m3 copy (ops/conv._conv_param_grads): the
                 # bf16 input is not kept for the backward
                 ctx.x8 = (x8, sx)
+            elif getattr(x, "_tdl_fp8_only", False):
+                # the producing BN wrote only the e4m3 copy (models.enable_fp8): the bf16 weight
+                # gradient reads its dequantised values, never the unwritten bf16 bytes
+                from .fp8 import dequantize
+                x = dequantize(x8, sx).to(x.dtype)
         else:
+            if getattr(x, "_tdl_fp8_only", False):
+                raise RuntimeError("conv input has only an e4m3 copy (BatchNorm.fp8_only) but this "
+                                   "conv does not run on fp8 operands")
             y = conv_fwd(x, w, geom, bias=b, relu=relu, stats=stats, residual=residual)
         ctx.has_res = residual is not None
         ctx.res_link = res_link
@@ -465,7 +474,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.x_shape = tuple(x.shape)
         # the ReLU-mask token of the BN that produced x (ops/gradjoin.py): a single-consumer conv
         # applies the mask in its dgrad and may fuse that BN's backward statistics
-        ctx.bn_tok = getattr(x, "_tdl_mask_token", None) if join is None else None
+        ctx.bn_tok = getattr(x_in, "_tdl_mask_token", None) if join is None else None
         ctx.save_for_backward(None if getattr(ctx, "x8", None) is not None else x, weight, bias,
                               y if relu else None)
         if stats is None:

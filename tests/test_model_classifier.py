@@ -176,10 +176,15 @@ def test_resnet50_classifier_through_model_on_gpu(tmp_path, gpu):
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_model_graph_training_tracks_eager(tmp_path, gpu):
-    """The HIP-graph fold loop replays the eager fold loop: at lr = 0 (no chaotic amplification
-    of the fp32-atomic run-to-run noise of batch-statistics BN) every step's loss — on a new
-    batch each step, copied into the graph's static inputs — matches the eager loop's; with a
-    small learning rate the first steps still track."""
+    """The HIP-graph fold loop replays the eager fold loop.  In deterministic mode
+    (csrc/kernels/det.hip: every cross-workgroup fp32 atomic reduction — BN statistics, BN-backward
+    sums, loss terms — becomes per-workgroup slabs summed in a fixed order) the two loops run the
+    same kernels on the same data, so every step's loss — a new batch each step, copied into the
+    graph's static inputs, with SGD updates in between — must agree to 1e-6 relative.  Without
+    deterministic mode the fp32-atomic run-to-run noise is amplified by the updates (two EAGER
+    runs differ by up to 2.4 % at step 4: profiles/r05_graph_eager_gap.txt), so that leg only
+    checks the lr = 0 replay (no amplification)."""
+    from tensorflowdistributedlearning_amd.ops.common import ext
     kw = dict(CLS, device=None, save_checkpoints_steps=100, save_best=0, lr=0.0)
     ra = Model(str(tmp_path / "e"), "", hip_graph="off", **kw).train(192, None, 16, 8)[0]
     rb = Model(str(tmp_path / "g"), "", **kw).train(192, None, 16, 8)[0]
@@ -187,13 +192,18 @@ def test_model_graph_training_tracks_eager(tmp_path, gpu):
     assert len(set(round(v, 4) for v in ra["train_loss"])) > 3  # the batches differ
     # (bf16 steps with fp32-atomic BN statistics: run-to-run noise of a few 1e-3 relative)
     np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=5e-3, atol=5e-3)
-    kw.update(lr=0.002, momentum=0.0)
-    ra = Model(str(tmp_path / "e2"), "", hip_graph="off", **kw).train(192, None, 16, 4)[0]
-    rb = Model(str(tmp_path / "g2"), "", **kw).train(192, None, 16, 4)[0]
-    # once the weights move, two EAGER runs differ by up to 2.4 % at step 4 themselves (fp32-atomic
-    # BN statistics, amplified by the updates; dev/tools/graph_eager_gap.py,
-    # profiles/r05_graph_eager_gap.txt) — the graph must stay within that noise band
-    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=0.05, atol=0.01)
+    kw.update(lr=0.002, momentum=0.9)
+    ext().det_set(1)
+    try:
+        ra = Model(str(tmp_path / "e2"), "", hip_graph="off", **kw).train(192, None, 16, 6)[0]
+        rb = Model(str(tmp_path / "g2"), "", **kw).train(192, None, 16, 6)[0]
+        rc = Model(str(tmp_path / "e3"), "", hip_graph="off", **kw).train(192, None, 16, 6)[0]
+    finally:
+        ext().det_set(-1)
+    assert rb["hip_graph"] and not ra["hip_graph"]
+    assert ra["train_loss"][-1] != ra["train_loss"][0]  # the weights moved
+    np.testing.assert_array_equal(rc["train_loss"], ra["train_loss"])  # eager is repeatable
+    np.testing.assert_allclose(rb["train_loss"], ra["train_loss"], rtol=1e-6, atol=0)
 
 
 @pytest.mark.gpu

@@ -1090,3 +1090,32 @@ def test_flat_flips_match_per_layer_flips(gpu):
         assert torch.equal(got, ref)
         n += 1
     assert n >= 40, n
+
+
+@pytest.mark.gpu
+def test_capture_after_one_warmup_matches_eager(gpu):
+    """Trainer.capture(warmup=1) on a fresh trainer (what bench.py --graph --warmup 1 and the
+    ≥ 2-GPU capture test do): the warm-up step only registers the convs with the flat filter-flip
+    buffer (models/layers.FlatFlips), so its work list is still pending when the capture starts.
+    It must not be rebuilt inside the capture (a host-to-device copy from a pageable temporary):
+    the pending layers flip on their own in the graph.  In deterministic mode the replayed steps
+    equal the eager steps bit for bit, and a later eager step (work list rebuilt then) still does."""
+    import copy
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    torch.manual_seed(5)
+    x, y = imagenet_batch(8, 64, device=gpu)
+    ma = models.resnet50(num_classes=1000)
+    mb = copy.deepcopy(ma)
+    opt = dict(lr=0.01, momentum=0.9)
+    ext().det_set(1)
+    try:
+        ta = Trainer(ma, softmax_cross_entropy, gpu, "sgd", opt)
+        la = [float(ta.train_step(x, y)[0]) for _ in range(5)]
+        tb = Trainer(mb, softmax_cross_entropy, gpu, "sgd", opt)
+        tb.capture(x, y, warmup=1)
+        lb = [float(tb.warmup_out[0])] + [float(tb.replay()[0]) for _ in range(3)]
+        lb.append(float(tb.train_step(x, y)[0]))  # eager again after the graph
+    finally:
+        ext().det_set(-1)
+    assert la[-1] < la[0]
+    assert lb == la, (lb, la)
