@@ -182,6 +182,9 @@ def main():
     if n != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {n}")
     dev = ctx.device
+    if dev.type == "cuda" and os.environ.get("TDL_COMPUTE_PRIO"):
+        # A/B knob: run the step on a stream of the given HIP priority (lower = more urgent)
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=int(os.environ["TDL_COMPUTE_PRIO"])))
     rccl_ranks = ctx.rccl_ranks
     if dev.type == "cuda" and n > 1 and os.environ.get("TDL_SHARE_GPU") != "1" \
             and rccl_ranks != args.gpus:

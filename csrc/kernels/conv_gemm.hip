@@ -788,7 +788,7 @@ static bool conv_fwd_route(const ConvArgs& a0, hipStream_t st) {
   for (int i = route_next(p, -1); i >= 0; i = route_next(p, i)) {
     bool ran = false;
     switch (route_rule(i).impl) {
-      case RT_HALO: ran = conv_fwd_halo(a0, st); break;
+      case RT_HALO: ran = route_cfg(i) == 1 ? conv_fwd_rw(a0, st) : conv_fwd_halo(a0, st); break;
       case RT_PC: ran = conv_fwd_pc_run(a0, st); break;
       case RT_GLDS: ran = conv_fwd_glds(a0, route_cfg(i), st); break;
       case RT_GEMM: conv_fwd_gemm(a0, st); ran = true; break;

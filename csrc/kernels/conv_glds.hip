@@ -1382,6 +1382,7 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   set_fastdivs(a);
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
   if (!stats) a.stats = nullptr;
+  if (cfg == 101) return conv_fwd_rw_depi(a, st, fused);  // (statistics and join both fit)
   // statistics + join: only the 8-wave 256×64 tiles (cfg 4; the 256×128 ones spill)
   if (stats && a.beta && cfg != 4) return false;
   if (cfg == 100) return conv_fwd_halo_depi(a, st, fused);

@@ -27,6 +27,8 @@
 // ds_read_b64_tr_b16).
 #include "conv_common.h"
 
+#include <type_traits>
+
 namespace tdl {
 
 namespace {
@@ -641,6 +643,259 @@ __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, Hal
 }
 
 // ------------------------------------------------------------------------------------------
+// Resident-weight halo conv: stride-1 3×3, 64 → 64 channels — the ResNet layer-1 body conv
+// (/root/reference/core/resnet.py:137-138) and its input gradient run as a forward conv.
+//
+// conv_halo_kernel above streams the weight tile of every (tap, chunk) K-step through a ring and
+// synchronises the workgroup once per 16 MFMAs per wave: on 56×56×64 it kept the MFMA pipes 19.5 %
+// busy with 38 % of wave cycles in s_waitcnt and one SALU + one VALU instruction per MFMA of
+// cursor / ring / address arithmetic (profiles/r05_halo_narrow_pmc.txt).  With 64 input channels
+// the whole filter (9 taps × 64 × 64 bf16 = 72 KiB) fits in LDS beside two 40 KiB halo buffers, so
+// here:
+//  * the filter is DMA'd to LDS once per (persistent) workgroup and stays resident;
+//  * a tile is 8 output rows × ≤ 30 columns (a 256-lane virtual 8 × 32 grid); its 10 × 32-slot
+//    input halo is DMA'd once, double-buffered: the next tile's halo streams in while the 18
+//    K-steps (9 taps × 2 × 32 channels) of this one run — ONE barrier per tile, none per K-step;
+//  * the halo pitch (32 slots) and the tile grid are compile-time, so every fragment address is
+//    one of 6 per-lane base registers (tap column s × K half) plus a compile-time ds_read offset
+//    (tap row r, fragment row): the K loop has no address arithmetic at all;
+//  * epilogue shared with the other conv kernels (store_tile_bf16, rows given): bias / ReLU / BN
+//    Σ, Σ² (forward), ReLU bit mask / residual join / BN-backward Σg, Σg·x (input gradient).
+// ------------------------------------------------------------------------------------------
+struct RwGeom {
+  int N, H, W, Ho, Wo;  // direct-conv input / output (DEPI: dy → dx)
+  int ph, pw;           // top / left padding: tap (0, 0) of output (h, w) reads input (h−ph, w−pw)
+  int TW;               // valid output columns per tile (≤ RW_HP − 2)
+  int nrt, nct;         // row / column tiles per image
+  int ntiles, tpb;      // tiles in all, tiles per workgroup
+  int ldb;              // weight row (output channel) stride in elements: 9·64
+};
+
+constexpr int RW_TR = 8, RW_HP = 32;             // tile rows; halo pitch = virtual tile width
+constexpr int RW_HB = (RW_TR + 2) * RW_HP * 128;  // 40 KiB halo buffer (64 channels per slot)
+constexpr int RW_WOFF = 2 * RW_HB;               // resident filter: 9 taps × [64 rows][64 ch]
+constexpr int RW_REDOFF = RW_WOFF + 9 * 8192;    // BN statistics reduction rows
+constexpr int RW_LDS = RW_REDOFF + 2 * 4 * 64 * 4;
+static_assert(RW_LDS <= 160 * 1024, "LDS budget");
+constexpr int RW_HF = RW_HB / (8 * 1024);  // halo DMA instructions per wave (5)
+
+template <int IMM>
+__device__ __forceinline__ bf16x8 rw_read(uint32_t base) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(IMM) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// fragments of K-step k = tap·2 + kk: A (pixels) rows 2wm + (rm >> 1), column halves rm & 1
+// (ve / vo: the lane's slot in an even / odd fragment at tap column s); B (output channels
+// wn·32 + rn·16 + …) from the resident filter, tap blocks 8 KiB apart (vb4: taps 4–8, keeping the
+// offsets inside ds_read's 16-bit field)
+template <int K>
+__device__ __forceinline__ void rw_frags(const uint32_t (&ve)[3][2], const uint32_t (&vo)[3][2],
+                                         const uint32_t (&vb)[2], const uint32_t (&vb4)[2],
+                                         bf16x8 (&af)[4], bf16x8 (&bfg)[2]) {
+  constexpr int t = K >> 1, kk = K & 1, r = t / 3, s = t % 3;
+  constexpr int RO = RW_HP * 128;  // one halo row
+  af[0] = rw_read<r * RO>(ve[s][kk]);
+  af[1] = rw_read<r * RO>(vo[s][kk]);
+  af[2] = rw_read<(r + 1) * RO>(ve[s][kk]);
+  af[3] = rw_read<(r + 1) * RO>(vo[s][kk]);
+  constexpr int tb = t < 4 ? t : t - 4;
+  const uint32_t b = t < 4 ? vb[kk] : vb4[kk];
+  bfg[0] = rw_read<tb * 8192>(b);
+  bfg[1] = rw_read<tb * 8192 + 2048>(b);
+}
+
+template <int K, int N, typename F>
+__device__ __forceinline__ void rw_static_for(F&& f) {
+  if constexpr (K < N) {
+    f(std::integral_constant<int, K>{});
+    rw_static_for<K + 1, N>(f);
+  }
+}
+
+template <bool DEPI, bool BIAS, bool STATS, bool NJ>
+__global__ void __launch_bounds__(512, 1) conv_rw_kernel(ConvArgs a, RwGeom g) {
+  static_assert(!(DEPI && BIAS), "no bias on an input gradient");
+  constexpr int NW = 8, RM = 4, RN = 2, TM = 64, TN = 32, NSTEP = 18;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int t0 = blk * g.tpb;
+  const int ntile = min(g.tpb, g.ntiles - t0);
+  if (ntile <= 0) return;
+  const rsrc_t rin = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t rw = make_rsrc(a.w, a.w_bytes);
+  const rsrc_t rout = make_rsrc(a.out, a.out_bytes);
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_char_t*)smem;
+  const int l15 = lane & 15, lch = lane >> 4;
+
+  // ---- resident filter: tap t, output channel row, 64 input channels as a KC row (kc_off) ----
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int q = j * NW + wid;  // 1-KiB piece: tap q >> 3, rows (q & 7)·8 … +7
+    const int tap = q >> 3, row = (q & 7) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    hdma16(rw, smem + RW_WOFF + q * 1024, (uint32_t)((row * g.ldb + tap * 64 + lc * 8) * 2));
+  }
+
+  struct RT {
+    int n, h0, w0;
+  };
+  auto tile_at = [&](int t) {
+    RT r;
+    const int tc = t % g.nct, rest = t / g.nct;
+    const int tr = rest % g.nrt;
+    r.n = rest / g.nrt;
+    r.h0 = tr * RW_TR;
+    r.w0 = tc * g.TW;
+    return r;
+  };
+  // halo slot (hr, hc) = input pixel (h0 − ph + hr, w0 − pw + hc); 16-B chunk c of slot s sits at
+  // position c ^ (s & 7) (conflict-free ds_read_b128 groups: a group reads 16 consecutive slots)
+  auto fill = [&](const RT& T, int buf) {
+    char* hb = smem + buf * RW_HB;
+#pragma unroll
+    for (int j = 0; j < RW_HF; ++j) {
+      const int q = j * NW + wid;
+      const int s = q * 8 + (lane >> 3);
+      const int hr = s / RW_HP, hc = s % RW_HP;
+      const int hi = T.h0 - g.ph + hr, wi = T.w0 - g.pw + hc;
+      const bool v = hc < g.TW + 2 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+      const int lc = (lane & 7) ^ (s & 7);
+      hdma16(rin, hb + q * 1024,
+             v ? (uint32_t)((((T.n * g.H + hi) * g.W + wi) * 64 + lc * 8) * 2) : HOOB);
+    }
+  };
+
+  // per-lane fragment bases.  A: slot of (row 2wm, column l15 + s) — an odd fragment adds 16
+  // columns, except in lanes whose column would pass the tile width: they read column l15 (finite
+  // halo data) and their output rows are dropped.  B: filter row wn·32 + l15, K half kk.
+  const uint32_t d16 = 16 + l15 < g.TW ? 16u * 128u : 0u;
+  uint32_t vb[2], vb4[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    vb[kk] = lds0 + (uint32_t)(RW_WOFF + (wn * 32 + l15) * 128 +
+                               ((((kk * 4 + lch) ^ ((l15 >> 1) & 7))) << 4));
+    vb4[kk] = vb[kk] + 4u * 8192u;
+  }
+  uint32_t va[3][2];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      va[s][kk] = (uint32_t)((2 * wm * RW_HP + l15 + s) * 128 +
+                             ((((l15 + s) & 7) ^ (kk * 4 + lch)) << 4));
+
+  f32x4 acc[RM][RN];
+  float s_sum[RN][4], s_sq[RN][4];
+#pragma unroll
+  for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_sum[rn][i] = s_sq[rn][i] = 0.f;
+  Tile Tep;  // the shared epilogue reads bn0 (mask slab column) only; rows come from rows_in
+  Tep.bm0 = 0;
+  Tep.bn0 = 0;
+  Tep.cls = 0;
+  Tep.Mc = 0;
+  Tep.Kgc = 0;
+  Tep.kt0 = Tep.kt1 = 0;
+  Tep.split = 0;
+  constexpr int E = RM * RN / 2;  // epilogue 16-B stores per lane (64 = WN·TN columns: wide)
+
+  RT cur = tile_at(t0);
+  fill(cur, 0);
+  hwait<0>();
+  hbarrier();
+  for (int i = 0; i < ntile; ++i) {
+    const int buf = i & 1;
+    RT nxt = cur;
+    if (i + 1 < ntile) {
+      nxt = tile_at(t0 + i + 1);
+      fill(nxt, buf ^ 1);  // last read in tile i − 1 (barrier below)
+    }
+    const uint32_t hb = lds0 + (uint32_t)(buf * RW_HB);
+    uint32_t ve[3][2], vo[3][2];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ve[s][kk] = hb + va[s][kk];
+        vo[s][kk] = ve[s][kk] + d16;
+      }
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) acc[rm][rn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[2][RM], fb[2][RN];
+    rw_frags<0>(ve, vo, vb, vb4, fa[0], fb[0]);
+    hlgkm0();
+    rw_static_for<0, NSTEP>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k + 1 < NSTEP) rw_frags<k + 1>(ve, vo, vb, vb4, fa[(k + 1) & 1], fb[(k + 1) & 1]);
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn)
+          acc[rm][rn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[k & 1][rn], fa[k & 1][rm],
+                                                                acc[rm][rn], 0, 0, 0);
+      hlgkm0();
+    });
+    // ---- epilogue: lane rows (2wm + (rm >> 1), (rm & 1)·16 + l15) of the tile ----
+    uint32_t rows_in[RM];
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const int h = cur.h0 + 2 * wm + (rm >> 1), col = (rm & 1) * 16 + l15, w = cur.w0 + col;
+      rows_in[rm] = h < g.Ho && col < g.TW && w < g.Wo
+                        ? (uint32_t)(((cur.n * g.Ho + h) * g.Wo + w) * a.ldc) * 2u
+                        : ROW_OOB;
+    }
+    store_tile_bf16<DEPI ? DGRAD : FWD, RM, RN, TM, TN, BIAS, STATS, false, false, NJ, false,
+                    true>(a, Tep, acc, wm, wn, lane, rout, 1.f, false, s_sum, s_sq, rows_in);
+    // the next tile's halo has landed (only this epilogue's stores may still be in flight) and
+    // every wave is done with this tile's buffer
+    hwait<E>();
+    hbarrier();
+    cur = nxt;
+  }
+
+  if constexpr (STATS) {
+#pragma unroll
+    for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s_sum[rn][i] += __shfl_xor(s_sum[rn][i], o, 64);
+          s_sq[rn][i] += __shfl_xor(s_sq[rn][i], o, 64);
+        }
+      }
+    float* red = (float*)(smem + RW_REDOFF);
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int nl = wn * TN + rn * 16 + (lane >> 4) * 4 + i;
+          red[(wm * 2 + 0) * 64 + nl] = s_sum[rn][i];
+          red[(wm * 2 + 1) * 64 + nl] = s_sq[rn][i];
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < 2 * 64; t += 64 * NW) {
+      const int which = t / 64, nl = t - which * 64;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += red[(w * 2 + which) * 64 + nl];
+      atomicAdd(a.stats + which * 64 + nl, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
 struct HCfg {
@@ -824,7 +1079,81 @@ bool plan_halo_wgrad(const ConvArgs& a, HaloGeom& g, HaloWg& q, int& bm) {
   return true;
 }
 
+// the resident-weight conv's geometry; false when the kernel does not take the problem
+bool plan_rw(const ConvArgs& a, RwGeom& g, int& blocks) {
+  if (a.R != 3 || a.S != 3 || a.sh != 1 || a.sw != 1 || a.dh != 1 || a.dw != 1) return false;
+  if (a.C != 64 || a.K != 64 || a.ldc < 64 || a.ldc % 8) return false;
+  if (a.aff || a.fp8 || a.res) return false;
+  if (a.mask && a.ldc % 64) return false;  // mask slabs: 64-column rows
+  if (a.x_bytes >= 0x70000000u || a.w_bytes >= 0x70000000u || a.out_bytes >= ROW_OOB) return false;
+  if (a.Ho < 1 || a.Wo < 1 || a.Ho > a.H + 2 || a.Wo > a.W + 2) return false;
+  g = RwGeom{};
+  g.N = a.N; g.H = a.H; g.W = a.W; g.Ho = a.Ho; g.Wo = a.Wo;
+  g.ph = a.ph; g.pw = a.pw;
+  g.nct = cdiv(a.Wo, RW_HP - 2);
+  g.TW = cdiv(a.Wo, g.nct);
+  g.nrt = cdiv(a.Ho, RW_TR);
+  const long tiles = (long)a.N * g.nrt * g.nct;
+  if (tiles >= (1L << 30)) return false;
+  g.ntiles = (int)tiles;
+  const int cus = henv("TDL_RW_SLOTS", 256);
+  g.tpb = std::max(1, cdiv(g.ntiles, cus));
+  blocks = cdiv(g.ntiles, g.tpb);
+  g.ldb = 9 * 64;
+  return true;
+}
+
+template <bool DEPI, bool BIAS, bool STATS, bool NJ>
+void launch_rw(const ConvArgs& a, const RwGeom& g, int blocks, hipStream_t st) {
+  auto k = conv_rw_kernel<DEPI, BIAS, STATS, NJ>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, RW_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(512), RW_LDS, st, a, g);
+}
+
 }  // namespace
+
+// route row fwd.halo.rw64: the resident-weight 3×3 64 → 64 forward (false: not eligible)
+bool conv_fwd_rw(const ConvArgs& a, hipStream_t st) {
+  RwGeom g;
+  int blocks;
+  if (!plan_rw(a, g, blocks)) return false;
+  const bool stats = a.stats != nullptr, bias = a.bias != nullptr;
+  if (bias) {
+    if (stats) launch_rw<false, true, true, true>(a, g, blocks, st);
+    else launch_rw<false, true, false, true>(a, g, blocks, st);
+  } else {
+    if (stats) launch_rw<false, false, true, true>(a, g, blocks, st);
+    else launch_rw<false, false, false, true>(a, g, blocks, st);
+  }
+  return true;
+}
+
+// route row dgrad.asfwd.rw64: a stride-1 3×3 64 → 64 input gradient already rewritten as the
+// forward conv of dy with the flipped filter (conv_dgrad_as_fwd), DGRAD epilogue (ReLU bit mask,
+// residual join, BN-backward sums); *fused: a.stats was filled
+bool conv_fwd_rw_depi(const ConvArgs& a, hipStream_t st, bool* fused) {
+  if (fused) *fused = false;
+  RwGeom g;
+  int blocks;
+  if (a.bias || !plan_rw(a, g, blocks)) return false;
+  const bool stats = a.stats != nullptr && a.bn_x != nullptr;
+  ConvArgs b = a;
+  if (!stats) b.stats = nullptr;
+  b.Ng = 64;
+  if (stats) {
+    if (a.beta) launch_rw<true, false, true, false>(b, g, blocks, st);
+    else launch_rw<true, false, true, true>(b, g, blocks, st);
+  } else {
+    if (a.beta) launch_rw<true, false, false, false>(b, g, blocks, st);
+    else launch_rw<true, false, false, true>(b, g, blocks, st);
+  }
+  if (fused) *fused = stats;
+  return true;
+}
 
 // route rows wgrad.halo.*: false when the kernel does not take the problem
 bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p) {

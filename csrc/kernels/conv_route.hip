@@ -16,7 +16,7 @@ constexpr int FWD = 0, DGRAD = 1, WGRAD = 2;
 constexpr int INF = 1 << 30;
 constexpr int TAPS = 1 << 20;  // no upper bound on filter taps
 constexpr int HT = 16;         // the halo kernel's tap table (conv_halo.hip HALO_MAXTAP)
-constexpr int ASF_HALO = 100, ASF_PC = 102;
+constexpr int ASF_HALO = 100, ASF_RW = 101, ASF_PC = 102;
 
 // Rows are tried in order; the first whose window matches and whose kernel takes the problem
 // runs.  `test` rows are live only while their family is forced onto every aligned problem
@@ -31,6 +31,8 @@ const RouteRule kRoutes[] = {
    "fp8 forward with < 128 outputs: 4-wave 256x64 tiles"},
   {"fwd.pc.folded_bn",            FWD,   RT_PC,    1, TAPS,  0, 64, INF,     128, INF,    4096,  256, 128, 128, RF_AFF,           RF_BIAS | RF_RES | RF_FP8,            0,    true,  false,
    "opt-in BN+ReLU fold: the producer waves stage the transformed A tile (profiles/r05_bnconv_fold_ab.txt)"},
+  {"fwd.halo.rw64",               FWD,   RT_HALO,  9, 9,     1, 64, 64,      64, 64,      4096,  0, 0,     0,  0,                  RF_AFF | RF_RES | RF_FP8,             1,    true,  false,
+   "stride-1 3x3 64->64: filter resident in LDS, one barrier per 8-row halo tile (conv_halo.hip conv_rw_kernel)"},
   {"fwd.halo.narrow",             FWD,   RT_HALO,  3, HT,    1, 64, INF,     1, 64,       4096,  0, 0,     0,  0,                  RF_AFF | RF_RES | RF_FP8,             0,    true,  false,
    "stride-1 3x3 with <= 64 outputs: halo tiles, ResNet layer1 683 -> 520 us at b1024 (profiles/r04_halo_ab.txt)"},
   {"fwd.halo.aligned",            FWD,   RT_HALO,  3, HT,    1, 64, INF,     1, INF,      0,     0, 0,     0,  0,                  RF_AFF | RF_RES | RF_FP8,             0,    true,  true,
@@ -60,6 +62,8 @@ const RouteRule kRoutes[] = {
    "fp8 dgrad (e5m2 dy x e4m3 W^T): LDS-DMA kernel only"},
   {"dgrad.glds.fp8",              DGRAD, RT_GLDS,  1, TAPS,  0, 65, INF,     128, INF,    0,     0, 0,     0,  RF_FP8,             0,                                    0,    true,  false,
    "fp8 dgrad (e5m2 dy x e4m3 W^T): LDS-DMA kernel only"},
+  {"dgrad.asfwd.rw64",            DGRAD, RT_ASFWD, 9, 9,     1, 64, 64,      64, 64,      4096,  0, 0,     0,  RF_WFLIP,           RF_AFF | RF_FP8 | RF_STRIDED,         ASF_RW, true, false,
+   "stride-1 3x3 64->64 dgrad as the forward conv on the resident-filter halo kernel (mask, join, BN-backward sums)"},
   {"dgrad.asfwd.halo",            DGRAD, RT_ASFWD, 3, HT,    1, 8, 64,       64, INF,     4096,  0, 0,     0,  RF_WFLIP,           RF_STATS | RF_AFF | RF_FP8,           ASF_HALO, true, false,
    "<= 64-wide dx as the forward conv of dy on the halo loader: 698 -> 503 us (bench/dgrad_paths.py, profiles/r05_dgrad_as_fwd.txt)"},
   {"dgrad.asfwd.halo.aligned",    DGRAD, RT_ASFWD, 3, HT,    1, 8, INF,      64, INF,     0,     0, 0,     0,  RF_WFLIP,           RF_STATS | RF_AFF | RF_FP8,           ASF_HALO, true, true,
@@ -248,12 +252,13 @@ void route_reset() { state() = defaults(); }
 bool route_cfg_instantiated(int impl, int op, int cfg, int flags) {
   switch (impl) {
     case RT_GEMM:
-    case RT_HALO:
     case RT_PC:
       return cfg == 0;
+    case RT_HALO:  // 1: the resident-filter 3x3 64 -> 64 forward
+      return cfg == 0 || (op == FWD && cfg == 1 && !(flags & (RF_AFF | RF_RES | RF_FP8)));
     case RT_ASFWD:
       if (flags & RF_FP8) return op == DGRAD && cfg == 0;
-      return op == DGRAD && (cfg == 0 || cfg == 4 || cfg == ASF_HALO || cfg == ASF_PC);
+      return op == DGRAD && (cfg == 0 || cfg == 4 || cfg == ASF_HALO || cfg == ASF_RW || cfg == ASF_PC);
     case RT_GLDS:
       if (flags & RF_FP8) return op == WGRAD ? (cfg == 0 || cfg == 2) : (cfg == 0 || cfg == 1);
       if (op == FWD) return (flags & RF_RES) ? (cfg == 0 || cfg == 4) : (cfg >= 0 && cfg <= 5);
@@ -282,7 +287,7 @@ int route_family_mode(const RouteRule& r) {
       return glds;
     case RT_ASFWD:
       if (glds == 0) return 0;
-      return r.cfg == ASF_HALO ? halo : glds;
+      return r.cfg == ASF_HALO || r.cfg == ASF_RW ? halo : glds;
     default:
       // fp8 operands exist only on the LDS-DMA kernel: its rows ignore the mode switch
       return (r.need & RF_FP8) ? 1 : glds;

@@ -163,6 +163,10 @@ bool conv_dgrad_halo(const ConvArgs& a, hipStream_t st, bool* fused);
 // a stride-1 dgrad already rewritten as a forward conv (conv_dgrad_as_fwd) on the halo forward
 // loader with the DGRAD epilogue
 bool conv_fwd_halo_depi(const ConvArgs& a, hipStream_t st, bool* fused);
+// resident-weight halo conv (conv_halo.hip): stride-1 3×3, 64 → 64 channels — the forward and a
+// dgrad already rewritten as a forward conv (DGRAD epilogue); false: not eligible
+bool conv_fwd_rw(const ConvArgs& a, hipStream_t st);
+bool conv_fwd_rw_depi(const ConvArgs& a, hipStream_t st, bool* fused);
 // stride-1 3×3 weight gradient on the halo kernel: plan impl 2 (fp32 split slabs as usual)
 bool conv_wgrad_halo_plan(const ConvArgs& a, WgradPlan* p);
 void conv_wgrad_halo_launch(const ConvArgs& a, const WgradPlan& p, hipStream_t st);

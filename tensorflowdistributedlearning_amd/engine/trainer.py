@@ -245,6 +245,18 @@ class Trainer:
         _params.bump_version()
         return self.graph_out
 
+    def release_graph(self):
+        """Back to eager steps after :meth:`capture`: drop the graph (and its private arena) and
+        let the update kernel read the host learning rate again.  Counters carry on from the
+        replays."""
+        if self.graph is None:
+            return
+        torch.cuda.synchronize(self.device)
+        self.graph = None
+        self.graph_out = None
+        self.graph_arena = None
+        self.optimizer.set_device_lr(False)
+
     @torch.no_grad()
     def eval_step(self, x):
         self.model.eval()

@@ -82,6 +82,9 @@ _ORIGIN: dict = {}    # device -> the stream that last forked work onto the side
 # dgrad too); TDL_WGRAD_EARLY=0 records it after the dgrad launch (the previous ordering, for A/B).
 EARLY_WAIT = os.environ.get("TDL_WGRAD_EARLY", "1") == "1"
 _SIDE: dict = {}
+# HIP stream priority of the side stream (A/B knob; torch.cuda.Stream.priority_range(): lower is
+# more urgent)
+SIDE_PRIO = int(os.environ.get("TDL_SIDE_PRIO", "0"))
 
 
 def enabled() -> bool:
@@ -105,7 +108,7 @@ def side(device):
         _FORKED.add(torch.device(device))
     s = _SIDE.get(device)
     if s is None:
-        s = _SIDE[device] = torch.cuda.Stream(device=device)
+        s = _SIDE[device] = torch.cuda.Stream(device=device, priority=SIDE_PRIO)
     cur = current(device)
     if cur != s:
         _ORIGIN[torch.device(device)] = cur

@@ -49,7 +49,7 @@ def test_rows_are_well_formed(e):
 # statistics), dgrad (fused BN-backward sums; stride 1: flipped filter available), wgrad
 RESNET50 = [
     ((56, 64, 64, 1, 1), "fwd.glds.1x1n64", "dgrad.asfwd.glds.n64", "wgrad.gemm"),
-    ((56, 64, 64, 3, 1), "fwd.halo.narrow", "dgrad.asfwd.glds.n64", "wgrad.gemm"),
+    ((56, 64, 64, 3, 1), "fwd.halo.rw64", "dgrad.asfwd.rw64", "wgrad.gemm"),
     ((56, 64, 256, 1, 1), "fwd.glds.wide", "dgrad.asfwd.glds.n64", "wgrad.glds.1x1"),
     ((56, 256, 64, 1, 1), "fwd.glds.1x1n64", "dgrad.asfwd.glds", "wgrad.gemm"),
     ((28, 128, 128, 3, 2), "fwd.glds.wide", "dgrad.glds.stats", "wgrad.gemm"),
@@ -74,9 +74,11 @@ def test_resnet50_default_routes(e, shape, fwd, dgrad, wgrad):
 
 def test_dgrad_variants(e):
     rows = 256 * 56 * 56
-    # no statistics: the producer/consumer dgrad-as-forward for wide 3x3s, the halo one for narrow
+    # no statistics: the producer/consumer dgrad-as-forward for wide 3x3s, the resident-filter
+    # halo one for 64 -> 64 and the streaming halo one for other narrow ones
     assert e.conv_route_select(DGRAD, 9, 1, 256, 256, 256 * 14 * 14, W)[0] == "dgrad.asfwd.pc"
-    assert e.conv_route_select(DGRAD, 9, 1, 64, 64, rows, W)[0] == "dgrad.asfwd.halo"
+    assert e.conv_route_select(DGRAD, 9, 1, 64, 64, rows, W)[0] == "dgrad.asfwd.rw64"
+    assert e.conv_route_select(DGRAD, 9, 1, 64, 128, rows, W)[0] == "dgrad.asfwd.halo"
     # statistics + join: 8-wave tiles only — the forward K loop's with a flipped filter, else the
     # DGRAD kernel's
     f = S | J | 128 | W

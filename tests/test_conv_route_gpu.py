@@ -218,3 +218,58 @@ def test_route_cfg_override_runs_that_config(gpu):
     finally:
         e.conv_route_force(0, "")
         e.conv_route_reset()
+
+
+@pytest.mark.parametrize("N,H", [(2, 56), (3, 28), (2, 26), (3, 13)])
+def test_resident_filter_conv_epilogues(gpu, N, H):
+    """The resident-filter 3x3 64 -> 64 kernel (conv_halo.hip conv_rw_kernel; route rows
+    fwd.halo.rw64 / dgrad.asfwd.rw64) with every epilogue it takes, against the fp32 oracle:
+    forward with bias + fused BN sums (Σy, Σy²); input gradient (as the forward conv of dy with
+    the flipped filter) with the ReLU bit mask, the residual join (dx += …) and the BN-backward
+    sums (Σg, Σg·x) — on tile grids with ragged rows (H % 8) and a single column tile (H ≤ 30)."""
+    e = _ext()
+    torch.manual_seed(H)
+    g = C.ConvGeom((1, 1), (1, 1, 1, 1), (1, 1))
+    x = (torch.randn(N, H, H, 64) * 1.3 + 0.2).bfloat16().to(gpu)
+    w = (torch.randn(64, 3, 3, 64) / 24).bfloat16().to(gpu)
+    bias = torch.randn(64, device=gpu) * 0.1
+    e.conv_route_force(0, "fwd.halo.rw64")
+    try:
+        stats = torch.zeros(2, 64, device=gpu)
+        y = torch.empty(N, H, H, 64, device=gpu, dtype=torch.bfloat16)
+        e.conv_fwd(x, w, y, bias, stats, *_args(g), False)
+        torch.cuda.synchronize()
+        assert e.conv_last_route(0) == "fwd.halo.rw64"
+    finally:
+        e.conv_route_force(0, "")
+    ref = C.ref_conv_fwd(x.float().cpu(), w.float().cpu(), g) + bias.cpu()
+    assert _rel(y, ref) < 1e-2
+    yb = y.float().cpu().reshape(-1, 64)
+    assert _rel(stats, torch.stack([yb.sum(0), (yb * yb).sum(0)])) < 1e-3
+
+    # input gradient: mask of a BN output, join onto an existing dx, BN-backward sums against x
+    dy = torch.randn(N, H, H, 64).bfloat16().to(gpu)
+    coef = _coef(64, gpu)
+    mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+    B.bn_apply(x, coef, None, True, mask=mask)
+    m = B.unpack_relu_mask(mask.cpu(), 64).reshape(N, H, H, 64)
+    wf = torch.empty(64, 3, 3, 64, device=gpu, dtype=torch.bfloat16)
+    e.conv_flip_weight(w, wf)
+    base = C.ref_conv_dgrad(dy.float().cpu(), w.float().cpu(), x.shape, g)
+    for join in (False, True):
+        prev = torch.randn(N, H, H, 64).bfloat16().to(gpu) if join else None
+        dx = prev.clone() if join else torch.empty_like(x)
+        red = torch.zeros(2, 64, device=gpu)
+        e.conv_route_force(1, "dgrad.asfwd.rw64")
+        try:
+            fused = e.conv_dgrad(dy, w, dx, *_args(g), join, mask, None, x, red, None, wf)
+            torch.cuda.synchronize()
+            assert e.conv_last_route(1) == "dgrad.asfwd.rw64"
+        finally:
+            e.conv_route_force(1, "")
+        want = (base + (prev.float().cpu() if join else 0)) * m
+        assert _rel(dx, want) < 1e-2, join
+        if not e.deterministic():
+            assert fused
+            gf, xf = dx.float().cpu().reshape(-1, 64), x.float().cpu().reshape(-1, 64)
+            assert _rel(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-3

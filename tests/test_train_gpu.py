@@ -567,6 +567,76 @@ def test_bench_two_ranks_share_one_gpu(gpu, tmp_path):
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
 
 
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+def test_two_ranks_equal_single_process_average(gpu, tmp_path, grad_dtype):
+    """Data-parallel numerics on the real GPU paths (reference towers: one all-reduced pack of
+    gradients, /root/reference/model.py:114-116,156-159): two ranks share the one visible device
+    (TDL_SHARE_GPU, gloo collectives), each trains ResNet-50 on its own half-batch with the weight
+    gradients on the side stream and the bucketed all-reduce overlapping backward
+    (tests/_dp_worker.py, deterministic mode).  After 3 SGD-momentum steps both ranks' master
+    weights must be bit-identical (the broadcast and the averaged update) and equal a
+    single-process run that computes each half-batch's gradients with its own BN statistics,
+    sums them (bf16 buckets: rounded to bf16 first, summed and rounded again, as the bf16
+    collective does) and applies the update with the 1/world scale."""
+    import os
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _dp_worker as W
+    from tensorflowdistributedlearning_amd.ops.common import ext
+    from tensorflowdistributedlearning_amd.ops import streams
+    from tensorflowdistributedlearning_amd.ops import workspace
+    steps = 3
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TDL_SHARE_GPU="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port",
+           "29641" if grad_dtype == "fp32" else "29643",
+           os.path.join(root, "tests", "_dp_worker.py"), str(tmp_path), grad_dtype, str(steps)]
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert r0["side_stream"] and r0["buckets"] >= 2
+    assert torch.equal(r0["master"], r1["master"]), "ranks diverged"
+    assert r0["losses"] != r1["losses"]  # different half-batches
+
+    # single-process reference: the same two half-batches, gradients averaged by hand
+    ext().det_set(1)
+    try:
+        torch.manual_seed(1234)
+        model = models.build("resnet50", num_classes=1000)
+        tr = Trainer(model, softmax_cross_entropy, gpu, "sgd",
+                     dict(lr=W.LR, momentum=W.MOMENTUM, weight_decay=W.WD))
+        halves = [imagenet_batch(W.BATCH, W.SIZE, device=gpu, seed=s) for s in (0, 1)]
+        losses = [[], []]
+        for _ in range(steps):
+            total = None
+            for i, (x, y) in enumerate(halves):
+                workspace.reset(gpu)
+                tr.flat.begin_step()
+                loss = softmax_cross_entropy(model(x), y)
+                loss.backward()
+                streams.join(gpu)
+                tr.flat.finish_grads()
+                losses[i].append(float(loss))
+                g = tr.flat.grad.clone()
+                if grad_dtype == "bf16":
+                    g = g.bfloat16()
+                total = g if total is None else total + g
+            tr.flat.grad.copy_(total.float())
+            tr.optimizer.step(grad_scale=0.5)
+        torch.cuda.synchronize(gpu)
+    finally:
+        ext().det_set(-1)
+    assert losses[0] == r0["losses"] and losses[1] == r1["losses"], (losses, r0["losses"],
+                                                                      r1["losses"])
+    ref = tr.flat.master.detach().cpu()
+    diff = (ref - r0["master"]).abs().max().item()
+    assert torch.equal(ref, r0["master"]), f"max |Δ| {diff:g} vs the single-process average"
+
+
 def _stall_side_stream(gpu, cycles=20_000_000):
     """Queue a long spin kernel on the wgrad side stream so that every side-stream write lands
     milliseconds after the compute stream could have moved on: a missing join then reads stale
@@ -1114,6 +1184,7 @@ def test_capture_after_one_warmup_matches_eager(gpu):
         tb = Trainer(mb, softmax_cross_entropy, gpu, "sgd", opt)
         tb.capture(x, y, warmup=1)
         lb = [float(tb.warmup_out[0])] + [float(tb.replay()[0]) for _ in range(3)]
+        tb.release_graph()
         lb.append(float(tb.train_step(x, y)[0]))  # eager again after the graph
     finally:
         ext().det_set(-1)
