@@ -933,6 +933,56 @@ bool maxpool_bwd_stats(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, i
                                   pt, pl, stream());
 }
 
+// the ResNet stem's training BN + ReLU + max-pool in one pass (pool.hip bn_maxpool_fwd_kernel):
+// y = maxpool(relu(x·coef[0] + coef[1])) with the ReLU bit of each window maximum in idx bit 7;
+// false: not eligible (C % 8), nothing launched
+bool bn_maxpool_fwd(Tensor x, Tensor coef, Tensor y, Tensor idx, int64_t k, int64_t s, int64_t pt,
+                    int64_t pl) {
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(y, torch::kBFloat16);
+  CHECK_T(idx, torch::kUInt8);
+  CHECK_T(coef, torch::kFloat32);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(3) == y.size(3) &&
+                  idx.numel() == y.numel() && coef.numel() >= 2 * x.size(3) && k * k <= 127 &&
+                  k >= 1 && s >= 1,
+              "bn_maxpool_fwd: x [N,H,W,C], y / idx [N,Ho,Wo,C], coef [>=2, C], k*k < 128");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && idx.is_contiguous() && coef.is_contiguous(),
+              "bn_maxpool_fwd: contiguous operands");
+  return bn_maxpool_fwd_launch(BF(x), coef.data_ptr<float>(), BFW(y), idx.data_ptr<uint8_t>(),
+                               x.size(0), x.size(1), x.size(2), x.size(3), y.size(1), y.size(2), k,
+                               s, pt, pl, stream());
+}
+
+// backward of bn_maxpool_fwd: dx = the gathered dy where the window maximum was > 0 (idx bit 7);
+// with bn_x / bn_red (and outside deterministic mode) also the BN-backward sums (Σg, Σg·x) into
+// bn_red [2, C] (zeroed by the caller) — returns whether they were accumulated
+bool maxpool_bwd_rb(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, int64_t pt, int64_t pl,
+                    c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_red) {
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  CHECK_T(idx, torch::kUInt8);
+  TORCH_CHECK(dy.dim() == 4 && dx.dim() == 4 && dy.size(0) == dx.size(0) &&
+                  dy.size(3) == dx.size(3) && dx.size(3) % 8 == 0 && idx.numel() == dy.numel() &&
+                  dy.is_contiguous() && dx.is_contiguous() && idx.is_contiguous(),
+              "maxpool_bwd_rb: dy / idx [N,Ho,Wo,C], dx [N,H,W,C], C % 8 == 0");
+  const bool stats = bn_x.has_value() && bn_x->defined() && bn_red.has_value() &&
+                     bn_red->defined() && !deterministic();
+  if (stats) {
+    CHECK_T((*bn_x), torch::kBFloat16);
+    CHECK_T((*bn_red), torch::kFloat32);
+    TORCH_CHECK(bn_x->sizes() == dx.sizes() && bn_x->is_contiguous() &&
+                    bn_red->numel() == 2 * dx.size(3),
+                "maxpool_bwd_rb: bn_x like dx, bn_red [2, C]");
+    if (maxpool_bwd_stats_launch(BF(dy), idx.data_ptr<uint8_t>(), BFW(dx), BF((*bn_x)), nullptr,
+                                 bn_red->data_ptr<float>(), dx.size(0), dx.size(1), dx.size(2),
+                                 dx.size(3), dy.size(1), dy.size(2), k, s, pt, pl, stream()))
+      return true;
+  }
+  maxpool_bwd_rb_launch(BF(dy), idx.data_ptr<uint8_t>(), BFW(dx), dx.size(0), dx.size(1),
+                        dx.size(2), dx.size(3), dy.size(1), dy.size(2), k, s, pt, pl, stream());
+  return false;
+}
+
 void avgpool_fwd(Tensor x, Tensor y) {
   if (is_f32(x)) {
     CHECK_T(x, torch::kFloat32);
@@ -1587,6 +1637,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("maxpool_bwd_stats", &maxpool_bwd_stats);
+  m.def("bn_maxpool_fwd", &bn_maxpool_fwd);
+  m.def("maxpool_bwd_rb", &maxpool_bwd_rb, py::arg("dy"), py::arg("idx"), py::arg("dx"),
+        py::arg("k"), py::arg("s"), py::arg("pt"), py::arg("pl"), py::arg("bn_x") = py::none(),
+        py::arg("bn_red") = py::none());
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd, py::arg("dy"), py::arg("dx"), py::arg("dadd") = py::none());
   m.def("softmax_xent", &softmax_xent);

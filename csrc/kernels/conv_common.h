@@ -271,13 +271,74 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 // values that must not reach memory or the statistics, so STATS then masks by row validity)
 // AFM (DGRAD with STATS): the ReLU mask of a folded BN (ConvArgs::aff) — a·x + b > 0 of the BN
 // input x the statistics load anyway
+// DGRAD epilogue operands loaded ahead (epi_preload_dgrad): the BN input x of the statistics,
+// the ReLU mask words and the previous dx of a join — issued before the tile's K loop so their
+// latency hides under it (conv_halo.hip conv_rw_kernel)
+template <int RM, int RN>
+struct EpiPre {
+  v2u32 xv[RM][RN];
+  uint32_t mrow[RM][2];
+  v2u32 pv[RM][RN];
+};
+
+// the loads store_tile_bf16<DGRAD, …, ROWS> would issue, into `p` (same addressing)
+template <int RM, int RN, int TN, bool STATS, bool NJ>
+__device__ __forceinline__ void epi_preload_dgrad(const ConvArgs& a, const Tile& T, int wn,
+                                                  int lane, rsrc_t rout, const uint32_t* rbase,
+                                                  EpiPre<RM, RN>& p) {
+  const int c0 = T.bn0 + wn * TN + (lane >> 4) * 4;
+  const bool cols_ok = T.bn0 + wn * TN + TN <= a.Ng;
+  if constexpr (STATS) {
+    const rsrc_t rbx = make_rsrc(a.bn_x, a.out_bytes);
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) {
+        const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+        p.xv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
+            rbx, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+      }
+  }
+  if (a.mask) {
+    const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const uint32_t boff = (rbase[rm] / 2u + (uint32_t)(T.bn0 + wn * TN)) >> 3;
+      const uint32_t o = rbase[rm] != ROW_OOB ? boff : OOB;
+      if constexpr (TN == 64) {
+        const v2u32 m2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, o, 0, 0);
+        p.mrow[rm][0] = m2[0];
+        p.mrow[rm][1] = m2[1];
+      } else {
+        static_assert(TN == 32, "mask slab of 4 or 8 bytes");
+        p.mrow[rm][0] = __builtin_amdgcn_raw_buffer_load_b32(rmask, o, 0, 0);
+        p.mrow[rm][1] = 0;
+      }
+    }
+  }
+  if constexpr (!NJ) {
+    if (a.beta) {
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn) {
+          const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+          p.pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
+              rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+        }
+    }
+  }
+}
+
 template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false,
-          bool NJ = false, bool FRES = false, bool ROWS = false, bool AFM = false>
+          bool NJ = false, bool FRES = false, bool ROWS = false, bool AFM = false, bool PRE = false>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
                                                 float (&s_sum)[RN][4], float (&s_sq)[RN][4],
-                                                const uint32_t* rows_in = nullptr) {
+                                                const uint32_t* rows_in = nullptr,
+                                                const EpiPre<RM, RN>* pre = nullptr) {
+  static_assert(!PRE || (MODE == DGRAD && ROWS && !AFM), "preloaded operands: DGRAD, rows given");
   // Row byte offsets are 32-bit with invalid rows pushed past the buffer (ROW_OOB): a
   // fragment's store offset is then row base + a compile-time constant.  Rows past the GEMM's
   // M hold zeros (their A rows were fetched out of range), so the statistics need no mask.
@@ -325,7 +386,18 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
   // DGRAD BN-backward statistics (STATS): the BN input x at the stored positions — Σg·x with g
   // the stored (masked) dx; the BN backward converts to Σg·x̂ (bn.hip, red_raw)
   v2u32 xv[RM][RN];
-  if constexpr (MODE == DGRAD && STATS) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      mrow[rm][0] = pre->mrow[rm][0];
+      mrow[rm][1] = pre->mrow[rm][1];
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) {
+        if constexpr (STATS) xv[rm][rn] = pre->xv[rm][rn];
+        if constexpr (!NJ) pv[rm][rn] = pre->pv[rm][rn];
+      }
+    }
+  } else if constexpr (MODE == DGRAD && STATS) {
     const rsrc_t rbx = make_rsrc(a.bn_x, no_mem ? 0u : a.out_bytes);
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm)
@@ -352,7 +424,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
       }
     }
   }
-  if constexpr (MODE == DGRAD) {
+  if constexpr (MODE == DGRAD && !PRE) {
     if (join_mask) {
       const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
 #pragma unroll
@@ -371,7 +443,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
       }
     }
   }
-  if constexpr ((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) {
+  if constexpr (((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) && !PRE) {
     if (join_prev) {
       // DGRAD: the previous dx of the output buffer itself; FWD: the residual tensor
       const rsrc_t rprev = MODE == FWD ? make_rsrc(a.res, a.out_bytes) : rout;

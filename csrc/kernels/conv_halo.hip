@@ -817,6 +817,19 @@ __global__ void __launch_bounds__(512, 1) conv_rw_kernel(ConvArgs a, RwGeom g) {
       nxt = tile_at(t0 + i + 1);
       fill(nxt, buf ^ 1);  // last read in tile i − 1 (barrier below)
     }
+    // the output rows of this tile's lanes: (2wm + (rm >> 1), (rm & 1)·16 + l15)
+    uint32_t rows_in[RM];
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+      const int h = cur.h0 + 2 * wm + (rm >> 1), col = (rm & 1) * 16 + l15, w = cur.w0 + col;
+      rows_in[rm] = h < g.Ho && col < g.TW && w < g.Wo
+                        ? (uint32_t)(((cur.n * g.Ho + h) * g.Wo + w) * a.ldc) * 2u
+                        : ROW_OOB;
+    }
+    // input gradient: its epilogue's loads (BN input, mask words, previous dx) go out now and
+    // land under the K loop
+    EpiPre<RM, RN> pre;
+    if constexpr (DEPI) epi_preload_dgrad<RM, RN, TN, STATS, NJ>(a, Tep, wn, lane, rout, rows_in, pre);
     const uint32_t hb = lds0 + (uint32_t)(buf * RW_HB);
     uint32_t ve[3][2], vo[3][2];
 #pragma unroll
@@ -844,17 +857,10 @@ __global__ void __launch_bounds__(512, 1) conv_rw_kernel(ConvArgs a, RwGeom g) {
                                                                 acc[rm][rn], 0, 0, 0);
       hlgkm0();
     });
-    // ---- epilogue: lane rows (2wm + (rm >> 1), (rm & 1)·16 + l15) of the tile ----
-    uint32_t rows_in[RM];
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      const int h = cur.h0 + 2 * wm + (rm >> 1), col = (rm & 1) * 16 + l15, w = cur.w0 + col;
-      rows_in[rm] = h < g.Ho && col < g.TW && w < g.Wo
-                        ? (uint32_t)(((cur.n * g.Ho + h) * g.Wo + w) * a.ldc) * 2u
-                        : ROW_OOB;
-    }
+    // ---- epilogue ----
     store_tile_bf16<DEPI ? DGRAD : FWD, RM, RN, TM, TN, BIAS, STATS, false, false, NJ, false,
-                    true>(a, Tep, acc, wm, wn, lane, rout, 1.f, false, s_sum, s_sq, rows_in);
+                    true, false, DEPI>(a, Tep, acc, wm, wn, lane, rout, 1.f, false, s_sum, s_sq,
+                                       rows_in, &pre);
     // the next tile's halo has landed (only this epilogue's stores may still be in flight) and
     // every wave is done with this tile's buffer
     hwait<E>();

@@ -267,6 +267,13 @@ void maxpool_fwd_launch(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, 
 bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, const bf16_t* bx,
                               const uint8_t* mask, float* red, int N, int H, int W, int C, int Ho,
                               int Wo, int k, int s, int pt, int pl, hipStream_t st);
+// the stem's BN + ReLU + max-pool in one pass (ReLU bit in idx bit 7; C % 8 == 0, else false) and
+// the matching backward gather without statistics (deterministic mode)
+bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_t* idx, int N,
+                           int H, int W, int C, int Ho, int Wo, int k, int s, int pt, int pl,
+                           hipStream_t st);
+void maxpool_bwd_rb_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
+                           int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
 void maxpool_bwd_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
                         int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);
 void avgpool_fwd_launch(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);

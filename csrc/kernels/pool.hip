@@ -68,7 +68,9 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
   }
 }
 
-template <int V, typename T>
+// RB: the index bytes carry the producing BN's ReLU bit in bit 7 (bn_maxpool_fwd_kernel): a window
+// whose maximum was 0 passes no gradient
+template <int V, typename T, bool RB = false>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
                                    T* __restrict__ dx, int N, int H, int W, int C, int Ho,
                                    int Wo, int k, int s, int pt, int pl) {
@@ -104,7 +106,7 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
           for (int j = 0; j < 8; ++j) {
             const uint32_t word = j < 4 ? packed.x : packed.y;
             const int a = (word >> ((j & 3) * 8)) & 0xff;
-            if (a == want) acc[j] += g[j];
+            if (RB ? a == (want | 0x80) : a == want) acc[j] += g[j];
           }
         } else {
           if (idx[o] == want) acc[0] += load1(dy + o);
@@ -126,7 +128,8 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
 // KK / SS: compile-time window and stride (the ResNet stem's 3×3 / 2: constant divisions, unrolled
 // window loops), 0 = runtime k / s; I: uint32_t index math when every element offset fits (64-bit
 // divisions cost ≈4× the 32-bit ones per thread)
-template <int KK, int SS, typename I>
+// RB: ReLU bit in the index bytes (bn_maxpool_fwd_kernel) instead of the BN's bit mask
+template <int KK, int SS, typename I, bool RB = false>
 __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
     const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
     const bf16_t* __restrict__ bx, const uint8_t* __restrict__ mask, float* __restrict__ red, int N,
@@ -164,14 +167,16 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint32_t word = j < 4 ? packed.x : packed.y;
-          if ((int)((word >> ((j & 3) * 8)) & 0xff) == want) acc[j] += g[j];
+          if ((int)((word >> ((j & 3) * 8)) & 0xff) == (RB ? want | 0x80 : want)) acc[j] += g[j];
         }
       }
     }
     const I off = (((I)n * H + h) * W + w) * C + c;
-    const uint32_t mb = mask[off >> 3];
+    if constexpr (!RB) {
+      const uint32_t mb = mask[off >> 3];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = (mb >> j) & 1u ? acc[j] : 0.f;
+      for (int j = 0; j < 8; ++j) acc[j] = (mb >> j) & 1u ? acc[j] : 0.f;
+    }
     const uint4 st = pack8(acc);
     *(uint4*)(dx + off) = st;
     float q[8], xv[8];
@@ -195,6 +200,73 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
     float sum = 0.f;
     for (int r = v; r < NT; r += cv) sum += lds[which][r][j];
     atomicAdd(red + which * C + c, sum);
+  }
+}
+
+// Max-pool of u = relu(x·scale + shift) rounded to bf16 exactly as bn.hip apply_vec stores it — the
+// ResNet stem's training BN + ReLU + 3×3/2 max-pool (/root/reference/core/resnet.py:238-241) in
+// one pass over the conv output: the BN output is never written or re-read.  coef = bn_finalize's
+// fp32 rows (scale, shift, …).  The index byte's bit 7 records u_max > 0 — the BN's ReLU mask at
+// the argmax, the only position the backward routes gradient to (maxpool_bwd*<RB>).
+template <int KK, int SS, typename I>
+__global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ coef, bf16_t* __restrict__ y,
+    uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho, int Wo, int k_, int s_, int pt,
+    int pl) {
+  const int k = KK ? KK : k_, s = SS ? SS : s_;
+  const int cv = C / 8;
+  const I total = (I)N * Ho * Wo * cv;
+  for (I t = blockIdx.x * (I)NT + threadIdx.x; t < total; t += (I)gridDim.x * NT) {
+    const int c = (int)(t % (I)cv) * 8;
+    I p = t / (I)cv;
+    const int wo = (int)(p % (I)Wo);
+    p /= (I)Wo;
+    const int ho = (int)(p % (I)Ho);
+    const int n = (int)(p / (I)Ho);
+    float sc[8], sh[8];
+    {
+      const float4 s0 = *(const float4*)(coef + c), s1 = *(const float4*)(coef + c + 4);
+      const float4 h0 = *(const float4*)(coef + C + c), h1 = *(const float4*)(coef + C + c + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+      sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
+      sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+    }
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      arg[j] = 0;
+    }
+    for (int r = 0; r < k; ++r) {
+      const int hi = ho * s - pt + r;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      for (int q = 0; q < k; ++q) {
+        const int wi = wo * s - pl + q;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        const I off = (((I)n * H + hi) * W + wi) * C + c;
+        float v[8];
+        load8(x + off, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sh[j], 0.f);
+        unpack8(pack8(v), v);  // the bf16 value apply_vec would have stored
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j]) {
+            best[j] = v[j];
+            arg[j] = r * k + q;
+          }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) arg[j] |= best[j] > 0.f ? 0x80 : 0;
+    const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
+    store8(y + o, best);
+    uint2 packed;
+    packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+    *(uint2*)(idx + o) = packed;
   }
 }
 
@@ -304,12 +376,39 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
   const long n = (long)N * H * W * C;
   static const bool spec = getenv("TDL_POOL_SPEC") == nullptr || atoi(getenv("TDL_POOL_SPEC")) != 0;
   const bool small = spec && n < (1L << 31) && (long)N * Ho * Wo * C < (1L << 31);
-  auto kern = maxpool_bwd_stats_kernel<0, 0, long>;
-  if (small) kern = k == 3 && s == 2 ? maxpool_bwd_stats_kernel<3, 2, uint32_t>
-                                     : maxpool_bwd_stats_kernel<0, 0, uint32_t>;
+  // mask == nullptr: the ReLU bit travels in the index bytes (bn_maxpool_fwd_launch)
+  auto kern = mask ? maxpool_bwd_stats_kernel<0, 0, long> : maxpool_bwd_stats_kernel<0, 0, long, true>;
+  if (small) {
+    if (mask)
+      kern = k == 3 && s == 2 ? maxpool_bwd_stats_kernel<3, 2, uint32_t>
+                              : maxpool_bwd_stats_kernel<0, 0, uint32_t>;
+    else
+      kern = k == 3 && s == 2 ? maxpool_bwd_stats_kernel<3, 2, uint32_t, true>
+                              : maxpool_bwd_stats_kernel<0, 0, uint32_t, true>;
+  }
   hipLaunchKernelGGL(kern, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, idx, dx, bx, mask, red, N,
                      H, W, C, Ho, Wo, k, s, pt, pl);
   return true;
+}
+
+bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_t* idx, int N,
+                           int H, int W, int C, int Ho, int Wo, int k, int s, int pt, int pl,
+                           hipStream_t st) {
+  if (C % 8) return false;
+  const long no = (long)N * Ho * Wo * C / 8;
+  if (k == 3 && s == 2 && (long)N * H * W * C < (1L << 31))
+    hipLaunchKernelGGL((bn_maxpool_fwd_kernel<3, 2, uint32_t>), dim3(blocks_for(no)), dim3(NT), 0,
+                       st, x, coef, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  else
+    hipLaunchKernelGGL((bn_maxpool_fwd_kernel<0, 0, long>), dim3(blocks_for(no)), dim3(NT), 0, st,
+                       x, coef, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  return true;
+}
+
+void maxpool_bwd_rb_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
+                           int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
+  hipLaunchKernelGGL((maxpool_bwd_kernel<8, bf16_t, true>), dim3(blocks_for((long)N * H * W * C / 8)),
+                     dim3(NT), 0, st, dy, idx, dx, N, H, W, C, Ho, Wo, k, s, pt, pl);
 }
 
 template <typename T>

@@ -166,6 +166,8 @@ class Conv2d(nn.Module):
     shape; gradients are un-padded on delivery.
     """
 
+    no_decay_params = ("bias",)  # (models/params.FlatParams)
+
     def __init__(self, cin, cout, k, stride=1, padding="sym", dilation=1, bias=False, relu=False,
                  init="he_tf", init_std=None, pad_cin_to=None, pad_cout_to=None):
         super().__init__()
@@ -429,6 +431,8 @@ class BatchNorm(nn.Module):
     convs, :class:`Conv2d` ``pad_cout_to``); γ/β are read zero-padded so those channels stay
     exactly zero, and the moving statistics keep their logical size ``c``."""
 
+    no_decay_params = ("gamma", "beta")  # (models/params.FlatParams)
+
     def __init__(self, c, decay=0.997, eps=1e-5, scale=True, zero_init=False, c_phys=None):
         super().__init__()
         self.c, self.decay, self.eps = c, decay, eps
@@ -641,6 +645,8 @@ class Linear(nn.Module):
 
 class DepthwiseConv2d(nn.Module):
     """Depthwise k×k (depth multiplier 1), weight [R, S, C], optional bias + ReLU."""
+
+    no_decay_params = ("bias",)  # (models/params.FlatParams)
 
     def __init__(self, c, k=3, stride=1, padding="SAME", dilation=1, bias=True, relu=True,
                  init_std=0.33):

@@ -69,7 +69,14 @@ class FlatParams:
         self.lowp = (torch.zeros(self.total, dtype=lowp_dtype, device=self.device)
                      if lowp_dtype is not None else None)
         flags = torch.ones(self.total // ALIGN, dtype=torch.uint8)
-        no_decay = no_decay or (lambda name, p: getattr(p, "_no_decay", False))
+        if no_decay is None:
+            # exempt from weight decay: parameters a module lists in ``no_decay_params`` (BN γ/β,
+            # biases — a class attribute, so it survives copy.deepcopy, which drops attributes
+            # set on a Parameter) or flagged ``_no_decay`` directly
+            exempt = {id(getattr(m, a)) for m in module.modules()
+                      for a in getattr(m, "no_decay_params", ())
+                      if isinstance(getattr(m, a, None), torch.nn.Parameter)}
+            no_decay = lambda name, p: id(p) in exempt or getattr(p, "_no_decay", False)  # noqa: E731
         for name, p, o in zip(self.names, self.params, self.offsets):
             n = p.numel()
             with torch.no_grad():

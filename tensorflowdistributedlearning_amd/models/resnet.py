@@ -16,7 +16,9 @@ import torch.nn as nn
 
 from ..ops import gradjoin
 
-from .layers import ConvBN, MaxPool, GlobalAvgPool, Linear, RowPackedConv2d
+from .layers import ConvBN, MaxPool, GlobalAvgPool, Linear, RowPackedConv2d, resolve_padding
+from ..ops.pool import bn_relu_max_pool, bn_relu_max_pool_ok
+
 
 _CFG = {
     18: ("basic", (2, 2, 2, 2)),
@@ -119,8 +121,15 @@ class ResNet(nn.Module):
     def forward_features(self, x):
         if x.shape[-1] != self.stem.conv._cin_store:
             x = nn.functional.pad(x, (0, self.stem.conv._cin_store - x.shape[-1]))
-        x = self.stem(x)
-        x = self.pool(x)
+        if self.training and self.stem.relu and bn_relu_max_pool_ok(x, self.stem.bn):
+            # training: the stem BN + ReLU runs inside the max-pool (ops/pool.bn_relu_max_pool)
+            z, stats = self.stem.conv(x, want_stats=True)
+            pad = resolve_padding(self.pool.padding, z.shape[1], z.shape[2], self.pool.k,
+                                  self.pool.k, (self.pool.stride, self.pool.stride), (1, 1))
+            x = bn_relu_max_pool(z, stats, self.stem.bn, self.pool.k, self.pool.stride, pad)
+        else:
+            x = self.stem(x)
+            x = self.pool(x)
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

@@ -86,6 +86,82 @@ def max_pool2d(x, k, s, pad):
     return _MaxPoolFn.apply(x, k, s, tuple(pad))
 
 
+# the ResNet stem's BN + ReLU folded into its max-pool (bn_relu_max_pool); 0: apply pass + pool
+STEM_FUSE = os.environ.get("TDL_STEM_POOL_FUSE", "1") == "1"
+
+
+class _BNReluMaxPoolFn(torch.autograd.Function):
+    """max_pool(relu(BN(z))) of a training BN in one pass over z (pool.hip bn_maxpool_fwd_kernel):
+    the BN output — the largest activation of the network, 112×112×64 per ResNet image — is never
+    written or read back.  The index bytes carry the ReLU bit of each window maximum, so the
+    backward gather routes gradient only to positions the BN's ReLU passed, and accumulates the
+    BN-backward sums (Σg, Σg·z) on the way (outside deterministic mode); the BN backward apply then
+    produces dz.  Reference: the stem's conv + batch_norm(relu) + max_pool2d(3, 2, 'SAME')
+    (/root/reference/core/resnet.py:238-241)."""
+
+    @staticmethod
+    def forward(ctx, z, stats, gamma, beta, bn, k, s, pad):
+        from .bn import bn_stats, bn_finalize, _phys_params
+        N, H, W, C = z.shape
+        count = z.numel() // C
+        if stats is None or stats.numel() == 0:
+            stats = bn_stats(z)
+        gp, bp = _phys_params(bn, gamma, beta)
+        coef = bn_finalize(stats, count, gp, bp, bn.running_mean, bn.running_var, bn.decay,
+                           bn.eps, True)
+        Ho, Wo = _out(H, k, s, pad[0], pad[1]), _out(W, k, s, pad[2], pad[3])
+        y = torch.empty((N, Ho, Wo, C), device=z.device, dtype=z.dtype)
+        idx = torch.empty((N, Ho, Wo, C), device=z.device, dtype=torch.uint8)
+        if not ext().bn_maxpool_fwd(z, coef, y, idx, k, s, pad[0], pad[2]):
+            raise RuntimeError("bn_relu_max_pool: channel count not a multiple of 8")
+        ctx.k, ctx.s, ctx.pad, ctx.bn, ctx.count = k, s, pad, bn, count
+        ctx.save_for_backward(z, idx, coef, gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .bn import (bn_bwd_reduce, bn_bwd_apply, bn_red_xhat, _phys_params,
+                         _grad_target_phys)
+        from .common import deliver_grad
+        z, idx, coef, gamma, beta = ctx.saved_tensors
+        dy = dy.contiguous()
+        C, c = z.shape[-1], beta.numel()
+        g = torch.empty_like(z)
+        red = workspace.zeros((2, C), dy.device)
+        fused = ext().maxpool_bwd_rb(dy, idx, g, ctx.k, ctx.s, ctx.pad[0], ctx.pad[2], z, red)
+        if not fused:
+            red = bn_bwd_reduce(g, None, z, coef, 0)  # (Σg, Σg·ẑ), deterministic mode
+        want_g = gamma is not None and gamma.requires_grad
+        want_b = beta.requires_grad
+        gt, gfresh = _grad_target_phys(gamma, C) if want_g else (None, False)
+        bt, bfresh = _grad_target_phys(beta, C) if want_b else (None, False)
+        direct_g, direct_b = gt is not None and gfresh, bt is not None and bfresh
+        gp, _ = _phys_params(ctx.bn, gamma, beta)
+        dz, _ = bn_bwd_apply(g, None, z, coef, red, gp, ctx.count, 0, False,
+                             gt if direct_g else None, bt if direct_b else None, red_raw=fused)
+        if fused and want_g and not direct_g:
+            red = bn_red_xhat(red, coef)
+        if want_g:
+            deliver_grad(gamma, None if direct_g else red[1][:c], written=direct_g)
+        if want_b:
+            deliver_grad(beta, None if direct_b else red[0][:c], written=direct_b)
+        return dz, None, None, None, None, None, None, None
+
+
+def bn_relu_max_pool_ok(z, bn):
+    """Can max_pool(relu(BN(z))) of this training BN run as one fused pass?"""
+    from .common import fused_gpu
+    return (STEM_FUSE and fused_gpu(z) and z.dtype == torch.bfloat16 and z.shape[-1] % 8 == 0
+            and export_impl() is None and torch.is_grad_enabled()
+            and not getattr(bn, "emit_fp8", False))
+
+
+def bn_relu_max_pool(z, stats, bn, k, s, pad):
+    """max_pool2d(relu(BN(z)), k, s, pad) for a training-mode ``bn`` (models.layers.BatchNorm)
+    with the producer's BN sums ``stats`` — see :class:`_BNReluMaxPoolFn`."""
+    return _BNReluMaxPoolFn.apply(z, stats, bn.gamma, bn.beta, bn, k, s, tuple(pad))
+
+
 class _GAPFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, keepdims, join=None):

@@ -169,3 +169,17 @@ def test_exponential_decay():
     assert abs(exponential_decay(1e-3, 10000) - 5e-4) < 1e-15
     assert abs(exponential_decay(1e-3, 5000) - 1e-3 * 0.5 ** 0.5) < 1e-15
     assert exponential_decay(1e-3, 15000, staircase=True) == 5e-4
+
+
+def test_weight_decay_exemptions_survive_deepcopy():
+    """BN γ/β and biases are exempt from weight decay (models/params.FlatParams).  The exemption is
+    a module-level declaration (``no_decay_params``): copy.deepcopy drops attributes set on a
+    Parameter, and a deep-copied model used to train with decay on its BN parameters."""
+    import copy
+    from tensorflowdistributedlearning_amd import models
+    from tensorflowdistributedlearning_amd.models.params import FlatParams
+    m = models.resnet18(num_classes=10)
+    a = FlatParams(m, "cpu", lowp_dtype=None).decay_flags
+    b = FlatParams(copy.deepcopy(models.resnet18(num_classes=10)), "cpu", lowp_dtype=None).decay_flags
+    assert torch.equal(a, b)
+    assert 0 < int(a.sum()) < a.numel()  # conv weights decay, BN parameters do not

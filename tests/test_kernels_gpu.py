@@ -1416,3 +1416,42 @@ def test_conv_dgrad_as_forward_strided(gpu, shape, epi):
         gf, xf = got.float().reshape(-1, Cin), x.float().reshape(-1, Cin)
         want = torch.stack([gf.sum(0), (gf * xf).sum(0)])
         assert rel_err(red1, want) < 1e-4
+
+
+@pytest.mark.parametrize("det", [0, 1])
+@pytest.mark.parametrize("H", [30, 112])
+def test_bn_relu_max_pool_matches_unfused(gpu, det, H):
+    """The stem's BN + ReLU folded into the max-pool (ops/pool.bn_relu_max_pool, pool.hip
+    bn_maxpool_fwd_kernel) against the unfused BN apply + max-pool: the pooled output bit for bit
+    (same bf16 rounding, same argmax ties), the input gradient and dγ, dβ to fp32 rounding — with
+    negative γ (channels whose window maximum is the minimum of z) and in deterministic mode (no
+    fused sums: the BN reduces itself)."""
+    import copy
+    from tensorflowdistributedlearning_amd.models.layers import BatchNorm, resolve_padding
+    torch.manual_seed(H + det)
+    bn_a = BatchNorm(64).to(gpu)
+    with torch.no_grad():
+        bn_a.gamma.uniform_(-1.0, 2.0)
+        bn_a.beta.normal_(0, 0.5)
+    bn_b = copy.deepcopy(bn_a)
+    z0 = (torch.randn(4, H, H, 64) * 1.5 + 0.3).bfloat16().to(gpu)
+    pad = resolve_padding("sym", H, H, 3, 3, (2, 2), (1, 1))
+    Ho = (H + pad[0] + pad[1] - 3) // 2 + 1
+    dy = torch.randn(4, Ho, Ho, 64).bfloat16().to(gpu)
+    ext().det_set(det)
+    try:
+        za = z0.clone().requires_grad_(True)
+        ref = P.max_pool2d(B.batch_norm_act(za, bn_a, relu=True), 3, 2, pad)
+        ref.backward(dy)
+        zb = z0.clone().requires_grad_(True)
+        assert P.bn_relu_max_pool_ok(zb, bn_b)
+        y = P.bn_relu_max_pool(zb, None, bn_b, 3, 2, pad)
+        y.backward(dy)
+        torch.cuda.synchronize()
+    finally:
+        ext().det_set(-1)
+    assert torch.equal(y, ref)
+    assert rel_err(zb.grad, za.grad) < 1e-2
+    assert rel_err(bn_b.gamma.grad, bn_a.gamma.grad) < 1e-3
+    assert rel_err(bn_b.beta.grad, bn_a.beta.grad) < 1e-3
+    assert torch.allclose(bn_b.running_mean, bn_a.running_mean)

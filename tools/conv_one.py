@@ -23,6 +23,8 @@ def main():
                                                     "dgrad_reduce"])
     ap.add_argument("--shape", default="256,14,512,512,3,2,1")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--flip", action="store_true",
+                    help="dgrad ops: pass the flipped filter (the dgrad-as-forward routes)")
     a = ap.parse_args()
     N, H, Cin, Cout, k, s, p = [int(v) for v in a.shape.split(",")]
     dev = torch.device("cuda")
@@ -32,6 +34,10 @@ def main():
     Ho, Wo = g.out_hw(H, H, k, k)
     dy = torch.randn(N, Ho, Wo, Cout, device=dev, dtype=torch.bfloat16)
     ext().conv_set_glds_mode(a.mode)
+    wf = None
+    if a.flip and s == 1:
+        wf = torch.empty(Cin, k, k, Cout, device=dev, dtype=torch.bfloat16)
+        ext().conv_flip_weight(w, wf)
     if a.op in ("dgrad_bnstat", "dgrad_reduce"):
         # BN-backward statistics: fused into the dgrad epilogue vs dgrad + the BN reduce pass
         # (x plays the BN input; its ReLU bit mask and coefficients from a real BN forward)
@@ -44,7 +50,7 @@ def main():
         yb = B.bn_apply(x, coef, None, True, mask=mask)
         for _ in range(a.iters):
             if a.op == "dgrad_bnstat":
-                C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask)
+                C.conv_dgrad_bnstat(dy, w, x.shape, g, x, mask=mask, w_flip=wf)
             else:
                 B.bn_bwd_reduce(C.conv_dgrad(dy, w, x.shape, g), yb, x, coef, 2)
         torch.cuda.synchronize()
@@ -54,7 +60,7 @@ def main():
         if a.op == "fwd":
             C.conv_fwd(x, w, g)
         elif a.op == "dgrad":
-            C.conv_dgrad(dy, w, x.shape, g)
+            C.conv_dgrad(dy, w, x.shape, g, w_flip=wf)
         else:
             C.conv_wgrad(dy, x, tuple(w.shape), g)
     torch.cuda.synchronize()
