@@ -121,8 +121,9 @@ class ResNet(nn.Module):
     def forward_features(self, x):
         if x.shape[-1] != self.stem.conv._cin_store:
             x = nn.functional.pad(x, (0, self.stem.conv._cin_store - x.shape[-1]))
-        if self.training and self.stem.relu and bn_relu_max_pool_ok(x, self.stem.bn):
-            # training: the stem BN + ReLU runs inside the max-pool (ops/pool.bn_relu_max_pool)
+        if (self.training and self.stem.bn.training and self.stem.relu
+                and bn_relu_max_pool_ok(x, self.stem.bn)):
+            # training BN: the stem BN + ReLU runs inside the max-pool (ops/pool.bn_relu_max_pool)
             z, stats = self.stem.conv(x, want_stats=True)
             pad = resolve_padding(self.pool.padding, z.shape[1], z.shape[2], self.pool.k,
                                   self.pool.k, (self.pool.stride, self.pool.stride), (1, 1))

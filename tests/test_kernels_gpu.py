@@ -1440,12 +1440,13 @@ def test_bn_relu_max_pool_matches_unfused(gpu, det, H):
     dy = torch.randn(4, Ho, Ho, 64).bfloat16().to(gpu)
     ext().det_set(det)
     try:
+        st = B.bn_stats(z0)  # one set of batch sums for both (fp32-atomic order otherwise)
         za = z0.clone().requires_grad_(True)
-        ref = P.max_pool2d(B.batch_norm_act(za, bn_a, relu=True), 3, 2, pad)
+        ref = P.max_pool2d(B.batch_norm_act(za, bn_a, stats=st.clone(), relu=True), 3, 2, pad)
         ref.backward(dy)
         zb = z0.clone().requires_grad_(True)
         assert P.bn_relu_max_pool_ok(zb, bn_b)
-        y = P.bn_relu_max_pool(zb, None, bn_b, 3, 2, pad)
+        y = P.bn_relu_max_pool(zb, st.clone(), bn_b, 3, 2, pad)
         y.backward(dy)
         torch.cuda.synchronize()
     finally:
