@@ -468,7 +468,9 @@ struct HaloWg {
   int rb_per_split;      // pixel tiles (row blocks) per split
 };
 
-template <int BM, int HL>
+// BURST: the x fragments of all 9 taps read up front, MFMAs in two bursts (0: one LDS wait per tap,
+// the round-5 loop — A/B, TDL_HALO_WG_BURST=0)
+template <int BM, int HL, bool BURST = true>
 __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, HaloGeom g, HaloWg q) {
   constexpr int NW = 8, NTAP = 9, RM = BM / 32;
   constexpr int PX = 128;                      // pixels per tile (k-rows of the dy image)
@@ -595,6 +597,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, Hal
       prep(i);
       const uint32_t As = smem_lds + (uint32_t)(b * STAGE);
       const uint32_t Hs = As + (uint32_t)A_BYTES;
+      if constexpr (!BURST) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         bf16x8 af[RM];
@@ -621,6 +624,59 @@ __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, Hal
           hlgkm0();
           if (t + 1 < NTAP) xf = xn;
         }
+      }
+      } else {
+      // per 32-pixel k-block: the dy fragments (RM) and the x fragments of all 9 taps are read up
+      // front and the 9·RM MFMAs run in two bursts (taps 0–4, 5–8) with the reads of the next
+      // block's dy and first 5 taps under the second — one LDS wait per burst, not per tap
+      auto xaddr = [&](uint32_t s0) {
+        return Hs + (s0 << 7) + ((cq ^ ((s0 >> 1) & 7u)) << 4) + cbyte;
+      };
+      bf16x8 af[2][RM], xf[NTAP];
+      auto read_a = [&](int kb, bf16x8 (&a)[RM]) {
+#pragma unroll
+        for (int f = 0; f < RM; ++f) {
+          const uint32_t ad = As + aoff[f] + (uint32_t)(kb * 32 * BM * 2);
+          a[f] = hread_tr_pair<0>(ad, ad + 8 * BM);
+        }
+      };
+      auto read_x = [&](int kb, int t0, int t1) {
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t)
+          if (t >= t0 && t < t1)
+            xf[t] = hread_tr_pair<0>(xaddr(sl[kb][0] + (uint32_t)g.tap_d[t]),
+                                     xaddr(sl[kb][1] + (uint32_t)g.tap_d[t]));
+      };
+      auto mfma_taps = [&](const bf16x8 (&a)[RM], int t0, int t1) {
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t)
+          if (t >= t0 && t < t1)
+#pragma unroll
+            for (int f = 0; f < RM; ++f)
+              acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[t], a[f], acc[f][t], 0, 0, 0);
+      };
+      // (BM = 128: 36 accumulator fragments — the next block's dy is read only once this
+      // block's MFMAs are issued, a second dy buffer would spill)
+      constexpr bool DBA = RM <= 2;
+      read_a(0, af[0]);
+      read_x(0, 0, 5);
+      hlgkm0();
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const int ab = DBA ? (kb & 1) : 0;
+        read_x(kb, 5, NTAP);
+        mfma_taps(af[ab], 0, 5);
+        hlgkm0();
+        if (kb + 1 < 4) {
+          if constexpr (DBA) read_a(kb + 1, af[(kb + 1) & 1]);
+          read_x(kb + 1, 0, 5);
+        }
+        mfma_taps(af[ab], 5, NTAP);
+        if constexpr (!DBA) {
+          if (kb + 1 < 4) read_a(kb + 1, af[0]);
+        }
+        hlgkm0();
+      }
       }
       hbarrier();  // every wave is done with stage b before step i+1 refills it
     }
@@ -1019,7 +1075,8 @@ bool halo_common(const ConvArgs& a, HaloGeom& g, int R, int S, const int* oy, co
 
 template <int BM>
 void launch_hw(const ConvArgs& a, const HaloGeom& g, const HaloWg& q, hipStream_t st) {
-  auto k = conv_halo_wgrad_kernel<BM, 4>;
+  static const bool burst = henv("TDL_HALO_WG_BURST", 1) != 0;
+  auto k = burst ? conv_halo_wgrad_kernel<BM, 4, true> : conv_halo_wgrad_kernel<BM, 4, false>;
   constexpr int lds = 2 * (128 * BM * 2 + 4 * 8 * 1024);
   static_assert(lds <= 160 * 1024, "LDS budget");
   static bool attr = false;

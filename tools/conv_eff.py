@@ -75,6 +75,9 @@ def main():
             impl, mode = "pc", 0
         elif "conv_halo_wgrad_kernel<" in name:
             impl, mode = "halo", 2
+        elif "conv_rw_kernel<" in name:  # resident-filter 3x3 64->64 (first flag: DGRAD epilogue)
+            impl = "rw"
+            mode = 1 if re.search(r"conv_rw_kernel<\s*true", name) else 0
         # dgrad as the forward conv of dy (DEPI: the dgrad epilogue on a forward kernel)
         tp = re.search(r"conv_(glds|halo|pc)_kernel<([^>]*)>", name)
         if tp and mode == 0:
