@@ -12,3 +12,5 @@ Layout
   model.py      ``Model`` — the reference's entry point (k-fold train / eval / export / predict)
 """
 __version__ = "0.1.0"
+
+from . import experimental  # noqa: E402,F401  (TDL_EXPERIMENTAL knobs, before any module reads them)

@@ -21,7 +21,7 @@ w.r.t. the unfolded step: same fma, same rounding, same mask.  Anything the kern
 (CPU, fp32, fp8 layers, channel-padded or row-packed convs, a bias) materialises the BN the
 ordinary way (:meth:`DeferredBNAct.materialize`).
 
-Off by default (``TDL_BN_CONV_FOLD=1`` turns it on): measured on MI355X it loses.  The transform
+Off by default (experimental: ``TDL_EXPERIMENTAL=bnconv`` turns it on): measured on MI355X it loses.  The transform
 runs once per A element per filter tap and per output-column tile (9× for a 3×3 conv, Cout/128×
 for a 1×1), and the producer waves' VALU does not overlap the consumers' MFMA issue on the same
 SIMD — every transformed 8-channel chunk costs its ≈24 instructions of SIMD time.  ResNet-50 b1024
@@ -44,7 +44,7 @@ from .bn import (bn_stats, bn_finalize, bn_apply, bn_bwd_reduce, bn_bwd_apply, b
                  _phys_params, _grad_target_phys)
 from .conv import ConvGeom, conv_fwd, conv_dgrad, conv_wgrad
 
-ENABLED = os.environ.get("TDL_BN_CONV_FOLD", "0") == "1"
+ENABLED = os.environ.get("TDL_EXP_BNCONV", "0") == "1"  # experimental (TDL_EXPERIMENTAL=bnconv)
 
 
 class DeferredBNAct:

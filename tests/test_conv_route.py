@@ -54,7 +54,7 @@ RESNET50 = [
     ((56, 256, 64, 1, 1), "fwd.glds.1x1n64", "dgrad.asfwd.glds", "wgrad.gemm"),
     ((28, 128, 128, 3, 2), "fwd.glds.wide", "dgrad.glds.stats", "wgrad.gemm"),
     ((28, 128, 128, 3, 1), "fwd.glds.wide", "dgrad.asfwd.glds", "wgrad.halo.wide3x3"),
-    ((14, 256, 256, 3, 1), "fwd.pc.wide3x3", "dgrad.asfwd.glds", "wgrad.gemm"),
+    ((14, 256, 256, 3, 1), "fwd.pc.wide3x3", "dgrad.asfwd.glds", "wgrad.halo.wide3x3"),
     ((14, 1024, 256, 1, 1), "fwd.glds.wide", "dgrad.asfwd.glds", "wgrad.glds.1x1"),
     ((7, 512, 512, 3, 1), "fwd.pc.wide3x3", "dgrad.asfwd.glds", "wgrad.gemm"),
     ((7, 1024, 2048, 1, 2), "fwd.glds.wide", "dgrad.glds.stats", "wgrad.glds.1x1"),
