@@ -937,7 +937,12 @@ bool maxpool_bwd_stats(Tensor dy, Tensor idx, Tensor dx, int64_t k, int64_t s, i
 // y = maxpool(relu(x·coef[0] + coef[1])) with the ReLU bit of each window maximum in idx bit 7;
 // false: not eligible (C % 8), nothing launched
 bool bn_maxpool_fwd(Tensor x, Tensor coef, Tensor y, Tensor idx, int64_t k, int64_t s, int64_t pt,
-                    int64_t pl) {
+                    int64_t pl, c10::optional<Tensor> zarg) {
+  const bool za = zarg.has_value() && zarg->defined();
+  if (za) {
+    CHECK_T((*zarg), torch::kBFloat16);
+    TORCH_CHECK(zarg->sizes() == y.sizes() && zarg->is_contiguous(), "bn_maxpool_fwd: zarg like y");
+  }
   CHECK_T(x, torch::kBFloat16);
   CHECK_T(y, torch::kBFloat16);
   CHECK_T(idx, torch::kUInt8);
@@ -949,8 +954,45 @@ bool bn_maxpool_fwd(Tensor x, Tensor coef, Tensor y, Tensor idx, int64_t k, int6
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && idx.is_contiguous() && coef.is_contiguous(),
               "bn_maxpool_fwd: contiguous operands");
   return bn_maxpool_fwd_launch(BF(x), coef.data_ptr<float>(), BFW(y), idx.data_ptr<uint8_t>(),
-                               x.size(0), x.size(1), x.size(2), x.size(3), y.size(1), y.size(2), k,
-                               s, pt, pl, stream());
+                               za ? BFW((*zarg)) : nullptr, x.size(0), x.size(1), x.size(2),
+                               x.size(3), y.size(1), y.size(2), k, s, pt, pl, stream());
+}
+
+// fused backward of bn_maxpool_fwd(zarg=…): dx of the BN input from the pool's dy in two passes
+// (pool.hip maxpool_bn_sums_kernel + maxpool_bn_apply_kernel); red [2, C] zeroed by the caller
+// receives (Σg, Σg·x); dgamma / dbeta [C] fp32 (optional) receive dγ, dβ.  False (nothing
+// launched) in deterministic mode (the sums use fp32 atomics) or when C does not fit
+bool maxpool_bn_bwd(Tensor dy, Tensor idx, Tensor zarg, Tensor x, Tensor coef, Tensor red,
+                    c10::optional<Tensor> gamma, Tensor dx, c10::optional<Tensor> dgamma,
+                    c10::optional<Tensor> dbeta, double count, int64_t k, int64_t s, int64_t pt,
+                    int64_t pl) {
+  if (deterministic()) return false;
+  CHECK_T(dy, torch::kBFloat16);
+  CHECK_T(zarg, torch::kBFloat16);
+  CHECK_T(x, torch::kBFloat16);
+  CHECK_T(dx, torch::kBFloat16);
+  CHECK_T(idx, torch::kUInt8);
+  CHECK_T(coef, torch::kFloat32);
+  CHECK_T(red, torch::kFloat32);
+  const int64_t C = x.size(3);
+  TORCH_CHECK(dy.dim() == 4 && x.dim() == 4 && dx.sizes() == x.sizes() && zarg.sizes() == dy.sizes() &&
+                  idx.numel() == dy.numel() && dy.size(0) == x.size(0) && dy.size(3) == C &&
+                  coef.numel() >= 4 * C && red.numel() == 2 * C,
+              "maxpool_bn_bwd: dy / zarg / idx [N,Ho,Wo,C], x / dx [N,H,W,C], coef [4, C], red [2, C]");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dx.is_contiguous() && zarg.is_contiguous() &&
+                  idx.is_contiguous() && coef.is_contiguous() && red.is_contiguous(),
+              "maxpool_bn_bwd: contiguous operands");
+  auto f32opt = [&](const c10::optional<Tensor>& t) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    CHECK_T((*t), torch::kFloat32);
+    TORCH_CHECK(t->numel() >= C && t->is_contiguous(), "maxpool_bn_bwd: per-channel fp32 [C]");
+    return t->data_ptr<float>();
+  };
+  return maxpool_bn_bwd_launch(BF(dy), idx.data_ptr<uint8_t>(), BF(zarg), BF(x),
+                               coef.data_ptr<float>(), red.data_ptr<float>(), f32opt(gamma),
+                               BFW(dx), f32opt(dgamma), f32opt(dbeta), x.size(0), x.size(1),
+                               x.size(2), C, dy.size(1), dy.size(2), k, s, pt, pl,
+                               (float)(1.0 / count), stream());
 }
 
 // backward of bn_maxpool_fwd: dx = the gathered dy where the window maximum was > 0 (idx bit 7);
@@ -1637,7 +1679,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("maxpool_bwd_stats", &maxpool_bwd_stats);
-  m.def("bn_maxpool_fwd", &bn_maxpool_fwd);
+  m.def("bn_maxpool_fwd", &bn_maxpool_fwd, py::arg("x"), py::arg("coef"), py::arg("y"),
+        py::arg("idx"), py::arg("k"), py::arg("s"), py::arg("pt"), py::arg("pl"),
+        py::arg("zarg") = py::none());
+  m.def("maxpool_bn_bwd", &maxpool_bn_bwd);
   m.def("maxpool_bwd_rb", &maxpool_bwd_rb, py::arg("dy"), py::arg("idx"), py::arg("dx"),
         py::arg("k"), py::arg("s"), py::arg("pt"), py::arg("pl"), py::arg("bn_x") = py::none(),
         py::arg("bn_red") = py::none());

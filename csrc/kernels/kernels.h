@@ -269,8 +269,15 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
                               int Wo, int k, int s, int pt, int pl, hipStream_t st);
 // the stem's BN + ReLU + max-pool in one pass (ReLU bit in idx bit 7; C % 8 == 0, else false) and
 // the matching backward gather without statistics (deterministic mode)
-bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_t* idx, int N,
-                           int H, int W, int C, int Ho, int Wo, int k, int s, int pt, int pl,
+bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_t* idx,
+                           bf16_t* zarg, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                           int pt, int pl, hipStream_t st);
+// the fused backward of bn_maxpool_fwd (with zarg): BN sums per pool output, then the gather +
+// BN backward apply per input pixel; red [2, C] zeroed by the caller; false: C does not fit
+bool maxpool_bn_bwd_launch(const bf16_t* dy, const uint8_t* idx, const bf16_t* zarg,
+                           const bf16_t* x, const float* coef, float* red, const float* gamma,
+                           bf16_t* dx, float* dgamma, float* dbeta, int N, int H, int W, int C,
+                           int Ho, int Wo, int k, int s, int pt, int pl, float inv_count,
                            hipStream_t st);
 void maxpool_bwd_rb_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W,
                            int C, int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st);

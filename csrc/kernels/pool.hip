@@ -211,8 +211,10 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
 template <int KK, int SS, typename I>
 __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ coef, bf16_t* __restrict__ y,
-    uint8_t* __restrict__ idx, int N, int H, int W, int C, int Ho, int Wo, int k_, int s_, int pt,
-    int pl) {
+    uint8_t* __restrict__ idx, bf16_t* __restrict__ zarg, int N, int H, int W, int C, int Ho,
+    int Wo, int k_, int s_, int pt, int pl) {
+  // zarg (optional): the BN input x at each window's argmax — the fused backward's BN sums
+  // (maxpool_bn_sums_kernel) read it instead of gathering x
   const int k = KK ? KK : k_, s = SS ? SS : s_;
   const int cv = C / 8;
   const I total = (I)N * Ho * Wo * cv;
@@ -232,12 +234,13 @@ __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
       sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
       sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
     }
-    float best[8];
+    float best[8], zbest[8];
     int arg[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       best[j] = -INFINITY;
       arg[j] = 0;
+      zbest[j] = 0.f;
     }
     for (int r = 0; r < k; ++r) {
       const int hi = ho * s - pt + r;
@@ -246,16 +249,17 @@ __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
         const int wi = wo * s - pl + q;
         if ((unsigned)wi >= (unsigned)W) continue;
         const I off = (((I)n * H + hi) * W + wi) * C + c;
-        float v[8];
-        load8(x + off, v);
+        float v[8], xr[8];
+        load8(x + off, xr);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sh[j], 0.f);
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(xr[j] * sc[j] + sh[j], 0.f);
         unpack8(pack8(v), v);  // the bf16 value apply_vec would have stored
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (v[j] > best[j]) {
             best[j] = v[j];
             arg[j] = r * k + q;
+            zbest[j] = xr[j];
           }
       }
     }
@@ -263,10 +267,128 @@ __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
     for (int j = 0; j < 8; ++j) arg[j] |= best[j] > 0.f ? 0x80 : 0;
     const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
     store8(y + o, best);
+    if (zarg) store8(zarg + o, zbest);  // (bf16 in, bf16 out: exact)
     uint2 packed;
     packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
     packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
     *(uint2*)(idx + o) = packed;
+  }
+}
+
+// Fused backward of bn_maxpool_fwd (max-pool backward + the BN backward in two passes instead of
+// a gather pass that writes g plus a BN backward-apply pass that reads it back):
+//  1. maxpool_bn_sums_kernel — per pool OUTPUT: Σg = Σ dy·[ReLU bit] and Σg·x = Σ dy·[bit]·x_argmax
+//     (linear in the windows' contributions, x_argmax saved by the forward as zarg): reads dy, idx
+//     and zarg, a quarter of the input's size each;
+//  2. maxpool_bn_apply_kernel — per pool INPUT: g = the gathered dy (rounded to bf16 as the
+//     unfused gather stores it), dx = A·g + B·x + C with the BN-backward coefficients (bn.hip
+//     bwd_apply_vec_kernel's formula); block 0 writes dγ, dβ.
+// NT % (C / 8) == 0: a thread's channel vector is fixed over the grid-stride loop.
+__global__ void __launch_bounds__(NT) maxpool_bn_sums_kernel(
+    const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx,
+    const bf16_t* __restrict__ zarg, float* __restrict__ red, long nvec, int C) {
+  __shared__ float lds[2][NT][9];
+  const int cv = C / 8;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < nvec; t += (long)gridDim.x * NT) {
+    float g[8], z[8];
+    unpack8(((const uint4*)dy)[t], g);
+    unpack8(((const uint4*)zarg)[t], z);
+    const uint2 packed = ((const uint2*)idx)[t];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t word = j < 4 ? packed.x : packed.y;
+      const float a = (word >> ((j & 3) * 8)) & 0x80u ? g[j] : 0.f;
+      s0[j] += a;
+      s1[j] = fmaf(a, z[j], s1[j]);
+    }
+  }
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lds[0][tid][j] = s0[j];
+    lds[1][tid][j] = s1[j];
+  }
+  __syncthreads();
+  for (int o = tid; o < 2 * C; o += NT) {
+    const int which = o / C, c = o - which * C, v = c >> 3, j = c & 7;
+    float sum = 0.f;
+    for (int r = v; r < NT; r += cv) sum += lds[which][r][j];
+    atomicAdd(red + which * C + c, sum);
+  }
+  (void)cv;
+}
+
+template <int KK, int SS, typename I>
+__global__ void __launch_bounds__(NT) maxpool_bn_apply_kernel(
+    const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ x,
+    const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
+    bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int N, int H,
+    int W, int C, int Ho, int Wo, int k_, int s_, int pt, int pl, float inv_count) {
+  const int k = KK ? KK : k_, s = SS ? SS : s_;
+  const int cv = C / 8;
+  if (blockIdx.x == 0) {  // (red holds the raw Σg·x: Σg·x̂ = invstd·(Σg·x − mean·Σg))
+    for (int c = threadIdx.x; c < C; c += NT) {
+      if (dgamma) dgamma[c] = coef[3 * C + c] * (red[C + c] - coef[2 * C + c] * red[c]);
+      if (dbeta) dbeta[c] = red[c];
+    }
+  }
+  const I total = (I)N * H * W * cv;
+  I t = blockIdx.x * (I)NT + threadIdx.x;
+  float A[8], Bc[8], Cc[8];
+  {
+    const int c = (int)(t % (I)cv) * 8;  // fixed per thread: the grid stride is a multiple of cv
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float mean = coef[2 * C + c + j], inv = coef[3 * C + c + j];
+      const float s0 = red[c + j], s1 = inv * (red[C + c + j] - mean * s0);
+      const float a = (gamma ? gamma[c + j] : 1.f) * inv;
+      const float b = -a * inv * s1 * inv_count;
+      A[j] = a;
+      Bc[j] = b;
+      Cc[j] = -a * s0 * inv_count - b * mean;
+    }
+  }
+  for (; t < total; t += (I)gridDim.x * NT) {
+    const int c = (int)(t % (I)cv) * 8;
+    I p = t / (I)cv;
+    const int w = (int)(p % (I)W);
+    p /= (I)W;
+    const int h = (int)(p % (I)H);
+    const int n = (int)(p / (I)H);
+    const I off = (((I)n * H + h) * W + w) * C + c;
+    const uint4 xv = *(const uint4*)(x + off);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    const int hh = h + pt, ww = w + pl;
+    const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
+    const int ho_hi = min(Ho - 1, hh / s);
+    const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
+    const int wo_hi = min(Wo - 1, ww / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int r = hh - ho * s;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int want = (r * k + (ww - wo * s)) | 0x80;
+        const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
+        float g[8];
+        unpack8(*(const uint4*)(dy + o), g);
+        const uint2 packed = *(const uint2*)(idx + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t word = j < 4 ? packed.x : packed.y;
+          if ((int)((word >> ((j & 3) * 8)) & 0xff) == want) acc[j] += g[j];
+        }
+      }
+    }
+    float gq[8], vx[8], o[8];
+    unpack8(pack8(acc), gq);  // g as the unfused gather stores it
+    unpack8(xv, vx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = A[j] * gq[j] + Bc[j] * vx[j] + Cc[j];
+    *(uint4*)(dx + off) = pack8(o);
   }
 }
 
@@ -391,17 +513,38 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
   return true;
 }
 
-bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_t* idx, int N,
-                           int H, int W, int C, int Ho, int Wo, int k, int s, int pt, int pl,
-                           hipStream_t st) {
+bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_t* idx,
+                           bf16_t* zarg, int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                           int pt, int pl, hipStream_t st) {
   if (C % 8) return false;
   const long no = (long)N * Ho * Wo * C / 8;
   if (k == 3 && s == 2 && (long)N * H * W * C < (1L << 31))
     hipLaunchKernelGGL((bn_maxpool_fwd_kernel<3, 2, uint32_t>), dim3(blocks_for(no)), dim3(NT), 0,
-                       st, x, coef, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+                       st, x, coef, y, idx, zarg, N, H, W, C, Ho, Wo, k, s, pt, pl);
   else
     hipLaunchKernelGGL((bn_maxpool_fwd_kernel<0, 0, long>), dim3(blocks_for(no)), dim3(NT), 0, st,
-                       x, coef, y, idx, N, H, W, C, Ho, Wo, k, s, pt, pl);
+                       x, coef, y, idx, zarg, N, H, W, C, Ho, Wo, k, s, pt, pl);
+  return true;
+}
+
+bool maxpool_bn_bwd_launch(const bf16_t* dy, const uint8_t* idx, const bf16_t* zarg,
+                           const bf16_t* x, const float* coef, float* red, const float* gamma,
+                           bf16_t* dx, float* dgamma, float* dbeta, int N, int H, int W, int C,
+                           int Ho, int Wo, int k, int s, int pt, int pl, float inv_count,
+                           hipStream_t st) {
+  if (C % 8 || NT % (C / 8)) return false;
+  const long nout = (long)N * Ho * Wo * C / 8;
+  hipLaunchKernelGGL(maxpool_bn_sums_kernel, dim3(blocks_for(nout)), dim3(NT), 0, st, dy, idx, zarg,
+                     red, nout, C);
+  const long nin = (long)N * H * W * C / 8;
+  if (k == 3 && s == 2 && nin * 8 < (1L << 31) && nout * 8 < (1L << 31))
+    hipLaunchKernelGGL((maxpool_bn_apply_kernel<3, 2, uint32_t>), dim3(blocks_for(nin)), dim3(NT), 0,
+                       st, dy, idx, x, coef, red, gamma, dx, dgamma, dbeta, N, H, W, C, Ho, Wo, k, s,
+                       pt, pl, inv_count);
+  else
+    hipLaunchKernelGGL((maxpool_bn_apply_kernel<0, 0, long>), dim3(blocks_for(nin)), dim3(NT), 0, st,
+                       dy, idx, x, coef, red, gamma, dx, dgamma, dbeta, N, H, W, C, Ho, Wo, k, s, pt,
+                       pl, inv_count);
   return true;
 }
 

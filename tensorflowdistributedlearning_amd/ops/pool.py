@@ -88,6 +88,9 @@ def max_pool2d(x, k, s, pad):
 
 # the ResNet stem's BN + ReLU folded into its max-pool (bn_relu_max_pool); 0: apply pass + pool
 STEM_FUSE = os.environ.get("TDL_STEM_POOL_FUSE", "1") == "1"
+# its backward as BN sums per pool output + one gather-and-apply pass (0: gather pass writing g,
+# then the BN backward apply)
+FUSED_BWD = os.environ.get("TDL_STEM_POOL_FUSED_BWD", "1") == "1"
 
 
 class _BNReluMaxPoolFn(torch.autograd.Function):
@@ -112,10 +115,13 @@ class _BNReluMaxPoolFn(torch.autograd.Function):
         Ho, Wo = _out(H, k, s, pad[0], pad[1]), _out(W, k, s, pad[2], pad[3])
         y = torch.empty((N, Ho, Wo, C), device=z.device, dtype=z.dtype)
         idx = torch.empty((N, Ho, Wo, C), device=z.device, dtype=torch.uint8)
-        if not ext().bn_maxpool_fwd(z, coef, y, idx, k, s, pad[0], pad[2]):
+        # z at each window's argmax: the two-pass fused backward (BN sums per pool output) reads
+        # it; deterministic mode keeps the gather + reduce + apply backward
+        zarg = (torch.empty_like(y) if FUSED_BWD and not ext().deterministic() else None)
+        if not ext().bn_maxpool_fwd(z, coef, y, idx, k, s, pad[0], pad[2], zarg=zarg):
             raise RuntimeError("bn_relu_max_pool: channel count not a multiple of 8")
         ctx.k, ctx.s, ctx.pad, ctx.bn, ctx.count = k, s, pad, bn, count
-        ctx.save_for_backward(z, idx, coef, gamma, beta)
+        ctx.save_for_backward(z, idx, coef, gamma, beta, zarg)
         return y
 
     @staticmethod
@@ -123,20 +129,36 @@ class _BNReluMaxPoolFn(torch.autograd.Function):
         from .bn import (bn_bwd_reduce, bn_bwd_apply, bn_red_xhat, _phys_params,
                          _grad_target_phys)
         from .common import deliver_grad
-        z, idx, coef, gamma, beta = ctx.saved_tensors
+        z, idx, coef, gamma, beta, zarg = ctx.saved_tensors
         dy = dy.contiguous()
         C, c = z.shape[-1], beta.numel()
-        g = torch.empty_like(z)
         red = workspace.zeros((2, C), dy.device)
-        fused = ext().maxpool_bwd_rb(dy, idx, g, ctx.k, ctx.s, ctx.pad[0], ctx.pad[2], z, red)
-        if not fused:
-            red = bn_bwd_reduce(g, None, z, coef, 0)  # (Σg, Σg·ẑ), deterministic mode
         want_g = gamma is not None and gamma.requires_grad
         want_b = beta.requires_grad
         gt, gfresh = _grad_target_phys(gamma, C) if want_g else (None, False)
         bt, bfresh = _grad_target_phys(beta, C) if want_b else (None, False)
         direct_g, direct_b = gt is not None and gfresh, bt is not None and bfresh
         gp, _ = _phys_params(ctx.bn, gamma, beta)
+        if zarg is not None:
+            # two passes: (Σg, Σg·z) per pool output from zarg, then the gather + BN backward
+            # apply per input pixel — g is never written
+            dz = torch.empty_like(z)
+            dg = gt if direct_g else (torch.empty(C, device=z.device) if want_g else None)
+            db = bt if direct_b else (torch.empty(C, device=z.device) if want_b else None)
+            if ext().maxpool_bn_bwd(dy, idx, zarg, z, coef, red,
+                                    gp.detach().float().contiguous() if gp is not None else None,
+                                    dz, dg, db, float(ctx.count), ctx.k, ctx.s, ctx.pad[0],
+                                    ctx.pad[2]):
+                if want_g:
+                    deliver_grad(gamma, None if direct_g else dg[:c], written=direct_g)
+                if want_b:
+                    deliver_grad(beta, None if direct_b else db[:c], written=direct_b)
+                return dz, None, None, None, None, None, None, None
+            red.zero_()
+        g = torch.empty_like(z)
+        fused = ext().maxpool_bwd_rb(dy, idx, g, ctx.k, ctx.s, ctx.pad[0], ctx.pad[2], z, red)
+        if not fused:
+            red = bn_bwd_reduce(g, None, z, coef, 0)  # (Σg, Σg·ẑ), deterministic mode
         dz, _ = bn_bwd_apply(g, None, z, coef, red, gp, ctx.count, 0, False,
                              gt if direct_g else None, bt if direct_b else None, red_raw=fused)
         if fused and want_g and not direct_g:

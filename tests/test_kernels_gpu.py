@@ -1453,6 +1453,9 @@ def test_bn_relu_max_pool_matches_unfused(gpu, det, H):
         ext().det_set(-1)
     assert torch.equal(y, ref)
     assert rel_err(zb.grad, za.grad) < 1e-2
-    assert rel_err(bn_b.gamma.grad, bn_a.gamma.grad) < 1e-3
-    assert rel_err(bn_b.beta.grad, bn_a.beta.grad) < 1e-3
+    # the two-pass fused backward sums every window's fp32 contribution; the unfused gather first
+    # stores g per pixel as bf16 (relative rounding 2^-8 per term of Σg·x̂): a few 1e-3 apart
+    tol = 1e-3 if det else 5e-3
+    assert rel_err(bn_b.gamma.grad, bn_a.gamma.grad) < tol
+    assert rel_err(bn_b.beta.grad, bn_a.beta.grad) < tol
     assert torch.allclose(bn_b.running_mean, bn_a.running_mean)
