@@ -990,6 +990,10 @@ def test_row_packed_stem_gpu(gpu):
         ref = C.row_pack(x, 3, 7, sw, pl, Wo, 24)
         got = C.row_pack(x.to(gpu), 3, 7, sw, pl, Wo, 24)
         assert torch.equal(got.cpu(), ref)
+    xs = torch.randn(2, 5, 224, 8).bfloat16()  # the ResNet stem's row width (LDS-staged kernel)
+    xs[..., 3:] = 0
+    assert torch.equal(C.row_pack(xs.to(gpu), 3, 7, 2, 3, 112, 24).cpu(),
+                       C.row_pack(xs, 3, 7, 2, 3, 112, 24))
     plain = Conv2d(3, 64, 7, 2, "sym", pad_cin_to=8).to(gpu)
     packed = RowPackedConv2d(3, 64, 7, 2, "sym", pad_cin_to=8).to(gpu)
     packed.weight.data.copy_(plain.weight.data)
