@@ -11,6 +11,100 @@ inline int blocks_for(long n) {
   return (int)std::min<long>(8192, std::max<long>(1, (n + NT - 1) / NT));
 }
 
+// Compile-time windows (KK / SS > 0) can load every tap before using the first: a per-tap bounds
+// check around each load otherwise puts a vmcnt(0) between consecutive loads.  Measured at the
+// ResNet-50 stem, batch 1024 (profiles/r06_pool_gather.txt): −3 % for bn_maxpool_fwd, +5 % for
+// maxpool_bn_apply (which keeps its per-window loop).
+
+// one raw 8-channel vector (bf16: one 16-B load, fp32: two)
+template <typename T>
+struct Raw8 {
+  uint4 u[sizeof(T) / 2];
+};
+template <typename T>
+__device__ __forceinline__ Raw8<T> ldraw8(const T* p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.u[i] = ((const uint4*)p)[i];
+  return r;
+}
+__device__ __forceinline__ void cvt8(const Raw8<bf16_t>& r, float* f) { unpack8(r.u[0], f); }
+__device__ __forceinline__ void cvt8(const Raw8<float>& r, float* f) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f[4 * i + 0] = __uint_as_float(r.u[i].x);
+    f[4 * i + 1] = __uint_as_float(r.u[i].y);
+    f[4 * i + 2] = __uint_as_float(r.u[i].z);
+    f[4 * i + 3] = __uint_as_float(r.u[i].w);
+  }
+}
+
+// the KK×KK window of output (n, ho, wo): taps outside the image load the clamped pixel and have
+// their bit clear in the returned mask (bit r·KK + q)
+template <int KK, int SS, typename I, typename T>
+__device__ __forceinline__ uint32_t window_load(const T* x, int n, int ho, int wo, int H, int W,
+                                                int C, int c, int pt, int pl,
+                                                Raw8<T> (&v)[KK * KK]) {
+  uint32_t ok = 0;
+#pragma unroll
+  for (int r = 0; r < KK; ++r) {
+    const int hi = ho * SS - pt + r;
+    const bool okr = (unsigned)hi < (unsigned)H;
+    const int hc = min(max(hi, 0), H - 1);
+#pragma unroll
+    for (int q = 0; q < KK; ++q) {
+      const int wi = wo * SS - pl + q;
+      const bool okq = (unsigned)wi < (unsigned)W;
+      const int wc = min(max(wi, 0), W - 1);
+      v[r * KK + q] = ldraw8(x + (((I)n * H + hc) * W + wc) * C + c);
+      ok |= (okr && okq ? 1u : 0u) << (r * KK + q);
+    }
+  }
+  return ok;
+}
+
+// the ≤NW×NW (NW = ⌈KK/SS⌉) windows that contain input pixel (n, h, w), in the runtime loops'
+// ascending (ho, wo) order: dy vectors and index bytes all issued up front; a window that does not
+// contain the pixel gets want = −1 (no index byte matches it).  flag: 0x80 for the ReLU-bit
+// indices of bn_maxpool_fwd_kernel.
+template <int KK, int SS, typename I>
+struct PoolGather {
+  static constexpr int NW = (KK + SS - 1) / SS;
+  uint4 g[NW * NW];
+  uint2 ix[NW * NW];
+  int want[NW * NW];
+  __device__ __forceinline__ void load(const bf16_t* dy, const uint8_t* idx, int n, int h, int w,
+                                       int Ho, int Wo, int C, int c, int pt, int pl, int flag) {
+    const int hh = h + pt, ww = w + pl, hb = hh / SS, wb = ww / SS;
+#pragma unroll
+    for (int a = 0; a < NW; ++a) {
+      const int ho = hb - (NW - 1) + a, r = hh - ho * SS;
+      const bool okr = ho >= 0 && ho < Ho && r < KK;
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int wo = wb - (NW - 1) + b, q = ww - wo * SS;
+        const bool ok = okr && wo >= 0 && wo < Wo && q < KK;
+        const I o = (((I)n * Ho + (ok ? ho : 0)) * Wo + (ok ? wo : 0)) * C + c;
+        g[a * NW + b] = *(const uint4*)(dy + o);
+        ix[a * NW + b] = *(const uint2*)(idx + o);
+        want[a * NW + b] = ok ? ((r * KK + q) | flag) : -1;
+      }
+    }
+  }
+  __device__ __forceinline__ void sum(float* acc) const {
+#pragma unroll
+    for (int i = 0; i < NW * NW; ++i) {
+      float gv[8];
+      unpack8(g[i], gv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t word = j < 4 ? ix[i].x : ix[i].y;
+        if ((int)((word >> ((j & 3) * 8)) & 0xff) == want[i]) acc[j] += gv[j];
+      }
+    }
+  }
+};
+
 // V = 8 (vector) or 1 (scalar); T = bf16_t or float storage; KK / SS / I as maxpool_bwd_stats
 template <int V, typename T, int KK = 0, int SS = 0, typename I = long>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
@@ -33,6 +127,22 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
       best[j] = -INFINITY;
       arg[j] = 0;
     }
+    if constexpr (KK > 0 && V == 8) {
+      Raw8<T> raw[KK * KK];
+      const uint32_t ok = window_load<KK, SS, I>(x, n, ho, wo, H, W, C, c, pt, pl, raw);
+#pragma unroll
+      for (int i = 0; i < KK * KK; ++i) {
+        if (!((ok >> i) & 1u)) continue;
+        float v[8];
+        cvt8(raw[i], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j]) {
+            best[j] = v[j];
+            arg[j] = i;
+          }
+      }
+    } else
     for (int r = 0; r < k; ++r) {
       const int hi = ho * s - pt + r;
       if ((unsigned)hi >= (unsigned)H) continue;
@@ -151,27 +261,34 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    const int hh = h + pt, ww = w + pl;
-    const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
-    const int ho_hi = min(Ho - 1, hh / s);
-    const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
-    const int wo_hi = min(Wo - 1, ww / s);
-    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
-      const int r = hh - ho * s;
-      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-        const int want = r * k + (ww - wo * s);
-        const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
-        float g[8];
-        unpack8(*(const uint4*)(dy + o), g);
-        const uint2 packed = *(const uint2*)(idx + o);
+    const I off = (((I)n * H + h) * W + w) * C + c;
+    const uint4 bxv = *(const uint4*)(bx + off);
+    if constexpr (KK > 0) {
+      PoolGather<KK, SS, I> pg;
+      pg.load(dy, idx, n, h, w, Ho, Wo, C, c, pt, pl, RB ? 0x80 : 0);
+      pg.sum(acc);
+    } else {
+      const int hh = h + pt, ww = w + pl;
+      const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
+      const int ho_hi = min(Ho - 1, hh / s);
+      const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
+      const int wo_hi = min(Wo - 1, ww / s);
+      for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+        const int r = hh - ho * s;
+        for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+          const int want = r * k + (ww - wo * s);
+          const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
+          float g[8];
+          unpack8(*(const uint4*)(dy + o), g);
+          const uint2 packed = *(const uint2*)(idx + o);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t word = j < 4 ? packed.x : packed.y;
-          if ((int)((word >> ((j & 3) * 8)) & 0xff) == (RB ? want | 0x80 : want)) acc[j] += g[j];
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t word = j < 4 ? packed.x : packed.y;
+            if ((int)((word >> ((j & 3) * 8)) & 0xff) == (RB ? want | 0x80 : want)) acc[j] += g[j];
+          }
         }
       }
     }
-    const I off = (((I)n * H + h) * W + w) * C + c;
     if constexpr (!RB) {
       const uint32_t mb = mask[off >> 3];
 #pragma unroll
@@ -181,7 +298,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
     *(uint4*)(dx + off) = st;
     float q[8], xv[8];
     unpack8(st, q);  // statistics of the stored bf16 values
-    unpack8(*(const uint4*)(bx + off), xv);
+    unpack8(bxv, xv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       s0[j] += q[j];
@@ -208,7 +325,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
 // one pass over the conv output: the BN output is never written or re-read.  coef = bn_finalize's
 // fp32 rows (scale, shift, …).  The index byte's bit 7 records u_max > 0 — the BN's ReLU mask at
 // the argmax, the only position the backward routes gradient to (maxpool_bwd*<RB>).
-template <int KK, int SS, typename I>
+template <int KK, int SS, typename I, bool PRE = true>
 __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ coef, bf16_t* __restrict__ y,
     uint8_t* __restrict__ idx, bf16_t* __restrict__ zarg, int N, int H, int W, int C, int Ho,
@@ -242,6 +359,26 @@ __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
       arg[j] = 0;
       zbest[j] = 0.f;
     }
+    if constexpr (KK > 0 && PRE) {
+      Raw8<bf16_t> raw[KK * KK];
+      const uint32_t ok = window_load<KK, SS, I>(x, n, ho, wo, H, W, C, c, pt, pl, raw);
+#pragma unroll
+      for (int i = 0; i < KK * KK; ++i) {
+        if (!((ok >> i) & 1u)) continue;
+        float v[8], xr[8];
+        cvt8(raw[i], xr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(xr[j] * sc[j] + sh[j], 0.f);
+        unpack8(pack8(v), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j]) {
+            best[j] = v[j];
+            arg[j] = i;
+            zbest[j] = xr[j];
+          }
+      }
+    } else
     for (int r = 0; r < k; ++r) {
       const int hi = ho * s - pt + r;
       if ((unsigned)hi >= (unsigned)H) continue;
@@ -292,17 +429,35 @@ __global__ void __launch_bounds__(NT) maxpool_bn_sums_kernel(
   float s0[8], s1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
-  for (long t = blockIdx.x * (long)NT + threadIdx.x; t < nvec; t += (long)gridDim.x * NT) {
-    float g[8], z[8];
-    unpack8(((const uint4*)dy)[t], g);
-    unpack8(((const uint4*)zarg)[t], z);
-    const uint2 packed = ((const uint2*)idx)[t];
+  // U vectors per thread per trip, all loads issued first; the grid is a few blocks per CU (the
+  // per-block atomics onto 2·C addresses serialise in L2: 8192 blocks cost ≈150 µs)
+  constexpr int U = 4;
+  const long stride = (long)gridDim.x * NT;
+  long t = blockIdx.x * (long)NT + threadIdx.x;
+  for (; t < nvec; t += U * stride) {
+    uint4 gv[U], zv[U];
+    uint2 iv[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t word = j < 4 ? packed.x : packed.y;
-      const float a = (word >> ((j & 3) * 8)) & 0x80u ? g[j] : 0.f;
-      s0[j] += a;
-      s1[j] = fmaf(a, z[j], s1[j]);
+    for (int u = 0; u < U; ++u) {
+      const long tu = min(t + u * stride, nvec - 1);
+      gv[u] = ((const uint4*)dy)[tu];
+      zv[u] = ((const uint4*)zarg)[tu];
+      iv[u] = ((const uint2*)idx)[tu];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      // (a past-the-end vector counts as zero: no branch the compiler could sink the loads into)
+      const uint32_t live = t + u * stride < nvec ? 0x80u : 0u;
+      float g[8], z[8];
+      unpack8(gv[u], g);
+      unpack8(zv[u], z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t word = j < 4 ? iv[u].x : iv[u].y;
+        const float a = (word >> ((j & 3) * 8)) & live ? g[j] : 0.f;
+        s0[j] += a;
+        s1[j] = fmaf(a, z[j], s1[j]);
+      }
     }
   }
   const int tid = threadIdx.x;
@@ -363,23 +518,25 @@ __global__ void __launch_bounds__(NT) maxpool_bn_apply_kernel(
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    const int hh = h + pt, ww = w + pl;
-    const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
-    const int ho_hi = min(Ho - 1, hh / s);
-    const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
-    const int wo_hi = min(Wo - 1, ww / s);
-    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
-      const int r = hh - ho * s;
-      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-        const int want = (r * k + (ww - wo * s)) | 0x80;
-        const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
-        float g[8];
-        unpack8(*(const uint4*)(dy + o), g);
-        const uint2 packed = *(const uint2*)(idx + o);
+    {  // (the per-window loop: PoolGather's loads-up-front measured 5 % slower here)
+      const int hh = h + pt, ww = w + pl;
+      const int ho_lo = hh - (k - 1) <= 0 ? 0 : (hh - (k - 1) + s - 1) / s;
+      const int ho_hi = min(Ho - 1, hh / s);
+      const int wo_lo = ww - (k - 1) <= 0 ? 0 : (ww - (k - 1) + s - 1) / s;
+      const int wo_hi = min(Wo - 1, ww / s);
+      for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+        const int r = hh - ho * s;
+        for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+          const int want = (r * k + (ww - wo * s)) | 0x80;
+          const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
+          float g[8];
+          unpack8(*(const uint4*)(dy + o), g);
+          const uint2 packed = *(const uint2*)(idx + o);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t word = j < 4 ? packed.x : packed.y;
-          if ((int)((word >> ((j & 3) * 8)) & 0xff) == want) acc[j] += g[j];
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t word = j < 4 ? packed.x : packed.y;
+            if ((int)((word >> ((j & 3) * 8)) & 0xff) == want) acc[j] += g[j];
+          }
         }
       }
     }
@@ -508,7 +665,9 @@ bool maxpool_bwd_stats_launch(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, 
       kern = k == 3 && s == 2 ? maxpool_bwd_stats_kernel<3, 2, uint32_t, true>
                               : maxpool_bwd_stats_kernel<0, 0, uint32_t, true>;
   }
-  hipLaunchKernelGGL(kern, dim3(blocks_for(n / 8)), dim3(NT), 0, st, dy, idx, dx, bx, mask, red, N,
+  // (a few blocks per CU: every block ends in 2·C atomics onto the same addresses)
+  hipLaunchKernelGGL(kern, dim3(std::min(2048, blocks_for(n / 8))), dim3(NT), 0, st, dy, idx, dx, bx,
+                     mask, red, N,
                      H, W, C, Ho, Wo, k, s, pt, pl);
   return true;
 }
@@ -518,9 +677,12 @@ bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_
                            int pt, int pl, hipStream_t st) {
   if (C % 8) return false;
   const long no = (long)N * Ho * Wo * C / 8;
+  // TDL_POOL_PRELOAD=0: the per-tap loop (loads serialised by its bounds checks; A/B only)
+  static const bool pre = getenv("TDL_POOL_PRELOAD") == nullptr || atoi(getenv("TDL_POOL_PRELOAD")) != 0;
   if (k == 3 && s == 2 && (long)N * H * W * C < (1L << 31))
-    hipLaunchKernelGGL((bn_maxpool_fwd_kernel<3, 2, uint32_t>), dim3(blocks_for(no)), dim3(NT), 0,
-                       st, x, coef, y, idx, zarg, N, H, W, C, Ho, Wo, k, s, pt, pl);
+    hipLaunchKernelGGL((pre ? bn_maxpool_fwd_kernel<3, 2, uint32_t> : bn_maxpool_fwd_kernel<3, 2, uint32_t, false>),
+                       dim3(blocks_for(no)), dim3(NT), 0, st, x, coef, y, idx, zarg, N, H, W, C, Ho, Wo,
+                       k, s, pt, pl);
   else
     hipLaunchKernelGGL((bn_maxpool_fwd_kernel<0, 0, long>), dim3(blocks_for(no)), dim3(NT), 0, st,
                        x, coef, y, idx, zarg, N, H, W, C, Ho, Wo, k, s, pt, pl);
@@ -534,8 +696,8 @@ bool maxpool_bn_bwd_launch(const bf16_t* dy, const uint8_t* idx, const bf16_t* z
                            hipStream_t st) {
   if (C % 8 || NT % (C / 8)) return false;
   const long nout = (long)N * Ho * Wo * C / 8;
-  hipLaunchKernelGGL(maxpool_bn_sums_kernel, dim3(blocks_for(nout)), dim3(NT), 0, st, dy, idx, zarg,
-                     red, nout, C);
+  hipLaunchKernelGGL(maxpool_bn_sums_kernel, dim3(std::min(1024, blocks_for(nout))), dim3(NT), 0, st,
+                     dy, idx, zarg, red, nout, C);
   const long nin = (long)N * H * W * C / 8;
   if (k == 3 && s == 2 && nin * 8 < (1L << 31) && nout * 8 < (1L << 31))
     hipLaunchKernelGGL((maxpool_bn_apply_kernel<3, 2, uint32_t>), dim3(blocks_for(nin)), dim3(NT), 0,
