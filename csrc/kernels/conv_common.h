@@ -331,7 +331,8 @@ __device__ __forceinline__ void epi_preload_dgrad(const ConvArgs& a, const Tile&
 }
 
 template <int MODE, int RM, int RN, int TM, int TN, bool BIAS, bool STATS, bool SCALE, bool DGM = false,
-          bool NJ = false, bool FRES = false, bool ROWS = false, bool AFM = false, bool PRE = false>
+          bool NJ = false, bool FRES = false, bool ROWS = false, bool AFM = false, bool PRE = false,
+          int RG = RM>
 __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T,
                                                 const f32x4 (&acc)[RM][RN], int wm, int wn,
                                                 int lane, rsrc_t rout, float scale, bool no_mem,
@@ -339,6 +340,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
                                                 const uint32_t* rows_in = nullptr,
                                                 const EpiPre<RM, RN>* pre = nullptr) {
   static_assert(!PRE || (MODE == DGRAD && ROWS && !AFM), "preloaded operands: DGRAD, rows given");
+  static_assert(RG >= 1 && RM % RG == 0, "fragment-row groups");
   // Row byte offsets are 32-bit with invalid rows pushed past the buffer (ROW_OOB): a
   // fragment's store offset is then row base + a compile-time constant.  Rows past the GEMM's
   // M hold zeros (their A rows were fetched out of range), so the statistics need no mask.
@@ -386,28 +388,6 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
   // DGRAD BN-backward statistics (STATS): the BN input x at the stored positions — Σg·x with g
   // the stored (masked) dx; the BN backward converts to Σg·x̂ (bn.hip, red_raw)
   v2u32 xv[RM][RN];
-  if constexpr (PRE) {
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-      mrow[rm][0] = pre->mrow[rm][0];
-      mrow[rm][1] = pre->mrow[rm][1];
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) {
-        if constexpr (STATS) xv[rm][rn] = pre->xv[rm][rn];
-        if constexpr (!NJ) pv[rm][rn] = pre->pv[rm][rn];
-      }
-    }
-  } else if constexpr (MODE == DGRAD && STATS) {
-    const rsrc_t rbx = make_rsrc(a.bn_x, no_mem ? 0u : a.out_bytes);
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) {
-        const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-        xv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
-            rbx, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-      }
-  }
   // folded BN + ReLU of this dgrad's output (ConvArgs::aff): dx is masked by a·x + b > 0 of the
   // BN input x the statistics read anyway — no bit mask exists (ops/bnconv.py)
   constexpr bool aff_mask = AFM && MODE == DGRAD && STATS;
@@ -424,133 +404,162 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
       }
     }
   }
-  if constexpr (MODE == DGRAD && !PRE) {
-    if (join_mask) {
-      const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
+  const bool relu = a.relu;
+  const bool wide = cols_ok;
+  // RG < RM: the epilogue operands are loaded and consumed RG fragment rows at a time (two
+  // memory round trips instead of one, half the live operand registers — the 256×128 tiles'
+  // statistics + join epilogue otherwise spills)
 #pragma unroll
-      for (int rm = 0; rm < RM; ++rm) {
-        const uint32_t boff = (rbase[rm] / 2u + (uint32_t)(T.bn0 + wn * TN)) >> 3;
-        const uint32_t o = rbase[rm] != ROW_OOB ? boff : OOB;
-        if constexpr (TN == 64) {
-          const v2u32 m2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, o, 0, 0);
-          mrow[rm][0] = m2[0];
-          mrow[rm][1] = m2[1];
-        } else {
-          static_assert(TN == 32, "mask slab of 4 or 8 bytes");
-          mrow[rm][0] = __builtin_amdgcn_raw_buffer_load_b32(rmask, o, 0, 0);
-          mrow[rm][1] = 0;
+  for (int g0 = 0; g0 < RM; g0 += RG) {
+    if constexpr (PRE) {
+#pragma unroll
+      for (int rm = g0; rm < g0 + RG; ++rm) {
+        mrow[rm][0] = pre->mrow[rm][0];
+        mrow[rm][1] = pre->mrow[rm][1];
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn) {
+          if constexpr (STATS) xv[rm][rn] = pre->xv[rm][rn];
+          if constexpr (!NJ) pv[rm][rn] = pre->pv[rm][rn];
         }
       }
-    }
-  }
-  if constexpr (((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) && !PRE) {
-    if (join_prev) {
-      // DGRAD: the previous dx of the output buffer itself; FWD: the residual tensor
-      const rsrc_t rprev = MODE == FWD ? make_rsrc(a.res, a.out_bytes) : rout;
+    } else if constexpr (MODE == DGRAD && STATS) {
+      const rsrc_t rbx = make_rsrc(a.bn_x, no_mem ? 0u : a.out_bytes);
 #pragma unroll
-      for (int rm = 0; rm < RM; ++rm)
+      for (int rm = g0; rm < g0 + RG; ++rm)
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
           const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-          pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
-              rprev, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+          xv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
+              rbx, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
         }
     }
-  }
-  const bool relu = a.relu;
-  const bool wide = cols_ok;
+    if constexpr (MODE == DGRAD && !PRE) {
+      if (join_mask) {
+        const rsrc_t rmask = make_rsrc(a.mask, a.out_bytes / 16u);
 #pragma unroll
-  for (int rm = 0; rm < RM; ++rm) {
-    v2u32 pk[RN];
-#pragma unroll
-    for (int rn = 0; rn < RN; ++rn) {
-      f32x4 t = acc[rm][rn];
-      if constexpr (SCALE) t = t * scale;
-      if constexpr (BIAS) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] += __uint_as_float(bias_v[rn][i]);
-      }
-      if constexpr ((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) {
-        if (join_prev) {
-          t[0] += __uint_as_float(pv[rm][rn][0] << 16);
-          t[1] += __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
-          t[2] += __uint_as_float(pv[rm][rn][1] << 16);
-          t[3] += __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
+        for (int rm = g0; rm < g0 + RG; ++rm) {
+          const uint32_t boff = (rbase[rm] / 2u + (uint32_t)(T.bn0 + wn * TN)) >> 3;
+          const uint32_t o = rbase[rm] != ROW_OOB ? boff : OOB;
+          if constexpr (TN == 64) {
+            const v2u32 m2 = __builtin_amdgcn_raw_buffer_load_b64(rmask, o, 0, 0);
+            mrow[rm][0] = m2[0];
+            mrow[rm][1] = m2[1];
+          } else {
+            static_assert(TN == 32, "mask slab of 4 or 8 bytes");
+            mrow[rm][0] = __builtin_amdgcn_raw_buffer_load_b32(rmask, o, 0, 0);
+            mrow[rm][1] = 0;
+          }
         }
-      }
-      if constexpr (MODE == DGRAD) {
-        if (join_mask) {
-          // bit (rn·16 + group·4 + i) of the wave's TN-column slab; v_bfe_i32 → 0 / ~0
-          const int sh = (rn & 1) * 16 + (lane >> 4) * 4;
-          const uint32_t w = mrow[rm][rn >> 1];
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            t[i] = __uint_as_float(__float_as_uint(t[i]) &
-                                   (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + i, 1));
-        }
-      }
-      if constexpr (aff_mask) {
-        {
-          const float z[4] = {__uint_as_float(xv[rm][rn][0] << 16),
-                              __uint_as_float(xv[rm][rn][0] & 0xffff0000u),
-                              __uint_as_float(xv[rm][rn][1] << 16),
-                              __uint_as_float(xv[rm][rn][1] & 0xffff0000u)};
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            t[i] = fmaf(z[i], __uint_as_float(aff_a[rn][i]), __uint_as_float(aff_b[rn][i])) > 0.f
-                       ? t[i] : 0.f;
-        }
-      }
-      pk[rn][0] = cvt_pk_bf16(t[0], t[1]);
-      pk[rn][1] = cvt_pk_bf16(t[2], t[3]);
-      if (relu) {
-        pk[rn][0] = relu_pk_bf16(pk[rn][0]);
-        pk[rn][1] = relu_pk_bf16(pk[rn][1]);
-      }
-      // ragged column tiles: columns ≥ Ng hold zeros (B rows fetched out of range) and must
-      // not be stored (they would land in the next row)
-      const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
-      if (!no_mem && !wide)
-        __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
-      if constexpr (STATS && MODE == DGRAD) {
-        // (Σg, Σg·x) of the stored bf16 g; rows past M store zeros (x reads there return 0)
-        const float rg = (!ROWS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
-        const float v0 = __uint_as_float(pk[rn][0] << 16) * rg, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rg;
-        const float v2 = __uint_as_float(pk[rn][1] << 16) * rg, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rg;
-        s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
-        s_sq[rn][0] = fmaf(v0, __uint_as_float(xv[rm][rn][0] << 16), s_sq[rn][0]);
-        s_sq[rn][1] = fmaf(v1, __uint_as_float(xv[rm][rn][0] & 0xffff0000u), s_sq[rn][1]);
-        s_sq[rn][2] = fmaf(v2, __uint_as_float(xv[rm][rn][1] << 16), s_sq[rn][2]);
-        s_sq[rn][3] = fmaf(v3, __uint_as_float(xv[rm][rn][1] & 0xffff0000u), s_sq[rn][3]);
-      } else if constexpr (STATS) {
-        // statistics of the stored bf16 values; rows past M are zero unless a bias was added
-        const float rv = (!(BIAS || ROWS) || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
-        const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;
-        const float v2 = __uint_as_float(pk[rn][1] << 16) * rv, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rv;
-        s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
-        s_sq[rn][0] = fmaf(v0, v0, s_sq[rn][0]);
-        s_sq[rn][1] = fmaf(v1, v1, s_sq[rn][1]);
-        s_sq[rn][2] = fmaf(v2, v2, s_sq[rn][2]);
-        s_sq[rn][3] = fmaf(v3, v3, s_sq[rn][3]);
       }
     }
-    if (!no_mem && wide) {
-      // 16-B stores: v_permlane16_swap trades the odd 16-lane rows of fragment p with the
-      // even rows of fragment p+1, so lanes l and l^16 (column groups 2j, 2j+1 of one row)
-      // each end up with 8 consecutive columns — even lanes of block p, odd lanes of block
-      // p+1 — and an instruction writes 16 rows × 64 B instead of 16 rows × 32 B (half the
-      // write requests: −20 % on the 1×1 dgrads, profiles/r02_dgrad_ablation.txt)
-      const int g = lane >> 4;
-      const uint32_t lcol = (uint32_t)(T.bn0 + wn * TN + (g & 1) * 16 + (g & ~1) * 4) * 2u;
+    if constexpr (((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) && !PRE) {
+      if (join_prev) {
+        // DGRAD: the previous dx of the output buffer itself; FWD: the residual tensor
+        const rsrc_t rprev = MODE == FWD ? make_rsrc(a.res, a.out_bytes) : rout;
 #pragma unroll
-      for (int p = 0; p < RN; p += 2) {
-        const auto s0 = __builtin_amdgcn_permlane16_swap(pk[p][0], pk[p + 1][0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(pk[p][1], pk[p + 1][1], false, false);
-        v4u32 q;
-        q[0] = s0[0]; q[1] = s1[0]; q[2] = s0[1]; q[3] = s1[1];
-        __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, 0);
+        for (int rm = g0; rm < g0 + RG; ++rm)
+#pragma unroll
+          for (int rn = 0; rn < RN; ++rn) {
+            const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+            pv[rm][rn] = __builtin_amdgcn_raw_buffer_load_b64(
+                rprev, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+          }
       }
     }
+#pragma unroll
+    for (int rm = g0; rm < g0 + RG; ++rm) {
+      v2u32 pk[RN];
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) {
+        f32x4 t = acc[rm][rn];
+        if constexpr (SCALE) t = t * scale;
+        if constexpr (BIAS) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) t[i] += __uint_as_float(bias_v[rn][i]);
+        }
+        if constexpr ((MODE == DGRAD && !NJ) || (MODE == FWD && FRES)) {
+          if (join_prev) {
+            t[0] += __uint_as_float(pv[rm][rn][0] << 16);
+            t[1] += __uint_as_float(pv[rm][rn][0] & 0xffff0000u);
+            t[2] += __uint_as_float(pv[rm][rn][1] << 16);
+            t[3] += __uint_as_float(pv[rm][rn][1] & 0xffff0000u);
+          }
+        }
+        if constexpr (MODE == DGRAD) {
+          if (join_mask) {
+            // bit (rn·16 + group·4 + i) of the wave's TN-column slab; v_bfe_i32 → 0 / ~0
+            const int sh = (rn & 1) * 16 + (lane >> 4) * 4;
+            const uint32_t w = mrow[rm][rn >> 1];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              t[i] = __uint_as_float(__float_as_uint(t[i]) &
+                                     (uint32_t)__builtin_amdgcn_sbfe((int)w, sh + i, 1));
+          }
+        }
+        if constexpr (aff_mask) {
+          {
+            const float z[4] = {__uint_as_float(xv[rm][rn][0] << 16),
+                                __uint_as_float(xv[rm][rn][0] & 0xffff0000u),
+                                __uint_as_float(xv[rm][rn][1] << 16),
+                                __uint_as_float(xv[rm][rn][1] & 0xffff0000u)};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              t[i] = fmaf(z[i], __uint_as_float(aff_a[rn][i]), __uint_as_float(aff_b[rn][i])) > 0.f
+                         ? t[i] : 0.f;
+          }
+        }
+        pk[rn][0] = cvt_pk_bf16(t[0], t[1]);
+        pk[rn][1] = cvt_pk_bf16(t[2], t[3]);
+        if (relu) {
+          pk[rn][0] = relu_pk_bf16(pk[rn][0]);
+          pk[rn][1] = relu_pk_bf16(pk[rn][1]);
+        }
+        // ragged column tiles: columns ≥ Ng hold zeros (B rows fetched out of range) and must
+        // not be stored (they would land in the next row)
+        const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
+        if (!no_mem && !wide)
+          __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+        if constexpr (STATS && MODE == DGRAD) {
+          // (Σg, Σg·x) of the stored bf16 g; rows past M store zeros (x reads there return 0)
+          const float rg = (!ROWS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
+          const float v0 = __uint_as_float(pk[rn][0] << 16) * rg, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rg;
+          const float v2 = __uint_as_float(pk[rn][1] << 16) * rg, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rg;
+          s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
+          s_sq[rn][0] = fmaf(v0, __uint_as_float(xv[rm][rn][0] << 16), s_sq[rn][0]);
+          s_sq[rn][1] = fmaf(v1, __uint_as_float(xv[rm][rn][0] & 0xffff0000u), s_sq[rn][1]);
+          s_sq[rn][2] = fmaf(v2, __uint_as_float(xv[rm][rn][1] << 16), s_sq[rn][2]);
+          s_sq[rn][3] = fmaf(v3, __uint_as_float(xv[rm][rn][1] & 0xffff0000u), s_sq[rn][3]);
+        } else if constexpr (STATS) {
+          // statistics of the stored bf16 values; rows past M are zero unless a bias was added
+          const float rv = (!(BIAS || ROWS) || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
+          const float v0 = __uint_as_float(pk[rn][0] << 16) * rv, v1 = __uint_as_float(pk[rn][0] & 0xffff0000u) * rv;
+          const float v2 = __uint_as_float(pk[rn][1] << 16) * rv, v3 = __uint_as_float(pk[rn][1] & 0xffff0000u) * rv;
+          s_sum[rn][0] += v0; s_sum[rn][1] += v1; s_sum[rn][2] += v2; s_sum[rn][3] += v3;
+          s_sq[rn][0] = fmaf(v0, v0, s_sq[rn][0]);
+          s_sq[rn][1] = fmaf(v1, v1, s_sq[rn][1]);
+          s_sq[rn][2] = fmaf(v2, v2, s_sq[rn][2]);
+          s_sq[rn][3] = fmaf(v3, v3, s_sq[rn][3]);
+        }
+      }
+      if (!no_mem && wide) {
+        // 16-B stores: v_permlane16_swap trades the odd 16-lane rows of fragment p with the
+        // even rows of fragment p+1, so lanes l and l^16 (column groups 2j, 2j+1 of one row)
+        // each end up with 8 consecutive columns — even lanes of block p, odd lanes of block
+        // p+1 — and an instruction writes 16 rows × 64 B instead of 16 rows × 32 B (half the
+        // write requests: −20 % on the 1×1 dgrads, profiles/r02_dgrad_ablation.txt)
+        const int g = lane >> 4;
+        const uint32_t lcol = (uint32_t)(T.bn0 + wn * TN + (g & 1) * 16 + (g & ~1) * 4) * 2u;
+#pragma unroll
+        for (int p = 0; p < RN; p += 2) {
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk[p][0], pk[p + 1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk[p][1], pk[p + 1][1], false, false);
+          v4u32 q;
+          q[0] = s0[0]; q[1] = s1[0]; q[2] = s0[1]; q[3] = s1[1];
+          __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, 0);
+        }
+      }
+    }
+
   }
 }
 

@@ -674,8 +674,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) conv_glds_kernel(ConvArgs a) 
       }
     } else {
       if constexpr (M32) acc32_to_16<QM, QN>(acc32, acc);
+      // (statistics + join of the dgrad-as-forward: operands in two halves, else they spill)
+      constexpr int RG = DEPI && STATS && !NJ && RM >= 4 ? RM / 2 : RM;
       store_tile_bf16<DEPI ? DGRAD : MODE, RM, RN, TM, TN, BIAS, STATS, FP8, false, NJ, FRES,
-                      false, AFM>(
+                      false, AFM, false, RG>(
           a, T, acc, wm, wn, lane, rout, out_scale, no_epi_mem, s_sum, s_sq);
     }
   };
@@ -1383,8 +1385,9 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
   const bool stats = a.stats != nullptr && a.bn_x != nullptr;
   if (!stats) a.stats = nullptr;
   if (cfg == 101) return conv_fwd_rw_depi(a, st, fused);  // (statistics and join both fit)
-  // statistics + join: only the 8-wave 256×64 tiles (cfg 4; the 256×128 ones spill)
-  if (stats && a.beta && cfg != 4) return false;
+  // statistics + join: the LDS-DMA tiles (cfg 0 / 4; the 256×128 epilogue loads its operands in
+  // two halves) — not the halo or producer/consumer loaders
+  if (stats && a.beta && cfg != 4 && cfg != 0) return false;
   if (cfg == 100) return conv_fwd_halo_depi(a, st, fused);
   if (cfg == 102) {
     // (not with the statistics epilogue: its x registers spill at the 12-wave register budget)
@@ -1400,7 +1403,8 @@ bool conv_dgrad_as_fwd(const ConvArgs& a0, const bf16_t* wf, uint32_t wf_bytes, 
     else if (stats) launch_g<FWD, 256, 64, 8, 1, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
     else launch_g<FWD, 256, 64, 8, 1, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
   } else {
-    if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
+    if (stats && a.beta) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, false, false, false, false, true>(a, blocks, st);
+    else if (stats) launch_g<FWD, 256, 128, 4, 2, 3, true, false, 1, false, true, false, false, false, true>(a, blocks, st);
     else launch_g<FWD, 256, 128, 4, 2, 3, false, false, 1, false, false, false, false, false, true>(a, blocks, st);
   }
   if (fused) *fused = stats;

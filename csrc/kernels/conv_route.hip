@@ -70,8 +70,10 @@ const RouteRule kRoutes[] = {
    "tests: every eligible dgrad as a forward on the halo loader"},
   {"dgrad.asfwd.pc",              DGRAD, RT_ASFWD, 2, TAPS,  1, 65, INF,     256, INF,    4096,  256, 128, 128, RF_WFLIP,         RF_STATS | RF_AFF | RF_FP8,           ASF_PC, true,  false,
    "3x3 dgrad as the forward conv on the producer/consumer kernel, 22-31 % (profiles/r05_dgrad_as_fwd.txt)"},
+  {"dgrad.asfwd.glds.join.wide",  DGRAD, RT_ASFWD, 1, TAPS,  1, 65, INF,     64, INF,     4096,  256, 128, 128, RF_WFLIP | RF_STATS | RF_JOIN, RF_AFF | RF_FP8,      0,    true,  false,
+   "statistics + residual join on the 256x128 tiles, epilogue operands in two halves (229 VGPRs, no spill; conv_common.h store_tile_bf16 RG)"},
   {"dgrad.asfwd.glds.join",       DGRAD, RT_ASFWD, 1, TAPS,  1, 8, INF,      64, INF,     4096,  256, 64,  128, RF_WFLIP | RF_STATS | RF_JOIN, RF_AFF | RF_FP8,      4,    true,  false,
-   "statistics + residual join on the forward K loop's 8-wave 256x64 tiles (the 256x128 ones spill); reached with TDL_BNSTAT_FUSE=1 only: 12,990 vs 13,175 img/s (ops/gradjoin.py)"},
+   "statistics + residual join on the forward K loop's 8-wave 256x64 tiles (narrow dx: the wide row takes C >= 65)"},
   {"dgrad.asfwd.glds.n64",        DGRAD, RT_ASFWD, 1, TAPS,  1, 8, 64,       64, INF,     4096,  256, 64,  128, RF_WFLIP,         RF_STATS_JOIN | RF_AFF | RF_FP8,      4,    true,  false,
    "stride-1 dgrad as the forward conv: LDS-DMA K loop, DGRAD epilogue (profiles/r05_dgrad_as_fwd.txt)"},
   {"dgrad.asfwd.glds",            DGRAD, RT_ASFWD, 1, TAPS,  1, 65, INF,     64, INF,     4096,  256, 128, 128, RF_WFLIP,         RF_STATS_JOIN | RF_AFF | RF_FP8,      0,    true,  false,

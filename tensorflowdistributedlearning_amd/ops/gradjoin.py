@@ -44,7 +44,10 @@ MASK_ENABLED = os.environ.get("TDL_PREMASK", "1") == "1"  # 0: the BN applies it
 # 3 11882 / 11840 img/s — the join variant's smaller tiles (the 256×128 ones spill with both the
 # previous-dx and the x loads) lose next to the side-stream weight gradients.  Round 5, with the
 # joins' statistics on the dgrad-as-forward 8-wave tiles (route row dgrad.asfwd.glds.join): 1
-# 12,990 / 12,992 vs 2 13,179 / 13,170 img/s (dev/scripts/gpu_r05_statsjoin.sh) — still slower
+# 12,990 / 12,992 vs 2 13,179 / 13,170 img/s (dev/scripts/gpu_r05_statsjoin.sh) — still slower.
+# Round 6, the joins on the 256×128 tiles (route row dgrad.asfwd.glds.join.wide): a tie — serial
+# 77.19 vs 77.23 ms (12 fused joins +2.2 ms, 8 reduce passes −2.1 ms), bench 14,027 / 13,989 /
+# 14,028 vs 14,020 / 14,024 / 14,026 img/s (profiles/r06_join_stats.txt)
 _FUSE = os.environ.get("TDL_BNSTAT_FUSE", "2")
 STATS_ENABLED = _FUSE != "0"
 STATS_SINGLE = _FUSE in ("1", "2")

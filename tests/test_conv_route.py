@@ -79,10 +79,12 @@ def test_dgrad_variants(e):
     assert e.conv_route_select(DGRAD, 9, 1, 256, 256, 256 * 14 * 14, W)[0] == "dgrad.asfwd.pc"
     assert e.conv_route_select(DGRAD, 9, 1, 64, 64, rows, W)[0] == "dgrad.asfwd.rw64"
     assert e.conv_route_select(DGRAD, 9, 1, 64, 128, rows, W)[0] == "dgrad.asfwd.halo"
-    # statistics + join: 8-wave tiles only — the forward K loop's with a flipped filter, else the
-    # DGRAD kernel's
+    # statistics + join: the forward K loop's 256×128 tiles with a flipped filter (its 8-wave
+    # tiles for narrow dx), else the DGRAD kernel's 8-wave ones
     f = S | J | 128 | W
-    assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f)[0] == "dgrad.asfwd.glds.join"
+    assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f)[0] == \
+        "dgrad.asfwd.glds.join.wide"
+    assert e.conv_route_select(DGRAD, 1, 1, 64, 256, 256 * 56 * 56, f)[0] == "dgrad.asfwd.glds.join"
     assert e.conv_route_select(DGRAD, 1, 1, 256, 1024, 256 * 14 * 14, f & ~W)[0] == \
         "dgrad.glds.stats.join"
     # no flipped filter: the DGRAD kernel

@@ -273,3 +273,42 @@ def test_resident_filter_conv_epilogues(gpu, N, H):
             assert fused
             gf, xf = dx.float().cpu().reshape(-1, 64), x.float().cpu().reshape(-1, 64)
             assert _rel(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-3
+
+
+@pytest.mark.parametrize("k,cin,cout", [(1, 256, 64), (1, 1024, 256), (3, 128, 128)])
+def test_wide_join_statistics_epilogue(gpu, k, cin, cout):
+    """The residual join's last dgrad with the BN-backward sums on the 256×128 tiles (route row
+    dgrad.asfwd.glds.join.wide: conv_common.h store_tile_bf16 loads its epilogue operands in two
+    fragment-row halves): dx = (previous dx + dgrad)·[ReLU bit], (Σg, Σg·x) of the stored dx —
+    the bottleneck conv1 joins of ResNet (1×1, C = 256 … 2048) and a 3×3 one."""
+    e = _ext()
+    torch.manual_seed(cin + k)
+    N, H = 4, 14
+    p = (k - 1) // 2
+    g = C.ConvGeom((1, 1), (p, p, p, p), (1, 1))
+    x = (torch.randn(N, H, H, cin) * 1.3 + 0.2).bfloat16().to(gpu)
+    w = (torch.randn(cout, k, k, cin) / math.sqrt(k * k * cout)).bfloat16().to(gpu)
+    dy = torch.randn(N, H, H, cout).bfloat16().to(gpu)
+    coef = _coef(cin, gpu)
+    mask = torch.empty(x.numel() // 8, device=gpu, dtype=torch.uint8)
+    B.bn_apply(x, coef, None, True, mask=mask)
+    m = B.unpack_relu_mask(mask.cpu(), cin).reshape(N, H, H, cin)
+    wf = torch.empty(cin, k, k, cout, device=gpu, dtype=torch.bfloat16)
+    e.conv_flip_weight(w, wf)
+    prev = torch.randn(N, H, H, cin).bfloat16().to(gpu)
+    dx = prev.clone()
+    red = torch.zeros(2, cin, device=gpu)
+    e.conv_route_force(1, "dgrad.asfwd.glds.join.wide")
+    try:
+        fused = e.conv_dgrad(dy, w, dx, *_args(g), True, mask, None, x, red, None, wf)
+        torch.cuda.synchronize()
+        assert e.conv_last_route(1) == "dgrad.asfwd.glds.join.wide"
+    finally:
+        e.conv_route_force(1, "")
+    want = (C.ref_conv_dgrad(dy.float().cpu(), w.float().cpu(), x.shape, g)
+            + prev.float().cpu()) * m
+    assert _rel(dx, want) < 1e-2
+    if not e.deterministic():
+        assert fused
+        gf, xf = dx.float().cpu().reshape(-1, cin), x.float().cpu().reshape(-1, cin)
+        assert _rel(red, torch.stack([gf.sum(0), (gf * xf).sum(0)])) < 1e-3
