@@ -1036,6 +1036,29 @@ int persistent_tpb(long tiles) {
   return (int)std::max<long>(1, (tiles + cus - 1) / cus);
 }
 
+// the same for a column-grouped grid (every workgroup walks tpb row tiles of ONE column tile;
+// class c contributes ⌈ntm[c] / tpb⌉ groups per column): raised until the grid fits the slots.
+// ⌈tiles / CUs⌉ alone can round the groups up past them — Xception-41's 38×38×728 pointwise
+// convs got 43 groups × 6 columns = 258 workgroups for 256 CUs, and the two extra ran as a
+// second wave of whole groups: 613 instead of ~330 µs (profiles/r06_grouped_tiling.txt)
+int grouped_tpb(const long* ntm, int ncls, long ntn) {
+  const long slots = env_int("TDL_GLDS_SLOTS", 256);
+  long tiles = 0, ntm_max = 1;
+  for (int c = 0; c < ncls; ++c) {
+    tiles += ntm[c];
+    ntm_max = std::max(ntm_max, ntm[c]);
+  }
+  long tpb = std::min<long>(std::max(1, persistent_tpb(tiles * ntn)), ntm_max);
+  auto blocks = [&](long t) {
+    long g = 0;
+    for (int c = 0; c < ncls; ++c) g += (ntm[c] + t - 1) / t;
+    return g * ntn;
+  };
+  static const bool fit = env_int("TDL_GROUPED_FIT", 1) != 0;  // (0: the old rounding, A/B)
+  while (fit && tpb < ntm_max && blocks(tpb) > slots) ++tpb;
+  return (int)tpb;
+}
+
 }  // namespace
 
 // fp8 forward: LDS-DMA kernel only (C % 16 == 0: a 16-B chunk never crosses a filter tap); the
@@ -1056,8 +1079,7 @@ void conv_fwd_fp8_launch(const ConvArgs& a0, hipStream_t st) {
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
   a.ncls = 1;
   a.splits = 1;
-  a.tpb = std::max(1, persistent_tpb(ntm * ntn));
-  a.tpb = (int)std::min<long>(a.tpb, ntm);
+  a.tpb = grouped_tpb(&ntm, 1, ntn);
   const long groups = (ntm + a.tpb - 1) / a.tpb;
   const int blocks = (int)(groups * ntn);
   a.cls_tile0[0] = 0;
@@ -1105,7 +1127,7 @@ static int fwd_tiling(ConvArgs& a, const GCfg& g) {
   const long ntm = cdiv(a.M, g.bm), ntn = cdiv(a.Ng, g.bn);
   a.ncls = 1;
   a.splits = 1;
-  a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm * ntn)), ntm);
+  a.tpb = grouped_tpb(&ntm, 1, ntn);
   const long groups = (ntm + a.tpb - 1) / a.tpb;
   a.cls_tile0[0] = 0;
   a.cls_tile0[1] = (int)(groups * ntn * a.tpb);
@@ -1587,13 +1609,9 @@ bool conv_dgrad_glds(const ConvArgs& a0, int cfg, hipStream_t st, bool* fused) {
   const bool rag_stats = a.K % 64 != 0;
   if (bn_stats) {
     const long ntn = cdiv(a.Ng, g.bn);
-    long ntm_all = 0, ntm_max = 1;
-    for (int c = 0; c < a.ncls; ++c) {
-      const long ntm_c = cdiv((long)a.N * a.cls_Hc[c] * a.cls_Wc[c], g.bm);
-      ntm_all += ntm_c;
-      ntm_max = std::max(ntm_max, ntm_c);
-    }
-    a.tpb = (int)std::min<long>(std::max(1, persistent_tpb(ntm_all * ntn)), ntm_max);
+    long ntm_c[MAX_DG_CLASSES];
+    for (int c = 0; c < a.ncls; ++c) ntm_c[c] = cdiv((long)a.N * a.cls_Hc[c] * a.cls_Wc[c], g.bm);
+    a.tpb = grouped_tpb(ntm_c, a.ncls, ntn);
     a.cls_tile0[0] = 0;
     for (int c = 0; c < a.ncls; ++c) {
       const long groups_c = cdiv(cdiv((long)a.N * a.cls_Hc[c] * a.cls_Wc[c], g.bm), a.tpb);
