@@ -262,10 +262,7 @@ class Conv2d(nn.Module):
         c = self.__dict__.get("_flipc")
         if c is not None and c[0] == v and c[1].device == w.device:
             return c[1]
-        f = flip_classes(w, geom)
-        if c is not None and c[1].device == w.device and c[1].shape == f.shape:
-            c[1].copy_(f)
-            f = c[1]
+        f = flip_classes(w, geom, out=c[1] if c is not None else None)  # (in place when it fits)
         self.__dict__["_flipc"] = (v, f)
         return f
 

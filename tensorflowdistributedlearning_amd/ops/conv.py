@@ -242,16 +242,19 @@ def _classes(s, R, pad):
     return out
 
 
-def flip_classes(w, geom: ConvGeom):
+def flip_classes(w, geom: ConvGeom, out=None):
     """The per-parity-class flipped sub-filters of a strided conv's weight w [K, R, S, C], each
     [C, Th, Tw, K], concatenated a-major over the classes with taps (csrc/kernels/conv_glds.hip
     dgrad_as_fwd_strided reads them in the same order): class (a, b) of dx is the stride-1
-    forward conv of dy with its sub-filter."""
+    forward conv of dy with its sub-filter.  ``out``: a previous result's buffer to rebuild in
+    place (GPU; the persistent per-layer copy — no new buffer and no copy)."""
     (sh, sw), ph, pw = geom.stride, geom.padding[0], geom.padding[2]
     R, S = w.shape[1], w.shape[2]
     if on_gpu(w) and w.dtype == torch.bfloat16 and sh <= 4 and sw <= 4:
         n = sum(len(rr) for rr in _classes(sh, R, ph)) * sum(len(ss) for ss in _classes(sw, S, pw))
-        out = torch.empty(n * w.shape[0] * w.shape[3], device=w.device, dtype=w.dtype)
+        n *= w.shape[0] * w.shape[3]
+        if out is None or out.numel() != n or out.dtype != w.dtype or out.device != w.device:
+            out = torch.empty(n, device=w.device, dtype=w.dtype)
         ext().conv_flip_classes(w.contiguous(), out, sh, sw, ph, pw)  # one launch
         return out
     parts = []
