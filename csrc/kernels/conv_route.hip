@@ -45,6 +45,8 @@ const RouteRule kRoutes[] = {
    "1x1 with 64 outputs: 8-wave 256x64 tiles, 35 vs 53 us on 56x56 64->64 (profiles/r02_conv_n64_configs.txt)"},
   {"fwd.glds.stem",               FWD,   RT_GLDS,  2, TAPS,  0, 8, 32,       49, 64,      65536, 256, 64,  128, 0,                RF_AFF | RF_FP8,                      4,    false, false,
    "opt-in: row-packed ResNet stem (7 taps x 24 channels -> 64) on 8-wave 256x64 tiles, 914 vs 1017 us alone at b1024 but no step gain (13,386 / 13,398 vs 13,396 / 13,435 img/s; profiles/r05_stem_ab.txt)"},
+  {"fwd.glds.narrow3x3",          FWD,   RT_GLDS,  9, 9,     0, 8, 32,       49, 64,      65536, 256, 64,  128, 0,                RF_AFF | RF_FP8,                      4,    true,  false,
+   "3x3 with <= 32 inputs and <= 64 outputs: 8-wave 256x64 LDS-DMA tiles, 256 vs 307 us on the GEMM (Xception-41 150x150 32->64 b128, profiles/r06_narrow_rows.txt)"},
   {"fwd.pc.aligned.aff",          FWD,   RT_PC,    1, TAPS,  0, 64, INF,     65, INF,     0,     0, 0,     0,  RF_AFF,             RF_BIAS | RF_RES | RF_FP8,            0,    true,  true,
    "tests: folded-BN forwards of any size"},
   {"fwd.pc.aligned",              FWD,   RT_PC,    2, TAPS,  0, 256, INF,    65, INF,     0,     0, 0,     0,  0,                  RF_AFF | RF_RES | RF_FP8,             0,    true,  true,
@@ -64,6 +66,8 @@ const RouteRule kRoutes[] = {
    "fp8 dgrad (e5m2 dy x e4m3 W^T): LDS-DMA kernel only"},
   {"dgrad.asfwd.rw64",            DGRAD, RT_ASFWD, 9, 9,     1, 64, 64,      64, 64,      4096,  0, 0,     0,  RF_WFLIP,           RF_AFF | RF_FP8 | RF_STRIDED,         ASF_RW, true, false,
    "stride-1 3x3 64->64 dgrad as the forward conv on the resident-filter halo kernel (mask, join, BN-backward sums)"},
+  {"dgrad.asfwd.glds.n32",        DGRAD, RT_ASFWD, 1, TAPS,  1, 8, 32,       64, INF,     4096,  256, 64,  128, RF_WFLIP,         RF_STATS_JOIN | RF_AFF | RF_FP8,      4,    true,  false,
+   "<= 32-wide dx: the LDS-DMA 8-wave tiles, not the halo loader: 361 vs 714 us (Xception-41 150x150 32<-64 b128, profiles/r06_narrow_rows.txt)"},
   {"dgrad.asfwd.halo",            DGRAD, RT_ASFWD, 3, HT,    1, 8, 64,       64, INF,     4096,  0, 0,     0,  RF_WFLIP,           RF_STATS | RF_AFF | RF_FP8,           ASF_HALO, true, false,
    "<= 64-wide dx as the forward conv of dy on the halo loader: 698 -> 503 us (bench/dgrad_paths.py, profiles/r05_dgrad_as_fwd.txt)"},
   {"dgrad.asfwd.halo.aligned",    DGRAD, RT_ASFWD, 3, HT,    1, 8, INF,      64, INF,     0,     0, 0,     0,  RF_WFLIP,           RF_STATS | RF_AFF | RF_FP8,           ASF_HALO, true, true,
