@@ -39,6 +39,41 @@ __device__ __forceinline__ void cvt8(const Raw8<float>& r, float* f) {
   }
 }
 
+// non-temporal 16-B / 8-B accesses for the streamed-once tensors of the stem pool passes (NT):
+// keep them out of the caches the re-read operands (dy, the index bytes, the window rows) and
+// the concurrent side-stream GEMMs use — as bn.hip's ld16 / st16
+typedef uint32_t pnt_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t pnt_u32x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ uint4 pld16(const void* p) {
+  if constexpr (NT) {
+    const pnt_u32x4 v = __builtin_nontemporal_load((const pnt_u32x4*)p);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+    return *(const uint4*)p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void pst16(void* p, const uint4& v) {
+  if constexpr (NT) {
+    pnt_u32x4 w;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    __builtin_nontemporal_store(w, (pnt_u32x4*)p);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void pst8(void* p, const uint2& v) {
+  if constexpr (NT) {
+    pnt_u32x2 w;
+    w[0] = v.x; w[1] = v.y;
+    __builtin_nontemporal_store(w, (pnt_u32x2*)p);
+  } else {
+    *(uint2*)p = v;
+  }
+}
+
 // the KK×KK window of output (n, ho, wo): taps outside the image load the clamped pixel and have
 // their bit clear in the returned mask (bit r·KK + q)
 template <int KK, int SS, typename I, typename T>
@@ -325,7 +360,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_stats_kernel(
 // one pass over the conv output: the BN output is never written or re-read.  coef = bn_finalize's
 // fp32 rows (scale, shift, …).  The index byte's bit 7 records u_max > 0 — the BN's ReLU mask at
 // the argmax, the only position the backward routes gradient to (maxpool_bwd*<RB>).
-template <int KK, int SS, typename I, bool PRE = true>
+template <int KK, int SS, typename I, bool PRE = true, bool NTS = false>
 __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ coef, bf16_t* __restrict__ y,
     uint8_t* __restrict__ idx, bf16_t* __restrict__ zarg, int N, int H, int W, int C, int Ho,
@@ -403,12 +438,12 @@ __global__ void __launch_bounds__(NT) bn_maxpool_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) arg[j] |= best[j] > 0.f ? 0x80 : 0;
     const I o = (((I)n * Ho + ho) * Wo + wo) * C + c;
-    store8(y + o, best);
-    if (zarg) store8(zarg + o, zbest);  // (bf16 in, bf16 out: exact)
+    pst16<NTS>(y + o, pack8(best));
+    if (zarg) pst16<NTS>(zarg + o, pack8(zbest));  // (bf16 in, bf16 out: exact)
     uint2 packed;
     packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
     packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
-    *(uint2*)(idx + o) = packed;
+    pst8<NTS>(idx + o, packed);
   }
 }
 
@@ -476,7 +511,7 @@ __global__ void __launch_bounds__(NT) maxpool_bn_sums_kernel(
   (void)cv;
 }
 
-template <int KK, int SS, typename I>
+template <int KK, int SS, typename I, bool NTS = false>
 __global__ void __launch_bounds__(NT) maxpool_bn_apply_kernel(
     const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ x,
     const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
@@ -514,7 +549,7 @@ __global__ void __launch_bounds__(NT) maxpool_bn_apply_kernel(
     const int h = (int)(p % (I)H);
     const int n = (int)(p / (I)H);
     const I off = (((I)n * H + h) * W + w) * C + c;
-    const uint4 xv = *(const uint4*)(x + off);
+    const uint4 xv = pld16<NTS>(x + off);
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -545,7 +580,7 @@ __global__ void __launch_bounds__(NT) maxpool_bn_apply_kernel(
     unpack8(xv, vx);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = A[j] * gq[j] + Bc[j] * vx[j] + Cc[j];
-    *(uint4*)(dx + off) = pack8(o);
+    pst16<NTS>(dx + off, pack8(o));
   }
 }
 
@@ -622,6 +657,12 @@ __global__ void avgpool_scalar_bwd(const T* __restrict__ dy, T* __restrict__ dx,
 
 }  // namespace
 
+// TDL_POOL_NT=0: cached stores / loads for the stem pool passes' streamed tensors (A/B)
+static bool pool_nt() {
+  static const bool on = getenv("TDL_POOL_NT") == nullptr || atoi(getenv("TDL_POOL_NT")) != 0;
+  return on;
+}
+
 template <typename T>
 static void maxpool_fwd_impl(const T* x, T* y, uint8_t* idx, int N, int H, int W, int C,
                         int Ho, int Wo, int k, int s, int pt, int pl, hipStream_t st) {
@@ -680,7 +721,9 @@ bool bn_maxpool_fwd_launch(const bf16_t* x, const float* coef, bf16_t* y, uint8_
   // TDL_POOL_PRELOAD=0: the per-tap loop (loads serialised by its bounds checks; A/B only)
   static const bool pre = getenv("TDL_POOL_PRELOAD") == nullptr || atoi(getenv("TDL_POOL_PRELOAD")) != 0;
   if (k == 3 && s == 2 && (long)N * H * W * C < (1L << 31))
-    hipLaunchKernelGGL((pre ? bn_maxpool_fwd_kernel<3, 2, uint32_t> : bn_maxpool_fwd_kernel<3, 2, uint32_t, false>),
+    hipLaunchKernelGGL((!pre ? bn_maxpool_fwd_kernel<3, 2, uint32_t, false>
+                        : pool_nt() ? bn_maxpool_fwd_kernel<3, 2, uint32_t, true, true>
+                                    : bn_maxpool_fwd_kernel<3, 2, uint32_t>),
                        dim3(blocks_for(no)), dim3(NT), 0, st, x, coef, y, idx, zarg, N, H, W, C, Ho, Wo,
                        k, s, pt, pl);
   else
@@ -700,7 +743,8 @@ bool maxpool_bn_bwd_launch(const bf16_t* dy, const uint8_t* idx, const bf16_t* z
                      dy, idx, zarg, red, nout, C);
   const long nin = (long)N * H * W * C / 8;
   if (k == 3 && s == 2 && nin * 8 < (1L << 31) && nout * 8 < (1L << 31))
-    hipLaunchKernelGGL((maxpool_bn_apply_kernel<3, 2, uint32_t>), dim3(blocks_for(nin)), dim3(NT), 0,
+    hipLaunchKernelGGL((pool_nt() ? maxpool_bn_apply_kernel<3, 2, uint32_t, true>
+                                  : maxpool_bn_apply_kernel<3, 2, uint32_t>), dim3(blocks_for(nin)), dim3(NT), 0,
                        st, dy, idx, x, coef, red, gamma, dx, dgamma, dbeta, N, H, W, C, Ho, Wo, k, s,
                        pt, pl, inv_count);
   else
