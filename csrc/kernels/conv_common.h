@@ -274,6 +274,14 @@ __device__ __forceinline__ uint32_t out_row_fast(const ConvArgs& a, const Tile& 
 // DGRAD epilogue operands loaded ahead (epi_preload_dgrad): the BN input x of the statistics,
 // the ReLU mask words and the previous dx of a join — issued before the tile's K loop so their
 // latency hides under it (conv_halo.hip conv_rw_kernel)
+// cache policy of the bf16 output-tile stores (buffer instruction aux bits: 2 = nt, streamed).
+// Non-temporal measured 2 % slower on ResNet-50 and Xception-41: the next BN pass reads the output
+// back soon after, partly from the caches (profiles/r06_epilogue_nt.txt)
+#ifndef TDL_EPI_STORE_AUX
+#define TDL_EPI_STORE_AUX 0
+#endif
+constexpr int kEpiStoreAux = TDL_EPI_STORE_AUX;
+
 template <int RM, int RN>
 struct EpiPre {
   v2u32 xv[RM][RN];
@@ -518,7 +526,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
         // not be stored (they would land in the next row)
         const bool cv = cols_ok || c0 + rn * 16 < a.Ng;
         if (!no_mem && !wide)
-          __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(pk[rn], rout, cv ? rbase[rm] + (uint32_t)(c0 + rn * 16) * 2u : ROW_OOB, 0, kEpiStoreAux);
         if constexpr (STATS && MODE == DGRAD) {
           // (Σg, Σg·x) of the stored bf16 g; rows past M store zeros (x reads there return 0)
           const float rg = (!ROWS || rbase[rm] != ROW_OOB) ? 1.f : 0.f;
@@ -555,7 +563,7 @@ __device__ __forceinline__ void store_tile_bf16(const ConvArgs& a, const Tile& T
           const auto s1 = __builtin_amdgcn_permlane16_swap(pk[p][1], pk[p + 1][1], false, false);
           v4u32 q;
           q[0] = s0[0]; q[1] = s1[0]; q[2] = s0[1]; q[3] = s1[1];
-          __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(q, rout, rbase[rm] + lcol + (uint32_t)p * 32u, 0, kEpiStoreAux);
         }
       }
     }
