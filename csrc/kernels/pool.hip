@@ -584,6 +584,106 @@ __global__ void __launch_bounds__(NT) maxpool_bn_apply_kernel(
   }
 }
 
+// maxpool_bn_apply_kernel for the 3×3 / 2 window on 2×2 blocks of input pixels: the four pixels
+// of a block share the 2×2 windows that can contain any of them (rows R0, R0+1 with
+// R0 = ⌊(h0 + pt − 1) / 2⌋ for an even h0; likewise columns), so a thread loads 4 dy vectors and
+// index words for 4 outputs instead of 1–4 per pixel (≈2.25× fewer L1 requests: the per-pixel
+// gather was L1-access bound, profiles/r06_pool_gather.txt).  Per pixel the windows accumulate
+// in the per-pixel kernel's ascending (ho, wo) order: bit-identical results.
+template <bool NTS>
+__global__ void __launch_bounds__(NT) maxpool_bn_apply2x2_kernel(
+    const bf16_t* __restrict__ dy, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ x,
+    const float* __restrict__ coef, const float* __restrict__ red, const float* __restrict__ gamma,
+    bf16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta, int N, int H,
+    int W, int C, int Ho, int Wo, int pt, int pl, float inv_count) {
+  const int cv = C / 8;
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += NT) {
+      if (dgamma) dgamma[c] = coef[3 * C + c] * (red[C + c] - coef[2 * C + c] * red[c]);
+      if (dbeta) dbeta[c] = red[c];
+    }
+  }
+  const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+  const uint32_t total = (uint32_t)N * Hb * Wb * cv;
+  uint32_t t = blockIdx.x * NT + threadIdx.x;
+  float A[8], Bc[8], Cc[8];
+  {
+    const int c = (int)(t % (uint32_t)cv) * 8;  // fixed per thread: the grid stride is a multiple of cv
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float mean = coef[2 * C + c + j], inv = coef[3 * C + c + j];
+      const float s0 = red[c + j], s1 = inv * (red[C + c + j] - mean * s0);
+      const float a = (gamma ? gamma[c + j] : 1.f) * inv;
+      const float b = -a * inv * s1 * inv_count;
+      A[j] = a;
+      Bc[j] = b;
+      Cc[j] = -a * s0 * inv_count - b * mean;
+    }
+  }
+  for (; t < total; t += gridDim.x * NT) {
+    const int c = (int)(t % (uint32_t)cv) * 8;
+    uint32_t p = t / (uint32_t)cv;
+    const int wb = (int)(p % (uint32_t)Wb);
+    p /= (uint32_t)Wb;
+    const int hb = (int)(p % (uint32_t)Hb);
+    const int n = (int)(p / (uint32_t)Hb);
+    const int h0 = 2 * hb, w0 = 2 * wb;
+    const int R0 = (h0 + pt - 1) >> 1, C0 = (w0 + pl - 1) >> 1;  // (arithmetic: −1 → −1)
+    uint4 g[2][2];
+    uint2 ix[2][2];
+    bool ok[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int ho = R0 + a, wo = C0 + b;
+        ok[a][b] = ho >= 0 && ho < Ho && wo >= 0 && wo < Wo;
+        const uint32_t o = (((uint32_t)n * Ho + (ok[a][b] ? ho : 0)) * Wo + (ok[a][b] ? wo : 0)) * C + c;
+        g[a][b] = *(const uint4*)(dy + o);
+        ix[a][b] = *(const uint2*)(idx + o);
+      }
+    uint4 xv[2][2];
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int h = min(h0 + dh, H - 1), w = min(w0 + dw, W - 1);
+        xv[dh][dw] = pld16<NTS>(x + (((uint32_t)n * H + h) * W + w) * C + c);
+      }
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int h = h0 + dh, w = w0 + dw;
+        if (h >= H || w >= W) continue;
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int r = h + pt - 2 * (R0 + a), q = w + pl - 2 * (C0 + b);
+            if (!ok[a][b] || r < 0 || r > 2 || q < 0 || q > 2) continue;
+            const int want = (r * 3 + q) | 0x80;
+            float gv[8];
+            unpack8(g[a][b], gv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const uint32_t word = j < 4 ? ix[a][b].x : ix[a][b].y;
+              if ((int)((word >> ((j & 3) * 8)) & 0xff) == want) acc[j] += gv[j];
+            }
+          }
+        float gq[8], vx[8], o[8];
+        unpack8(pack8(acc), gq);  // g as the unfused gather stores it
+        unpack8(xv[dh][dw], vx);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = A[j] * gq[j] + Bc[j] * vx[j] + Cc[j];
+        pst16<NTS>(dx + (((uint32_t)n * H + h) * W + w) * C + c, pack8(o));
+      }
+  }
+}
+
 // global average pool: one thread per (n, channel vector), loop over HW
 template <typename T>
 __global__ void avgpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N,
@@ -742,7 +842,15 @@ bool maxpool_bn_bwd_launch(const bf16_t* dy, const uint8_t* idx, const bf16_t* z
   hipLaunchKernelGGL(maxpool_bn_sums_kernel, dim3(std::min(1024, blocks_for(nout))), dim3(NT), 0, st,
                      dy, idx, zarg, red, nout, C);
   const long nin = (long)N * H * W * C / 8;
-  if (k == 3 && s == 2 && nin * 8 < (1L << 31) && nout * 8 < (1L << 31))
+  // TDL_POOL_APPLY2X2=0: the per-pixel gather (A/B)
+  static const bool b2 = getenv("TDL_POOL_APPLY2X2") == nullptr || atoi(getenv("TDL_POOL_APPLY2X2")) != 0;
+  if (b2 && k == 3 && s == 2 && pt >= 0 && pt <= 1 && pl >= 0 && pl <= 1 && nin * 8 < (1L << 31) &&
+      nout * 8 < (1L << 31)) {
+    const long nblk = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+    hipLaunchKernelGGL((pool_nt() ? maxpool_bn_apply2x2_kernel<true> : maxpool_bn_apply2x2_kernel<false>),
+                       dim3(blocks_for(nblk)), dim3(NT), 0, st, dy, idx, x, coef, red, gamma, dx, dgamma,
+                       dbeta, N, H, W, C, Ho, Wo, pt, pl, inv_count);
+  } else if (k == 3 && s == 2 && nin * 8 < (1L << 31) && nout * 8 < (1L << 31))
     hipLaunchKernelGGL((pool_nt() ? maxpool_bn_apply_kernel<3, 2, uint32_t, true>
                                   : maxpool_bn_apply_kernel<3, 2, uint32_t>), dim3(blocks_for(nin)), dim3(NT), 0,
                        st, dy, idx, x, coef, red, gamma, dx, dgamma, dbeta, N, H, W, C, Ho, Wo, k, s,

@@ -57,6 +57,10 @@ def main():
     cases = {"fwd": (fwd, xb + 2 * yb + yb // 2), "bwd": (bwd, 2 * xb + 2 * yb + yb // 2 + yb + yb // 2),
              "copy": (copy, 2 * xb)}
     fwd()
+    bwd()
+    torch.cuda.synchronize()
+    # checksum of dx for cross-build / cross-knob exactness checks (same inputs every run)
+    print(f"dx checksum {dx.double().sum().item():.10e} {dx.float().abs().sum().item():.10e}", flush=True)
     for name, (fn, nbytes) in cases.items():
         if a.only and name != a.only:
             continue
