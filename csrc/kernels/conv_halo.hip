@@ -463,6 +463,15 @@ __device__ __forceinline__ bf16x8 hread_tr_pair(uint32_t a0, uint32_t a1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// 16-B chunk swizzle of the weight gradient's x-halo slot rows (chunk c of slot s at c ^ swz(s)),
+// shared by the fill and the transposed reads.  TDL_HALO_WG_SWZ1 selects it at compile time:
+// 1 = s & 7 (what the forward halo uses), 0 = (s >> 1) & 7 (round 5; PMC 36 % LDS bank conflicts
+// in the step, profiles/r06_resnet50_b1024_pmc.txt)
+#ifndef TDL_HALO_WG_SWZ1
+#define TDL_HALO_WG_SWZ1 1
+#endif
+__device__ __forceinline__ int halo_wg_swz(int s) { return TDL_HALO_WG_SWZ1 ? (s & 7) : ((s >> 1) & 7); }
+
 struct HaloWg {
   int nsplit, ncb, nch;  // splits, co blocks, ci chunks
   int rb_per_split;      // pixel tiles (row blocks) per split
@@ -544,7 +553,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, Hal
         const int wi = g.ox_min + hc;
         const bool v = hr < hr_total && hc < g.Wo + g.ext_w && (unsigned)hi < (unsigned)g.Hi &&
                        (unsigned)wi < (unsigned)g.Wi;
-        const int lc = (lane & 7) ^ ((s >> 1) & 7);
+        const int lc = (lane & 7) ^ halo_wg_swz(s);
         const int n = t.n_first + k;
         hdma16(rx, Hs + (j * NW + wid) * 1024,
                v ? (uint32_t)((((n * g.Hi + hi) * g.Wi + wi) * g.Ci + c0 + lc * 8) * 2) : HOOB);
@@ -607,7 +616,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, Hal
           af[f] = hread_tr_pair<0>(ad, ad + 8 * BM);
         }
         auto xaddr = [&](uint32_t s0) {
-          return Hs + (s0 << 7) + ((cq ^ ((s0 >> 1) & 7u)) << 4) + cbyte;
+          return Hs + (s0 << 7) + ((cq ^ (uint32_t)halo_wg_swz((int)s0)) << 4) + cbyte;
         };
         bf16x8 xf = hread_tr_pair<0>(xaddr(sl[kb][0] + (uint32_t)g.tap_d[0]),
                                      xaddr(sl[kb][1] + (uint32_t)g.tap_d[0]));
@@ -630,7 +639,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_wgrad_kernel(ConvArgs a, Hal
       // front and the 9·RM MFMAs run in two bursts (taps 0–4, 5–8) with the reads of the next
       // block's dy and first 5 taps under the second — one LDS wait per burst, not per tap
       auto xaddr = [&](uint32_t s0) {
-        return Hs + (s0 << 7) + ((cq ^ ((s0 >> 1) & 7u)) << 4) + cbyte;
+        return Hs + (s0 << 7) + ((cq ^ (uint32_t)halo_wg_swz((int)s0)) << 4) + cbyte;
       };
       bf16x8 af[2][RM], xf[NTAP];
       auto read_a = [&](int kb, bf16x8 (&a)[RM]) {
