@@ -119,6 +119,8 @@ const RouteRule kRoutes[] = {
    "fp8 weight gradient with <= 128 output channels: 128x128 tiles"},
   {"wgrad.halo.wide3x3",          WGRAD, RT_HALO,  9, 9,     1, 128, INF,    8, INF,      32768, 0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  false,
    "3x3 with >= 128 inputs: halo weight gradient, ResNet-50 layers 2-4 362 -> 295 us at b1024 (profiles/r04_halo_ab.txt); 7x7x512 b1024 287 vs 375 us on the GEMM (profiles/r06_wgrad3x3.txt)"},
+  {"wgrad.halo.c64",              WGRAD, RT_HALO,  9, 9,     1, 64, 127,     8, INF,      1000000, 0, 0,   0,  0,                  RF_AFF | RF_FP8,                               0,    true,  false,
+   "3x3 weight gradients of 64-127 input channels over >= 1M pixels on the halo kernel: 441 vs 481 us on the register GEMM after its swizzle change (ResNet-50 b1024 56x56x64; profiles/r06_halo_wgrad_swizzle.txt)"},
   {"wgrad.halo.aligned",          WGRAD, RT_HALO,  9, 9,     1, 64, INF,     8, INF,      0,     0, 0,     0,  0,                  RF_AFF | RF_FP8,                               0,    true,  true,
    "tests: every eligible problem on the halo kernel"},
   {"wgrad.glds.stem",             WGRAD, RT_GLDS,  1, TAPS,  0, 1, 32,       1, 64,       65536, 0, 0,     0,  0,                  RF_AFF | RF_FP8,                               7,    false, false,
